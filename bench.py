@@ -1,0 +1,180 @@
+"""Benchmark: PPO train steps on BASELINE config 2 (PPO CartPole-v1, 256 envs per GPU,
+MLP[64,64], n_steps=128, synthetic observation replay), one process per GPU.
+
+    python bench.py --gpus N --steps K --warmup W
+    (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+
+A step = one PPO train_step: fused rollout of 256 envs x 128 steps (+GAE) and
+4 epochs x 4 minibatches of 8192 (shuffle-gather, forward, clipped loss, backward,
+global-norm clip, Keras Adam; RCCL all-reduce of the gradient when N>1).
+Weak scaling: every rank owns 256 envs. Rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+METRIC = 'env-steps/sec/GPU (PPO 16-env) + update ms; 1/2/4/8 MI355X'
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
+# rollout kernel algorithmic bytes per env-step (replay env): reads obs 16 + state 16 +
+# reward 4 + done 4; writes obs 16 + action/logp/value/entropy/reward/done/epret/return 32
+ROLLOUT_BYTES_PER_ENV_STEP = 40 + 48
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument('--gpus', type=int, default=1)
+    p.add_argument('--steps', type=int, default=20)
+    p.add_argument('--warmup', type=int, default=5)
+    p.add_argument('--n-envs', type=int, default=256)
+    p.add_argument('--n-steps', type=int, default=128)
+    p.add_argument('--t-rec', type=int, default=4096)
+    p.add_argument('--seed', type=int, default=55)
+    p.add_argument('--no-graph', action='store_true')
+    p.add_argument('--cpu-baseline-seconds', type=float, default=15.0)
+    p.add_argument('--cpu-threads', type=int, default=0)
+    return p.parse_args()
+
+
+def cpu_baseline(args, record, theta0):
+    sys.path.insert(0, str(ROOT / 'oracle'))
+    import torch
+    from cpu_ppo import time_cpu_baseline
+
+    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    value, info = time_cpu_baseline(record, theta0, n_steps=args.n_steps,
+                                    seconds=args.cpu_baseline_seconds, threads=threads)
+    torch.set_num_threads(threads)
+    return {
+        'value': round(value, 1),
+        'unit': 'env-steps/s',
+        'cores': info['threads'],
+        'kind': 'port',
+        'sample': (f"{info['train_steps']} PPO train steps of the same workload "
+                   f"({info['n_envs']} envs x {args.n_steps} steps, 4x4 minibatches) in "
+                   f"{info['seconds']:.1f} s: per-env Python step_envs loop, torch-CPU f32 "
+                   f"MLP + autograd, numpy GAE, Keras Adam (oracle/cpu_ppo.py)"),
+    }
+
+
+def load_traffic(workload_key):
+    f = ROOT / 'profiles' / 'traffic.json'
+    if not f.exists():
+        return None
+    data = json.loads(f.read_text())
+    entry = data.get(workload_key)
+    return entry.get('bytes_per_launch') if entry else None
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local_rank = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local_rank))
+    device = torch.device('cuda', local_rank)
+
+    from xagents_amd import PPO
+    from xagents_amd.envs import ReplayVecEnv, record_cartpole_replay
+    from xagents_amd.utils.common import create_model
+
+    record = record_cartpole_replay(args.n_envs, args.t_rec, seed=args.seed + rank)
+    envs = ReplayVecEnv('CartPole-v1', args.n_envs, device=device, record=record)
+    model = create_model(envs, 'ppo', 'model', optimizer_kwargs=dict(learning_rate=7e-4),
+                         seed=args.seed, device=device)
+    theta0 = model.theta.cpu().numpy().copy()
+    agent = PPO(envs, model, n_steps=args.n_steps, seed=args.seed, quiet=True,
+                use_graph=not args.no_graph)
+
+    for _ in range(args.warmup):
+        agent.train_step()
+    torch.cuda.synchronize()
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        agent.fused_train_step(events[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    rollout_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in events]))
+    update_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in events]))
+    env_steps = args.n_envs * args.n_steps * args.steps * world
+    value = env_steps / elapsed
+    agent._drain_episode_stats()
+
+    if rank == 0:
+        launch_bytes = ROLLOUT_BYTES_PER_ENV_STEP * args.n_envs * args.n_steps
+        achieved = launch_bytes / (rollout_ms * 1e-3) / 1e9
+        workload_key = f'ppo_mlp_rollout_n{args.n_envs}_t{args.n_steps}'
+        traffic = load_traffic(workload_key)
+        line = {
+            'metric': METRIC,
+            'value': round(value, 1),
+            'unit': 'env-steps/s',
+            'n_gpus': world,
+            'steps': args.steps,
+            'warmup': args.warmup,
+            'ms_per_step': round(elapsed / args.steps * 1e3, 4),
+            'higher_is_better': True,
+            'scaling': 'weak',
+            'vs_baseline': None,
+            'dtype': 'f32',
+            'data': 'synthetic: CartPole-v1 observation replay recorded on the host '
+                    '(np.random.default_rng(55+rank)), random-init weights',
+            'config': {
+                'workload': 'PPO CartPole-v1, 256 envs/GPU, MLP[64,64], n_steps=128, '
+                            'synthetic obs replay (BASELINE configs[1])',
+                'n_envs_per_gpu': args.n_envs,
+                'n_steps': args.n_steps,
+                'batch_per_gpu': args.n_envs * args.n_steps,
+                'minibatch_per_gpu': args.n_envs * args.n_steps // 4,
+                'ppo_epochs': 4,
+                'parallelism': f'dp{world}',
+                'graph': not args.no_graph,
+            },
+            'update_ms': round(update_ms, 4),
+            'rollout_ms': round(rollout_ms, 4),
+            'env_steps_per_sec_per_gpu': round(value / world, 1),
+            'roofline': {
+                'kernel': 'xa_mlp_rollout (mlp_rollout_kernel<4,2>)',
+                'bound': 'hbm',
+                'achieved': round(achieved, 3),
+                'peak': HBM_PEAK_GBS,
+                'unit': 'GB/s',
+                'frac': round(achieved / HBM_PEAK_GBS, 6),
+                'traffic': traffic,
+                'note': 'latency-bound: 128 dependent policy steps per env; '
+                        f'{ROLLOUT_BYTES_PER_ENV_STEP} algorithmic B/env-step x '
+                        f'{args.n_envs * args.n_steps} env-steps per launch',
+            },
+        }
+        if world == 1 and args.cpu_baseline_seconds > 0:
+            line['cpu_baseline'] = cpu_baseline(args, record, theta0)
+        else:
+            line['cpu_baseline'] = None
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -1,0 +1,213 @@
+/*
+ * xagents_hip.h -- C ABI of libxagents_hip.so, the MI355X (gfx950) hot path of an
+ * xagents-compatible RL training core.
+ *
+ * Conventions:
+ *   - Caller owns all memory. Every pointer is a device pointer (hipMalloc /
+ *     torch tensor data_ptr) unless stated. The library never allocates or frees.
+ *   - Every function is asynchronous on `stream` (a hipStream_t, NULL = default)
+ *     and may be captured into a hipGraph (no sync, no malloc inside).
+ *   - Return 0 on success, negative on error; xa_last_error() gives the message
+ *     (thread-local).
+ *   - Rollout and batch tensors are env-major: [n_envs, n_steps, ...]. The flat
+ *     index i = env * n_steps + t is exactly the order the reference produces with
+ *     BaseAgent.concat_step_batches (xagents/base.py:549-564, swapaxes(0,1).reshape).
+ *   - Actor-critic MLP parameters live in ONE flat f32 buffer laid out in Keras
+ *     trainable_variables order for the .cfg topology
+ *       dense-0 (obs->64, tanh), dense-1 (64->64, tanh, common), dense-2 (64->A
+ *       logits), dense-3 (64->1 value)     (xagents/ppo/models/ann-actor-critic.cfg)
+ *     i.e. W1[obs][64], b1[64], W2[64][64], b2[64], W3[64][A], b3[A], W4[64][1], b4[1]
+ *     (Keras Dense kernel is (in, out), y = x @ W + b; xagents/utils/common.py:239-258).
+ *     Gradients and Adam moments use the same layout.
+ */
+#ifndef XAGENTS_HIP_H
+#define XAGENTS_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define XA_ABI_VERSION 1
+#define XA_MLP_HIDDEN 64
+
+/* environment kinds for the fused rollout */
+#define XA_ENV_REPLAY 0   /* synthetic pre-recorded observation replay (BASELINE config 2) */
+#define XA_ENV_CARTPOLE 1 /* CartPole-v1 dynamics on device (gym classic_control semantics) */
+
+/* return kinds computed at the end of the fused rollout */
+#define XA_RETURNS_NONE 0
+#define XA_RETURNS_GAE 1   /* PPO.calculate_returns, xagents/ppo/agent.py:48-94 */
+#define XA_RETURNS_NSTEP 2 /* A2C.calculate_returns, xagents/a2c/agent.py:141-171 */
+
+/* loss kinds of the fused actor-critic gradient */
+#define XA_LOSS_PPO 0 /* PPO.update_gradients, xagents/ppo/agent.py:96-137 */
+#define XA_LOSS_A2C 1 /* A2C.train_step, xagents/a2c/agent.py:190-218 */
+
+int xa_abi_version(void);
+const char* xa_last_error(void);
+
+/* Number of parameters of the actor-critic MLP (obs -> 64 -> 64 -> {A, 1}). */
+int xa_mlp_param_count(int obs_dim, int n_actions);
+
+/* Increment a device-side u64 counter (RNG stream position) by one. */
+int xa_counter_bump(uint64_t* counter, void* stream);
+
+/*
+ * GAE returns. Replaces PPO.calculate_returns (xagents/ppo/agent.py:48-94).
+ *   rewards [N,T], values [N,T], dones [N,T+1] (dones[:,0] = carried-in flags,
+ *   dones[:,t+1] = done returned by step t, as A2C.get_batch records them,
+ *   xagents/a2c/agent.py:116,129,138), next_values [N] = V(get_states()).
+ *   returns [N,T] = GAE advantages + values.
+ *   gamma_lam must be (float)((double)gamma * (double)lam): the reference forms
+ *   gamma*lam as a Python float product before the f32 multiply.
+ * Bit-exact with the reference numpy f32 arithmetic (LDS-staged, one lane per env).
+ */
+int xa_gae(const float* rewards, const float* values, const float* dones,
+           const float* next_values, float* returns, int n_envs, int n_steps, float gamma,
+           float gamma_lam, void* stream);
+
+/*
+ * n-step discounted returns. Replaces A2C.calculate_returns
+ * (xagents/a2c/agent.py:141-171): R_T = V(s_T); R_t = r_t + gamma*R_{t+1}*(1-d_{t+1}).
+ * Same layouts as xa_gae. Bit-exact with the reference f32 arithmetic.
+ */
+int xa_nstep_returns(const float* rewards, const float* dones, const float* next_values,
+                     float* returns, int n_envs, int n_steps, float gamma, void* stream);
+
+/*
+ * Fused vectorized rollout: n_steps x (policy forward -> Categorical sample ->
+ * log-prob/entropy/value -> env step -> store) for every env, plus the bootstrap
+ * value V(s_T) and (optionally) the returns. One wave64 per env.
+ * Replaces: A2C.get_batch (xagents/a2c/agent.py:96-139), A2C.get_model_outputs
+ * (a2c/agent.py:65-94), BaseAgent.step_envs (xagents/base.py:388-426) and the
+ * return computation (ppo/agent.py:48-94 or a2c/agent.py:141-171).
+ * Reference quirks reproduced: the policy input of step t+1 is the PRE-reset
+ * observation returned by step t (a2c/agent.py:132-136); the carried state
+ * (env_state) and the bootstrap use the POST-reset state (base.py:424,
+ * ppo/agent.py:72).
+ * Sampling: action = first a with u * sum_k e_k < cumsum(e)_a, e_k =
+ * exp(logit_k - max), u from `uniforms` [N,T] if given, else Philox4x32-10 keyed
+ * by seed at counter (env, t, *rng_counter).
+ */
+typedef struct XaRolloutArgs {
+  int n_envs, n_steps, obs_dim, n_actions;
+  const float* theta; /* flat actor-critic parameters */
+
+  int env_kind;           /* XA_ENV_REPLAY / XA_ENV_CARTPOLE */
+  float* env_state;       /* [N,obs] post-reset current observation (BaseAgent.states) */
+  double* env_state64;    /* [N,4]   CartPole internal f64 state (cartpole only) */
+  float* env_done;        /* [N]     last done flags (BaseAgent.dones) */
+  int* env_cursor;        /* [N]     replay position / elapsed episode steps */
+  float* ep_return;       /* [N]     running episode return (BaseAgent.episode_rewards) */
+  const float* rep_obs;   /* [N,t_rec,obs] obs returned by env.step at replay position p */
+  const float* rep_state; /* [N,t_rec,obs] state after step p (post-reset if done) */
+  const float* rep_rew;   /* [N,t_rec] */
+  const float* rep_done;  /* [N,t_rec] 0/1 */
+  int t_rec;
+  int max_episode_steps;  /* CartPole TimeLimit (500 for v1) */
+
+  const float* uniforms;  /* [N,T] or NULL */
+  uint64_t seed;
+  const uint64_t* rng_counter; /* device u64, read-only here */
+
+  float* obs_out;   /* [N,T,obs] policy inputs (A2C.get_batch `states`) */
+  int* act_out;     /* [N,T] */
+  float* logp_out;  /* [N,T] */
+  float* val_out;   /* [N,T] */
+  float* ent_out;   /* [N,T] or NULL */
+  float* rew_out;   /* [N,T] */
+  float* done_out;  /* [N,T+1] */
+  float* epret_out; /* [N,T] running episode return after step t, or NULL */
+  float* next_val;  /* [N] V(post-reset s_T) */
+  float* ret_out;   /* [N,T] or NULL */
+  int return_kind;  /* XA_RETURNS_* */
+  float gamma, gamma_lam;
+} XaRolloutArgs;
+
+int xa_mlp_rollout(const XaRolloutArgs* args, void* stream);
+
+/*
+ * Batched actor-critic forward (A2C.get_model_outputs, a2c/agent.py:65-94) over
+ * an arbitrary batch: logits, value, and either the log-prob of given actions
+ * (actions_in != NULL) or a sampled action (uniforms [B] required).
+ * Same arithmetic as the rollout. Outputs may be NULL when not wanted.
+ */
+int xa_mlp_forward(const float* theta, const float* obs, int batch, int obs_dim, int n_actions,
+                   const int* actions_in, const float* uniforms, int* actions_out, float* logp,
+                   float* value, float* entropy, float* logits, void* stream);
+
+/*
+ * Minibatch shuffle spec (replaces tf.random.shuffle + slicing,
+ * ppo/agent.py:139-155). If perm != NULL it holds epochs x batch indices (host
+ * permutations, parity mode). Otherwise a keyed Feistel permutation of [0,batch)
+ * per epoch, keyed by (seed, *rng_counter, epoch).
+ */
+typedef struct XaShuffle {
+  const int* perm;
+  uint64_t seed;
+  const uint64_t* rng_counter;
+} XaShuffle;
+
+/*
+ * Per-minibatch advantage statistics for every (epoch, minibatch):
+ * stats[(e*n_mb + m)*2 + {0,1}] = (sum adv, sum adv^2) in f64 over the minibatch,
+ * adv = returns - values (ppo/agent.py:180-183). The caller all-reduces them across
+ * ranks for exact global normalization.
+ */
+int xa_ppo_adv_stats(const float* returns, const float* values, int batch, int mb_size,
+                     int epochs, const XaShuffle* shuffle, double* stats, void* stream);
+
+/* Fused minibatch gather + actor-critic forward + loss + backward. Writes per-block
+ * partial gradients [n_blocks, P] and per-block loss sums [n_blocks, 4]
+ * (pg, value, entropy, count) when loss_partials != NULL. */
+typedef struct XaAcGradArgs {
+  int obs_dim, n_actions;
+  int loss_kind; /* XA_LOSS_PPO / XA_LOSS_A2C */
+  const float* theta;
+  int batch;    /* rollout batch N*T (flat, env-major) */
+  int mb_size;  /* minibatch size (PPO) or batch (A2C) */
+  int epoch, mb_index;
+  XaShuffle shuffle; /* ignored for A2C (identity order) */
+  const float* obs;      /* [batch, obs] */
+  const int* actions;    /* [batch] */
+  const float* old_logp; /* [batch] (PPO) */
+  const float* old_values; /* [batch] */
+  const float* returns;  /* [batch] */
+  const double* adv_stats; /* [(e*n_mb+m)*2] sums (PPO) */
+  double adv_count;        /* number of samples the stats were summed over (global) */
+  const float* adv_in;     /* [batch] precomputed (already normalised) advantages, or NULL */
+  float clip_norm, entropy_coef, value_coef, adv_eps;
+  float loss_scale; /* 1 / global minibatch size */
+  int n_blocks;
+  float* partials;      /* [n_blocks, P] */
+  float* loss_partials; /* [n_blocks, 4] or NULL */
+} XaAcGradArgs;
+
+int xa_ac_grad(const XaAcGradArgs* args, void* stream);
+int xa_ac_grad_blocks(int mb_size);
+
+/* grad[p] = sum_b partials[b*P + p] (f64 accumulation, fixed order). If adam_step
+ * != NULL it is incremented by one (Keras `iterations`) for the following
+ * xa_clip_adam. */
+int xa_grad_reduce(const float* partials, int n_parts, int n_params, float* grad,
+                   int* adam_step, void* stream);
+
+/*
+ * g' = grad * grad_scale; if clip_norm > 0: tf.clip_by_global_norm(g', clip_norm)
+ * (a2c/agent.py:217, ppo/agent.py:135-136); then Keras Adam (OptimizerV2,
+ * training_ops ApplyAdam): m += (g-m)(1-b1); v += (g^2-v)(1-b2);
+ * theta -= (m*alpha)/(sqrt(v)+eps), alpha = lr*sqrt(1-b2^t)/(1-b1^t), t = *adam_step.
+ * workspace: >= 1024 doubles (used when n_params > 65536). gnorm_out (device f32,
+ * optional) receives the pre-clip global norm.
+ */
+int xa_clip_adam(float* theta, float* adam_m, float* adam_v, const float* grad, int n_params,
+                 float grad_scale, float clip_norm, float lr, float beta1, float beta2,
+                 float eps, const int* adam_step, double* workspace, float* gnorm_out,
+                 void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

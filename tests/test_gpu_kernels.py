@@ -1,0 +1,340 @@
+"""GPU parity tests: libxagents_hip.so (through the C ABI) vs the oracle.
+
+Bars: bit-exact for integer actions, returns, rollout buffers and the Adam step
+(same f32 operation order as oracle/xa_oracle.c); losses and gradients within
+1e-5 relative (f32) of the float64 restatement of the reference TF math.
+"""
+import numpy as np
+import oracle
+import pytest
+import torch
+
+from xagents_amd import _lib, kernels
+
+pytestmark = pytest.mark.gpu
+
+GAE_GL = lambda g, l: float(np.float32(g * l))  # noqa: E731
+
+
+def T(x, dtype=None):
+    return torch.as_tensor(np.ascontiguousarray(x), device='cuda', dtype=dtype)
+
+
+def N(t):
+    torch.cuda.synchronize()
+    return t.detach().cpu().numpy()
+
+
+def _cases(golden, name):
+    d = golden(name)
+    for k in range(int(d['n_cases'])):
+        yield k, {key[len(f'c{k}_'):]: d[key] for key in d.files if key.startswith(f'c{k}_')}
+
+
+# ---- returns -------------------------------------------------------------
+def test_gae_matches_reference_golden(device, golden):
+    for k, c in _cases(golden, 'gae_cases.npz'):
+        out = kernels.gae(T(c['rewards'].T), T(c['values'].T), T(c['dones'].T),
+                          T(c['next_values']), float(c['gamma']), float(c['lam']))
+        np.testing.assert_array_equal(N(out).T, c['returns'].astype(np.float32), err_msg=f'{k}')
+
+
+def test_nstep_matches_reference_golden(device, golden):
+    for k, c in _cases(golden, 'nstep_cases.npz'):
+        out = kernels.nstep_returns(T(c['rewards'].T), T(c['dones'].T), T(c['next_values']),
+                                    float(c['gamma']))
+        np.testing.assert_array_equal(N(out).T, c['returns'], err_msg=f'{k}')
+
+
+@pytest.mark.parametrize('n,t', [(1000, 300), (256, 128), (3, 1)])
+def test_gae_large_vs_oracle(device, n, t):
+    rng = np.random.default_rng(n + t)
+    rew = rng.standard_normal((n, t)).astype(np.float32)
+    val = rng.standard_normal((n, t)).astype(np.float32)
+    done = (rng.random((n, t + 1)) < 0.03).astype(np.float32)
+    nv = rng.standard_normal(n).astype(np.float32)
+    out = kernels.gae(T(rew), T(val), T(done), T(nv), 0.99, 0.95)
+    np.testing.assert_array_equal(N(out), oracle.gae(rew, val, done, nv, 0.99, GAE_GL(0.99, 0.95)))
+
+
+# ---- forward / sampling ------------------------------------------------------
+def _theta(obs_dim, A, seed, scale=0.3):
+    P = kernels.mlp_param_count(obs_dim, A)
+    return (np.random.default_rng(seed).standard_normal(P) * scale).astype(np.float32)
+
+
+@pytest.mark.parametrize('obs_dim,A', [(4, 2), (6, 3), (8, 4), (2, 3)])
+def test_mlp_forward_bit_exact(device, obs_dim, A):
+    rng = np.random.default_rng(obs_dim)
+    theta = _theta(obs_dim, A, 1)
+    obs = (rng.standard_normal((1003, obs_dim)) * 2).astype(np.float32)
+    u = rng.random(1003, dtype=np.float32)
+    got = kernels.mlp_forward(T(theta), T(obs), A, uniforms=T(u), want_logits=True)
+    ref = oracle.mlp_forward(theta, obs, A, uniforms=u)
+    for g, r, name in zip(got, ref, ('act', 'logp', 'value', 'ent', 'logits')):
+        np.testing.assert_array_equal(N(g), r, err_msg=name)
+    acts = rng.integers(0, A, 1003).astype(np.int32)
+    got = kernels.mlp_forward(T(theta), T(obs), A, actions=T(acts))
+    ref = oracle.mlp_forward(theta, obs, A, actions=acts)
+    np.testing.assert_array_equal(N(got[1]), ref[1])
+    # float64 sanity of the whole forward
+    *_, logits64, v64 = oracle.forward_f64(theta, obs, obs_dim, A)
+    np.testing.assert_allclose(ref[4], logits64, rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(ref[2], v64, rtol=1e-5, atol=1e-5)
+
+
+# ---- rollout -------------------------------------------------------------------
+def _replay_env(n, t_rec, seed):
+    from xagents_amd.envs import record_cartpole_replay
+
+    return record_cartpole_replay(n, t_rec, seed=seed)
+
+
+def _run_rollout(theta, rec, n, t, uniforms, seed, ctr, return_kind, n_rollouts=2):
+    s0, rep_obs, rep_state, rep_rew, rep_done = rec
+    dev_env = dict(state=T(s0), done=torch.zeros(n, device='cuda'),
+                   cursor=torch.zeros(n, dtype=torch.int32, device='cuda'),
+                   ep_return=torch.zeros(n, device='cuda'))
+    reps = [T(x) for x in (rep_obs, rep_state, rep_rew, rep_done)]
+    host_env = dict(kind=0, state=s0.copy(), done=np.zeros(n, np.float32),
+                    cursor=np.zeros(n, np.int32), ep_return=np.zeros(n, np.float32),
+                    rep_obs=rep_obs, rep_state=rep_state, rep_rew=rep_rew, rep_done=rep_done)
+    th = T(theta)
+    ctr_t = torch.tensor([ctr], dtype=torch.int64, device='cuda')
+    for r in range(n_rollouts):
+        bufs = dict(obs=torch.zeros(n, t, 4, device='cuda'),
+                    act=torch.zeros(n, t, dtype=torch.int32, device='cuda'),
+                    logp=torch.zeros(n, t, device='cuda'), val=torch.zeros(n, t, device='cuda'),
+                    ent=torch.zeros(n, t, device='cuda'), rew=torch.zeros(n, t, device='cuda'),
+                    done=torch.zeros(n, t + 1, device='cuda'), epret=torch.zeros(n, t, device='cuda'),
+                    next_val=torch.zeros(n, device='cuda'), ret=torch.zeros(n, t, device='cuda'))
+        a = _lib.XaRolloutArgs()
+        a.n_envs, a.n_steps, a.obs_dim, a.n_actions = n, t, 4, 2
+        a.theta = th.data_ptr()
+        a.env_kind = 0
+        a.env_state, a.env_done = dev_env['state'].data_ptr(), dev_env['done'].data_ptr()
+        a.env_cursor, a.ep_return = dev_env['cursor'].data_ptr(), dev_env['ep_return'].data_ptr()
+        a.rep_obs, a.rep_state, a.rep_rew, a.rep_done = (x.data_ptr() for x in reps)
+        a.t_rec = rep_obs.shape[1]
+        u_r = None if uniforms is None else uniforms[r]
+        u_t = None if u_r is None else T(u_r)
+        a.uniforms = None if u_t is None else u_t.data_ptr()
+        a.seed, a.rng_counter = seed, ctr_t.data_ptr()
+        for k in ('obs', 'act', 'logp', 'val', 'ent', 'rew', 'done', 'epret', 'next_val', 'ret'):
+            setattr(a, {'obs': 'obs_out', 'act': 'act_out', 'logp': 'logp_out', 'val': 'val_out',
+                        'ent': 'ent_out', 'rew': 'rew_out', 'done': 'done_out',
+                        'epret': 'epret_out', 'next_val': 'next_val', 'ret': 'ret_out'}[k],
+                    bufs[k].data_ptr())
+        a.return_kind = return_kind
+        a.gamma, a.gamma_lam = 0.99, GAE_GL(0.99, 0.95)
+        kernels.rollout(a)
+        ref = oracle.mlp_rollout(theta, 2, host_env, t, uniforms=u_r, seed=seed, ctr=ctr + r,
+                                 return_kind=return_kind)
+        kernels.counter_bump(ctr_t)
+        for k, v in bufs.items():
+            np.testing.assert_array_equal(N(v), ref[k], err_msg=f'rollout {r} {k}')
+        for k in ('state', 'done', 'cursor', 'ep_return'):
+            np.testing.assert_array_equal(N(dev_env[k]), host_env[k], err_msg=f'env {k}')
+    return ref
+
+
+@pytest.mark.parametrize('return_kind', [1, 2])
+def test_rollout_replay_uniforms_bit_exact(device, return_kind):
+    n, t = 37, 50
+    rec = _replay_env(n, 40, seed=5)
+    rng = np.random.default_rng(9)
+    u = [rng.random((n, t), dtype=np.float32) for _ in range(2)]
+    ref = _run_rollout(_theta(4, 2, 3), rec, n, t, u, 0, 0, return_kind)
+    assert ref['done'].sum() > 0
+
+
+def test_rollout_replay_philox_bit_exact(device):
+    n, t = 64, 128
+    rec = _replay_env(n, 300, seed=6)
+    ref = _run_rollout(_theta(4, 2, 4, 0.5), rec, n, t, None, 0x1234567890, 77, 1, n_rollouts=3)
+    acts = ref['act']
+    assert 0.2 < acts.mean() < 0.8  # both actions are sampled
+
+
+def test_rollout_cartpole_dynamics(device):
+    from xagents_amd.envs import CartPoleVecEnv
+
+    n, t = 16, 64
+    env = CartPoleVecEnv(n, seed=3, device='cuda')
+    host = dict(kind=1, state=N(env.state).copy(), state64=N(env.state64).copy(),
+                done=np.zeros(n, np.float32), cursor=np.zeros(n, np.int32),
+                ep_return=np.zeros(n, np.float32))
+    theta = _theta(4, 2, 8, 0.2)
+    th = T(theta)
+    ctr = torch.zeros(1, dtype=torch.int64, device='cuda')
+    bufs = [torch.zeros(n, t, 4, device='cuda'), torch.zeros(n, t, dtype=torch.int32, device='cuda')]
+    bufs += [torch.zeros(n, t, device='cuda') for _ in range(5)]
+    done = torch.zeros(n, t + 1, device='cuda')
+    nv = torch.zeros(n, device='cuda')
+    a = _lib.XaRolloutArgs()
+    a.n_envs, a.n_steps, a.obs_dim, a.n_actions = n, t, 4, 2
+    a.theta = th.data_ptr()
+    env.fill_rollout_args(a)
+    a.seed, a.rng_counter = 99, ctr.data_ptr()
+    (a.obs_out, a.act_out, a.logp_out, a.val_out, a.ent_out, a.rew_out, a.epret_out) = (
+        b.data_ptr() for b in bufs)
+    a.done_out, a.next_val, a.ret_out, a.return_kind = done.data_ptr(), nv.data_ptr(), None, 0
+    kernels.rollout(a)
+    ref = oracle.mlp_rollout(theta, 2, host, t, seed=99, ctr=0, return_kind=0)
+    # gym dynamics in f64 use cos/sin: device and host libm may differ in the last ulp
+    np.testing.assert_allclose(N(bufs[0]), ref['obs'], rtol=0, atol=1e-6)
+    np.testing.assert_array_equal(N(bufs[1]), ref['act'])
+    np.testing.assert_array_equal(N(done), ref['done'])
+    np.testing.assert_allclose(N(env.state64), host['state64'], rtol=0, atol=1e-9)
+    assert ref['done'].sum() > 0
+
+
+# ---- update -----------------------------------------------------------------------
+def _rand_batch(rng, B, obs_dim, A, theta):
+    obs = rng.standard_normal((B, obs_dim)).astype(np.float32)
+    acts = rng.integers(0, A, B).astype(np.int32)
+    _, logp, val, _, _ = oracle.mlp_forward(theta, obs, A, actions=acts)
+    old_logp = (logp + rng.normal(0, 0.1, B)).astype(np.float32)
+    old_val = (val + rng.normal(0, 0.3, B)).astype(np.float32)
+    ret = (old_val + rng.normal(0, 1.0, B)).astype(np.float32)
+    return obs, acts, old_logp, old_val, ret
+
+
+def _grad_on_gpu(kind, theta, obs, acts, old_logp, old_val, ret, perm, epoch, m, MB,
+                 stats=None, count=None):
+    B, obs_dim = obs.shape
+    A = 2 if theta.size == kernels.mlp_param_count(obs_dim, 2) else 3
+    nb = kernels.ac_grad_blocks(MB)
+    P = theta.size
+    part = torch.zeros(nb, P, device='cuda')
+    lossp = torch.zeros(nb, 4, device='cuda')
+    keep = [T(theta), T(obs), T(acts), T(old_logp), T(old_val), T(ret)]
+    g = _lib.XaAcGradArgs()
+    g.obs_dim, g.n_actions, g.loss_kind = obs_dim, A, kind
+    g.theta, g.obs, g.actions, g.old_logp, g.old_values, g.returns = (k.data_ptr() for k in keep)
+    g.batch, g.mb_size, g.epoch, g.mb_index = B, MB, epoch, m
+    sh = _lib.XaShuffle()
+    perm_t = T(perm.astype(np.int32)) if perm is not None else None
+    sh.perm = None if perm_t is None else perm_t.data_ptr()
+    g.shuffle = sh
+    if stats is not None:
+        keep.append(stats)
+        g.adv_stats, g.adv_count = stats.data_ptr(), float(count)
+    g.clip_norm, g.entropy_coef, g.value_coef, g.adv_eps = 0.1, 0.01, 0.5, 1e-8
+    cnt = min(MB, B - m * MB)
+    g.loss_scale = 1.0 / cnt
+    g.n_blocks, g.partials, g.loss_partials = nb, part.data_ptr(), lossp.data_ptr()
+    kernels.ac_grad(g)
+    grad = torch.zeros(P, device='cuda')
+    kernels.grad_reduce(part, grad)
+    return N(grad), N(lossp).sum(0)
+
+
+def _assert_grad_close(got, ref, what):
+    err = np.abs(got - ref).max() / np.abs(ref).max()
+    rel_norm = np.linalg.norm(got - ref) / np.linalg.norm(ref)
+    assert err < 1e-5 and rel_norm < 1e-5, f'{what}: max-rel {err:.2e} norm-rel {rel_norm:.2e}'
+
+
+@pytest.mark.parametrize('B,MB', [(2048, 512), (1000, 333), (32768, 8192)])
+def test_ppo_grad_vs_f64(device, B, MB):
+    rng = np.random.default_rng(B)
+    theta = _theta(4, 2, 11, 0.2)
+    obs, acts, old_logp, old_val, ret = _rand_batch(rng, B, 4, 2, theta)
+    E = 2
+    perms = np.stack([rng.permutation(B) for _ in range(E)]).astype(np.int32)
+    n_mb = (B + MB - 1) // MB
+    stats = torch.zeros(E * n_mb * 2, dtype=torch.float64, device='cuda')
+    sh = _lib.XaShuffle()
+    perm_t = T(perms)
+    sh.perm = perm_t.data_ptr()
+    kernels.adv_stats(T(ret), T(old_val), B, MB, E, sh, stats)
+    st = N(stats).reshape(E, n_mb, 2)
+    for e in range(E):
+        for m in range(n_mb):
+            idx = perms[e, m * MB:(m + 1) * MB]
+            adv = ret[idx].astype(np.float64) - old_val[idx]
+            adv32 = (ret[idx] - old_val[idx]).astype(np.float64)
+            np.testing.assert_allclose(st[e, m], [adv32.sum(), (adv32 ** 2).sum()], rtol=1e-12)
+            if (e, m) not in ((0, 0), (E - 1, n_mb - 1)):
+                continue
+            got, lp = _grad_on_gpu(0, theta, obs, acts, old_logp, old_val, ret, perms, e, m, MB,
+                                   stats, len(idx))
+            advn = oracle.normalize_advantages(ret[idx], old_val[idx])
+            terms, ref = oracle.ac_loss_grad_f64(theta, obs[idx], acts[idx], ret[idx],
+                                                 old_val[idx], 2, 'ppo', old_logp[idx], advn)
+            _assert_grad_close(got, ref, f'e{e} m{m}')
+            assert lp[3] == len(idx)
+            np.testing.assert_allclose(lp[0], terms['pg_sum'], rtol=1e-5, atol=1e-4)
+            np.testing.assert_allclose(lp[1], terms['vl_sum'], rtol=1e-5)
+            np.testing.assert_allclose(lp[2], terms['ent_sum'], rtol=1e-5)
+
+
+def test_a2c_grad_vs_f64(device):
+    rng = np.random.default_rng(2)
+    B = 1280
+    theta = _theta(4, 2, 12, 0.2)
+    obs, acts, old_logp, old_val, ret = _rand_batch(rng, B, 4, 2, theta)
+    got, lp = _grad_on_gpu(1, theta, obs, acts, old_logp, old_val, ret, None, 0, 0, B)
+    terms, ref = oracle.ac_loss_grad_f64(theta, obs, acts, ret, old_val, 2, 'a2c')
+    _assert_grad_close(got, ref, 'a2c')
+    np.testing.assert_allclose(lp[1], terms['vl_sum'], rtol=1e-5)
+
+
+def test_feistel_shuffle_matches_oracle(device):
+    """The device shuffle (no host perm) visits exactly oracle.shuffle_perm's order."""
+    B, MB, E = 4096, 1024, 3
+    rng = np.random.default_rng(0)
+    ret = rng.standard_normal(B).astype(np.float32)
+    val = np.zeros(B, np.float32)
+    ctr = torch.tensor([5], dtype=torch.int64, device='cuda')
+    sh = _lib.XaShuffle()
+    sh.perm, sh.seed, sh.rng_counter = None, 4242, ctr.data_ptr()
+    stats = torch.zeros(E * 4 * 2, dtype=torch.float64, device='cuda')
+    kernels.adv_stats(T(ret), T(val), B, MB, E, sh, stats)
+    st = N(stats).reshape(E, 4, 2)
+    for e in range(E):
+        p = oracle.shuffle_perm(B, e, 4242, 5)
+        for m in range(4):
+            np.testing.assert_allclose(st[e, m, 0], ret[p[m * MB:(m + 1) * MB]].astype(np.float64).sum(),
+                                       rtol=1e-12)
+
+
+@pytest.mark.parametrize('P', [4675, 70001])
+def test_clip_adam_bit_exact(device, P):
+    rng = np.random.default_rng(P)
+    theta = rng.standard_normal(P).astype(np.float32)
+    m = (rng.standard_normal(P) * 1e-2).astype(np.float32)
+    v = np.abs(rng.standard_normal(P) * 1e-3).astype(np.float32)
+    g = rng.standard_normal(P).astype(np.float32)
+    tt, mt, vt, gt = T(theta), T(m), T(v), T(g)
+    step = torch.tensor([4], dtype=torch.int32, device='cuda')
+    ws = torch.zeros(1024, dtype=torch.float64, device='cuda')
+    gn = torch.zeros(1, device='cuda')
+    kernels.clip_adam(tt, mt, vt, gt, step, 7e-4, 0.9, 0.999, 1e-7, clip_norm=0.5,
+                      workspace=ws, gnorm_out=gn)
+    th_r, m_r, v_r, gn_r = oracle.clip_adam(theta, m, v, g, 4, 7e-4, 0.9, 0.999, 1e-7, 0.5)
+    assert abs(float(N(gn)[0]) - gn_r) <= 1e-6 * gn_r
+    np.testing.assert_array_equal(N(mt), m_r)
+    np.testing.assert_array_equal(N(vt), v_r)
+    np.testing.assert_array_equal(N(tt), th_r)
+
+
+def test_grad_reduce_and_adam_step_counter(device):
+    part = torch.randn(37, 999, device='cuda')
+    grad = torch.zeros(999, device='cuda')
+    step = torch.zeros(1, dtype=torch.int32, device='cuda')
+    kernels.grad_reduce(part, grad, step)
+    kernels.grad_reduce(part, grad, step)
+    ref = N(part).astype(np.float64).sum(0).astype(np.float32)
+    np.testing.assert_allclose(N(grad), ref, rtol=1e-6, atol=1e-6)
+    assert int(N(step)[0]) == 2
+
+
+def test_errors_are_loud(device):
+    a = _lib.XaRolloutArgs()
+    with pytest.raises(_lib.HipLibraryError, match='n_envs'):
+        kernels.rollout(a)
+    with pytest.raises(_lib.HipLibraryError, match='unsupported'):
+        kernels.mlp_forward(torch.zeros(100, device='cuda'), torch.zeros(3, 5, device='cuda'), 2,
+                            uniforms=torch.zeros(3, device='cuda'))

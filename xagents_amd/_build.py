@@ -1,0 +1,71 @@
+"""Build libxagents_hip.so for gfx950 with hipcc (in-tree, so it travels with the repo).
+
+The library is plain C-ABI (include/xagents_hip.h); no torch headers are involved.
+"""
+import os
+import subprocess
+from concurrent.futures import ThreadPoolExecutor
+from pathlib import Path
+
+PKG_DIR = Path(__file__).resolve().parent
+CSRC = PKG_DIR / 'csrc'
+LIB_PATH = PKG_DIR / 'libxagents_hip.so'
+BUILD_DIR = PKG_DIR.parent / 'build' / 'hip'
+HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
+ARCH = 'gfx950'
+CFLAGS = [
+    f'--offload-arch={ARCH}',
+    '-O3',
+    '-std=c++17',
+    '-fPIC',
+    # every fused multiply-add is written explicitly (fmaf); nothing else may be
+    # contracted, so the CPU oracle can restate the exact f32 operation order
+    '-ffp-contract=off',
+    '-Wall',
+    '-Wno-unused-function',
+]
+
+
+def sources():
+    return sorted(CSRC.glob('*.hip'))
+
+
+def _newest_input_mtime():
+    files = list(sources()) + list(CSRC.glob('*.hpp'))
+    files.append(PKG_DIR.parent / 'include' / 'xagents_hip.h')
+    return max(f.stat().st_mtime for f in files)
+
+
+def needs_build():
+    return not LIB_PATH.exists() or LIB_PATH.stat().st_mtime < _newest_input_mtime()
+
+
+def build_library(force=False, verbose=False):
+    """Compile every csrc/*.hip for gfx950 and link libxagents_hip.so."""
+    if not force and not needs_build():
+        return LIB_PATH
+    BUILD_DIR.mkdir(parents=True, exist_ok=True)
+
+    def compile_one(src):
+        obj = BUILD_DIR / (src.stem + '.o')
+        cmd = [HIPCC, *CFLAGS, '-c', str(src), '-o', str(obj)]
+        if verbose:
+            print(' '.join(cmd))
+        res = subprocess.run(cmd, capture_output=True, text=True)
+        if res.returncode != 0:
+            raise RuntimeError(f'hipcc failed for {src.name}:\n{res.stderr}')
+        return obj
+
+    with ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as pool:
+        objs = list(pool.map(compile_one, sources()))
+    tmp = LIB_PATH.with_suffix('.so.tmp')
+    cmd = [HIPCC, f'--offload-arch={ARCH}', '-shared', '-o', str(tmp), *map(str, objs)]
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError(f'link failed:\n{res.stderr}')
+    os.replace(tmp, LIB_PATH)
+    return LIB_PATH
+
+
+if __name__ == '__main__':
+    print(build_library(force=True, verbose=True))

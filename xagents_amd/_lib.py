@@ -1,0 +1,185 @@
+"""ctypes binding of libxagents_hip.so (C ABI declared in include/xagents_hip.h).
+
+There is no CPU fallback: if the HIP library is missing or fails to load, every
+device op raises. Torch tensors are passed as raw device pointers plus sizes; the
+stream is torch's current HIP stream so the calls compose with torch ops and can
+be captured into a hipGraph (torch.cuda.CUDAGraph).
+"""
+import ctypes
+from ctypes import (POINTER, Structure, c_double, c_float, c_int, c_uint64,
+                    c_void_p)
+from pathlib import Path
+
+import torch
+
+LIB_PATH = Path(__file__).resolve().parent / 'libxagents_hip.so'
+
+XA_ENV_REPLAY = 0
+XA_ENV_CARTPOLE = 1
+XA_RETURNS_NONE = 0
+XA_RETURNS_GAE = 1
+XA_RETURNS_NSTEP = 2
+XA_LOSS_PPO = 0
+XA_LOSS_A2C = 1
+MLP_HIDDEN = 64
+
+
+class XaRolloutArgs(Structure):
+    _fields_ = [
+        ('n_envs', c_int),
+        ('n_steps', c_int),
+        ('obs_dim', c_int),
+        ('n_actions', c_int),
+        ('theta', c_void_p),
+        ('env_kind', c_int),
+        ('env_state', c_void_p),
+        ('env_state64', c_void_p),
+        ('env_done', c_void_p),
+        ('env_cursor', c_void_p),
+        ('ep_return', c_void_p),
+        ('rep_obs', c_void_p),
+        ('rep_state', c_void_p),
+        ('rep_rew', c_void_p),
+        ('rep_done', c_void_p),
+        ('t_rec', c_int),
+        ('max_episode_steps', c_int),
+        ('uniforms', c_void_p),
+        ('seed', c_uint64),
+        ('rng_counter', c_void_p),
+        ('obs_out', c_void_p),
+        ('act_out', c_void_p),
+        ('logp_out', c_void_p),
+        ('val_out', c_void_p),
+        ('ent_out', c_void_p),
+        ('rew_out', c_void_p),
+        ('done_out', c_void_p),
+        ('epret_out', c_void_p),
+        ('next_val', c_void_p),
+        ('ret_out', c_void_p),
+        ('return_kind', c_int),
+        ('gamma', c_float),
+        ('gamma_lam', c_float),
+    ]
+
+
+class XaShuffle(Structure):
+    _fields_ = [('perm', c_void_p), ('seed', c_uint64), ('rng_counter', c_void_p)]
+
+
+class XaAcGradArgs(Structure):
+    _fields_ = [
+        ('obs_dim', c_int),
+        ('n_actions', c_int),
+        ('loss_kind', c_int),
+        ('theta', c_void_p),
+        ('batch', c_int),
+        ('mb_size', c_int),
+        ('epoch', c_int),
+        ('mb_index', c_int),
+        ('shuffle', XaShuffle),
+        ('obs', c_void_p),
+        ('actions', c_void_p),
+        ('old_logp', c_void_p),
+        ('old_values', c_void_p),
+        ('returns', c_void_p),
+        ('adv_stats', c_void_p),
+        ('adv_count', c_double),
+        ('adv_in', c_void_p),
+        ('clip_norm', c_float),
+        ('entropy_coef', c_float),
+        ('value_coef', c_float),
+        ('adv_eps', c_float),
+        ('loss_scale', c_float),
+        ('n_blocks', c_int),
+        ('partials', c_void_p),
+        ('loss_partials', c_void_p),
+    ]
+
+
+_SIGNATURES = {
+    'xa_abi_version': (c_int, []),
+    'xa_last_error': (ctypes.c_char_p, []),
+    'xa_mlp_param_count': (c_int, [c_int, c_int]),
+    'xa_counter_bump': (c_int, [c_void_p, c_void_p]),
+    'xa_gae': (
+        c_int,
+        [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_float,
+         c_void_p],
+    ),
+    'xa_nstep_returns': (
+        c_int,
+        [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_void_p],
+    ),
+    'xa_mlp_rollout': (c_int, [POINTER(XaRolloutArgs), c_void_p]),
+    'xa_mlp_forward': (
+        c_int,
+        [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+         c_void_p, c_void_p, c_void_p, c_void_p],
+    ),
+    'xa_ppo_adv_stats': (
+        c_int,
+        [c_void_p, c_void_p, c_int, c_int, c_int, POINTER(XaShuffle), c_void_p, c_void_p],
+    ),
+    'xa_ac_grad': (c_int, [POINTER(XaAcGradArgs), c_void_p]),
+    'xa_ac_grad_blocks': (c_int, [c_int]),
+    'xa_grad_reduce': (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    'xa_clip_adam': (
+        c_int,
+        [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_float, c_float, c_float, c_float,
+         c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p],
+    ),
+}
+
+EXPORTED_SYMBOLS = tuple(_SIGNATURES)
+
+_lib = None
+
+
+class HipLibraryError(RuntimeError):
+    pass
+
+
+def load(path=None):
+    """Load (once) and return the ctypes handle. Raises if the .so is missing."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = Path(path) if path else LIB_PATH
+    if not p.exists():
+        raise HipLibraryError(
+            f'{p} not found: build it with `python -m xagents_amd._build` '
+            f'(or __graft_entry__.build()). There is no CPU fallback.'
+        )
+    lib = ctypes.CDLL(str(p))
+    for name, (res, args) in _SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def check(ret, name):
+    if ret != 0:
+        msg = load().xa_last_error().decode()
+        raise HipLibraryError(f'{name} failed ({ret}): {msg}')
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise HipLibraryError('xagents_amd device ops need tensors on a HIP device')
+    if not t.is_contiguous():
+        raise HipLibraryError('xagents_amd device ops need contiguous tensors')
+    return t.data_ptr()
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def call(name, *args):
+    check(getattr(load(), name)(*args), name)

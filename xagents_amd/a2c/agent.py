@@ -1,0 +1,250 @@
+"""A2C with the xagents class surface (xagents/a2c/agent.py:9-218) on the fused
+MI355X path.
+
+train_step = one hipGraph replay of:
+    xa_mlp_rollout (n_steps x [forward, sample, env step, store] + n-step returns)
+    xa_ac_grad (A2C loss, full batch) -> xa_grad_reduce -> [RCCL all_reduce]
+    -> xa_clip_adam (tf.clip_by_global_norm + Keras Adam) -> xa_counter_bump
+"""
+import ctypes
+import warnings
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from xagents_amd import kernels
+from xagents_amd._lib import (XA_RETURNS_GAE, XA_RETURNS_NONE, XA_RETURNS_NSTEP,
+                              XaAcGradArgs, XaRolloutArgs, XaShuffle)
+from xagents_amd.base import OnPolicy
+from xagents_amd.envs import Discrete
+
+
+class A2C(OnPolicy):
+    """Asynchronous Methods for Deep Reinforcement Learning
+    https://arxiv.org/abs/1602.01783"""
+
+    loss_kind = kernels.XA_LOSS_A2C
+    return_kind = XA_RETURNS_NSTEP
+
+    def __init__(
+        self,
+        envs,
+        model,
+        entropy_coef=0.01,
+        value_loss_coef=0.5,
+        grad_norm=0.5,
+        use_graph=True,
+        **kwargs,
+    ):
+        super(A2C, self).__init__(envs, model, **kwargs)
+        self.entropy_coef = entropy_coef
+        self.value_loss_coef = value_loss_coef
+        self.grad_norm = grad_norm
+        # the reference counts Keras' InputLayer in model.layers
+        assert (
+            len(model.layers) + 1 > 2
+        ), f'Expected a model that has at least 3 layers, got {len(model.layers) + 1}'
+        activations = [layer.activation for layer in model.layers[-2:]]
+        self.output_is_softmax = 'softmax' in activations
+        self.distribution_type = (
+            'Categorical' if isinstance(self.envs[0].action_space, Discrete)
+            else 'MultivariateNormalDiag')
+        if getattr(model, 'fused_kind', None) != 'actor_critic_mlp':
+            raise NotImplementedError(
+                'The fused on-policy path supports the actor-critic MLP topology '
+                '(obs->64 tanh->64 tanh->{A,1}); got a model that does not match it')
+        if self.output_is_softmax or self.distribution_type != 'Categorical':
+            raise NotImplementedError('Only Categorical(logits) policies are fused')
+        self.use_graph = use_graph
+        self._graph = None
+        self._setup_device()
+
+    # ---- device state ------------------------------------------------------
+    def _setup_device(self):
+        self.distributed = dist.is_available() and dist.is_initialized()
+        self.world_size = dist.get_world_size() if self.distributed else 1
+        self.rank = dist.get_rank() if self.distributed else 0
+        N, T, obs = self.n_envs, self.n_steps, self.model.obs_dim
+        dev = self.device
+        f32 = dict(dtype=torch.float32, device=dev)
+        self.b_obs = torch.zeros(N, T, obs, **f32)
+        self.b_act = torch.zeros(N, T, dtype=torch.int32, device=dev)
+        self.b_logp = torch.zeros(N, T, **f32)
+        self.b_val = torch.zeros(N, T, **f32)
+        self.b_ent = torch.zeros(N, T, **f32)
+        self.b_rew = torch.zeros(N, T, **f32)
+        self.b_done = torch.zeros(N, T + 1, **f32)
+        self.b_epret = torch.zeros(N, T, **f32)
+        self.b_ret = torch.zeros(N, T, **f32)
+        self.next_val = torch.zeros(N, **f32)
+        self.rng_counter = torch.zeros(1, dtype=torch.int64, device=dev)
+        seed = self.seed if self.seed is not None else int(np.random.SeedSequence().entropy % 2**63)
+        self.rng_seed = (int(seed) * 1000003 + self.rank * 7919 + 17) % 2**64
+        P = self.model.n_params
+        self.grad = torch.zeros(P, **f32)
+        self.adam_ws = torch.zeros(1024, dtype=torch.float64, device=dev)
+        if self.distributed:
+            dist.broadcast(self.model.theta, 0)
+        a = XaRolloutArgs()
+        a.n_envs, a.n_steps, a.obs_dim, a.n_actions = N, T, obs, self.n_actions
+        a.theta = self.model.theta.data_ptr()
+        self.envs.fill_rollout_args(a)
+        a.uniforms = None
+        a.seed = self.rng_seed
+        a.rng_counter = self.rng_counter.data_ptr()
+        a.obs_out, a.act_out = self.b_obs.data_ptr(), self.b_act.data_ptr()
+        a.logp_out, a.val_out = self.b_logp.data_ptr(), self.b_val.data_ptr()
+        a.ent_out, a.rew_out = self.b_ent.data_ptr(), self.b_rew.data_ptr()
+        a.done_out, a.epret_out = self.b_done.data_ptr(), self.b_epret.data_ptr()
+        a.next_val, a.ret_out = self.next_val.data_ptr(), self.b_ret.data_ptr()
+        a.return_kind = self.return_kind
+        a.gamma = float(np.float32(self.gamma))
+        a.gamma_lam = kernels.gamma_lam_f32(self.gamma, getattr(self, 'lam', 0.0))
+        self._rargs = a
+        self._setup_update()
+
+    def _grad_args(self, mb_size, n_blocks, partials, loss_partials):
+        g = XaAcGradArgs()
+        g.obs_dim, g.n_actions = self.model.obs_dim, self.n_actions
+        g.loss_kind = self.loss_kind
+        g.theta = self.model.theta.data_ptr()
+        g.batch = self.n_envs * self.n_steps
+        g.mb_size = mb_size
+        g.obs, g.actions = self.b_obs.data_ptr(), self.b_act.data_ptr()
+        g.old_logp, g.old_values = self.b_logp.data_ptr(), self.b_val.data_ptr()
+        g.returns = self.b_ret.data_ptr()
+        g.clip_norm = float(getattr(self, 'clip_norm', 0.0))
+        g.entropy_coef = float(self.entropy_coef)
+        g.value_coef = float(self.value_loss_coef)
+        g.adv_eps = float(getattr(self, 'advantage_epsilon', 0.0))
+        g.n_blocks = n_blocks
+        g.partials = partials.data_ptr()
+        g.loss_partials = loss_partials.data_ptr()
+        return g
+
+    def _setup_update(self):
+        B = self.n_envs * self.n_steps
+        nb = kernels.ac_grad_blocks(B)
+        self.partials = torch.zeros(nb, self.model.n_params, dtype=torch.float32,
+                                    device=self.device)
+        self.loss_partials = torch.zeros(nb, 4, dtype=torch.float32, device=self.device)
+        g = self._grad_args(B, nb, self.partials, self.loss_partials)
+        g.epoch = g.mb_index = 0
+        g.loss_scale = 1.0 / (B * self.world_size)
+        self._gargs = g
+
+    # ---- the fused train step ----------------------------------------------
+    def _all_reduce(self, t):
+        if self.distributed:
+            dist.all_reduce(t)
+
+    def _apply_gradients(self, partials):
+        opt = self.model.optimizer
+        kernels.grad_reduce(partials, self.grad, opt.iterations)
+        self._all_reduce(self.grad)
+        kernels.clip_adam(self.model.theta, opt.m, opt.v, self.grad, opt.iterations,
+                          opt.learning_rate, opt.beta_1, opt.beta_2, opt.epsilon,
+                          clip_norm=self.grad_norm, workspace=self.adam_ws)
+
+    def _update(self):
+        kernels.ac_grad(self._gargs)
+        self._apply_gradients(self.partials)
+
+    def _rollout_impl(self):
+        kernels.rollout(self._rargs)
+
+    def _update_impl(self):
+        self._update()
+        kernels.counter_bump(self.rng_counter)
+
+    def _step_impl(self):
+        self._rollout_impl()
+        self._update_impl()
+
+    def _capture(self):
+        """Capture the rollout and the update as two hipGraphs (replayed back to back;
+        two graphs so the update can be timed on its own)."""
+        try:
+            graphs = []
+            for fn in (self._rollout_impl, self._update_impl):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    fn()
+                graphs.append(g)
+            self._graph = graphs
+        except Exception as exc:  # collectives that refuse capture -> eager launches
+            warnings.warn(f'hipGraph capture failed ({exc}); running the train step eagerly')
+            self.use_graph = False
+            self._graph = None
+
+    def _on_lr_change(self):
+        self._graph = None
+
+    def fused_train_step(self, events=None):
+        """One train step. `events` = (start, mid, end) torch.cuda.Events recorded
+        around the rollout and the update on the replay stream (bench timing)."""
+        rec = (lambda i: events[i].record()) if events else (lambda i: None)  # noqa: E731
+        if self.use_graph and self._graph is not None:
+            rec(0)
+            self._graph[0].replay()
+            rec(1)
+            self._graph[1].replay()
+            rec(2)
+        else:
+            rec(0)
+            self._rollout_impl()
+            rec(1)
+            self._update_impl()
+            rec(2)
+            if self.use_graph:
+                self._capture()
+        self.steps += self.n_envs * self.n_steps
+        self._queue_episode_stats(self.b_done, self.b_epret)
+
+    def train_step(self):
+        self.fused_train_step()
+
+    # ---- reference-level pieces (composable, not used by the fused step) -----
+    def get_model_outputs(self, inputs, models, training=True, actions=None):
+        """[actions, log probs, critic output, entropy, actor output]
+        (xagents/a2c/agent.py:65-94); sampling uses torch's generator for u."""
+        model = models[0] if isinstance(models, (list, tuple)) else models
+        obs = torch.as_tensor(inputs, dtype=torch.float32, device=self.device)
+        obs = obs.reshape(-1, model.obs_dim).contiguous()
+        uniforms = None
+        if actions is None:
+            uniforms = torch.rand(obs.shape[0], device=self.device)
+        else:
+            actions = torch.as_tensor(actions, device=self.device).to(torch.int32).reshape(-1)
+        act, logp, value, ent, logits = kernels.mlp_forward(
+            model.theta, obs, self.n_actions, actions=actions, uniforms=uniforms,
+            want_logits=True)
+        return act, logp, value, ent, logits
+
+    def get_batch(self, return_kind=XA_RETURNS_NONE):
+        """Run one fused rollout; returns time-major views
+        [states, rewards, actions, critic_output, dones, log_probs, entropies, None]
+        shaped like the reference's per-step lists (xagents/a2c/agent.py:96-139)."""
+        a = self._rargs
+        saved = a.return_kind
+        a.return_kind = return_kind
+        try:
+            kernels.rollout(a)
+            kernels.counter_bump(self.rng_counter)
+        finally:
+            a.return_kind = saved
+        self.steps += self.n_envs * self.n_steps
+        self._queue_episode_stats(self.b_done, self.b_epret)
+        tm = lambda x: x.transpose(0, 1)  # noqa: E731
+        return [tm(self.b_obs), tm(self.b_rew), tm(self.b_act), tm(self.b_val),
+                tm(self.b_done), tm(self.b_logp), tm(self.b_ent), None]
+
+    def calculate_returns(self, rewards, dones, values=None, selected_critic_logits=None,
+                          selected_importance=None):
+        """n-step returns from time-major rewards [T,N], dones [T+1,N]
+        (xagents/a2c/agent.py:141-171); bootstraps on V(get_states())."""
+        next_values = self.get_model_outputs(self.get_states(), self.output_models)[2]
+        r = torch.as_tensor(rewards, dtype=torch.float32, device=self.device).t().contiguous()
+        d = torch.as_tensor(dones, dtype=torch.float32, device=self.device).t().contiguous()
+        return kernels.nstep_returns(r, d, next_values.contiguous(), self.gamma).t()

@@ -1,0 +1,423 @@
+"""BaseAgent / OnPolicy / OffPolicy with the reference's class surface
+(xagents/base.py:22-751). The host-side bookkeeping (metrics, checkpoints, early
+stopping, history) is kept in Python as in the reference; env stepping, batching
+and math go to libxagents_hip.so through the subclasses.
+
+Differences forced by the device design (documented in DESIGN.md):
+* `envs` is a device vector env (xagents_amd.envs) rather than a list of gym envs;
+  it supports len(), envs[0].observation_space / action_space.
+* Episode statistics of a fused rollout are copied back asynchronously and folded
+  into total_rewards / games / done_envs in the reference's step-major, env-minor
+  order at the next train_step (one train_step of lag), so the host never stalls
+  the device between steps.
+"""
+import os
+import random
+from abc import ABC
+from collections import deque
+from datetime import timedelta
+from pathlib import Path
+from time import perf_counter
+
+import numpy as np
+import torch
+
+from xagents_amd.envs import Box, Discrete
+from xagents_amd.utils.common import write_from_dict
+
+
+class BaseAgent(ABC):
+    def __init__(
+        self,
+        envs,
+        model,
+        checkpoints=None,
+        reward_buffer_size=100,
+        n_steps=1,
+        gamma=0.99,
+        display_precision=2,
+        seed=None,
+        log_frequency=None,
+        history_checkpoint=None,
+        plateau_reduce_factor=0.9,
+        plateau_reduce_patience=10,
+        early_stop_patience=3,
+        divergence_monitoring_steps=None,
+        quiet=False,
+        trial=None,
+    ):
+        assert envs, 'No environments given'
+        self.n_envs = len(envs)
+        self.envs = envs
+        self.model = model
+        self.checkpoints = checkpoints
+        self.total_rewards = deque(maxlen=reward_buffer_size)
+        self.n_steps = n_steps
+        self.gamma = gamma
+        self.display_precision = display_precision
+        self.seed = seed
+        self.output_models = [self.model]
+        self.log_frequency = log_frequency or self.n_envs
+        self.id = self.__module__.split('.')[1]
+        self.history_checkpoint = history_checkpoint
+        self.plateau_reduce_factor = plateau_reduce_factor
+        self.plateau_reduce_patience = plateau_reduce_patience
+        self.early_stop_patience = early_stop_patience
+        self.divergence_monitoring_steps = divergence_monitoring_steps
+        self.quiet = quiet
+        self.trial = trial
+        self.reported_rewards = 0
+        self.plateau_count = 0
+        self.early_stop_count = 0
+        self.target_reward = None
+        self.max_steps = None
+        self.input_shape = self.envs[0].observation_space.shape
+        self.n_actions = None
+        self.best_reward = -float('inf')
+        self.mean_reward = -float('inf')
+        self.device = getattr(envs, 'device', torch.device('cuda'))
+        self.dones = [False] * self.n_envs
+        self.steps = 0
+        self.frame_speed = 0
+        self.last_reset_step = 0
+        self.training_start_time = None
+        self.last_reset_time = None
+        self.games = 0
+        self.episode_rewards = np.zeros(self.n_envs)
+        self.done_envs = 0
+        self.supported_action_spaces = Box, Discrete
+        self._pending_stats = None
+        if seed:
+            self.set_seeds(seed)
+        self.reset_envs()
+        self.set_action_count()
+        self.img_inputs = len(self.input_shape) >= 2
+        self.display_titles = (
+            'time',
+            'steps',
+            'games',
+            'speed',
+            'mean reward',
+            'best reward',
+        )
+
+    # ---- reference surface (host bookkeeping) -----------------------------
+    def assert_valid_env(self, env, valid_type):
+        assert isinstance(env.action_space, valid_type), (
+            f'Invalid environment: {env.spec.id}. {self.__class__.__name__} supports '
+            f'environments with a {valid_type} action space only, got {env.action_space}'
+        )
+
+    def display_message(self, *args, **kwargs):
+        if not self.quiet:
+            print(*args, **kwargs)
+
+    def set_seeds(self, seed):
+        torch.manual_seed(seed)
+        np.random.seed(seed)
+        self.envs.seed(seed)
+        os.environ['PYTHONHASHSEED'] = f'{seed}'
+        random.seed(seed)
+
+    def reset_envs(self):
+        self.envs.reset()
+
+    @property
+    def states(self):
+        return self.envs.state
+
+    def set_action_count(self):
+        action_space = self.envs[0].action_space
+        assert (
+            type(action_space) in self.supported_action_spaces
+        ), f'Expected one of {self.supported_action_spaces}, got {action_space}'
+        if isinstance(action_space, Discrete):
+            self.n_actions = action_space.n
+        if isinstance(action_space, Box):
+            self.n_actions = action_space.shape[0]
+
+    def check_checkpoints(self):
+        n_models = len(self.output_models)
+        n_checkpoints = len(self.checkpoints)
+        assert n_models == n_checkpoints, (
+            f'Expected {n_models} checkpoints for {n_models} '
+            f'given output models, got {n_checkpoints}'
+        )
+
+    def checkpoint(self):
+        if self.mean_reward > self.best_reward:
+            self.plateau_count = 0
+            self.early_stop_count = 0
+            self.display_message(
+                f'Best reward updated: {self.best_reward} -> {self.mean_reward}'
+            )
+            if self.checkpoints:
+                for model, checkpoint in zip(self.output_models, self.checkpoints):
+                    model.save_weights(checkpoint)
+        self.best_reward = max(self.mean_reward, self.best_reward)
+
+    def display_metrics(self):
+        display_values = (
+            timedelta(seconds=perf_counter() - self.training_start_time),
+            self.steps,
+            self.games,
+            f'{round(self.frame_speed)} steps/s',
+            self.mean_reward,
+            self.best_reward,
+        )
+        display = (
+            f'{title}: {value}'
+            for title, value in zip(self.display_titles, display_values)
+        )
+        self.display_message(', '.join(display))
+
+    def update_metrics(self):
+        self.checkpoint()
+        if (
+            self.divergence_monitoring_steps
+            and self.steps >= self.divergence_monitoring_steps
+            and self.mean_reward <= self.best_reward
+        ):
+            self.plateau_count += 1
+        if self.plateau_count >= self.plateau_reduce_patience:
+            current_lr, new_lr = None, None
+            for model in self.output_models:
+                current_lr = model.optimizer.learning_rate
+                new_lr = current_lr * self.plateau_reduce_factor
+            self.display_message(f'Learning rate reduced {current_lr} -> {new_lr}')
+            # the reference only updates the LAST output model (xagents/base.py:277-284)
+            self.output_models[-1].optimizer.learning_rate = new_lr
+            self._on_lr_change()
+            self.plateau_count = 0
+            self.early_stop_count += 1
+        self.frame_speed = (self.steps - self.last_reset_step) / (
+            perf_counter() - self.last_reset_time
+        )
+        self.last_reset_step = self.steps
+        self.mean_reward = np.around(
+            np.mean(self.total_rewards), self.display_precision
+        )
+
+    def _on_lr_change(self):
+        """Subclasses holding captured graphs re-capture them (lr is a kernel arg)."""
+
+    def report_rewards(self):
+        self.trial.report(np.mean(self.total_rewards), self.reported_rewards)
+        self.reported_rewards += 1
+        if self.trial.should_prune():
+            import optuna
+
+            raise optuna.exceptions.TrialPruned()
+
+    def check_episodes(self):
+        self._drain_episode_stats()
+        if self.done_envs >= self.log_frequency:
+            self.update_metrics()
+            if self.trial:
+                self.report_rewards()
+            self.last_reset_time = perf_counter()
+            self.display_metrics()
+            self.done_envs = 0
+
+    def training_done(self):
+        if self.early_stop_count >= self.early_stop_patience:
+            self.display_message('Early stopping')
+            return True
+        if self.target_reward and self.mean_reward >= self.target_reward:
+            self.display_message(f'Reward achieved in {self.steps} steps')
+            return True
+        if self.max_steps and self.steps >= self.max_steps:
+            self.display_message('Maximum steps exceeded')
+            return True
+        return False
+
+    def concat_buffer_samples(self):
+        """Concatenate per-env buffer samples (xagents/base.py:344-368)."""
+        if hasattr(self, 'buffers'):
+            batches = []
+            for i in range(self.n_envs):
+                batches.append(self.buffers[i].get_sample())
+            dtypes = (
+                self.batch_dtypes
+                if hasattr(self, 'batch_dtypes')
+                else [np.float32 for _ in range(len(batches[0]))]
+            )
+            if len(batches) > 1:
+                return [
+                    np.concatenate(item).astype(dtype)
+                    for (item, dtype) in zip(zip(*batches), dtypes)
+                ]
+            return [item.astype(dtype) for (item, dtype) in zip(batches[0], dtypes)]
+
+    def update_history(self, episode_reward):
+        data = {
+            'mean_reward': [self.mean_reward],
+            'best_reward': [self.best_reward],
+            'episode_reward': [episode_reward],
+            'step': [self.steps],
+            'time': [perf_counter() - self.training_start_time],
+        }
+        write_from_dict(data, self.history_checkpoint)
+
+    def init_from_checkpoint(self):
+        import pandas as pd
+
+        previous_history = pd.read_parquet(self.history_checkpoint)
+        expected_columns = {'time', 'mean_reward', 'best_reward', 'step', 'episode_reward'}
+        assert (
+            set(previous_history.columns) == expected_columns
+        ), f'Expected the following columns: {expected_columns}, got {set(previous_history.columns)}'
+        last_row = previous_history.loc[previous_history['time'].idxmax()]
+        self.mean_reward = last_row['mean_reward']
+        self.best_reward = previous_history['best_reward'].max()
+        history_start_steps = last_row['step']
+        history_start_time = last_row['time']
+        self.training_start_time = perf_counter() - history_start_time
+        self.last_reset_step = self.steps = int(history_start_steps)
+        self.total_rewards.append(last_row['episode_reward'])
+        self.games = previous_history.shape[0]
+
+    def init_training(self, target_reward, max_steps, monitor_session):
+        self.target_reward = target_reward
+        self.max_steps = max_steps
+        if monitor_session:
+            import wandb
+
+            wandb.init(name=monitor_session)
+        if self.checkpoints:
+            self.check_checkpoints()
+        self.training_start_time = perf_counter()
+        self.last_reset_time = perf_counter()
+        if self.history_checkpoint and Path(self.history_checkpoint).exists():
+            self.init_from_checkpoint()
+
+    def train_step(self):
+        raise NotImplementedError(
+            f'train_step() should be implemented by {self.__class__.__name__} subclasses'
+        )
+
+    def get_model_outputs(self, inputs, models, training=True):
+        if self.img_inputs:
+            inputs = torch.as_tensor(inputs, device=self.device).float() / 255.0
+        if not isinstance(models, (list, tuple)):
+            return models(inputs, training=training)
+        elif len(models) == 1:
+            return models[0](inputs, training=training)
+        return [sub_model(inputs, training=training) for sub_model in models]
+
+    def at_step_start(self):
+        pass
+
+    def at_step_end(self):
+        pass
+
+    def get_states(self):
+        """Most recent (post-reset) states, [n_envs, *obs] on device."""
+        return self.envs.state
+
+    def get_dones(self):
+        return self.envs.done
+
+    @staticmethod
+    def concat_step_batches(*args):
+        """Time-major [T, N, ...] -> env-major flat [N*T, ...] (xagents/base.py:549-564).
+
+        Works on numpy arrays and torch tensors. The device rollout already stores its
+        buffers env-major, so the fused path never needs this copy."""
+        concatenated = []
+        for arg in args:
+            if len(arg.shape) == 1:
+                arg = arg[..., None] if isinstance(arg, torch.Tensor) else np.expand_dims(arg, -1)
+            if isinstance(arg, torch.Tensor):
+                concatenated.append(arg.transpose(0, 1).reshape(-1, *arg.shape[2:]))
+            else:
+                concatenated.append(arg.swapaxes(0, 1).reshape(-1, *arg.shape[2:]))
+        return concatenated
+
+    # ---- device episode bookkeeping ----------------------------------------
+    def _queue_episode_stats(self, done_out, epret_out):
+        """Async D2H copy of one rollout's done flags [N,T+1] and running returns [N,T]."""
+        if self._pending_stats is None or self._pending_stats[0].shape != done_out.shape:
+            self._host_done = [torch.empty(done_out.shape, dtype=done_out.dtype).pin_memory()
+                               for _ in range(2)]
+            self._host_epret = [torch.empty(epret_out.shape, dtype=epret_out.dtype).pin_memory()
+                                for _ in range(2)]
+            self._stats_slot = 0
+            self._stats_queue = []
+        slot = self._stats_slot
+        self._host_done[slot].copy_(done_out, non_blocking=True)
+        self._host_epret[slot].copy_(epret_out, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._stats_queue.append((slot, ev))
+        self._stats_slot ^= 1
+        self._pending_stats = (done_out, epret_out)
+        # keep at most one rollout in flight: fold the previous one now
+        while len(self._stats_queue) > 1:
+            self._fold_stats(*self._stats_queue.pop(0))
+
+    def _fold_stats(self, slot, ev):
+        ev.synchronize()
+        done = self._host_done[slot].numpy()[:, 1:]
+        epret = self._host_epret[slot].numpy()
+        t_idx, env_idx = np.nonzero(done.T)  # step-major, env-minor like step_envs
+        finished = epret[env_idx, t_idx]
+        for env, ret in zip(env_idx, finished):
+            if self.history_checkpoint:
+                self.update_history(ret)
+            self.total_rewards.append(float(ret))
+        self.games += len(finished)
+        self.done_envs += len(finished)
+        self.episode_rewards = epret[:, -1] * (1.0 - done[:, -1])
+        self.dones = [bool(d) for d in done[:, -1]]
+
+    def _drain_episode_stats(self):
+        while getattr(self, '_stats_queue', None):
+            self._fold_stats(*self._stats_queue.pop(0))
+
+    def fit(
+        self,
+        target_reward=None,
+        max_steps=None,
+        monitor_session=None,
+    ):
+        assert (
+            target_reward or max_steps
+        ), '`target_reward` or `max_steps` should be specified when fit() is called'
+        self.init_training(target_reward, max_steps, monitor_session)
+        while True:
+            self.check_episodes()
+            if self.training_done():
+                break
+            self.at_step_start()
+            self.train_step()
+            self.at_step_end()
+        self._drain_episode_stats()
+
+    def play(self, *args, **kwargs):
+        raise NotImplementedError('play() renders gym frames; no gym in this build')
+
+
+class OnPolicy(BaseAgent, ABC):
+    def __init__(self, envs, model, **kwargs):
+        super(OnPolicy, self).__init__(envs, model, **kwargs)
+
+
+class OffPolicy(BaseAgent, ABC):
+    def __init__(
+        self,
+        envs,
+        model,
+        buffers,
+        **kwargs,
+    ):
+        super(OffPolicy, self).__init__(envs, model, **kwargs)
+        assert len(envs) == len(buffers), (
+            f'Expected equal env and replay buffer sizes, got {self.n_envs} '
+            f'and {len(buffers)}'
+        )
+        self.buffers = buffers
+
+    def fit(self, target_reward=None, max_steps=None, monitor_session=None):
+        self.fill_buffers()
+        super(OffPolicy, self).fit(target_reward, max_steps, monitor_session)

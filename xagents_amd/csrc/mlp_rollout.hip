@@ -1,0 +1,445 @@
+// Fused vectorized rollout for the actor-critic MLP (obs -> 64 tanh -> 64 tanh ->
+// {A logits, 1 value}) -- replaces A2C.get_batch (xagents/a2c/agent.py:96-139),
+// A2C.get_model_outputs (a2c/agent.py:65-94), BaseAgent.step_envs
+// (xagents/base.py:388-426) and the return computation (ppo/agent.py:48-94,
+// a2c/agent.py:141-171).
+//
+// Schedule: ONE wave64 per env, lane j = hidden unit j. Each lane keeps the
+// weights it needs for the whole rollout in VGPRs (column j of W1 and W2, row j of
+// the heads: ~75 registers), so the T-step loop touches HBM only for the replay
+// stream and the rollout stores. Per step:
+//   h1_j = tanh(sum_k x_k W1[k][j] + b1_j)              (fma chain over k)
+//   h1 -> LDS (wave-private row), 16 x ds_read_b128 broadcast back
+//   h2_j = tanh(((c0 + c1) + (c2 + c3)) + b2_j)          (4 interleaved 16-long fma chains)
+//   logit_a = butterfly_sum_j(h2_j * W3[j][a]) + b3_a ;  value likewise
+//   softmax / log-prob / entropy / inverse-CDF sample on every lane (wave-uniform)
+//   env step (replay: next record prefetched one step ahead; cartpole: f64 dynamics)
+// Envs are independent, so no inter-wave synchronisation exists anywhere.
+// The arithmetic order above is restated exactly by oracle/xa_oracle.c.
+#include "../../include/xagents_hip.h"
+#include "xa_common.hpp"
+
+namespace {
+
+constexpr int H = XA_MLP_HIDDEN;
+constexpr int kWaves = 4;
+constexpr int kFusedMaxT = 1024;
+
+XA_DEV void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+struct ParamOffsets {
+  int w1, b1, w2, b2, w3, b3, w4, b4;
+};
+
+__host__ __device__ inline ParamOffsets param_offsets(int obs, int A) {
+  ParamOffsets o;
+  o.w1 = 0;
+  o.b1 = o.w1 + obs * H;
+  o.w2 = o.b1 + H;
+  o.b2 = o.w2 + H * H;
+  o.w3 = o.b2 + H;
+  o.b3 = o.w3 + H * A;
+  o.w4 = o.b3 + A;
+  o.b4 = o.w4 + H;
+  return o;
+}
+
+template <int OBS, int A>
+struct LaneMlp {
+  float w1[OBS];
+  float b1;
+  float w2[H];
+  float b2;
+  float w3[A];
+  float w4;
+  float b3[A];
+  float b4;
+
+  XA_DEV void load(const float* __restrict__ theta, int lane) {
+    const ParamOffsets o = param_offsets(OBS, A);
+#pragma unroll
+    for (int k = 0; k < OBS; ++k) w1[k] = theta[o.w1 + k * H + lane];
+    b1 = theta[o.b1 + lane];
+#pragma unroll
+    for (int k = 0; k < H; ++k) w2[k] = theta[o.w2 + k * H + lane];
+    b2 = theta[o.b2 + lane];
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+      w3[a] = theta[o.w3 + lane * A + a];
+      b3[a] = theta[o.b3 + a];
+    }
+    w4 = theta[o.w4 + lane];
+    b4 = theta[o.b4];
+  }
+
+  // x: wave-uniform observation. sh: this wave's 64-float LDS row.
+  XA_DEV void forward(const float (&x)[OBS], float* sh, int lane, float (&logits)[A],
+                      float& value) const {
+    float z1 = 0.0f;
+#pragma unroll
+    for (int k = 0; k < OBS; ++k) z1 = fmaf(x[k], w1[k], z1);
+    const float h1 = xa_tanhf(z1 + b1);
+    sh[lane] = h1;
+    wave_sync();
+    float hv[H];
+#pragma unroll
+    for (int k = 0; k < H; k += 4) {
+      const float4 q = *reinterpret_cast<const float4*>(sh + k);
+      hv[k] = q.x;
+      hv[k + 1] = q.y;
+      hv[k + 2] = q.z;
+      hv[k + 3] = q.w;
+    }
+    wave_sync();  // the row is rewritten by the next forward
+    float c0 = 0.0f, c1 = 0.0f, c2 = 0.0f, c3 = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      c0 = fmaf(hv[i], w2[i], c0);
+      c1 = fmaf(hv[16 + i], w2[16 + i], c1);
+      c2 = fmaf(hv[32 + i], w2[32 + i], c2);
+      c3 = fmaf(hv[48 + i], w2[48 + i], c3);
+    }
+    const float h2 = xa_tanhf(((c0 + c1) + (c2 + c3)) + b2);
+#pragma unroll
+    for (int a = 0; a < A; ++a) logits[a] = xa_wave_sum(h2 * w3[a]) + b3[a];
+    value = xa_wave_sum(h2 * w4) + b4;
+  }
+};
+
+// Categorical over logits (TFP Categorical(logits=...), a2c/agent.py:59-94):
+// log_prob(a) = (l_a - m) - log(sum_k e^{l_k - m}); entropy = -sum p_k log p_k.
+template <int A>
+struct CatOut {
+  int action;
+  float logp, entropy;
+};
+
+template <int A>
+XA_DEV CatOut<A> categorical(const float (&l)[A], float u, int given_action) {
+  float m = l[0];
+#pragma unroll
+  for (int a = 1; a < A; ++a) m = fmaxf(m, l[a]);
+  float e[A];
+  float s = 0.0f;
+#pragma unroll
+  for (int a = 0; a < A; ++a) {
+    e[a] = xa_expf(l[a] - m);
+    s = s + e[a];
+  }
+  const float ls = xa_logf(s);
+  int act = given_action;
+  if (act < 0) {
+    const float target = u * s;
+    act = A - 1;
+    float c = 0.0f;
+    bool found = false;
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+      c = c + e[a];
+      if (!found && target < c) {
+        act = a;
+        found = true;
+      }
+    }
+  }
+  float ent = 0.0f, logp = 0.0f;
+#pragma unroll
+  for (int a = 0; a < A; ++a) {
+    const float lp = (l[a] - m) - ls;
+    const float p = e[a] / s;
+    ent = ent - p * lp;
+    if (a == act) logp = lp;
+  }
+  return CatOut<A>{act, logp, ent};
+}
+
+// gym CartPole-v1 (classic_control/cartpole.py), Euler integration in f64.
+XA_DEV bool cartpole_step(double (&s)[4], int action) {
+  const double gravity = 9.8, masspole = 0.1, total_mass = 1.1, length = 0.5;
+  const double polemass_length = 0.05, force_mag = 10.0, tau = 0.02;
+  const double force = action == 1 ? force_mag : -force_mag;
+  const double costheta = cos(s[2]), sintheta = sin(s[2]);
+  const double temp = (force + polemass_length * s[3] * s[3] * sintheta) / total_mass;
+  const double thetaacc = (gravity * sintheta - costheta * temp) /
+                          (length * (4.0 / 3.0 - masspole * costheta * costheta / total_mass));
+  const double xacc = temp - polemass_length * thetaacc * costheta / total_mass;
+  s[0] = s[0] + tau * s[1];
+  s[1] = s[1] + tau * xacc;
+  s[2] = s[2] + tau * s[3];
+  s[3] = s[3] + tau * thetaacc;
+  const double theta_thr = 12.0 * 2.0 * 3.141592653589793 / 360.0;
+  return s[0] < -2.4 || s[0] > 2.4 || s[2] < -theta_thr || s[2] > theta_thr;
+}
+
+template <int OBS, int A>
+__global__ __launch_bounds__(256) void mlp_rollout_kernel(XaRolloutArgs p) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int env = blockIdx.x * kWaves + wid;
+  if (env >= p.n_envs) return;  // wave-uniform; no block barriers below
+  const int T = p.n_steps;
+  float* sh = smem + wid * H;
+  const bool fused = p.ret_out != nullptr && p.return_kind != XA_RETURNS_NONE;
+  float* hist = smem + kWaves * H + wid * 3 * T;  // [rew | val | done] per wave when fused
+
+  LaneMlp<OBS, A> net;
+  net.load(p.theta, lane);
+
+  const uint64_t ctr = p.rng_counter ? *p.rng_counter : 0ull;
+  const uint32_t k0 = (uint32_t)p.seed, k1 = (uint32_t)(p.seed >> 32);
+
+  float x[OBS];  // policy input (wave-uniform)
+  float st[OBS]; // post-reset env state
+#pragma unroll
+  for (int k = 0; k < OBS; ++k) st[k] = x[k] = p.env_state[(size_t)env * OBS + k];
+  double cp[4] = {0.0, 0.0, 0.0, 0.0};
+  if (p.env_kind == XA_ENV_CARTPOLE) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) cp[k] = p.env_state64[(size_t)env * 4 + k];
+  }
+  int cur = p.env_cursor[env];
+  float ep_ret = p.ep_return[env];
+  float d_last = p.env_done[env];
+  if (lane == 0) p.done_out[(size_t)env * (T + 1)] = d_last;
+
+  // replay prefetch of step 0 (the record stream does not depend on actions)
+  float n_obs[OBS], n_st[OBS], n_r = 0.0f, n_d = 0.0f;
+  auto fetch = [&](int c) {
+    const size_t base = (size_t)env * p.t_rec + c;
+#pragma unroll
+    for (int k = 0; k < OBS; ++k) {
+      n_obs[k] = p.rep_obs[base * OBS + k];
+      n_st[k] = p.rep_state[base * OBS + k];
+    }
+    n_r = p.rep_rew[base];
+    n_d = p.rep_done[base];
+  };
+  if (p.env_kind == XA_ENV_REPLAY) fetch(cur);
+
+  for (int t = 0; t < T; ++t) {
+    const size_t it = (size_t)env * T + t;
+    float logits[A], value;
+    net.forward(x, sh, lane, logits, value);
+    float u = 0.0f;
+    if (p.uniforms) {
+      u = p.uniforms[it];
+    } else {
+      const xa_u4 r = xa_philox((uint32_t)env, (uint32_t)t, (uint32_t)ctr, (uint32_t)(ctr >> 32),
+                                k0, k1);
+      u = xa_u01(r.x);
+    }
+    const CatOut<A> c = categorical<A>(logits, u, -1);
+    if (lane < OBS) p.obs_out[it * OBS + lane] = x[lane];
+    // env step
+    float r, d;
+    float o_obs[OBS];
+    if (p.env_kind == XA_ENV_REPLAY) {
+      r = n_r;
+      d = n_d;
+#pragma unroll
+      for (int k = 0; k < OBS; ++k) {
+        o_obs[k] = n_obs[k];
+        st[k] = n_st[k];
+      }
+      cur = cur + 1;
+      if (cur >= p.t_rec) cur = 0;
+      if (t + 1 < T) fetch(cur);
+    } else {
+      bool done = cartpole_step(cp, c.action);
+      cur = cur + 1;
+      if (cur >= p.max_episode_steps) done = true;  // gym TimeLimit
+      r = 1.0f;
+      d = done ? 1.0f : 0.0f;
+#pragma unroll
+      for (int k = 0; k < OBS; ++k) o_obs[k] = (float)cp[k < 4 ? k : 3];
+      if (done) {
+        // reset: np_random.uniform(-0.05, 0.05, size=(4,))
+        const xa_u4 rr = xa_philox((uint32_t)env, (uint32_t)t, (uint32_t)ctr,
+                                   (uint32_t)(ctr >> 32) ^ 0x5eed5eedu, k0, k1);
+        const uint32_t rv[4] = {rr.x, rr.y, rr.z, rr.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) cp[k] = -0.05 + 0.1 * ((double)rv[k] * 2.3283064365386963e-10);
+        cur = 0;
+      }
+#pragma unroll
+      for (int k = 0; k < OBS; ++k) st[k] = (float)cp[k < 4 ? k : 3];
+    }
+    ep_ret = ep_ret + r;
+    if (lane == 0) {
+      p.act_out[it] = c.action;
+      p.logp_out[it] = c.logp;
+      p.val_out[it] = value;
+      if (p.ent_out) p.ent_out[it] = c.entropy;
+      p.rew_out[it] = r;
+      p.done_out[(size_t)env * (T + 1) + t + 1] = d;
+      if (p.epret_out) p.epret_out[it] = ep_ret;
+    }
+    if (fused && lane == 0) {
+      hist[t] = r;
+      hist[T + t] = value;
+      hist[2 * T + t] = d;
+    }
+    if (d != 0.0f) ep_ret = 0.0f;
+    d_last = d;
+#pragma unroll
+    for (int k = 0; k < OBS; ++k) x[k] = o_obs[k];  // pre-reset obs feeds the next step
+  }
+
+  // bootstrap V(get_states()) on the post-reset state (ppo/agent.py:72)
+  float logits[A], v_next;
+  net.forward(st, sh, lane, logits, v_next);
+  if (lane < OBS) p.env_state[(size_t)env * OBS + lane] = st[lane];
+  if (p.env_kind == XA_ENV_CARTPOLE && lane < 4) p.env_state64[(size_t)env * 4 + lane] = cp[lane];
+  if (lane == 0) {
+    p.env_cursor[env] = cur;
+    p.ep_return[env] = ep_ret;
+    p.env_done[env] = d_last;
+    p.next_val[env] = v_next;
+  }
+  if (fused && lane == 0) {
+    wave_sync();
+    const float* hr = hist;
+    const float* hv = hist + T;
+    const float* hd = hist + 2 * T;
+    float* out = p.ret_out + (size_t)env * T;
+    if (p.return_kind == XA_RETURNS_GAE) {
+      float carry = 0.0f, vn = v_next;
+      for (int t = T - 1; t >= 0; --t) {
+        const float nnt = 1.0f - hd[t];
+        const float vt = hv[t];
+        const float delta = (hr[t] + (p.gamma * vn) * nnt) - vt;
+        carry = delta + ((p.gamma_lam * nnt) * carry);
+        out[t] = carry + vt;
+        vn = vt;
+      }
+    } else {
+      float carry = v_next;
+      for (int t = T - 1; t >= 0; --t) {
+        const float nnt = 1.0f - hd[t];
+        carry = hr[t] + (p.gamma * carry) * nnt;
+        out[t] = carry;
+      }
+    }
+  }
+}
+
+// Batched forward: one wave per sample (a2c/agent.py:65-94).
+template <int OBS, int A>
+__global__ __launch_bounds__(256) void mlp_forward_kernel(const float* __restrict__ theta,
+                                                          const float* __restrict__ obs, int B,
+                                                          const int* __restrict__ actions_in,
+                                                          const float* __restrict__ uniforms,
+                                                          int* actions_out, float* logp,
+                                                          float* value, float* entropy,
+                                                          float* logits_out) {
+  __shared__ __attribute__((aligned(16))) float smem[kWaves * H];
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  LaneMlp<OBS, A> net;
+  net.load(theta, lane);
+  for (int b = blockIdx.x * kWaves + wid; b < B; b += gridDim.x * kWaves) {
+    float x[OBS];
+#pragma unroll
+    for (int k = 0; k < OBS; ++k) x[k] = obs[(size_t)b * OBS + k];
+    float l[A], v;
+    net.forward(x, smem + wid * H, lane, l, v);
+    const int given = actions_in ? actions_in[b] : -1;
+    const float u = (given < 0 && uniforms) ? uniforms[b] : 0.0f;
+    const CatOut<A> c = categorical<A>(l, u, given);
+    if (lane == 0) {
+      if (actions_out) actions_out[b] = c.action;
+      if (logp) logp[b] = c.logp;
+      if (value) value[b] = v;
+      if (entropy) entropy[b] = c.entropy;
+    }
+    if (logits_out && lane < A) {
+#pragma unroll
+      for (int a = 0; a < A; ++a)
+        if (lane == a) logits_out[(size_t)b * A + a] = l[a];
+    }
+  }
+}
+
+template <int OBS, int A>
+int launch_rollout(const XaRolloutArgs* p, hipStream_t s) {
+  const bool fused = p->ret_out != nullptr && p->return_kind != XA_RETURNS_NONE;
+  const size_t lds = (size_t)kWaves * H * sizeof(float) +
+                     (fused ? (size_t)kWaves * 3 * p->n_steps * sizeof(float) : 0);
+  dim3 grid((p->n_envs + kWaves - 1) / kWaves);
+  hipLaunchKernelGGL((mlp_rollout_kernel<OBS, A>), grid, dim3(256), lds, s, *p);
+  XA_CHECK_LAUNCH("xa_mlp_rollout");
+  return 0;
+}
+
+template <int OBS, int A>
+int launch_forward(const float* theta, const float* obs, int B, const int* ain, const float* u,
+                   int* aout, float* logp, float* value, float* ent, float* logits,
+                   hipStream_t s) {
+  const int blocks = min((B + kWaves - 1) / kWaves, 2048);
+  hipLaunchKernelGGL((mlp_forward_kernel<OBS, A>), dim3(blocks), dim3(256), 0, s, theta, obs, B,
+                     ain, u, aout, logp, value, ent, logits);
+  XA_CHECK_LAUNCH("xa_mlp_forward");
+  return 0;
+}
+
+#define XA_DISPATCH_OBS_A(OBSV, AV, CALL)                                  \
+  if (obs_dim == OBSV && n_actions == AV) return CALL<OBSV, AV>
+
+}  // namespace
+
+extern "C" int xa_mlp_rollout(const XaRolloutArgs* p, void* stream) {
+  XA_CHECK_ARG(p != nullptr, "xa_mlp_rollout: null args");
+  XA_CHECK_ARG(p->n_envs > 0 && p->n_steps > 0, "xa_mlp_rollout: n_envs, n_steps must be > 0");
+  XA_CHECK_ARG(p->theta && p->env_state && p->env_done && p->env_cursor && p->ep_return,
+               "xa_mlp_rollout: null env/param pointer");
+  XA_CHECK_ARG(p->obs_out && p->act_out && p->logp_out && p->val_out && p->rew_out &&
+                   p->done_out && p->next_val,
+               "xa_mlp_rollout: null output pointer");
+  if (p->env_kind == XA_ENV_REPLAY) {
+    XA_CHECK_ARG(p->rep_obs && p->rep_state && p->rep_rew && p->rep_done && p->t_rec > 0,
+                 "xa_mlp_rollout: replay env needs rep_obs/rep_state/rep_rew/rep_done/t_rec");
+  } else if (p->env_kind == XA_ENV_CARTPOLE) {
+    XA_CHECK_ARG(p->env_state64 && p->obs_dim == 4 && p->n_actions == 2 &&
+                     p->max_episode_steps > 0,
+                 "xa_mlp_rollout: cartpole env needs env_state64, obs_dim 4, 2 actions");
+  } else {
+    XA_CHECK_ARG(false, "xa_mlp_rollout: unknown env_kind %d", p->env_kind);
+  }
+  XA_CHECK_ARG(p->ret_out == nullptr || p->return_kind == XA_RETURNS_NONE ||
+                   p->n_steps <= kFusedMaxT,
+               "xa_mlp_rollout: fused returns need n_steps <= %d (use xa_gae)", kFusedMaxT);
+  XA_CHECK_ARG(p->uniforms || p->rng_counter, "xa_mlp_rollout: need uniforms or rng_counter");
+  const int obs_dim = p->obs_dim, n_actions = p->n_actions;
+  hipStream_t s = (hipStream_t)stream;
+  XA_DISPATCH_OBS_A(4, 2, launch_rollout)(p, s);
+  XA_DISPATCH_OBS_A(6, 3, launch_rollout)(p, s);
+  XA_DISPATCH_OBS_A(8, 4, launch_rollout)(p, s);
+  XA_DISPATCH_OBS_A(2, 3, launch_rollout)(p, s);
+  xa_set_error("xa_mlp_rollout: unsupported (obs_dim, n_actions) = (%d, %d)", obs_dim, n_actions);
+  return -3;
+}
+
+extern "C" int xa_mlp_forward(const float* theta, const float* obs, int batch, int obs_dim,
+                              int n_actions, const int* actions_in, const float* uniforms,
+                              int* actions_out, float* logp, float* value, float* entropy,
+                              float* logits, void* stream) {
+  XA_CHECK_ARG(theta && obs && batch > 0, "xa_mlp_forward: bad arguments");
+  XA_CHECK_ARG(actions_in || uniforms || !actions_out,
+               "xa_mlp_forward: sampling needs uniforms");
+  hipStream_t s = (hipStream_t)stream;
+  XA_DISPATCH_OBS_A(4, 2, launch_forward)(theta, obs, batch, actions_in, uniforms, actions_out,
+                                          logp, value, entropy, logits, s);
+  XA_DISPATCH_OBS_A(6, 3, launch_forward)(theta, obs, batch, actions_in, uniforms, actions_out,
+                                          logp, value, entropy, logits, s);
+  XA_DISPATCH_OBS_A(8, 4, launch_forward)(theta, obs, batch, actions_in, uniforms, actions_out,
+                                          logp, value, entropy, logits, s);
+  XA_DISPATCH_OBS_A(2, 3, launch_forward)(theta, obs, batch, actions_in, uniforms, actions_out,
+                                          logp, value, entropy, logits, s);
+  xa_set_error("xa_mlp_forward: unsupported (obs_dim, n_actions) = (%d, %d)", obs_dim, n_actions);
+  return -3;
+}

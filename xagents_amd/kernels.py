@@ -1,0 +1,110 @@
+"""Tensor-level wrappers over libxagents_hip.so (one function per C entry point).
+
+Shapes follow the C ABI (include/xagents_hip.h): env-major [n_envs, n_steps, ...].
+Every function runs asynchronously on torch's current stream and raises on error.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from xagents_amd import _lib
+from xagents_amd._lib import (XA_LOSS_A2C, XA_LOSS_PPO, XaAcGradArgs, XaRolloutArgs,
+                              XaShuffle, call, ptr, stream)
+
+
+def _f32(x):
+    return ctypes.c_float(float(np.float32(x)))
+
+
+def gamma_lam_f32(gamma, lam):
+    """The reference forms gamma*lam as a Python (f64) product before the f32 multiply
+    (xagents/ppo/agent.py:92)."""
+    return float(np.float32(float(gamma) * float(lam)))
+
+
+def mlp_param_count(obs_dim, n_actions):
+    return _lib.load().xa_mlp_param_count(obs_dim, n_actions)
+
+
+def gae(rewards, values, dones, next_values, gamma, lam, out=None):
+    """GAE returns (PPO.calculate_returns, xagents/ppo/agent.py:48-94).
+
+    rewards/values [N,T], dones [N,T+1], next_values [N] -> returns [N,T] f32.
+    """
+    n, t = rewards.shape
+    out = torch.empty_like(rewards) if out is None else out
+    call('xa_gae', ptr(rewards), ptr(values), ptr(dones), ptr(next_values), ptr(out), n, t,
+         _f32(gamma), _f32(gamma_lam_f32(gamma, lam)), stream())
+    return out
+
+
+def nstep_returns(rewards, dones, next_values, gamma, out=None):
+    """n-step returns (A2C.calculate_returns, xagents/a2c/agent.py:141-171)."""
+    n, t = rewards.shape
+    out = torch.empty_like(rewards) if out is None else out
+    call('xa_nstep_returns', ptr(rewards), ptr(dones), ptr(next_values), ptr(out), n, t,
+         _f32(gamma), stream())
+    return out
+
+
+def mlp_forward(theta, obs, n_actions, actions=None, uniforms=None, want_logits=False):
+    """Actor-critic forward (A2C.get_model_outputs, xagents/a2c/agent.py:65-94).
+
+    Returns (actions, log_probs, values, entropies, logits-or-None).
+    """
+    b, obs_dim = obs.shape
+    dev = obs.device
+    act_out = None if actions is not None else torch.empty(b, dtype=torch.int32, device=dev)
+    if actions is not None and actions.dtype != torch.int32:
+        actions = actions.to(torch.int32)
+    if actions is None and uniforms is None:
+        raise ValueError('mlp_forward: sampling needs `uniforms`')
+    logp = torch.empty(b, dtype=torch.float32, device=dev)
+    value = torch.empty(b, dtype=torch.float32, device=dev)
+    ent = torch.empty(b, dtype=torch.float32, device=dev)
+    logits = torch.empty(b, n_actions, dtype=torch.float32, device=dev) if want_logits else None
+    call('xa_mlp_forward', ptr(theta), ptr(obs.contiguous()), b, obs_dim, n_actions, ptr(actions),
+         ptr(uniforms), ptr(act_out), ptr(logp), ptr(value), ptr(ent), ptr(logits), stream())
+    return (actions if actions is not None else act_out), logp, value, ent, logits
+
+
+def rollout(args: XaRolloutArgs):
+    call('xa_mlp_rollout', ctypes.byref(args), stream())
+
+
+def counter_bump(counter):
+    call('xa_counter_bump', ptr(counter), stream())
+
+
+def adv_stats(returns, values, batch, mb_size, epochs, shuffle: XaShuffle, stats):
+    call('xa_ppo_adv_stats', ptr(returns), ptr(values), batch, mb_size, epochs,
+         ctypes.byref(shuffle), ptr(stats), stream())
+
+
+def ac_grad_blocks(mb_size):
+    return _lib.load().xa_ac_grad_blocks(mb_size)
+
+
+def ac_grad(args: XaAcGradArgs):
+    call('xa_ac_grad', ctypes.byref(args), stream())
+
+
+def grad_reduce(partials, grad, adam_step=None):
+    nb, p = partials.shape
+    call('xa_grad_reduce', ptr(partials), nb, p, ptr(grad), ptr(adam_step), stream())
+
+
+def clip_adam(theta, m, v, grad, adam_step, lr, beta1, beta2, eps, clip_norm=None,
+              grad_scale=1.0, workspace=None, gnorm_out=None):
+    """tf.clip_by_global_norm + Keras Adam (xagents/ppo/agent.py:135-137)."""
+    call('xa_clip_adam', ptr(theta), ptr(m), ptr(v), ptr(grad), theta.numel(), _f32(grad_scale),
+         _f32(clip_norm if clip_norm is not None else 0.0), _f32(lr), _f32(beta1), _f32(beta2),
+         _f32(eps), ptr(adam_step), ptr(workspace), ptr(gnorm_out), stream())
+
+
+__all__ = [
+    'XA_LOSS_A2C', 'XA_LOSS_PPO', 'XaAcGradArgs', 'XaRolloutArgs', 'XaShuffle', 'gae',
+    'nstep_returns', 'mlp_forward', 'rollout', 'counter_bump', 'adv_stats', 'ac_grad',
+    'ac_grad_blocks', 'grad_reduce', 'clip_adam', 'mlp_param_count', 'gamma_lam_f32',
+]

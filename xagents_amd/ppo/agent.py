@@ -1,0 +1,174 @@
+"""PPO with the xagents class surface (xagents/ppo/agent.py:7-225) on the fused
+MI355X path.
+
+train_step = one hipGraph replay of:
+    xa_mlp_rollout (n_steps x [forward, sample, env step, store] + GAE)
+    xa_ppo_adv_stats (per-minibatch adv sums, all epochs)  -> [RCCL all_reduce]
+    ppo_epochs x mini_batches x:
+        xa_ac_grad (shuffle-gather + fwd + clipped PPO loss + bwd, partial grads)
+        -> xa_grad_reduce -> [RCCL all_reduce] -> xa_clip_adam
+    xa_counter_bump
+Multi-GPU: every rank owns n_envs envs (weak scaling); the minibatch of a step is the
+union of the ranks' local minibatches, advantage normalisation and the loss mean use
+the global statistics/count, so the update equals a single-GPU update on the union.
+"""
+import numpy as np
+import torch
+
+from xagents_amd import kernels
+from xagents_amd._lib import XA_RETURNS_GAE, XaShuffle
+from xagents_amd.a2c.agent import A2C
+
+
+class PPO(A2C):
+    """Proximal Policy Optimization Algorithms https://arxiv.org/abs/1707.06347"""
+
+    loss_kind = kernels.XA_LOSS_PPO
+    return_kind = XA_RETURNS_GAE
+
+    def __init__(
+        self,
+        envs,
+        model,
+        lam=0.95,
+        ppo_epochs=4,
+        mini_batches=4,
+        advantage_epsilon=1e-8,
+        clip_norm=0.1,
+        **kwargs,
+    ):
+        self.lam = lam
+        self.ppo_epochs = ppo_epochs
+        self.mini_batches = mini_batches
+        self.advantage_epsilon = advantage_epsilon
+        self.clip_norm = clip_norm
+        n_envs = len(envs)
+        n_steps = kwargs.get('n_steps', 1)
+        self.batch_size = n_envs * n_steps
+        self.mini_batch_size = self.batch_size // self.mini_batches
+        assert (
+            self.mini_batch_size > 0
+        ), f'Invalid batch size to mini-batch size ratio {self.batch_size}: {self.mini_batches}'
+        super(PPO, self).__init__(envs, model, **kwargs)
+
+    def _setup_update(self):
+        B, MB, E = self.batch_size, self.mini_batch_size, self.ppo_epochs
+        # range(0, B, MB) slicing: a ragged last minibatch when MB does not divide B
+        # (xagents/ppo/agent.py:152)
+        self.n_mb = (B + MB - 1) // MB
+        nb = kernels.ac_grad_blocks(MB)
+        dev = self.device
+        self.partials = torch.zeros(nb, self.model.n_params, dtype=torch.float32, device=dev)
+        self.loss_partials = torch.zeros(nb, 4, dtype=torch.float32, device=dev)
+        self.adv_stats = torch.zeros(E * self.n_mb * 2, dtype=torch.float64, device=dev)
+        self.shuffle = XaShuffle()
+        self.shuffle.perm = None
+        self.shuffle.seed = self.rng_seed ^ 0x9E3779B97F4A7C15
+        self.shuffle.rng_counter = self.rng_counter.data_ptr()
+        self._gargs_list = []
+        for e in range(E):
+            for m in range(self.n_mb):
+                g = self._grad_args(MB, nb, self.partials, self.loss_partials)
+                g.epoch, g.mb_index = e, m
+                g.shuffle = self.shuffle
+                count = min(MB, B - m * MB)
+                g.adv_stats = self.adv_stats.data_ptr()
+                g.adv_count = float(count * self.world_size)
+                g.adv_in = None
+                g.loss_scale = 1.0 / (count * self.world_size)
+                self._gargs_list.append(g)
+
+    def _update(self):
+        B, MB = self.batch_size, self.mini_batch_size
+        kernels.adv_stats(self.b_ret, self.b_val, B, MB, self.ppo_epochs, self.shuffle,
+                          self.adv_stats)
+        self._all_reduce(self.adv_stats)
+        for g in self._gargs_list:
+            kernels.ac_grad(g)
+            self._apply_gradients(self.partials)
+
+    # ---- reference-level pieces --------------------------------------------
+    def calculate_returns(self, rewards, dones, values=None, selected_critic_logits=None,
+                          selected_importance=None):
+        """GAE from time-major rewards [T,N], dones [T+1,N], values [T,N]
+        (xagents/ppo/agent.py:48-94); bootstraps on V(get_states())."""
+        next_values = self.get_model_outputs(self.get_states(), self.output_models)[2]
+        f = lambda x: torch.as_tensor(x, dtype=torch.float32,  # noqa: E731
+                                      device=self.device).reshape(x.shape[0], -1).t().contiguous()
+        ret = kernels.gae(f(rewards), f(values), f(dones), next_values.contiguous(), self.gamma,
+                          self.lam)
+        return ret.t()
+
+    def get_batch(self):
+        """Fused rollout + GAE; returns env-major flat [states, actions, returns, values,
+        log_probs] exactly as concat_step_batches lays them out
+        (xagents/ppo/agent.py:193-213, xagents/base.py:549-564)."""
+        a = self._rargs
+        kernels.rollout(a)
+        kernels.counter_bump(self.rng_counter)
+        self.steps += self.n_envs * self.n_steps
+        self._queue_episode_stats(self.b_done, self.b_epret)
+        B = self.batch_size
+        return [self.b_obs.reshape(B, -1), self.b_act.reshape(B).float(),
+                self.b_ret.reshape(B), self.b_val.reshape(B), self.b_logp.reshape(B)]
+
+    def get_mini_batches(self, *args):
+        """Per epoch: reshuffle, then contiguous minibatch slices
+        (xagents/ppo/agent.py:139-155)."""
+        mini_batches = []
+        indices = torch.arange(self.batch_size, device=self.device)
+        for _ in range(self.ppo_epochs):
+            indices = indices[torch.randperm(self.batch_size, device=self.device)]
+            for i in range(0, self.batch_size, self.mini_batch_size):
+                batch_indices = indices[i: i + self.mini_batch_size]
+                mini_batches.append([item[batch_indices] for item in args])
+        return mini_batches
+
+    def update_gradients(self, states, actions, old_values, returns, old_log_probs, advantages):
+        """One clipped-PPO Adam step on a given minibatch (xagents/ppo/agent.py:96-137)."""
+        n = states.shape[0]
+        dev = self.device
+        c = lambda x, dt=torch.float32: torch.as_tensor(  # noqa: E731
+            x, device=dev).to(dt).reshape(n, -1).squeeze(-1).contiguous()
+        obs = torch.as_tensor(states, device=dev).float().reshape(n, -1).contiguous()
+        act, oldv, ret = c(actions, torch.int32), c(old_values), c(returns)
+        oldlp, adv = c(old_log_probs), c(advantages)
+        nb = kernels.ac_grad_blocks(n)
+        partials = torch.zeros(nb, self.model.n_params, dtype=torch.float32, device=dev)
+        lossp = torch.zeros(nb, 4, dtype=torch.float32, device=dev)
+        g = self._grad_args(n, nb, partials, lossp)
+        g.batch = n
+        g.epoch = g.mb_index = 0
+        ident = torch.arange(n, dtype=torch.int32, device=dev)
+        sh = XaShuffle()
+        sh.perm, sh.seed, sh.rng_counter = ident.data_ptr(), 0, None
+        g.shuffle = sh
+        g.obs, g.actions, g.old_logp = obs.data_ptr(), act.data_ptr(), oldlp.data_ptr()
+        g.old_values, g.returns, g.adv_in = oldv.data_ptr(), ret.data_ptr(), adv.data_ptr()
+        g.adv_stats, g.adv_count = None, 0.0
+        g.loss_scale = 1.0 / (n * self.world_size)
+        kernels.ac_grad(g)
+        self._apply_gradients(partials)
+        lp = lossp.sum(0)
+        return {'pg_loss': lp[0] / lp[3], 'value_loss': 0.5 * lp[1] / lp[3],
+                'entropy': lp[2] / lp[3]}
+
+    def run_ppo_epochs(self, states, actions, returns, old_values, old_log_probs):
+        """Minibatch loop with per-minibatch advantage normalisation
+        (xagents/ppo/agent.py:157-191)."""
+        for states_mb, actions_mb, returns_mb, old_values_mb, old_log_probs_mb in (
+                self.get_mini_batches(states, actions, returns, old_values, old_log_probs)):
+            adv = returns_mb - old_values_mb
+            adv = (adv - adv.mean()) / (adv.std(unbiased=False) + self.advantage_epsilon)
+            self.update_gradients(states_mb, actions_mb, old_values_mb, returns_mb,
+                                  old_log_probs_mb, adv)
+
+    def train_step(self):
+        hooks = ('get_batch', 'calculate_returns', 'update_gradients', 'run_ppo_epochs',
+                 'get_mini_batches')
+        if any(getattr(type(self), h) is not getattr(PPO, h) for h in hooks):
+            # a subclass overrode a reference hook: compose the pieces instead of
+            # the fused graph so the override is honoured
+            self.run_ppo_epochs(*self.get_batch())
+            return
+        self.fused_train_step()
