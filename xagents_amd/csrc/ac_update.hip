@@ -1,18 +1,22 @@
 // Actor-critic update for the MLP: minibatch shuffle/gather, per-minibatch
-// advantage statistics, fused forward + PPO/A2C loss + backward, gradient
-// reduction, tf.clip_by_global_norm + Keras Adam.
+// advantage statistics, fused forward + PPO/A2C loss + backward, deterministic
+// gradient reduction fused with tf.clip_by_global_norm + Keras Adam.
 //
 // Replaces PPO.get_mini_batches / run_ppo_epochs / update_gradients
 // (xagents/ppo/agent.py:96-191) and A2C.train_step (xagents/a2c/agent.py:190-218).
 //
-// xa_ac_grad schedule: a workgroup of 256 threads walks 64-sample tiles of the
-// minibatch. Weights (W2 in both orientations) sit in LDS; every activation and
-// back-propagated tile is an LDS-resident [64 x 64] f32 tile, and the three
-// 64x64x64 products (H1*W2, H1^T*dA2, dA2*W2^T) run as 16x16 thread grids with
-// 4x4 register tiles fed by ds_read_b128 (conflict-free: one operand broadcast
-// across 16 lanes, the other one 256 contiguous bytes). Weight gradients stay in
-// registers across tiles and each block writes ONE partial-gradient row; the
-// rows are summed in f64 in fixed order by xa_grad_reduce (deterministic).
+// xa_ac_grad schedule (one 256-thread workgroup per 32-sample tile, 4 waves):
+//   gather X -> H1 = tanh(X W1 + b1)               (VALU, K = obs)
+//   Z2 = H1 W2                                      (MFMA f32 16x16x4, K = 64)
+//   heads + loss + dL/dz, 8 lanes per sample        (VALU + xor shuffles)
+//   dA2 = (dZ W34^T) * (1 - H2^2)                   (VALU, K = A + 1)
+//   dW2 += H1^T dA2  and  dH1 = dA2 W2^T            (MFMA f32 16x16x4, K = 32 / 64)
+//   dW1 += X^T dA1                                  (VALU, K = 32)
+// Every operand of an MFMA is read from LDS as contiguous 16-byte rows: the K index
+// that lane group q feeds is remapped to a contiguous block (k = 16q + kk), which
+// only reorders the f32 accumulation (tolerance-checked against float64).
+// Weight gradients stay in registers over the tiles a block walks; each block
+// writes ONE partial-gradient row, reduced in f64 in fixed order (deterministic).
 #include <math.h>
 
 #include "../../include/xagents_hip.h"
@@ -21,7 +25,19 @@
 namespace {
 
 constexpr int H = XA_MLP_HIDDEN;
-constexpr int S = 64;  // samples per tile
+constexpr int S = 32;    // samples per tile
+constexpr int LDW = 68;  // LDS row stride of [*][64] tiles (16-B aligned, conflict-spreading)
+constexpr int LDT = 36;  // LDS row stride of transposed [64][32] tiles
+constexpr int kStatsChunk = 1024;
+constexpr int kRedParams = 16, kRedGroups = 16;
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// D = A B + C on a 16x16 tile, K = 4: lane l feeds A[l&15][k=l>>4], B[k=l>>4][l&15];
+// D[row = 4*(l>>4) + r][col = l&15] lands in register r (exact f32 fma chain).
+XA_DEV f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
 
 struct Offs {
   int w1, b1, w2, b2, w3, b3, w4, b4, P;
@@ -67,20 +83,24 @@ XA_DEV int shuffle_index(const XaShuffle& sh, const ShuffleKeys& keys, int epoch
                          keys.k[2], keys.k[3]);
 }
 
+__host__ __device__ inline int stats_chunks(int mb_size) { return (mb_size + kStatsChunk - 1) / kStatsChunk; }
+
 // ---------------------------------------------------------------------------
-// advantage statistics: one block per (epoch, minibatch)
+// advantage statistics: one block per (epoch, minibatch, 1024-sample chunk)
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void adv_stats_kernel(const float* __restrict__ ret,
                                                         const float* __restrict__ val, int batch,
-                                                        int mb_size, int n_mb, XaShuffle sh,
-                                                        double* stats) {
+                                                        int mb_size, int n_mb, int n_chunks,
+                                                        XaShuffle sh, double* stats) {
   __shared__ double red[2][4];
-  const int e = blockIdx.x / n_mb, m = blockIdx.x % n_mb;
+  const int sidx = blockIdx.x / n_chunks, chunk = blockIdx.x % n_chunks;
+  const int e = sidx / n_mb, m = sidx % n_mb;
   const ShuffleKeys keys = shuffle_keys(sh, e, batch);
   const int start = m * mb_size;
   const int cnt = min(mb_size, batch - start);
+  const int q0 = chunk * kStatsChunk, q1 = min(cnt, q0 + kStatsChunk);
   double s1 = 0.0, s2 = 0.0;
-  for (int q = threadIdx.x; q < cnt; q += blockDim.x) {
+  for (int q = q0 + (int)threadIdx.x; q < q1; q += blockDim.x) {
     const int idx = shuffle_index(sh, keys, e, batch, start + q);
     const float adv = ret[idx] - val[idx];
     s1 += (double)adv;
@@ -105,31 +125,40 @@ __global__ __launch_bounds__(256) void adv_stats_kernel(const float* __restrict_
 // ---------------------------------------------------------------------------
 template <int OBS, int A>
 __global__ __launch_bounds__(256) void ac_grad_kernel(XaAcGradArgs p) {
-  constexpr int AH = A + 1;  // logits + value head
-  __shared__ __attribute__((aligned(16))) float sW2[H * H];
-  __shared__ __attribute__((aligned(16))) float sW2T[H * H];
-  __shared__ __attribute__((aligned(16))) float sH1[S * H];   // [s][i]
-  __shared__ __attribute__((aligned(16))) float sH1T[H * S];  // [i][s]
-  __shared__ __attribute__((aligned(16))) float sH2[S * H];   // [s][j]
-  __shared__ __attribute__((aligned(16))) float sH2T[H * S];  // [j][s]; reused as dA1 [s][i]
-  __shared__ __attribute__((aligned(16))) float sdA2[S * H];  // [s][j]
-  __shared__ __attribute__((aligned(16))) float sdA2T[H * S]; // [j][s]
+  constexpr int AH = A + 1;           // logits + value head
+  constexpr int NSLOT = AH + 2 + OBS; // per-feature partial sums combined at the end
+  __shared__ __attribute__((aligned(16))) float sW2[H * LDW];   // [i][j]
+  __shared__ __attribute__((aligned(16))) float sW2T[H * LDW];  // [j][k] = W2[k][j]
+  __shared__ __attribute__((aligned(16))) float sH1[S * LDW];   // [s][i]
+  __shared__ __attribute__((aligned(16))) float sH1T[H * LDT];  // [i][s]
+  __shared__ __attribute__((aligned(16))) float sH2[S * LDW];   // [s][j]; then dA1 [s][i]
+  __shared__ __attribute__((aligned(16))) float sdA2[S * LDW];  // [s][j]
+  __shared__ __attribute__((aligned(16))) float sdA2T[H * LDT]; // [j][s]
   __shared__ float sW1[OBS * H], sb1[H], sb2[H], sW34[H * AH], sb34[AH];
-  __shared__ float sX[S * OBS];
-  __shared__ float sdZ[S * AH];
+  __shared__ float sX[S * OBS], sdZ[S * AH];
   __shared__ int sIdx[S];
+  __shared__ float sRed[4 * H * NSLOT];
   __shared__ float sLoss[4][4];
 
   const Offs o = offs(OBS, A);
   const int tid = threadIdx.x;
-  const int ti = tid >> 4, tj = tid & 15;
-  const int r0 = ti * 4, c0 = tj * 4;
+  const int lane = tid & 63, w = tid >> 6;
+  const int li = lane & 15, lq = lane >> 4;  // MFMA lane coordinates
+  const int f = tid & 63, c8 = (tid >> 6) * 8;  // element-wise phases: feature, 8-sample chunk
   const float* __restrict__ th = p.theta;
 
-  for (int i = tid; i < H * H; i += 256) {
-    const float w = th[o.w2 + i];
-    sW2[i] = w;
-    sW2T[(i & 63) * H + (i >> 6)] = w;
+  {  // W2 in both orientations: each thread moves one 4x4 sub-block
+    const int k0 = 4 * (tid >> 4), j0 = 4 * (tid & 15);
+    float4 r[4];
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr)
+      r[rr] = *reinterpret_cast<const float4*>(&th[o.w2 + (k0 + rr) * H + j0]);
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) *reinterpret_cast<float4*>(&sW2[(k0 + rr) * LDW + j0]) = r[rr];
+    *reinterpret_cast<float4*>(&sW2T[(j0 + 0) * LDW + k0]) = make_float4(r[0].x, r[1].x, r[2].x, r[3].x);
+    *reinterpret_cast<float4*>(&sW2T[(j0 + 1) * LDW + k0]) = make_float4(r[0].y, r[1].y, r[2].y, r[3].y);
+    *reinterpret_cast<float4*>(&sW2T[(j0 + 2) * LDW + k0]) = make_float4(r[0].z, r[1].z, r[2].z, r[3].z);
+    *reinterpret_cast<float4*>(&sW2T[(j0 + 3) * LDW + k0]) = make_float4(r[0].w, r[1].w, r[2].w, r[3].w);
   }
   for (int i = tid; i < OBS * H; i += 256) sW1[i] = th[o.w1 + i];
   if (tid < H) {
@@ -150,33 +179,36 @@ __global__ __launch_bounds__(256) void ac_grad_kernel(XaAcGradArgs p) {
   if (is_ppo) keys = shuffle_keys(p.shuffle, p.epoch, p.batch);
   float adv_mean = 0.0f, adv_std = 0.0f;
   if (is_ppo && p.adv_in == nullptr) {
-    const int sidx = p.epoch * ((p.batch + p.mb_size - 1) / p.mb_size) + p.mb_index;
+    const int n_mb = (p.batch + p.mb_size - 1) / p.mb_size;
+    const int sidx = p.epoch * n_mb + p.mb_index;
+    const int nc = stats_chunks(p.mb_size);
+    double s1 = 0.0, s2 = 0.0;
+    for (int c = 0; c < nc; ++c) {
+      s1 += p.adv_stats[2 * ((size_t)sidx * nc + c)];
+      s2 += p.adv_stats[2 * ((size_t)sidx * nc + c) + 1];
+    }
     const double n = p.adv_count;
-    const double mean = p.adv_stats[2 * sidx] / n;
-    const double var = fmax(p.adv_stats[2 * sidx + 1] / n - mean * mean, 0.0);
+    const double mean = s1 / n;
+    const double var = fmax(s2 / n - mean * mean, 0.0);
     adv_mean = (float)mean;
     adv_std = (float)sqrt(var);
   }
 
   // register accumulators
-  float gW2[4][4];
+  f32x4 gW2[4];
 #pragma unroll
-  for (int a = 0; a < 4; ++a)
+  for (int jt = 0; jt < 4; ++jt) gW2[jt] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  float gW34[AH], gW1[OBS];
 #pragma unroll
-    for (int b = 0; b < 4; ++b) gW2[a][b] = 0.0f;
-  constexpr int NW34 = (H * AH + 255) / 256;
-  constexpr int NW1 = (OBS * H + 255) / 256;
-  float gW34[NW34], gW1[NW1];
+  for (int a = 0; a < AH; ++a) gW34[a] = 0.0f;
 #pragma unroll
-  for (int q = 0; q < NW34; ++q) gW34[q] = 0.0f;
-#pragma unroll
-  for (int q = 0; q < NW1; ++q) gW1[q] = 0.0f;
+  for (int k = 0; k < OBS; ++k) gW1[k] = 0.0f;
   float gb1 = 0.0f, gb2 = 0.0f, gb34 = 0.0f;
   float l_pg = 0.0f, l_v = 0.0f, l_ent = 0.0f, l_cnt = 0.0f;
 
   for (int tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
     __syncthreads();
-    // ---- P1: gather ----
+    // ---- gather ----
     if (tid < S) {
       const int q = tile * S + tid;
       int idx = -1;
@@ -191,311 +223,381 @@ __global__ __launch_bounds__(256) void ac_grad_kernel(XaAcGradArgs p) {
       sX[e] = idx >= 0 ? p.obs[(size_t)idx * OBS + k] : 0.0f;
     }
     __syncthreads();
-    // ---- P2: H1 = tanh(X W1 + b1) ----
+    // ---- H1 = tanh(X W1 + b1): feature f, samples c8..c8+7 ----
     {
-      float h[4][4];
+      float hv[8];
 #pragma unroll
-      for (int ii = 0; ii < 4; ++ii)
+      for (int ss = 0; ss < 8; ++ss) {
+        const int s = c8 + ss;
+        float z = 0.0f;
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          float z = 0.0f;
-#pragma unroll
-          for (int k = 0; k < OBS; ++k) z = fmaf(sX[(r0 + ii) * OBS + k], sW1[k * H + c0 + jj], z);
-          h[ii][jj] = xa_tanhf(z + sb1[c0 + jj]);
-        }
-#pragma unroll
-      for (int ii = 0; ii < 4; ++ii)
-        *reinterpret_cast<float4*>(&sH1[(r0 + ii) * H + c0]) =
-            make_float4(h[ii][0], h[ii][1], h[ii][2], h[ii][3]);
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj)
-        *reinterpret_cast<float4*>(&sH1T[(c0 + jj) * S + r0]) =
-            make_float4(h[0][jj], h[1][jj], h[2][jj], h[3][jj]);
-    }
-    __syncthreads();
-    // ---- P3: H2 = tanh(H1 W2 + b2) ----
-    {
-      float acc[4][4];
-#pragma unroll
-      for (int ii = 0; ii < 4; ++ii)
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) acc[ii][jj] = 0.0f;
-#pragma unroll 8
-      for (int k = 0; k < H; ++k) {
-        const float4 a4 = *reinterpret_cast<const float4*>(&sH1T[k * S + r0]);
-        const float4 b4 = *reinterpret_cast<const float4*>(&sW2[k * H + c0]);
-        const float av[4] = {a4.x, a4.y, a4.z, a4.w};
-        const float bv[4] = {b4.x, b4.y, b4.z, b4.w};
-#pragma unroll
-        for (int ii = 0; ii < 4; ++ii)
-#pragma unroll
-          for (int jj = 0; jj < 4; ++jj) acc[ii][jj] = fmaf(av[ii], bv[jj], acc[ii][jj]);
+        for (int k = 0; k < OBS; ++k) z = fmaf(sX[s * OBS + k], sW1[k * H + f], z);
+        hv[ss] = xa_tanhf(z + sb1[f]);
+        sH1[s * LDW + f] = hv[ss];
       }
-#pragma unroll
-      for (int ii = 0; ii < 4; ++ii)
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) acc[ii][jj] = xa_tanhf(acc[ii][jj] + sb2[c0 + jj]);
-#pragma unroll
-      for (int ii = 0; ii < 4; ++ii)
-        *reinterpret_cast<float4*>(&sH2[(r0 + ii) * H + c0]) =
-            make_float4(acc[ii][0], acc[ii][1], acc[ii][2], acc[ii][3]);
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj)
-        *reinterpret_cast<float4*>(&sH2T[(c0 + jj) * S + r0]) =
-            make_float4(acc[0][jj], acc[1][jj], acc[2][jj], acc[3][jj]);
+      *reinterpret_cast<float4*>(&sH1T[f * LDT + c8]) = make_float4(hv[0], hv[1], hv[2], hv[3]);
+      *reinterpret_cast<float4*>(&sH1T[f * LDT + c8 + 4]) = make_float4(hv[4], hv[5], hv[6], hv[7]);
     }
     __syncthreads();
-    // ---- P4: heads + loss + dL/dz (one thread per sample) ----
-    if (tid < S) {
-      const int s = tid;
-      const int idx = sIdx[s];
+    // ---- Z2 = H1 W2 (MFMA): wave w owns hidden columns 16w..16w+15 ----
+    {
+      float bv[16];
+#pragma unroll
+      for (int v4 = 0; v4 < 4; ++v4) {
+        const float4 t4 = *reinterpret_cast<const float4*>(&sW2T[(16 * w + li) * LDW + 16 * lq + 4 * v4]);
+        bv[4 * v4] = t4.x; bv[4 * v4 + 1] = t4.y; bv[4 * v4 + 2] = t4.z; bv[4 * v4 + 3] = t4.w;
+      }
+      const float bias = sb2[16 * w + li];
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        float av[16];
+#pragma unroll
+        for (int v4 = 0; v4 < 4; ++v4) {
+          const float4 t4 = *reinterpret_cast<const float4*>(&sH1[(16 * st + li) * LDW + 16 * lq + 4 * v4]);
+          av[4 * v4] = t4.x; av[4 * v4 + 1] = t4.y; av[4 * v4 + 2] = t4.z; av[4 * v4 + 3] = t4.w;
+        }
+        f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int kk = 0; kk < 16; ++kk) acc = mfma4(av[kk], bv[kk], acc);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          sH2[(16 * st + 4 * lq + r) * LDW + 16 * w + li] = xa_tanhf(acc[r] + bias);
+      }
+    }
+    __syncthreads();
+    // ---- heads + loss + dL/dz: 8 lanes per sample ----
+    {
+      const int s = tid >> 3, pp = tid & 7;
       float z[AH];
 #pragma unroll
       for (int a = 0; a < AH; ++a) z[a] = 0.0f;
-      for (int j = 0; j < H; ++j) {
-        const float hj = sH2T[j * S + s];
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) {
+        const int j = 8 * pp + jj;
+        const float hj = sH2[s * LDW + j];
 #pragma unroll
         for (int a = 0; a < AH; ++a) z[a] = fmaf(hj, sW34[j * AH + a], z[a]);
       }
 #pragma unroll
-      for (int a = 0; a < AH; ++a) z[a] = z[a] + sb34[a];
-      float dz[AH];
-#pragma unroll
-      for (int a = 0; a < AH; ++a) dz[a] = 0.0f;
-      if (idx >= 0) {
-        const int act = p.actions[idx];
-        float m = z[0];
-#pragma unroll
-        for (int a = 1; a < A; ++a) m = fmaxf(m, z[a]);
-        float e[A], ssum = 0.0f;
-#pragma unroll
-        for (int a = 0; a < A; ++a) {
-          e[a] = xa_expf(z[a] - m);
-          ssum = ssum + e[a];
-        }
-        const float ls = xa_logf(ssum);
-        float lp[A], pr[A], ent = 0.0f, logp = 0.0f;
-#pragma unroll
-        for (int a = 0; a < A; ++a) {
-          lp[a] = (z[a] - m) - ls;
-          pr[a] = e[a] / ssum;
-          ent = ent - pr[a] * lp[a];
-          if (a == act) logp = lp[a];
-        }
-        const float v = z[A];
-        const float R = p.returns[idx];
-        const float oldv = p.old_values[idx];
-        const float adv_raw = R - oldv;
-        const float sc = p.loss_scale;
-        float dlogp, dv, pg, vl;
-        if (is_ppo) {
-          const float adv =
-              p.adv_in ? p.adv_in[idx] : (adv_raw - adv_mean) / (adv_std + p.adv_eps);
-          const float ratio = xa_expf(logp - p.old_logp[idx]);
-          const float c = p.clip_norm;
-          const float pg1 = -adv * ratio;
-          const float pg2 = -adv * fminf(fmaxf(ratio, 1.0f - c), 1.0f + c);
-          pg = fmaxf(pg1, pg2);
-          dlogp = (pg1 >= pg2) ? (sc * -adv) * ratio : 0.0f;
-          const float vclip = oldv + fminf(fmaxf(v - oldv, -c), c);
-          const float vl1 = (v - R) * (v - R);
-          const float vl2 = (vclip - R) * (vclip - R);
-          vl = fmaxf(vl1, vl2);
-          dv = (vl1 >= vl2) ? sc * p.value_coef * 0.5f * 2.0f * (v - R) : 0.0f;
-        } else {
-          pg = -(adv_raw * logp);
-          dlogp = -sc * adv_raw;
-          vl = (v - R) * (v - R);
-          dv = sc * p.value_coef * 2.0f * (v - R);
-        }
-        const float ec = sc * p.entropy_coef;
-#pragma unroll
-        for (int a = 0; a < A; ++a)
-          dz[a] = dlogp * ((a == act ? 1.0f : 0.0f) - pr[a]) + ec * pr[a] * (lp[a] + ent);
-        dz[A] = dv;
-        l_pg += pg;
-        l_v += vl;
-        l_ent += ent;
-        l_cnt += 1.0f;
+      for (int a = 0; a < AH; ++a) {
+        z[a] = z[a] + __shfl_xor(z[a], 1, 64);
+        z[a] = z[a] + __shfl_xor(z[a], 2, 64);
+        z[a] = z[a] + __shfl_xor(z[a], 4, 64);
+        z[a] = z[a] + sb34[a];
       }
+      const int idx = sIdx[s];
+      if (pp == 0) {
+        float dz[AH];
 #pragma unroll
-      for (int a = 0; a < AH; ++a) sdZ[s * AH + a] = dz[a];
+        for (int a = 0; a < AH; ++a) dz[a] = 0.0f;
+        if (idx >= 0) {
+          const int act = p.actions[idx];
+          float m = z[0];
+#pragma unroll
+          for (int a = 1; a < A; ++a) m = fmaxf(m, z[a]);
+          float e[A], ssum = 0.0f;
+#pragma unroll
+          for (int a = 0; a < A; ++a) {
+            e[a] = xa_expf(z[a] - m);
+            ssum = ssum + e[a];
+          }
+          const float ls = xa_logf(ssum);
+          float lp[A], pr[A], ent = 0.0f, logp = 0.0f;
+#pragma unroll
+          for (int a = 0; a < A; ++a) {
+            lp[a] = (z[a] - m) - ls;
+            pr[a] = e[a] / ssum;
+            ent = ent - pr[a] * lp[a];
+            if (a == act) logp = lp[a];
+          }
+          const float v = z[A];
+          const float R = p.returns[idx];
+          const float oldv = p.old_values[idx];
+          const float adv_raw = R - oldv;
+          const float sc = p.loss_scale;
+          float dlogp, dv, pg, vl;
+          if (is_ppo) {
+            const float adv =
+                p.adv_in ? p.adv_in[idx] : (adv_raw - adv_mean) / (adv_std + p.adv_eps);
+            const float ratio = xa_expf(logp - p.old_logp[idx]);
+            const float c = p.clip_norm;
+            const float pg1 = -adv * ratio;
+            const float pg2 = -adv * fminf(fmaxf(ratio, 1.0f - c), 1.0f + c);
+            pg = fmaxf(pg1, pg2);
+            // tf.maximum routes the gradient to its first input when x >= y; the
+            // second input's gradient passes tf.clip_by_value only inside [lo, hi]
+            const bool r_in = ratio >= 1.0f - c && ratio <= 1.0f + c;
+            dlogp = (pg1 >= pg2 || r_in) ? (sc * -adv) * ratio : 0.0f;
+            const float dvo = v - oldv;
+            const float vclip = oldv + fminf(fmaxf(dvo, -c), c);
+            const float vl1 = (v - R) * (v - R);
+            const float vl2 = (vclip - R) * (vclip - R);
+            vl = fmaxf(vl1, vl2);
+            // rounding can make oldv + (v - oldv) != v inside the clip range: the
+            // clipped branch then still carries the gradient 2 (v_clip - R)
+            const float kv = sc * p.value_coef * 0.5f * 2.0f;
+            if (vl1 >= vl2) dv = kv * (v - R);
+            else dv = (dvo >= -c && dvo <= c) ? kv * (vclip - R) : 0.0f;
+          } else {
+            pg = -(adv_raw * logp);
+            dlogp = -sc * adv_raw;
+            vl = (v - R) * (v - R);
+            dv = sc * p.value_coef * 2.0f * (v - R);
+          }
+          const float ec = sc * p.entropy_coef;
+#pragma unroll
+          for (int a = 0; a < A; ++a)
+            dz[a] = dlogp * ((a == act ? 1.0f : 0.0f) - pr[a]) + ec * pr[a] * (lp[a] + ent);
+          dz[A] = dv;
+          l_pg += pg;
+          l_v += vl;
+          l_ent += ent;
+          l_cnt += 1.0f;
+        }
+#pragma unroll
+        for (int a = 0; a < AH; ++a) sdZ[s * AH + a] = dz[a];
+      }
     }
     __syncthreads();
-    // ---- P5: head grads, dA2 = (dZ W34^T) * (1 - H2^2) ----
-#pragma unroll
-    for (int q = 0; q < NW34; ++q) {
-      const int oo = tid + q * 256;
-      if (oo < H * AH) {
-        const int j = oo & 63, a = oo >> 6;
-        float acc = gW34[q];
-        for (int s = 0; s < S; ++s) acc = fmaf(sH2[s * H + j], sdZ[s * AH + a], acc);
-        gW34[q] = acc;
-      }
-    }
-    if (tid < AH) {
-      float acc = gb34;
-      for (int s = 0; s < S; ++s) acc = acc + sdZ[s * AH + tid];
-      gb34 = acc;
-    }
+    // ---- dA2 = (dZ W34^T) * (1 - H2^2); head / b2 partial grads ----
     {
-      float d[4][4];
+      float dv8[8];
 #pragma unroll
-      for (int ii = 0; ii < 4; ++ii)
+      for (int ss = 0; ss < 8; ++ss) {
+        const int s = c8 + ss;
+        float dh = 0.0f;
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          float dh = 0.0f;
+        for (int a = 0; a < AH; ++a) dh = fmaf(sdZ[s * AH + a], sW34[f * AH + a], dh);
+        const float hv = sH2[s * LDW + f];
 #pragma unroll
-          for (int a = 0; a < AH; ++a)
-            dh = fmaf(sdZ[(r0 + ii) * AH + a], sW34[(c0 + jj) * AH + a], dh);
-          const float hv = sH2[(r0 + ii) * H + c0 + jj];
-          d[ii][jj] = dh * (1.0f - hv * hv);
-        }
-#pragma unroll
-      for (int ii = 0; ii < 4; ++ii)
-        *reinterpret_cast<float4*>(&sdA2[(r0 + ii) * H + c0]) =
-            make_float4(d[ii][0], d[ii][1], d[ii][2], d[ii][3]);
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj)
-        *reinterpret_cast<float4*>(&sdA2T[(c0 + jj) * S + r0]) =
-            make_float4(d[0][jj], d[1][jj], d[2][jj], d[3][jj]);
+        for (int a = 0; a < AH; ++a) gW34[a] = fmaf(hv, sdZ[s * AH + a], gW34[a]);
+        const float d = dh * (1.0f - hv * hv);
+        gb2 = gb2 + d;
+        sdA2[s * LDW + f] = d;
+        dv8[ss] = d;
+      }
+      *reinterpret_cast<float4*>(&sdA2T[f * LDT + c8]) = make_float4(dv8[0], dv8[1], dv8[2], dv8[3]);
+      *reinterpret_cast<float4*>(&sdA2T[f * LDT + c8 + 4]) = make_float4(dv8[4], dv8[5], dv8[6], dv8[7]);
+      if (tid < AH) {
+        float acc = gb34;
+        for (int s = 0; s < S; ++s) acc = acc + sdZ[s * AH + tid];
+        gb34 = acc;
+      }
     }
     __syncthreads();
-    // ---- P6: dW2 += H1^T dA2 ; db2 ; dA1 = (dA2 W2^T) * (1 - H1^2) -> sH2T ----
-#pragma unroll 8
-    for (int s = 0; s < S; ++s) {
-      const float4 a4 = *reinterpret_cast<const float4*>(&sH1[s * H + r0]);
-      const float4 b4 = *reinterpret_cast<const float4*>(&sdA2[s * H + c0]);
-      const float av[4] = {a4.x, a4.y, a4.z, a4.w};
-      const float bv[4] = {b4.x, b4.y, b4.z, b4.w};
-#pragma unroll
-      for (int ii = 0; ii < 4; ++ii)
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) gW2[ii][jj] = fmaf(av[ii], bv[jj], gW2[ii][jj]);
-    }
-    if (tid < H) {
-      float acc = gb2;
-      for (int s = 0; s < S; ++s) acc = acc + sdA2[s * H + tid];
-      gb2 = acc;
-    }
+    // ---- dW2 += H1^T dA2 (rows 16w.., K = samples 8q+kk) and dH1 = dA2 W2^T ----
     {
-      float acc[4][4];
-#pragma unroll
-      for (int ii = 0; ii < 4; ++ii)
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) acc[ii][jj] = 0.0f;
-#pragma unroll 8
-      for (int j = 0; j < H; ++j) {
-        const float4 a4 = *reinterpret_cast<const float4*>(&sdA2T[j * S + r0]);
-        const float4 b4 = *reinterpret_cast<const float4*>(&sW2T[j * H + c0]);
-        const float av[4] = {a4.x, a4.y, a4.z, a4.w};
-        const float bv[4] = {b4.x, b4.y, b4.z, b4.w};
-#pragma unroll
-        for (int ii = 0; ii < 4; ++ii)
-#pragma unroll
-          for (int jj = 0; jj < 4; ++jj) acc[ii][jj] = fmaf(av[ii], bv[jj], acc[ii][jj]);
+      float av[8];
+      {
+        const float4 t0 = *reinterpret_cast<const float4*>(&sH1T[(16 * w + li) * LDT + 8 * lq]);
+        const float4 t1 = *reinterpret_cast<const float4*>(&sH1T[(16 * w + li) * LDT + 8 * lq + 4]);
+        av[0] = t0.x; av[1] = t0.y; av[2] = t0.z; av[3] = t0.w;
+        av[4] = t1.x; av[5] = t1.y; av[6] = t1.z; av[7] = t1.w;
       }
 #pragma unroll
-      for (int ii = 0; ii < 4; ++ii) {
-        const float4 h4 = *reinterpret_cast<const float4*>(&sH1[(r0 + ii) * H + c0]);
-        const float hv[4] = {h4.x, h4.y, h4.z, h4.w};
-        float dd[4];
+      for (int jt = 0; jt < 4; ++jt) {
+        const float4 t0 = *reinterpret_cast<const float4*>(&sdA2T[(16 * jt + li) * LDT + 8 * lq]);
+        const float4 t1 = *reinterpret_cast<const float4*>(&sdA2T[(16 * jt + li) * LDT + 8 * lq + 4]);
+        const float bv[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) dd[jj] = acc[ii][jj] * (1.0f - hv[jj] * hv[jj]);
-        *reinterpret_cast<float4*>(&sH2T[(r0 + ii) * H + c0]) =
-            make_float4(dd[0], dd[1], dd[2], dd[3]);
+        for (int kk = 0; kk < 8; ++kk) gW2[jt] = mfma4(av[kk], bv[kk], gW2[jt]);
+      }
+      float wv[16];
+#pragma unroll
+      for (int v4 = 0; v4 < 4; ++v4) {
+        const float4 t4 = *reinterpret_cast<const float4*>(&sW2[(16 * w + li) * LDW + 16 * lq + 4 * v4]);
+        wv[4 * v4] = t4.x; wv[4 * v4 + 1] = t4.y; wv[4 * v4 + 2] = t4.z; wv[4 * v4 + 3] = t4.w;
+      }
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        float dv16[16];
+#pragma unroll
+        for (int v4 = 0; v4 < 4; ++v4) {
+          const float4 t4 = *reinterpret_cast<const float4*>(&sdA2[(16 * st + li) * LDW + 16 * lq + 4 * v4]);
+          dv16[4 * v4] = t4.x; dv16[4 * v4 + 1] = t4.y; dv16[4 * v4 + 2] = t4.z; dv16[4 * v4 + 3] = t4.w;
+        }
+        f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int kk = 0; kk < 16; ++kk) acc = mfma4(dv16[kk], wv[kk], acc);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int s = 16 * st + 4 * lq + r;
+          const float h1 = sH1[s * LDW + 16 * w + li];
+          sH2[s * LDW + 16 * w + li] = acc[r] * (1.0f - h1 * h1);  // dA1
+        }
       }
     }
     __syncthreads();
-    // ---- P7: dW1 += X^T dA1 ; db1 ----
-    const float* sdA1 = sH2T;
+    // ---- dW1 += X^T dA1 ; db1 ----
 #pragma unroll
-    for (int q = 0; q < NW1; ++q) {
-      const int oo = tid + q * 256;
-      if (oo < OBS * H) {
-        const int k = oo >> 6, i = oo & 63;
-        float acc = gW1[q];
-        for (int s = 0; s < S; ++s) acc = fmaf(sX[s * OBS + k], sdA1[s * H + i], acc);
-        gW1[q] = acc;
-      }
-    }
-    if (tid < H) {
-      float acc = gb1;
-      for (int s = 0; s < S; ++s) acc = acc + sdA1[s * H + tid];
-      gb1 = acc;
+    for (int ss = 0; ss < 8; ++ss) {
+      const int s = c8 + ss;
+      const float d = sH2[s * LDW + f];
+      gb1 = gb1 + d;
+#pragma unroll
+      for (int k = 0; k < OBS; ++k) gW1[k] = fmaf(sX[s * OBS + k], d, gW1[k]);
     }
   }
 
-  // ---- write this block's partial-gradient row ----
+  // ---- combine the 4 sample-chunk partials per feature, write the partial row ----
   float* part = p.partials + (size_t)blockIdx.x * o.P;
+  {
+    float* r = sRed + ((tid >> 6) * H + f) * NSLOT;
 #pragma unroll
-  for (int ii = 0; ii < 4; ++ii)
-    *reinterpret_cast<float4*>(&part[o.w2 + (r0 + ii) * H + c0]) =
-        make_float4(gW2[ii][0], gW2[ii][1], gW2[ii][2], gW2[ii][3]);
+    for (int a = 0; a < AH; ++a) r[a] = gW34[a];
+    r[AH] = gb2;
+    r[AH + 1] = gb1;
 #pragma unroll
-  for (int q = 0; q < NW34; ++q) {
-    const int oo = tid + q * 256;
-    if (oo < H * AH) {
-      const int j = oo & 63, a = oo >> 6;
-      if (a < A) part[o.w3 + j * A + a] = gW34[q];
-      else part[o.w4 + j] = gW34[q];
-    }
+    for (int k = 0; k < OBS; ++k) r[AH + 2 + k] = gW1[k];
   }
+#pragma unroll
+  for (int jt = 0; jt < 4; ++jt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) part[o.w2 + (16 * w + 4 * lq + r) * H + 16 * jt + li] = gW2[jt][r];
   if (tid < AH) {
     if (tid < A) part[o.b3 + tid] = gb34;
     else part[o.b4] = gb34;
   }
-#pragma unroll
-  for (int q = 0; q < NW1; ++q) {
-    const int oo = tid + q * 256;
-    if (oo < OBS * H) part[o.w1 + oo] = gW1[q];
-  }
-  if (tid < H) {
-    part[o.b1 + tid] = gb1;
-    part[o.b2 + tid] = gb2;
+  __syncthreads();
+  for (int e = tid; e < H * NSLOT; e += 256) {
+    const int ff = e / NSLOT, slot = e - ff * NSLOT;
+    const float v = ((sRed[(0 * H + ff) * NSLOT + slot] + sRed[(1 * H + ff) * NSLOT + slot]) +
+                     (sRed[(2 * H + ff) * NSLOT + slot] + sRed[(3 * H + ff) * NSLOT + slot]));
+    if (slot < A) part[o.w3 + ff * A + slot] = v;
+    else if (slot == A) part[o.w4 + ff] = v;
+    else if (slot == AH) part[o.b2 + ff] = v;
+    else if (slot == AH + 1) part[o.b1 + ff] = v;
+    else part[o.w1 + (slot - AH - 2) * H + ff] = v;
   }
   if (p.loss_partials) {
-    if (tid < 64) {  // wave 0 holds every per-sample loss accumulator
-      l_pg = xa_wave_sum(l_pg);
-      l_v = xa_wave_sum(l_v);
-      l_ent = xa_wave_sum(l_ent);
-      l_cnt = xa_wave_sum(l_cnt);
-      if (tid == 0) {
-        float* lp = p.loss_partials + (size_t)blockIdx.x * 4;
-        lp[0] = l_pg;
-        lp[1] = l_v;
-        lp[2] = l_ent;
-        lp[3] = l_cnt;
-      }
+    l_pg = xa_wave_sum(l_pg);
+    l_v = xa_wave_sum(l_v);
+    l_ent = xa_wave_sum(l_ent);
+    l_cnt = xa_wave_sum(l_cnt);
+    if (lane == 0) {
+      sLoss[w][0] = l_pg;
+      sLoss[w][1] = l_v;
+      sLoss[w][2] = l_ent;
+      sLoss[w][3] = l_cnt;
     }
+    __syncthreads();
+    if (tid < 4)
+      p.loss_partials[(size_t)blockIdx.x * 4 + tid] =
+          (sLoss[0][tid] + sLoss[1][tid]) + (sLoss[2][tid] + sLoss[3][tid]);
   }
-  (void)sLoss;
 }
 
 // ---------------------------------------------------------------------------
-// gradient reduction over partial rows
+// gradient reduction over partial rows (16 params x 16 row groups per block),
+// optionally fused with global-norm clip + Keras Adam by the last-arriving block
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void grad_reduce_kernel(const float* __restrict__ part, int nb,
-                                                          int P, float* __restrict__ g,
-                                                          int* adam_step) {
-  const int pi = blockIdx.x * blockDim.x + threadIdx.x;
-  if (blockIdx.x == 0 && threadIdx.x == 0 && adam_step) adam_step[0] += 1;
-  if (pi >= P) return;
+XA_DEV void adam_apply(float* __restrict__ theta, float* __restrict__ m, float* __restrict__ v,
+                       const float* __restrict__ g, int P, float grad_scale, float sc, int t,
+                       float lr, float b1, float b2, float eps, int i0, int stride) {
+  const float b1p = (float)pow((double)b1, (double)t);
+  const float b2p = (float)pow((double)b2, (double)t);
+  const float alpha = lr * sqrtf(1.0f - b2p) / (1.0f - b1p);
+  const float omb1 = 1.0f - b1, omb2 = 1.0f - b2;
+  for (int i = i0; i < P; i += stride) {
+    const float gg = (g[i] * grad_scale) * sc;
+    float mm = m[i], vv = v[i];
+    mm = mm + (gg - mm) * omb1;
+    vv = vv + (gg * gg - vv) * omb2;
+    m[i] = mm;
+    v[i] = vv;
+    theta[i] = theta[i] - (mm * alpha) / (sqrtf(vv) + eps);
+  }
+}
+
+XA_DEV float clip_scale(double total, float clip) {
+  const float gn = (float)sqrt(total);
+  return clip > 0.0f ? clip * fminf(1.0f / gn, 1.0f / clip) : 1.0f;
+}
+
+__global__ __launch_bounds__(256) void reduce_adam_kernel(
+    const float* __restrict__ part, int nb, int P, float* g_out, int* adam_step, int fuse_adam,
+    float* theta, float* m, float* v, float lr, float b1, float b2, float eps, float clip,
+    double* ws, unsigned* counter, float* gnorm_out) {
+  __shared__ double red[kRedGroups][kRedParams];
+  __shared__ double wred[4];
+  __shared__ int s_last;
+  const int tid = threadIdx.x;
+  const int pp = tid & (kRedParams - 1), rg = tid / kRedParams;
+  const int pidx = blockIdx.x * kRedParams + pp;
   double acc = 0.0;
-  int b = 0;
-  for (; b + 4 <= nb; b += 4) {
-    const float a0 = part[(size_t)b * P + pi];
-    const float a1 = part[(size_t)(b + 1) * P + pi];
-    const float a2 = part[(size_t)(b + 2) * P + pi];
-    const float a3 = part[(size_t)(b + 3) * P + pi];
-    acc += ((double)a0 + (double)a1) + ((double)a2 + (double)a3);
+  if (pidx < P) {
+    int b = rg;
+    for (; b + 3 * kRedGroups < nb; b += 4 * kRedGroups) {
+      const float a0 = part[(size_t)b * P + pidx];
+      const float a1 = part[(size_t)(b + kRedGroups) * P + pidx];
+      const float a2 = part[(size_t)(b + 2 * kRedGroups) * P + pidx];
+      const float a3 = part[(size_t)(b + 3 * kRedGroups) * P + pidx];
+      acc += ((double)a0 + (double)a1) + ((double)a2 + (double)a3);
+    }
+    for (; b < nb; b += kRedGroups) acc += (double)part[(size_t)b * P + pidx];
   }
-  for (; b < nb; ++b) acc += (double)part[(size_t)b * P + pi];
-  g[pi] = (float)acc;
+  red[rg][pp] = acc;
+  __syncthreads();
+  if (!fuse_adam) {
+    if (tid < kRedParams && pidx < P) {
+      double s = 0.0;
+#pragma unroll
+      for (int r = 0; r < kRedGroups; ++r) s += red[r][tid];
+      g_out[pidx] = (float)s;
+    }
+    if (blockIdx.x == 0 && tid == 0 && adam_step) adam_step[0] += 1;
+    return;
+  }
+  if (tid < 64) {  // wave 0: finish 16 params and the block's sum of squares
+    double sq = 0.0;
+    if (tid < kRedParams && pidx < P) {
+      double s = 0.0;
+#pragma unroll
+      for (int r = 0; r < kRedGroups; ++r) s += red[r][tid];
+      const float gf = (float)s;
+      g_out[pidx] = gf;
+      sq = (double)gf * (double)gf;
+    }
+    sq = xa_wave_sum_f64(sq);
+    if (tid == 0) ws[blockIdx.x] = sq;
+  }
+  // publish (plain stores) -> agent release -> ticket (cdna_hip_programming.md G16)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned t = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+    s_last = (t == gridDim.x - 1);
+  }
+  __syncthreads();
+  if (!s_last) return;
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  // last block: total sum of squares in fixed order, then Adam over every parameter
+  double tot = 0.0;
+  for (int i = tid; i < (int)gridDim.x; i += 256) tot += ws[i];
+  tot = xa_wave_sum_f64(tot);
+  if ((tid & 63) == 0) wred[tid >> 6] = tot;
+  __syncthreads();
+  tot = (wred[0] + wred[1]) + (wred[2] + wred[3]);
+  const float sc = clip_scale(tot, clip);
+  const int t = adam_step[0] + 1;
+  adam_apply(theta, m, v, g_out, P, 1.0f, sc, t, lr, b1, b2, eps, tid, 256);
+  __syncthreads();
+  if (tid == 0) {
+    adam_step[0] = t;
+    counter[0] = 0u;  // re-arm for the next launch (stream-ordered)
+    if (gnorm_out) gnorm_out[0] = (float)sqrt(tot);
+  }
 }
 
 // ---------------------------------------------------------------------------
-// global norm + clip + Keras Adam
+// standalone global norm + clip + Keras Adam (multi-GPU: runs after the all-reduce)
 // ---------------------------------------------------------------------------
 constexpr int kSmallP = 65536;
 
@@ -522,7 +624,6 @@ __global__ __launch_bounds__(256) void clip_adam_kernel(float* __restrict__ thet
                                                         const int* step, const double* ws,
                                                         int n_ws, float* gnorm_out) {
   __shared__ double red[4];
-  __shared__ float s_scale;
   double total = 0.0;
   if (ws == nullptr) {
     double acc = 0.0;
@@ -537,29 +638,12 @@ __global__ __launch_bounds__(256) void clip_adam_kernel(float* __restrict__ thet
   } else {
     for (int i = 0; i < n_ws; ++i) total += ws[i];
   }
-  if (threadIdx.x == 0) {
-    const float gn = (float)sqrt(total);
-    float sc = 1.0f;
-    if (clip > 0.0f) sc = clip * fminf(1.0f / gn, 1.0f / clip);
-    s_scale = sc;
-    if (blockIdx.x == 0 && gnorm_out) gnorm_out[0] = gn;
-  }
-  __syncthreads();
-  const float sc = s_scale;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && gnorm_out) gnorm_out[0] = (float)sqrt(total);
+  const float sc = clip_scale(total, clip);
   const int t = step ? *step : 1;
-  const float b1p = (float)pow((double)b1, (double)t);
-  const float b2p = (float)pow((double)b2, (double)t);
-  const float alpha = lr * sqrtf(1.0f - b2p) / (1.0f - b1p);
-  const float omb1 = 1.0f - b1, omb2 = 1.0f - b2;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= P) return;
-  const float gg = (g[i] * grad_scale) * sc;
-  float mm = m[i], vv = v[i];
-  mm = mm + (gg - mm) * omb1;
-  vv = vv + (gg * gg - vv) * omb2;
-  m[i] = mm;
-  v[i] = vv;
-  theta[i] = theta[i] - (mm * alpha) / (sqrtf(vv) + eps);
+  adam_apply(theta, m, v, g, P, grad_scale, sc, t, lr, b1, b2, eps, i, P);
 }
 
 template <int OBS, int A>
@@ -573,9 +657,16 @@ int launch_grad(const XaAcGradArgs* p, hipStream_t s) {
 
 extern "C" int xa_ac_grad_blocks(int mb_size) {
   const int tiles = (mb_size + S - 1) / S;
-  // one tile per block up to 128 blocks; more samples per block beyond that keeps
-  // the partial-gradient rows (the update's dominant HBM traffic) bounded
-  return tiles < 128 ? tiles : 128;
+  // one 32-sample tile per block up to one block per CU; beyond that blocks walk
+  // several tiles, which keeps the partial-gradient rows (the reduction's traffic)
+  // at <= 256 x P floats
+  return tiles < 256 ? tiles : 256;
+}
+
+extern "C" int xa_ppo_adv_stats_size(int batch, int mb_size, int epochs) {
+  if (batch <= 0 || mb_size <= 0 || epochs <= 0) return 0;
+  const int n_mb = (batch + mb_size - 1) / mb_size;
+  return 2 * epochs * n_mb * stats_chunks(mb_size);
 }
 
 extern "C" int xa_ppo_adv_stats(const float* returns, const float* values, int batch, int mb_size,
@@ -584,8 +675,10 @@ extern "C" int xa_ppo_adv_stats(const float* returns, const float* values, int b
   XA_CHECK_ARG(returns && values && stats && shuffle, "xa_ppo_adv_stats: null pointer");
   XA_CHECK_ARG(batch > 0 && mb_size > 0 && epochs > 0, "xa_ppo_adv_stats: bad sizes");
   const int n_mb = (batch + mb_size - 1) / mb_size;
-  hipLaunchKernelGGL(adv_stats_kernel, dim3(epochs * n_mb), dim3(256), 0, (hipStream_t)stream,
-                     returns, values, batch, mb_size, n_mb, *shuffle, stats);
+  const int nc = stats_chunks(mb_size);
+  hipLaunchKernelGGL(adv_stats_kernel, dim3(epochs * n_mb * nc), dim3(256), 0,
+                     (hipStream_t)stream, returns, values, batch, mb_size, n_mb, nc, *shuffle,
+                     stats);
   XA_CHECK_LAUNCH("xa_ppo_adv_stats");
   return 0;
 }
@@ -596,6 +689,7 @@ extern "C" int xa_ac_grad(const XaAcGradArgs* p, void* stream) {
                "xa_ac_grad: null pointer");
   XA_CHECK_ARG(p->batch > 0 && p->mb_size > 0 && p->n_blocks > 0, "xa_ac_grad: bad sizes");
   XA_CHECK_ARG(p->mb_index * p->mb_size < p->batch, "xa_ac_grad: minibatch index out of range");
+  XA_CHECK_ARG(((uintptr_t)p->theta & 15) == 0, "xa_ac_grad: theta must be 16-byte aligned");
   if (p->loss_kind == XA_LOSS_PPO)
     XA_CHECK_ARG(p->old_logp && (p->adv_in || (p->adv_stats && p->adv_count > 0)),
                  "xa_ac_grad: PPO needs old_logp and adv_stats (or adv_in)");
@@ -612,9 +706,31 @@ extern "C" int xa_ac_grad(const XaAcGradArgs* p, void* stream) {
 extern "C" int xa_grad_reduce(const float* partials, int n_parts, int n_params, float* grad,
                               int* adam_step, void* stream) {
   XA_CHECK_ARG(partials && grad && n_parts > 0 && n_params > 0, "xa_grad_reduce: bad arguments");
-  hipLaunchKernelGGL(grad_reduce_kernel, dim3((n_params + 255) / 256), dim3(256), 0,
-                     (hipStream_t)stream, partials, n_parts, n_params, grad, adam_step);
+  const int blocks = (n_params + kRedParams - 1) / kRedParams;
+  hipLaunchKernelGGL(reduce_adam_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                     partials, n_parts, n_params, grad, adam_step, 0, nullptr, nullptr, nullptr,
+                     0.0f, 0.0f, 0.0f, 0.0f, 0.0f, nullptr, nullptr, nullptr);
   XA_CHECK_LAUNCH("xa_grad_reduce");
+  return 0;
+}
+
+extern "C" int xa_grad_reduce_adam_workspace(int n_params) {
+  return (n_params + kRedParams - 1) / kRedParams;
+}
+
+extern "C" int xa_grad_reduce_adam(const float* partials, int n_parts, int n_params, float* grad,
+                                   float* theta, float* adam_m, float* adam_v, int* adam_step,
+                                   float lr, float beta1, float beta2, float eps, float clip_norm,
+                                   double* workspace, unsigned* counter, float* gnorm_out,
+                                   void* stream) {
+  XA_CHECK_ARG(partials && grad && theta && adam_m && adam_v && adam_step && workspace && counter &&
+                   n_parts > 0 && n_params > 0,
+               "xa_grad_reduce_adam: bad arguments");
+  const int blocks = (n_params + kRedParams - 1) / kRedParams;
+  hipLaunchKernelGGL(reduce_adam_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                     partials, n_parts, n_params, grad, adam_step, 1, theta, adam_m, adam_v, lr,
+                     beta1, beta2, eps, clip_norm, workspace, counter, gnorm_out);
+  XA_CHECK_LAUNCH("xa_grad_reduce_adam");
   return 0;
 }
 

@@ -90,9 +90,27 @@ def ac_grad(args: XaAcGradArgs):
     call('xa_ac_grad', ctypes.byref(args), stream())
 
 
+def adv_stats_size(batch, mb_size, epochs):
+    return _lib.load().xa_ppo_adv_stats_size(batch, mb_size, epochs)
+
+
 def grad_reduce(partials, grad, adam_step=None):
     nb, p = partials.shape
     call('xa_grad_reduce', ptr(partials), nb, p, ptr(grad), ptr(adam_step), stream())
+
+
+def grad_reduce_adam_workspace(n_params):
+    return _lib.load().xa_grad_reduce_adam_workspace(n_params)
+
+
+def grad_reduce_adam(partials, grad, theta, m, v, adam_step, lr, beta1, beta2, eps, clip_norm,
+                     workspace, counter, gnorm_out=None):
+    """Fused reduce + clip_by_global_norm + Keras Adam (single-GPU update)."""
+    nb, p = partials.shape
+    call('xa_grad_reduce_adam', ptr(partials), nb, p, ptr(grad), ptr(theta), ptr(m), ptr(v),
+         ptr(adam_step), _f32(lr), _f32(beta1), _f32(beta2), _f32(eps),
+         _f32(clip_norm if clip_norm is not None else 0.0), ptr(workspace), ptr(counter),
+         ptr(gnorm_out), stream())
 
 
 def clip_adam(theta, m, v, grad, adam_step, lr, beta1, beta2, eps, clip_norm=None,

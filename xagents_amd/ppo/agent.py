@@ -60,7 +60,8 @@ class PPO(A2C):
         dev = self.device
         self.partials = torch.zeros(nb, self.model.n_params, dtype=torch.float32, device=dev)
         self.loss_partials = torch.zeros(nb, 4, dtype=torch.float32, device=dev)
-        self.adv_stats = torch.zeros(E * self.n_mb * 2, dtype=torch.float64, device=dev)
+        self.adv_stats = torch.zeros(kernels.adv_stats_size(B, MB, E), dtype=torch.float64,
+                                     device=dev)
         self.shuffle = XaShuffle()
         self.shuffle.perm = None
         self.shuffle.seed = self.rng_seed ^ 0x9E3779B97F4A7C15
