@@ -151,20 +151,55 @@ typedef struct XaShuffle {
 } XaShuffle;
 
 /*
- * Per-minibatch advantage statistics for every (epoch, minibatch), in 1024-sample
- * chunks: stats[((e*n_mb + m)*n_chunks + c)*2 + {0,1}] = (sum adv, sum adv^2) in f64,
- * adv = returns - values (ppo/agent.py:180-183); n_chunks = ceil(mb_size/1024).
- * xa_ac_grad sums the chunks of its minibatch. The sums are linear, so the caller
- * all-reduces the whole array across ranks for exact global normalisation.
- * xa_ppo_adv_stats_size gives the number of doubles to allocate.
+ * PPO minibatch preparation for a whole train step (ppo/agent.py:139-155, 180-183):
+ * for every (epoch e, minibatch m) the shuffled sample indices, and
+ *  - stats[((e*n_mb + m)*n_chunks + c)*2 + {0,1}] = f64 (sum adv, sum adv^2) of
+ *    1024-sample chunk c, adv = returns - values, n_chunks = ceil(mb_size/1024)
+ *    (xa_ppo_adv_stats_size doubles). The sums are linear: all-reduce the array
+ *    across ranks for exact global normalisation.
+ *  - if mb_obs != NULL, the gather: row e*batch + m*mb_size + q of mb_* holds
+ *    sample q of minibatch (e, m) (all minibatches materialised up front, as the
+ *    reference's get_mini_batches does).
  */
-int xa_ppo_adv_stats_size(int batch, int mb_size, int epochs);
-int xa_ppo_adv_stats(const float* returns, const float* values, int batch, int mb_size,
-                     int epochs, const XaShuffle* shuffle, double* stats, void* stream);
+typedef struct XaMinibatchArgs {
+  int batch, mb_size, epochs, obs_dim;
+  XaShuffle shuffle;
+  const float* returns; /* [batch] */
+  const float* values;  /* [batch] */
+  const float* obs;     /* [batch, obs] (gather sources, NULL for stats only) */
+  const int* actions;
+  const float* old_logp;
+  double* stats;
+  float* mb_obs;       /* [epochs*batch, obs] */
+  int* mb_actions;     /* [epochs*batch] */
+  float* mb_old_logp;
+  float* mb_values;
+  float* mb_returns;
+} XaMinibatchArgs;
 
-/* Fused minibatch gather + actor-critic forward + loss + backward. Writes per-block
- * partial gradients [n_blocks, P] and per-block loss sums [n_blocks, 4]
- * (pg, value, entropy, count) when loss_partials != NULL. */
+int xa_ppo_adv_stats_size(int batch, int mb_size, int epochs);
+int xa_ppo_minibatches(const XaMinibatchArgs* args, void* stream);
+
+/* Keras Adam hyper-parameters + tf.clip_by_global_norm (a2c/agent.py:217,
+ * ppo/agent.py:135-137, utils/common.py:476). grad_scale multiplies the gradient
+ * before the norm (1 when the loss is already scaled by the global count). */
+typedef struct XaAdam {
+  float lr, beta1, beta2, eps;
+  float clip_norm; /* <= 0: no clipping */
+  float grad_scale;
+} XaAdam;
+
+/*
+ * Fused [pending optimizer step] + minibatch gather + actor-critic forward + loss +
+ * backward. Writes per-block partial gradients [n_blocks, P] (reduce with
+ * xa_grad_reduce) and per-block loss sums [n_blocks, 4] (pg, value, entropy, count)
+ * when loss_partials != NULL.
+ * Pending step (pend_grad != NULL): every block first applies clip + Keras Adam with
+ * t = *adam_step to (theta, pend_m, pend_v, pend_grad) -- identical arithmetic in
+ * every block -- trains on the result, and block 0 stores it to theta_out / m_out /
+ * v_out (ping-pong buffers, never aliasing the inputs). This folds minibatch k-1's
+ * optimizer step into minibatch k's launch.
+ */
 typedef struct XaAcGradArgs {
   int obs_dim, n_actions;
   int loss_kind; /* XA_LOSS_PPO / XA_LOSS_A2C */
@@ -172,13 +207,14 @@ typedef struct XaAcGradArgs {
   int batch;    /* rollout batch N*T (flat, env-major) */
   int mb_size;  /* minibatch size (PPO) or batch (A2C) */
   int epoch, mb_index;
-  XaShuffle shuffle; /* ignored for A2C (identity order) */
-  const float* obs;      /* [batch, obs] */
-  const int* actions;    /* [batch] */
-  const float* old_logp; /* [batch] (PPO) */
+  XaShuffle shuffle; /* ignored for A2C (identity order) and when gathered */
+  int gathered;      /* 1: inputs are xa_ppo_minibatches' mb_* rows */
+  const float* obs;        /* [batch, obs] */
+  const int* actions;      /* [batch] */
+  const float* old_logp;   /* [batch] (PPO) */
   const float* old_values; /* [batch] */
-  const float* returns;  /* [batch] */
-  const double* adv_stats; /* [(e*n_mb+m)*2] sums (PPO) */
+  const float* returns;    /* [batch] */
+  const double* adv_stats; /* xa_ppo_minibatches stats (PPO) */
   double adv_count;        /* number of samples the stats were summed over (global) */
   const float* adv_in;     /* [batch] precomputed (already normalised) advantages, or NULL */
   float clip_norm, entropy_coef, value_coef, adv_eps;
@@ -186,41 +222,37 @@ typedef struct XaAcGradArgs {
   int n_blocks;
   float* partials;      /* [n_blocks, P] */
   float* loss_partials; /* [n_blocks, 4] or NULL */
+  const float* pend_grad; /* pending optimizer step, or NULL */
+  const float* pend_m;
+  const float* pend_v;
+  float* theta_out;
+  float* m_out;
+  float* v_out;
+  const int* adam_step;
+  XaAdam adam;
 } XaAcGradArgs;
 
 int xa_ac_grad(const XaAcGradArgs* args, void* stream);
 int xa_ac_grad_blocks(int mb_size);
 
 /* grad[p] = sum_b partials[b*P + p] (f64 accumulation, fixed order). If adam_step
- * != NULL it is incremented by one (Keras `iterations`) for the following
- * xa_clip_adam (multi-GPU path: reduce -> all-reduce -> xa_clip_adam). */
+ * != NULL it is incremented by one (Keras `iterations`): the following optimizer
+ * step (xa_ac_grad's pending step or xa_clip_adam) uses the new value as t. */
 int xa_grad_reduce(const float* partials, int n_parts, int n_params, float* grad,
                    int* adam_step, void* stream);
-
-/* Single-launch reduce + tf.clip_by_global_norm + Keras Adam (single-GPU path):
- * the blocks reduce 16-parameter slices, publish them with an agent-scope release,
- * and the last-arriving block (atomic ticket on `counter`, a zero-initialised
- * uint32 re-armed by the kernel) forms the global norm and applies Adam to every
- * parameter; *adam_step is incremented. workspace: >= xa_grad_reduce_adam_workspace
- * doubles. Same arithmetic as xa_grad_reduce + xa_clip_adam. */
-int xa_grad_reduce_adam_workspace(int n_params);
-int xa_grad_reduce_adam(const float* partials, int n_parts, int n_params, float* grad,
-                        float* theta, float* adam_m, float* adam_v, int* adam_step, float lr,
-                        float beta1, float beta2, float eps, float clip_norm, double* workspace,
-                        unsigned* counter, float* gnorm_out, void* stream);
 
 /*
  * g' = grad * grad_scale; if clip_norm > 0: tf.clip_by_global_norm(g', clip_norm)
  * (a2c/agent.py:217, ppo/agent.py:135-136); then Keras Adam (OptimizerV2,
  * training_ops ApplyAdam): m += (g-m)(1-b1); v += (g^2-v)(1-b2);
  * theta -= (m*alpha)/(sqrt(v)+eps), alpha = lr*sqrt(1-b2^t)/(1-b1^t), t = *adam_step.
- * workspace: >= 1024 doubles (used when n_params > 65536). gnorm_out (device f32,
- * optional) receives the pre-clip global norm.
+ * Results go to theta_out/m_out/v_out (NULL = in place). workspace: >= 1024 doubles
+ * (used when n_params > 65536). gnorm_out (device f32, optional): pre-clip norm.
  */
 int xa_clip_adam(float* theta, float* adam_m, float* adam_v, const float* grad, int n_params,
                  float grad_scale, float clip_norm, float lr, float beta1, float beta2,
                  float eps, const int* adam_step, double* workspace, float* gnorm_out,
-                 void* stream);
+                 float* theta_out, float* m_out, float* v_out, void* stream);
 
 #ifdef __cplusplus
 }

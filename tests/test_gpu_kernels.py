@@ -340,30 +340,55 @@ def test_errors_are_loud(device):
                             uniforms=torch.zeros(3, device='cuda'))
 
 
-@pytest.mark.parametrize('nb,P', [(256, 4675), (7, 1000), (300, 70001)])
-def test_grad_reduce_adam_fused_matches_two_kernel_path(device, nb, P):
-    """Last-arriver fused reduce + clip + Adam == xa_grad_reduce + xa_clip_adam, bit for bit,
-    over several launches (the ticket re-arms itself)."""
-    rng = np.random.default_rng(nb)
-    part = T((rng.standard_normal((nb, P)) * 1e-2).astype(np.float32))
-    theta = rng.standard_normal(P).astype(np.float32)
-    t1, t2 = T(theta), T(theta)
-    m1, m2, v1, v2 = (torch.zeros(P, device='cuda') for _ in range(4))
-    s1, s2 = (torch.zeros(1, dtype=torch.int32, device='cuda') for _ in range(2))
-    g1, g2 = torch.zeros(P, device='cuda'), torch.zeros(P, device='cuda')
-    ws = torch.zeros(max(1024, kernels.grad_reduce_adam_workspace(P)), dtype=torch.float64,
-                     device='cuda')
-    ticket = torch.zeros(1, dtype=torch.int32, device='cuda')
-    gn1, gn2 = torch.zeros(1, device='cuda'), torch.zeros(1, device='cuda')
-    for _ in range(3):
-        kernels.grad_reduce_adam(part, g1, t1, m1, v1, s1, 7e-4, 0.9, 0.999, 1e-7, 0.5, ws, ticket,
-                                 gnorm_out=gn1)
-        kernels.grad_reduce(part, g2, s2)
-        kernels.clip_adam(t2, m2, v2, g2, s2, 7e-4, 0.9, 0.999, 1e-7, clip_norm=0.5,
-                          workspace=ws, gnorm_out=gn2)
-    assert int(N(s1)[0]) == int(N(s2)[0]) == 3 and int(N(ticket)[0]) == 0
-    np.testing.assert_array_equal(N(g1), N(g2))
-    np.testing.assert_array_equal(N(g1), N(part).astype(np.float64).sum(0).astype(np.float32))
-    np.testing.assert_allclose(N(gn1), N(gn2), rtol=1e-7)
-    for a, b in ((t1, t2), (m1, m2), (v1, v2)):
-        np.testing.assert_array_equal(N(a), N(b))
+def test_pending_optimizer_step_in_ac_grad_prologue(device):
+    """xa_ac_grad with a pending step == xa_clip_adam (out of place) followed by a plain
+    xa_ac_grad: same new theta/m/v (written by block 0) and the same partial gradients."""
+    rng = np.random.default_rng(77)
+    B, MB = 4096, 1024
+    theta = _theta(4, 2, 21, 0.2)
+    obs, acts, old_logp, old_val, ret = _rand_batch(rng, B, 4, 2, theta)
+    P = theta.size
+    g_pend = T((rng.standard_normal(P) * 1e-2).astype(np.float32))
+    m0 = T((rng.standard_normal(P) * 1e-3).astype(np.float32))
+    v0 = T(np.abs(rng.standard_normal(P) * 1e-5).astype(np.float32))
+    step = torch.tensor([7], dtype=torch.int32, device='cuda')
+    th_t = T(theta)
+    # reference path: out-of-place clip + Adam, then a plain gradient launch
+    th_r, m_r, v_r = (torch.zeros(P, device='cuda') for _ in range(3))
+    kernels.clip_adam(th_t, m0, v0, g_pend, step, 7e-4, 0.9, 0.999, 1e-7, clip_norm=0.5,
+                      out=(th_r, m_r, v_r))
+    nb = kernels.ac_grad_blocks(MB)
+    keep = [T(obs), T(acts), T(old_logp), T(old_val), T(ret)]
+    perm = T(np.stack([rng.permutation(B)]).astype(np.int32))
+    stats = torch.zeros(kernels.adv_stats_size(B, MB, 1), dtype=torch.float64, device='cuda')
+    sh = _lib.XaShuffle()
+    sh.perm = perm.data_ptr()
+    kernels.adv_stats(keep[4], keep[3], B, MB, 1, sh, stats)
+
+    def launch(theta_src, pending):
+        part = torch.zeros(nb, P, device='cuda')
+        g = _lib.XaAcGradArgs()
+        g.obs_dim, g.n_actions, g.loss_kind = 4, 2, 0
+        g.theta = theta_src.data_ptr()
+        g.obs, g.actions, g.old_logp, g.old_values, g.returns = (k.data_ptr() for k in keep)
+        g.batch, g.mb_size, g.epoch, g.mb_index = B, MB, 0, 1
+        g.shuffle = sh
+        g.adv_stats, g.adv_count = stats.data_ptr(), float(MB)
+        g.clip_norm, g.entropy_coef, g.value_coef, g.adv_eps = 0.1, 0.01, 0.5, 1e-8
+        g.loss_scale = 1.0 / MB
+        g.n_blocks, g.partials = nb, part.data_ptr()
+        outs = None
+        if pending:
+            outs = [torch.zeros(P, device='cuda') for _ in range(3)]
+            g.pend_grad, g.pend_m, g.pend_v = g_pend.data_ptr(), m0.data_ptr(), v0.data_ptr()
+            g.theta_out, g.m_out, g.v_out = (o.data_ptr() for o in outs)
+            g.adam_step = step.data_ptr()
+            g.adam = kernels.adam_struct(7e-4, 0.9, 0.999, 1e-7, clip_norm=0.5)
+        kernels.ac_grad(g)
+        return part, outs
+
+    part_ref, _ = launch(th_r, False)
+    part_got, outs = launch(th_t, True)
+    for got, ref, name in zip(outs, (th_r, m_r, v_r), ('theta', 'm', 'v')):
+        np.testing.assert_array_equal(N(got), N(ref), err_msg=name)
+    np.testing.assert_array_equal(N(part_got), N(part_ref))

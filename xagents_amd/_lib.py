@@ -66,6 +66,32 @@ class XaShuffle(Structure):
     _fields_ = [('perm', c_void_p), ('seed', c_uint64), ('rng_counter', c_void_p)]
 
 
+class XaMinibatchArgs(Structure):
+    _fields_ = [
+        ('batch', c_int),
+        ('mb_size', c_int),
+        ('epochs', c_int),
+        ('obs_dim', c_int),
+        ('shuffle', XaShuffle),
+        ('returns', c_void_p),
+        ('values', c_void_p),
+        ('obs', c_void_p),
+        ('actions', c_void_p),
+        ('old_logp', c_void_p),
+        ('stats', c_void_p),
+        ('mb_obs', c_void_p),
+        ('mb_actions', c_void_p),
+        ('mb_old_logp', c_void_p),
+        ('mb_values', c_void_p),
+        ('mb_returns', c_void_p),
+    ]
+
+
+class XaAdam(Structure):
+    _fields_ = [('lr', c_float), ('beta1', c_float), ('beta2', c_float), ('eps', c_float),
+                ('clip_norm', c_float), ('grad_scale', c_float)]
+
+
 class XaAcGradArgs(Structure):
     _fields_ = [
         ('obs_dim', c_int),
@@ -77,6 +103,7 @@ class XaAcGradArgs(Structure):
         ('epoch', c_int),
         ('mb_index', c_int),
         ('shuffle', XaShuffle),
+        ('gathered', c_int),
         ('obs', c_void_p),
         ('actions', c_void_p),
         ('old_logp', c_void_p),
@@ -93,6 +120,14 @@ class XaAcGradArgs(Structure):
         ('n_blocks', c_int),
         ('partials', c_void_p),
         ('loss_partials', c_void_p),
+        ('pend_grad', c_void_p),
+        ('pend_m', c_void_p),
+        ('pend_v', c_void_p),
+        ('theta_out', c_void_p),
+        ('m_out', c_void_p),
+        ('v_out', c_void_p),
+        ('adam_step', c_void_p),
+        ('adam', XaAdam),
     ]
 
 
@@ -116,24 +151,16 @@ _SIGNATURES = {
         [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
          c_void_p, c_void_p, c_void_p, c_void_p],
     ),
-    'xa_ppo_adv_stats': (
-        c_int,
-        [c_void_p, c_void_p, c_int, c_int, c_int, POINTER(XaShuffle), c_void_p, c_void_p],
-    ),
+    'xa_ppo_adv_stats_size': (c_int, [c_int, c_int, c_int]),
+    'xa_ppo_minibatches': (c_int, [POINTER(XaMinibatchArgs), c_void_p]),
     'xa_ac_grad': (c_int, [POINTER(XaAcGradArgs), c_void_p]),
     'xa_ac_grad_blocks': (c_int, [c_int]),
-    'xa_ppo_adv_stats_size': (c_int, [c_int, c_int, c_int]),
     'xa_grad_reduce': (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
-    'xa_grad_reduce_adam_workspace': (c_int, [c_int]),
-    'xa_grad_reduce_adam': (
-        c_int,
-        [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float,
-         c_float, c_float, c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p],
-    ),
     'xa_clip_adam': (
         c_int,
         [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_float, c_float, c_float, c_float,
-         c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p],
+         c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+         c_void_p],
     ),
 }
 

@@ -83,9 +83,11 @@ class A2C(OnPolicy):
         self.rng_seed = (int(seed) * 1000003 + self.rank * 7919 + 17) % 2**64
         P = self.model.n_params
         self.grad = torch.zeros(P, **f32)
-        self.adam_ws = torch.zeros(max(1024, kernels.grad_reduce_adam_workspace(P)),
-                                   dtype=torch.float64, device=dev)
-        self.adam_ticket = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.adam_ws = torch.zeros(1024, dtype=torch.float64, device=dev)
+        # second (ping-pong) slot of theta / Adam moments for the fused optimizer step
+        self.theta_alt = torch.zeros(P, **f32)
+        self.m_alt = torch.zeros(P, **f32)
+        self.v_alt = torch.zeros(P, **f32)
         if self.distributed:
             dist.broadcast(self.model.theta, 0)
         a = XaRolloutArgs()
@@ -141,19 +143,23 @@ class A2C(OnPolicy):
         if self.distributed:
             dist.all_reduce(t)
 
-    def _apply_gradients(self, partials):
-        opt = self.model.optimizer
-        if not self.distributed:
-            # one launch: reduce partial rows, global-norm clip, Keras Adam
-            kernels.grad_reduce_adam(partials, self.grad, self.model.theta, opt.m, opt.v,
-                                     opt.iterations, opt.learning_rate, opt.beta_1, opt.beta_2,
-                                     opt.epsilon, self.grad_norm, self.adam_ws, self.adam_ticket)
-            return
-        kernels.grad_reduce(partials, self.grad, opt.iterations)
+    def _reduce_gradients(self, partials):
+        """Partial rows -> gradient (Adam step += 1) -> [RCCL all-reduce]."""
+        kernels.grad_reduce(partials, self.grad, self.model.optimizer.iterations)
         self._all_reduce(self.grad)
-        kernels.clip_adam(self.model.theta, opt.m, opt.v, self.grad, opt.iterations,
-                          opt.learning_rate, opt.beta_1, opt.beta_2, opt.epsilon,
-                          clip_norm=self.grad_norm, workspace=self.adam_ws)
+
+    def _optimizer_step(self, src=None):
+        """Clip + Keras Adam of self.grad applied to slot `src` = (theta, m, v), result
+        in the canonical slot (model.theta, optimizer.m, optimizer.v)."""
+        opt = self.model.optimizer
+        src = src or (self.model.theta, opt.m, opt.v)
+        kernels.clip_adam(*src, self.grad, opt.iterations, opt.learning_rate, opt.beta_1,
+                          opt.beta_2, opt.epsilon, clip_norm=self.grad_norm,
+                          workspace=self.adam_ws, out=(self.model.theta, opt.m, opt.v))
+
+    def _apply_gradients(self, partials):
+        self._reduce_gradients(partials)
+        self._optimizer_step()
 
     def _update(self):
         kernels.ac_grad(self._gargs)

@@ -1,22 +1,32 @@
-// Actor-critic update for the MLP: minibatch shuffle/gather, per-minibatch
-// advantage statistics, fused forward + PPO/A2C loss + backward, deterministic
-// gradient reduction fused with tf.clip_by_global_norm + Keras Adam.
+// Actor-critic update for the MLP: minibatch shuffle + gather + advantage
+// statistics, fused forward + PPO/A2C loss + backward, deterministic gradient
+// reduction, tf.clip_by_global_norm + Keras Adam.
 //
 // Replaces PPO.get_mini_batches / run_ppo_epochs / update_gradients
 // (xagents/ppo/agent.py:96-191) and A2C.train_step (xagents/a2c/agent.py:190-218).
 //
-// xa_ac_grad schedule (one 256-thread workgroup per 32-sample tile, 4 waves):
-//   gather X -> H1 = tanh(X W1 + b1)               (VALU, K = obs)
-//   Z2 = H1 W2                                      (MFMA f32 16x16x4, K = 64)
-//   heads + loss + dL/dz, 8 lanes per sample        (VALU + xor shuffles)
-//   dA2 = (dZ W34^T) * (1 - H2^2)                   (VALU, K = A + 1)
-//   dW2 += H1^T dA2  and  dH1 = dA2 W2^T            (MFMA f32 16x16x4, K = 32 / 64)
-//   dW1 += X^T dA1                                  (VALU, K = 32)
-// Every operand of an MFMA is read from LDS as contiguous 16-byte rows: the K index
-// that lane group q feeds is remapped to a contiguous block (k = 16q + kk), which
-// only reorders the f32 accumulation (tolerance-checked against float64).
-// Weight gradients stay in registers over the tiles a block walks; each block
-// writes ONE partial-gradient row, reduced in f64 in fixed order (deterministic).
+// Per PPO train step (E epochs x M minibatches, k = 0 .. E*M-1):
+//   xa_ppo_minibatches      shuffle (host perm or Feistel), gather every minibatch into
+//                           contiguous rows, f64 advantage sums per 1024-sample chunk
+//   xa_ac_grad(k)           [prologue: clip + Keras Adam of minibatch k-1's gradient,
+//                           recomputed identically by every block from the reduced
+//                           gradient; block 0 writes the new theta/m/v (ping-pong)]
+//                           forward, loss, backward of 32-sample tiles -> partial rows
+//   xa_grad_reduce(k)       partial rows -> gradient (f64, fixed order), Adam step += 1
+//   [RCCL all-reduce of the gradient when data-parallel]
+//   xa_clip_adam            the last minibatch's optimizer step
+// so the optimizer costs no launch of its own inside the minibatch chain.
+//
+// xa_ac_grad tile schedule (256 threads = 4 waves, 32 samples):
+//   H1 = tanh(X W1 + b1)                (VALU, K = obs)
+//   Z2 = H1 W2                          (MFMA f32 16x16x4, K = 64)
+//   heads + loss + dL/dz                (8 lanes per sample, xor shuffles)
+//   dA2 = (dZ W34^T) * (1 - H2^2)       (VALU, K = A + 1)
+//   dW2 += H1^T dA2 ; dH1 = dA2 W2^T    (MFMA f32 16x16x4, K = 32 / 64)
+//   dW1 += X^T dA1                      (VALU, K = 32)
+// MFMA operands are read from LDS as contiguous 16-byte rows: the K index lane
+// group q feeds is remapped to a contiguous block (k = 16q + kk), which only
+// reorders the f32 accumulation (tolerance-checked against float64).
 #include <math.h>
 
 #include "../../include/xagents_hip.h"
@@ -29,7 +39,7 @@ constexpr int S = 32;    // samples per tile
 constexpr int LDW = 68;  // LDS row stride of [*][64] tiles (16-B aligned, conflict-spreading)
 constexpr int LDT = 36;  // LDS row stride of transposed [64][32] tiles
 constexpr int kStatsChunk = 1024;
-constexpr int kRedParams = 16, kRedGroups = 16;
+constexpr int kRedParams = 16, kRedGroups = 16, kRedRows = 16;  // reduce: <= 256 partial rows
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
@@ -83,28 +93,59 @@ XA_DEV int shuffle_index(const XaShuffle& sh, const ShuffleKeys& keys, int epoch
                          keys.k[2], keys.k[3]);
 }
 
-__host__ __device__ inline int stats_chunks(int mb_size) { return (mb_size + kStatsChunk - 1) / kStatsChunk; }
+__host__ __device__ inline int stats_chunks(int mb_size) {
+  return (mb_size + kStatsChunk - 1) / kStatsChunk;
+}
+
+XA_DEV float clip_scale(double total, float clip) {
+  const float gn = (float)sqrt(total);
+  return clip > 0.0f ? clip * fminf(1.0f / gn, 1.0f / clip) : 1.0f;
+}
+
+// Keras OptimizerV2 Adam step size, computed as training_ops ApplyAdam receives it
+XA_DEV float adam_alpha(float lr, float b1, float b2, int t) {
+  const float b1p = (float)pow((double)b1, (double)t);
+  const float b2p = (float)pow((double)b2, (double)t);
+  return lr * sqrtf(1.0f - b2p) / (1.0f - b1p);
+}
+
+// one ApplyAdam element: m += (g-m)(1-b1); v += (g^2-v)(1-b2); theta -= m*alpha/(sqrt(v)+eps)
+XA_DEV void adam_elem(float g, float& th, float& m, float& v, float alpha, float omb1,
+                      float omb2, float eps) {
+  m = m + (g - m) * omb1;
+  v = v + (g * g - v) * omb2;
+  th = th - (m * alpha) / (sqrtf(v) + eps);
+}
 
 // ---------------------------------------------------------------------------
-// advantage statistics: one block per (epoch, minibatch, 1024-sample chunk)
+// minibatch preparation: one block per (epoch, minibatch, 1024-sample chunk)
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void adv_stats_kernel(const float* __restrict__ ret,
-                                                        const float* __restrict__ val, int batch,
-                                                        int mb_size, int n_mb, int n_chunks,
-                                                        XaShuffle sh, double* stats) {
+__global__ __launch_bounds__(256) void minibatch_kernel(XaMinibatchArgs a, int n_mb,
+                                                        int n_chunks) {
   __shared__ double red[2][4];
   const int sidx = blockIdx.x / n_chunks, chunk = blockIdx.x % n_chunks;
   const int e = sidx / n_mb, m = sidx % n_mb;
-  const ShuffleKeys keys = shuffle_keys(sh, e, batch);
-  const int start = m * mb_size;
-  const int cnt = min(mb_size, batch - start);
+  const ShuffleKeys keys = shuffle_keys(a.shuffle, e, a.batch);
+  const int start = m * a.mb_size;
+  const int cnt = min(a.mb_size, a.batch - start);
   const int q0 = chunk * kStatsChunk, q1 = min(cnt, q0 + kStatsChunk);
+  const bool gather = a.mb_obs != nullptr;
   double s1 = 0.0, s2 = 0.0;
   for (int q = q0 + (int)threadIdx.x; q < q1; q += blockDim.x) {
-    const int idx = shuffle_index(sh, keys, e, batch, start + q);
-    const float adv = ret[idx] - val[idx];
+    const int idx = shuffle_index(a.shuffle, keys, e, a.batch, start + q);
+    const float r = a.returns[idx], v = a.values[idx];
+    const float adv = r - v;
     s1 += (double)adv;
     s2 += (double)adv * (double)adv;
+    if (gather) {
+      const size_t row = (size_t)e * a.batch + start + q;
+      for (int k = 0; k < a.obs_dim; ++k)
+        a.mb_obs[row * a.obs_dim + k] = a.obs[(size_t)idx * a.obs_dim + k];
+      a.mb_actions[row] = a.actions[idx];
+      a.mb_old_logp[row] = a.old_logp[idx];
+      a.mb_values[row] = v;
+      a.mb_returns[row] = r;
+    }
   }
   s1 = xa_wave_sum_f64(s1);
   s2 = xa_wave_sum_f64(s2);
@@ -115,18 +156,20 @@ __global__ __launch_bounds__(256) void adv_stats_kernel(const float* __restrict_
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    stats[(size_t)blockIdx.x * 2 + 0] = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
-    stats[(size_t)blockIdx.x * 2 + 1] = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+    a.stats[(size_t)blockIdx.x * 2 + 0] = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+    a.stats[(size_t)blockIdx.x * 2 + 1] = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
   }
 }
 
 // ---------------------------------------------------------------------------
-// fused gather + forward + loss + backward
+// fused [pending optimizer step] + forward + loss + backward
 // ---------------------------------------------------------------------------
 template <int OBS, int A>
 __global__ __launch_bounds__(256) void ac_grad_kernel(XaAcGradArgs p) {
-  constexpr int AH = A + 1;           // logits + value head
-  constexpr int NSLOT = AH + 2 + OBS; // per-feature partial sums combined at the end
+  constexpr int AH = A + 1;            // logits + value head
+  constexpr int NSLOT = AH + 2 + OBS;  // per-feature partial sums combined at the end
+  constexpr int NREST = OBS * H + H + H + H * A + A + H + 1;  // parameters outside W2
+  constexpr int RPT = (NREST + 255) / 256;                    // of them per thread
   __shared__ __attribute__((aligned(16))) float sW2[H * LDW];   // [i][j]
   __shared__ __attribute__((aligned(16))) float sW2T[H * LDW];  // [j][k] = W2[k][j]
   __shared__ __attribute__((aligned(16))) float sH1[S * LDW];   // [s][i]
@@ -136,47 +179,126 @@ __global__ __launch_bounds__(256) void ac_grad_kernel(XaAcGradArgs p) {
   __shared__ __attribute__((aligned(16))) float sdA2T[H * LDT]; // [j][s]
   __shared__ float sW1[OBS * H], sb1[H], sb2[H], sW34[H * AH], sb34[AH];
   __shared__ float sX[S * OBS], sdZ[S * AH];
-  __shared__ int sIdx[S];
+  __shared__ float sAct[S], sOldLp[S], sOldV[S], sRet[S], sAdvIn[S];
+  __shared__ int sValid[S];
   __shared__ float sRed[4 * H * NSLOT];
   __shared__ float sLoss[4][4];
+  __shared__ double sNorm[4];
+  __shared__ float sAlpha;
 
   const Offs o = offs(OBS, A);
   const int tid = threadIdx.x;
   const int lane = tid & 63, w = tid >> 6;
-  const int li = lane & 15, lq = lane >> 4;  // MFMA lane coordinates
+  const int li = lane & 15, lq = lane >> 4;     // MFMA lane coordinates
   const int f = tid & 63, c8 = (tid >> 6) * 8;  // element-wise phases: feature, 8-sample chunk
-  const float* __restrict__ th = p.theta;
 
-  {  // W2 in both orientations: each thread moves one 4x4 sub-block
-    const int k0 = 4 * (tid >> 4), j0 = 4 * (tid & 15);
-    float4 r[4];
+  // ---- parameters (optionally after the pending clip + Keras Adam step) ----
+  {
+    const int k0 = 4 * (tid >> 4), j0 = 4 * (tid & 15);  // this thread's 4x4 block of W2
+    float wv[16], rv[RPT];
+    int ri[RPT];
 #pragma unroll
-    for (int rr = 0; rr < 4; ++rr)
-      r[rr] = *reinterpret_cast<const float4*>(&th[o.w2 + (k0 + rr) * H + j0]);
+    for (int q = 0; q < RPT; ++q) {
+      const int r = tid + 256 * q;
+      ri[q] = r < NREST ? (r < o.w2 ? r : r + H * H) : -1;
+    }
+    auto w2_at = [&](const float* base, int rr) {
+      return *reinterpret_cast<const float4*>(&base[o.w2 + (k0 + rr) * H + j0]);
+    };
+    if (p.pend_grad == nullptr) {
 #pragma unroll
-    for (int rr = 0; rr < 4; ++rr) *reinterpret_cast<float4*>(&sW2[(k0 + rr) * LDW + j0]) = r[rr];
-    *reinterpret_cast<float4*>(&sW2T[(j0 + 0) * LDW + k0]) = make_float4(r[0].x, r[1].x, r[2].x, r[3].x);
-    *reinterpret_cast<float4*>(&sW2T[(j0 + 1) * LDW + k0]) = make_float4(r[0].y, r[1].y, r[2].y, r[3].y);
-    *reinterpret_cast<float4*>(&sW2T[(j0 + 2) * LDW + k0]) = make_float4(r[0].z, r[1].z, r[2].z, r[3].z);
-    *reinterpret_cast<float4*>(&sW2T[(j0 + 3) * LDW + k0]) = make_float4(r[0].w, r[1].w, r[2].w, r[3].w);
+      for (int rr = 0; rr < 4; ++rr) {
+        const float4 t4 = w2_at(p.theta, rr);
+        wv[4 * rr] = t4.x; wv[4 * rr + 1] = t4.y; wv[4 * rr + 2] = t4.z; wv[4 * rr + 3] = t4.w;
+      }
+#pragma unroll
+      for (int q = 0; q < RPT; ++q) rv[q] = ri[q] >= 0 ? p.theta[ri[q]] : 0.0f;
+    } else {
+      float gw[16], gr[RPT];
+      double sq = 0.0;
+      const float gs = p.adam.grad_scale;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const float4 t4 = w2_at(p.pend_grad, rr);
+        gw[4 * rr] = t4.x * gs; gw[4 * rr + 1] = t4.y * gs;
+        gw[4 * rr + 2] = t4.z * gs; gw[4 * rr + 3] = t4.w * gs;
+      }
+#pragma unroll
+      for (int q = 0; q < RPT; ++q) gr[q] = ri[q] >= 0 ? p.pend_grad[ri[q]] * gs : 0.0f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sq += (double)gw[i] * (double)gw[i];
+#pragma unroll
+      for (int q = 0; q < RPT; ++q) sq += (double)gr[q] * (double)gr[q];
+      sq = xa_wave_sum_f64(sq);
+      if (lane == 0) sNorm[w] = sq;
+      if (tid == 0) sAlpha = adam_alpha(p.adam.lr, p.adam.beta1, p.adam.beta2, *p.adam_step);
+      __syncthreads();
+      // every block forms the identical norm and step (fixed assignment and order)
+      const double tot = (sNorm[0] + sNorm[1]) + (sNorm[2] + sNorm[3]);
+      const float sc = clip_scale(tot, p.adam.clip_norm);
+      const float alpha = sAlpha;
+      const float omb1 = 1.0f - p.adam.beta1, omb2 = 1.0f - p.adam.beta2, eps = p.adam.eps;
+      const bool writer = blockIdx.x == 0;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const float4 t4 = w2_at(p.theta, rr), m4 = w2_at(p.pend_m, rr), v4 = w2_at(p.pend_v, rr);
+        float th[4] = {t4.x, t4.y, t4.z, t4.w}, mm[4] = {m4.x, m4.y, m4.z, m4.w},
+              vv[4] = {v4.x, v4.y, v4.z, v4.w};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          adam_elem(gw[4 * rr + c] * sc, th[c], mm[c], vv[c], alpha, omb1, omb2, eps);
+          wv[4 * rr + c] = th[c];
+        }
+        if (writer) {
+          const size_t off = o.w2 + (k0 + rr) * H + j0;
+          *reinterpret_cast<float4*>(&p.theta_out[off]) = make_float4(th[0], th[1], th[2], th[3]);
+          *reinterpret_cast<float4*>(&p.m_out[off]) = make_float4(mm[0], mm[1], mm[2], mm[3]);
+          *reinterpret_cast<float4*>(&p.v_out[off]) = make_float4(vv[0], vv[1], vv[2], vv[3]);
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < RPT; ++q) {
+        if (ri[q] < 0) continue;
+        float th = p.theta[ri[q]], mm = p.pend_m[ri[q]], vv = p.pend_v[ri[q]];
+        adam_elem(gr[q] * sc, th, mm, vv, alpha, omb1, omb2, eps);
+        rv[q] = th;
+        if (writer) {
+          p.theta_out[ri[q]] = th;
+          p.m_out[ri[q]] = mm;
+          p.v_out[ri[q]] = vv;
+        }
+      }
+    }
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      *reinterpret_cast<float4*>(&sW2[(k0 + rr) * LDW + j0]) =
+          make_float4(wv[4 * rr], wv[4 * rr + 1], wv[4 * rr + 2], wv[4 * rr + 3]);
+      *reinterpret_cast<float4*>(&sW2T[(j0 + rr) * LDW + k0]) =
+          make_float4(wv[rr], wv[4 + rr], wv[8 + rr], wv[12 + rr]);
+    }
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) {
+      const int e = ri[q];
+      if (e < 0) continue;
+      const float x = rv[q];
+      if (e < o.b1) sW1[e] = x;
+      else if (e < o.w2) sb1[e - o.b1] = x;
+      else if (e < o.w3) sb2[e - o.b2] = x;
+      else if (e < o.b3) {
+        const int jj = (e - o.w3) / A, a = (e - o.w3) - jj * A;
+        sW34[jj * AH + a] = x;
+      } else if (e < o.w4) sb34[e - o.b3] = x;
+      else if (e < o.b4) sW34[(e - o.w4) * AH + A] = x;
+      else sb34[A] = x;
+    }
   }
-  for (int i = tid; i < OBS * H; i += 256) sW1[i] = th[o.w1 + i];
-  if (tid < H) {
-    sb1[tid] = th[o.b1 + tid];
-    sb2[tid] = th[o.b2 + tid];
-  }
-  for (int i = tid; i < H * AH; i += 256) {
-    const int j = i / AH, a = i - j * AH;
-    sW34[i] = a < A ? th[o.w3 + j * A + a] : th[o.w4 + j];
-  }
-  if (tid < AH) sb34[tid] = tid < A ? th[o.b3 + tid] : th[o.b4];
 
   const bool is_ppo = p.loss_kind == XA_LOSS_PPO;
   const int start = p.mb_index * p.mb_size;
   const int cnt = min(p.mb_size, p.batch - start);
   const int n_tiles = (cnt + S - 1) / S;
   ShuffleKeys keys;
-  if (is_ppo) keys = shuffle_keys(p.shuffle, p.epoch, p.batch);
+  if (is_ppo && !p.gathered) keys = shuffle_keys(p.shuffle, p.epoch, p.batch);
   float adv_mean = 0.0f, adv_std = 0.0f;
   if (is_ppo && p.adv_in == nullptr) {
     const int n_mb = (p.batch + p.mb_size - 1) / p.mb_size;
@@ -205,22 +327,28 @@ __global__ __launch_bounds__(256) void ac_grad_kernel(XaAcGradArgs p) {
   for (int k = 0; k < OBS; ++k) gW1[k] = 0.0f;
   float gb1 = 0.0f, gb2 = 0.0f, gb34 = 0.0f;
   float l_pg = 0.0f, l_v = 0.0f, l_ent = 0.0f, l_cnt = 0.0f;
+  const size_t row0 = p.gathered ? (size_t)p.epoch * p.batch + start : 0;
 
   for (int tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
     __syncthreads();
-    // ---- gather ----
+    // ---- gather: observations and every per-sample scalar up front ----
     if (tid < S) {
       const int q = tile * S + tid;
-      int idx = -1;
-      if (q < cnt) idx = is_ppo ? shuffle_index(p.shuffle, keys, p.epoch, p.batch, start + q)
-                                : start + q;
-      sIdx[tid] = idx;
-    }
-    __syncthreads();
-    for (int e = tid; e < S * OBS; e += 256) {
-      const int s = e / OBS, k = e - s * OBS;
-      const int idx = sIdx[s];
-      sX[e] = idx >= 0 ? p.obs[(size_t)idx * OBS + k] : 0.0f;
+      long idx = -1;
+      if (q < cnt) {
+        if (p.gathered) idx = (long)(row0 + q);
+        else idx = is_ppo ? shuffle_index(p.shuffle, keys, p.epoch, p.batch, start + q)
+                          : start + q;
+      }
+      sValid[tid] = idx >= 0;
+      const size_t ix = idx >= 0 ? (size_t)idx : 0;
+#pragma unroll
+      for (int k = 0; k < OBS; ++k) sX[tid * OBS + k] = idx >= 0 ? p.obs[ix * OBS + k] : 0.0f;
+      sAct[tid] = idx >= 0 ? (float)p.actions[ix] : 0.0f;
+      sRet[tid] = idx >= 0 ? p.returns[ix] : 0.0f;
+      sOldV[tid] = idx >= 0 ? p.old_values[ix] : 0.0f;
+      sOldLp[tid] = (idx >= 0 && is_ppo) ? p.old_logp[ix] : 0.0f;
+      sAdvIn[tid] = (idx >= 0 && p.adv_in) ? p.adv_in[ix] : 0.0f;
     }
     __syncthreads();
     // ---- H1 = tanh(X W1 + b1): feature f, samples c8..c8+7 ----
@@ -285,13 +413,12 @@ __global__ __launch_bounds__(256) void ac_grad_kernel(XaAcGradArgs p) {
         z[a] = z[a] + __shfl_xor(z[a], 4, 64);
         z[a] = z[a] + sb34[a];
       }
-      const int idx = sIdx[s];
       if (pp == 0) {
         float dz[AH];
 #pragma unroll
         for (int a = 0; a < AH; ++a) dz[a] = 0.0f;
-        if (idx >= 0) {
-          const int act = p.actions[idx];
+        if (sValid[s]) {
+          const int act = (int)sAct[s];
           float m = z[0];
 #pragma unroll
           for (int a = 1; a < A; ++a) m = fmaxf(m, z[a]);
@@ -311,15 +438,15 @@ __global__ __launch_bounds__(256) void ac_grad_kernel(XaAcGradArgs p) {
             if (a == act) logp = lp[a];
           }
           const float v = z[A];
-          const float R = p.returns[idx];
-          const float oldv = p.old_values[idx];
+          const float R = sRet[s];
+          const float oldv = sOldV[s];
           const float adv_raw = R - oldv;
           const float sc = p.loss_scale;
           float dlogp, dv, pg, vl;
           if (is_ppo) {
             const float adv =
-                p.adv_in ? p.adv_in[idx] : (adv_raw - adv_mean) / (adv_std + p.adv_eps);
-            const float ratio = xa_expf(logp - p.old_logp[idx]);
+                p.adv_in ? sAdvIn[s] : (adv_raw - adv_mean) / (adv_std + p.adv_eps);
+            const float ratio = xa_expf(logp - sOldLp[s]);
             const float c = p.clip_norm;
             const float pg1 = -adv * ratio;
             const float pg2 = -adv * fminf(fmaxf(ratio, 1.0f - c), 1.0f + c);
@@ -488,116 +615,43 @@ __global__ __launch_bounds__(256) void ac_grad_kernel(XaAcGradArgs p) {
 }
 
 // ---------------------------------------------------------------------------
-// gradient reduction over partial rows (16 params x 16 row groups per block),
-// optionally fused with global-norm clip + Keras Adam by the last-arriving block
+// gradient reduction: 16 parameters x 16 row groups per block, every row load of
+// a thread issued before the first use (one memory round trip for <= 256 rows)
 // ---------------------------------------------------------------------------
-XA_DEV void adam_apply(float* __restrict__ theta, float* __restrict__ m, float* __restrict__ v,
-                       const float* __restrict__ g, int P, float grad_scale, float sc, int t,
-                       float lr, float b1, float b2, float eps, int i0, int stride) {
-  const float b1p = (float)pow((double)b1, (double)t);
-  const float b2p = (float)pow((double)b2, (double)t);
-  const float alpha = lr * sqrtf(1.0f - b2p) / (1.0f - b1p);
-  const float omb1 = 1.0f - b1, omb2 = 1.0f - b2;
-  for (int i = i0; i < P; i += stride) {
-    const float gg = (g[i] * grad_scale) * sc;
-    float mm = m[i], vv = v[i];
-    mm = mm + (gg - mm) * omb1;
-    vv = vv + (gg * gg - vv) * omb2;
-    m[i] = mm;
-    v[i] = vv;
-    theta[i] = theta[i] - (mm * alpha) / (sqrtf(vv) + eps);
-  }
-}
-
-XA_DEV float clip_scale(double total, float clip) {
-  const float gn = (float)sqrt(total);
-  return clip > 0.0f ? clip * fminf(1.0f / gn, 1.0f / clip) : 1.0f;
-}
-
-__global__ __launch_bounds__(256) void reduce_adam_kernel(
-    const float* __restrict__ part, int nb, int P, float* g_out, int* adam_step, int fuse_adam,
-    float* theta, float* m, float* v, float lr, float b1, float b2, float eps, float clip,
-    double* ws, unsigned* counter, float* gnorm_out) {
+__global__ __launch_bounds__(256) void grad_reduce_kernel(const float* __restrict__ part, int nb,
+                                                          int P, float* __restrict__ g,
+                                                          int* adam_step) {
   __shared__ double red[kRedGroups][kRedParams];
-  __shared__ double wred[4];
-  __shared__ int s_last;
   const int tid = threadIdx.x;
-  const int pp = tid & (kRedParams - 1), rg = tid / kRedParams;
+  const int pp = tid % kRedParams, rg = tid / kRedParams;
   const int pidx = blockIdx.x * kRedParams + pp;
   double acc = 0.0;
   if (pidx < P) {
-    int b = rg;
-    for (; b + 3 * kRedGroups < nb; b += 4 * kRedGroups) {
-      const float a0 = part[(size_t)b * P + pidx];
-      const float a1 = part[(size_t)(b + kRedGroups) * P + pidx];
-      const float a2 = part[(size_t)(b + 2 * kRedGroups) * P + pidx];
-      const float a3 = part[(size_t)(b + 3 * kRedGroups) * P + pidx];
-      acc += ((double)a0 + (double)a1) + ((double)a2 + (double)a3);
+    for (int b0 = rg; b0 < nb; b0 += kRedGroups * kRedRows) {
+      float x[kRedRows];
+#pragma unroll
+      for (int r = 0; r < kRedRows; ++r) {
+        const int b = b0 + r * kRedGroups;
+        x[r] = b < nb ? part[(size_t)b * P + pidx] : 0.0f;
+      }
+#pragma unroll
+      for (int r = 0; r < kRedRows; r += 4)
+        acc += ((double)x[r] + (double)x[r + 1]) + ((double)x[r + 2] + (double)x[r + 3]);
     }
-    for (; b < nb; b += kRedGroups) acc += (double)part[(size_t)b * P + pidx];
   }
   red[rg][pp] = acc;
   __syncthreads();
-  if (!fuse_adam) {
-    if (tid < kRedParams && pidx < P) {
-      double s = 0.0;
+  if (tid < kRedParams && pidx < P) {
+    double s = 0.0;
 #pragma unroll
-      for (int r = 0; r < kRedGroups; ++r) s += red[r][tid];
-      g_out[pidx] = (float)s;
-    }
-    if (blockIdx.x == 0 && tid == 0 && adam_step) adam_step[0] += 1;
-    return;
+    for (int r = 0; r < kRedGroups; ++r) s += red[r][tid];
+    g[pidx] = (float)s;
   }
-  if (tid < 64) {  // wave 0: finish 16 params and the block's sum of squares
-    double sq = 0.0;
-    if (tid < kRedParams && pidx < P) {
-      double s = 0.0;
-#pragma unroll
-      for (int r = 0; r < kRedGroups; ++r) s += red[r][tid];
-      const float gf = (float)s;
-      g_out[pidx] = gf;
-      sq = (double)gf * (double)gf;
-    }
-    sq = xa_wave_sum_f64(sq);
-    if (tid == 0) ws[blockIdx.x] = sq;
-  }
-  // publish (plain stores) -> agent release -> ticket (cdna_hip_programming.md G16)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned t = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_AGENT);
-    s_last = (t == gridDim.x - 1);
-  }
-  __syncthreads();
-  if (!s_last) return;
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-  // last block: total sum of squares in fixed order, then Adam over every parameter
-  double tot = 0.0;
-  for (int i = tid; i < (int)gridDim.x; i += 256) tot += ws[i];
-  tot = xa_wave_sum_f64(tot);
-  if ((tid & 63) == 0) wred[tid >> 6] = tot;
-  __syncthreads();
-  tot = (wred[0] + wred[1]) + (wred[2] + wred[3]);
-  const float sc = clip_scale(tot, clip);
-  const int t = adam_step[0] + 1;
-  adam_apply(theta, m, v, g_out, P, 1.0f, sc, t, lr, b1, b2, eps, tid, 256);
-  __syncthreads();
-  if (tid == 0) {
-    adam_step[0] = t;
-    counter[0] = 0u;  // re-arm for the next launch (stream-ordered)
-    if (gnorm_out) gnorm_out[0] = (float)sqrt(tot);
-  }
+  if (blockIdx.x == 0 && tid == 0 && adam_step) adam_step[0] += 1;
 }
 
 // ---------------------------------------------------------------------------
-// standalone global norm + clip + Keras Adam (multi-GPU: runs after the all-reduce)
+// standalone global norm + clip + Keras Adam (out of place allowed)
 // ---------------------------------------------------------------------------
 constexpr int kSmallP = 65536;
 
@@ -615,16 +669,14 @@ __global__ __launch_bounds__(256) void sumsq_partial_kernel(const float* __restr
   if (threadIdx.x == 0) ws[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
-__global__ __launch_bounds__(256) void clip_adam_kernel(float* __restrict__ theta,
-                                                        float* __restrict__ m,
-                                                        float* __restrict__ v,
-                                                        const float* __restrict__ g, int P,
-                                                        float grad_scale, float clip, float lr,
-                                                        float b1, float b2, float eps,
-                                                        const int* step, const double* ws,
-                                                        int n_ws, float* gnorm_out) {
+__global__ __launch_bounds__(256) void clip_adam_kernel(
+    const float* theta, const float* m, const float* v, const float* __restrict__ g, int P,
+    float grad_scale, float clip, float lr, float b1, float b2, float eps, const int* step,
+    const double* ws, int n_ws, float* gnorm_out, float* theta_o, float* m_o, float* v_o) {
   __shared__ double red[4];
+  __shared__ float s_alpha;
   double total = 0.0;
+  if (threadIdx.x == 0) s_alpha = adam_alpha(lr, b1, b2, step ? *step : 1);
   if (ws == nullptr) {
     double acc = 0.0;
     for (int i = threadIdx.x; i < P; i += blockDim.x) {
@@ -636,14 +688,18 @@ __global__ __launch_bounds__(256) void clip_adam_kernel(float* __restrict__ thet
     __syncthreads();
     total = (red[0] + red[1]) + (red[2] + red[3]);
   } else {
+    __syncthreads();
     for (int i = 0; i < n_ws; ++i) total += ws[i];
   }
   if (blockIdx.x == 0 && threadIdx.x == 0 && gnorm_out) gnorm_out[0] = (float)sqrt(total);
   const float sc = clip_scale(total, clip);
-  const int t = step ? *step : 1;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= P) return;
-  adam_apply(theta, m, v, g, P, grad_scale, sc, t, lr, b1, b2, eps, i, P);
+  float th = theta[i], mm = m[i], vv = v[i];
+  adam_elem((g[i] * grad_scale) * sc, th, mm, vv, s_alpha, 1.0f - b1, 1.0f - b2, eps);
+  theta_o[i] = th;
+  m_o[i] = mm;
+  v_o[i] = vv;
 }
 
 template <int OBS, int A>
@@ -658,8 +714,7 @@ int launch_grad(const XaAcGradArgs* p, hipStream_t s) {
 extern "C" int xa_ac_grad_blocks(int mb_size) {
   const int tiles = (mb_size + S - 1) / S;
   // one 32-sample tile per block up to one block per CU; beyond that blocks walk
-  // several tiles, which keeps the partial-gradient rows (the reduction's traffic)
-  // at <= 256 x P floats
+  // several tiles, which keeps the partial-gradient rows at <= 256 x P floats
   return tiles < 256 ? tiles : 256;
 }
 
@@ -669,17 +724,18 @@ extern "C" int xa_ppo_adv_stats_size(int batch, int mb_size, int epochs) {
   return 2 * epochs * n_mb * stats_chunks(mb_size);
 }
 
-extern "C" int xa_ppo_adv_stats(const float* returns, const float* values, int batch, int mb_size,
-                                int epochs, const XaShuffle* shuffle, double* stats,
-                                void* stream) {
-  XA_CHECK_ARG(returns && values && stats && shuffle, "xa_ppo_adv_stats: null pointer");
-  XA_CHECK_ARG(batch > 0 && mb_size > 0 && epochs > 0, "xa_ppo_adv_stats: bad sizes");
-  const int n_mb = (batch + mb_size - 1) / mb_size;
-  const int nc = stats_chunks(mb_size);
-  hipLaunchKernelGGL(adv_stats_kernel, dim3(epochs * n_mb * nc), dim3(256), 0,
-                     (hipStream_t)stream, returns, values, batch, mb_size, n_mb, nc, *shuffle,
-                     stats);
-  XA_CHECK_LAUNCH("xa_ppo_adv_stats");
+extern "C" int xa_ppo_minibatches(const XaMinibatchArgs* a, void* stream) {
+  XA_CHECK_ARG(a && a->returns && a->values && a->stats, "xa_ppo_minibatches: null pointer");
+  XA_CHECK_ARG(a->batch > 0 && a->mb_size > 0 && a->epochs > 0, "xa_ppo_minibatches: bad sizes");
+  XA_CHECK_ARG(a->mb_obs == nullptr ||
+                   (a->obs && a->actions && a->old_logp && a->mb_actions && a->mb_old_logp &&
+                    a->mb_values && a->mb_returns && a->obs_dim > 0),
+               "xa_ppo_minibatches: gather needs obs/actions/old_logp and every mb_* output");
+  const int n_mb = (a->batch + a->mb_size - 1) / a->mb_size;
+  const int nc = stats_chunks(a->mb_size);
+  hipLaunchKernelGGL(minibatch_kernel, dim3(a->epochs * n_mb * nc), dim3(256), 0,
+                     (hipStream_t)stream, *a, n_mb, nc);
+  XA_CHECK_LAUNCH("xa_ppo_minibatches");
   return 0;
 }
 
@@ -690,6 +746,14 @@ extern "C" int xa_ac_grad(const XaAcGradArgs* p, void* stream) {
   XA_CHECK_ARG(p->batch > 0 && p->mb_size > 0 && p->n_blocks > 0, "xa_ac_grad: bad sizes");
   XA_CHECK_ARG(p->mb_index * p->mb_size < p->batch, "xa_ac_grad: minibatch index out of range");
   XA_CHECK_ARG(((uintptr_t)p->theta & 15) == 0, "xa_ac_grad: theta must be 16-byte aligned");
+  XA_CHECK_ARG(p->pend_grad == nullptr ||
+                   (p->pend_m && p->pend_v && p->theta_out && p->m_out && p->v_out &&
+                    p->adam_step && ((uintptr_t)p->pend_grad & 15) == 0 &&
+                    ((uintptr_t)p->pend_m & 15) == 0 && ((uintptr_t)p->pend_v & 15) == 0 &&
+                    ((uintptr_t)p->theta_out & 15) == 0 && ((uintptr_t)p->m_out & 15) == 0 &&
+                    ((uintptr_t)p->v_out & 15) == 0 && p->theta_out != p->theta),
+               "xa_ac_grad: a pending optimizer step needs 16-byte aligned grad/m/v and "
+               "separate (ping-pong) theta/m/v outputs and adam_step");
   if (p->loss_kind == XA_LOSS_PPO)
     XA_CHECK_ARG(p->old_logp && (p->adv_in || (p->adv_stats && p->adv_count > 0)),
                  "xa_ac_grad: PPO needs old_logp and adv_stats (or adv_in)");
@@ -707,37 +771,17 @@ extern "C" int xa_grad_reduce(const float* partials, int n_parts, int n_params, 
                               int* adam_step, void* stream) {
   XA_CHECK_ARG(partials && grad && n_parts > 0 && n_params > 0, "xa_grad_reduce: bad arguments");
   const int blocks = (n_params + kRedParams - 1) / kRedParams;
-  hipLaunchKernelGGL(reduce_adam_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
-                     partials, n_parts, n_params, grad, adam_step, 0, nullptr, nullptr, nullptr,
-                     0.0f, 0.0f, 0.0f, 0.0f, 0.0f, nullptr, nullptr, nullptr);
+  hipLaunchKernelGGL(grad_reduce_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                     partials, n_parts, n_params, grad, adam_step);
   XA_CHECK_LAUNCH("xa_grad_reduce");
-  return 0;
-}
-
-extern "C" int xa_grad_reduce_adam_workspace(int n_params) {
-  return (n_params + kRedParams - 1) / kRedParams;
-}
-
-extern "C" int xa_grad_reduce_adam(const float* partials, int n_parts, int n_params, float* grad,
-                                   float* theta, float* adam_m, float* adam_v, int* adam_step,
-                                   float lr, float beta1, float beta2, float eps, float clip_norm,
-                                   double* workspace, unsigned* counter, float* gnorm_out,
-                                   void* stream) {
-  XA_CHECK_ARG(partials && grad && theta && adam_m && adam_v && adam_step && workspace && counter &&
-                   n_parts > 0 && n_params > 0,
-               "xa_grad_reduce_adam: bad arguments");
-  const int blocks = (n_params + kRedParams - 1) / kRedParams;
-  hipLaunchKernelGGL(reduce_adam_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
-                     partials, n_parts, n_params, grad, adam_step, 1, theta, adam_m, adam_v, lr,
-                     beta1, beta2, eps, clip_norm, workspace, counter, gnorm_out);
-  XA_CHECK_LAUNCH("xa_grad_reduce_adam");
   return 0;
 }
 
 extern "C" int xa_clip_adam(float* theta, float* adam_m, float* adam_v, const float* grad,
                             int n_params, float grad_scale, float clip_norm, float lr,
                             float beta1, float beta2, float eps, const int* adam_step,
-                            double* workspace, float* gnorm_out, void* stream) {
+                            double* workspace, float* gnorm_out, float* theta_out, float* m_out,
+                            float* v_out, void* stream) {
   XA_CHECK_ARG(theta && adam_m && adam_v && grad && n_params > 0, "xa_clip_adam: bad arguments");
   hipStream_t s = (hipStream_t)stream;
   const double* ws = nullptr;
@@ -752,7 +796,8 @@ extern "C" int xa_clip_adam(float* theta, float* adam_m, float* adam_v, const fl
   }
   hipLaunchKernelGGL(clip_adam_kernel, dim3((n_params + 255) / 256), dim3(256), 0, s, theta,
                      adam_m, adam_v, grad, n_params, grad_scale, clip_norm, lr, beta1, beta2, eps,
-                     adam_step, ws, n_ws, gnorm_out);
+                     adam_step, ws, n_ws, gnorm_out, theta_out ? theta_out : theta,
+                     m_out ? m_out : adam_m, v_out ? v_out : adam_v);
   XA_CHECK_LAUNCH("xa_clip_adam");
   return 0;
 }

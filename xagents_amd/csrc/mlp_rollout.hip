@@ -221,18 +221,24 @@ __global__ __launch_bounds__(256) void mlp_rollout_kernel(XaRolloutArgs p) {
   };
   if (p.env_kind == XA_ENV_REPLAY) fetch(cur);
 
+  // the sampling uniforms of 64 consecutive steps are drawn in parallel (lane j holds
+  // step t0 + j) and broadcast per step with readlane: off the per-step critical path
+  float u_chunk = 0.0f;
   for (int t = 0; t < T; ++t) {
     const size_t it = (size_t)env * T + t;
+    if ((t & 63) == 0) {
+      const int tj = t + lane;
+      if (p.uniforms) {
+        u_chunk = tj < T ? p.uniforms[(size_t)env * T + tj] : 0.0f;
+      } else {
+        const xa_u4 r = xa_philox((uint32_t)env, (uint32_t)tj, (uint32_t)ctr,
+                                  (uint32_t)(ctr >> 32), k0, k1);
+        u_chunk = xa_u01(r.x);
+      }
+    }
     float logits[A], value;
     net.forward(x, sh, lane, logits, value);
-    float u = 0.0f;
-    if (p.uniforms) {
-      u = p.uniforms[it];
-    } else {
-      const xa_u4 r = xa_philox((uint32_t)env, (uint32_t)t, (uint32_t)ctr, (uint32_t)(ctr >> 32),
-                                k0, k1);
-      u = xa_u01(r.x);
-    }
+    const float u = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(u_chunk), t & 63));
     const CatOut<A> c = categorical<A>(logits, u, -1);
     if (lane < OBS) p.obs_out[it * OBS + lane] = x[lane];
     // env step

@@ -154,9 +154,30 @@ XA_DEV float xa_u01(uint32_t v) { return (float)(v >> 8) * 5.9604644775390625e-0
 // f32 addition is commutative, so every lane ends with the identical value and
 // the order is the fixed pairwise tree the oracle restates.
 // ----------------------------------------------------------------------------
+// Partners come from DPP / permlane swaps instead of ds_bpermute (VALU latency, no
+// LDS round trip): quad_perm gives exact xor-1/xor-2, row_half_mirror/row_mirror pair
+// each lane with the other half of its 8/16-lane group (after the previous levels
+// every lane of a group holds the same value, so this equals xor-4/xor-8), and the
+// gfx950 permlane16/32 swaps give exact xor-16/xor-32.
+#define XA_DPP_F(v, ctrl) \
+  __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), ctrl, 0xF, 0xF, false))
+
 XA_DEV float xa_wave_sum(float v) {
-#pragma unroll
-  for (int m = 1; m < 64; m <<= 1) v = v + __shfl_xor(v, m, 64);
+  v = v + XA_DPP_F(v, 0xB1);   // quad_perm [1,0,3,2]
+  v = v + XA_DPP_F(v, 0x4E);   // quad_perm [2,3,0,1]
+  v = v + XA_DPP_F(v, 0x141);  // row_half_mirror
+  v = v + XA_DPP_F(v, 0x140);  // row_mirror
+  const int lane = __lane_id();
+  {
+    const auto s = __builtin_amdgcn_permlane16_swap(__float_as_int(v), __float_as_int(v), false,
+                                                    false);
+    v = v + __int_as_float(((lane >> 4) & 1) ? s[0] : s[1]);
+  }
+  {
+    const auto s = __builtin_amdgcn_permlane32_swap(__float_as_int(v), __float_as_int(v), false,
+                                                    false);
+    v = v + __int_as_float((lane >> 5) ? s[0] : s[1]);
+  }
   return v;
 }
 

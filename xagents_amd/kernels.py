@@ -9,8 +9,8 @@ import numpy as np
 import torch
 
 from xagents_amd import _lib
-from xagents_amd._lib import (XA_LOSS_A2C, XA_LOSS_PPO, XaAcGradArgs, XaRolloutArgs,
-                              XaShuffle, call, ptr, stream)
+from xagents_amd._lib import (XA_LOSS_A2C, XA_LOSS_PPO, XaAcGradArgs, XaAdam,
+                              XaMinibatchArgs, XaRolloutArgs, XaShuffle, call, ptr, stream)
 
 
 def _f32(x):
@@ -77,9 +77,18 @@ def counter_bump(counter):
     call('xa_counter_bump', ptr(counter), stream())
 
 
+def minibatches(args: XaMinibatchArgs):
+    """Shuffle + gather + per-chunk advantage sums for a whole PPO train step."""
+    call('xa_ppo_minibatches', ctypes.byref(args), stream())
+
+
 def adv_stats(returns, values, batch, mb_size, epochs, shuffle: XaShuffle, stats):
-    call('xa_ppo_adv_stats', ptr(returns), ptr(values), batch, mb_size, epochs,
-         ctypes.byref(shuffle), ptr(stats), stream())
+    """Advantage sums only (no gather)."""
+    a = XaMinibatchArgs()
+    a.batch, a.mb_size, a.epochs, a.obs_dim = batch, mb_size, epochs, 0
+    a.shuffle = shuffle
+    a.returns, a.values, a.stats = ptr(returns), ptr(values), ptr(stats)
+    minibatches(a)
 
 
 def ac_grad_blocks(mb_size):
@@ -99,26 +108,23 @@ def grad_reduce(partials, grad, adam_step=None):
     call('xa_grad_reduce', ptr(partials), nb, p, ptr(grad), ptr(adam_step), stream())
 
 
-def grad_reduce_adam_workspace(n_params):
-    return _lib.load().xa_grad_reduce_adam_workspace(n_params)
-
-
-def grad_reduce_adam(partials, grad, theta, m, v, adam_step, lr, beta1, beta2, eps, clip_norm,
-                     workspace, counter, gnorm_out=None):
-    """Fused reduce + clip_by_global_norm + Keras Adam (single-GPU update)."""
-    nb, p = partials.shape
-    call('xa_grad_reduce_adam', ptr(partials), nb, p, ptr(grad), ptr(theta), ptr(m), ptr(v),
-         ptr(adam_step), _f32(lr), _f32(beta1), _f32(beta2), _f32(eps),
-         _f32(clip_norm if clip_norm is not None else 0.0), ptr(workspace), ptr(counter),
-         ptr(gnorm_out), stream())
+def adam_struct(lr, beta1, beta2, eps, clip_norm=None, grad_scale=1.0):
+    a = XaAdam()
+    a.lr, a.beta1, a.beta2, a.eps = lr, beta1, beta2, eps
+    a.clip_norm = clip_norm if clip_norm is not None else 0.0
+    a.grad_scale = grad_scale
+    return a
 
 
 def clip_adam(theta, m, v, grad, adam_step, lr, beta1, beta2, eps, clip_norm=None,
-              grad_scale=1.0, workspace=None, gnorm_out=None):
-    """tf.clip_by_global_norm + Keras Adam (xagents/ppo/agent.py:135-137)."""
+              grad_scale=1.0, workspace=None, gnorm_out=None, out=None):
+    """tf.clip_by_global_norm + Keras Adam (xagents/ppo/agent.py:135-137).
+    `out` = (theta_out, m_out, v_out) for an out-of-place step (default in place)."""
+    to, mo, vo = out if out is not None else (None, None, None)
     call('xa_clip_adam', ptr(theta), ptr(m), ptr(v), ptr(grad), theta.numel(), _f32(grad_scale),
          _f32(clip_norm if clip_norm is not None else 0.0), _f32(lr), _f32(beta1), _f32(beta2),
-         _f32(eps), ptr(adam_step), ptr(workspace), ptr(gnorm_out), stream())
+         _f32(eps), ptr(adam_step), ptr(workspace), ptr(gnorm_out), ptr(to), ptr(mo), ptr(vo),
+         stream())
 
 
 __all__ = [

@@ -66,27 +66,71 @@ class PPO(A2C):
         self.shuffle.perm = None
         self.shuffle.seed = self.rng_seed ^ 0x9E3779B97F4A7C15
         self.shuffle.rng_counter = self.rng_counter.data_ptr()
+        # every minibatch of the train step materialised up front (ppo/agent.py:139-155)
+        obs_dim = self.model.obs_dim
+        f32 = dict(dtype=torch.float32, device=dev)
+        self.mb_obs = torch.zeros(E * B, obs_dim, **f32)
+        self.mb_act = torch.zeros(E * B, dtype=torch.int32, device=dev)
+        self.mb_logp = torch.zeros(E * B, **f32)
+        self.mb_val = torch.zeros(E * B, **f32)
+        self.mb_ret = torch.zeros(E * B, **f32)
+        mb = kernels.XaMinibatchArgs()
+        mb.batch, mb.mb_size, mb.epochs, mb.obs_dim = B, MB, E, obs_dim
+        mb.shuffle = self.shuffle
+        mb.returns, mb.values = self.b_ret.data_ptr(), self.b_val.data_ptr()
+        mb.obs, mb.actions, mb.old_logp = (self.b_obs.data_ptr(), self.b_act.data_ptr(),
+                                           self.b_logp.data_ptr())
+        mb.stats = self.adv_stats.data_ptr()
+        mb.mb_obs, mb.mb_actions, mb.mb_old_logp = (self.mb_obs.data_ptr(),
+                                                    self.mb_act.data_ptr(),
+                                                    self.mb_logp.data_ptr())
+        mb.mb_values, mb.mb_returns = self.mb_val.data_ptr(), self.mb_ret.data_ptr()
+        self._mbargs = mb
+        # minibatch k applies minibatch k-1's optimizer step in its prologue, reading
+        # theta/m/v from slot (k-1)%2 and writing slot k%2 (slot 0 = the model's)
+        opt = self.model.optimizer
+        slots = [(self.model.theta, opt.m, opt.v), (self.theta_alt, self.m_alt, self.v_alt)]
+        self._slots = slots
+        adam = kernels.adam_struct(opt.learning_rate, opt.beta_1, opt.beta_2, opt.epsilon,
+                                   clip_norm=self.grad_norm)
         self._gargs_list = []
         for e in range(E):
             for m in range(self.n_mb):
+                k = len(self._gargs_list)
                 g = self._grad_args(MB, nb, self.partials, self.loss_partials)
                 g.epoch, g.mb_index = e, m
-                g.shuffle = self.shuffle
+                g.gathered = 1
+                g.obs, g.actions = self.mb_obs.data_ptr(), self.mb_act.data_ptr()
+                g.old_logp, g.old_values = self.mb_logp.data_ptr(), self.mb_val.data_ptr()
+                g.returns = self.mb_ret.data_ptr()
                 count = min(MB, B - m * MB)
                 g.adv_stats = self.adv_stats.data_ptr()
                 g.adv_count = float(count * self.world_size)
                 g.adv_in = None
                 g.loss_scale = 1.0 / (count * self.world_size)
+                src = slots[(k - 1) % 2] if k else slots[0]
+                g.theta = src[0].data_ptr()
+                if k:
+                    dst = slots[k % 2]
+                    g.pend_grad = self.grad.data_ptr()
+                    g.pend_m, g.pend_v = src[1].data_ptr(), src[2].data_ptr()
+                    g.theta_out, g.m_out, g.v_out = (x.data_ptr() for x in dst)
+                    g.adam_step = opt.iterations.data_ptr()
+                    g.adam = adam
                 self._gargs_list.append(g)
+        self._final_src = slots[(len(self._gargs_list) - 1) % 2]
 
     def _update(self):
-        B, MB = self.batch_size, self.mini_batch_size
-        kernels.adv_stats(self.b_ret, self.b_val, B, MB, self.ppo_epochs, self.shuffle,
-                          self.adv_stats)
+        kernels.minibatches(self._mbargs)
         self._all_reduce(self.adv_stats)
         for g in self._gargs_list:
             kernels.ac_grad(g)
-            self._apply_gradients(self.partials)
+            self._reduce_gradients(self.partials)
+        self._optimizer_step(self._final_src)
+
+    def _on_lr_change(self):
+        super()._on_lr_change()
+        self._setup_update()  # the learning rate is baked into the launch arguments
 
     # ---- reference-level pieces --------------------------------------------
     def calculate_returns(self, rewards, dones, values=None, selected_critic_logits=None,
