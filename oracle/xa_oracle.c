@@ -89,24 +89,33 @@ float xo_logf(float x) {
   return dk * 6.9313812256e-01f - ((hfsq - (s * (hfsq + R) + dk * 9.0580006145e-06f)) - f);
 }
 
+/* odd rational minimax tanh on the input clamped to +-7.905311 */
 float xo_tanhf(float x) {
-  float ax = fabsf(x);
-  if (ax < 0.625f) {
-    float z = x * x;
-    float p = fmaf(-5.70498872745e-3f, z, 2.06390887954e-2f);
-    p = fmaf(p, z, -5.37397155531e-2f);
-    p = fmaf(p, z, 1.33314422036e-1f);
-    p = fmaf(p, z, -3.33332819422e-1f);
-    return fmaf(p * z, x, x);
+  const float c = 7.90531110763549805f;
+  float xc = fminf(fmaxf(x, -c), c);
+  float x2 = xc * xc;
+  float p = fmaf(x2, -2.76076847742355e-16f, 2.00018790482477e-13f);
+  p = fmaf(x2, p, -8.60467152213735e-11f);
+  p = fmaf(x2, p, 5.12229709037114e-08f);
+  p = fmaf(x2, p, 1.48572235717979e-05f);
+  p = fmaf(x2, p, 6.37261928875436e-04f);
+  p = fmaf(x2, p, 4.89352455891786e-03f);
+  p = xc * p;
+  float q = fmaf(x2, 1.19825839466702e-06f, 1.18534705686654e-04f);
+  q = fmaf(x2, q, 2.26843463243900e-03f);
+  q = fmaf(x2, q, 4.89352518554385e-03f);
+  return p / q;
+}
+
+/* b^t by binary exponentiation in f64 (the kernels' xa_powi) */
+static double powi(double b, int t) {
+  double r = 1.0;
+  while (t > 0) {
+    if (t & 1) r *= b;
+    b *= b;
+    t >>= 1;
   }
-  float r;
-  if (ax > 9.0f) {
-    r = 1.0f;
-  } else {
-    float e = xo_expf(ax + ax);
-    r = 1.0f - 2.0f / (e + 1.0f);
-  }
-  return x < 0.0f ? -r : r;
+  return r;
 }
 
 void xo_expf_arr(const float* x, float* y, int n) {
@@ -263,9 +272,10 @@ static void categorical(const float* l, int A, float u, int given, int* act_out,
     }
   }
   float ent = 0.0f, logp = 0.0f;
+  float inv_s = 1.0f / s;
   for (int a = 0; a < A; ++a) {
     float lp = (l[a] - m) - ls;
-    float p = e[a] / s;
+    float p = e[a] * inv_s;
     ent = ent - p * lp;
     if (a == act) logp = lp;
   }
@@ -440,8 +450,8 @@ void xo_clip_adam(float* theta, float* m, float* v, const float* g, int P, float
   float sc = 1.0f;
   if (clip > 0.0f) sc = clip * fminf(1.0f / gn, 1.0f / clip);
   if (gnorm_out) *gnorm_out = gn;
-  float b1p = (float)pow((double)b1, (double)t);
-  float b2p = (float)pow((double)b2, (double)t);
+  float b1p = (float)powi((double)b1, t);
+  float b2p = (float)powi((double)b2, t);
   float alpha = lr * sqrtf(1.0f - b2p) / (1.0f - b1p);
   float omb1 = 1.0f - b1, omb2 = 1.0f - b2;
   for (int i = 0; i < P; ++i) {

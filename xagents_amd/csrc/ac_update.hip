@@ -104,8 +104,8 @@ XA_DEV float clip_scale(double total, float clip) {
 
 // Keras OptimizerV2 Adam step size, computed as training_ops ApplyAdam receives it
 XA_DEV float adam_alpha(float lr, float b1, float b2, int t) {
-  const float b1p = (float)pow((double)b1, (double)t);
-  const float b2p = (float)pow((double)b2, (double)t);
+  const float b1p = (float)xa_powi((double)b1, t);
+  const float b2p = (float)xa_powi((double)b2, t);
   return lr * sqrtf(1.0f - b2p) / (1.0f - b1p);
 }
 
@@ -191,6 +191,38 @@ __global__ __launch_bounds__(256) void ac_grad_kernel(XaAcGradArgs p) {
   const int lane = tid & 63, w = tid >> 6;
   const int li = lane & 15, lq = lane >> 4;     // MFMA lane coordinates
   const int f = tid & 63, c8 = (tid >> 6) * 8;  // element-wise phases: feature, 8-sample chunk
+  XA_STAMP_DECL
+  XA_STAMP(10);
+
+  const bool is_ppo = p.loss_kind == XA_LOSS_PPO;
+  const int start = p.mb_index * p.mb_size;
+  const int cnt = min(p.mb_size, p.batch - start);
+  const int n_tiles = (cnt + S - 1) / S;
+  const size_t row0 = p.gathered ? (size_t)p.epoch * p.batch + start : 0;
+  ShuffleKeys keys;
+  if (is_ppo && !p.gathered) keys = shuffle_keys(p.shuffle, p.epoch, p.batch);
+  // per-sample inputs of the next tile, fetched one tile ahead by threads < S
+  float nx[OBS], n_act = 0.0f, n_ret = 0.0f, n_oldv = 0.0f, n_oldlp = 0.0f, n_adv = 0.0f;
+  int n_valid = 0;
+  auto fetch_tile = [&](int tile) {
+    if (tid >= S) return;
+    const int q = tile * S + tid;
+    long idx = -1;
+    if (tile < n_tiles && q < cnt) {
+      if (p.gathered) idx = (long)(row0 + q);
+      else idx = is_ppo ? shuffle_index(p.shuffle, keys, p.epoch, p.batch, start + q) : start + q;
+    }
+    n_valid = idx >= 0;
+    const size_t ix = idx >= 0 ? (size_t)idx : 0;
+#pragma unroll
+    for (int k = 0; k < OBS; ++k) nx[k] = idx >= 0 ? p.obs[ix * OBS + k] : 0.0f;
+    n_act = idx >= 0 ? (float)p.actions[ix] : 0.0f;
+    n_ret = idx >= 0 ? p.returns[ix] : 0.0f;
+    n_oldv = idx >= 0 ? p.old_values[ix] : 0.0f;
+    n_oldlp = (idx >= 0 && is_ppo) ? p.old_logp[ix] : 0.0f;
+    n_adv = (idx >= 0 && p.adv_in) ? p.adv_in[ix] : 0.0f;
+  };
+  fetch_tile(blockIdx.x);  // in flight while the parameters are prepared
 
   // ---- parameters (optionally after the pending clip + Keras Adam step) ----
   {
@@ -215,6 +247,22 @@ __global__ __launch_bounds__(256) void ac_grad_kernel(XaAcGradArgs p) {
       for (int q = 0; q < RPT; ++q) rv[q] = ri[q] >= 0 ? p.theta[ri[q]] : 0.0f;
     } else {
       float gw[16], gr[RPT];
+      // every load of the step (g, theta, m, v) is issued before the first use
+      float4 tw4[4], mw4[4], vw4[4];
+      float tr[RPT], mr[RPT], vr[RPT];
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        tw4[rr] = w2_at(p.theta, rr);
+        mw4[rr] = w2_at(p.pend_m, rr);
+        vw4[rr] = w2_at(p.pend_v, rr);
+      }
+#pragma unroll
+      for (int q = 0; q < RPT; ++q) {
+        const int e = ri[q] >= 0 ? ri[q] : 0;
+        tr[q] = p.theta[e];
+        mr[q] = p.pend_m[e];
+        vr[q] = p.pend_v[e];
+      }
       double sq = 0.0;
       const float gs = p.adam.grad_scale;
 #pragma unroll
@@ -241,7 +289,7 @@ __global__ __launch_bounds__(256) void ac_grad_kernel(XaAcGradArgs p) {
       const bool writer = blockIdx.x == 0;
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
-        const float4 t4 = w2_at(p.theta, rr), m4 = w2_at(p.pend_m, rr), v4 = w2_at(p.pend_v, rr);
+        const float4 t4 = tw4[rr], m4 = mw4[rr], v4 = vw4[rr];
         float th[4] = {t4.x, t4.y, t4.z, t4.w}, mm[4] = {m4.x, m4.y, m4.z, m4.w},
               vv[4] = {v4.x, v4.y, v4.z, v4.w};
 #pragma unroll
@@ -259,7 +307,7 @@ __global__ __launch_bounds__(256) void ac_grad_kernel(XaAcGradArgs p) {
 #pragma unroll
       for (int q = 0; q < RPT; ++q) {
         if (ri[q] < 0) continue;
-        float th = p.theta[ri[q]], mm = p.pend_m[ri[q]], vv = p.pend_v[ri[q]];
+        float th = tr[q], mm = mr[q], vv = vr[q];
         adam_elem(gr[q] * sc, th, mm, vv, alpha, omb1, omb2, eps);
         rv[q] = th;
         if (writer) {
@@ -293,12 +341,6 @@ __global__ __launch_bounds__(256) void ac_grad_kernel(XaAcGradArgs p) {
     }
   }
 
-  const bool is_ppo = p.loss_kind == XA_LOSS_PPO;
-  const int start = p.mb_index * p.mb_size;
-  const int cnt = min(p.mb_size, p.batch - start);
-  const int n_tiles = (cnt + S - 1) / S;
-  ShuffleKeys keys;
-  if (is_ppo && !p.gathered) keys = shuffle_keys(p.shuffle, p.epoch, p.batch);
   float adv_mean = 0.0f, adv_std = 0.0f;
   if (is_ppo && p.adv_in == nullptr) {
     const int n_mb = (p.batch + p.mb_size - 1) / p.mb_size;
@@ -327,30 +369,24 @@ __global__ __launch_bounds__(256) void ac_grad_kernel(XaAcGradArgs p) {
   for (int k = 0; k < OBS; ++k) gW1[k] = 0.0f;
   float gb1 = 0.0f, gb2 = 0.0f, gb34 = 0.0f;
   float l_pg = 0.0f, l_v = 0.0f, l_ent = 0.0f, l_cnt = 0.0f;
-  const size_t row0 = p.gathered ? (size_t)p.epoch * p.batch + start : 0;
 
   for (int tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
     __syncthreads();
-    // ---- gather: observations and every per-sample scalar up front ----
+    XA_STAMP(11);
+    // ---- gather: the prefetched samples into LDS, next tile's loads issued ----
     if (tid < S) {
-      const int q = tile * S + tid;
-      long idx = -1;
-      if (q < cnt) {
-        if (p.gathered) idx = (long)(row0 + q);
-        else idx = is_ppo ? shuffle_index(p.shuffle, keys, p.epoch, p.batch, start + q)
-                          : start + q;
-      }
-      sValid[tid] = idx >= 0;
-      const size_t ix = idx >= 0 ? (size_t)idx : 0;
+      sValid[tid] = n_valid;
 #pragma unroll
-      for (int k = 0; k < OBS; ++k) sX[tid * OBS + k] = idx >= 0 ? p.obs[ix * OBS + k] : 0.0f;
-      sAct[tid] = idx >= 0 ? (float)p.actions[ix] : 0.0f;
-      sRet[tid] = idx >= 0 ? p.returns[ix] : 0.0f;
-      sOldV[tid] = idx >= 0 ? p.old_values[ix] : 0.0f;
-      sOldLp[tid] = (idx >= 0 && is_ppo) ? p.old_logp[ix] : 0.0f;
-      sAdvIn[tid] = (idx >= 0 && p.adv_in) ? p.adv_in[ix] : 0.0f;
+      for (int k = 0; k < OBS; ++k) sX[tid * OBS + k] = nx[k];
+      sAct[tid] = n_act;
+      sRet[tid] = n_ret;
+      sOldV[tid] = n_oldv;
+      sOldLp[tid] = n_oldlp;
+      sAdvIn[tid] = n_adv;
     }
+    if (tile + (int)gridDim.x < n_tiles) fetch_tile(tile + gridDim.x);
     __syncthreads();
+    XA_STAMP(12);
     // ---- H1 = tanh(X W1 + b1): feature f, samples c8..c8+7 ----
     {
       float hv[8];
@@ -367,6 +403,7 @@ __global__ __launch_bounds__(256) void ac_grad_kernel(XaAcGradArgs p) {
       *reinterpret_cast<float4*>(&sH1T[f * LDT + c8 + 4]) = make_float4(hv[4], hv[5], hv[6], hv[7]);
     }
     __syncthreads();
+    XA_STAMP(13);
     // ---- Z2 = H1 W2 (MFMA): wave w owns hidden columns 16w..16w+15 ----
     {
       float bv[16];
@@ -393,6 +430,7 @@ __global__ __launch_bounds__(256) void ac_grad_kernel(XaAcGradArgs p) {
       }
     }
     __syncthreads();
+    XA_STAMP(14);
     // ---- heads + loss + dL/dz: 8 lanes per sample ----
     {
       const int s = tid >> 3, pp = tid & 7;
@@ -486,6 +524,7 @@ __global__ __launch_bounds__(256) void ac_grad_kernel(XaAcGradArgs p) {
       }
     }
     __syncthreads();
+    XA_STAMP(15);
     // ---- dA2 = (dZ W34^T) * (1 - H2^2); head / b2 partial grads ----
     {
       float dv8[8];
@@ -512,6 +551,7 @@ __global__ __launch_bounds__(256) void ac_grad_kernel(XaAcGradArgs p) {
       }
     }
     __syncthreads();
+    XA_STAMP(16);
     // ---- dW2 += H1^T dA2 (rows 16w.., K = samples 8q+kk) and dH1 = dA2 W2^T ----
     {
       float av[8];
@@ -555,6 +595,7 @@ __global__ __launch_bounds__(256) void ac_grad_kernel(XaAcGradArgs p) {
       }
     }
     __syncthreads();
+    XA_STAMP(17);
     // ---- dW1 += X^T dA1 ; db1 ----
 #pragma unroll
     for (int ss = 0; ss < 8; ++ss) {
@@ -566,6 +607,7 @@ __global__ __launch_bounds__(256) void ac_grad_kernel(XaAcGradArgs p) {
     }
   }
 
+  XA_STAMP(18);
   // ---- combine the 4 sample-chunk partials per feature, write the partial row ----
   float* part = p.partials + (size_t)blockIdx.x * o.P;
   {
@@ -612,6 +654,7 @@ __global__ __launch_bounds__(256) void ac_grad_kernel(XaAcGradArgs p) {
       p.loss_partials[(size_t)blockIdx.x * 4 + tid] =
           (sLoss[0][tid] + sLoss[1][tid]) + (sLoss[2][tid] + sLoss[3][tid]);
   }
+  XA_STAMP(19);
 }
 
 // ---------------------------------------------------------------------------
@@ -801,3 +844,4 @@ extern "C" int xa_clip_adam(float* theta, float* adam_m, float* adam_v, const fl
   XA_CHECK_LAUNCH("xa_clip_adam");
   return 0;
 }
+XA_DIAG_READER(xa_diag_read_stamps_update)

@@ -77,15 +77,14 @@ struct LaneMlp {
   }
 
   // x: wave-uniform observation. sh: this wave's 64-float LDS row.
-  XA_DEV void forward(const float (&x)[OBS], float* sh, int lane, float (&logits)[A],
-                      float& value) const {
+  // layer 1 and the h1 broadcast through this wave's LDS row
+  XA_DEV void layer1(const float (&x)[OBS], float* sh, int lane, float (&hv)[H]) const {
     float z1 = 0.0f;
 #pragma unroll
     for (int k = 0; k < OBS; ++k) z1 = fmaf(x[k], w1[k], z1);
     const float h1 = xa_tanhf(z1 + b1);
     sh[lane] = h1;
     wave_sync();
-    float hv[H];
 #pragma unroll
     for (int k = 0; k < H; k += 4) {
       const float4 q = *reinterpret_cast<const float4*>(sh + k);
@@ -95,6 +94,9 @@ struct LaneMlp {
       hv[k + 3] = q.w;
     }
     wave_sync();  // the row is rewritten by the next forward
+  }
+
+  XA_DEV float layer2(const float (&hv)[H]) const {
     float c0 = 0.0f, c1 = 0.0f, c2 = 0.0f, c3 = 0.0f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -103,10 +105,21 @@ struct LaneMlp {
       c2 = fmaf(hv[32 + i], w2[32 + i], c2);
       c3 = fmaf(hv[48 + i], w2[48 + i], c3);
     }
-    const float h2 = xa_tanhf(((c0 + c1) + (c2 + c3)) + b2);
+    return xa_tanhf(((c0 + c1) + (c2 + c3)) + b2);
+  }
+
+  XA_DEV void heads(float h2, float (&logits)[A], float& value) const {
 #pragma unroll
     for (int a = 0; a < A; ++a) logits[a] = xa_wave_sum(h2 * w3[a]) + b3[a];
     value = xa_wave_sum(h2 * w4) + b4;
+  }
+
+  // x: wave-uniform observation. sh: this wave's 64-float LDS row.
+  XA_DEV void forward(const float (&x)[OBS], float* sh, int lane, float (&logits)[A],
+                      float& value) const {
+    float hv[H];
+    layer1(x, sh, lane, hv);
+    heads(layer2(hv), logits, value);
   }
 };
 
@@ -147,10 +160,11 @@ XA_DEV CatOut<A> categorical(const float (&l)[A], float u, int given_action) {
     }
   }
   float ent = 0.0f, logp = 0.0f;
+  const float inv_s = 1.0f / s;
 #pragma unroll
   for (int a = 0; a < A; ++a) {
     const float lp = (l[a] - m) - ls;
-    const float p = e[a] / s;
+    const float p = e[a] * inv_s;
     ent = ent - p * lp;
     if (a == act) logp = lp;
   }
@@ -187,6 +201,7 @@ __global__ __launch_bounds__(256) void mlp_rollout_kernel(XaRolloutArgs p) {
   const bool fused = p.ret_out != nullptr && p.return_kind != XA_RETURNS_NONE;
   float* hist = smem + kWaves * H + wid * 3 * T;  // [rew | val | done] per wave when fused
 
+  XA_STAMP_DECL
   LaneMlp<OBS, A> net;
   net.load(p.theta, lane);
 
@@ -224,6 +239,8 @@ __global__ __launch_bounds__(256) void mlp_rollout_kernel(XaRolloutArgs p) {
   // the sampling uniforms of 64 consecutive steps are drawn in parallel (lane j holds
   // step t0 + j) and broadcast per step with readlane: off the per-step critical path
   float u_chunk = 0.0f;
+  int b_act = 0;
+  float b_logp = 0.0f, b_val = 0.0f, b_ent = 0.0f, b_rew = 0.0f, b_done = 0.0f, b_epret = 0.0f;
   for (int t = 0; t < T; ++t) {
     const size_t it = (size_t)env * T + t;
     if ((t & 63) == 0) {
@@ -236,10 +253,20 @@ __global__ __launch_bounds__(256) void mlp_rollout_kernel(XaRolloutArgs p) {
         u_chunk = xa_u01(r.x);
       }
     }
+    XA_STAMP(0);
     float logits[A], value;
-    net.forward(x, sh, lane, logits, value);
+    {
+      float hv[H];
+      net.layer1(x, sh, lane, hv);
+      XA_STAMP(1);
+      const float h2 = net.layer2(hv);
+      XA_STAMP(2);
+      net.heads(h2, logits, value);
+    }
+    XA_STAMP(3);
     const float u = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(u_chunk), t & 63));
     const CatOut<A> c = categorical<A>(logits, u, -1);
+    XA_STAMP(4);
     if (lane < OBS) p.obs_out[it * OBS + lane] = x[lane];
     // env step
     float r, d;
@@ -276,26 +303,43 @@ __global__ __launch_bounds__(256) void mlp_rollout_kernel(XaRolloutArgs p) {
       for (int k = 0; k < OBS; ++k) st[k] = (float)cp[k < 4 ? k : 3];
     }
     ep_ret = ep_ret + r;
-    if (lane == 0) {
-      p.act_out[it] = c.action;
-      p.logp_out[it] = c.logp;
-      p.val_out[it] = value;
-      if (p.ent_out) p.ent_out[it] = c.entropy;
-      p.rew_out[it] = r;
-      p.done_out[(size_t)env * (T + 1) + t + 1] = d;
-      if (p.epret_out) p.epret_out[it] = ep_ret;
+    // per-step scalars park in lane (t & 63) and leave as one coalesced store per
+    // output every 64 steps (no per-step scalar stores on the step's critical path)
+    if (lane == (t & 63)) {
+      b_act = c.action;
+      b_logp = c.logp;
+      b_val = value;
+      b_ent = c.entropy;
+      b_rew = r;
+      b_done = d;
+      b_epret = ep_ret;
     }
-    if (fused && lane == 0) {
-      hist[t] = r;
-      hist[T + t] = value;
-      hist[2 * T + t] = d;
+    if ((t & 63) == 63 || t == T - 1) {
+      const int t0 = t & ~63;
+      if (t0 + lane <= t) {
+        const size_t o = (size_t)env * T + t0 + lane;
+        p.act_out[o] = b_act;
+        p.logp_out[o] = b_logp;
+        p.val_out[o] = b_val;
+        if (p.ent_out) p.ent_out[o] = b_ent;
+        p.rew_out[o] = b_rew;
+        p.done_out[(size_t)env * (T + 1) + 1 + t0 + lane] = b_done;
+        if (p.epret_out) p.epret_out[o] = b_epret;
+        if (fused) {
+          hist[t0 + lane] = b_rew;
+          hist[T + t0 + lane] = b_val;
+          hist[2 * T + t0 + lane] = b_done;
+        }
+      }
     }
     if (d != 0.0f) ep_ret = 0.0f;
     d_last = d;
 #pragma unroll
     for (int k = 0; k < OBS; ++k) x[k] = o_obs[k];  // pre-reset obs feeds the next step
+    XA_STAMP(6);
   }
 
+  XA_STAMP(5);
   // bootstrap V(get_states()) on the post-reset state (ppo/agent.py:72)
   float logits[A], v_next;
   net.forward(st, sh, lane, logits, v_next);
@@ -307,8 +351,8 @@ __global__ __launch_bounds__(256) void mlp_rollout_kernel(XaRolloutArgs p) {
     p.env_done[env] = d_last;
     p.next_val[env] = v_next;
   }
+  wave_sync();  // every lane's chunk of the history is in LDS
   if (fused && lane == 0) {
-    wave_sync();
     const float* hr = hist;
     const float* hv = hist + T;
     const float* hd = hist + 2 * T;
@@ -449,3 +493,5 @@ extern "C" int xa_mlp_forward(const float* theta, const float* obs, int batch, i
   xa_set_error("xa_mlp_forward: unsupported (obs_dim, n_actions) = (%d, %d)", obs_dim, n_actions);
   return -3;
 }
+
+XA_DIAG_READER(xa_diag_read_stamps_rollout)

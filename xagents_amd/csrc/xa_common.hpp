@@ -38,6 +38,41 @@ void xa_set_error(const char* fmt, ...);
   } while (0)
 
 // ----------------------------------------------------------------------------
+// diagnostic in-kernel stamps (only in the -DXA_STAMPS build, tools/diag): thread 0
+// of block 0 accumulates s_memtime deltas per phase slot; read back with
+// xa_diag_read_stamps. Production builds compile every XA_STAMP to nothing.
+// ----------------------------------------------------------------------------
+#ifdef XA_STAMPS
+static __device__ unsigned long long xa_stamp_acc[64];
+// one reader per translation unit (no relocatable device code)
+#define XA_DIAG_READER(name)                                                         \
+  extern "C" int name(unsigned long long* host) {                                    \
+    unsigned long long zero[64] = {0};                                               \
+    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(xa_stamp_acc), sizeof(zero)) != hipSuccess) \
+      return -1;                                                                     \
+    return hipMemcpyToSymbol(HIP_SYMBOL(xa_stamp_acc), zero, sizeof(zero)) == hipSuccess ? 0 : -1; \
+  }
+#define XA_STAMP_DECL unsigned long long xa_t_last_ = 0;
+#define XA_STAMP(slot)                                                              \
+  do {                                                                              \
+    if (threadIdx.x == 0 && blockIdx.x == 0) {                                      \
+      unsigned long long t_;                                                        \
+      __builtin_amdgcn_sched_barrier(0);                                            \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");    \
+      __builtin_amdgcn_sched_barrier(0);                                            \
+      if (xa_t_last_) xa_stamp_acc[slot] += t_ - xa_t_last_;                        \
+      xa_t_last_ = t_;                                                              \
+    }                                                                               \
+  } while (0)
+#else
+#define XA_DIAG_READER(name)
+#define XA_STAMP_DECL
+#define XA_STAMP(slot) \
+  do {                 \
+  } while (0)
+#endif
+
+// ----------------------------------------------------------------------------
 // deterministic f32 math
 // ----------------------------------------------------------------------------
 XA_DEV float xa_as_float(uint32_t u) { return __uint_as_float(u); }
@@ -98,25 +133,35 @@ XA_DEV float xa_logf(float x) {
   return dk * 6.9313812256e-01f - ((hfsq - (s * (hfsq + R) + dk * 9.0580006145e-06f)) - f);
 }
 
-// tanh(x): odd minimax polynomial on |x| < 0.625, 1 - 2/(e^{2|x|}+1) above.
+// tanh(x): branch-free odd rational minimax x*P(x^2)/Q(x^2) (13/6) on the input
+// clamped to +-7.905311 (where tanh rounds to +-1); <= 5 ulp, no exp, no divergence.
 XA_DEV float xa_tanhf(float x) {
-  float ax = fabsf(x);
-  if (ax < 0.625f) {
-    float z = x * x;
-    float p = fmaf(-5.70498872745e-3f, z, 2.06390887954e-2f);
-    p = fmaf(p, z, -5.37397155531e-2f);
-    p = fmaf(p, z, 1.33314422036e-1f);
-    p = fmaf(p, z, -3.33332819422e-1f);
-    return fmaf(p * z, x, x);
+  const float c = 7.90531110763549805f;
+  const float xc = fminf(fmaxf(x, -c), c);
+  const float x2 = xc * xc;
+  float p = fmaf(x2, -2.76076847742355e-16f, 2.00018790482477e-13f);
+  p = fmaf(x2, p, -8.60467152213735e-11f);
+  p = fmaf(x2, p, 5.12229709037114e-08f);
+  p = fmaf(x2, p, 1.48572235717979e-05f);
+  p = fmaf(x2, p, 6.37261928875436e-04f);
+  p = fmaf(x2, p, 4.89352455891786e-03f);
+  p = xc * p;
+  float q = fmaf(x2, 1.19825839466702e-06f, 1.18534705686654e-04f);
+  q = fmaf(x2, q, 2.26843463243900e-03f);
+  q = fmaf(x2, q, 4.89352518554385e-03f);
+  return p / q;
+}
+
+// b^t for integer t >= 0 by binary exponentiation in f64 (deterministic: the
+// oracle restates the same multiply sequence). Keras forms beta^t with tf.pow.
+__host__ __device__ inline double xa_powi(double b, int t) {
+  double r = 1.0;
+  while (t > 0) {
+    if (t & 1) r *= b;
+    b *= b;
+    t >>= 1;
   }
-  float r;
-  if (ax > 9.0f) {
-    r = 1.0f;
-  } else {
-    float e = xa_expf(ax + ax);
-    r = 1.0f - 2.0f / (e + 1.0f);
-  }
-  return x < 0.0f ? -r : r;
+  return r;
 }
 
 // ----------------------------------------------------------------------------
