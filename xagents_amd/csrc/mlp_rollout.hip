@@ -13,7 +13,8 @@
 //   h2_j = tanh(((c0 + c1) + (c2 + c3)) + b2_j)          (4 interleaved 16-long fma chains)
 //   logit_a = butterfly_sum_j(h2_j * W3[j][a]) + b3_a ;  value likewise
 //   softmax / log-prob / entropy / inverse-CDF sample on every lane (wave-uniform)
-//   env step (replay: next record prefetched one step ahead; cartpole: f64 dynamics)
+//   env step (replay: records of 64 steps fetched a chunk ahead, one lane per step,
+//   read back with readlane; cartpole: f64 dynamics)
 // Envs are independent, so no inter-wave synchronisation exists anywhere.
 // The arithmetic order above is restated exactly by oracle/xa_oracle.c.
 #include "../../include/xagents_hip.h"
@@ -189,7 +190,45 @@ XA_DEV bool cartpole_step(double (&s)[4], int action) {
   return s[0] < -2.4 || s[0] > 2.4 || s[2] < -theta_thr || s[2] > theta_thr;
 }
 
-template <int OBS, int A>
+// The per-step inputs of 64 consecutive steps, lane j holding step t0 + j: the
+// sampling uniform and, for the replay env, the record (the record stream does not
+// depend on the actions, so a whole chunk is fetched a chunk ahead and read back per
+// step with readlane -- no memory access on the step's critical path).
+template <int OBS>
+struct StepChunk {
+  float u_given, u_philox;  // picked per step: a select here would wait on the load
+  float obs[OBS], st[OBS], r, d;
+};
+
+template <int OBS, bool REPLAY>
+XA_DEV void load_chunk(const XaRolloutArgs& p, int env, int lane, int cur0, int t0, uint64_t ctr,
+                       StepChunk<OBS>& c) {
+  const int T = p.n_steps;
+  const int tj = t0 + lane;
+  // loads are unconditional (indices clamped) so every path issues the same number
+  // of them and the waits the compiler places stay exact
+  const float* up = p.uniforms ? p.uniforms + (size_t)env * T : p.theta;
+  c.u_given = up[p.uniforms ? min(tj, T - 1) : 0];
+  const xa_u4 r = xa_philox((uint32_t)env, (uint32_t)tj, (uint32_t)ctr, (uint32_t)(ctr >> 32),
+                            (uint32_t)p.seed, (uint32_t)(p.seed >> 32));
+  c.u_philox = xa_u01(r.x);
+  if constexpr (REPLAY) {
+    const size_t base = (size_t)env * p.t_rec + (size_t)(((long long)cur0 + tj) % p.t_rec);
+#pragma unroll
+    for (int k = 0; k < OBS; ++k) {
+      c.obs[k] = p.rep_obs[base * OBS + k];
+      c.st[k] = p.rep_state[base * OBS + k];
+    }
+    c.r = p.rep_rew[base];
+    c.d = p.rep_done[base];
+  }
+}
+
+XA_DEV float xa_readlane(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
+template <int OBS, int A, bool REPLAY>
 __global__ __launch_bounds__(256) void mlp_rollout_kernel(XaRolloutArgs p) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int lane = threadIdx.x & 63;
@@ -206,145 +245,135 @@ __global__ __launch_bounds__(256) void mlp_rollout_kernel(XaRolloutArgs p) {
   net.load(p.theta, lane);
 
   const uint64_t ctr = p.rng_counter ? *p.rng_counter : 0ull;
-  const uint32_t k0 = (uint32_t)p.seed, k1 = (uint32_t)(p.seed >> 32);
 
   float x[OBS];  // policy input (wave-uniform)
   float st[OBS]; // post-reset env state
 #pragma unroll
   for (int k = 0; k < OBS; ++k) st[k] = x[k] = p.env_state[(size_t)env * OBS + k];
   double cp[4] = {0.0, 0.0, 0.0, 0.0};
-  if (p.env_kind == XA_ENV_CARTPOLE) {
+  if constexpr (!REPLAY) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) cp[k] = p.env_state64[(size_t)env * 4 + k];
   }
-  int cur = p.env_cursor[env];
+  const int cur0 = p.env_cursor[env];
+  int cur = cur0;
   float ep_ret = p.ep_return[env];
   float d_last = p.env_done[env];
   if (lane == 0) p.done_out[(size_t)env * (T + 1)] = d_last;
 
-  // replay prefetch of step 0 (the record stream does not depend on actions)
-  float n_obs[OBS], n_st[OBS], n_r = 0.0f, n_d = 0.0f;
-  auto fetch = [&](int c) {
-    const size_t base = (size_t)env * p.t_rec + c;
-#pragma unroll
-    for (int k = 0; k < OBS; ++k) {
-      n_obs[k] = p.rep_obs[base * OBS + k];
-      n_st[k] = p.rep_state[base * OBS + k];
-    }
-    n_r = p.rep_rew[base];
-    n_d = p.rep_done[base];
-  };
-  if (p.env_kind == XA_ENV_REPLAY) fetch(cur);
-
-  // the sampling uniforms of 64 consecutive steps are drawn in parallel (lane j holds
-  // step t0 + j) and broadcast per step with readlane: off the per-step critical path
-  float u_chunk = 0.0f;
+  // per-step scalars park in lane (t & 63) and leave as one coalesced store per
+  // output after each 64-step chunk (no stores inside the step loop)
+  float b_obs[OBS] = {};
   int b_act = 0;
   float b_logp = 0.0f, b_val = 0.0f, b_ent = 0.0f, b_rew = 0.0f, b_done = 0.0f, b_epret = 0.0f;
-  for (int t = 0; t < T; ++t) {
-    const size_t it = (size_t)env * T + t;
-    if ((t & 63) == 0) {
-      const int tj = t + lane;
-      if (p.uniforms) {
-        u_chunk = tj < T ? p.uniforms[(size_t)env * T + tj] : 0.0f;
-      } else {
-        const xa_u4 r = xa_philox((uint32_t)env, (uint32_t)tj, (uint32_t)ctr,
-                                  (uint32_t)(ctr >> 32), k0, k1);
-        u_chunk = xa_u01(r.x);
+
+  auto run_chunk = [&](const StepChunk<OBS>& c, int t0) {
+    const int n = min(64, T - t0);
+    for (int j = 0; j < n; ++j) {
+      XA_STAMP(0);
+      float logits[A], value;
+      {
+        float hv[H];
+        net.layer1(x, sh, lane, hv);
+        XA_STAMP(1);
+        const float h2 = net.layer2(hv);
+        XA_STAMP(2);
+        net.heads(h2, logits, value);
       }
-    }
-    XA_STAMP(0);
-    float logits[A], value;
-    {
-      float hv[H];
-      net.layer1(x, sh, lane, hv);
-      XA_STAMP(1);
-      const float h2 = net.layer2(hv);
-      XA_STAMP(2);
-      net.heads(h2, logits, value);
-    }
-    XA_STAMP(3);
-    const float u = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(u_chunk), t & 63));
-    const CatOut<A> c = categorical<A>(logits, u, -1);
-    XA_STAMP(4);
-    if (lane < OBS) p.obs_out[it * OBS + lane] = x[lane];
-    // env step
-    float r, d;
-    float o_obs[OBS];
-    if (p.env_kind == XA_ENV_REPLAY) {
-      r = n_r;
-      d = n_d;
+      XA_STAMP(3);
+      const float u = p.uniforms ? xa_readlane(c.u_given, j) : xa_readlane(c.u_philox, j);
+      const CatOut<A> cat = categorical<A>(logits, u, -1);
+      XA_STAMP(4);
+      // env step
+      float r, d;
+      float o_obs[OBS];
+      if constexpr (REPLAY) {
+        r = xa_readlane(c.r, j);
+        d = xa_readlane(c.d, j);
 #pragma unroll
-      for (int k = 0; k < OBS; ++k) {
-        o_obs[k] = n_obs[k];
-        st[k] = n_st[k];
-      }
-      cur = cur + 1;
-      if (cur >= p.t_rec) cur = 0;
-      if (t + 1 < T) fetch(cur);
-    } else {
-      bool done = cartpole_step(cp, c.action);
-      cur = cur + 1;
-      if (cur >= p.max_episode_steps) done = true;  // gym TimeLimit
-      r = 1.0f;
-      d = done ? 1.0f : 0.0f;
-#pragma unroll
-      for (int k = 0; k < OBS; ++k) o_obs[k] = (float)cp[k < 4 ? k : 3];
-      if (done) {
-        // reset: np_random.uniform(-0.05, 0.05, size=(4,))
-        const xa_u4 rr = xa_philox((uint32_t)env, (uint32_t)t, (uint32_t)ctr,
-                                   (uint32_t)(ctr >> 32) ^ 0x5eed5eedu, k0, k1);
-        const uint32_t rv[4] = {rr.x, rr.y, rr.z, rr.w};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) cp[k] = -0.05 + 0.1 * ((double)rv[k] * 2.3283064365386963e-10);
-        cur = 0;
-      }
-#pragma unroll
-      for (int k = 0; k < OBS; ++k) st[k] = (float)cp[k < 4 ? k : 3];
-    }
-    ep_ret = ep_ret + r;
-    // per-step scalars park in lane (t & 63) and leave as one coalesced store per
-    // output every 64 steps (no per-step scalar stores on the step's critical path)
-    if (lane == (t & 63)) {
-      b_act = c.action;
-      b_logp = c.logp;
-      b_val = value;
-      b_ent = c.entropy;
-      b_rew = r;
-      b_done = d;
-      b_epret = ep_ret;
-    }
-    if ((t & 63) == 63 || t == T - 1) {
-      const int t0 = t & ~63;
-      if (t0 + lane <= t) {
-        const size_t o = (size_t)env * T + t0 + lane;
-        p.act_out[o] = b_act;
-        p.logp_out[o] = b_logp;
-        p.val_out[o] = b_val;
-        if (p.ent_out) p.ent_out[o] = b_ent;
-        p.rew_out[o] = b_rew;
-        p.done_out[(size_t)env * (T + 1) + 1 + t0 + lane] = b_done;
-        if (p.epret_out) p.epret_out[o] = b_epret;
-        if (fused) {
-          hist[t0 + lane] = b_rew;
-          hist[T + t0 + lane] = b_val;
-          hist[2 * T + t0 + lane] = b_done;
+        for (int k = 0; k < OBS; ++k) {
+          o_obs[k] = xa_readlane(c.obs[k], j);
+          st[k] = xa_readlane(c.st[k], j);
         }
+      } else {
+        bool done = cartpole_step(cp, cat.action);
+        cur = cur + 1;
+        if (cur >= p.max_episode_steps) done = true;  // gym TimeLimit
+        r = 1.0f;
+        d = done ? 1.0f : 0.0f;
+#pragma unroll
+        for (int k = 0; k < OBS; ++k) o_obs[k] = (float)cp[k < 4 ? k : 3];
+        if (done) {
+          // reset: np_random.uniform(-0.05, 0.05, size=(4,))
+          const xa_u4 rr = xa_philox((uint32_t)env, (uint32_t)(t0 + j), (uint32_t)ctr,
+                                     (uint32_t)(ctr >> 32) ^ 0x5eed5eedu, (uint32_t)p.seed,
+                                     (uint32_t)(p.seed >> 32));
+          const uint32_t rv[4] = {rr.x, rr.y, rr.z, rr.w};
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            cp[k] = -0.05 + 0.1 * ((double)rv[k] * 2.3283064365386963e-10);
+          cur = 0;
+        }
+#pragma unroll
+        for (int k = 0; k < OBS; ++k) st[k] = (float)cp[k < 4 ? k : 3];
+      }
+      ep_ret = ep_ret + r;
+      if (lane == j) {
+#pragma unroll
+        for (int k = 0; k < OBS; ++k) b_obs[k] = x[k];
+        b_act = cat.action;
+        b_logp = cat.logp;
+        b_val = value;
+        b_ent = cat.entropy;
+        b_rew = r;
+        b_done = d;
+        b_epret = ep_ret;
+      }
+      if (d != 0.0f) ep_ret = 0.0f;
+      d_last = d;
+#pragma unroll
+      for (int k = 0; k < OBS; ++k) x[k] = o_obs[k];  // pre-reset obs feeds the next step
+      XA_STAMP(6);
+    }
+    if (lane < n) {
+      const size_t o = (size_t)env * T + t0 + lane;
+#pragma unroll
+      for (int k = 0; k < OBS; ++k) p.obs_out[o * OBS + k] = b_obs[k];
+      p.act_out[o] = b_act;
+      p.logp_out[o] = b_logp;
+      p.val_out[o] = b_val;
+      if (p.ent_out) p.ent_out[o] = b_ent;
+      p.rew_out[o] = b_rew;
+      p.done_out[(size_t)env * (T + 1) + 1 + t0 + lane] = b_done;
+      if (p.epret_out) p.epret_out[o] = b_epret;
+      if (fused) {
+        hist[t0 + lane] = b_rew;
+        hist[T + t0 + lane] = b_val;
+        hist[2 * T + t0 + lane] = b_done;
       }
     }
-    if (d != 0.0f) ep_ret = 0.0f;
-    d_last = d;
-#pragma unroll
-    for (int k = 0; k < OBS; ++k) x[k] = o_obs[k];  // pre-reset obs feeds the next step
-    XA_STAMP(6);
+  };
+
+  // two chunk buffers: the next chunk's loads are in flight while this one runs
+  StepChunk<OBS> ca, cb;
+  load_chunk<OBS, REPLAY>(p, env, lane, cur0, 0, ctr, ca);
+  for (int t0 = 0; t0 < T; t0 += 128) {
+    load_chunk<OBS, REPLAY>(p, env, lane, cur0, t0 + 64, ctr, cb);
+    run_chunk(ca, t0);
+    if (t0 + 64 >= T) break;
+    load_chunk<OBS, REPLAY>(p, env, lane, cur0, t0 + 128, ctr, ca);
+    run_chunk(cb, t0 + 64);
   }
+  if constexpr (REPLAY) cur = (int)(((long long)cur0 + T) % p.t_rec);
 
   XA_STAMP(5);
   // bootstrap V(get_states()) on the post-reset state (ppo/agent.py:72)
   float logits[A], v_next;
   net.forward(st, sh, lane, logits, v_next);
   if (lane < OBS) p.env_state[(size_t)env * OBS + lane] = st[lane];
-  if (p.env_kind == XA_ENV_CARTPOLE && lane < 4) p.env_state64[(size_t)env * 4 + lane] = cp[lane];
+  if constexpr (!REPLAY) {
+    if (lane < 4) p.env_state64[(size_t)env * 4 + lane] = cp[lane];
+  }
   if (lane == 0) {
     p.env_cursor[env] = cur;
     p.ep_return[env] = ep_ret;
@@ -421,7 +450,11 @@ int launch_rollout(const XaRolloutArgs* p, hipStream_t s) {
   const size_t lds = (size_t)kWaves * H * sizeof(float) +
                      (fused ? (size_t)kWaves * 3 * p->n_steps * sizeof(float) : 0);
   dim3 grid((p->n_envs + kWaves - 1) / kWaves);
-  hipLaunchKernelGGL((mlp_rollout_kernel<OBS, A>), grid, dim3(256), lds, s, *p);
+  if (p->env_kind == XA_ENV_REPLAY) {
+    hipLaunchKernelGGL((mlp_rollout_kernel<OBS, A, true>), grid, dim3(256), lds, s, *p);
+  } else if constexpr (OBS == 4 && A == 2) {
+    hipLaunchKernelGGL((mlp_rollout_kernel<OBS, A, false>), grid, dim3(256), lds, s, *p);
+  }
   XA_CHECK_LAUNCH("xa_mlp_rollout");
   return 0;
 }

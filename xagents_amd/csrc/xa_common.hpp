@@ -80,10 +80,11 @@ XA_DEV uint32_t xa_as_uint(float f) { return __float_as_uint(f); }
 
 // exp(x): Cody-Waite reduction by ln2, degree-7 Taylor on |r| <= ln2/2, exact
 // two-step scaling by 2^n (no intermediate underflow).
+// Branch-free: the core runs on the input clamped to the finite range and the
+// special cases are fixed up with selects (no exec-mask branches in the callers).
 XA_DEV float xa_expf(float x) {
-  if (x != x) return x;
-  if (x > 88.72283935546875f) return __builtin_inff();
-  if (x < -103.97208404541015625f) return 0.0f;
+  const float xin = x;
+  x = fminf(fmaxf(x, -104.0f), 89.0f);
   float n = rintf(x * 1.44269502162933349609375f);
   float r = fmaf(n, -0.693145751953125f, x);
   r = fmaf(n, -1.428606765330187045e-06f, r);
@@ -100,22 +101,23 @@ XA_DEV float xa_expf(float x) {
   int n2 = ni - n1;
   float s1 = xa_as_float((uint32_t)(n1 + 127) << 23);
   float s2 = xa_as_float((uint32_t)(n2 + 127) << 23);
-  return (p * s1) * s2;
+  float y = (p * s1) * s2;
+  y = xin > 88.72283935546875f ? __builtin_inff() : y;
+  y = xin < -103.97208404541015625f ? 0.0f : y;
+  return xin != xin ? xin : y;
 }
 
 // log(x): FreeBSD e_logf reduction (mantissa in [sqrt(.5), sqrt(2))), s = f/(2+f).
+// Branch-free like xa_expf: the core runs on a sanitised input.
 XA_DEV float xa_logf(float x) {
-  if (x != x) return x;
-  if (x < 0.0f) return __builtin_nanf("");
-  if (x == 0.0f) return -__builtin_inff();
-  if (x == __builtin_inff()) return x;
-  int k = 0;
+  const float xin = x;
+  const bool ok = x > 0.0f && x < __builtin_inff();
+  x = ok ? x : 1.0f;
   uint32_t hx = xa_as_uint(x);
-  if (hx < 0x00800000u) {  // subnormal
-    x = x * 33554432.0f;
-    hx = xa_as_uint(x);
-    k = -25;
-  }
+  const bool sub = hx < 0x00800000u;  // subnormal: scale by 2^25
+  x = sub ? x * 33554432.0f : x;
+  hx = xa_as_uint(x);
+  int k = sub ? -25 : 0;
   k += (int)((hx >> 23) & 0xffu) - 127;
   hx &= 0x007fffffu;
   uint32_t i = (hx + (0x95f64u << 3)) & 0x800000u;
@@ -130,7 +132,11 @@ XA_DEV float xa_logf(float x) {
   float R = t2 + t1;
   float hfsq = (0.5f * f) * f;
   float dk = (float)k;
-  return dk * 6.9313812256e-01f - ((hfsq - (s * (hfsq + R) + dk * 9.0580006145e-06f)) - f);
+  float r = dk * 6.9313812256e-01f - ((hfsq - (s * (hfsq + R) + dk * 9.0580006145e-06f)) - f);
+  r = xin == __builtin_inff() ? xin : r;
+  r = xin == 0.0f ? -__builtin_inff() : r;
+  r = xin < 0.0f ? __builtin_nanf("") : r;
+  return xin != xin ? xin : r;
 }
 
 // tanh(x): branch-free odd rational minimax x*P(x^2)/Q(x^2) (13/6) on the input
