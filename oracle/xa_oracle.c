@@ -235,10 +235,12 @@ static void mlp_forward1(const float* th, int obs, int A, const float* x, float*
     h1[j] = xo_tanhf(z + th[o.b1 + j]);
   }
   for (int j = 0; j < H; ++j) {
-    float c[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-    for (int i = 0; i < 16; ++i)
-      for (int q = 0; q < 4; ++q) c[q] = fmaf(h1[16 * q + i], th[o.w2 + (16 * q + i) * H + j], c[q]);
-    h2[j] = xo_tanhf(((c[0] + c[1]) + (c[2] + c[3])) + th[o.b2 + j]);
+    /* 8 chains, chain r over k = r (mod 8) (mlp_rollout.hip LaneMlp::layer2) */
+    float c[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    for (int i = 0; i < H; i += 8)
+      for (int r = 0; r < 8; ++r) c[r] = fmaf(h1[i + r], th[o.w2 + (i + r) * H + j], c[r]);
+    h2[j] = xo_tanhf((((c[0] + c[1]) + (c[2] + c[3])) + ((c[4] + c[5]) + (c[6] + c[7]))) +
+                     th[o.b2 + j]);
   }
   for (int a = 0; a < A; ++a) {
     for (int j = 0; j < H; ++j) prod[j] = h2[j] * th[o.w3 + j * A + a];

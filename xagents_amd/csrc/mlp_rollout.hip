@@ -10,7 +10,7 @@
 // stream and the rollout stores. Per step:
 //   h1_j = tanh(sum_k x_k W1[k][j] + b1_j)              (fma chain over k)
 //   h1 -> LDS (wave-private row), 16 x ds_read_b128 broadcast back
-//   h2_j = tanh(((c0 + c1) + (c2 + c3)) + b2_j)          (4 interleaved 16-long fma chains)
+//   h2_j = tanh(sum of 8 interleaved 8-long fma chains + b2_j)
 //   logit_a = butterfly_sum_j(h2_j * W3[j][a]) + b3_a ;  value likewise
 //   softmax / log-prob / entropy / inverse-CDF sample on every lane (wave-uniform)
 //   env step (replay: records of 64 steps fetched a chunk ahead, one lane per step,
@@ -78,8 +78,8 @@ struct LaneMlp {
   }
 
   // x: wave-uniform observation. sh: this wave's 64-float LDS row.
-  // layer 1 and the h1 broadcast through this wave's LDS row
-  XA_DEV void layer1(const float (&x)[OBS], float* sh, int lane, float (&hv)[H]) const {
+  // layer 1 and the h1 broadcast through this wave's LDS row (16 x ds_read_b128)
+  XA_DEV void layer1(const float (&x)[OBS], float* sh, int lane, float4 (&hv)[H / 4]) const {
     float z1 = 0.0f;
 #pragma unroll
     for (int k = 0; k < OBS; ++k) z1 = fmaf(x[k], w1[k], z1);
@@ -87,26 +87,24 @@ struct LaneMlp {
     sh[lane] = h1;
     wave_sync();
 #pragma unroll
-    for (int k = 0; k < H; k += 4) {
-      const float4 q = *reinterpret_cast<const float4*>(sh + k);
-      hv[k] = q.x;
-      hv[k + 1] = q.y;
-      hv[k + 2] = q.z;
-      hv[k + 3] = q.w;
-    }
+    for (int k = 0; k < H / 4; ++k) hv[k] = reinterpret_cast<const float4*>(sh)[k];
     wave_sync();  // the row is rewritten by the next forward
   }
 
-  XA_DEV float layer2(const float (&hv)[H]) const {
-    float c0 = 0.0f, c1 = 0.0f, c2 = 0.0f, c3 = 0.0f;
+  // 8 interleaved 8-long fma chains, chain r over k = r (mod 8), run as 4 packed
+  // (v_pk_fma_f32) chains fed straight from the ds_read_b128 registers
+  XA_DEV float layer2(const float4 (&hv)[H / 4]) const {
+    xa_f2 c01 = {0.0f, 0.0f}, c23 = c01, c45 = c01, c67 = c01;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      c0 = fmaf(hv[i], w2[i], c0);
-      c1 = fmaf(hv[16 + i], w2[16 + i], c1);
-      c2 = fmaf(hv[32 + i], w2[32 + i], c2);
-      c3 = fmaf(hv[48 + i], w2[48 + i], c3);
+    for (int m = 0; m < H / 8; ++m) {
+      const float4 q0 = hv[2 * m], q1 = hv[2 * m + 1];
+      c01 = xa_fma2(xa_f2{q0.x, q0.y}, xa_f2{w2[8 * m + 0], w2[8 * m + 1]}, c01);
+      c23 = xa_fma2(xa_f2{q0.z, q0.w}, xa_f2{w2[8 * m + 2], w2[8 * m + 3]}, c23);
+      c45 = xa_fma2(xa_f2{q1.x, q1.y}, xa_f2{w2[8 * m + 4], w2[8 * m + 5]}, c45);
+      c67 = xa_fma2(xa_f2{q1.z, q1.w}, xa_f2{w2[8 * m + 6], w2[8 * m + 7]}, c67);
     }
-    return xa_tanhf(((c0 + c1) + (c2 + c3)) + b2);
+    return xa_tanhf((((c01.x + c01.y) + (c23.x + c23.y)) + ((c45.x + c45.y) + (c67.x + c67.y))) +
+                    b2);
   }
 
   XA_DEV void heads(float h2, float (&logits)[A], float& value) const {
@@ -118,7 +116,7 @@ struct LaneMlp {
   // x: wave-uniform observation. sh: this wave's 64-float LDS row.
   XA_DEV void forward(const float (&x)[OBS], float* sh, int lane, float (&logits)[A],
                       float& value) const {
-    float hv[H];
+    float4 hv[H / 4];
     layer1(x, sh, lane, hv);
     heads(layer2(hv), logits, value);
   }
@@ -273,7 +271,7 @@ __global__ __launch_bounds__(256) void mlp_rollout_kernel(XaRolloutArgs p) {
       XA_STAMP(0);
       float logits[A], value;
       {
-        float hv[H];
+        float4 hv[H / 4];
         net.layer1(x, sh, lane, hv);
         XA_STAMP(1);
         const float h2 = net.layer2(hv);

@@ -75,6 +75,10 @@ static __device__ unsigned long long xa_stamp_acc[64];
 // ----------------------------------------------------------------------------
 // deterministic f32 math
 // ----------------------------------------------------------------------------
+typedef float xa_f2 __attribute__((ext_vector_type(2)));
+// two IEEE fmas in one v_pk_fma_f32 (each lane rounds exactly like fmaf)
+XA_DEV xa_f2 xa_fma2(xa_f2 a, xa_f2 b, xa_f2 c) { return __builtin_elementwise_fma(a, b, c); }
+
 XA_DEV float xa_as_float(uint32_t u) { return __uint_as_float(u); }
 XA_DEV uint32_t xa_as_uint(float f) { return __float_as_uint(f); }
 
@@ -209,7 +213,7 @@ XA_DEV float xa_u01(uint32_t v) { return (float)(v >> 8) * 5.9604644775390625e-0
 // LDS round trip): quad_perm gives exact xor-1/xor-2, row_half_mirror/row_mirror pair
 // each lane with the other half of its 8/16-lane group (after the previous levels
 // every lane of a group holds the same value, so this equals xor-4/xor-8), and the
-// gfx950 permlane16/32 swaps give exact xor-16/xor-32.
+// row broadcasts finish the xor-16/xor-32 levels in lane 63, read back as a scalar.
 #define XA_DPP_F(v, ctrl) \
   __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), ctrl, 0xF, 0xF, false))
 
@@ -217,19 +221,12 @@ XA_DEV float xa_wave_sum(float v) {
   v = v + XA_DPP_F(v, 0xB1);   // quad_perm [1,0,3,2]
   v = v + XA_DPP_F(v, 0x4E);   // quad_perm [2,3,0,1]
   v = v + XA_DPP_F(v, 0x141);  // row_half_mirror
-  v = v + XA_DPP_F(v, 0x140);  // row_mirror
-  const int lane = __lane_id();
-  {
-    const auto s = __builtin_amdgcn_permlane16_swap(__float_as_int(v), __float_as_int(v), false,
-                                                    false);
-    v = v + __int_as_float(((lane >> 4) & 1) ? s[0] : s[1]);
-  }
-  {
-    const auto s = __builtin_amdgcn_permlane32_swap(__float_as_int(v), __float_as_int(v), false,
-                                                    false);
-    v = v + __int_as_float((lane >> 5) ? s[0] : s[1]);
-  }
-  return v;
+  v = v + XA_DPP_F(v, 0x140);  // row_mirror: every lane of row r holds S_r
+  // row_bcast:15 into rows 1,3 then row_bcast:31 into rows 2,3: lane 63 ends with
+  // (S2 + S3) + (S0 + S1), bitwise equal to the xor-16 / xor-32 butterfly
+  v = v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x142, 0xA, 0xF, false));
+  v = v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x143, 0xC, 0xF, false));
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
 
 XA_DEV double xa_wave_sum_f64(double v) {
