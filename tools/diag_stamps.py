@@ -53,7 +53,9 @@ def main():
                           2: 'layer2+tanh', 3: 'heads (3 wave sums)', 4: 'categorical',
                           6: 'env step + stores', 5: 'tail'}),
                         ('xa_diag_read_stamps_update',
-                         {11: 'params/pending Adam', 12: 'gather', 13: 'H1', 14: 'G1 (MFMA)+tanh',
+                         {20: 'prologue: param/grad loads', 21: 'prologue: norm + barrier',
+                          22: 'prologue: Adam + LDS stores', 11: 'adv stats + tile-loop barrier',
+                          12: 'gather', 13: 'H1', 14: 'G1 (MFMA)+tanh',
                           15: 'heads+loss', 16: 'dA2', 17: 'G2+G3 (MFMA)', 18: 'dW1',
                           19: 'epilogue (partials)'})):
         getattr(L, name)(buf)

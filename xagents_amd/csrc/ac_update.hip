@@ -39,7 +39,7 @@ constexpr int S = 32;    // samples per tile
 constexpr int LDW = 68;  // LDS row stride of [*][64] tiles (16-B aligned, conflict-spreading)
 constexpr int LDT = 36;  // LDS row stride of transposed [64][32] tiles
 constexpr int kStatsChunk = 1024;
-constexpr int kRedParams = 16, kRedGroups = 16, kRedRows = 16;  // reduce: <= 256 partial rows
+constexpr int kRedThreads = 1024, kRedBatch = 16;  // reduce: 16 waves x 16 rows, one batch for <= 256 rows
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
@@ -184,7 +184,6 @@ __global__ __launch_bounds__(256) void ac_grad_kernel(XaAcGradArgs p) {
   __shared__ float sRed[4 * H * NSLOT];
   __shared__ float sLoss[4][4];
   __shared__ double sNorm[4];
-  __shared__ float sAlpha;
 
   const Offs o = offs(OBS, A);
   const int tid = threadIdx.x;
@@ -223,6 +222,20 @@ __global__ __launch_bounds__(256) void ac_grad_kernel(XaAcGradArgs p) {
     n_adv = (idx >= 0 && p.adv_in) ? p.adv_in[ix] : 0.0f;
   };
   fetch_tile(blockIdx.x);  // in flight while the parameters are prepared
+
+  // advantage statistics of this minibatch and the Adam step: loaded up front so
+  // their round trip overlaps the parameter loads
+  double st1 = 0.0, st2 = 0.0;
+  if (is_ppo && p.adv_in == nullptr) {
+    const int n_mb = (p.batch + p.mb_size - 1) / p.mb_size;
+    const int sidx = p.epoch * n_mb + p.mb_index;
+    const int nc = stats_chunks(p.mb_size);
+    for (int c = 0; c < nc; ++c) {
+      st1 += p.adv_stats[2 * ((size_t)sidx * nc + c)];
+      st2 += p.adv_stats[2 * ((size_t)sidx * nc + c) + 1];
+    }
+  }
+  const int pend_t = p.pend_grad ? *p.adam_step : 0;
 
   // ---- parameters (optionally after the pending clip + Keras Adam step) ----
   {
@@ -277,14 +290,15 @@ __global__ __launch_bounds__(256) void ac_grad_kernel(XaAcGradArgs p) {
       for (int i = 0; i < 16; ++i) sq += (double)gw[i] * (double)gw[i];
 #pragma unroll
       for (int q = 0; q < RPT; ++q) sq += (double)gr[q] * (double)gr[q];
+      XA_STAMP(20);
       sq = xa_wave_sum_f64(sq);
       if (lane == 0) sNorm[w] = sq;
-      if (tid == 0) sAlpha = adam_alpha(p.adam.lr, p.adam.beta1, p.adam.beta2, *p.adam_step);
+      const float alpha = adam_alpha(p.adam.lr, p.adam.beta1, p.adam.beta2, pend_t);
       __syncthreads();
+      XA_STAMP(21);
       // every block forms the identical norm and step (fixed assignment and order)
       const double tot = (sNorm[0] + sNorm[1]) + (sNorm[2] + sNorm[3]);
       const float sc = clip_scale(tot, p.adam.clip_norm);
-      const float alpha = sAlpha;
       const float omb1 = 1.0f - p.adam.beta1, omb2 = 1.0f - p.adam.beta2, eps = p.adam.eps;
       const bool writer = blockIdx.x == 0;
 #pragma unroll
@@ -341,19 +355,12 @@ __global__ __launch_bounds__(256) void ac_grad_kernel(XaAcGradArgs p) {
     }
   }
 
+  XA_STAMP(22);
   float adv_mean = 0.0f, adv_std = 0.0f;
   if (is_ppo && p.adv_in == nullptr) {
-    const int n_mb = (p.batch + p.mb_size - 1) / p.mb_size;
-    const int sidx = p.epoch * n_mb + p.mb_index;
-    const int nc = stats_chunks(p.mb_size);
-    double s1 = 0.0, s2 = 0.0;
-    for (int c = 0; c < nc; ++c) {
-      s1 += p.adv_stats[2 * ((size_t)sidx * nc + c)];
-      s2 += p.adv_stats[2 * ((size_t)sidx * nc + c) + 1];
-    }
     const double n = p.adv_count;
-    const double mean = s1 / n;
-    const double var = fmax(s2 / n - mean * mean, 0.0);
+    const double mean = st1 / n;
+    const double var = fmax(st2 / n - mean * mean, 0.0);
     adv_mean = (float)mean;
     adv_std = (float)sqrt(var);
   }
@@ -445,12 +452,7 @@ __global__ __launch_bounds__(256) void ac_grad_kernel(XaAcGradArgs p) {
         for (int a = 0; a < AH; ++a) z[a] = fmaf(hj, sW34[j * AH + a], z[a]);
       }
 #pragma unroll
-      for (int a = 0; a < AH; ++a) {
-        z[a] = z[a] + __shfl_xor(z[a], 1, 64);
-        z[a] = z[a] + __shfl_xor(z[a], 2, 64);
-        z[a] = z[a] + __shfl_xor(z[a], 4, 64);
-        z[a] = z[a] + sb34[a];
-      }
+      for (int a = 0; a < AH; ++a) z[a] = xa_sum8(z[a]) + sb34[a];
       if (pp == 0) {
         float dz[AH];
 #pragma unroll
@@ -658,39 +660,40 @@ __global__ __launch_bounds__(256) void ac_grad_kernel(XaAcGradArgs p) {
 }
 
 // ---------------------------------------------------------------------------
-// gradient reduction: 16 parameters x 16 row groups per block, every row load of
-// a thread issued before the first use (one memory round trip for <= 256 rows)
+// gradient reduction: a block owns 64 consecutive parameters (lane = parameter,
+// so every row load of a wave is one contiguous 256-B segment); its 16 waves take
+// rows w, w + 16, ...; each thread issues 16 row loads before the first use
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void grad_reduce_kernel(const float* __restrict__ part, int nb,
-                                                          int P, float* __restrict__ g,
-                                                          int* adam_step) {
-  __shared__ double red[kRedGroups][kRedParams];
-  const int tid = threadIdx.x;
-  const int pp = tid % kRedParams, rg = tid / kRedParams;
-  const int pidx = blockIdx.x * kRedParams + pp;
+__global__ __launch_bounds__(kRedThreads) void grad_reduce_kernel(const float* __restrict__ part,
+                                                                  int nb, int P,
+                                                                  float* __restrict__ g,
+                                                                  int* adam_step) {
+  constexpr int W = kRedThreads / 64;
+  __shared__ double red[W][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int pidx = blockIdx.x * 64 + lane;
+  const int pc = min(pidx, P - 1);  // clamped: loads stay unconditional
   double acc = 0.0;
-  if (pidx < P) {
-    for (int b0 = rg; b0 < nb; b0 += kRedGroups * kRedRows) {
-      float x[kRedRows];
+  for (int b0 = w; b0 < nb; b0 += W * kRedBatch) {
+    float x[kRedBatch];
 #pragma unroll
-      for (int r = 0; r < kRedRows; ++r) {
-        const int b = b0 + r * kRedGroups;
-        x[r] = b < nb ? part[(size_t)b * P + pidx] : 0.0f;
-      }
-#pragma unroll
-      for (int r = 0; r < kRedRows; r += 4)
-        acc += ((double)x[r] + (double)x[r + 1]) + ((double)x[r + 2] + (double)x[r + 3]);
+    for (int r = 0; r < kRedBatch; ++r) {
+      const int b = b0 + r * W;
+      x[r] = b < nb ? part[(size_t)b * P + pc] : 0.0f;
     }
+#pragma unroll
+    for (int r = 0; r < kRedBatch; r += 4)
+      acc += ((double)x[r] + (double)x[r + 1]) + ((double)x[r + 2] + (double)x[r + 3]);
   }
-  red[rg][pp] = acc;
+  red[w][lane] = acc;
   __syncthreads();
-  if (tid < kRedParams && pidx < P) {
+  if (w == 0 && pidx < P) {
     double s = 0.0;
 #pragma unroll
-    for (int r = 0; r < kRedGroups; ++r) s += red[r][tid];
+    for (int r = 0; r < W; ++r) s += red[r][lane];
     g[pidx] = (float)s;
   }
-  if (blockIdx.x == 0 && tid == 0 && adam_step) adam_step[0] += 1;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && adam_step) adam_step[0] += 1;
 }
 
 // ---------------------------------------------------------------------------
@@ -813,8 +816,8 @@ extern "C" int xa_ac_grad(const XaAcGradArgs* p, void* stream) {
 extern "C" int xa_grad_reduce(const float* partials, int n_parts, int n_params, float* grad,
                               int* adam_step, void* stream) {
   XA_CHECK_ARG(partials && grad && n_parts > 0 && n_params > 0, "xa_grad_reduce: bad arguments");
-  const int blocks = (n_params + kRedParams - 1) / kRedParams;
-  hipLaunchKernelGGL(grad_reduce_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+  const int blocks = (n_params + 63) / 64;
+  hipLaunchKernelGGL(grad_reduce_kernel, dim3(blocks), dim3(kRedThreads), 0, (hipStream_t)stream,
                      partials, n_parts, n_params, grad, adam_step);
   XA_CHECK_LAUNCH("xa_grad_reduce");
   return 0;

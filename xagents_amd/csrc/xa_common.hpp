@@ -229,10 +229,34 @@ XA_DEV float xa_wave_sum(float v) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
 
+// f64 DPP move: the two 32-bit halves take the same lane permutation
+template <int CTRL, int ROW_MASK = 0xF>
+XA_DEV double xa_dpp_f64(double v) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, CTRL, ROW_MASK, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), CTRL, ROW_MASK, 0xF, false);
+  return __longlong_as_double((long long)(((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo));
+}
+
+// same tree as xa_wave_sum, in f64; the result is wave-uniform
 XA_DEV double xa_wave_sum_f64(double v) {
-#pragma unroll
-  for (int m = 1; m < 64; m <<= 1) v = v + __shfl_xor(v, m, 64);
-  return v;
+  v = v + xa_dpp_f64<0xB1>(v);
+  v = v + xa_dpp_f64<0x4E>(v);
+  v = v + xa_dpp_f64<0x141>(v);
+  v = v + xa_dpp_f64<0x140>(v);
+  v = v + xa_dpp_f64<0x142, 0xA>(v);
+  v = v + xa_dpp_f64<0x143, 0xC>(v);
+  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, 63);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), 63);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+// sum over aligned 8-lane groups (xor 1, 2, 4), every lane of a group ends with it
+XA_DEV float xa_sum8(float v) {
+  v = v + XA_DPP_F(v, 0xB1);
+  v = v + XA_DPP_F(v, 0x4E);
+  return v + XA_DPP_F(v, 0x141);
 }
 
 // ----------------------------------------------------------------------------
