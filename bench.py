@@ -21,9 +21,15 @@ sys.path.insert(0, str(ROOT))
 
 METRIC = 'env-steps/sec/GPU (PPO 16-env) + update ms; 1/2/4/8 MI355X'
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
+F32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: f32-input MFMA dense peak (= vector peak)
 # rollout kernel algorithmic bytes per env-step (replay env): reads obs 16 + state 16 +
 # reward 4 + done 4; writes obs 16 + action/logp/value/entropy/reward/done/epret/return 32
 ROLLOUT_BYTES_PER_ENV_STEP = 40 + 48
+
+
+def mlp_fwd_flops(obs_dim=4, n_actions=2, hidden=64):
+    """F = forward FLOPs per sample of the actor-critic MLP (9,088)."""
+    return 2 * (obs_dim * hidden + hidden * hidden + hidden * (n_actions + 1))
 
 
 def parse():
@@ -62,12 +68,12 @@ def cpu_baseline(args, record, theta0):
     }
 
 
-def load_traffic(workload_key):
+def load_traffic(key):
+    """HBM bytes per launch from the committed PMC passes (profiles/traffic.json)."""
     f = ROOT / 'profiles' / 'traffic.json'
     if not f.exists():
         return None
-    data = json.loads(f.read_text())
-    entry = data.get(workload_key)
+    entry = json.loads(f.read_text()).get(key)
     return entry.get('bytes_per_launch') if entry else None
 
 
@@ -111,6 +117,12 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    # per-kernel durations: HIP events around the rollout launch and the 16 xa_ac_grad
+    # launches of 3 eagerly launched train steps right after the timed region
+    ktimes = {'rollout': [], 'ac_grad': []}
+    for _ in range(3):
+        for k, v in agent.timed_train_step().items():
+            ktimes[k] += v
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -122,10 +134,15 @@ def main():
     agent._drain_episode_stats()
 
     if rank == 0:
-        launch_bytes = ROLLOUT_BYTES_PER_ENV_STEP * args.n_envs * args.n_steps
-        achieved = launch_bytes / (rollout_ms * 1e-3) / 1e9
-        workload_key = f'ppo_mlp_rollout_n{args.n_envs}_t{args.n_steps}'
-        traffic = load_traffic(workload_key)
+        # dominant kernel: xa_ac_grad (16 launches per step); one launch processes one
+        # minibatch: forward + backward = 3F FLOPs per sample
+        mb = args.n_envs * args.n_steps // 4
+        grad_ms = float(np.mean(ktimes['ac_grad']))
+        grad_flops = 3 * mlp_fwd_flops() * mb
+        grad_tflops = grad_flops / (grad_ms * 1e-3) / 1e12
+        roll_kms = float(np.mean(ktimes['rollout']))
+        roll_bytes = ROLLOUT_BYTES_PER_ENV_STEP * args.n_envs * args.n_steps
+        roll_gbs = roll_bytes / (roll_kms * 1e-3) / 1e9
         line = {
             'metric': METRIC,
             'value': round(value, 1),
@@ -155,13 +172,27 @@ def main():
             'rollout_ms': round(rollout_ms, 4),
             'env_steps_per_sec_per_gpu': round(value / world, 1),
             'roofline': {
-                'kernel': 'xa_mlp_rollout (mlp_rollout_kernel<4,2>)',
+                'kernel': 'xa_ac_grad (ac_grad_kernel<4,2>)',
+                'bound': 'mfma',
+                'achieved': round(grad_tflops, 3),
+                'peak': F32_MFMA_PEAK_TFLOPS,
+                'unit': 'TFLOP/s',
+                'frac': round(grad_tflops / F32_MFMA_PEAK_TFLOPS, 5),
+                'traffic': load_traffic('ac_grad'),
+                'launch_ms': round(grad_ms, 5),
+                'note': f'3F = {3 * mlp_fwd_flops()} FLOP/sample (fwd + bwd) x {mb} samples '
+                        'per launch; latency-bound (one 32-sample tile per workgroup); '
+                        'traffic = PMC FETCH_SIZE x 2 + WRITE_SIZE per launch',
+            },
+            'rollout_roofline': {
+                'kernel': 'xa_mlp_rollout (mlp_rollout_kernel<4,2,replay>)',
                 'bound': 'hbm',
-                'achieved': round(achieved, 3),
+                'achieved': round(roll_gbs, 3),
                 'peak': HBM_PEAK_GBS,
                 'unit': 'GB/s',
-                'frac': round(achieved / HBM_PEAK_GBS, 6),
-                'traffic': traffic,
+                'frac': round(roll_gbs / HBM_PEAK_GBS, 6),
+                'traffic': load_traffic('rollout'),
+                'launch_ms': round(roll_kms, 5),
                 'note': 'latency-bound: 128 dependent policy steps per env; '
                         f'{ROLLOUT_BYTES_PER_ENV_STEP} algorithmic B/env-step x '
                         f'{args.n_envs * args.n_steps} env-steps per launch',

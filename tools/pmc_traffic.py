@@ -1,0 +1,57 @@
+"""Turn the two rocprofv3 PMC passes (tools/gpurun_pmc.sh) into profiles/traffic.json:
+HBM bytes per launch of the hot kernels. FETCH_SIZE / WRITE_SIZE are in KB; on gfx950
+FETCH_SIZE counts half the bytes of wide coalesced reads (MI355X_MICROARCH.md, HBM), so
+it is doubled; WRITE_SIZE is exact for 16-B-per-lane stores."""
+import csv
+import json
+import sys
+from collections import defaultdict
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+KERNELS = {'ac_grad': 'ac_grad_kernel<4, 2>', 'rollout': 'mlp_rollout_kernel<4, 2, true>',
+           'grad_reduce': 'grad_reduce_kernel', 'minibatch': 'minibatch_kernel'}
+
+
+def per_kernel(counter, src):
+    files = sorted(Path(src).rglob('*counter_collection.csv'))
+    if not files:
+        raise SystemExit(f'no counter_collection.csv under {src}')
+    vals = defaultdict(list)
+    for f in files:
+        for row in csv.DictReader(open(f)):
+            if row.get('Counter_Name') != counter:
+                continue
+            name = row.get('Kernel_Name', '')
+            for key, pat in KERNELS.items():
+                if pat in name:
+                    vals[key].append(float(row['Counter_Value']))
+    return {k: (sum(v) / len(v), len(v)) for k, v in vals.items()}
+
+
+def main(out_dir='gpurun_out'):
+    fetch = per_kernel('FETCH_SIZE', Path(out_dir) / 'pmc_FETCH_SIZE')
+    write = per_kernel('WRITE_SIZE', Path(out_dir) / 'pmc_WRITE_SIZE')
+    res = {}
+    for k in KERNELS:
+        if k in fetch and k in write:
+            f_kb, n = fetch[k]
+            w_kb, _ = write[k]
+            res[k] = {'bytes_per_launch': round((2 * f_kb + w_kb) * 1024),
+                      'fetch_size_kb_raw': round(f_kb, 1), 'write_size_kb': round(w_kb, 1),
+                      'dispatches': n,
+                      'correction': 'FETCH_SIZE x 2 (gfx950 wide-read tally), KB = 1024 B'}
+    if 'grad_reduce' in res:
+        # calibration on a known byte count (MI355X_MICROARCH.md: other access widths are
+        # uncalibrated): xa_grad_reduce reads exactly 256 rows x 4675 f32 with 4-B lanes
+        known = 256 * 4675 * 4
+        res['calibration'] = {'kernel': 'grad_reduce', 'known_read_bytes': known,
+                              'fetch_raw_bytes': round(fetch['grad_reduce'][0] * 1024),
+                              'factor': round(known / (fetch['grad_reduce'][0] * 1024), 3)}
+    (ROOT / 'profiles').mkdir(exist_ok=True)
+    (ROOT / 'profiles' / 'traffic.json').write_text(json.dumps(res, indent=1) + '\n')
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == '__main__':
+    main(*sys.argv[1:])

@@ -162,11 +162,42 @@ class A2C(OnPolicy):
         self._optimizer_step()
 
     def _update(self):
+        self._kernel_event('ac_grad', 0, 0)
         kernels.ac_grad(self._gargs)
+        self._kernel_event('ac_grad', 0, 1)
         self._apply_gradients(self.partials)
 
     def _rollout_impl(self):
+        self._kernel_event('rollout', 0, 0)
         kernels.rollout(self._rargs)
+        self._kernel_event('rollout', 0, 1)
+
+    # ---- per-kernel timing (bench): HIP event pairs around the rollout launch and
+    # every xa_ac_grad launch of an eagerly launched train step (ROCm torch refuses
+    # external events inside graph capture, so captured steps record none) --------
+    def timed_train_step(self):
+        """One eager train step with events around the hot launches; returns
+        {'rollout': [ms], 'ac_grad': [ms per launch]} (synchronizes)."""
+        ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
+        n_grad = len(getattr(self, '_gargs_list', [None]))
+        self._kernel_events = {'rollout': [(ev(), ev())],
+                               'ac_grad': [(ev(), ev()) for _ in range(n_grad)]}
+        try:
+            # park the stream on a spin kernel so the host enqueues the whole step behind
+            # it: the event pairs then bracket GPU execution, not host launch gaps
+            torch.cuda._sleep(20_000_000)
+            self._step_impl()
+            self.steps += self.n_envs * self.n_steps
+            self._queue_episode_stats(self.b_done, self.b_epret)
+            torch.cuda.synchronize()
+            return {k: [a.elapsed_time(b) for a, b in v] for k, v in self._kernel_events.items()}
+        finally:
+            self._kernel_events = None
+
+    def _kernel_event(self, name, i, j):
+        evs = getattr(self, '_kernel_events', None)
+        if evs is not None:
+            evs[name][i][j].record()
 
     def _update_impl(self):
         self._update()

@@ -123,8 +123,10 @@ class PPO(A2C):
     def _update(self):
         kernels.minibatches(self._mbargs)
         self._all_reduce(self.adv_stats)
-        for g in self._gargs_list:
+        for i, g in enumerate(self._gargs_list):
+            self._kernel_event('ac_grad', i, 0)
             kernels.ac_grad(g)
+            self._kernel_event('ac_grad', i, 1)
             self._reduce_gradients(self.partials)
         self._optimizer_step(self._final_src)
 
