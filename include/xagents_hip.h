@@ -23,6 +23,7 @@
 #ifndef XAGENTS_HIP_H
 #define XAGENTS_HIP_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -253,6 +254,91 @@ int xa_clip_adam(float* theta, float* adam_m, float* adam_v, const float* grad, 
                  float grad_scale, float clip_norm, float lr, float beta1, float beta2,
                  float eps, const int* adam_step, double* workspace, float* gnorm_out,
                  float* theta_out, float* m_out, float* v_out, void* stream);
+
+/* ------------------------------------------------------------------------- */
+/* Dense / Conv1D building blocks (CNN cfgs: xagents/dqn/models/cnn.cfg,      */
+/* xagents/ppo/models/cnn-actor-critic.cfg; TD3/DDPG MLPs in td3/models)     */
+/* ------------------------------------------------------------------------- */
+#define XA_ACT_NONE 0
+#define XA_ACT_RELU 1
+#define XA_ACT_TANH 2
+
+/*
+ * f32 GEMM with grouped-affine operand addressing (gemm.hip):
+ *   C(m, n) = [C(m, n) +] act(sum_k A(m, k) B(k, n) + bias[n]) * [gate(m, n) > 0]
+ *   A(m, k) = a[f(m) + g(k)], f(m) = (m / a_pm) a_rm + (m % a_pm) a_sm,
+ *                             g(k) = (k / a_pk) a_rk + (k % a_pk) a_sk
+ *   B(k, n) = b[k b_ks + n b_ns];  C(m, n) = c[m ldc + n];  gate(m, n) = gate[m ld_gate + n]
+ * a == NULL means A = 1 (column sums of B, e.g. bias gradients). a_u8: A holds uint8
+ * pixels scaled as f32(x) / 255 (xagents/base.py:505-506). Keras Conv1D on (B,H,W,C)
+ * input is a_pm = W_out, a_rm = W_in C, a_sm = stride C, g(k) = k.
+ * splits > 1 splits K over workgroups; partials (>= xa_gemm_workspace_floats) holds
+ * the split sums, reduced in fixed order (deterministic).
+ */
+typedef struct XaGemmArgs {
+  int M, N, K;
+  const void* a;
+  int a_u8;
+  int64_t a_pm, a_rm, a_sm, a_pk, a_rk, a_sk;
+  const float* b;
+  int64_t b_ks, b_ns;
+  float* c;
+  int64_t ldc;
+  int splits;
+  float* partials;
+  const float* bias;
+  int act;
+  const float* gate;
+  int64_t ld_gate;
+  int beta;
+} XaGemmArgs;
+
+int xa_gemm(const XaGemmArgs* args, void* stream);
+int xa_gemm_splits(int M, int N, int K);
+size_t xa_gemm_workspace_floats(int M, int N, int K, int splits);
+
+/* Keras Conv1D input gradient (col2im as a fixed-order gather):
+ *   dinput[row][q][c] = sum over taps t, positions p with s p + t = q of
+ *                       dcol[(row P + p) (k C) + t C + c],  times [gate[row][q][c] > 0]
+ * dcol = dY W^T in im2col layout [rows P, k C]; gate = the ReLU output of the layer that
+ * produced the input (NULL: no gate). */
+int xa_conv1d_input_grad(const float* dcol, int rows, int positions, int kernel, int stride,
+                         int channels, int width_in, const float* gate, float* dinput,
+                         void* stream);
+
+/* DQN.get_actions (xagents/dqn/agent.py:107-116): actions[i] = tf.argmax(q[i]) (first max),
+ * or random_actions[i] when use_random (the host draws np.random.random() < epsilon and
+ * np.random.randint(0, A, n) exactly as the reference). */
+int xa_dqn_act(const float* q, int n, int n_actions, const int* random_actions, int use_random,
+               int* actions, void* stream);
+
+/* DQN.get_targets + update_gradients loss (dqn/agent.py:118-171): y = v' gamma + r with
+ * v' = max_a Qt(s') (or Qt(s')[argmax Q(s')] when q_next_online != NULL), 0 where done;
+ * MSE over actions, summed over the batch by minimize: dq[b][a_b] = -2 (y - q[b][a_b]) / A,
+ * 0 elsewhere; loss[b] (optional) = (y - q[b][a_b])^2 / A. */
+int xa_dqn_td_grad(const float* q, const float* q_next_target, const float* q_next_online,
+                   const int* actions, const float* rewards, const float* dones, int batch,
+                   int n_actions, float gamma, float* dq, float* loss, void* stream);
+
+/* Replay rings (ReplayBuffer1 xagents/utils/buffers.py:59-98, ReplayBuffer2 101-148):
+ * ring[slots[i]] = src[i] / dst[i] = ring[slots[i]] for items of item_bytes. The host
+ * computes slots with the reference's index semantics (deque order + random.sample for
+ * RB1, current_size % size with the row-0 overwrite + np.random.randint for RB2). */
+int xa_ring_scatter(const void* src, void* ring, const int64_t* slots, int n_items,
+                    int64_t item_bytes, void* stream);
+int xa_ring_gather(const void* ring, void* dst, const int64_t* slots, int n_items,
+                   int64_t item_bytes, void* stream);
+
+/* dst = (1 - tau) dst + tau src (DDPG.sync_target_models, xagents/ddpg/agent.py:73-85);
+ * tau = 1 copies (DQN.sync_target_model, dqn/agent.py:97-105). */
+int xa_polyak(const float* src, float* dst, int64_t n, float tau, void* stream);
+
+/* Keras OptimizerV2 `iterations += 1` on device (before xa_clip_adam reads t). */
+int xa_adam_step_bump(int* adam_step, void* stream);
+
+/* dz = dy * act'(y) given the activation OUTPUT y (relu: [y > 0]; tanh: 1 - y^2). */
+int xa_activation_grad(const float* y, const float* dy, int64_t n, int act, float* dz,
+                       void* stream);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,113 @@
+"""GPU parity of the GEMM building block and of .cfg models run by the layer executor
+(xagents_amd/layers.py) against the float64 restatement (oracle/nets_f64.py).
+Float tolerance: f32 accumulation vs f64, rtol 1e-4 relative to the output scale."""
+import ctypes
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+
+ROOT = Path(__file__).resolve().parents[1]
+pytestmark = pytest.mark.gpu
+
+
+def _close(got, ref, rtol=1e-4):
+    got = np.asarray(got, np.float64)
+    ref = np.asarray(ref, np.float64)
+    scale = max(np.abs(ref).max(), 1e-12)
+    err = np.abs(got - ref).max() / scale
+    assert err < rtol, f'max error {err:.3g} (relative to max |ref| = {scale:.3g})'
+
+
+@pytest.mark.parametrize('M,N,K,splits', [(37, 50, 29, 1), (64, 512, 3000, 8), (130, 70, 1000, 4)])
+def test_gemm_plain_bias_relu_split(device, M, N, K, splits):
+    from xagents_amd.layers import gemm
+    from xagents_amd._lib import XA_ACT_RELU
+    rng = np.random.default_rng(M + N + K)
+    A = rng.normal(size=(M, K)).astype(np.float32)
+    B = rng.normal(size=(K, N)).astype(np.float32)
+    b = rng.normal(size=N).astype(np.float32)
+    ta, tb, tbias = (torch.from_numpy(x).to(device) for x in (A, B, b))
+    C = torch.empty(M, N, device=device)
+    ws = torch.empty(splits * M * N + 1, device=device)
+    gemm(M, N, K, ta.data_ptr(), tb.data_ptr(), C.data_ptr(), a_m=(1, K, 0), b_ks=N, b_ns=1,
+         ldc=N, bias=tbias.data_ptr(), act=XA_ACT_RELU, workspace=ws, splits=splits)
+    ref = np.maximum(A.astype(np.float64) @ B + b, 0)
+    _close(C.cpu().numpy(), ref)
+
+
+def test_gemm_transposes_gate_beta_u8(device):
+    from xagents_amd.layers import gemm
+    rng = np.random.default_rng(3)
+    M, N, K = 70, 45, 33
+    At = rng.normal(size=(K, M)).astype(np.float32)      # A = At^T  (m-major loader)
+    Bt = rng.normal(size=(N, K)).astype(np.float32)      # B = Bt^T  (k-major loader)
+    gate = rng.normal(size=(M, N)).astype(np.float32)
+    C0 = rng.normal(size=(M, N)).astype(np.float32)
+    ta, tb, tg = (torch.from_numpy(x).to(device) for x in (At, Bt, gate))
+    C = torch.from_numpy(C0.copy()).to(device)
+    gemm(M, N, K, ta.data_ptr(), tb.data_ptr(), C.data_ptr(), a_m=(1, 1, 0), a_k=(1, M, 0),
+         b_ks=1, b_ns=K, ldc=N, gate=tg.data_ptr(), ld_gate=N, beta=True, splits=1)
+    ref = C0 + (At.T.astype(np.float64) @ Bt.T) * (gate > 0)
+    _close(C.cpu().numpy(), ref)
+    # uint8 A scaled by 1/255 (base.py:505-506), implicit Conv1D im2col: rows of W=20,
+    # C=3 channels, kernel 4, stride 2 -> P = 9 positions
+    rows, W, Cc, k, s = 11, 20, 3, 4, 2
+    P = (W - k) // s + 1
+    x = rng.integers(0, 256, size=(rows, W, Cc), dtype=np.uint8)
+    Wt = rng.normal(size=(k * Cc, 8)).astype(np.float32)
+    tx = torch.from_numpy(x).to(device)
+    tw = torch.from_numpy(Wt).to(device)
+    out = torch.empty(rows * P, 8, device=device)
+    gemm(rows * P, 8, k * Cc, tx.data_ptr(), tw.data_ptr(), out.data_ptr(), a_u8=True,
+         a_m=(P, W * Cc, s * Cc), b_ks=8, b_ns=1, ldc=8, splits=1)
+    xf = (x.astype(np.float32) / np.float32(255.0)).astype(np.float64)
+    idx = np.arange(P)[:, None] * s + np.arange(k)[None, :]
+    cols = xf[:, idx, :].reshape(rows * P, k * Cc)
+    _close(out.cpu().numpy(), cols @ Wt)
+
+
+def _model(cfg, units, input_shape, device, seed=5):
+    from xagents_amd.nets import Adam, ModelReader
+    return ModelReader(str(cfg), units, input_shape, Adam(), seed=seed,
+                       device=device).build_model()
+
+
+@pytest.mark.parametrize('cfg,units,shape,B', [
+    ('dqn/models/cnn.cfg', [6], (84, 84, 1), 2),
+    ('ppo/models/cnn-actor-critic.cfg', [4, 1], (84, 84, 1), 3),
+    ('td3/models/ann-actor.cfg', [4], (24,), 9),
+    ('td3/models/ann-critic.cfg', [1], (28,), 9),
+])
+def test_layer_executor_forward_backward_vs_f64(device, cfg, units, shape, B):
+    import sys
+    sys.path.insert(0, str(ROOT / 'oracle'))
+    import nets_f64 as O
+    from xagents_amd.layers import LayerExecutor
+    model = _model(ROOT / 'xagents_amd' / cfg, units, shape, device)
+    rng = np.random.default_rng(11)
+    if len(shape) == 3:
+        x = rng.integers(0, 256, size=(B, *shape), dtype=np.uint8)
+    else:
+        x = rng.normal(size=(B, *shape)).astype(np.float32)
+    ex = LayerExecutor(model, B)
+    outs = ex.forward(torch.from_numpy(x).to(device))
+    theta = model.theta.cpu().numpy()
+    x64, ref_outs = O.forward(model.layers, theta, x, shape)
+    for o, i in zip(outs, model.outputs):
+        _close(o.cpu().numpy(), ref_outs[i])
+    douts = [rng.normal(size=o.shape).astype(np.float32) for o in outs]
+    grad = torch.zeros(model.n_params, device=device)
+    ex.backward([torch.from_numpy(d).to(device) for d in douts], grad)
+    ref_g = O.backward(model.layers, theta, x64, ref_outs,
+                       {i: d for i, d in zip(model.outputs, douts)})
+    # per parameter tensor, relative to that tensor's scale
+    sls, _ = O.param_slices(model.layers)
+    g = grad.cpu().numpy()
+    for sl in sls:
+        if sl is None:
+            continue
+        for off, s in sl:
+            n = int(np.prod(s))
+            _close(g[off:off + n], ref_g[off:off + n], rtol=2e-4)

@@ -6,7 +6,7 @@ stream is torch's current HIP stream so the calls compose with torch ops and can
 be captured into a hipGraph (torch.cuda.CUDAGraph).
 """
 import ctypes
-from ctypes import (POINTER, Structure, c_double, c_float, c_int, c_uint64,
+from ctypes import (POINTER, Structure, c_double, c_float, c_int, c_int64, c_uint64,
                     c_void_p)
 from pathlib import Path
 
@@ -131,6 +131,31 @@ class XaAcGradArgs(Structure):
     ]
 
 
+class XaGemmArgs(Structure):
+    _fields_ = [
+        ('M', c_int), ('N', c_int), ('K', c_int),
+        ('a', c_void_p),
+        ('a_u8', c_int),
+        ('a_pm', c_int64), ('a_rm', c_int64), ('a_sm', c_int64),
+        ('a_pk', c_int64), ('a_rk', c_int64), ('a_sk', c_int64),
+        ('b', c_void_p),
+        ('b_ks', c_int64), ('b_ns', c_int64),
+        ('c', c_void_p),
+        ('ldc', c_int64),
+        ('splits', c_int),
+        ('partials', c_void_p),
+        ('bias', c_void_p),
+        ('act', c_int),
+        ('gate', c_void_p),
+        ('ld_gate', c_int64),
+        ('beta', c_int),
+    ]
+
+
+XA_ACT_NONE = 0
+XA_ACT_RELU = 1
+XA_ACT_TANH = 2
+
 _SIGNATURES = {
     'xa_abi_version': (c_int, []),
     'xa_last_error': (ctypes.c_char_p, []),
@@ -162,6 +187,23 @@ _SIGNATURES = {
          c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
          c_void_p],
     ),
+    'xa_gemm': (c_int, [POINTER(XaGemmArgs), c_void_p]),
+    'xa_gemm_splits': (c_int, [c_int, c_int, c_int]),
+    'xa_gemm_workspace_floats': (ctypes.c_size_t, [c_int, c_int, c_int, c_int]),
+    'xa_conv1d_input_grad': (
+        c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
+    ),
+    'xa_dqn_act': (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p]),
+    'xa_dqn_td_grad': (
+        c_int,
+        [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float,
+         c_void_p, c_void_p, c_void_p],
+    ),
+    'xa_ring_scatter': (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int64, c_void_p]),
+    'xa_ring_gather': (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int64, c_void_p]),
+    'xa_polyak': (c_int, [c_void_p, c_void_p, c_int64, c_float, c_void_p]),
+    'xa_adam_step_bump': (c_int, [c_void_p, c_void_p]),
+    'xa_activation_grad': (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p, c_void_p]),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGNATURES)

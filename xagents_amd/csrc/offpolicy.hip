@@ -1,0 +1,253 @@
+// Off-policy hot path pieces around the GEMMs (gemm.hip):
+//   * Conv1D input gradient (col2im as a gather, deterministic) with the ReLU gate of
+//     the layer below,
+//   * DQN epsilon-greedy action selection and TD targets + MSE gradient
+//     (xagents/dqn/agent.py:107-171),
+//   * replay rings on device: ReplayBuffer1 (deque + random.sample,
+//     xagents/utils/buffers.py:59-98) and ReplayBuffer2 (row-0 overwrite when full,
+//     buffers.py:101-148) append / gather. The ring position arithmetic that
+//     reproduces the reference's index semantics lives on the host; the kernels move
+//     the bytes.
+#include "../../include/xagents_hip.h"
+#include "xa_common.hpp"
+
+namespace {
+
+// dAct[row][q][c] = sum_t dcol[(row P + (q - t) / s) (k C) + t C + c] over taps t with
+// (q - t) >= 0, (q - t) % s == 0, (q - t) / s < P; then * [gate > 0]
+__global__ __launch_bounds__(256) void col2im_kernel(const float* __restrict__ dcol, int rows,
+                                                     int P, int k, int s, int C, int W_in,
+                                                     const float* __restrict__ gate,
+                                                     float* __restrict__ out) {
+  const int64_t total = (int64_t)rows * W_in * C;
+  for (int64_t e = blockIdx.x * 256ll + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int c = (int)(e % C);
+    const int64_t rq = e / C;
+    const int q = (int)(rq % W_in);
+    const int64_t row = rq / W_in;
+    float acc = 0.0f;
+    for (int t = 0; t < k; ++t) {
+      const int d = q - t;
+      if (d < 0 || d % s != 0) continue;
+      const int p = d / s;
+      if (p >= P) continue;
+      acc = acc + dcol[((row * P + p) * k + t) * C + c];
+    }
+    if (gate && !(gate[e] > 0.0f)) acc = 0.0f;
+    out[e] = acc;
+  }
+}
+
+// argmax (first max, tf.argmax) of each row of q [n x A]; rows flagged random take the
+// host-drawn action (np.random.randint, dqn/agent.py:114-116)
+__global__ void dqn_act_kernel(const float* __restrict__ q, int n, int A,
+                               const int* __restrict__ random_actions, int use_random,
+                               int* __restrict__ actions) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (use_random) {
+    actions[i] = random_actions[i];
+    return;
+  }
+  const float* r = q + (size_t)i * A;
+  int best = 0;
+  float bv = r[0];
+  for (int a = 1; a < A; ++a)
+    if (r[a] > bv) {
+      bv = r[a];
+      best = a;
+    }
+  actions[i] = best;
+}
+
+// DQN.get_targets + the MSE gradient (dqn/agent.py:118-171):
+//   v' = double ? Qt(s')[argmax Q(s')] : max_a Qt(s');  v' = 0 where done
+//   y_b = v' gamma + r_b;   L = sum_b mean_a (y - Q)^2 (minimize on a [B] loss sums)
+//   dQ[b][a_b] = -2 (y_b - Q[b][a_b]) / A, zero elsewhere (y copies Q off the action)
+__global__ void dqn_td_kernel(const float* __restrict__ q, const float* __restrict__ q_next_t,
+                              const float* __restrict__ q_next_o, const int* __restrict__ act,
+                              const float* __restrict__ rew, const float* __restrict__ done,
+                              int B, int A, float gamma, float* __restrict__ dq,
+                              float* __restrict__ loss) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const float* qt = q_next_t + (size_t)b * A;
+  float v;
+  if (q_next_o) {
+    const float* qo = q_next_o + (size_t)b * A;
+    int best = 0;
+    float bv = qo[0];
+    for (int a = 1; a < A; ++a)
+      if (qo[a] > bv) {
+        bv = qo[a];
+        best = a;
+      }
+    v = qt[best];
+  } else {
+    v = qt[0];
+    for (int a = 1; a < A; ++a) v = fmaxf(v, qt[a]);
+  }
+  if (done[b] != 0.0f) v = 0.0f;
+  const float y = v * gamma + rew[b];
+  const int ab = act[b];
+  const float diff = y - q[(size_t)b * A + ab];
+  for (int a = 0; a < A; ++a) dq[(size_t)b * A + a] = a == ab ? (-2.0f * diff) / (float)A : 0.0f;
+  if (loss) loss[b] = (diff * diff) / (float)A;
+}
+
+// ring[slot[i]] <- src[i] for n_items items of item_bytes each (append)
+__global__ __launch_bounds__(256) void ring_scatter_kernel(const uint8_t* __restrict__ src,
+                                                           uint8_t* __restrict__ ring,
+                                                           const int64_t* __restrict__ slots,
+                                                           int n_items, int64_t item_bytes) {
+  const int i = blockIdx.y;
+  if (i >= n_items) return;
+  const uint8_t* s = src + (int64_t)i * item_bytes;
+  uint8_t* d = ring + slots[i] * item_bytes;
+  if ((item_bytes & 15) == 0 && ((uintptr_t)s & 15) == 0 && ((uintptr_t)d & 15) == 0) {
+    const int64_t n16 = item_bytes >> 4;
+    for (int64_t e = blockIdx.x * 256ll + threadIdx.x; e < n16; e += (int64_t)gridDim.x * 256)
+      reinterpret_cast<uint4*>(d)[e] = reinterpret_cast<const uint4*>(s)[e];
+  } else {
+    for (int64_t e = blockIdx.x * 256ll + threadIdx.x; e < item_bytes; e += (int64_t)gridDim.x * 256)
+      d[e] = s[e];
+  }
+}
+
+// dst[i] <- ring[slot[i]] (sample gather, env-major batch order)
+__global__ __launch_bounds__(256) void ring_gather_kernel(const uint8_t* __restrict__ ring,
+                                                          uint8_t* __restrict__ dst,
+                                                          const int64_t* __restrict__ slots,
+                                                          int n_items, int64_t item_bytes) {
+  const int i = blockIdx.y;
+  if (i >= n_items) return;
+  const uint8_t* s = ring + slots[i] * item_bytes;
+  uint8_t* d = dst + (int64_t)i * item_bytes;
+  if ((item_bytes & 15) == 0 && ((uintptr_t)s & 15) == 0 && ((uintptr_t)d & 15) == 0) {
+    const int64_t n16 = item_bytes >> 4;
+    for (int64_t e = blockIdx.x * 256ll + threadIdx.x; e < n16; e += (int64_t)gridDim.x * 256)
+      reinterpret_cast<uint4*>(d)[e] = reinterpret_cast<const uint4*>(s)[e];
+  } else {
+    for (int64_t e = blockIdx.x * 256ll + threadIdx.x; e < item_bytes; e += (int64_t)gridDim.x * 256)
+      d[e] = s[e];
+  }
+}
+
+// y = (1 - tau) y + tau x (DDPG.sync_target_models, ddpg/agent.py:73-85); tau = 1: copy
+__global__ __launch_bounds__(256) void polyak_kernel(const float* __restrict__ x,
+                                                     float* __restrict__ y, int64_t n,
+                                                     float tau) {
+  for (int64_t e = blockIdx.x * 256ll + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256)
+    y[e] = tau == 1.0f ? x[e] : (1.0f - tau) * y[e] + tau * x[e];
+}
+
+__global__ void step_bump_kernel(int* step) { step[0] += 1; }
+
+// dz = dy * act'(y) from the layer output y (relu: y > 0; tanh: 1 - y^2)
+__global__ __launch_bounds__(256) void act_grad_kernel(const float* __restrict__ y,
+                                                       const float* __restrict__ dy, int64_t n,
+                                                       int act, float* __restrict__ dz) {
+  for (int64_t e = blockIdx.x * 256ll + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256) {
+    const float v = y[e];
+    float d = dy[e];
+    if (act == XA_ACT_RELU) d = v > 0.0f ? d : 0.0f;
+    else if (act == XA_ACT_TANH) d = d * (1.0f - v * v);
+    dz[e] = d;
+  }
+}
+
+int grid_for(int64_t n) {
+  const int64_t b = (n + 255) / 256;
+  return (int)(b < 8192 ? (b > 0 ? b : 1) : 8192);
+}
+
+// workgroups per item: one 256-thread pass of 16-B chunks each, at most 64
+int ring_grid_x(int64_t item_bytes) {
+  const int64_t g = ((item_bytes + 15) / 16 + 255) / 256;
+  return (int)(g < 1 ? 1 : (g > 64 ? 64 : g));
+}
+
+}  // namespace
+
+extern "C" int xa_conv1d_input_grad(const float* dcol, int rows, int positions, int kernel,
+                                    int stride, int channels, int width_in, const float* gate,
+                                    float* dinput, void* stream) {
+  XA_CHECK_ARG(dcol && dinput && rows > 0 && positions > 0 && kernel > 0 && stride > 0 &&
+                   channels > 0 && width_in >= (positions - 1) * stride + kernel,
+               "xa_conv1d_input_grad: bad arguments");
+  const int64_t total = (int64_t)rows * width_in * channels;
+  hipLaunchKernelGGL(col2im_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream,
+                     dcol, rows, positions, kernel, stride, channels, width_in, gate, dinput);
+  XA_CHECK_LAUNCH("xa_conv1d_input_grad");
+  return 0;
+}
+
+extern "C" int xa_dqn_act(const float* q, int n, int n_actions, const int* random_actions,
+                          int use_random, int* actions, void* stream) {
+  XA_CHECK_ARG(actions && n > 0 && n_actions > 0 && (use_random ? random_actions != nullptr : q != nullptr),
+               "xa_dqn_act: bad arguments");
+  hipLaunchKernelGGL(dqn_act_kernel, dim3((n + 63) / 64), dim3(64), 0, (hipStream_t)stream, q, n,
+                     n_actions, random_actions, use_random, actions);
+  XA_CHECK_LAUNCH("xa_dqn_act");
+  return 0;
+}
+
+extern "C" int xa_dqn_td_grad(const float* q, const float* q_next_target,
+                              const float* q_next_online, const int* actions,
+                              const float* rewards, const float* dones, int batch, int n_actions,
+                              float gamma, float* dq, float* loss, void* stream) {
+  XA_CHECK_ARG(q && q_next_target && actions && rewards && dones && dq && batch > 0 &&
+                   n_actions > 0,
+               "xa_dqn_td_grad: bad arguments");
+  hipLaunchKernelGGL(dqn_td_kernel, dim3((batch + 63) / 64), dim3(64), 0, (hipStream_t)stream, q,
+                     q_next_target, q_next_online, actions, rewards, dones, batch, n_actions,
+                     gamma, dq, loss);
+  XA_CHECK_LAUNCH("xa_dqn_td_grad");
+  return 0;
+}
+
+extern "C" int xa_ring_scatter(const void* src, void* ring, const int64_t* slots, int n_items,
+                               int64_t item_bytes, void* stream) {
+  XA_CHECK_ARG(src && ring && slots && n_items > 0 && item_bytes > 0,
+               "xa_ring_scatter: bad arguments");
+  const int gx = ring_grid_x(item_bytes);
+  hipLaunchKernelGGL(ring_scatter_kernel, dim3(gx, n_items), dim3(256), 0, (hipStream_t)stream,
+                     (const uint8_t*)src, (uint8_t*)ring, slots, n_items, item_bytes);
+  XA_CHECK_LAUNCH("xa_ring_scatter");
+  return 0;
+}
+
+extern "C" int xa_ring_gather(const void* ring, void* dst, const int64_t* slots, int n_items,
+                              int64_t item_bytes, void* stream) {
+  XA_CHECK_ARG(dst && ring && slots && n_items > 0 && item_bytes > 0,
+               "xa_ring_gather: bad arguments");
+  const int gx = ring_grid_x(item_bytes);
+  hipLaunchKernelGGL(ring_gather_kernel, dim3(gx, n_items), dim3(256), 0, (hipStream_t)stream,
+                     (const uint8_t*)ring, (uint8_t*)dst, slots, n_items, item_bytes);
+  XA_CHECK_LAUNCH("xa_ring_gather");
+  return 0;
+}
+
+extern "C" int xa_polyak(const float* src, float* dst, int64_t n, float tau, void* stream) {
+  XA_CHECK_ARG(src && dst && n > 0, "xa_polyak: bad arguments");
+  hipLaunchKernelGGL(polyak_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, src,
+                     dst, n, tau);
+  XA_CHECK_LAUNCH("xa_polyak");
+  return 0;
+}
+
+extern "C" int xa_adam_step_bump(int* adam_step, void* stream) {
+  XA_CHECK_ARG(adam_step != nullptr, "xa_adam_step_bump: null step");
+  hipLaunchKernelGGL(step_bump_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, adam_step);
+  XA_CHECK_LAUNCH("xa_adam_step_bump");
+  return 0;
+}
+
+extern "C" int xa_activation_grad(const float* y, const float* dy, int64_t n, int act,
+                                  float* dz, void* stream) {
+  XA_CHECK_ARG(y && dy && dz && n > 0, "xa_activation_grad: bad arguments");
+  hipLaunchKernelGGL(act_grad_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, y,
+                     dy, n, act, dz);
+  XA_CHECK_LAUNCH("xa_activation_grad");
+  return 0;
+}

@@ -1,0 +1,243 @@
+"""Device executor for .cfg-defined models (Conv1D / flatten / dense), the CNN and
+wide-MLP path of the off-policy agents and the CNN actor-critic
+(xagents/utils/common.py:169-290 builds the same graphs with Keras).
+
+Every layer runs as one `xa_gemm` (gemm.hip) with grouped-affine operand addressing:
+Conv1D on (B, H, W, C) input (conv along W, H folded into the batch)
+is an implicit-im2col GEMM, its weight gradient the same GEMM with the im2col moved to
+the reduction index, its input gradient a dY W^T GEMM followed by a fixed-order col2im
+gather (`xa_conv1d_input_grad`). Biases, ReLU / tanh and the ReLU gate of the backward
+pass are GEMM epilogues. Image inputs stay uint8 in HBM and are scaled f32(x) / 255 in
+the GEMM loader (xagents/base.py:505-506).
+
+Buffers are allocated per batch size and reused; all launches go to torch's current
+stream (graph-capturable).
+"""
+import torch
+
+from xagents_amd import _lib
+from xagents_amd._lib import XA_ACT_NONE, XA_ACT_RELU, XA_ACT_TANH, XaGemmArgs, call, stream
+
+_ACTS = {None: XA_ACT_NONE, 'linear': XA_ACT_NONE, 'relu': XA_ACT_RELU, 'tanh': XA_ACT_TANH}
+
+
+def act_code(name):
+    if name not in _ACTS:
+        raise NotImplementedError(f'activation {name!r} has no device epilogue')
+    return _ACTS[name]
+
+
+def gemm(M, N, K, a, b, c, *, a_u8=False, a_m=(1, 0, 0), a_k=(1, 1, 0), b_ks, b_ns,
+         ldc, bias=None, act=XA_ACT_NONE, gate=None, ld_gate=0, beta=False, workspace=None,
+         splits=None):
+    """C = [C +] act(A B + bias) * [gate > 0] with A(m, k) = a[f(m) + g(k)],
+    f / g given as (group, row stride, in-group stride) triples (gemm.hip)."""
+    lib = _lib.load()
+    s = splits if splits is not None else lib.xa_gemm_splits(M, N, K)
+    g = XaGemmArgs()
+    g.M, g.N, g.K = int(M), int(N), int(K)
+    ip = lambda v: None if v is None else int(v)  # noqa: E731  (numpy ints -> pointers)
+    a, b, c, bias, gate = ip(a), ip(b), ip(c), ip(bias), ip(gate)
+    g.a = a
+    g.a_u8 = int(a_u8)
+    g.a_pm, g.a_rm, g.a_sm = a_m
+    g.a_pk, g.a_rk, g.a_sk = a_k
+    g.b, g.b_ks, g.b_ns = b, b_ks, b_ns
+    g.c, g.ldc = c, ldc
+    g.splits = s
+    if s > 1:
+        need = s * M * N
+        if workspace is None or workspace.numel() < need:
+            raise _lib.HipLibraryError(f'xa_gemm: split workspace of {need} floats needed')
+        g.partials = workspace.data_ptr()
+    g.bias = bias
+    g.act = act
+    g.gate, g.ld_gate = gate, ld_gate
+    g.beta = int(beta)
+    call('xa_gemm', ctypes_ref(g), stream())
+
+
+def ctypes_ref(x):
+    import ctypes
+    return ctypes.byref(x)
+
+
+class LayerExecutor:
+    """Forward / backward of a DeviceModel's layer list at a fixed batch size."""
+
+    def __init__(self, model, batch):
+        self.model = model
+        self.B = batch
+        self.dev = model.theta.device
+        self.layers = model.layers
+        self.in_shape = tuple(model.input_shape)
+        self.offsets = []
+        off = 0
+        for l in self.layers:
+            if l.kind in ('dense', 'convolutional'):
+                wn = (l.in_features * l.units if l.kind == 'dense'
+                      else l.size * l.in_features * l.filters)
+                bn = l.units if l.kind == 'dense' else l.filters
+                self.offsets.append((off, off + wn))
+                off += wn + bn
+            else:
+                self.offsets.append(None)
+        assert off == model.n_params
+        f32 = dict(dtype=torch.float32, device=self.dev)
+        self.outs = [None if l.kind == 'flatten' else
+                     torch.empty(batch, *l.out_shape, **f32) for l in self.layers]
+        for i, l in enumerate(self.layers):
+            if l.kind == 'flatten':
+                self.outs[i] = self._src(i).reshape(batch, -1) if l.input_index != -1 else None
+        self.douts = [None if l.kind == 'flatten' else torch.empty_like(self.outs[i])
+                      for i, l in enumerate(self.layers)]
+        ws = 0
+        dcol = 0
+        lib = _lib.load()
+        for i, l in enumerate(self.layers):
+            for (M, N, K) in self._gemm_shapes(i):
+                s = lib.xa_gemm_splits(M, N, K)
+                ws = max(ws, s * M * N if s > 1 else 0)
+            if l.kind == 'convolutional' and l.input_index != -1:
+                rows, P, kC = self._conv_dims(i)[0], self._conv_dims(i)[2], l.size * l.in_features
+                dcol = max(dcol, rows * P * kC)
+        self.workspace = torch.empty(max(ws, 1), **f32)
+        self.dcol = torch.empty(max(dcol, 1), **f32)
+
+    # ---- shapes --------------------------------------------------------------
+    def _src_shape(self, i):
+        l = self.layers[i]
+        return self.in_shape if l.input_index == -1 else self.layers[l.input_index].out_shape
+
+    def _src(self, i):
+        j = self.layers[i].input_index
+        while j != -1 and self.layers[j].kind == 'flatten':
+            j = self.layers[j].input_index
+        return None if j == -1 else self.outs[j]
+
+    def _src_layer(self, i):
+        """Index of the layer whose buffer feeds layer i (flatten resolved), or -1."""
+        j = self.layers[i].input_index
+        while j != -1 and self.layers[j].kind == 'flatten':
+            j = self.layers[j].input_index
+        return j
+
+    def _conv_dims(self, i):
+        l = self.layers[i]
+        H, Win, C = self._src_shape(i)[-3:]
+        P = l.out_shape[-2]
+        return self.B * H, Win, P, C
+
+    def _gemm_shapes(self, i):
+        l = self.layers[i]
+        B = self.B
+        if l.kind == 'dense':
+            return [(B, l.units, l.in_features), (l.in_features, l.units, B), (1, l.units, B),
+                    (B, l.in_features, l.units)]
+        if l.kind == 'convolutional':
+            rows, Win, P, C = self._conv_dims(i)
+            kC = l.size * C
+            return [(rows * P, l.filters, kC), (kC, l.filters, rows * P),
+                    (1, l.filters, rows * P), (rows * P, kC, l.filters)]
+        return []
+
+    # ---- forward ---------------------------------------------------------------
+    def forward(self, x):
+        """x: [B, *input_shape] uint8 (images) or f32. Returns the output layers' tensors."""
+        assert x.shape[0] == self.B and x.is_contiguous()
+        theta = self.model.theta
+        tp = theta.data_ptr()
+        u8 = x.dtype == torch.uint8
+        self.x = x
+        for i, l in enumerate(self.layers):
+            if l.kind == 'flatten':
+                continue
+            j = self._src_layer(i)
+            src = x if j == -1 else self.outs[j]
+            src_u8 = u8 and j == -1
+            w0, b0 = self.offsets[i]
+            if l.kind == 'dense':
+                gemm(self.B, l.units, l.in_features, src.data_ptr(), tp + 4 * w0,
+                     self.outs[i].data_ptr(), a_u8=src_u8, a_m=(1, l.in_features, 0),
+                     b_ks=l.units, b_ns=1, ldc=l.units, bias=tp + 4 * b0,
+                     act=act_code(l.activation), workspace=self.workspace)
+            else:
+                rows, Win, P, C = self._conv_dims(i)
+                gemm(rows * P, l.filters, l.size * C, src.data_ptr(), tp + 4 * w0,
+                     self.outs[i].data_ptr(), a_u8=src_u8, a_m=(P, Win * C, l.stride * C),
+                     b_ks=l.filters, b_ns=1, ldc=l.filters, bias=tp + 4 * b0,
+                     act=act_code(l.activation), workspace=self.workspace)
+        return [self.outs[i] for i in self.model.outputs]
+
+    # ---- backward ----------------------------------------------------------------
+    def backward(self, d_outputs, grad):
+        """d_outputs: gradients w.r.t. the output layers (model.outputs order, [B, n]).
+        Writes the flat parameter gradient into `grad` (Keras variable order)."""
+        tp = self.model.theta.data_ptr()
+        gp = grad.data_ptr()
+        written = [False] * len(self.layers)
+        dz = {}
+        for i, d in zip(self.model.outputs, d_outputs):
+            l = self.layers[i]
+            a = act_code(l.activation)
+            if a == XA_ACT_NONE:
+                dz[i] = d.contiguous()
+            else:
+                out = self.douts[i]
+                call('xa_activation_grad', self.outs[i].data_ptr(), d.contiguous().data_ptr(),
+                     out.numel(), a, out.data_ptr(), stream())
+                dz[i] = out
+        u8 = self.x.dtype == torch.uint8
+        for i in range(len(self.layers) - 1, -1, -1):
+            l = self.layers[i]
+            if l.kind == 'flatten':
+                continue
+            if i not in dz:
+                if not written[i]:
+                    continue
+                # hidden layer: its ReLU gate was applied by the consumers (gate=out);
+                # a tanh hidden layer takes the derivative here
+                if act_code(l.activation) == XA_ACT_TANH:
+                    call('xa_activation_grad', self.outs[i].data_ptr(),
+                         self.douts[i].data_ptr(), self.douts[i].numel(), XA_ACT_TANH,
+                         self.douts[i].data_ptr(), stream())
+                dz[i] = self.douts[i]
+            d = dz[i]
+            j = self._src_layer(i)
+            src = self.x if j == -1 else self.outs[j]
+            src_u8 = u8 and j == -1
+            w0, b0 = self.offsets[i]
+            gate_j = None
+            if j != -1 and act_code(self.layers[j].activation) == XA_ACT_RELU:
+                gate_j = self.outs[j].data_ptr()
+            if l.kind == 'dense':
+                n_in, n_out = l.in_features, l.units
+                # dW = X^T dZ ; db = 1^T dZ
+                gemm(n_in, n_out, self.B, src.data_ptr(), d.data_ptr(), gp + 4 * w0,
+                     a_u8=src_u8, a_m=(1, 1, 0), a_k=(1, n_in, 0), b_ks=n_out, b_ns=1,
+                     ldc=n_out, workspace=self.workspace)
+                gemm(1, n_out, self.B, None, d.data_ptr(), gp + 4 * b0, a_m=(1, 0, 0),
+                     a_k=(1, 0, 0), b_ks=n_out, b_ns=1, ldc=n_out, workspace=self.workspace)
+                if j != -1:
+                    # dX = dZ W^T (gated by the source layer's ReLU), accumulated over heads
+                    gemm(self.B, n_in, n_out, d.data_ptr(), tp + 4 * w0,
+                         self.douts[j].data_ptr(), a_m=(1, n_out, 0), b_ks=1, b_ns=n_out,
+                         ldc=n_in, gate=gate_j, ld_gate=n_in if gate_j else 0,
+                         beta=written[j], workspace=self.workspace)
+                    written[j] = True
+            else:
+                rows, Win, P, C = self._conv_dims(i)
+                k, s, F = l.size, l.stride, l.filters
+                gemm(k * C, F, rows * P, src.data_ptr(), d.data_ptr(), gp + 4 * w0,
+                     a_u8=src_u8, a_m=(1, 1, 0), a_k=(P, Win * C, s * C), b_ks=F, b_ns=1,
+                     ldc=F, workspace=self.workspace)
+                gemm(1, F, rows * P, None, d.data_ptr(), gp + 4 * b0, a_m=(1, 0, 0),
+                     a_k=(1, 0, 0), b_ks=F, b_ns=1, ldc=F, workspace=self.workspace)
+                if j != -1:
+                    assert not written[j], 'a conv input with two consumers is not supported'
+                    gemm(rows * P, k * C, F, d.data_ptr(), tp + 4 * w0, self.dcol.data_ptr(),
+                         a_m=(1, F, 0), b_ks=1, b_ns=F, ldc=k * C, workspace=self.workspace)
+                    call('xa_conv1d_input_grad', self.dcol.data_ptr(), rows, P, k, s, C, Win,
+                         gate_j, self.douts[j].data_ptr(), stream())
+                    written[j] = True
+        return grad
