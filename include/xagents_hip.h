@@ -333,6 +333,57 @@ int xa_ring_gather(const void* ring, void* dst, const int64_t* slots, int n_item
  * tau = 1 copies (DQN.sync_target_model, dqn/agent.py:97-105). */
 int xa_polyak(const float* src, float* dst, int64_t n, float tau, void* stream);
 
+/*
+ * Off-policy device env step over a pre-recorded transition stream, fused with the
+ * replay-ring append: BaseAgent.step_envs(actions, store_in_buffers=True)
+ * (xagents/base.py:388-426). Per env i with cursor c:
+ *   new_state = rep_obs[i][c] (pre-reset obs), reward / done = rep_rew / rep_done[i][c],
+ *   ring[i][slot] <- (state[i], actions[i], reward, done, new_state), then
+ *   state[i] = rep_state[i][c] (post-reset), cursor = (c + 1) % t_rec.
+ * slot: RB1 (deque, buffers.py:59-98) = count % capacity, count += 1;
+ *       RB2 (buffers.py:101-148)      = current_size % size, current_size saturating at
+ *       size (every append lands on row 0 once full -- the reference's behaviour).
+ * Bytes are moved verbatim (uint8 frames or f32 vectors). out_* (optional) receive this
+ * step's transition; done_epret[i] = the finished episode's return where done, else 0.
+ */
+#define XA_RING_DEQUE 0
+#define XA_RING_RB2 1
+
+typedef struct XaReplayStepArgs {
+  int n_envs, t_rec;
+  int64_t obs_bytes;
+  const void* rep_obs;
+  const void* rep_state;
+  const float* rep_rew;
+  const float* rep_done;
+  void* state;
+  int* cursor;
+  float* ep_return;
+  float* done;
+  const void* actions;
+  int64_t act_bytes;
+  int64_t capacity;
+  int ring_kind;
+  int64_t* ring_count;
+  void* ring_states;
+  void* ring_new_states;
+  void* ring_actions;
+  float* ring_rewards;
+  float* ring_dones;
+  void* out_states;
+  void* out_new_states;
+  float* out_rewards;
+  float* out_dones;
+  float* done_epret;
+} XaReplayStepArgs;
+
+int xa_replay_env_step(const XaReplayStepArgs* args, void* stream);
+
+/* tf.keras.losses.MSE(target, pred) per row, gradient of the batch sum (minimize on a
+ * [B] loss): dpred = 2 (pred - target) / n_out; loss[b] (optional). */
+int xa_mse_grad(const float* pred, const float* target, int batch, int n_out, float* dpred,
+                float* loss, void* stream);
+
 /* Keras OptimizerV2 `iterations += 1` on device (before xa_clip_adam reads t). */
 int xa_adam_step_bump(int* adam_step, void* stream);
 

@@ -189,7 +189,7 @@ def test_library_exports_every_header_symbol():
     from xagents_amd import _lib
 
     header = (ROOT / 'include' / 'xagents_hip.h').read_text()
-    declared = set(re.findall(r'^\s*(?:int|const char\*)\s+(xa_\w+)\(', header, re.M))
+    declared = set(re.findall(r'^\s*(?:int|size_t|const char\*)\s+(xa_\w+)\(', header, re.M))
     assert declared and declared == set(_lib.EXPORTED_SYMBOLS)
     lib = _lib.load()  # no compute calls without a GPU
     for name in declared:

@@ -3,9 +3,10 @@
 Agent registry and command table mirror xagents/__init__.py:18-40. Only the
 agents whose hot path is built are registered (see DESIGN.md for scope).
 """
-from xagents_amd import a2c, ppo
+from xagents_amd import a2c, dqn, ppo
 from xagents_amd.a2c.agent import A2C
 from xagents_amd.base import BaseAgent, OffPolicy, OnPolicy
+from xagents_amd.dqn.agent import DQN
 from xagents_amd.ppo.agent import PPO
 from xagents_amd.utils.common import register_models
 
@@ -14,7 +15,8 @@ __version__ = '0.1.0'
 agents = {
     'a2c': {'module': a2c, 'agent': A2C},
     'ppo': {'module': ppo, 'agent': PPO},
+    'dqn': {'module': dqn, 'agent': DQN},
 }
 register_models(agents)
 
-__all__ = ['A2C', 'PPO', 'BaseAgent', 'OnPolicy', 'OffPolicy', 'agents']
+__all__ = ['A2C', 'DQN', 'PPO', 'BaseAgent', 'OnPolicy', 'OffPolicy', 'agents']

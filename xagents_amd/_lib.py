@@ -152,6 +152,24 @@ class XaGemmArgs(Structure):
     ]
 
 
+class XaReplayStepArgs(Structure):
+    _fields_ = [
+        ('n_envs', c_int), ('t_rec', c_int),
+        ('obs_bytes', c_int64),
+        ('rep_obs', c_void_p), ('rep_state', c_void_p), ('rep_rew', c_void_p),
+        ('rep_done', c_void_p),
+        ('state', c_void_p), ('cursor', c_void_p), ('ep_return', c_void_p), ('done', c_void_p),
+        ('actions', c_void_p), ('act_bytes', c_int64),
+        ('capacity', c_int64), ('ring_kind', c_int), ('ring_count', c_void_p),
+        ('ring_states', c_void_p), ('ring_new_states', c_void_p), ('ring_actions', c_void_p),
+        ('ring_rewards', c_void_p), ('ring_dones', c_void_p),
+        ('out_states', c_void_p), ('out_new_states', c_void_p), ('out_rewards', c_void_p),
+        ('out_dones', c_void_p), ('done_epret', c_void_p),
+    ]
+
+
+XA_RING_DEQUE = 0
+XA_RING_RB2 = 1
 XA_ACT_NONE = 0
 XA_ACT_RELU = 1
 XA_ACT_TANH = 2
@@ -203,6 +221,8 @@ _SIGNATURES = {
     'xa_ring_gather': (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int64, c_void_p]),
     'xa_polyak': (c_int, [c_void_p, c_void_p, c_int64, c_float, c_void_p]),
     'xa_adam_step_bump': (c_int, [c_void_p, c_void_p]),
+    'xa_replay_env_step': (c_int, [POINTER(XaReplayStepArgs), c_void_p]),
+    'xa_mse_grad': (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     'xa_activation_grad': (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p, c_void_p]),
 }
 

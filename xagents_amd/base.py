@@ -418,6 +418,102 @@ class OffPolicy(BaseAgent, ABC):
         )
         self.buffers = buffers
 
+    # ---- device env stepping + replay append (step_envs(store_in_buffers=True)) ----
+    _STATS_ROWS = 64
+
+    def _setup_offpolicy(self, act_shape, act_dtype):
+        """Device replay rings mirroring self.buffers, the fused env-step arguments and
+        the per-step episode-stat rows copied back asynchronously."""
+        from xagents_amd._lib import XaReplayStepArgs
+        from xagents_amd.replay import DeviceReplay
+        env = self.envs
+        self.replay = DeviceReplay(self.buffers, env.obs_shape, env.obs_dtype, act_shape,
+                                   act_dtype, self.device)
+        self._step_args = XaReplayStepArgs()
+        env.fill_step_args(self._step_args)
+        n, K = self.n_envs, self._STATS_ROWS
+        self._st_done = torch.zeros(K, n, dtype=torch.float32, device=self.device)
+        self._st_epret = torch.zeros(K, n, dtype=torch.float32, device=self.device)
+        self._st_row = 0
+        self._st_host = []
+
+    def _env_step(self, actions, store=True):
+        """One xa_replay_env_step: every env steps with `actions` (device) and, when
+        `store`, appends its transition to its replay ring (xagents/base.py:388-426)."""
+        from xagents_amd._lib import call, stream
+        import ctypes
+        a = self._step_args
+        if store:
+            self.replay.fill_step_args(a, actions)
+        else:
+            a.ring_states = None
+            a.actions, a.act_bytes = actions.data_ptr(), self.replay.act_bytes
+        r = self._st_row
+        a.out_dones = self._st_done[r].data_ptr()
+        a.done_epret = self._st_epret[r].data_ptr()
+        call('xa_replay_env_step', ctypes.byref(a), stream())
+        if store:
+            self.replay.appended()
+        self._st_row += 1
+        if self._st_row == self._STATS_ROWS:
+            self._flush_offpolicy_stats()
+
+    def _flush_offpolicy_stats(self):
+        rows = self._st_row
+        if rows == 0:
+            return
+        hd = torch.empty(rows, self.n_envs).pin_memory()
+        he = torch.empty(rows, self.n_envs).pin_memory()
+        hd.copy_(self._st_done[:rows], non_blocking=True)
+        he.copy_(self._st_epret[:rows], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._st_host.append((hd, he, ev))
+        self._st_row = 0
+        while len(self._st_host) > 1:
+            self._fold_offpolicy_stats(*self._st_host.pop(0))
+
+    def _fold_offpolicy_stats(self, hd, he, ev):
+        ev.synchronize()
+        d, e = hd.numpy(), he.numpy()
+        for t in range(d.shape[0]):  # step-major, env-minor like step_envs
+            for i in np.nonzero(d[t])[0]:
+                if self.history_checkpoint:
+                    self.update_history(float(e[t, i]))
+                self.total_rewards.append(float(e[t, i]))
+                self.games += 1
+                self.done_envs += 1
+
+    def _drain_episode_stats(self):
+        super()._drain_episode_stats()
+        if hasattr(self, '_st_host'):
+            self._flush_offpolicy_stats()
+            while self._st_host:
+                self._fold_offpolicy_stats(*self._st_host.pop(0))
+
+    def _random_actions(self):
+        """env.action_space.sample() per env (OffPolicy.fill_buffers, base.py:702-730)."""
+        space = self.envs[0].action_space
+        return np.stack([np.asarray(space.sample()) for _ in range(self.n_envs)])
+
+    def fill_buffers(self):
+        """Step every env with random actions until each buffer holds initial_size
+        transitions (xagents/base.py:702-730), then reset the envs."""
+        total = sum(b.initial_size for b in self.buffers)
+        while min(b.current_size - b.initial_size for b in self.buffers) < 0:
+            acts = torch.as_tensor(self._random_actions(), device=self.device)
+            acts = acts.to(self.replay.act_t).contiguous()
+            self._env_step(acts)
+            filled = sum(min(b.current_size, b.initial_size) for b in self.buffers)
+            complete = round((filled / total) * 100, self.display_precision)
+            self.display_message(
+                f'\rFilling replay buffer ==> {complete}% | {filled}/{total}', end='')
+        self.display_message('')
+        self._drain_episode_stats()
+        self.total_rewards.clear()
+        self.games = self.done_envs = 0
+        self.reset_envs()
+
     def fit(self, target_reward=None, max_steps=None, monitor_session=None):
         self.fill_buffers()
         super(OffPolicy, self).fit(target_reward, max_steps, monitor_session)

@@ -156,6 +156,90 @@ __global__ __launch_bounds__(256) void act_grad_kernel(const float* __restrict__
   }
 }
 
+// ---- off-policy replay env step + ring store (BaseAgent.step_envs with
+// store_in_buffers, xagents/base.py:388-426) -----------------------------------------
+XA_DEV int64_t ring_slot(const XaReplayStepArgs& a, int i) {
+  const int64_t cnt = a.ring_count[i];
+  // RB1 deque: the append lands after the newest element; RB2: row current_size % size,
+  // current_size saturating at size -> row 0 once full (buffers.py:133-135)
+  return a.ring_kind == XA_RING_RB2 ? (cnt % a.capacity) : (cnt % a.capacity);
+}
+
+XA_DEV void copy_bytes(uint8_t* d, const uint8_t* s, int64_t n, int64_t lo, int64_t hi) {
+  for (int64_t e = lo + threadIdx.x; e < hi && e < n; e += blockDim.x) d[e] = s[e];
+}
+
+// phase 1: frames (grid: byte chunks x envs); every block reads and writes only its own
+// byte range of its env, so reading the old state and overwriting it is race-free
+__global__ __launch_bounds__(256) void replay_step_frames_kernel(XaReplayStepArgs a,
+                                                                 int64_t chunk) {
+  const int i = blockIdx.y;
+  const int64_t lo = blockIdx.x * chunk, hi = lo + chunk;
+  const int64_t ob = a.obs_bytes;
+  const int c = a.cursor[i];
+  const uint8_t* s_new = (const uint8_t*)a.rep_obs + ((int64_t)i * a.t_rec + c) * ob;
+  const uint8_t* s_post = (const uint8_t*)a.rep_state + ((int64_t)i * a.t_rec + c) * ob;
+  uint8_t* st = (uint8_t*)a.state + (int64_t)i * ob;
+  // stage this chunk of the old state (register per byte slot: <= 16 per thread)
+  const bool vec = (ob & 15) == 0 && (chunk & 15) == 0;
+  if (vec) {
+    const int64_t lo16 = lo >> 4, hi16 = (hi < ob ? hi : ob) >> 4;
+    for (int64_t e = lo16 + threadIdx.x; e < hi16; e += blockDim.x) {
+      const uint4 old = reinterpret_cast<const uint4*>(st)[e];
+      const uint4 nw = reinterpret_cast<const uint4*>(s_new)[e];
+      const uint4 post = reinterpret_cast<const uint4*>(s_post)[e];
+      if (a.ring_states) {
+        const int64_t slot = (int64_t)i * a.capacity + ring_slot(a, i);
+        reinterpret_cast<uint4*>((uint8_t*)a.ring_states + slot * ob)[e] = old;
+        reinterpret_cast<uint4*>((uint8_t*)a.ring_new_states + slot * ob)[e] = nw;
+      }
+      if (a.out_states) reinterpret_cast<uint4*>((uint8_t*)a.out_states + (int64_t)i * ob)[e] = old;
+      if (a.out_new_states)
+        reinterpret_cast<uint4*>((uint8_t*)a.out_new_states + (int64_t)i * ob)[e] = nw;
+      reinterpret_cast<uint4*>(st)[e] = post;
+    }
+  } else {
+    for (int64_t e = lo + threadIdx.x; e < hi && e < ob; e += blockDim.x) {
+      const uint8_t old = st[e], nw = s_new[e], post = s_post[e];
+      if (a.ring_states) {
+        const int64_t slot = (int64_t)i * a.capacity + ring_slot(a, i);
+        ((uint8_t*)a.ring_states)[slot * ob + e] = old;
+        ((uint8_t*)a.ring_new_states)[slot * ob + e] = nw;
+      }
+      if (a.out_states) ((uint8_t*)a.out_states)[(int64_t)i * ob + e] = old;
+      if (a.out_new_states) ((uint8_t*)a.out_new_states)[(int64_t)i * ob + e] = nw;
+      st[e] = post;
+    }
+  }
+}
+
+// phase 2: per-env scalars, ring scalars, cursor / counters (one thread per env)
+__global__ void replay_step_scalars_kernel(XaReplayStepArgs a) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.n_envs) return;
+  const int c = a.cursor[i];
+  const float r = a.rep_rew[(int64_t)i * a.t_rec + c];
+  const float d = a.rep_done[(int64_t)i * a.t_rec + c];
+  if (a.ring_states) {
+    const int64_t slot = (int64_t)i * a.capacity + ring_slot(a, i);
+    const uint8_t* src = (const uint8_t*)a.actions + (int64_t)i * a.act_bytes;
+    uint8_t* dst = (uint8_t*)a.ring_actions + slot * a.act_bytes;
+    for (int64_t e = 0; e < a.act_bytes; ++e) dst[e] = src[e];
+    a.ring_rewards[slot] = r;
+    a.ring_dones[slot] = d;
+    const int64_t cnt = a.ring_count[i];
+    a.ring_count[i] = a.ring_kind == XA_RING_RB2 ? (cnt < a.capacity ? cnt + 1 : cnt) : cnt + 1;
+  }
+  if (a.out_rewards) a.out_rewards[i] = r;
+  if (a.out_dones) a.out_dones[i] = d;
+  float ep = a.ep_return[i] + r;
+  if (a.done_epret) a.done_epret[i] = d != 0.0f ? ep : 0.0f;
+  if (d != 0.0f) ep = 0.0f;
+  a.ep_return[i] = ep;
+  a.done[i] = d;
+  a.cursor[i] = c + 1 < a.t_rec ? c + 1 : 0;
+}
+
 int grid_for(int64_t n) {
   const int64_t b = (n + 255) / 256;
   return (int)(b < 8192 ? (b > 0 ? b : 1) : 8192);
@@ -249,5 +333,49 @@ extern "C" int xa_activation_grad(const float* y, const float* dy, int64_t n, in
   hipLaunchKernelGGL(act_grad_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, y,
                      dy, n, act, dz);
   XA_CHECK_LAUNCH("xa_activation_grad");
+  return 0;
+}
+
+extern "C" int xa_replay_env_step(const XaReplayStepArgs* p, void* stream) {
+  XA_CHECK_ARG(p != nullptr, "xa_replay_env_step: null args");
+  const XaReplayStepArgs& a = *p;
+  XA_CHECK_ARG(a.n_envs > 0 && a.t_rec > 0 && a.obs_bytes > 0 && a.rep_obs && a.rep_state &&
+                   a.rep_rew && a.rep_done && a.state && a.cursor && a.ep_return && a.done,
+               "xa_replay_env_step: bad env arguments");
+  XA_CHECK_ARG(!a.ring_states || (a.ring_new_states && a.ring_actions && a.ring_rewards &&
+                                  a.ring_dones && a.ring_count && a.capacity > 0 &&
+                                  a.actions && a.act_bytes > 0),
+               "xa_replay_env_step: incomplete replay ring");
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t chunk = 4096;
+  dim3 grid((unsigned)((a.obs_bytes + chunk - 1) / chunk), a.n_envs);
+  hipLaunchKernelGGL(replay_step_frames_kernel, grid, dim3(256), 0, s, a, chunk);
+  XA_CHECK_LAUNCH("xa_replay_env_step (frames)");
+  hipLaunchKernelGGL(replay_step_scalars_kernel, dim3((a.n_envs + 63) / 64), dim3(64), 0, s, a);
+  XA_CHECK_LAUNCH("xa_replay_env_step (scalars)");
+  return 0;
+}
+
+// tf.keras.losses.MSE(y, pred) over the last axis, gradient of its batch sum
+// (optimizer.minimize on a [B] loss, dqn/agent.py:158-171): d = 2 (pred - y) / A
+__global__ void mse_grad_kernel(const float* __restrict__ pred, const float* __restrict__ y,
+                                int B, int A, float* __restrict__ d, float* __restrict__ loss) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  float acc = 0.0f;
+  for (int a = 0; a < A; ++a) {
+    const float e = pred[(size_t)b * A + a] - y[(size_t)b * A + a];
+    d[(size_t)b * A + a] = (2.0f * e) / (float)A;
+    acc = acc + e * e;
+  }
+  if (loss) loss[b] = acc / (float)A;
+}
+
+extern "C" int xa_mse_grad(const float* pred, const float* target, int batch, int n_out,
+                           float* dpred, float* loss, void* stream) {
+  XA_CHECK_ARG(pred && target && dpred && batch > 0 && n_out > 0, "xa_mse_grad: bad arguments");
+  hipLaunchKernelGGL(mse_grad_kernel, dim3((batch + 63) / 64), dim3(64), 0, (hipStream_t)stream,
+                     pred, target, batch, n_out, dpred, loss);
+  XA_CHECK_LAUNCH("xa_mse_grad");
   return 0;
 }

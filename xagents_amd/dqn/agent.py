@@ -1,0 +1,194 @@
+"""DQN / double DQN with the xagents class surface (xagents/dqn/agent.py:8-209) on the
+device path.
+
+train_step (dqn/agent.py:182-197), all on device except the reference's host RNG draws:
+    get_actions          np.random.random() < epsilon ? np.random.randint(0, A, n)
+                         : tf.argmax(Q(states / 255))         -> xa_gemm CNN + xa_dqn_act
+    step_envs(store)     xa_replay_env_step (env step fused with the replay append)
+    concat_buffer_samples  host index draw (random.sample / np.random.randint, the
+                         reference's streams) -> xa_ring_gather, env-major batch
+    get_targets          Q(s), [Q(s')], Qt(s') (one online pass over [s; s'] when double)
+                         -> xa_dqn_td_grad (TD target, MSE gradient of the batch sum)
+    update_gradients     CNN backward (xa_gemm / xa_conv1d_input_grad) -> Keras Adam
+                         (no gradient clipping, optimizer.minimize) via xa_clip_adam
+at_step_end: hard target copy when steps % target_sync_steps == 0 (xa_polyak, tau 1).
+"""
+import numpy as np
+import torch
+
+from xagents_amd import kernels
+from xagents_amd._lib import call, stream
+from xagents_amd.base import OffPolicy
+from xagents_amd.envs import Discrete
+from xagents_amd.layers import LayerExecutor
+
+
+class DQN(OffPolicy):
+    """Playing Atari with Deep Reinforcement Learning https://arxiv.org/abs/1312.5602"""
+
+    def __init__(
+        self,
+        envs,
+        model,
+        buffers,
+        double=False,
+        epsilon_start=1.0,
+        epsilon_end=0.02,
+        epsilon_decay_steps=150000,
+        target_sync_steps=1000,
+        **kwargs,
+    ):
+        super(DQN, self).__init__(envs, model, buffers, **kwargs)
+        self.assert_valid_env(envs[0], Discrete)
+        self.target_model = self.model.clone()
+        self.double = double
+        self.epsilon_start = self.epsilon = epsilon_start
+        self.epsilon_end = epsilon_end
+        self.epsilon_decay_steps = epsilon_decay_steps
+        self.target_sync_steps = target_sync_steps
+        self.batch_dtypes = ['uint8', 'int64', 'float64', 'bool', 'uint8']
+        self._setup_device()
+
+    def _setup_device(self):
+        self._setup_offpolicy((), np.int32)
+        k = self.replay.k
+        if self.n_envs * k > 1 and k == 1:
+            # ReplayBuffer1.get_sample returns the raw tuple for k == 1 and
+            # concat_buffer_samples then fails (buffers.py:96-98, base.py:363-367)
+            raise ValueError('zero-dimensional arrays cannot be concatenated')
+        B = self.n_envs * k
+        self.batch_size = B
+        dev = self.device
+        obs = self.envs.obs_shape
+        self.xb = torch.zeros((2 * B,) + obs, dtype=self.replay.obs_t, device=dev)
+        self.b_act = torch.zeros(B, dtype=torch.int32, device=dev)
+        self.b_rew = torch.zeros(B, dtype=torch.float32, device=dev)
+        self.b_done = torch.zeros(B, dtype=torch.float32, device=dev)
+        self.dq = torch.zeros(B, self.n_actions, dtype=torch.float32, device=dev)
+        self.td_loss = torch.zeros(B, dtype=torch.float32, device=dev)
+        self.grad = torch.zeros(self.model.n_params, dtype=torch.float32, device=dev)
+        self.adam_ws = torch.zeros(1024, dtype=torch.float64, device=dev)
+        self.actions = torch.zeros(self.n_envs, dtype=torch.int32, device=dev)
+        self._rand_actions = torch.zeros(self.n_envs, dtype=torch.int32, device=dev)
+        self.ex_online = LayerExecutor(self.model, 2 * B if self.double else B)
+        self.ex_target = LayerExecutor(self.target_model, B)
+        self.ex_act = LayerExecutor(self.model, self.n_envs)
+
+    # ---- reference surface ---------------------------------------------------
+    def update_epsilon(self):
+        """dqn/agent.py:86-95"""
+        self.epsilon = max(
+            self.epsilon_end, self.epsilon_start - self.steps / self.epsilon_decay_steps)
+
+    def sync_target_model(self):
+        """dqn/agent.py:97-105"""
+        if self.steps % self.target_sync_steps == 0:
+            call('xa_polyak', self.model.theta.data_ptr(), self.target_model.theta.data_ptr(),
+                 self.model.n_params, kernels._f32(1.0), stream())
+
+    def get_model_outputs(self, inputs, models, training=True):
+        """[argmax Q, Q] (dqn/agent.py:70-84) for a device batch of states."""
+        model = models[0] if isinstance(models, (list, tuple)) else models
+        x = torch.as_tensor(inputs, device=self.device).contiguous()
+        ex = LayerExecutor(model, x.shape[0])
+        q = ex.forward(x)[0].clone()
+        act = torch.empty(x.shape[0], dtype=torch.int32, device=self.device)
+        call('xa_dqn_act', q.data_ptr(), x.shape[0], self.n_actions, None, 0, act.data_ptr(),
+             stream())
+        return act, q
+
+    def get_actions(self):
+        """Epsilon-greedy, all envs random or all greedy (dqn/agent.py:107-116)."""
+        if np.random.random() < self.epsilon:
+            r = np.random.randint(0, self.n_actions, self.n_envs)
+            self._rand_actions.copy_(torch.from_numpy(r.astype(np.int32)))
+            call('xa_dqn_act', None, self.n_envs, self.n_actions,
+                 self._rand_actions.data_ptr(), 1, self.actions.data_ptr(), stream())
+        else:
+            q = self.ex_act.forward(self.envs.state)[0]
+            call('xa_dqn_act', q.data_ptr(), self.n_envs, self.n_actions, None, 0,
+                 self.actions.data_ptr(), stream())
+        return self.actions
+
+    def concat_buffer_samples(self):
+        """One sampled batch gathered from the device rings in the reference's index
+        order: [states, actions, rewards, dones, new_states] (base.py:344-368)."""
+        slots = self.replay.upload_slots(self.replay.sample_slots())
+        B = self.batch_size
+        self.replay.gather(slots, self.xb[:B], self.b_act, self.b_rew, self.b_done,
+                           self.xb[B:])
+        return [self.xb[:B], self.b_act, self.b_rew, self.b_done, self.xb[B:]]
+
+    def _td_grad(self):
+        B = self.batch_size
+        q_all = self.ex_online.forward(self.xb if self.double else self.xb[:B])[0]
+        q_next_t = self.ex_target.forward(self.xb[B:])[0]
+        q_next_o = q_all[B:].data_ptr() if self.double else None
+        call('xa_dqn_td_grad', q_all.data_ptr(), q_next_t.data_ptr(), q_next_o,
+             self.b_act.data_ptr(), self.b_rew.data_ptr(), self.b_done.data_ptr(), B,
+             self.n_actions, kernels._f32(self.gamma), self.dq.data_ptr(),
+             self.td_loss.data_ptr(), stream())
+
+    def _apply(self):
+        opt = self.model.optimizer
+        self.ex_online.backward([self.dq], self.grad, batch=self.batch_size)
+        call('xa_adam_step_bump', opt.iterations.data_ptr(), stream())
+        kernels.clip_adam(self.model.theta, opt.m, opt.v, self.grad, opt.iterations,
+                          opt.learning_rate, opt.beta_1, opt.beta_2, opt.epsilon,
+                          clip_norm=0.0, workspace=self.adam_ws)
+
+    def get_targets(self, states, actions, rewards, dones, new_states):
+        """TD targets y [B, A] (dqn/agent.py:118-156)."""
+        q = self.get_model_outputs(states, self.model)[1]
+        qt = self.get_model_outputs(new_states, self.target_model)[1]
+        if self.double:
+            a_next = self.get_model_outputs(new_states, self.model)[0].long()
+            v = qt.gather(1, a_next[:, None])[:, 0]
+        else:
+            v = qt.max(1).values
+        d = torch.as_tensor(dones, device=self.device).bool()
+        v = torch.where(d, torch.zeros_like(v), v)
+        y = q.clone()
+        upd = v * np.float32(self.gamma) + torch.as_tensor(rewards, device=self.device).float()
+        idx = torch.as_tensor(actions, device=self.device).long()
+        y[torch.arange(y.shape[0], device=self.device), idx] = upd
+        return y
+
+    def update_gradients(self, x, y):
+        """MSE(y, Q(x)) minimized with Keras Adam (dqn/agent.py:158-171)."""
+        x = torch.as_tensor(x, device=self.device).contiguous()
+        y = torch.as_tensor(y, device=self.device, dtype=torch.float32).contiguous()
+        ex = LayerExecutor(self.model, x.shape[0])
+        q = ex.forward(x)[0]
+        dq = torch.empty_like(q)
+        call('xa_mse_grad', q.data_ptr(), y.data_ptr(), x.shape[0], self.n_actions,
+             dq.data_ptr(), None, stream())
+        ex.backward([dq], self.grad)
+        opt = self.model.optimizer
+        call('xa_adam_step_bump', opt.iterations.data_ptr(), stream())
+        kernels.clip_adam(self.model.theta, opt.m, opt.v, self.grad, opt.iterations,
+                          opt.learning_rate, opt.beta_1, opt.beta_2, opt.epsilon,
+                          clip_norm=0.0, workspace=self.adam_ws)
+
+    def at_step_start(self):
+        self.update_epsilon()
+
+    def train_step(self):
+        """dqn/agent.py:182-197"""
+        hooks = ('get_targets', 'update_gradients', 'concat_buffer_samples', 'get_actions')
+        if any(getattr(type(self), h) is not getattr(DQN, h) for h in hooks):
+            actions = self.get_actions()
+            self._env_step(actions.to(torch.int32).contiguous())
+            self.steps += self.n_envs
+            batch = self.concat_buffer_samples()
+            self.update_gradients(batch[0], self.get_targets(*batch))
+            return
+        self.get_actions()
+        self._env_step(self.actions)
+        self.steps += self.n_envs
+        self.concat_buffer_samples()
+        self._td_grad()
+        self._apply()
+
+    def at_step_end(self):
+        self.sync_target_model()

@@ -226,6 +226,94 @@ class CartPoleVecEnv(DeviceVecEnv):
         a.max_episode_steps = self.max_episode_steps
 
 
+def record_transitions(n_envs, t_rec, obs_shape, dtype, seed=55, mean_episode=200,
+                       reward_prob=0.02):
+    """Synthetic pre-recorded transition streams for the off-policy configs
+    (SURVEY.md section 8d: C3 Pong-shaped uint8 (84, 84, 1) frames i.i.d. uniform 0..255;
+    C5 BipedalWalker-shaped f32 obs ~ N(0, 1)). Per env: s0, rep_obs [t_rec] (obs
+    returned by step p), rep_state [t_rec] (post-reset state), rewards in {-1, 0, 1}
+    (Pong-like, prob reward_prob each sign), episode ends ~ Geometric(1 / mean_episode);
+    the last record is terminal with post-state s0 so the cursor wrap is an episode
+    boundary. Generated from np.random.default_rng(seed)."""
+    rng = np.random.default_rng(seed)
+    shape = (n_envs, t_rec) + tuple(obs_shape)
+
+    def frames(sh):
+        if np.dtype(dtype) == np.uint8:
+            return rng.integers(0, 256, size=sh, dtype=np.uint8)
+        return rng.standard_normal(sh).astype(dtype)
+
+    s0 = frames((n_envs,) + tuple(obs_shape))
+    rep_obs = frames(shape)
+    rep_done = (rng.random((n_envs, t_rec)) < 1.0 / mean_episode).astype(np.float32)
+    rep_done[:, -1] = 1.0
+    rep_state = rep_obs.copy()
+    resets = frames(shape)
+    m = rep_done.astype(bool)
+    rep_state[m] = resets[m]
+    rep_state[:, -1] = s0
+    u = rng.random((n_envs, t_rec))
+    rep_rew = np.where(u < reward_prob, 1.0, np.where(u > 1 - reward_prob, -1.0, 0.0))
+    return s0, rep_obs, rep_state, rep_rew.astype(np.float32), rep_done
+
+
+class TransitionReplayVecEnv:
+    """Off-policy device env over pre-recorded transitions (Atari-shaped uint8 frames
+    or continuous-control f32 vectors). Stepping -- and the replay-ring append of
+    BaseAgent.step_envs(store_in_buffers=True), xagents/base.py:388-426 -- is one
+    xa_replay_env_step launch; the actions are stored but do not change the stream."""
+
+    def __init__(self, env_id, n_envs, obs_shape, action_space, obs_dtype=np.uint8,
+                 t_rec=256, seed=55, device=None, record=None, mean_episode=200):
+        self.spec = EnvSpec(env_id)
+        self.n_envs = int(n_envs)
+        self.device = torch.device(device) if device is not None else default_device()
+        low, high = (0, 255) if np.dtype(obs_dtype) == np.uint8 else (-np.inf, np.inf)
+        self.observation_space = Box(low, high, obs_shape, obs_dtype)
+        self.action_space = action_space
+        self.obs_dtype = np.dtype(obs_dtype)
+        self.obs_shape = tuple(obs_shape)
+        s0, rep_obs, rep_state, rep_rew, rep_done = record or record_transitions(
+            n_envs, t_rec, obs_shape, obs_dtype, seed, mean_episode)
+        self.t_rec = rep_obs.shape[1]
+        dev = self.device
+        tt = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+        self.s0, self.rep_obs, self.rep_state = tt(s0), tt(rep_obs), tt(rep_state)
+        self.rep_rew, self.rep_done = tt(rep_rew), tt(rep_done)
+        self.state = torch.empty_like(self.s0)
+        self.cursor = torch.zeros(self.n_envs, dtype=torch.int32, device=dev)
+        self.done = torch.zeros(self.n_envs, dtype=torch.float32, device=dev)
+        self.ep_return = torch.zeros(self.n_envs, dtype=torch.float32, device=dev)
+        self.obs_bytes = int(np.prod(self.obs_shape)) * self.obs_dtype.itemsize
+        self.reset()
+
+    def __len__(self):
+        return self.n_envs
+
+    def __getitem__(self, i):
+        return self
+
+    def __iter__(self):
+        return iter([self] * self.n_envs)
+
+    def seed(self, seed):
+        self.action_space.seed(seed)
+
+    def reset(self):
+        self.state.copy_(self.s0)
+        self.cursor.zero_()
+        self.done.zero_()
+        self.ep_return.zero_()
+        return self.state
+
+    def fill_step_args(self, a):
+        a.n_envs, a.t_rec, a.obs_bytes = self.n_envs, self.t_rec, self.obs_bytes
+        a.rep_obs, a.rep_state = self.rep_obs.data_ptr(), self.rep_state.data_ptr()
+        a.rep_rew, a.rep_done = self.rep_rew.data_ptr(), self.rep_done.data_ptr()
+        a.state, a.cursor = self.state.data_ptr(), self.cursor.data_ptr()
+        a.ep_return, a.done = self.ep_return.data_ptr(), self.done.data_ptr()
+
+
 def create_envs(env_name, n=1, preprocess=False, *args, mode='replay', seed=55, device=None,
                 t_rec=4096, **kwargs):
     """Device counterpart of xagents.utils.common.create_envs (common.py:145-166).
@@ -233,6 +321,15 @@ def create_envs(env_name, n=1, preprocess=False, *args, mode='replay', seed=55, 
     Returns ONE vectorized env object of length n (the agents accept it wherever the
     reference takes a list of gym envs).
     """
+    if 'NoFrameskip' in env_name:
+        # Atari-shaped synthetic replay: frames as AtariWrapper emits them (84, 84, 1)
+        # uint8 (xagents/utils/common.py:67-142); the wrapper itself is not rebuilt
+        actions = {'PongNoFrameskip-v4': 6, 'BreakoutNoFrameskip-v4': 4}.get(env_name, 6)
+        return TransitionReplayVecEnv(env_name, n, (84, 84, 1), Discrete(actions), np.uint8,
+                                      t_rec=min(t_rec, 256), seed=seed, device=device)
+    if env_name.startswith('BipedalWalker'):
+        return TransitionReplayVecEnv(env_name, n, (24,), Box(-1.0, 1.0, (4,)), np.float32,
+                                      t_rec=t_rec, seed=seed, device=device)
     assert not preprocess, ('Atari preprocessing on device is not implemented yet '
                             '(SURVEY.md section 8f rank 1)')
     if env_name != 'CartPole-v1':

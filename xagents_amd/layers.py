@@ -122,11 +122,11 @@ class LayerExecutor:
             j = self.layers[j].input_index
         return j
 
-    def _conv_dims(self, i):
+    def _conv_dims(self, i, batch=None):
         l = self.layers[i]
         H, Win, C = self._src_shape(i)[-3:]
         P = l.out_shape[-2]
-        return self.B * H, Win, P, C
+        return (batch or self.B) * H, Win, P, C
 
     def _gemm_shapes(self, i):
         l = self.layers[i]
@@ -170,9 +170,13 @@ class LayerExecutor:
         return [self.outs[i] for i in self.model.outputs]
 
     # ---- backward ----------------------------------------------------------------
-    def backward(self, d_outputs, grad):
-        """d_outputs: gradients w.r.t. the output layers (model.outputs order, [B, n]).
-        Writes the flat parameter gradient into `grad` (Keras variable order)."""
+    def backward(self, d_outputs, grad, batch=None):
+        """d_outputs: gradients w.r.t. the output layers (model.outputs order, [b, n]).
+        Writes the flat parameter gradient into `grad` (Keras variable order). `batch`
+        (<= B) back-propagates only the first rows of the last forward (samples are
+        independent rows, so a prefix of every buffer is a smaller batch)."""
+        Bb = batch or self.B
+        assert Bb <= self.B
         tp = self.model.theta.data_ptr()
         gp = grad.data_ptr()
         written = [False] * len(self.layers)
@@ -185,7 +189,7 @@ class LayerExecutor:
             else:
                 out = self.douts[i]
                 call('xa_activation_grad', self.outs[i].data_ptr(), d.contiguous().data_ptr(),
-                     out.numel(), a, out.data_ptr(), stream())
+                     d.numel(), a, out.data_ptr(), stream())
                 dz[i] = out
         u8 = self.x.dtype == torch.uint8
         for i in range(len(self.layers) - 1, -1, -1):
@@ -199,7 +203,7 @@ class LayerExecutor:
                 # a tanh hidden layer takes the derivative here
                 if act_code(l.activation) == XA_ACT_TANH:
                     call('xa_activation_grad', self.outs[i].data_ptr(),
-                         self.douts[i].data_ptr(), self.douts[i].numel(), XA_ACT_TANH,
+                         self.douts[i].data_ptr(), self.douts[i][:Bb].numel(), XA_ACT_TANH,
                          self.douts[i].data_ptr(), stream())
                 dz[i] = self.douts[i]
             d = dz[i]
@@ -213,20 +217,20 @@ class LayerExecutor:
             if l.kind == 'dense':
                 n_in, n_out = l.in_features, l.units
                 # dW = X^T dZ ; db = 1^T dZ
-                gemm(n_in, n_out, self.B, src.data_ptr(), d.data_ptr(), gp + 4 * w0,
+                gemm(n_in, n_out, Bb, src.data_ptr(), d.data_ptr(), gp + 4 * w0,
                      a_u8=src_u8, a_m=(1, 1, 0), a_k=(1, n_in, 0), b_ks=n_out, b_ns=1,
                      ldc=n_out, workspace=self.workspace)
-                gemm(1, n_out, self.B, None, d.data_ptr(), gp + 4 * b0, a_m=(1, 0, 0),
+                gemm(1, n_out, Bb, None, d.data_ptr(), gp + 4 * b0, a_m=(1, 0, 0),
                      a_k=(1, 0, 0), b_ks=n_out, b_ns=1, ldc=n_out, workspace=self.workspace)
                 if j != -1:
                     # dX = dZ W^T (gated by the source layer's ReLU), accumulated over heads
-                    gemm(self.B, n_in, n_out, d.data_ptr(), tp + 4 * w0,
+                    gemm(Bb, n_in, n_out, d.data_ptr(), tp + 4 * w0,
                          self.douts[j].data_ptr(), a_m=(1, n_out, 0), b_ks=1, b_ns=n_out,
                          ldc=n_in, gate=gate_j, ld_gate=n_in if gate_j else 0,
                          beta=written[j], workspace=self.workspace)
                     written[j] = True
             else:
-                rows, Win, P, C = self._conv_dims(i)
+                rows, Win, P, C = self._conv_dims(i, Bb)
                 k, s, F = l.size, l.stride, l.filters
                 gemm(k * C, F, rows * P, src.data_ptr(), d.data_ptr(), gp + 4 * w0,
                      a_u8=src_u8, a_m=(1, 1, 0), a_k=(P, Win * C, s * C), b_ks=F, b_ns=1,

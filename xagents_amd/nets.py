@@ -136,6 +136,15 @@ class DeviceModel:
             weights += [w, np.zeros(nb, np.float32)]
         return weights
 
+    def clone(self, theta=None):
+        """Same architecture, own parameter buffer (copy of this model's unless
+        `theta` is given), no optimizer: the target networks of DQN / DDPG / TD3."""
+        import copy
+        m = copy.copy(self)
+        m.theta = self.theta.clone() if theta is None else theta
+        m.optimizer = None
+        return m
+
     # -- Keras-compatible weight access ------------------------------------
     def get_weights(self):
         flat = self.theta.detach().cpu().numpy()
