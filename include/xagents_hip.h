@@ -384,6 +384,27 @@ int xa_replay_env_step(const XaReplayStepArgs* args, void* stream);
 int xa_mse_grad(const float* pred, const float* target, int batch, int n_out, float* dpred,
                 float* loss, void* stream);
 
+/* dst[r][c] = src[r][c], rows x cols f32 block (tf.concat([states, actions], 1) and
+ * column slices of it). */
+int xa_copy_block(const float* src, int64_t ld_src, float* dst, int64_t ld_dst, int rows,
+                  int cols, void* stream);
+
+/* out = clip(x + clip(sigma N(0,1), -noise_clip, noise_clip), lo, hi) per element, the
+ * normals from Philox4x32-10 (counter *rng_counter, key seed) by Box-Muller; sigma = 0
+ * only clips. TD3 target smoothing (td3/agent.py:83-91: sigma 0.2, clip 0.5, [-1, 1]) and
+ * DDPG exploration (ddpg/agent.py:60-71: sigma 0.1). TF's RNG stream is not reproduced;
+ * noise_out (optional) receives the noise drawn. */
+int xa_noisy_actions(const float* x, int64_t ld_x, int rows, int cols, float sigma,
+                     float noise_clip, float lo, float hi, const uint64_t* rng_counter,
+                     uint64_t seed, float* out, int64_t ld_out, float* noise_out, void* stream);
+
+/* Critic targets + MSE gradients (ddpg/agent.py:104-127; TD3 twin critics
+ * td3/agent.py:66-110 when v2/tv2 != NULL): y = r + ((1 - d) gamma) min(tv1, tv2),
+ * dv_i = 2 (v_i - y), loss[b] = sum_i (v_i - y)^2. */
+int xa_critic_td_grad(const float* v1, const float* v2, const float* tv1, const float* tv2,
+                      const float* rewards, const float* dones, int batch, float gamma,
+                      float* dv1, float* dv2, float* loss, void* stream);
+
 /* Keras OptimizerV2 `iterations += 1` on device (before xa_clip_adam reads t). */
 int xa_adam_step_bump(int* adam_step, void* stream);
 

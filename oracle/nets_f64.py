@@ -92,12 +92,14 @@ def forward(layers, theta, x, input_shape):
     return x, outs
 
 
-def backward(layers, theta, x_in, outs, d_outputs):
-    """d_outputs: {layer index: d(loss)/d(layer output)} for the output layers."""
+def backward(layers, theta, x_in, outs, d_outputs, want_input_grad=False):
+    """d_outputs: {layer index: d(loss)/d(layer output)} for the output layers.
+    Returns the flat gradient, and d(loss)/d(input) too when want_input_grad."""
     sls, P = param_slices(layers)
     grad = np.zeros(P)
     B = x_in.shape[0]
     dys = {i: np.asarray(d, np.float64).reshape(outs[i].shape) for i, d in d_outputs.items()}
+    dx = None
     for i in range(len(layers) - 1, -1, -1):
         if i not in dys:
             continue
@@ -133,4 +135,6 @@ def backward(layers, theta, x_in, outs, d_outputs):
         if l.input_index != -1:
             j = l.input_index
             dys[j] = dys[j] + dsrc if j in dys else dsrc
-    return grad
+        else:
+            dx = dsrc if dx is None else dx + dsrc
+    return (grad, dx) if want_input_grad else grad

@@ -223,6 +223,17 @@ _SIGNATURES = {
     'xa_adam_step_bump': (c_int, [c_void_p, c_void_p]),
     'xa_replay_env_step': (c_int, [POINTER(XaReplayStepArgs), c_void_p]),
     'xa_mse_grad': (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    'xa_copy_block': (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int, c_int, c_void_p]),
+    'xa_noisy_actions': (
+        c_int,
+        [c_void_p, c_int64, c_int, c_int, c_float, c_float, c_float, c_float, c_void_p,
+         c_uint64, c_void_p, c_int64, c_void_p, c_void_p],
+    ),
+    'xa_critic_td_grad': (
+        c_int,
+        [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_float, c_void_p,
+         c_void_p, c_void_p, c_void_p],
+    ),
     'xa_activation_grad': (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p, c_void_p]),
 }
 

@@ -240,6 +240,68 @@ __global__ void replay_step_scalars_kernel(XaReplayStepArgs a) {
   a.cursor[i] = c + 1 < a.t_rec ? c + 1 : 0;
 }
 
+// dst[r][c] = src[r][c] for a rows x cols block (concat / column slices of [B, n] rows)
+__global__ __launch_bounds__(256) void copy_block_kernel(const float* __restrict__ src,
+                                                         int64_t ld_src, float* __restrict__ dst,
+                                                         int64_t ld_dst, int rows, int cols) {
+  const int64_t total = (int64_t)rows * cols;
+  for (int64_t e = blockIdx.x * 256ll + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int64_t r = e / cols, c = e % cols;
+    dst[r * ld_dst + c] = src[r * ld_src + c];
+  }
+}
+
+// standard normal from Philox4x32-10 (Box-Muller on two 24-bit uniforms in (0, 1])
+XA_DEV float philox_normal(uint32_t i, uint32_t j, uint64_t ctr, uint64_t seed) {
+  const xa_u4 r = xa_philox(i, j, (uint32_t)ctr, (uint32_t)(ctr >> 32), (uint32_t)seed,
+                            (uint32_t)(seed >> 32));
+  const float u1 = ((float)(r.x >> 8) + 1.0f) * 5.9604644775390625e-08f;
+  const float u2 = (float)(r.y >> 8) * 5.9604644775390625e-08f;
+  return sqrtf(-2.0f * logf(u1)) * cosf(6.283185307179586f * u2);
+}
+
+// out[b][a] = clip(x[b][a] + clip(sigma N(0,1), -noise_clip, noise_clip), lo, hi)
+// TD3 target smoothing (td3/agent.py:83-91) and DDPG exploration (ddpg/agent.py:60-71)
+__global__ void noisy_actions_kernel(const float* __restrict__ x, int64_t ld_x, int rows,
+                                     int cols, float sigma, float noise_clip, float lo, float hi,
+                                     const uint64_t* __restrict__ ctr, uint64_t seed,
+                                     float* __restrict__ out, int64_t ld_out,
+                                     float* __restrict__ noise_out) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= rows * cols) return;
+  const int b = e / cols, a = e % cols;
+  float n = 0.0f;
+  if (sigma != 0.0f) {
+    n = philox_normal((uint32_t)b, (uint32_t)a, ctr ? *ctr : 0ull, seed) * sigma;
+    n = fminf(fmaxf(n, -noise_clip), noise_clip);
+  }
+  if (noise_out) noise_out[e] = n;
+  out[(int64_t)b * ld_out + a] = fminf(fmaxf(x[(int64_t)b * ld_x + a] + n, lo), hi);
+}
+
+// DDPG / TD3 critic targets and MSE gradients (ddpg/agent.py:104-127, td3/agent.py:66-110):
+//   y = r + ((1 - d) gamma) min(tv1, tv2);  dv_i = 2 (v_i - y)  (MSE over a size-1 axis,
+//   minimize sums over the batch); loss_i[b] = (v_i - y)^2
+__global__ void critic_td_kernel(const float* __restrict__ v1, const float* __restrict__ v2,
+                                 const float* __restrict__ tv1, const float* __restrict__ tv2,
+                                 const float* __restrict__ rew, const float* __restrict__ done,
+                                 int B, float gamma, float* __restrict__ dv1,
+                                 float* __restrict__ dv2, float* __restrict__ loss) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const float tv = tv2 ? fminf(tv1[b], tv2[b]) : tv1[b];
+  const float y = rew[b] + ((1.0f - done[b]) * gamma) * tv;
+  const float e1 = v1[b] - y;
+  dv1[b] = 2.0f * e1;
+  float l = e1 * e1;
+  if (v2) {
+    const float e2 = v2[b] - y;
+    dv2[b] = 2.0f * e2;
+    l = l + e2 * e2;
+  }
+  if (loss) loss[b] = l;
+}
+
 int grid_for(int64_t n) {
   const int64_t b = (n + 255) / 256;
   return (int)(b < 8192 ? (b > 0 ? b : 1) : 8192);
@@ -377,5 +439,39 @@ extern "C" int xa_mse_grad(const float* pred, const float* target, int batch, in
   hipLaunchKernelGGL(mse_grad_kernel, dim3((batch + 63) / 64), dim3(64), 0, (hipStream_t)stream,
                      pred, target, batch, n_out, dpred, loss);
   XA_CHECK_LAUNCH("xa_mse_grad");
+  return 0;
+}
+
+extern "C" int xa_copy_block(const float* src, int64_t ld_src, float* dst, int64_t ld_dst,
+                             int rows, int cols, void* stream) {
+  XA_CHECK_ARG(src && dst && rows > 0 && cols > 0 && ld_src >= cols && ld_dst >= cols,
+               "xa_copy_block: bad arguments");
+  hipLaunchKernelGGL(copy_block_kernel, dim3(grid_for((int64_t)rows * cols)), dim3(256), 0,
+                     (hipStream_t)stream, src, ld_src, dst, ld_dst, rows, cols);
+  XA_CHECK_LAUNCH("xa_copy_block");
+  return 0;
+}
+
+extern "C" int xa_noisy_actions(const float* x, int64_t ld_x, int rows, int cols, float sigma,
+                                float noise_clip, float lo, float hi, const uint64_t* rng_counter,
+                                uint64_t seed, float* out, int64_t ld_out, float* noise_out,
+                                void* stream) {
+  XA_CHECK_ARG(x && out && rows > 0 && cols > 0, "xa_noisy_actions: bad arguments");
+  hipLaunchKernelGGL(noisy_actions_kernel, dim3((rows * cols + 63) / 64), dim3(64), 0,
+                     (hipStream_t)stream, x, ld_x, rows, cols, sigma, noise_clip, lo, hi,
+                     rng_counter, seed, out, ld_out, noise_out);
+  XA_CHECK_LAUNCH("xa_noisy_actions");
+  return 0;
+}
+
+extern "C" int xa_critic_td_grad(const float* v1, const float* v2, const float* tv1,
+                                 const float* tv2, const float* rewards, const float* dones,
+                                 int batch, float gamma, float* dv1, float* dv2, float* loss,
+                                 void* stream) {
+  XA_CHECK_ARG(v1 && tv1 && rewards && dones && dv1 && batch > 0 && (!v2 || dv2),
+               "xa_critic_td_grad: bad arguments");
+  hipLaunchKernelGGL(critic_td_kernel, dim3((batch + 63) / 64), dim3(64), 0, (hipStream_t)stream,
+                     v1, v2, tv1, tv2, rewards, dones, batch, gamma, dv1, dv2, loss);
+  XA_CHECK_LAUNCH("xa_critic_td_grad");
   return 0;
 }

@@ -1,0 +1,180 @@
+"""DDPG with the xagents class surface (xagents/ddpg/agent.py:7-166) on the device path.
+
+Per gradient step (ddpg/agent.py:129-147), all launches on device:
+    concat_buffer_samples   host index draw (np.random.randint per RB2, the reference's
+                            stream) -> xa_ring_gather
+    update_critic_weights   target_actor(s') -> [s', a'] -> target_critic -> y;
+                            critic([s, a]) -> xa_critic_td_grad -> backward -> Keras Adam
+    update_actor_weights    actor(s) -> critic([s, pi(s)]) -> d(-mean Q)/d input ->
+                            actor backward -> Keras Adam           (every policy_delay)
+    sync_target_models      xa_polyak (1 - tau) target + tau online (every policy_delay)
+The MLPs run on xa_gemm through the layer executor (xagents_amd/layers.py).
+"""
+import numpy as np
+import torch
+
+from xagents_amd import kernels
+from xagents_amd._lib import call, stream
+from xagents_amd.base import OffPolicy
+from xagents_amd.envs import Box
+from xagents_amd.layers import LayerExecutor
+
+
+class DDPG(OffPolicy):
+    """Continuous control with deep reinforcement learning https://arxiv.org/abs/1509.02971"""
+
+    def __init__(
+        self,
+        envs,
+        actor_model,
+        critic_model,
+        buffers,
+        gradient_steps=None,
+        tau=0.05,
+        step_noise_coef=0.1,
+        **kwargs,
+    ):
+        super(DDPG, self).__init__(envs, actor_model, buffers, **kwargs)
+        self.assert_valid_env(envs[0], Box)
+        self.actor = actor_model
+        self.critic = critic_model
+        self.policy_delay = 1
+        self.gradient_steps = gradient_steps
+        self.tau = tau
+        self.step_noise_coef = step_noise_coef
+        self.episode_steps = np.zeros(self.n_envs, np.float32)
+        self.output_models.append(self.critic)
+        self.target_actor = self.actor.clone()
+        self.target_critic = self.critic.clone()
+        self.model_groups = [(self.actor, self.target_actor), (self.critic, self.target_critic)]
+        self.batch_dtypes = 5 * ['float32']
+        self._setup_device()
+
+    # ---- device state ----------------------------------------------------------
+    def _setup_device(self):
+        S = int(np.prod(self.envs.obs_shape))
+        A = self.n_actions
+        self._setup_offpolicy((A,), np.float32)
+        B = self.n_envs * self.replay.k
+        self.batch_size, self.S, self.A = B, S, A
+        dev = self.device
+        f32 = dict(dtype=torch.float32, device=dev)
+        self.s, self.s2 = torch.zeros(B, S, **f32), torch.zeros(B, S, **f32)
+        self.a = torch.zeros(B, A, **f32)
+        self.r, self.d = torch.zeros(B, **f32), torch.zeros(B, **f32)
+        self.sa, self.s2a2 = torch.zeros(B, S + A, **f32), torch.zeros(B, S + A, **f32)
+        self.spa, self.dspa = torch.zeros(B, S + A, **f32), torch.zeros(B, S + A, **f32)
+        self.da = torch.zeros(B, A, **f32)
+        self.dv1, self.dv2 = torch.zeros(B, 1, **f32), torch.zeros(B, 1, **f32)
+        self.critic_loss = torch.zeros(B, **f32)
+        self.dq_actor = torch.full((B, 1), -1.0 / B, **f32)  # d(-mean Q)/dQ
+        self.noise = torch.zeros(B, A, **f32)
+        self.ta_smooth = torch.zeros(B, A, **f32)
+        self.step_actions = torch.zeros(self.n_envs, A, **f32)
+        self.adam_ws = torch.zeros(1024, dtype=torch.float64, device=dev)
+        self.rng_counter = torch.zeros(1, dtype=torch.int64, device=dev)
+        seed = self.seed if self.seed is not None else int(np.random.SeedSequence().entropy % 2**63)
+        self.rng_seed = (int(seed) * 2654435761 + 97) % 2**64
+        self.ex_step = LayerExecutor(self.actor, self.n_envs)
+        self.ex_actor = LayerExecutor(self.actor, B)
+        self.ex_target_actor = LayerExecutor(self.target_actor, B)
+        self.ex_critic = LayerExecutor(self.critic, B)
+        self.ex_critic_pi = LayerExecutor(self.critic, B)
+        self.ex_target_critic = LayerExecutor(self.target_critic, B)
+        self.g_actor = torch.zeros(self.actor.n_params, **f32)
+        self.g_critic = torch.zeros(self.critic.n_params, **f32)
+
+    def _concat(self, left, right, out):
+        B = self.batch_size
+        call('xa_copy_block', left.data_ptr(), left.shape[1], out.data_ptr(), out.shape[1], B,
+             left.shape[1], stream())
+        call('xa_copy_block', right.data_ptr(), right.shape[1], out.data_ptr() + 4 * left.shape[1],
+             out.shape[1], B, right.shape[1], stream())
+
+    def _adam(self, model, grad):
+        opt = model.optimizer
+        call('xa_adam_step_bump', opt.iterations.data_ptr(), stream())
+        kernels.clip_adam(model.theta, opt.m, opt.v, grad, opt.iterations, opt.learning_rate,
+                          opt.beta_1, opt.beta_2, opt.epsilon, clip_norm=0.0,
+                          workspace=self.adam_ws)
+
+    def _noisy(self, x, sigma, noise_clip, out, noise_out=None):
+        rows, cols = x.shape
+        call('xa_noisy_actions', x.data_ptr(), cols, rows, cols, kernels._f32(sigma),
+             kernels._f32(noise_clip), kernels._f32(-1.0), kernels._f32(1.0),
+             self.rng_counter.data_ptr(), self.rng_seed, out.data_ptr(), out.shape[1],
+             noise_out.data_ptr() if noise_out is not None else None, stream())
+        kernels.counter_bump(self.rng_counter)
+
+    # ---- reference surface ---------------------------------------------------------
+    def get_step_actions(self):
+        """clip(actor(s) + N(0, step_noise_coef), -1, 1) (ddpg/agent.py:60-71)."""
+        a = self.ex_step.forward(self.envs.state)[0]
+        self._noisy(a, self.step_noise_coef, float('inf'), self.step_actions)
+        return self.step_actions
+
+    def sync_target_models(self):
+        """target = (1 - tau) target + tau online, every model group (ddpg/agent.py:73-85)."""
+        for model, target in self.model_groups:
+            call('xa_polyak', model.theta.data_ptr(), target.theta.data_ptr(), model.n_params,
+                 kernels._f32(self.tau), stream())
+
+    def _target_inputs(self):
+        ta = self.ex_target_actor.forward(self.s2)[0]
+        self._concat(self.s2, ta, self.s2a2)
+
+    def update_critic_weights(self, states=None, actions=None, new_states=None, dones=None,
+                              rewards=None):
+        """ddpg/agent.py:104-127 on the gathered batch."""
+        self._target_inputs()
+        tv = self.ex_target_critic.forward(self.s2a2)[0]
+        self._concat(self.s, self.a, self.sa)
+        v = self.ex_critic.forward(self.sa)[0]
+        call('xa_critic_td_grad', v.data_ptr(), None, tv.data_ptr(), None, self.r.data_ptr(),
+             self.d.data_ptr(), self.batch_size, kernels._f32(self.gamma), self.dv1.data_ptr(),
+             None, self.critic_loss.data_ptr(), stream())
+        self.ex_critic.backward([self.dv1], self.g_critic)
+        self._adam(self.critic, self.g_critic)
+
+    def update_actor_weights(self, states=None):
+        """-mean(critic([s, actor(s)])) minimized over the actor (ddpg/agent.py:87-102)."""
+        pa = self.ex_actor.forward(self.s)[0]
+        self._concat(self.s, pa, self.spa)
+        self.ex_critic_pi.forward(self.spa)
+        self.ex_critic_pi.backward([self.dq_actor], None, dinput=self.dspa)
+        call('xa_copy_block', self.dspa.data_ptr() + 4 * self.S, self.S + self.A,
+             self.da.data_ptr(), self.A, self.batch_size, self.A, stream())
+        self.ex_actor.backward([self.da], self.g_actor)
+        self._adam(self.actor, self.g_actor)
+
+    def concat_buffer_samples(self):
+        slots = self.replay.upload_slots(self.replay.sample_slots())
+        self.replay.gather(slots, self.s, self.a, self.r, self.d, self.s2)
+        return [self.s, self.a, self.r, self.d, self.s2]
+
+    def update_weights(self, gradient_steps):
+        """ddpg/agent.py:129-147"""
+        for gradient_step in range(int(gradient_steps)):
+            self.concat_buffer_samples()
+            self.update_critic_weights()
+            if gradient_step % self.policy_delay == 0:
+                self.update_actor_weights()
+                self.sync_target_models()
+
+    def train_step(self):
+        """ddpg/agent.py:149-166: step every env, then for each env that finished an
+        episode run gradient_steps (or that env's episode length) gradient steps."""
+        actions = self.get_step_actions()
+        row = self._st_row
+        self._env_step(actions)
+        self.steps += self.n_envs
+        dones = self._host_row_dones(row)
+        for idx in np.nonzero(dones)[0]:
+            steps = self.gradient_steps or self.episode_steps[idx]
+            self.update_weights(steps)
+        self.episode_steps = (self.episode_steps + 1.0) * (1.0 - dones)
+
+    def _host_row_dones(self, row):
+        """The done flags of the step just taken (the reference returns them from the
+        numpy step_envs; here one small synchronous copy of the step's stats row)."""
+        return self._st_done[row].cpu().numpy()

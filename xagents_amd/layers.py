@@ -170,15 +170,17 @@ class LayerExecutor:
         return [self.outs[i] for i in self.model.outputs]
 
     # ---- backward ----------------------------------------------------------------
-    def backward(self, d_outputs, grad, batch=None):
+    def backward(self, d_outputs, grad, batch=None, dinput=None):
         """d_outputs: gradients w.r.t. the output layers (model.outputs order, [b, n]).
-        Writes the flat parameter gradient into `grad` (Keras variable order). `batch`
-        (<= B) back-propagates only the first rows of the last forward (samples are
-        independent rows, so a prefix of every buffer is a smaller batch)."""
+        Writes the flat parameter gradient into `grad` (Keras variable order; None skips
+        the parameter gradients) and, if given, d(loss)/d(input) into `dinput` [b, in]
+        (dense input layers). `batch` (<= B) back-propagates only the first rows of the
+        last forward (samples are independent rows, so a prefix of every buffer is a
+        smaller batch)."""
         Bb = batch or self.B
         assert Bb <= self.B
         tp = self.model.theta.data_ptr()
-        gp = grad.data_ptr()
+        gp = grad.data_ptr() if grad is not None else None
         written = [False] * len(self.layers)
         dz = {}
         for i, d in zip(self.model.outputs, d_outputs):
@@ -216,12 +218,17 @@ class LayerExecutor:
                 gate_j = self.outs[j].data_ptr()
             if l.kind == 'dense':
                 n_in, n_out = l.in_features, l.units
-                # dW = X^T dZ ; db = 1^T dZ
-                gemm(n_in, n_out, Bb, src.data_ptr(), d.data_ptr(), gp + 4 * w0,
-                     a_u8=src_u8, a_m=(1, 1, 0), a_k=(1, n_in, 0), b_ks=n_out, b_ns=1,
-                     ldc=n_out, workspace=self.workspace)
-                gemm(1, n_out, Bb, None, d.data_ptr(), gp + 4 * b0, a_m=(1, 0, 0),
-                     a_k=(1, 0, 0), b_ks=n_out, b_ns=1, ldc=n_out, workspace=self.workspace)
+                if gp is not None:
+                    # dW = X^T dZ ; db = 1^T dZ
+                    gemm(n_in, n_out, Bb, src.data_ptr(), d.data_ptr(), gp + 4 * w0,
+                         a_u8=src_u8, a_m=(1, 1, 0), a_k=(1, n_in, 0), b_ks=n_out, b_ns=1,
+                         ldc=n_out, workspace=self.workspace)
+                    gemm(1, n_out, Bb, None, d.data_ptr(), gp + 4 * b0, a_m=(1, 0, 0),
+                         a_k=(1, 0, 0), b_ks=n_out, b_ns=1, ldc=n_out, workspace=self.workspace)
+                if j == -1 and dinput is not None:
+                    gemm(Bb, n_in, n_out, d.data_ptr(), tp + 4 * w0, dinput.data_ptr(),
+                         a_m=(1, n_out, 0), b_ks=1, b_ns=n_out, ldc=n_in,
+                         workspace=self.workspace)
                 if j != -1:
                     # dX = dZ W^T (gated by the source layer's ReLU), accumulated over heads
                     gemm(Bb, n_in, n_out, d.data_ptr(), tp + 4 * w0,
@@ -232,11 +239,12 @@ class LayerExecutor:
             else:
                 rows, Win, P, C = self._conv_dims(i, Bb)
                 k, s, F = l.size, l.stride, l.filters
-                gemm(k * C, F, rows * P, src.data_ptr(), d.data_ptr(), gp + 4 * w0,
-                     a_u8=src_u8, a_m=(1, 1, 0), a_k=(P, Win * C, s * C), b_ks=F, b_ns=1,
-                     ldc=F, workspace=self.workspace)
-                gemm(1, F, rows * P, None, d.data_ptr(), gp + 4 * b0, a_m=(1, 0, 0),
-                     a_k=(1, 0, 0), b_ks=F, b_ns=1, ldc=F, workspace=self.workspace)
+                if gp is not None:
+                    gemm(k * C, F, rows * P, src.data_ptr(), d.data_ptr(), gp + 4 * w0,
+                         a_u8=src_u8, a_m=(1, 1, 0), a_k=(P, Win * C, s * C), b_ks=F, b_ns=1,
+                         ldc=F, workspace=self.workspace)
+                    gemm(1, F, rows * P, None, d.data_ptr(), gp + 4 * b0, a_m=(1, 0, 0),
+                         a_k=(1, 0, 0), b_ks=F, b_ns=1, ldc=F, workspace=self.workspace)
                 if j != -1:
                     assert not written[j], 'a conv input with two consumers is not supported'
                     gemm(rows * P, k * C, F, d.data_ptr(), tp + 4 * w0, self.dcol.data_ptr(),

@@ -1,0 +1,87 @@
+"""TD3 with the xagents class surface (xagents/td3/agent.py:6-110) on the device path:
+DDPG's device step with twin critics, target-policy smoothing and delayed actor /
+target updates.
+
+Kept reference behaviours: deterministic env stepping (no
+exploration noise, td3/agent.py:57-64); critic2 is a fresh clone of critic1's
+architecture (its own initialisation -- identical to critic1's when the model seed is
+set, as seeded Keras initializers give the same draw) with its own Adam at critic1's
+learning rate; target_critic2 copies critic2.
+"""
+import numpy as np
+import torch
+
+from xagents_amd import kernels
+from xagents_amd._lib import call, stream
+from xagents_amd.ddpg.agent import DDPG
+from xagents_amd.layers import LayerExecutor
+from xagents_amd.nets import Adam
+
+
+class TD3(DDPG):
+    """Addressing Function Approximation Error in Actor-Critic Methods
+    https://arxiv.org/abs/1802.09477"""
+
+    def __init__(
+        self,
+        envs,
+        actor_model,
+        critic_model,
+        buffers,
+        policy_delay=2,
+        policy_noise_coef=0.2,
+        noise_clip=0.5,
+        **kwargs,
+    ):
+        super(TD3, self).__init__(envs, actor_model, critic_model, buffers, **kwargs)
+        self.critic1 = self.critic
+        self.target_critic1 = self.target_critic
+        self.policy_delay = policy_delay
+        self.policy_noise_coef = policy_noise_coef
+        self.noise_clip = noise_clip
+        fresh = np.concatenate([w.ravel() for w in self.critic1._init_weights()])
+        self.critic2 = self.critic1.clone(torch.from_numpy(fresh).to(self.device))
+        opt1 = self.critic1.optimizer
+        self.critic2.optimizer = Adam(learning_rate=opt1.learning_rate)
+        self.critic2.optimizer.bind(self.critic2.n_params, self.device)
+        self.output_models.append(self.critic2)
+        self.target_critic2 = self.critic2.clone()
+        self.model_groups.append((self.critic2, self.target_critic2))
+        self._setup_twin()
+
+    def _setup_twin(self):
+        B = self.batch_size
+        self.ex_critic2 = LayerExecutor(self.critic2, B)
+        self.ex_target_critic2 = LayerExecutor(self.target_critic2, B)
+        self.g_critic2 = torch.zeros(self.critic2.n_params, dtype=torch.float32,
+                                     device=self.device)
+
+    def get_step_actions(self):
+        """actor(s), no exploration noise (td3/agent.py:57-64)."""
+        a = self.ex_step.forward(self.envs.state)[0]
+        call('xa_copy_block', a.data_ptr(), self.A, self.step_actions.data_ptr(), self.A,
+             self.n_envs, self.A, stream())
+        return self.step_actions
+
+    def _target_inputs(self):
+        """clip(target_actor(s') + clip(0.2 N, -0.5, 0.5), -1, 1) (td3/agent.py:83-91)."""
+        ta = self.ex_target_actor.forward(self.s2)[0]
+        self._noisy(ta, self.policy_noise_coef, self.noise_clip, self.ta_smooth, self.noise)
+        self._concat(self.s2, self.ta_smooth, self.s2a2)
+
+    def update_critic_weights(self, states=None, actions=None, new_states=None, dones=None,
+                              rewards=None):
+        """Both critics against min of the target critics (td3/agent.py:66-110)."""
+        self._target_inputs()
+        tv1 = self.ex_target_critic.forward(self.s2a2)[0]
+        tv2 = self.ex_target_critic2.forward(self.s2a2)[0]
+        self._concat(self.s, self.a, self.sa)
+        v1 = self.ex_critic.forward(self.sa)[0]
+        v2 = self.ex_critic2.forward(self.sa)[0]
+        call('xa_critic_td_grad', v1.data_ptr(), v2.data_ptr(), tv1.data_ptr(), tv2.data_ptr(),
+             self.r.data_ptr(), self.d.data_ptr(), self.batch_size, kernels._f32(self.gamma),
+             self.dv1.data_ptr(), self.dv2.data_ptr(), self.critic_loss.data_ptr(), stream())
+        self.ex_critic.backward([self.dv1], self.g_critic)
+        self.ex_critic2.backward([self.dv2], self.g_critic2)
+        self._adam(self.critic1, self.g_critic)
+        self._adam(self.critic2, self.g_critic2)
