@@ -375,6 +375,8 @@ typedef struct XaReplayStepArgs {
   float* out_rewards;
   float* out_dones;
   float* done_epret;
+  int64_t out_ld; /* element stride between envs of out_rewards / out_dones / done_epret
+                     (0 = 1; n_steps writes env-major [N, T] rollout rows) */
 } XaReplayStepArgs;
 
 int xa_replay_env_step(const XaReplayStepArgs* args, void* stream);
@@ -404,6 +406,43 @@ int xa_noisy_actions(const float* x, int64_t ld_x, int rows, int cols, float sig
 int xa_critic_td_grad(const float* v1, const float* v2, const float* tv1, const float* tv2,
                       const float* rewards, const float* dones, int batch, float gamma,
                       float* dv1, float* dv2, float* loss, void* stream);
+
+/* TFP Categorical(logits) over n logit rows (A2C.get_model_outputs, a2c/agent.py:65-94):
+ * log-prob and entropy of the given actions (actions_in) or of an inverse-CDF sample
+ * with uniforms[i] or Philox(i, step, *rng_counter, seed). Same arithmetic as the fused
+ * MLP rollout. Outputs (optional) are written at i * ld_out. n_actions <= 64. */
+int xa_categorical(const float* logits, int64_t ld_logits, int n, int n_actions,
+                   const float* uniforms, const uint64_t* rng_counter, uint64_t seed, int step,
+                   const int* actions_in, int* actions_out, float* logp, float* entropy,
+                   int64_t ld_out, void* stream);
+
+/* PPO / A2C loss of one minibatch (mean over its n samples) and its gradient w.r.t. the
+ * logits and the value head, for models run through xa_gemm (the CNN actor-critic):
+ * PPO.update_gradients (ppo/agent.py:96-137) with per-minibatch advantage normalisation
+ * (run_ppo_epochs 180-183), A2C.train_step (a2c/agent.py:190-218). loss (optional):
+ * [pg, value, entropy] means. */
+typedef struct XaHeadGradArgs {
+  int n, n_actions, loss_kind;
+  const float* logits;
+  int64_t ld_logits;
+  const float* values;
+  int64_t ld_values;
+  const int* actions;
+  const float* old_logp;
+  const float* old_values;
+  const float* returns;
+  float clip_norm, entropy_coef, value_coef, adv_eps;
+  float* dlogits;
+  float* dvalues;
+  float* loss;
+  /* advantage statistics: 0 = this minibatch's own; 1 = only write [sum, sum^2, n] of
+   * adv = returns - old_values to adv_stats (then all-reduce them over the ranks);
+   * 2 = use the all-reduced adv_stats (the union minibatch's mean / population std) */
+  int stats_mode;
+  double* adv_stats;
+} XaHeadGradArgs;
+
+int xa_ac_head_grad(const XaHeadGradArgs* args, void* stream);
 
 /* Keras OptimizerV2 `iterations += 1` on device (before xa_clip_adam reads t). */
 int xa_adam_step_bump(int* adam_step, void* stream);

@@ -164,7 +164,21 @@ class XaReplayStepArgs(Structure):
         ('ring_states', c_void_p), ('ring_new_states', c_void_p), ('ring_actions', c_void_p),
         ('ring_rewards', c_void_p), ('ring_dones', c_void_p),
         ('out_states', c_void_p), ('out_new_states', c_void_p), ('out_rewards', c_void_p),
-        ('out_dones', c_void_p), ('done_epret', c_void_p),
+        ('out_dones', c_void_p), ('done_epret', c_void_p), ('out_ld', c_int64),
+    ]
+
+
+class XaHeadGradArgs(Structure):
+    _fields_ = [
+        ('n', c_int), ('n_actions', c_int), ('loss_kind', c_int),
+        ('logits', c_void_p), ('ld_logits', c_int64),
+        ('values', c_void_p), ('ld_values', c_int64),
+        ('actions', c_void_p), ('old_logp', c_void_p), ('old_values', c_void_p),
+        ('returns', c_void_p),
+        ('clip_norm', c_float), ('entropy_coef', c_float), ('value_coef', c_float),
+        ('adv_eps', c_float),
+        ('dlogits', c_void_p), ('dvalues', c_void_p), ('loss', c_void_p),
+        ('stats_mode', c_int), ('adv_stats', c_void_p),
     ]
 
 
@@ -224,6 +238,12 @@ _SIGNATURES = {
     'xa_replay_env_step': (c_int, [POINTER(XaReplayStepArgs), c_void_p]),
     'xa_mse_grad': (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     'xa_copy_block': (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int, c_int, c_void_p]),
+    'xa_categorical': (
+        c_int,
+        [c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_uint64, c_int, c_void_p,
+         c_void_p, c_void_p, c_void_p, c_int64, c_void_p],
+    ),
+    'xa_ac_head_grad': (c_int, [POINTER(XaHeadGradArgs), c_void_p]),
     'xa_noisy_actions': (
         c_int,
         [c_void_p, c_int64, c_int, c_int, c_float, c_float, c_float, c_float, c_void_p,

@@ -18,9 +18,10 @@ from xagents_amd._lib import (XA_RETURNS_GAE, XA_RETURNS_NONE, XA_RETURNS_NSTEP,
                               XaAcGradArgs, XaRolloutArgs, XaShuffle)
 from xagents_amd.base import OnPolicy
 from xagents_amd.envs import Discrete
+from xagents_amd.onpolicy_executor import ExecutorActorCritic
 
 
-class A2C(OnPolicy):
+class A2C(ExecutorActorCritic, OnPolicy):
     """Asynchronous Methods for Deep Reinforcement Learning
     https://arxiv.org/abs/1602.01783"""
 
@@ -50,15 +51,20 @@ class A2C(OnPolicy):
         self.distribution_type = (
             'Categorical' if isinstance(self.envs[0].action_space, Discrete)
             else 'MultivariateNormalDiag')
-        if getattr(model, 'fused_kind', None) != 'actor_critic_mlp':
-            raise NotImplementedError(
-                'The fused on-policy path supports the actor-critic MLP topology '
-                '(obs->64 tanh->64 tanh->{A,1}); got a model that does not match it')
         if self.output_is_softmax or self.distribution_type != 'Categorical':
-            raise NotImplementedError('Only Categorical(logits) policies are fused')
+            raise NotImplementedError('Only Categorical(logits) policies are supported')
         self.use_graph = use_graph
         self._graph = None
-        self._setup_device()
+        # the actor-critic MLP runs on the fused kernels; any other .cfg actor-critic
+        # (the CNN) on the layer executor (xagents_amd/onpolicy_executor.py)
+        self.executor_path = getattr(model, 'fused_kind', None) != 'actor_critic_mlp'
+        if self.executor_path:
+            self.distributed = dist.is_available() and dist.is_initialized()
+            self.world_size = dist.get_world_size() if self.distributed else 1
+            self.rank = dist.get_rank() if self.distributed else 0
+            self._setup_executor_path()
+        else:
+            self._setup_device()
 
     # ---- device state ------------------------------------------------------
     def _setup_device(self):
@@ -230,6 +236,15 @@ class A2C(OnPolicy):
         """One train step. `events` = (start, mid, end) torch.cuda.Events recorded
         around the rollout and the update on the replay stream (bench timing)."""
         rec = (lambda i: events[i].record()) if events else (lambda i: None)  # noqa: E731
+        if self.executor_path:
+            rec(0)
+            self._executor_rollout()
+            rec(1)
+            self._executor_update()
+            rec(2)
+            self.steps += self.n_envs * self.n_steps
+            self._queue_episode_stats(self.b_done, self.b_epret)
+            return
         if self.use_graph and self._graph is not None:
             rec(0)
             self._graph[0].replay()

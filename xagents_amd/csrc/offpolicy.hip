@@ -230,10 +230,11 @@ __global__ void replay_step_scalars_kernel(XaReplayStepArgs a) {
     const int64_t cnt = a.ring_count[i];
     a.ring_count[i] = a.ring_kind == XA_RING_RB2 ? (cnt < a.capacity ? cnt + 1 : cnt) : cnt + 1;
   }
-  if (a.out_rewards) a.out_rewards[i] = r;
-  if (a.out_dones) a.out_dones[i] = d;
+  const int64_t o = (int64_t)i * (a.out_ld > 0 ? a.out_ld : 1);
+  if (a.out_rewards) a.out_rewards[o] = r;
+  if (a.out_dones) a.out_dones[o] = d;
   float ep = a.ep_return[i] + r;
-  if (a.done_epret) a.done_epret[i] = d != 0.0f ? ep : 0.0f;
+  if (a.done_epret) a.done_epret[o] = d != 0.0f ? ep : 0.0f;
   if (d != 0.0f) ep = 0.0f;
   a.ep_return[i] = ep;
   a.done[i] = d;

@@ -1,0 +1,186 @@
+"""On-policy actor-critic train step for models run through the layer executor (the
+CNN actor-critic of xagents/{a2c,ppo}/models/cnn-actor-critic.cfg, config C4) -- the
+counterpart of the fused MLP kernels for any .cfg actor-critic.
+
+Rollout (A2C.get_batch, xagents/a2c/agent.py:96-139), per step t:
+    CNN forward of obs[t] (uint8 frames, scaled in the GEMM loader)   xa_gemm x layers
+    Categorical sample / log-prob / entropy (Philox uniforms)          xa_categorical
+    value -> values[:, t]                                              xa_copy_block
+    env step: reward / done rows, obs[t+1] = the pre-reset obs (the
+    terminal-obs feed-through of a2c/agent.py:132-136)                 xa_replay_env_step
+then V(get_states()) and GAE / n-step returns (xa_gae / xa_nstep_returns).
+Update (PPO.run_ppo_epochs ppo/agent.py:157-191, A2C.train_step a2c/agent.py:190-218):
+per minibatch gather (xa_ring_gather) -> forward -> xa_ac_head_grad -> backward ->
+[RCCL all-reduce of the gradient and of the advantage sums] -> tf.clip_by_global_norm +
+Keras Adam (xa_clip_adam).
+Layouts: frames time-major [T+1, N, ...] (each step's batch is contiguous for the
+GEMMs); per-step scalars env-major [N, T] (concat_step_batches order, base.py:549-564).
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from xagents_amd import kernels
+from xagents_amd._lib import (XA_LOSS_PPO, XA_RETURNS_GAE, XaHeadGradArgs, XaReplayStepArgs,
+                              call, stream)
+from xagents_amd.layers import LayerExecutor
+
+
+class ExecutorActorCritic:
+    """Mixin for A2C / PPO when the model is not the fused actor-critic MLP."""
+
+    def _setup_executor_path(self):
+        env = self.envs
+        if not hasattr(env, 'fill_step_args'):
+            raise NotImplementedError('the executor on-policy path needs a transition-replay '
+                                      'device env (create_envs for Atari / BipedalWalker ids)')
+        if len(self.model.outputs) != 2:
+            raise NotImplementedError('actor-critic models need [logits, value] outputs')
+        N, T = self.n_envs, self.n_steps
+        dev = self.device
+        f32 = dict(dtype=torch.float32, device=dev)
+        self.obs_buf = torch.zeros((T + 1, N) + env.obs_shape,
+                                   dtype=env.state.dtype, device=dev)
+        self.b_act = torch.zeros(N, T, dtype=torch.int32, device=dev)
+        self.b_logp, self.b_val = torch.zeros(N, T, **f32), torch.zeros(N, T, **f32)
+        self.b_ent, self.b_rew = torch.zeros(N, T, **f32), torch.zeros(N, T, **f32)
+        self.b_done = torch.zeros(N, T + 1, **f32)
+        self.b_dstep = torch.zeros(N, T, **f32)
+        self.b_epret = torch.zeros(N, T, **f32)
+        self.b_ret = torch.zeros(N, T, **f32)
+        self.next_val = torch.zeros(N, **f32)
+        self.rng_counter = torch.zeros(1, dtype=torch.int64, device=dev)
+        seed = self.seed if self.seed is not None else int(np.random.SeedSequence().entropy % 2**63)
+        self.rng_seed = (int(seed) * 1000003 + self.rank * 7919 + 17) % 2**64
+        self.ex_roll = LayerExecutor(self.model, N)
+        self._sa = XaReplayStepArgs()
+        env.fill_step_args(self._sa)
+        self._sa.ring_states = None
+        B = N * T
+        mb = getattr(self, 'mini_batch_size', B)
+        self.mb = mb
+        self.n_mb = (B + mb - 1) // mb
+        self.ex_upd = LayerExecutor(self.model, mb)
+        self.mb_obs = torch.zeros((mb,) + env.obs_shape, dtype=env.state.dtype, device=dev)
+        self.mb_act = torch.zeros(mb, dtype=torch.int32, device=dev)
+        self.mb_logp, self.mb_val = torch.zeros(mb, **f32), torch.zeros(mb, **f32)
+        self.mb_ret = torch.zeros(mb, **f32)
+        self.dlogits = torch.zeros(mb, self.n_actions, **f32)
+        self.dvalue = torch.zeros(mb, 1, **f32)
+        self.head_loss = torch.zeros(3, **f32)
+        self.adv_sums = torch.zeros(3, dtype=torch.float64, device=dev)
+        self.grad = torch.zeros(self.model.n_params, **f32)
+        self.adam_ws = torch.zeros(1024, dtype=torch.float64, device=dev)
+        self._slots_obs = torch.zeros(mb, dtype=torch.int64, device=dev)
+        self._slots_flat = torch.zeros(mb, dtype=torch.int64, device=dev)
+        if self.distributed:
+            torch.distributed.broadcast(self.model.theta, 0)
+
+    # ---- rollout ------------------------------------------------------------------
+    def _executor_rollout(self):
+        N, T = self.n_envs, self.n_steps
+        env = self.envs
+        a = self._sa
+        self.obs_buf[0].copy_(env.state)
+        call('xa_copy_block', env.done.data_ptr(), 1, self.b_done.data_ptr(), T + 1, N, 1,
+             stream())
+        ob = env.obs_bytes
+        for t in range(T):
+            logits, value = self.ex_roll.forward(self.obs_buf[t])
+            call('xa_categorical', logits.data_ptr(), self.n_actions, N, self.n_actions, None,
+                 self.rng_counter.data_ptr(), self.rng_seed, t, None,
+                 self.b_act.data_ptr() + 4 * t, self.b_logp.data_ptr() + 4 * t,
+                 self.b_ent.data_ptr() + 4 * t, T, stream())
+            call('xa_copy_block', value.data_ptr(), 1, self.b_val.data_ptr() + 4 * t, T, N, 1,
+                 stream())
+            a.out_new_states = self.obs_buf.data_ptr() + (t + 1) * N * ob
+            a.out_rewards = self.b_rew.data_ptr() + 4 * t
+            a.out_dones = self.b_dstep.data_ptr() + 4 * t
+            a.done_epret = self.b_epret.data_ptr() + 4 * t
+            a.out_ld = T  # env-major [N, T] rows
+            call('xa_replay_env_step', ctypes.byref(a), stream())
+        # dones[:, t + 1] = done of step t (dones[:, 0] is the carried-in flag)
+        call('xa_copy_block', self.b_dstep.data_ptr(), T, self.b_done.data_ptr() + 4, T + 1, N,
+             T, stream())
+        value = self.ex_roll.forward(env.state)[1]
+        call('xa_copy_block', value.data_ptr(), 1, self.next_val.data_ptr(), 1, N, 1, stream())
+        if self.return_kind == XA_RETURNS_GAE:
+            kernels.gae(self.b_rew, self.b_val, self.b_done, self.next_val, self.gamma,
+                        self.lam, out=self.b_ret)
+        else:
+            kernels.nstep_returns(self.b_rew, self.b_done, self.next_val, self.gamma,
+                                  out=self.b_ret)
+        kernels.counter_bump(self.rng_counter)
+
+    # ---- update ---------------------------------------------------------------------
+    def _upload_slots(self, flat_idx):
+        """flat env-major sample indices i = env T + t -> frame slots t N + env."""
+        N, T = self.n_envs, self.n_steps
+        idx = np.asarray(flat_idx, np.int64)
+        obs_slots = (idx % T) * N + idx // T
+        self._slots_obs[:idx.size].copy_(torch.from_numpy(obs_slots))
+        self._slots_flat[:idx.size].copy_(torch.from_numpy(idx))
+        return idx.size
+
+    def _gather_minibatch(self, n):
+        so, sf = self._slots_obs.data_ptr(), self._slots_flat.data_ptr()
+        call('xa_ring_gather', self.obs_buf.data_ptr(), self.mb_obs.data_ptr(), so, n,
+             self.envs.obs_bytes, stream())
+        for src, dst in ((self.b_act, self.mb_act), (self.b_logp, self.mb_logp),
+                         (self.b_val, self.mb_val), (self.b_ret, self.mb_ret)):
+            call('xa_ring_gather', src.data_ptr(), dst.data_ptr(), sf, n, 4, stream())
+
+    def _minibatch_step(self, n):
+        logits, value = self.ex_upd.forward(self.mb_obs)
+        h = XaHeadGradArgs()
+        h.n, h.n_actions, h.loss_kind = n, self.n_actions, self.loss_kind
+        h.logits, h.ld_logits = logits.data_ptr(), self.n_actions
+        h.values, h.ld_values = value.data_ptr(), 1
+        h.actions, h.old_logp = self.mb_act.data_ptr(), self.mb_logp.data_ptr()
+        h.old_values, h.returns = self.mb_val.data_ptr(), self.mb_ret.data_ptr()
+        h.clip_norm = float(getattr(self, 'clip_norm', 0.0))
+        h.entropy_coef, h.value_coef = float(self.entropy_coef), float(self.value_loss_coef)
+        h.adv_eps = float(getattr(self, 'advantage_epsilon', 0.0))
+        h.dlogits, h.dvalues, h.loss = (self.dlogits.data_ptr(), self.dvalue.data_ptr(),
+                                        self.head_loss.data_ptr())
+        h.adv_stats = self.adv_sums.data_ptr()
+        h.stats_mode = 0
+        if self.distributed and self.loss_kind == XA_LOSS_PPO:
+            h.stats_mode = 1
+            call('xa_ac_head_grad', ctypes.byref(h), stream())
+            torch.distributed.all_reduce(self.adv_sums)
+            h.stats_mode = 2
+        call('xa_ac_head_grad', ctypes.byref(h), stream())
+        self.ex_upd.backward([self.dlogits[:n], self.dvalue[:n]], self.grad, batch=n)
+        if self.distributed:
+            torch.distributed.all_reduce(self.grad)
+        opt = self.model.optimizer
+        call('xa_adam_step_bump', opt.iterations.data_ptr(), stream())
+        kernels.clip_adam(self.model.theta, opt.m, opt.v, self.grad, opt.iterations,
+                          opt.learning_rate, opt.beta_1, opt.beta_2, opt.epsilon,
+                          clip_norm=self.grad_norm, grad_scale=1.0 / self.world_size,
+                          workspace=self.adam_ws)
+
+    def _executor_update(self):
+        B = self.n_envs * self.n_steps
+        if self.loss_kind == XA_LOSS_PPO:
+            # every epoch reshuffles the batch, then contiguous minibatch slices
+            # (ppo/agent.py:139-155); the permutation uses numpy's global RNG
+            for _ in range(self.ppo_epochs):
+                perm = np.random.permutation(B)
+                for m in range(self.n_mb):
+                    n = self._upload_slots(perm[m * self.mb:(m + 1) * self.mb])
+                    self._gather_minibatch(n)
+                    self._minibatch_step(n)
+        else:
+            n = self._upload_slots(np.arange(B))
+            self._gather_minibatch(n)
+            self._minibatch_step(n)
+
+    def _executor_train_step(self):
+        self._executor_rollout()
+        self._executor_update()
+        self.steps += self.n_envs * self.n_steps
+        self._queue_episode_stats(self.b_done, self.b_epret)
+

@@ -132,7 +132,8 @@ class PPO(A2C):
 
     def _on_lr_change(self):
         super()._on_lr_change()
-        self._setup_update()  # the learning rate is baked into the launch arguments
+        if not self.executor_path:
+            self._setup_update()  # the learning rate is baked into the launch arguments
 
     # ---- reference-level pieces --------------------------------------------
     def calculate_returns(self, rewards, dones, values=None, selected_critic_logits=None,
