@@ -44,6 +44,9 @@ def parse():
     p.add_argument('--no-graph', action='store_true')
     p.add_argument('--cpu-baseline-seconds', type=float, default=15.0)
     p.add_argument('--cpu-threads', type=int, default=0)
+    p.add_argument('--config', default='c2', choices=['c2', 'c3', 'c4', 'c5'],
+                   help='c2 (default, the BASELINE metric line); c3 DQN Pong-shaped, c4 PPO '
+                        'CNN Breakout-shaped (global 1024 envs, strong scaling), c5 TD3')
     return p.parse_args()
 
 
@@ -77,8 +80,125 @@ def load_traffic(key):
     return entry.get('bytes_per_launch') if entry else None
 
 
+def _dist_setup():
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local_rank = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local_rank))
+    return world, rank, torch.device('cuda', local_rank)
+
+
+def _timed(fn, steps, warmup, world):
+    """W untimed + K timed calls bracketed by barrier + synchronize; max over ranks."""
+    import torch
+    import torch.distributed as dist
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device='cuda')
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    return el
+
+
+def bench_offpolicy_and_cnn(args):
+    """Secondary configs; one JSON line each, same fields."""
+    import numpy as np
+    import torch
+    world, rank, device = _dist_setup()
+    from xagents_amd.envs import create_envs
+    from xagents_amd.utils.common import create_buffers, create_model
+    line = {'metric': METRIC, 'unit': 'env-steps/s', 'n_gpus': world, 'steps': args.steps,
+            'warmup': args.warmup, 'higher_is_better': True, 'vs_baseline': None,
+            'dtype': 'f32', 'cpu_baseline': None}
+    if args.config == 'c3':
+        from xagents_amd import DQN
+        n = 32
+        envs = create_envs('PongNoFrameskip-v4', n, device=device, seed=args.seed + rank)
+        model = create_model(envs, 'dqn', 'model', seed=args.seed, device=device)
+        bufs = create_buffers('dqn', 1_000_000, 64, n, initial_size=1_000_000)
+        agent = DQN(envs, model, bufs, double=True, seed=args.seed, quiet=True,
+                    epsilon_start=0.02, epsilon_end=0.02)
+        t_fill = time.perf_counter()
+        agent.fill_buffers()
+        t_fill = time.perf_counter() - t_fill
+
+        def step():
+            agent.at_step_start()
+            agent.train_step()
+            agent.at_step_end()
+        el = _timed(step, args.steps, args.warmup, world)
+        env_steps = n * args.steps * world
+        line.update(scaling='weak', data='synthetic: Pong-shaped uint8 (84,84,1) frames '
+                    'i.i.d. uniform (seed 55+rank), replay buffers pre-filled by device env steps',
+                    config={'workload': 'DQN/DDQN PongNoFrameskip-v4-shaped, 32 envs, NatureCNN '
+                                        '(Conv1D cfg), ReplayBuffer1 1M total, buffer batch 64, '
+                                        'double, epsilon 0.02 (BASELINE configs[2])',
+                            'n_envs_per_gpu': n, 'batch': 64, 'replay_fill_s': round(t_fill, 2),
+                            'parallelism': f'dp{world}'})
+    elif args.config == 'c4':
+        from xagents_amd import PPO
+        n = 1024 // world
+        envs = create_envs('BreakoutNoFrameskip-v4', n, device=device, seed=args.seed + rank)
+        model = create_model(envs, 'ppo', 'model', seed=args.seed, device=device)
+        agent = PPO(envs, model, n_steps=128, seed=args.seed, quiet=True)
+        el = _timed(agent.fused_train_step, args.steps, args.warmup, world)
+        env_steps = n * 128 * args.steps * world
+        line.update(scaling='strong', data='synthetic: Breakout-shaped uint8 (84,84,1) frames '
+                    'i.i.d. uniform (seed 55+rank), random-init CNN',
+                    config={'workload': 'PPO BreakoutNoFrameskip-v4-shaped, 1024 envs global '
+                                        'sharded over the GPUs, NatureCNN (Conv1D cfg), n_steps '
+                                        '128, 4x4 minibatches (BASELINE configs[3])',
+                            'n_envs_per_gpu': n, 'parallelism': f'dp{world}'})
+    else:
+        from xagents_amd import TD3
+        n = max(64 // world, 1)
+        envs = create_envs('BipedalWalker-v3', n, device=device, seed=args.seed + rank)
+        kw = dict(seed=args.seed, device=device)
+        actor = create_model(envs, 'td3', 'actor_model', **kw)
+        critic = create_model(envs, 'td3', 'critic_model', **kw)
+        bufs = create_buffers('td3', 1_000_000, 100, n, initial_size=n * 64)
+        agent = TD3(envs, actor, critic, bufs, gradient_steps=1, seed=args.seed, quiet=True)
+        agent.fill_buffers()
+        # env steps with their done-triggered gradient steps, and one gradient step alone
+        el = _timed(agent.train_step, args.steps, args.warmup, world)
+        g_el = _timed(lambda: agent.update_weights(1), args.steps, args.warmup, world)
+        env_steps = n * args.steps * world
+        line.update(scaling='weak', data='synthetic: BipedalWalker-shaped f32 obs ~N(0,1) '
+                    '(seed 55+rank)', config={
+                        'workload': 'TD3 BipedalWalker-v3-shaped, 64 envs, ReplayBuffer2, '
+                                    'per-buffer batch 1 (100 // 64), gradient_steps 1 '
+                                    '(BASELINE configs[4])',
+                        'n_envs_per_gpu': n, 'parallelism': f'dp{world}'},
+                    gradient_step_ms=round(g_el / args.steps * 1e3, 4))
+    line['value'] = round(env_steps / el, 1)
+    line['ms_per_step'] = round(el / args.steps * 1e3, 4)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if args.config != 'c2':
+        return bench_offpolicy_and_cnn(args)
     import numpy as np
     import torch
     import torch.distributed as dist

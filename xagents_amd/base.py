@@ -424,8 +424,14 @@ class OffPolicy(BaseAgent, ABC):
     def _setup_offpolicy(self, act_shape, act_dtype):
         """Device replay rings mirroring self.buffers, the fused env-step arguments and
         the per-step episode-stat rows copied back asynchronously."""
+        import torch.distributed as dist
         from xagents_amd._lib import XaReplayStepArgs
         from xagents_amd.replay import DeviceReplay
+        # data parallel over env shards: each rank samples its own buffers, gradients
+        # are all-reduced (sum) and scaled by 1 / world before Adam
+        self.distributed = dist.is_available() and dist.is_initialized()
+        self.world_size = dist.get_world_size() if self.distributed else 1
+        self.rank = dist.get_rank() if self.distributed else 0
         env = self.envs
         self.replay = DeviceReplay(self.buffers, env.obs_shape, env.obs_dtype, act_shape,
                                    act_dtype, self.device)
@@ -490,6 +496,20 @@ class OffPolicy(BaseAgent, ABC):
             self._flush_offpolicy_stats()
             while self._st_host:
                 self._fold_offpolicy_stats(*self._st_host.pop(0))
+
+    def _sync_params(self, *models):
+        if self.distributed:
+            import torch.distributed as dist
+            for m in models:
+                dist.broadcast(m.theta, 0)
+
+    def _reduce_grad(self, grad):
+        """All-reduce a gradient over the data-parallel ranks; returns Adam's grad_scale."""
+        if not self.distributed:
+            return 1.0
+        import torch.distributed as dist
+        dist.all_reduce(grad)
+        return 1.0 / self.world_size
 
     def _random_actions(self):
         """env.action_space.sample() per env (OffPolicy.fill_buffers, base.py:702-730)."""

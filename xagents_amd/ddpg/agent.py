@@ -83,6 +83,7 @@ class DDPG(OffPolicy):
         self.ex_target_critic = LayerExecutor(self.target_critic, B)
         self.g_actor = torch.zeros(self.actor.n_params, **f32)
         self.g_critic = torch.zeros(self.critic.n_params, **f32)
+        self._sync_params(self.actor, self.critic, self.target_actor, self.target_critic)
 
     def _concat(self, left, right, out):
         B = self.batch_size
@@ -93,10 +94,11 @@ class DDPG(OffPolicy):
 
     def _adam(self, model, grad):
         opt = model.optimizer
+        scale = self._reduce_grad(grad)
         call('xa_adam_step_bump', opt.iterations.data_ptr(), stream())
         kernels.clip_adam(model.theta, opt.m, opt.v, grad, opt.iterations, opt.learning_rate,
                           opt.beta_1, opt.beta_2, opt.epsilon, clip_norm=0.0,
-                          workspace=self.adam_ws)
+                          grad_scale=scale, workspace=self.adam_ws)
 
     def _noisy(self, x, sigma, noise_clip, out, noise_out=None):
         rows, cols = x.shape

@@ -73,6 +73,7 @@ class DQN(OffPolicy):
         self.ex_online = LayerExecutor(self.model, 2 * B if self.double else B)
         self.ex_target = LayerExecutor(self.target_model, B)
         self.ex_act = LayerExecutor(self.model, self.n_envs)
+        self._sync_params(self.model, self.target_model)
 
     # ---- reference surface ---------------------------------------------------
     def update_epsilon(self):
@@ -132,10 +133,11 @@ class DQN(OffPolicy):
     def _apply(self):
         opt = self.model.optimizer
         self.ex_online.backward([self.dq], self.grad, batch=self.batch_size)
+        scale = self._reduce_grad(self.grad)
         call('xa_adam_step_bump', opt.iterations.data_ptr(), stream())
         kernels.clip_adam(self.model.theta, opt.m, opt.v, self.grad, opt.iterations,
                           opt.learning_rate, opt.beta_1, opt.beta_2, opt.epsilon,
-                          clip_norm=0.0, workspace=self.adam_ws)
+                          clip_norm=0.0, grad_scale=scale, workspace=self.adam_ws)
 
     def get_targets(self, states, actions, rewards, dones, new_states):
         """TD targets y [B, A] (dqn/agent.py:118-156)."""

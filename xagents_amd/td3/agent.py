@@ -55,6 +55,7 @@ class TD3(DDPG):
         self.ex_target_critic2 = LayerExecutor(self.target_critic2, B)
         self.g_critic2 = torch.zeros(self.critic2.n_params, dtype=torch.float32,
                                      device=self.device)
+        self._sync_params(self.critic2, self.target_critic2)
 
     def get_step_actions(self):
         """actor(s), no exploration noise (td3/agent.py:57-64)."""
