@@ -715,15 +715,30 @@ __global__ __launch_bounds__(256) void sumsq_partial_kernel(const float* __restr
   if (threadIdx.x == 0) ws[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
+// fixed-order sum of the sumsq partials into ws[n] (one workgroup)
+__global__ __launch_bounds__(256) void sumsq_finalize_kernel(double* ws, int n) {
+  __shared__ double red[4];
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) acc += ws[i];
+  acc = xa_wave_sum_f64(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) ws[n] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// need_norm == 0: no clipping and no norm output (DQN / DDPG / TD3 minimize). Otherwise
+// the global norm comes from `total` (large P: sumsq partials + finalize) or, for small P,
+// from a full sum in every workgroup. Grid-stride over the parameters.
 __global__ __launch_bounds__(256) void clip_adam_kernel(
     const float* theta, const float* m, const float* v, const float* __restrict__ g, int P,
     float grad_scale, float clip, float lr, float b1, float b2, float eps, const int* step,
-    const double* ws, int n_ws, float* gnorm_out, float* theta_o, float* m_o, float* v_o) {
+    int need_norm, const double* total_p, float* gnorm_out, float* theta_o, float* m_o,
+    float* v_o) {
   __shared__ double red[4];
   __shared__ float s_alpha;
   double total = 0.0;
   if (threadIdx.x == 0) s_alpha = adam_alpha(lr, b1, b2, step ? *step : 1);
-  if (ws == nullptr) {
+  if (need_norm && total_p == nullptr) {
     double acc = 0.0;
     for (int i = threadIdx.x; i < P; i += blockDim.x) {
       const float x = g[i] * grad_scale;
@@ -731,21 +746,19 @@ __global__ __launch_bounds__(256) void clip_adam_kernel(
     }
     acc = xa_wave_sum_f64(acc);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
-    __syncthreads();
-    total = (red[0] + red[1]) + (red[2] + red[3]);
-  } else {
-    __syncthreads();
-    for (int i = 0; i < n_ws; ++i) total += ws[i];
   }
+  __syncthreads();
+  if (need_norm) total = total_p ? *total_p : (red[0] + red[1]) + (red[2] + red[3]);
   if (blockIdx.x == 0 && threadIdx.x == 0 && gnorm_out) gnorm_out[0] = (float)sqrt(total);
-  const float sc = clip_scale(total, clip);
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= P) return;
-  float th = theta[i], mm = m[i], vv = v[i];
-  adam_elem((g[i] * grad_scale) * sc, th, mm, vv, s_alpha, 1.0f - b1, 1.0f - b2, eps);
-  theta_o[i] = th;
-  m_o[i] = mm;
-  v_o[i] = vv;
+  const float sc = need_norm ? clip_scale(total, clip) : 1.0f;
+  const float alpha = s_alpha, omb1 = 1.0f - b1, omb2 = 1.0f - b2;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < P; i += gridDim.x * blockDim.x) {
+    float th = theta[i], mm = m[i], vv = v[i];
+    adam_elem((g[i] * grad_scale) * sc, th, mm, vv, alpha, omb1, omb2, eps);
+    theta_o[i] = th;
+    m_o[i] = mm;
+    v_o[i] = vv;
+  }
 }
 
 template <int OBS, int A>
@@ -830,20 +843,23 @@ extern "C" int xa_clip_adam(float* theta, float* adam_m, float* adam_v, const fl
                             float* v_out, void* stream) {
   XA_CHECK_ARG(theta && adam_m && adam_v && grad && n_params > 0, "xa_clip_adam: bad arguments");
   hipStream_t s = (hipStream_t)stream;
-  const double* ws = nullptr;
-  int n_ws = 0;
-  if (n_params > kSmallP) {
+  const int need_norm = clip_norm > 0.0f || gnorm_out != nullptr;
+  const double* total = nullptr;
+  if (need_norm && n_params > kSmallP) {
     XA_CHECK_ARG(workspace != nullptr, "xa_clip_adam: n_params > %d needs a workspace", kSmallP);
-    n_ws = min(1024, (n_params + 4095) / 4096);
+    const int n_ws = min(1023, (n_params + 4095) / 4096);
     hipLaunchKernelGGL(sumsq_partial_kernel, dim3(n_ws), dim3(256), 0, s, grad, n_params,
                        grad_scale, workspace);
     XA_CHECK_LAUNCH("xa_clip_adam(sumsq)");
-    ws = workspace;
+    hipLaunchKernelGGL(sumsq_finalize_kernel, dim3(1), dim3(256), 0, s, workspace, n_ws);
+    XA_CHECK_LAUNCH("xa_clip_adam(sumsq finalize)");
+    total = workspace + n_ws;
   }
-  hipLaunchKernelGGL(clip_adam_kernel, dim3((n_params + 255) / 256), dim3(256), 0, s, theta,
-                     adam_m, adam_v, grad, n_params, grad_scale, clip_norm, lr, beta1, beta2, eps,
-                     adam_step, ws, n_ws, gnorm_out, theta_out ? theta_out : theta,
-                     m_out ? m_out : adam_m, v_out ? v_out : adam_v);
+  const int blocks = min((n_params + 255) / 256, 8192);
+  hipLaunchKernelGGL(clip_adam_kernel, dim3(blocks), dim3(256), 0, s, theta, adam_m, adam_v, grad,
+                     n_params, grad_scale, clip_norm, lr, beta1, beta2, eps, adam_step, need_norm,
+                     total, gnorm_out, theta_out ? theta_out : theta, m_out ? m_out : adam_m,
+                     v_out ? v_out : adam_v);
   XA_CHECK_LAUNCH("xa_clip_adam");
   return 0;
 }

@@ -33,8 +33,13 @@ XA_DEV f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-XA_DEV int64_t grouped(int64_t i, int64_t p, int64_t r, int64_t s) {
-  return p == 1 ? i * r : (i / p) * r + (i % p) * s;
+// (i / p) r + (i % p) s with 32-bit division (indices and group sizes fit in 31 bits;
+// a 64-bit divide in the loader costs more than the MFMA work of a K step)
+XA_DEV int64_t grouped(int i, int p, int64_t r, int64_t s) {
+  if (p == 1) return (int64_t)i * r;
+  const unsigned q = (unsigned)i / (unsigned)p;
+  const unsigned m = (unsigned)i - q * (unsigned)p;
+  return (int64_t)q * r + (int64_t)m * s;
 }
 
 XA_DEV float epilogue(float v, int n, const XaGemmArgs& g) {
@@ -75,7 +80,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(XaGemmArgs g) {
   for (int i = 0; i < 4; ++i) {
     const int m = m0 + a_m + (A_KMAJOR ? 0 : i);
     a_ok[i] = m < g.M;
-    a_row[i] = a_ok[i] ? grouped(m, g.a_pm, g.a_rm, g.a_sm) : 0;
+    a_row[i] = a_ok[i] ? grouped(m, (int)g.a_pm, g.a_rm, g.a_sm) : 0;
   }
   const float* af = static_cast<const float*>(g.a);
   const uint8_t* au = static_cast<const uint8_t*>(g.a);
@@ -91,7 +96,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(XaGemmArgs g) {
         if (g.a == nullptr) {
           v = 1.0f;
         } else {
-          const int64_t off = a_row[ai] + grouped(k, g.a_pk, g.a_rk, g.a_sk);
+          const int64_t off = a_row[ai] + grouped(k, (int)g.a_pk, g.a_rk, g.a_sk);
           v = A_U8 ? (float)au[off] / 255.0f : af[off];
         }
       }
@@ -168,11 +173,13 @@ __global__ __launch_bounds__(256) void gemm_kernel(XaGemmArgs g) {
 // fixed-order sum of the split partials + epilogue
 __global__ __launch_bounds__(256) void gemm_split_reduce_kernel(XaGemmArgs g, int splits) {
   const int64_t total = (int64_t)g.M * g.N;
+  const unsigned N = (unsigned)g.N;
   for (int64_t e = blockIdx.x * 256ll + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
     float s = 0.0f;
     for (int z = 0; z < splits; ++z) s = s + g.partials[(int64_t)z * total + e];
-    const int m = (int)(e / g.N), n = (int)(e % g.N);
-    store_c(epilogue(s, n, g), m, n, g);
+    // M * N < 2^31 is checked on the host
+    const unsigned m = (unsigned)e / N, n = (unsigned)e - m * N;
+    store_c(epilogue(s, (int)n, g), (int)m, (int)n, g);
   }
 }
 
@@ -184,11 +191,11 @@ void launch(const XaGemmArgs& g, dim3 grid, hipStream_t s) {
 }  // namespace
 
 extern "C" int xa_gemm_splits(int M, int N, int K) {
-  // enough workgroups to cover the chip (>= 512), each split >= 8 K tiles
+  // enough workgroups to cover the chip (>= 1024), each split >= 8 K tiles
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   const int kt = (K + BK - 1) / BK;
   int s = 1;
-  while (tiles * s < 512 && kt / (s * 2) >= 8 && s < 256) s *= 2;
+  while (tiles * s < 1024 && kt / (s * 2) >= 8 && s < 4096) s *= 2;
   return s;
 }
 
@@ -206,6 +213,8 @@ extern "C" int xa_gemm(const XaGemmArgs* p, void* stream) {
   XA_CHECK_ARG(g.splits >= 1 && g.splits <= 4096, "xa_gemm: splits must be in [1, 4096]");
   XA_CHECK_ARG(g.splits == 1 || g.partials, "xa_gemm: splits > 1 needs partials");
   XA_CHECK_ARG(!g.gate || g.ld_gate > 0, "xa_gemm: gate needs ld_gate");
+  XA_CHECK_ARG((int64_t)g.M * g.N < (1ll << 31) && g.a_pm < (1ll << 31) && g.a_pk < (1ll << 31),
+               "xa_gemm: M * N and group sizes must stay below 2^31");
   hipStream_t s = (hipStream_t)stream;
   dim3 grid((g.M + BM - 1) / BM, (g.N + BN - 1) / BN, g.splits);
   const bool ak = g.a_pk == 1 && g.a_rk == 1;

@@ -21,10 +21,13 @@ __global__ __launch_bounds__(256) void col2im_kernel(const float* __restrict__ d
                                                      float* __restrict__ out) {
   const int64_t total = (int64_t)rows * W_in * C;
   for (int64_t e = blockIdx.x * 256ll + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
-    const int c = (int)(e % C);
-    const int64_t rq = e / C;
-    const int q = (int)(rq % W_in);
-    const int64_t row = rq / W_in;
+    // 32-bit index arithmetic (rows * W_in * C < 2^31, checked on the host)
+    const unsigned ue = (unsigned)e;
+    const unsigned rq = ue / (unsigned)C;
+    const int c = (int)(ue - rq * (unsigned)C);
+    const unsigned row_u = rq / (unsigned)W_in;
+    const int q = (int)(rq - row_u * (unsigned)W_in);
+    const int64_t row = row_u;
     float acc = 0.0f;
     for (int t = 0; t < k; ++t) {
       const int d = q - t;
@@ -323,6 +326,7 @@ extern "C" int xa_conv1d_input_grad(const float* dcol, int rows, int positions, 
                    channels > 0 && width_in >= (positions - 1) * stride + kernel,
                "xa_conv1d_input_grad: bad arguments");
   const int64_t total = (int64_t)rows * width_in * channels;
+  XA_CHECK_ARG(total < (1ll << 31), "xa_conv1d_input_grad: rows * width * channels >= 2^31");
   hipLaunchKernelGGL(col2im_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream,
                      dcol, rows, positions, kernel, stride, channels, width_in, gate, dinput);
   XA_CHECK_LAUNCH("xa_conv1d_input_grad");

@@ -170,13 +170,14 @@ class LayerExecutor:
         return [self.outs[i] for i in self.model.outputs]
 
     # ---- backward ----------------------------------------------------------------
-    def backward(self, d_outputs, grad, batch=None, dinput=None):
+    def backward(self, d_outputs, grad, batch=None, dinput=None, accumulate=False):
         """d_outputs: gradients w.r.t. the output layers (model.outputs order, [b, n]).
         Writes the flat parameter gradient into `grad` (Keras variable order; None skips
         the parameter gradients) and, if given, d(loss)/d(input) into `dinput` [b, in]
         (dense input layers). `batch` (<= B) back-propagates only the first rows of the
         last forward (samples are independent rows, so a prefix of every buffer is a
-        smaller batch)."""
+        smaller batch). `accumulate` adds the parameter gradient to `grad` (chunked
+        minibatches)."""
         Bb = batch or self.B
         assert Bb <= self.B
         tp = self.model.theta.data_ptr()
@@ -222,9 +223,10 @@ class LayerExecutor:
                     # dW = X^T dZ ; db = 1^T dZ
                     gemm(n_in, n_out, Bb, src.data_ptr(), d.data_ptr(), gp + 4 * w0,
                          a_u8=src_u8, a_m=(1, 1, 0), a_k=(1, n_in, 0), b_ks=n_out, b_ns=1,
-                         ldc=n_out, workspace=self.workspace)
+                         ldc=n_out, beta=accumulate, workspace=self.workspace)
                     gemm(1, n_out, Bb, None, d.data_ptr(), gp + 4 * b0, a_m=(1, 0, 0),
-                         a_k=(1, 0, 0), b_ks=n_out, b_ns=1, ldc=n_out, workspace=self.workspace)
+                         a_k=(1, 0, 0), b_ks=n_out, b_ns=1, ldc=n_out, beta=accumulate,
+                         workspace=self.workspace)
                 if j == -1 and dinput is not None:
                     gemm(Bb, n_in, n_out, d.data_ptr(), tp + 4 * w0, dinput.data_ptr(),
                          a_m=(1, n_out, 0), b_ks=1, b_ns=n_out, ldc=n_in,
@@ -242,9 +244,10 @@ class LayerExecutor:
                 if gp is not None:
                     gemm(k * C, F, rows * P, src.data_ptr(), d.data_ptr(), gp + 4 * w0,
                          a_u8=src_u8, a_m=(1, 1, 0), a_k=(P, Win * C, s * C), b_ks=F, b_ns=1,
-                         ldc=F, workspace=self.workspace)
+                         ldc=F, beta=accumulate, workspace=self.workspace)
                     gemm(1, F, rows * P, None, d.data_ptr(), gp + 4 * b0, a_m=(1, 0, 0),
-                         a_k=(1, 0, 0), b_ks=F, b_ns=1, ldc=F, workspace=self.workspace)
+                         a_k=(1, 0, 0), b_ks=F, b_ns=1, ldc=F, beta=accumulate,
+                         workspace=self.workspace)
                 if j != -1:
                     assert not written[j], 'a conv input with two consumers is not supported'
                     gemm(rows * P, k * C, F, d.data_ptr(), tp + 4 * w0, self.dcol.data_ptr(),

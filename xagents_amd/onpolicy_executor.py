@@ -30,6 +30,8 @@ from xagents_amd.layers import LayerExecutor
 class ExecutorActorCritic:
     """Mixin for A2C / PPO when the model is not the fused actor-critic MLP."""
 
+    CHUNK = 4096
+
     def _setup_executor_path(self):
         env = self.envs
         if not hasattr(env, 'fill_step_args'):
@@ -61,7 +63,17 @@ class ExecutorActorCritic:
         mb = getattr(self, 'mini_batch_size', B)
         self.mb = mb
         self.n_mb = (B + mb - 1) // mb
-        self.ex_upd = LayerExecutor(self.model, mb)
+        # the update minibatch runs in chunks of <= 4096 samples (each chunk keeps its own
+        # activations; GEMM index ranges stay 32-bit), gradients accumulate over chunks
+        self.chunk = min(mb, self.CHUNK)
+        self.ex_chunks = [LayerExecutor(self.model, min(self.chunk, mb - c0))
+                          for c0 in range(0, mb, self.chunk)]
+        ex0 = self.ex_chunks[0]
+        for ex in self.ex_chunks[1:]:  # backward buffers are used one chunk at a time
+            ex.workspace, ex.dcol = ex0.workspace, ex0.dcol
+            ex.douts = [None if d is None else d0[:ex.B] for d, d0 in zip(ex.douts, ex0.douts)]
+        self.mb_logits = torch.zeros(mb, self.n_actions, **f32)
+        self.mb_value = torch.zeros(mb, 1, **f32)
         self.mb_obs = torch.zeros((mb,) + env.obs_shape, dtype=env.state.dtype, device=dev)
         self.mb_act = torch.zeros(mb, dtype=torch.int32, device=dev)
         self.mb_logp, self.mb_val = torch.zeros(mb, **f32), torch.zeros(mb, **f32)
@@ -132,7 +144,18 @@ class ExecutorActorCritic:
             call('xa_ring_gather', src.data_ptr(), dst.data_ptr(), sf, n, 4, stream())
 
     def _minibatch_step(self, n):
-        logits, value = self.ex_upd.forward(self.mb_obs)
+        A = self.n_actions
+        for j, ex in enumerate(self.ex_chunks):
+            c0 = j * self.chunk
+            if c0 >= n:
+                break
+            lg, vl = ex.forward(self.mb_obs[c0:c0 + ex.B])
+            rows = min(ex.B, n - c0)
+            call('xa_copy_block', lg.data_ptr(), A, self.mb_logits.data_ptr() + 4 * c0 * A, A,
+                 rows, A, stream())
+            call('xa_copy_block', vl.data_ptr(), 1, self.mb_value.data_ptr() + 4 * c0, 1, rows,
+                 1, stream())
+        logits, value = self.mb_logits, self.mb_value
         h = XaHeadGradArgs()
         h.n, h.n_actions, h.loss_kind = n, self.n_actions, self.loss_kind
         h.logits, h.ld_logits = logits.data_ptr(), self.n_actions
@@ -152,7 +175,13 @@ class ExecutorActorCritic:
             torch.distributed.all_reduce(self.adv_sums)
             h.stats_mode = 2
         call('xa_ac_head_grad', ctypes.byref(h), stream())
-        self.ex_upd.backward([self.dlogits[:n], self.dvalue[:n]], self.grad, batch=n)
+        for j, ex in enumerate(self.ex_chunks):
+            c0 = j * self.chunk
+            if c0 >= n:
+                break
+            rows = min(ex.B, n - c0)
+            ex.backward([self.dlogits[c0:c0 + rows], self.dvalue[c0:c0 + rows]], self.grad,
+                        batch=rows, accumulate=j > 0)
         if self.distributed:
             torch.distributed.all_reduce(self.grad)
         opt = self.model.optimizer
