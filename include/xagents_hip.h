@@ -291,6 +291,7 @@ typedef struct XaGemmArgs {
   const float* gate;
   int64_t ld_gate;
   int beta;
+  int force_small; /* 1: always the 64 x 64 small-tile kernel (tests) */
 } XaGemmArgs;
 
 int xa_gemm(const XaGemmArgs* args, void* stream);

@@ -20,8 +20,14 @@ def _close(got, ref, rtol=1e-4):
     assert err < rtol, f'max error {err:.3g} (relative to max |ref| = {scale:.3g})'
 
 
-@pytest.mark.parametrize('M,N,K,splits', [(37, 50, 29, 1), (64, 512, 3000, 8), (130, 70, 1000, 4)])
-def test_gemm_plain_bias_relu_split(device, M, N, K, splits):
+# shapes reaching each kernel: small 64x64, square 128x128, tall 256x64, wide 64x256
+_SHAPES = [(37, 50, 29, 1), (64, 512, 3000, 8), (130, 70, 1000, 4), (300, 257, 400, 1),
+           (1000, 40, 333, 2), (50, 700, 290, 3), (40, 50, 20000, 16), (200, 64, 17001, 1)]
+
+
+@pytest.mark.parametrize('small', [False, True])
+@pytest.mark.parametrize('M,N,K,splits', _SHAPES)
+def test_gemm_plain_bias_relu_split(device, M, N, K, splits, small):
     from xagents_amd.layers import gemm
     from xagents_amd._lib import XA_ACT_RELU
     rng = np.random.default_rng(M + N + K)
@@ -32,15 +38,16 @@ def test_gemm_plain_bias_relu_split(device, M, N, K, splits):
     C = torch.empty(M, N, device=device)
     ws = torch.empty(splits * M * N + 1, device=device)
     gemm(M, N, K, ta.data_ptr(), tb.data_ptr(), C.data_ptr(), a_m=(1, K, 0), b_ks=N, b_ns=1,
-         ldc=N, bias=tbias.data_ptr(), act=XA_ACT_RELU, workspace=ws, splits=splits)
+         ldc=N, bias=tbias.data_ptr(), act=XA_ACT_RELU, workspace=ws, splits=splits,
+         force_small=small)
     ref = np.maximum(A.astype(np.float64) @ B + b, 0)
     _close(C.cpu().numpy(), ref)
 
 
-def test_gemm_transposes_gate_beta_u8(device):
+@pytest.mark.parametrize('M,N,K', [(70, 45, 33), (260, 300, 77), (700, 60, 45), (60, 400, 50)])
+def test_gemm_transposes_gate_beta_u8(device, M, N, K):
     from xagents_amd.layers import gemm
     rng = np.random.default_rng(3)
-    M, N, K = 70, 45, 33
     At = rng.normal(size=(K, M)).astype(np.float32)      # A = At^T  (m-major loader)
     Bt = rng.normal(size=(N, K)).astype(np.float32)      # B = Bt^T  (k-major loader)
     gate = rng.normal(size=(M, N)).astype(np.float32)
@@ -53,7 +60,7 @@ def test_gemm_transposes_gate_beta_u8(device):
     _close(C.cpu().numpy(), ref)
     # uint8 A scaled by 1/255 (base.py:505-506), implicit Conv1D im2col: rows of W=20,
     # C=3 channels, kernel 4, stride 2 -> P = 9 positions
-    rows, W, Cc, k, s = 11, 20, 3, 4, 2
+    rows, W, Cc, k, s = 11 + M // 10, 20, 3, 4, 2
     P = (W - k) // s + 1
     x = rng.integers(0, 256, size=(rows, W, Cc), dtype=np.uint8)
     Wt = rng.normal(size=(k * Cc, 8)).astype(np.float32)
@@ -111,3 +118,18 @@ def test_layer_executor_forward_backward_vs_f64(device, cfg, units, shape, B):
         for off, s in sl:
             n = int(np.prod(s))
             _close(g[off:off + n], ref_g[off:off + n], rtol=2e-4)
+
+
+@pytest.mark.parametrize('K,splits', [(100, 1), (50000, 64)])
+def test_gemm_column_sums(device, K, splits):
+    """A = NULL (ones) with M = 1: bias gradients (column sums of B)."""
+    from xagents_amd.layers import gemm
+    rng = np.random.default_rng(K)
+    N = 70
+    B = rng.normal(size=(K, N)).astype(np.float32)
+    tb = torch.from_numpy(B).to(device)
+    C = torch.zeros(1, N, device=device)
+    ws = torch.empty(splits * N + 1, device=device)
+    gemm(1, N, K, None, tb.data_ptr(), C.data_ptr(), b_ks=N, b_ns=1, ldc=N, workspace=ws,
+         splits=splits)
+    _close(C.cpu().numpy()[0], B.astype(np.float64).sum(0))

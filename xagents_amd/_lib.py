@@ -149,6 +149,7 @@ class XaGemmArgs(Structure):
         ('gate', c_void_p),
         ('ld_gate', c_int64),
         ('beta', c_int),
+        ('force_small', c_int),
     ]
 
 

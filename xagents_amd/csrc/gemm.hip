@@ -170,6 +170,260 @@ __global__ __launch_bounds__(256) void gemm_kernel(XaGemmArgs g) {
       }
 }
 
+// ---------------------------------------------------------------------------
+// Large-tile path: v_mfma_f32_32x32x2_f32 (A[i = l&31][k = l>>5], B[k = l>>5][j = l&31];
+// D col = l&31, row = (r&3) + 8 (r>>2) + 4 (l>>5)), 4 waves of 64 x 64 (2 x 2 tiles of
+// 32 x 32, 4 independent accumulators per wave), block (64 WM) x (64 WN) with
+// WM WN = 4, K in steps of 32 through double-buffered LDS.
+// ---------------------------------------------------------------------------
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+constexpr int TBK = 32;
+
+XA_DEV f32x16 mfma32(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+template <int WM, int WN, bool A_KMAJOR, bool B_NMAJOR, bool A_U8>
+__global__ __launch_bounds__(256) void gemm_tile_kernel(XaGemmArgs g) {
+  constexpr int TBM = 64 * WM, TBN = 64 * WN, TLA = TBM + 4, TLB = TBN + 4;
+  constexpr int EA = TBM * TBK / 256, EB = TBN * TBK / 256;  // elements per thread
+  __shared__ __attribute__((aligned(16))) float As[2][TBK * TLA];
+  __shared__ __attribute__((aligned(16))) float Bs[2][TBK * TLB];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w / WN, wn = w % WN;
+  const int m0 = blockIdx.x * TBM, n0 = blockIdx.y * TBN;
+  const int tiles_k = (g.K + TBK - 1) / TBK;
+  const int per = (tiles_k + (int)gridDim.z - 1) / (int)gridDim.z;
+  const int k_begin = blockIdx.z * per * TBK;
+  const int k_end = min(g.K, k_begin + per * TBK);
+
+  // A slots: k-major -> rows (tid >> 3) + 32 r, k quad (tid & 7);
+  //          m-major -> m quad (tid % (TBM/4)) * 4, k rows tid / (TBM/4) + (1024/TBM) r
+  constexpr int AQ = TBM / 4, AKR = 256 / AQ;  // m-major: threads per k row, k rows per pass
+  constexpr int NA = A_KMAJOR ? TBM / 32 : 4;   // distinct m per thread
+  int64_t a_row[NA];
+  bool a_ok[NA];
+#pragma unroll
+  for (int r = 0; r < NA; ++r) {
+    const int m = m0 + (A_KMAJOR ? (tid >> 3) + 32 * r : (tid % AQ) * 4 + r);
+    a_ok[r] = m < g.M;
+    a_row[r] = a_ok[r] ? grouped(m, (int)g.a_pm, g.a_rm, g.a_sm) : 0;
+  }
+  constexpr int BQ = TBN / 4, BKR = 256 / BQ;
+  const float* af = static_cast<const float*>(g.a);
+  const uint8_t* au = static_cast<const uint8_t*>(g.a);
+  float ra[EA], rb[EB];
+
+  auto load = [&](int kt) {
+#pragma unroll
+    for (int e = 0; e < EA; ++e) {
+      int mi, k;
+      if (A_KMAJOR) {
+        mi = e >> 2;
+        k = kt + (tid & 7) * 4 + (e & 3);
+      } else {
+        mi = e & 3;
+        k = kt + tid / AQ + AKR * (e >> 2);
+      }
+      float v = 0.0f;
+      if (a_ok[mi] && k < k_end) {
+        if (g.a == nullptr) {
+          v = 1.0f;
+        } else {
+          const int64_t off = a_row[mi] + grouped(k, (int)g.a_pk, g.a_rk, g.a_sk);
+          v = A_U8 ? (float)au[off] / 255.0f : af[off];
+        }
+      }
+      ra[e] = v;
+    }
+#pragma unroll
+    for (int e = 0; e < EB; ++e) {
+      int n, k;
+      if (B_NMAJOR) {
+        n = n0 + (tid % BQ) * 4 + (e & 3);
+        k = kt + tid / BQ + BKR * (e >> 2);
+      } else {
+        n = n0 + (tid >> 3) + 32 * (e >> 2);
+        k = kt + (tid & 7) * 4 + (e & 3);
+      }
+      rb[e] = (k < k_end && n < g.N) ? g.b[(int64_t)k * g.b_ks + (int64_t)n * g.b_ns] : 0.0f;
+    }
+  };
+  auto stash = [&](int buf) {
+#pragma unroll
+    for (int e = 0; e < EA; ++e) {
+      int ml, kl;
+      if (A_KMAJOR) {
+        ml = (tid >> 3) + 32 * (e >> 2);
+        kl = (tid & 7) * 4 + (e & 3);
+      } else {
+        ml = (tid % AQ) * 4 + (e & 3);
+        kl = tid / AQ + AKR * (e >> 2);
+      }
+      As[buf][kl * TLA + ml] = ra[e];
+    }
+#pragma unroll
+    for (int e = 0; e < EB; ++e) {
+      int nl, kl;
+      if (B_NMAJOR) {
+        nl = (tid % BQ) * 4 + (e & 3);
+        kl = tid / BQ + BKR * (e >> 2);
+      } else {
+        nl = (tid >> 3) + 32 * (e >> 2);
+        kl = (tid & 7) * 4 + (e & 3);
+      }
+      Bs[buf][kl * TLB + nl] = rb[e];
+    }
+  };
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+
+  if (k_begin < k_end) {
+    load(k_begin);
+    stash(0);
+    __syncthreads();
+    int buf = 0;
+    for (int kt = k_begin; kt < k_end; kt += TBK) {
+      const bool more = kt + TBK < k_end;
+      if (more) load(kt + TBK);
+      const float* as = As[buf] + wm * 64 + (lane & 31);
+      const float* bs = Bs[buf] + wn * 64 + (lane & 31);
+#pragma unroll
+      for (int s2 = 0; s2 < TBK / 2; ++s2) {
+        const int kk = 2 * s2 + (lane >> 5);
+        const float a0 = as[kk * TLA], a1 = as[kk * TLA + 32];
+        const float b0 = bs[kk * TLB], b1 = bs[kk * TLB + 32];
+        acc[0][0] = mfma32(a0, b0, acc[0][0]);
+        acc[0][1] = mfma32(a0, b1, acc[0][1]);
+        acc[1][0] = mfma32(a1, b0, acc[1][0]);
+        acc[1][1] = mfma32(a1, b1, acc[1][1]);
+      }
+      if (more) stash(buf ^ 1);
+      __syncthreads();
+      buf ^= 1;
+    }
+  }
+
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * 64 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int n = n0 + wn * 64 + 32 * j + (lane & 31);
+        if (m >= g.M || n >= g.N) continue;
+        if (gridDim.z > 1) {
+          g.partials[((int64_t)blockIdx.z * g.M + m) * g.N + n] = acc[i][j][r];
+        } else {
+          store_c(epilogue(acc[i][j][r], n, g), m, n, g);
+        }
+      }
+}
+
+// ---------------------------------------------------------------------------
+// Skinny path (weight gradients of the convs: M, N <= 256 / 64, K = rows x positions in
+// the millions): one wave per workgroup owns a 32 x 32 output tile and a K range; the
+// operands come straight from global memory (A rows / B rows are contiguous along m / n
+// for these shapes), 8 K-pairs in flight, one v_mfma_f32_32x32x2_f32 per pair.
+// ---------------------------------------------------------------------------
+template <bool A_U8>
+__global__ __launch_bounds__(64) void gemm_skinny_kernel(XaGemmArgs g) {
+  const int lane = threadIdx.x;
+  const int m0 = blockIdx.x * 32, n0 = blockIdx.y * 32;
+  const int kp = (g.K + 1) / 2;  // K pairs
+  const int per = (kp + (int)gridDim.z - 1) / (int)gridDim.z;
+  const int p_begin = blockIdx.z * per, p_end = min(kp, p_begin + per);
+  const int m = m0 + (lane & 31), n = n0 + (lane & 31), h = lane >> 5;
+  const bool m_ok = m < g.M, n_ok = n < g.N;
+  const int64_t a_m = m_ok ? grouped(m, (int)g.a_pm, g.a_rm, g.a_sm) : 0;
+  const float* af = static_cast<const float*>(g.a);
+  const uint8_t* au = static_cast<const uint8_t*>(g.a);
+  constexpr int U = 16;
+  float av[2][U], bv[2][U];
+  auto fetch = [&](int p0, int slot) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = 2 * (p0 + u) + h;
+      const bool ok = p0 + u < p_end && k < g.K;
+      float a = 0.0f, b = 0.0f;
+      if (ok && m_ok) {
+        if (g.a == nullptr) {
+          a = 1.0f;
+        } else {
+          const int64_t off = a_m + grouped(k, (int)g.a_pk, g.a_rk, g.a_sk);
+          a = A_U8 ? (float)au[off] / 255.0f : af[off];
+        }
+      }
+      if (ok && n_ok) b = g.b[(int64_t)k * g.b_ks + (int64_t)n * g.b_ns];
+      av[slot][u] = a;
+      bv[slot][u] = b;
+    }
+  };
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+  // two register stages (compile-time slots): the next 16 K-pairs are in flight while
+  // the current ones feed the MFMAs
+  if (p_begin < p_end) fetch(p_begin, 0);
+  for (int p0 = p_begin; p0 < p_end; p0 += 2 * U) {
+    if (p0 + U < p_end) fetch(p0 + U, 1);
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc = mfma32(av[0][u], bv[0][u], acc);
+    if (p0 + U >= p_end) break;
+    if (p0 + 2 * U < p_end) fetch(p0 + 2 * U, 0);
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc = mfma32(av[1][u], bv[1][u], acc);
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int mm = m0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+    const int nn = n0 + (lane & 31);
+    if (mm >= g.M || nn >= g.N) continue;
+    if (gridDim.z > 1) {
+      g.partials[((int64_t)blockIdx.z * g.M + mm) * g.N + nn] = acc[r];
+    } else {
+      store_c(epilogue(acc[r], nn, g), mm, nn, g);
+    }
+  }
+}
+
+// column sums of B (A == NULL, M == 1: bias gradients): rows split over workgroups, each
+// workgroup 4 waves x 64 columns, partial rows summed in fixed order by the split reduce
+__global__ __launch_bounds__(256) void colsum_kernel(XaGemmArgs g) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int n = blockIdx.y * 64 + lane;
+  const int rows_per = (g.K + (int)gridDim.z - 1) / (int)gridDim.z;
+  const int r0 = blockIdx.z * rows_per, r1 = min(g.K, r0 + rows_per);
+  __shared__ float red[4][64];
+  float acc = 0.0f;
+  if (n < g.N) {
+    // 8 independent loads in flight per thread, summed in fixed order
+    int k = r0 + w;
+    for (; k + 28 < r1; k += 32) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = g.b[(int64_t)(k + 4 * u) * g.b_ks + (int64_t)n * g.b_ns];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc = acc + v[u];
+    }
+    for (; k < r1; k += 4) acc = acc + g.b[(int64_t)k * g.b_ks + (int64_t)n * g.b_ns];
+  }
+  red[w][lane] = acc;
+  __syncthreads();
+  if (w == 0 && n < g.N) {
+    const float v = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+    if (gridDim.z > 1) g.partials[(int64_t)blockIdx.z * g.N + n] = v;
+    else store_c(epilogue(v, n, g), 0, n, g);
+  }
+}
+
 // fixed-order sum of the split partials + epilogue
 __global__ __launch_bounds__(256) void gemm_split_reduce_kernel(XaGemmArgs g, int splits) {
   const int64_t total = (int64_t)g.M * g.N;
@@ -188,14 +442,64 @@ void launch(const XaGemmArgs& g, dim3 grid, hipStream_t s) {
   hipLaunchKernelGGL((gemm_kernel<AK, BNM, U8>), grid, dim3(256), 0, s, g);
 }
 
+template <int WM, int WN, bool AK, bool BNM, bool U8>
+void launch_tile(const XaGemmArgs& g, int splits, hipStream_t s) {
+  dim3 grid((g.M + 64 * WM - 1) / (64 * WM), (g.N + 64 * WN - 1) / (64 * WN), splits);
+  hipLaunchKernelGGL((gemm_tile_kernel<WM, WN, AK, BNM, U8>), grid, dim3(256), 0, s, g);
+}
+
+template <int WM, int WN>
+void dispatch_tile(const XaGemmArgs& g, bool ak, bool bn, bool u8, hipStream_t s) {
+  if (u8) {
+    if (ak && bn) launch_tile<WM, WN, true, true, true>(g, g.splits, s);
+    else if (ak) launch_tile<WM, WN, true, false, true>(g, g.splits, s);
+    else if (bn) launch_tile<WM, WN, false, true, true>(g, g.splits, s);
+    else launch_tile<WM, WN, false, false, true>(g, g.splits, s);
+  } else {
+    if (ak && bn) launch_tile<WM, WN, true, true, false>(g, g.splits, s);
+    else if (ak) launch_tile<WM, WN, true, false, false>(g, g.splits, s);
+    else if (bn) launch_tile<WM, WN, false, true, false>(g, g.splits, s);
+    else launch_tile<WM, WN, false, false, false>(g, g.splits, s);
+  }
+}
+
+// kernel for a GEMM: 0 = 64 x 64 small-tile, 22 / 41 / 14 = tile kernel (WM, WN),
+// 1 = skinny (one wave per 32 x 32 tile, long K), 2 = column sums (A = ones, M = 1).
+// The tile kernel pays off only with >= 8 K steps of 32 per workgroup.
+int pick_shape(int M, int N, int K, int k_split, bool ones) {
+  if (ones && M == 1) return 2;
+  // conv weight gradients (K = rows x positions): the 64 x 64 kernel with many K splits
+  // (measured best: many small workgroups per CU hide the operand latency); below 64 rows
+  // the one-wave 32 x 32 skinny tile wastes less of the MFMA
+  if (N <= 64 && K >= 16384 && M < 64) return 1;
+  if (k_split < 256) return 0;
+  if (M >= 128 && N >= 128) return 22;
+  if (N <= 64 && M >= 256) return 41;
+  if (M <= 64 && N >= 256) return 14;
+  return 0;
+}
+
+void tile_dims(int shape, int& bm, int& bn) {
+  bm = bn = 64;
+  if (shape == 1) bm = bn = 32;
+  else if (shape == 2) bm = 1, bn = 64;
+  else if (shape > 2) bm = 64 * (shape / 10), bn = 64 * (shape % 10);
+}
+
 }  // namespace
 
 extern "C" int xa_gemm_splits(int M, int N, int K) {
   // enough workgroups to cover the chip (>= 1024), each split >= 8 K tiles
-  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  // without knowing A, assume a real A (the column-sum case is picked in xa_gemm)
+  const int shape = pick_shape(M, N, K, K, false);
+  int bm, bn;
+  tile_dims(shape, bm, bn);
+  const int tiles = ((M + bm - 1) / bm) * ((N + bn - 1) / bn);
   const int kt = (K + BK - 1) / BK;
+  // skinny workgroups are one wave: 4096 of them keep 4 waves per SIMD streaming
+  const int want = shape == 1 ? (M == 1 ? 512 : 4096) : 2048;
   int s = 1;
-  while (tiles * s < 1024 && kt / (s * 2) >= 8 && s < 4096) s *= 2;
+  while (tiles * s < want && kt / (s * 2) >= 8 && s < 4096) s *= 2;
   return s;
 }
 
@@ -220,7 +524,18 @@ extern "C" int xa_gemm(const XaGemmArgs* p, void* stream) {
   const bool ak = g.a_pk == 1 && g.a_rk == 1;
   const bool bn = g.b_ns == 1;
   const bool u8 = g.a_u8 != 0;
-  if (u8) {
+  const int per_split = (g.K + g.splits - 1) / g.splits;
+  const int shape = g.force_small ? 0 : pick_shape(g.M, g.N, g.K, per_split, g.a == nullptr);
+  if (shape == 2) {
+    hipLaunchKernelGGL(colsum_kernel, dim3(1, (g.N + 63) / 64, g.splits), dim3(256), 0, s, g);
+  } else if (shape == 1) {
+    dim3 gs((g.M + 31) / 32, (g.N + 31) / 32, g.splits);
+    if (u8) hipLaunchKernelGGL(gemm_skinny_kernel<true>, gs, dim3(64), 0, s, g);
+    else hipLaunchKernelGGL(gemm_skinny_kernel<false>, gs, dim3(64), 0, s, g);
+  } else if (shape == 22) dispatch_tile<2, 2>(g, ak, bn, u8, s);
+  else if (shape == 41) dispatch_tile<4, 1>(g, ak, bn, u8, s);
+  else if (shape == 14) dispatch_tile<1, 4>(g, ak, bn, u8, s);
+  else if (u8) {
     if (ak && bn) launch<true, true, true>(g, grid, s);
     else if (ak) launch<true, false, true>(g, grid, s);
     else if (bn) launch<false, true, true>(g, grid, s);

@@ -29,7 +29,7 @@ def act_code(name):
 
 def gemm(M, N, K, a, b, c, *, a_u8=False, a_m=(1, 0, 0), a_k=(1, 1, 0), b_ks, b_ns,
          ldc, bias=None, act=XA_ACT_NONE, gate=None, ld_gate=0, beta=False, workspace=None,
-         splits=None):
+         splits=None, force_small=False):
     """C = [C +] act(A B + bias) * [gate > 0] with A(m, k) = a[f(m) + g(k)],
     f / g given as (group, row stride, in-group stride) triples (gemm.hip)."""
     lib = _lib.load()
@@ -54,6 +54,7 @@ def gemm(M, N, K, a, b, c, *, a_u8=False, a_m=(1, 0, 0), a_k=(1, 1, 0), b_ks, b_
     g.act = act
     g.gate, g.ld_gate = gate, ld_gate
     g.beta = int(beta)
+    g.force_small = int(force_small)
     call('xa_gemm', ctypes_ref(g), stream())
 
 
