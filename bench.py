@@ -81,15 +81,34 @@ def load_traffic(key):
 
 
 def _dist_setup():
+    """One process per GPU over RCCL. Rehearsal knob for a one-GPU box only:
+    XA_BENCH_SHARED_DEVICE=1 puts every rank on cuda:0 with a gloo group (RCCL refuses
+    two ranks on one device); the peer all-reduce then runs between processes that
+    share the GPU, so that run checks the N>1 code path, not its speed."""
     import torch
     import torch.distributed as dist
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local_rank = int(os.environ.get('LOCAL_RANK', '0'))
-    if world > 1:
+    if os.environ.get('XA_BENCH_SHARED_DEVICE') == '1':
+        local_rank = 0
+        if world > 1:
+            torch.cuda.set_device(0)
+            dist.init_process_group('gloo')
+    elif world > 1:
         torch.cuda.set_device(local_rank)
         dist.init_process_group('nccl', device_id=torch.device('cuda', local_rank))
     return world, rank, torch.device('cuda', local_rank)
+
+
+def _max_over_ranks(x, device):
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    if dist.get_backend() == 'gloo':
+        t = t.cpu()
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
 
 
 def _timed(fn, steps, warmup, world):
@@ -110,9 +129,7 @@ def _timed(fn, steps, warmup, world):
         dist.barrier()
     el = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device='cuda')
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+        el = _max_over_ranks(el, torch.device('cuda', torch.cuda.current_device()))
     return el
 
 
@@ -203,13 +220,7 @@ def main():
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get('WORLD_SIZE', '1'))
-    rank = int(os.environ.get('RANK', '0'))
-    local_rank = int(os.environ.get('LOCAL_RANK', '0'))
-    if world > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local_rank))
-    device = torch.device('cuda', local_rank)
+    world, rank, device = _dist_setup()
 
     from xagents_amd import PPO
     from xagents_amd.envs import ReplayVecEnv, record_cartpole_replay
@@ -225,6 +236,9 @@ def main():
 
     for _ in range(args.warmup):
         agent.train_step()
+    transport = agent.check_peer_all_reduce()
+    if transport == 'rccl' and world > 1:
+        agent.train_step()  # re-capture on RCCL after a peer-path fallback
     torch.cuda.synchronize()
     events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
     if world > 1:
@@ -244,9 +258,7 @@ def main():
         for k, v in agent.timed_train_step().items():
             ktimes[k] += v
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = _max_over_ranks(elapsed, device)
     rollout_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in events]))
     update_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in events]))
     env_steps = args.n_envs * args.n_steps * args.steps * world
@@ -286,7 +298,8 @@ def main():
                 'minibatch_per_gpu': args.n_envs * args.n_steps // 4,
                 'ppo_epochs': 4,
                 'parallelism': f'dp{world}',
-                'graph': not args.no_graph,
+                'graph': bool(agent.use_graph and agent._graph is not None),
+                'allreduce': transport,
             },
             'update_ms': round(update_ms, 4),
             'rollout_ms': round(rollout_ms, 4),
@@ -324,6 +337,8 @@ def main():
             line['cpu_baseline'] = None
         print(json.dumps(line), flush=True)
     if world > 1:
+        if agent.peer is not None:
+            agent.peer.close()
         dist.destroy_process_group()
 
 

@@ -452,6 +452,47 @@ int xa_adam_step_bump(int* adam_step, void* stream);
 int xa_activation_grad(const float* y, const float* dy, int64_t n, int act, float* dz,
                        void* stream);
 
+/*
+ * One-shot peer all-reduce (SUM) of a small buffer over IPC-shared HBM blocks, for the
+ * per-minibatch gradient / advantage-sum exchange of the data-parallel update
+ * (the exchange a multi-worker run of ppo/agent.py:136-137 and the
+ * global advantage statistics of ppo/agent.py:180-183 need). Each rank owns one block
+ * per channel from xa_peer_block_alloc (uncached HBM), exports it with
+ * xa_peer_ipc_handle and opens the peers' with xa_peer_ipc_open; blocks[p] = rank p's
+ * block as mapped in this process. Every rank pushes (word, epoch) 8-byte pairs into
+ * every peer's block and polls its own, then sums in rank order (identical bits on
+ * every rank). `state` = xa_peer_state_words(slot_bytes) u32 of ordinary device
+ * memory, zeroed, private to the rank: state[0] is a sticky error (0 healthy, 1 + p =
+ * timed out waiting for rank p; afterwards calls return the local values without
+ * waiting), the rest are per-chunk epochs. Waits are bounded by timeout_ticks of the
+ * 100 MHz realtime clock. These are the only entry points that allocate: IPC blocks
+ * need the uncached flag.
+ */
+#define XA_PEER_MAX 16
+#define XA_DTYPE_F32 0
+#define XA_DTYPE_F64 1
+
+typedef struct XaPeerAllReduceArgs {
+  void* blocks[XA_PEER_MAX];
+  int rank, world;
+  int dtype;
+  int64_t count;
+  size_t slot_bytes; /* payload capacity per rank the blocks were sized with (multiple of 4096) */
+  const void* src;
+  void* dst;         /* may equal src (in place) */
+  uint32_t* state;
+  uint64_t timeout_ticks;
+} XaPeerAllReduceArgs;
+
+size_t xa_peer_block_bytes(size_t slot_bytes, int world);
+int xa_peer_state_words(size_t slot_bytes);
+int xa_peer_block_alloc(size_t bytes, void** block);
+int xa_peer_block_free(void* block);
+int xa_peer_ipc_handle(void* block, void* handle_out /* 64 bytes */);
+int xa_peer_ipc_open(const void* handle /* 64 bytes */, void** block);
+int xa_peer_ipc_close(void* block);
+int xa_peer_allreduce(const XaPeerAllReduceArgs* args, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

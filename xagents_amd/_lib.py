@@ -183,6 +183,24 @@ class XaHeadGradArgs(Structure):
     ]
 
 
+XA_PEER_MAX = 16
+XA_DTYPE_F32 = 0
+XA_DTYPE_F64 = 1
+
+
+class XaPeerAllReduceArgs(Structure):
+    _fields_ = [
+        ('blocks', c_void_p * XA_PEER_MAX),
+        ('rank', c_int), ('world', c_int),
+        ('dtype', c_int),
+        ('count', c_int64),
+        ('slot_bytes', ctypes.c_size_t),
+        ('src', c_void_p), ('dst', c_void_p),
+        ('state', c_void_p),
+        ('timeout_ticks', c_uint64),
+    ]
+
+
 XA_RING_DEQUE = 0
 XA_RING_RB2 = 1
 XA_ACT_NONE = 0
@@ -256,6 +274,14 @@ _SIGNATURES = {
          c_void_p, c_void_p, c_void_p],
     ),
     'xa_activation_grad': (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p, c_void_p]),
+    'xa_peer_block_bytes': (ctypes.c_size_t, [ctypes.c_size_t, c_int]),
+    'xa_peer_state_words': (c_int, [ctypes.c_size_t]),
+    'xa_peer_block_alloc': (c_int, [ctypes.c_size_t, POINTER(c_void_p)]),
+    'xa_peer_block_free': (c_int, [c_void_p]),
+    'xa_peer_ipc_handle': (c_int, [c_void_p, c_void_p]),
+    'xa_peer_ipc_open': (c_int, [c_void_p, POINTER(c_void_p)]),
+    'xa_peer_ipc_close': (c_int, [c_void_p]),
+    'xa_peer_allreduce': (c_int, [POINTER(XaPeerAllReduceArgs), c_void_p]),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGNATURES)

@@ -14,6 +14,7 @@ import torch
 import torch.distributed as dist
 
 from xagents_amd import kernels
+from xagents_amd.comm import maybe_peer_all_reduce
 from xagents_amd._lib import (XA_RETURNS_GAE, XA_RETURNS_NONE, XA_RETURNS_NSTEP,
                               XaAcGradArgs, XaRolloutArgs, XaShuffle)
 from xagents_amd.base import OnPolicy
@@ -96,6 +97,8 @@ class A2C(ExecutorActorCritic, OnPolicy):
         self.v_alt = torch.zeros(P, **f32)
         if self.distributed:
             dist.broadcast(self.model.theta, 0)
+        # small exchanges (gradient, advantage sums) over IPC peer blocks; RCCL otherwise
+        self.peer = maybe_peer_all_reduce(self.world_size)
         a = XaRolloutArgs()
         a.n_envs, a.n_steps, a.obs_dim, a.n_actions = N, T, obs, self.n_actions
         a.theta = self.model.theta.data_ptr()
@@ -146,8 +149,30 @@ class A2C(ExecutorActorCritic, OnPolicy):
 
     # ---- the fused train step ----------------------------------------------
     def _all_reduce(self, t):
-        if self.distributed:
+        if not self.distributed:
+            return
+        peer = getattr(self, 'peer', None)
+        if peer is not None and peer.fits(t):
+            peer.all_reduce(t)
+        else:
             dist.all_reduce(t)
+
+    def check_peer_all_reduce(self):
+        """After warm-up: if any rank's peer exchange timed out, every rank drops it,
+        re-broadcasts rank 0's parameters and re-captures the step on RCCL.
+        Returns the transport in use."""
+        peer = getattr(self, 'peer', None)
+        if peer is None:
+            return 'rccl' if self.distributed else 'none'
+        if peer.healthy_everywhere():
+            return 'peer-ipc'
+        warnings.warn('peer all-reduce timed out on some rank; falling back to RCCL')
+        self.peer = None
+        opt = self.model.optimizer
+        for t in (self.model.theta, opt.m, opt.v, opt.iterations):
+            dist.broadcast(t, 0)
+        self._graph = None
+        return 'rccl'
 
     def _reduce_gradients(self, partials):
         """Partial rows -> gradient (Adam step += 1) -> [RCCL all-reduce]."""
@@ -215,7 +240,14 @@ class A2C(ExecutorActorCritic, OnPolicy):
 
     def _capture(self):
         """Capture the rollout and the update as two hipGraphs (replayed back to back;
-        two graphs so the update can be timed on its own)."""
+        two graphs so the update can be timed on its own). Data-parallel steps are
+        captured only when every exchange goes through the peer kernel: a torch
+        collective inside a capture (gloo, or RCCL where capture is unsupported)
+        invalidates the capture and the stream, so those steps run eagerly."""
+        if self.distributed and getattr(self, 'peer', None) is None:
+            self.use_graph = False
+            self._graph = None
+            return
         try:
             graphs = []
             for fn in (self._rollout_impl, self._update_impl):
