@@ -238,9 +238,32 @@ int xa_ac_grad_blocks(int mb_size);
 
 /* grad[p] = sum_b partials[b*P + p] (f64 accumulation, fixed order). If adam_step
  * != NULL it is incremented by one (Keras `iterations`): the following optimizer
- * step (xa_ac_grad's pending step or xa_clip_adam) uses the new value as t. */
+ * step (xa_clip_adam or a peer all-reduce tail) uses the new value as t. */
 int xa_grad_reduce(const float* partials, int n_parts, int n_params, float* grad,
                    int* adam_step, void* stream);
+
+/*
+ * Optimizer tail run by the LAST workgroup of a gradient-producing kernel (elected
+ * with the self-resetting `arrivals` counter, a zeroed u32): clip + Keras Adam of the
+ * complete gradient, in place on theta/m/v, with exactly xa_clip_adam's arithmetic
+ * and norm order (so bit-identical to xa_grad_reduce + xa_clip_adam). t = *adam_step,
+ * incremented first when bump != 0. n_params <= XA_ADAM_TAIL_MAX_PARAMS.
+ */
+#define XA_ADAM_TAIL_MAX_PARAMS 65536
+typedef struct XaAdamTail {
+  float* theta;
+  float* m;
+  float* v;
+  int* adam_step;
+  int bump;
+  unsigned* arrivals;
+  float* gnorm_out; /* optional pre-clip global norm */
+  XaAdam adam;
+} XaAdamTail;
+
+/* xa_grad_reduce whose last block applies `tail` (one launch per optimizer step). */
+int xa_grad_reduce_adam(const float* partials, int n_parts, int n_params, float* grad,
+                        const XaAdamTail* tail, void* stream);
 
 /*
  * g' = grad * grad_scale; if clip_norm > 0: tf.clip_by_global_norm(g', clip_norm)
@@ -465,7 +488,8 @@ int xa_activation_grad(const float* y, const float* dy, int64_t n, int act, floa
  * memory, zeroed, private to the rank: state[0] is a sticky error (0 healthy, 1 + p =
  * timed out waiting for rank p; afterwards calls return the local values without
  * waiting), the rest are per-chunk epochs. Waits are bounded by timeout_ticks of the
- * 100 MHz realtime clock. These are the only entry points that allocate: IPC blocks
+ * 100 MHz realtime clock. With has_tail the summed gradient goes straight into the
+ * optimizer (XaAdamTail). These are the only entry points that allocate: IPC blocks
  * need the uncached flag.
  */
 #define XA_PEER_MAX 16
@@ -482,6 +506,8 @@ typedef struct XaPeerAllReduceArgs {
   void* dst;         /* may equal src (in place) */
   uint32_t* state;
   uint64_t timeout_ticks;
+  int has_tail;      /* 1: the last workgroup applies `tail` to dst (f32 gradients) */
+  XaAdamTail tail;
 } XaPeerAllReduceArgs;
 
 size_t xa_peer_block_bytes(size_t slot_bytes, int world);

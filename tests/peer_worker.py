@@ -54,6 +54,29 @@ def main():
     epoch, err = peer.status()
     assert err == 0 and epoch == 36, (epoch, err)  # every call touches chunk 0
 
+    # 1b. with the optimizer tail: == the exchange followed by xa_clip_adam, bit for bit
+    from xagents_amd import kernels
+    P = 4675
+    base = torch.randn(3, P, generator=torch.Generator().manual_seed(99))  # same on all ranks
+    th, m, v = (x.to(dev) for x in (base[0], base[1] * 1e-3, base[2].abs() * 1e-5))
+    th_r, m_r, v_r = th.clone(), m.clone(), v.clone()
+    step = torch.tensor([3], dtype=torch.int32, device=dev)
+    step_r = step.clone()
+    arrivals = torch.zeros(1, dtype=torch.int32, device=dev)
+    tail = kernels.adam_tail(th, m, v, step, arrivals, 7e-4, 0.9, 0.999, 1e-7, clip_norm=0.5,
+                             bump=False)
+    for it in range(3):
+        host = torch.randn(P, generator=gen) * 1e-2
+        want = expected_sum(host, world).to(dev)
+        kernels.clip_adam(th_r, m_r, v_r, want, step_r, 7e-4, 0.9, 0.999, 1e-7, clip_norm=0.5)
+        t = host.to(dev)
+        peer.all_reduce(t, tail=tail)
+        torch.cuda.synchronize()
+        assert torch.equal(t, want), f'rank {rank} tail it {it}: sum mismatch'
+        for a, b, name in ((th, th_r, 'theta'), (m, m_r, 'm'), (v, v_r, 'v')):
+            assert torch.equal(a, b), f'rank {rank} tail it {it}: {name} mismatch'
+        assert int(arrivals.item()) == 0
+
     # 2. captured into a graph, replayed
     buf = torch.zeros(4675, dtype=torch.float32, device=dev)
     side = torch.cuda.Stream()

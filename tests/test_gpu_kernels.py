@@ -340,6 +340,54 @@ def test_errors_are_loud(device):
                             uniforms=torch.zeros(3, device='cuda'))
 
 
+@pytest.mark.parametrize('P,nb,clip', [(4675, 256, 0.5), (999, 37, 0.0), (65536, 3, 0.5)])
+def test_grad_reduce_adam_tail_bit_exact(device, P, nb, clip):
+    """xa_grad_reduce_adam (last block: clip + Keras Adam) == xa_grad_reduce followed by
+    xa_clip_adam, bit for bit, incl. the step counter; repeated launches reuse the
+    self-resetting arrival counter; the C oracle agrees with the result."""
+    rng = np.random.default_rng(P)
+    part = T((rng.standard_normal((nb, P)) * 1e-2).astype(np.float32))
+    theta = rng.standard_normal(P).astype(np.float32)
+    m = (rng.standard_normal(P) * 1e-3).astype(np.float32)
+    v = np.abs(rng.standard_normal(P) * 1e-5).astype(np.float32)
+    ref = [T(theta), T(m), T(v)]
+    got = [T(theta), T(m), T(v)]
+    step_r = torch.tensor([6], dtype=torch.int32, device='cuda')
+    step_g = torch.tensor([6], dtype=torch.int32, device='cuda')
+    arrivals = torch.zeros(1, dtype=torch.int32, device='cuda')
+    grad_r = torch.zeros(P, device='cuda')
+    grad_g = torch.zeros(P, device='cuda')
+    gn = torch.zeros(1, device='cuda')
+    ws = torch.zeros(1024, dtype=torch.float64, device='cuda')
+    cn = clip if clip > 0 else None
+    tail = kernels.adam_tail(*got, step_g, arrivals, 7e-4, 0.9, 0.999, 1e-7, clip_norm=cn,
+                             gnorm_out=gn)
+    host_th, host_m, host_v = theta, m, v
+    for it in range(3):
+        kernels.grad_reduce(part, grad_r, step_r)
+        kernels.clip_adam(*ref, grad_r, step_r, 7e-4, 0.9, 0.999, 1e-7, clip_norm=cn,
+                          workspace=ws)
+        kernels.grad_reduce_adam(part, grad_g, tail)
+        np.testing.assert_array_equal(N(grad_g), N(grad_r))
+        for a, b, name in zip(got, ref, ('theta', 'm', 'v')):
+            np.testing.assert_array_equal(N(a), N(b), err_msg=f'{name} it {it}')
+        assert int(N(step_g)[0]) == int(N(step_r)[0]) == 7 + it
+        assert int(N(arrivals)[0]) == 0
+        host_th, host_m, host_v, gn_r = oracle.clip_adam(host_th, host_m, host_v, N(grad_r),
+                                                         7 + it, 7e-4, 0.9, 0.999, 1e-7, clip)
+        np.testing.assert_array_equal(N(got[0]), host_th)
+        assert abs(float(N(gn)[0]) - gn_r) <= 1e-6 * gn_r
+
+
+def test_grad_reduce_adam_rejects_large_models(device):
+    part = torch.zeros(2, 70000, device='cuda')
+    z = torch.zeros(70000, device='cuda')
+    one = torch.zeros(1, dtype=torch.int32, device='cuda')
+    tail = kernels.adam_tail(z, z, z, one, one, 7e-4, 0.9, 0.999, 1e-7)
+    with pytest.raises(_lib.HipLibraryError, match='n_params'):
+        kernels.grad_reduce_adam(part, z, tail)
+
+
 def test_pending_optimizer_step_in_ac_grad_prologue(device):
     """xa_ac_grad with a pending step == xa_clip_adam (out of place) followed by a plain
     xa_ac_grad: same new theta/m/v (written by block 0) and the same partial gradients."""

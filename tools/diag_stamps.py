@@ -15,7 +15,8 @@ OUT = ROOT / 'build' / 'diag'
 def build():
     OUT.mkdir(parents=True, exist_ok=True)
     objs = []
-    for src in ('xa_runtime', 'returns', 'mlp_rollout', 'ac_update'):
+    # every source (the loader binds every exported symbol); stamps only where XA_STAMP is used
+    for src in sorted(p.stem for p in (ROOT / 'xagents_amd' / 'csrc').glob('*.hip')):
         o = OUT / f'{src}.o'
         subprocess.run(['/opt/rocm/bin/hipcc', '--offload-arch=gfx950', '-O3', '-std=c++17', '-fPIC',
                         '-ffp-contract=off', '-DXA_STAMPS', '-c',

@@ -131,6 +131,20 @@ class XaAcGradArgs(Structure):
     ]
 
 
+class XaAdamTail(Structure):
+    _fields_ = [
+        ('theta', c_void_p), ('m', c_void_p), ('v', c_void_p),
+        ('adam_step', c_void_p),
+        ('bump', c_int),
+        ('arrivals', c_void_p),
+        ('gnorm_out', c_void_p),
+        ('adam', XaAdam),
+    ]
+
+
+XA_ADAM_TAIL_MAX_PARAMS = 65536
+
+
 class XaGemmArgs(Structure):
     _fields_ = [
         ('M', c_int), ('N', c_int), ('K', c_int),
@@ -198,6 +212,8 @@ class XaPeerAllReduceArgs(Structure):
         ('src', c_void_p), ('dst', c_void_p),
         ('state', c_void_p),
         ('timeout_ticks', c_uint64),
+        ('has_tail', c_int),
+        ('tail', XaAdamTail),
     ]
 
 
@@ -232,6 +248,8 @@ _SIGNATURES = {
     'xa_ac_grad': (c_int, [POINTER(XaAcGradArgs), c_void_p]),
     'xa_ac_grad_blocks': (c_int, [c_int]),
     'xa_grad_reduce': (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    'xa_grad_reduce_adam': (c_int, [c_void_p, c_int, c_int, c_void_p, POINTER(XaAdamTail),
+                                    c_void_p]),
     'xa_clip_adam': (
         c_int,
         [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_float, c_float, c_float, c_float,

@@ -91,7 +91,9 @@ class A2C(ExecutorActorCritic, OnPolicy):
         P = self.model.n_params
         self.grad = torch.zeros(P, **f32)
         self.adam_ws = torch.zeros(1024, dtype=torch.float64, device=dev)
-        # second (ping-pong) slot of theta / Adam moments for the fused optimizer step
+        # last-block election counter of the fused optimizer tails (self-resetting)
+        self.arrivals = torch.zeros(1, dtype=torch.int32, device=dev)
+        # second (ping-pong) slot of theta / Adam moments for PPO's prologue optimizer step
         self.theta_alt = torch.zeros(P, **f32)
         self.m_alt = torch.zeros(P, **f32)
         self.v_alt = torch.zeros(P, **f32)
@@ -137,6 +139,7 @@ class A2C(ExecutorActorCritic, OnPolicy):
         return g
 
     def _setup_update(self):
+        self._tail_bump, self._tail_nobump = self._adam_tail(True), self._adam_tail(False)
         B = self.n_envs * self.n_steps
         nb = kernels.ac_grad_blocks(B)
         self.partials = torch.zeros(nb, self.model.n_params, dtype=torch.float32,
@@ -174,8 +177,14 @@ class A2C(ExecutorActorCritic, OnPolicy):
         self._graph = None
         return 'rccl'
 
+    def _adam_tail(self, bump):
+        opt = self.model.optimizer
+        return kernels.adam_tail(self.model.theta, opt.m, opt.v, opt.iterations, self.arrivals,
+                                 opt.learning_rate, opt.beta_1, opt.beta_2, opt.epsilon,
+                                 clip_norm=self.grad_norm, bump=bump)
+
     def _reduce_gradients(self, partials):
-        """Partial rows -> gradient (Adam step += 1) -> [RCCL all-reduce]."""
+        """Partial rows -> gradient (Adam step += 1) -> [all-reduce]."""
         kernels.grad_reduce(partials, self.grad, self.model.optimizer.iterations)
         self._all_reduce(self.grad)
 
@@ -189,8 +198,21 @@ class A2C(ExecutorActorCritic, OnPolicy):
                           workspace=self.adam_ws, out=(self.model.theta, opt.m, opt.v))
 
     def _apply_gradients(self, partials):
-        self._reduce_gradients(partials)
-        self._optimizer_step()
+        """Partial rows -> gradient -> [all-reduce] -> clip + Keras Adam (t += 1) for one
+        optimizer step (A2C, PPO.update_gradients). One launch on one GPU (the reduce's
+        last block runs the optimizer); with data parallelism the peer exchange carries
+        the optimizer tail, RCCL is followed by xa_clip_adam."""
+        opt = self.model.optimizer
+        if not self.distributed:
+            kernels.grad_reduce_adam(partials, self.grad, self._tail_bump)
+            return
+        kernels.grad_reduce(partials, self.grad, opt.iterations)
+        peer = getattr(self, 'peer', None)
+        if peer is not None and peer.fits(self.grad):
+            peer.all_reduce(self.grad, tail=self._tail_nobump)
+        else:
+            dist.all_reduce(self.grad)
+            self._optimizer_step()
 
     def _update(self):
         self._kernel_event('ac_grad', 0, 0)
@@ -263,6 +285,8 @@ class A2C(ExecutorActorCritic, OnPolicy):
 
     def _on_lr_change(self):
         self._graph = None
+        if not self.executor_path:
+            self._setup_update()  # the learning rate is baked into the optimizer tails
 
     def fused_train_step(self, events=None):
         """One train step. `events` = (start, mid, end) torch.cuda.Events recorded

@@ -73,10 +73,15 @@ class PeerAllReduce:
                 and t.numel() * t.element_size() <= self.slot_bytes
                 and t.data_ptr() % 8 == 0 and t.device == self.device)
 
-    def all_reduce(self, t):
+    def all_reduce(self, t, tail=None):
         """In-place SUM of `t` over the group, asynchronous on torch's current stream
-        (capturable into a hipGraph: the epoch lives in device memory)."""
+        (capturable into a hipGraph: the epoch lives in device memory). `tail` (an
+        XaAdamTail, f32 gradients) applies clip + Keras Adam to the sum in the same
+        launch."""
         a = self._args
+        a.has_tail = int(tail is not None)
+        if tail is not None:
+            a.tail = tail
         a.dtype = XA_DTYPE_F64 if t.dtype == torch.float64 else XA_DTYPE_F32
         a.count = t.numel()
         a.src = a.dst = t.data_ptr()

@@ -13,9 +13,12 @@
 //                           gradient; block 0 writes the new theta/m/v (ping-pong)]
 //                           forward, loss, backward of 32-sample tiles -> partial rows
 //   xa_grad_reduce(k)       partial rows -> gradient (f64, fixed order), Adam step += 1
-//   [RCCL all-reduce of the gradient when data-parallel]
+//   [all-reduce of the gradient when data-parallel]
 //   xa_clip_adam            the last minibatch's optimizer step
-// so the optimizer costs no launch of its own inside the minibatch chain.
+// so the optimizer costs no launch of its own inside the minibatch chain. A single
+// optimizer step (A2C) uses xa_grad_reduce_adam instead: the reduce's last block runs
+// clip + Adam (measured: for PPO's 16 chained steps the redundant per-block prologue is
+// faster than a one-block tail, whose loads all miss the freshly invalidated L2).
 //
 // xa_ac_grad tile schedule (256 threads = 4 waves, 32 samples):
 //   H1 = tanh(X W1 + b1)                (VALU, K = obs)
@@ -30,6 +33,7 @@
 #include <math.h>
 
 #include "../../include/xagents_hip.h"
+#include "xa_adam.hpp"
 #include "xa_common.hpp"
 
 namespace {
@@ -95,26 +99,6 @@ XA_DEV int shuffle_index(const XaShuffle& sh, const ShuffleKeys& keys, int epoch
 
 __host__ __device__ inline int stats_chunks(int mb_size) {
   return (mb_size + kStatsChunk - 1) / kStatsChunk;
-}
-
-XA_DEV float clip_scale(double total, float clip) {
-  const float gn = (float)sqrt(total);
-  return clip > 0.0f ? clip * fminf(1.0f / gn, 1.0f / clip) : 1.0f;
-}
-
-// Keras OptimizerV2 Adam step size, computed as training_ops ApplyAdam receives it
-XA_DEV float adam_alpha(float lr, float b1, float b2, int t) {
-  const float b1p = (float)xa_powi((double)b1, t);
-  const float b2p = (float)xa_powi((double)b2, t);
-  return lr * sqrtf(1.0f - b2p) / (1.0f - b1p);
-}
-
-// one ApplyAdam element: m += (g-m)(1-b1); v += (g^2-v)(1-b2); theta -= m*alpha/(sqrt(v)+eps)
-XA_DEV void adam_elem(float g, float& th, float& m, float& v, float alpha, float omb1,
-                      float omb2, float eps) {
-  m = m + (g - m) * omb1;
-  v = v + (g * g - v) * omb2;
-  th = th - (m * alpha) / (sqrtf(v) + eps);
 }
 
 // ---------------------------------------------------------------------------
@@ -662,12 +646,15 @@ __global__ __launch_bounds__(256) void ac_grad_kernel(XaAcGradArgs p) {
 // ---------------------------------------------------------------------------
 // gradient reduction: a block owns 64 consecutive parameters (lane = parameter,
 // so every row load of a wave is one contiguous 256-B segment); its 16 waves take
-// rows w, w + 16, ...; each thread issues 16 row loads before the first use
+// rows w, w + 16, ...; each thread issues 16 row loads before the first use.
+// With a tail, the last block to finish applies clip + Keras Adam to the whole
+// gradient (xa_clip_adam's arithmetic and norm order, so bit-identical to it).
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kRedThreads) void grad_reduce_kernel(const float* __restrict__ part,
                                                                   int nb, int P,
                                                                   float* __restrict__ g,
-                                                                  int* adam_step) {
+                                                                  int* adam_step, XaAdamTail tail,
+                                                                  int has_tail) {
   constexpr int W = kRedThreads / 64;
   __shared__ double red[W][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -693,7 +680,11 @@ __global__ __launch_bounds__(kRedThreads) void grad_reduce_kernel(const float* _
     for (int r = 0; r < W; ++r) s += red[r][lane];
     g[pidx] = (float)s;
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0 && adam_step) adam_step[0] += 1;
+  if (!has_tail) {
+    if (blockIdx.x == 0 && threadIdx.x == 0 && adam_step) adam_step[0] += 1;
+    return;
+  }
+  if (last_block_arrived(tail.arrivals)) adam_tail_apply(tail, g, P);
 }
 
 // ---------------------------------------------------------------------------
@@ -738,17 +729,9 @@ __global__ __launch_bounds__(256) void clip_adam_kernel(
   __shared__ float s_alpha;
   double total = 0.0;
   if (threadIdx.x == 0) s_alpha = adam_alpha(lr, b1, b2, step ? *step : 1);
-  if (need_norm && total_p == nullptr) {
-    double acc = 0.0;
-    for (int i = threadIdx.x; i < P; i += blockDim.x) {
-      const float x = g[i] * grad_scale;
-      acc += (double)x * (double)x;
-    }
-    acc = xa_wave_sum_f64(acc);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
-  }
-  __syncthreads();
-  if (need_norm) total = total_p ? *total_p : (red[0] + red[1]) + (red[2] + red[3]);
+  if (need_norm && total_p == nullptr) total = clip_norm_sumsq(g, P, grad_scale, red);
+  else __syncthreads();
+  if (need_norm && total_p != nullptr) total = *total_p;
   if (blockIdx.x == 0 && threadIdx.x == 0 && gnorm_out) gnorm_out[0] = (float)sqrt(total);
   const float sc = need_norm ? clip_scale(total, clip) : 1.0f;
   const float alpha = s_alpha, omb1 = 1.0f - b1, omb2 = 1.0f - b2;
@@ -830,9 +813,26 @@ extern "C" int xa_grad_reduce(const float* partials, int n_parts, int n_params, 
                               int* adam_step, void* stream) {
   XA_CHECK_ARG(partials && grad && n_parts > 0 && n_params > 0, "xa_grad_reduce: bad arguments");
   const int blocks = (n_params + 63) / 64;
+  XaAdamTail none = {};
   hipLaunchKernelGGL(grad_reduce_kernel, dim3(blocks), dim3(kRedThreads), 0, (hipStream_t)stream,
-                     partials, n_parts, n_params, grad, adam_step);
+                     partials, n_parts, n_params, grad, adam_step, none, 0);
   XA_CHECK_LAUNCH("xa_grad_reduce");
+  return 0;
+}
+
+extern "C" int xa_grad_reduce_adam(const float* partials, int n_parts, int n_params, float* grad,
+                                   const XaAdamTail* tail, void* stream) {
+  XA_CHECK_ARG(partials && grad && n_parts > 0 && n_params > 0 && tail,
+               "xa_grad_reduce_adam: bad arguments");
+  XA_CHECK_ARG(n_params <= XA_ADAM_TAIL_MAX_PARAMS,
+               "xa_grad_reduce_adam: n_params %d > %d (use xa_grad_reduce + xa_clip_adam)",
+               n_params, XA_ADAM_TAIL_MAX_PARAMS);
+  XA_CHECK_ARG(tail->theta && tail->m && tail->v && tail->adam_step && tail->arrivals,
+               "xa_grad_reduce_adam: the tail needs theta, m, v, adam_step and arrivals");
+  const int blocks = (n_params + 63) / 64;
+  hipLaunchKernelGGL(grad_reduce_kernel, dim3(blocks), dim3(kRedThreads), 0, (hipStream_t)stream,
+                     partials, n_parts, n_params, grad, nullptr, *tail, 1);
+  XA_CHECK_LAUNCH("xa_grad_reduce_adam");
   return 0;
 }
 

@@ -24,6 +24,10 @@
 // which needs this rank's epoch-(e + 1) pairs for chunk c, which this rank pushes only
 // after its epoch-e kernel (and its reads of chunk c) finished on its stream.
 //
+// With has_tail, the last workgroup to finish applies clip + Keras Adam to the summed
+// gradient (xa_adam.hpp, same arithmetic as xa_clip_adam), so a data-parallel optimizer
+// step costs no launch beyond the exchange itself.
+//
 // Every wait is bounded (s_memrealtime, 100 MHz): on timeout the kernel records the
 // sticky error and returns the local values; later calls see the error and skip the
 // exchange, so a broken peer path can never hang the GPU. The host reads the error and
@@ -32,6 +36,7 @@
 #include <string.h>
 
 #include "../../include/xagents_hip.h"
+#include "xa_adam.hpp"
 #include "xa_common.hpp"
 
 namespace {
@@ -142,6 +147,11 @@ __global__ __launch_bounds__(kThreads) void peer_allreduce_kernel(XaPeerAllReduc
   }
   __syncthreads();  // every thread has read state[1 + chunk]
   if (threadIdx.x == 0) state[1 + chunk] = ep;
+  // optimizer tail on the summed gradient (f32 only; checked on the host)
+  if constexpr (sizeof(T) == 4) {
+    if (a.has_tail && last_block_arrived(a.tail.arrivals))
+      adam_tail_apply(a.tail, (const float*)a.dst, (int)a.count);
+  }
 }
 
 template <typename T>
@@ -253,6 +263,12 @@ extern "C" int xa_peer_allreduce(const XaPeerAllReduceArgs* a, void* stream) {
                  "xa_peer_allreduce: block of rank %d missing or not 256-byte aligned", p);
   XA_CHECK_ARG(((uintptr_t)a->src & 7) == 0 && ((uintptr_t)a->dst & 7) == 0,
                "xa_peer_allreduce: src/dst must be 8-byte aligned");
+  if (a->has_tail)
+    XA_CHECK_ARG(a->dtype == XA_DTYPE_F32 && a->count <= XA_ADAM_TAIL_MAX_PARAMS &&
+                     a->tail.theta && a->tail.m && a->tail.v && a->tail.adam_step &&
+                     a->tail.arrivals,
+                 "xa_peer_allreduce: an optimizer tail needs f32, <= %d elements, theta, m, v, "
+                 "adam_step and arrivals", XA_ADAM_TAIL_MAX_PARAMS);
   if (a->count == 0) return 0;
   const long words = a->count * (long)(esz / 4);
   const int chunks = (int)((words + kChunkWords - 1) / kChunkWords);

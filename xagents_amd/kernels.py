@@ -9,7 +9,7 @@ import numpy as np
 import torch
 
 from xagents_amd import _lib
-from xagents_amd._lib import (XA_LOSS_A2C, XA_LOSS_PPO, XaAcGradArgs, XaAdam,
+from xagents_amd._lib import (XA_LOSS_A2C, XA_LOSS_PPO, XaAcGradArgs, XaAdam, XaAdamTail,
                               XaMinibatchArgs, XaRolloutArgs, XaShuffle, call, ptr, stream)
 
 
@@ -108,6 +108,24 @@ def grad_reduce(partials, grad, adam_step=None):
     call('xa_grad_reduce', ptr(partials), nb, p, ptr(grad), ptr(adam_step), stream())
 
 
+def grad_reduce_adam(partials, grad, tail):
+    """grad_reduce whose last block applies clip + Keras Adam (`tail`, an XaAdamTail)."""
+    nb, p = partials.shape
+    call('xa_grad_reduce_adam', ptr(partials), nb, p, ptr(grad), ctypes.byref(tail), stream())
+
+
+def adam_tail(theta, m, v, adam_step, arrivals, lr, beta1, beta2, eps, clip_norm=None,
+              grad_scale=1.0, bump=True, gnorm_out=None):
+    """XaAdamTail for an in-place optimizer step on (theta, m, v); `arrivals` is a zeroed
+    int32 device tensor the tail's kernels use to elect their last block."""
+    t = XaAdamTail()  # launch arguments only: pointers are taken, nothing runs here
+    t.theta, t.m, t.v = theta.data_ptr(), m.data_ptr(), v.data_ptr()
+    t.adam_step, t.bump, t.arrivals = adam_step.data_ptr(), int(bool(bump)), arrivals.data_ptr()
+    t.gnorm_out = None if gnorm_out is None else gnorm_out.data_ptr()
+    t.adam = adam_struct(lr, beta1, beta2, eps, clip_norm=clip_norm, grad_scale=grad_scale)
+    return t
+
+
 def adam_struct(lr, beta1, beta2, eps, clip_norm=None, grad_scale=1.0):
     a = XaAdam()
     a.lr, a.beta1, a.beta2, a.eps = lr, beta1, beta2, eps
@@ -130,5 +148,5 @@ def clip_adam(theta, m, v, grad, adam_step, lr, beta1, beta2, eps, clip_norm=Non
 __all__ = [
     'XA_LOSS_A2C', 'XA_LOSS_PPO', 'XaAcGradArgs', 'XaRolloutArgs', 'XaShuffle', 'gae',
     'nstep_returns', 'mlp_forward', 'rollout', 'counter_bump', 'adv_stats', 'ac_grad',
-    'ac_grad_blocks', 'grad_reduce', 'clip_adam', 'mlp_param_count', 'gamma_lam_f32',
+    'ac_grad_blocks', 'grad_reduce', 'grad_reduce_adam', 'adam_tail', 'clip_adam', 'mlp_param_count', 'gamma_lam_f32',
 ]

@@ -119,6 +119,7 @@ class PPO(A2C):
                     g.adam = adam
                 self._gargs_list.append(g)
         self._final_src = slots[(len(self._gargs_list) - 1) % 2]
+        self._tail_bump, self._tail_nobump = self._adam_tail(True), self._adam_tail(False)
 
     def _update(self):
         kernels.minibatches(self._mbargs)
