@@ -330,6 +330,17 @@ int xa_conv1d_input_grad(const float* dcol, int rows, int positions, int kernel,
                          int channels, int width_in, const float* gate, float* dinput,
                          void* stream);
 
+/* Keras Conv1D input gradient in one launch (an implicit transposed-convolution GEMM; the
+ * tape.gradient through the Conv1D layers built at xagents/utils/common.py:231-237):
+ *   dinput[row][q][c] = (sum over taps t, positions p with s p + t = q, filters f of
+ *                        dy[row][p][f] kernel[t][c][f]) * [gate[row][q][c] > 0]
+ * dy [rows, P, F], kernel [k, C, F] (the Keras Conv1D kernel layout), dinput [rows, W_in, C].
+ * Same value as xa_gemm (dY W^T) + xa_conv1d_input_grad without the im2col buffer. Needs
+ * F % 4 == 0 and 16-byte aligned dy / kernel. */
+int xa_conv1d_dgrad(const float* dy, const float* kernel, int rows, int positions, int ksize,
+                    int stride, int channels, int filters, int width_in, const float* gate,
+                    float* dinput, void* stream);
+
 /* DQN.get_actions (xagents/dqn/agent.py:107-116): actions[i] = tf.argmax(q[i]) (first max),
  * or random_actions[i] when use_random (the host draws np.random.random() < epsilon and
  * np.random.randint(0, A, n) exactly as the reference). */

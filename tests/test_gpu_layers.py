@@ -120,7 +120,7 @@ def test_layer_executor_forward_backward_vs_f64(device, cfg, units, shape, B):
             _close(g[off:off + n], ref_g[off:off + n], rtol=2e-4)
 
 
-@pytest.mark.parametrize('K,splits', [(100, 1), (50000, 64)])
+@pytest.mark.parametrize('K,splits', [(100, 1), (50000, 64), (200000, 1024)])
 def test_gemm_column_sums(device, K, splits):
     """A = NULL (ones) with M = 1: bias gradients (column sums of B)."""
     from xagents_amd.layers import gemm
@@ -133,3 +133,43 @@ def test_gemm_column_sums(device, K, splits):
     gemm(1, N, K, None, tb.data_ptr(), C.data_ptr(), b_ks=N, b_ns=1, ldc=N, workspace=ws,
          splits=splits)
     _close(C.cpu().numpy()[0], B.astype(np.float64).sum(0))
+
+
+@pytest.mark.parametrize('rows,W,C,F,k,s', [
+    (7, 20, 32, 64, 4, 2),    # NatureCNN conv2 input (BNT = 32 tiles, two phases)
+    (5, 9, 64, 64, 3, 1),     # NatureCNN conv3 input (BNT = 64 tiles)
+    (3, 24, 96, 8, 5, 2),     # k not a multiple of s, W_in past the last window, 2 channel tiles
+    (4, 11, 17, 12, 2, 3),    # stride > kernel: phase 2 has no taps (all-zero rows)
+    (130, 84, 32, 64, 8, 4),  # many rows, stride 4
+])
+def test_conv1d_dgrad_vs_f64_and_col2im(device, rows, W, C, F, k, s):
+    """xa_conv1d_dgrad (implicit transposed-conv GEMM) against the f64 Conv1D input
+    gradient and the two-launch path it replaces (dY W^T GEMM + xa_conv1d_input_grad)."""
+    from xagents_amd._lib import call, stream
+    from xagents_amd.layers import gemm
+    rng = np.random.default_rng(rows * W + C)
+    P = (W - k) // s + 1
+    dy = rng.normal(size=(rows, P, F)).astype(np.float32)
+    wk = rng.normal(size=(k, C, F)).astype(np.float32)
+    gate = rng.normal(size=(rows, W, C)).astype(np.float32)
+    ref = np.zeros((rows, W, C))
+    for p in range(P):
+        for t in range(k):
+            ref[:, p * s + t, :] += dy[:, p, :].astype(np.float64) @ wk[t].T.astype(np.float64)
+    ref_g = ref * (gate > 0)
+    tdy, tw, tg = (torch.from_numpy(x).to(device) for x in (dy, wk, gate))
+    for g_ptr, want in ((None, ref), (tg.data_ptr(), ref_g)):
+        out = torch.full((rows, W, C), float('nan'), device=device)
+        call('xa_conv1d_dgrad', tdy.data_ptr(), tw.data_ptr(), rows, P, k, s, C, F, W, g_ptr,
+             out.data_ptr(), stream())
+        torch.cuda.synchronize()
+        _close(out.cpu().numpy(), want)
+        # the im2col + col2im path (same math, different summation order)
+        dcol = torch.empty(rows * P, k * C, device=device)
+        gemm(rows * P, k * C, F, tdy.data_ptr(), tw.data_ptr(), dcol.data_ptr(),
+             a_m=(1, F, 0), b_ks=1, b_ns=F, ldc=k * C, splits=1)
+        out2 = torch.empty_like(out)
+        call('xa_conv1d_input_grad', dcol.data_ptr(), rows, P, k, s, C, W, g_ptr,
+             out2.data_ptr(), stream())
+        torch.cuda.synchronize()
+        _close(out.cpu().numpy(), out2.cpu().numpy().astype(np.float64))

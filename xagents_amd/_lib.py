@@ -262,6 +262,11 @@ _SIGNATURES = {
     'xa_conv1d_input_grad': (
         c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
     ),
+    'xa_conv1d_dgrad': (
+        c_int,
+        [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p,
+         c_void_p, c_void_p],
+    ),
     'xa_dqn_act': (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p]),
     'xa_dqn_td_grad': (
         c_int,

@@ -437,6 +437,177 @@ __global__ __launch_bounds__(256) void gemm_split_reduce_kernel(XaGemmArgs g, in
   }
 }
 
+// fixed-order sum of many split partials over few outputs (bias / conv weight gradients:
+// M N <= 64 K, splits in the hundreds or thousands): lane = output (one 256-B row segment
+// per split), 16 waves cut the split range into contiguous pieces summed with 8 loads in
+// flight, pieces combined in wave order through LDS
+__global__ __launch_bounds__(1024) void gemm_split_reduce_wide_kernel(XaGemmArgs g, int splits) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int total = g.M * g.N;
+  const int e = blockIdx.x * 64 + lane;
+  const int per = (splits + 15) / 16;
+  const int z0 = w * per, z1 = min(splits, z0 + per);
+  __shared__ float part[16][64];
+  float acc = 0.0f;
+  if (e < total) {
+    const float* src = g.partials + e;
+    int z = z0;
+    for (; z + 8 <= z1; z += 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = src[(int64_t)(z + u) * total];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc = acc + v[u];
+    }
+    for (; z < z1; ++z) acc = acc + src[(int64_t)z * total];
+  }
+  part[w][lane] = acc;
+  __syncthreads();
+  if (w == 0 && e < total) {
+    float s = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s = s + part[i][lane];
+    const int m = e / g.N, n = e - m * g.N;
+    store_c(epilogue(s, n, g), m, n, g);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Keras Conv1D input gradient as one implicit GEMM (a transposed convolution), replacing
+// the dY W^T GEMM into an im2col buffer + col2im gather. For phase phi = w mod s
+// (blockIdx.z) and output position w = q s + phi:
+//   dX[row][w][c] = sum_{j < J_phi} sum_f dY[row][q - j][f] W[phi + j s][c][f]
+// with J_phi = ceil((k - phi) / s) taps and terms with q - j outside [0, P) zero, then
+// times [gate[row][w][c] > 0]. GEMM view per phase: M = rows Q_phi (m = (row, q)),
+// N = C, K = J_phi F (kk = (j, f), f fastest). Tiles as gemm_kernel (16 x 16 x 4 MFMA,
+// waves of 32 x 32, K steps of 16 through double-buffered LDS); BNT = 64 channel tiles
+// run 64 x 64 blocks, BNT = 32 runs 128 x 32 blocks. Needs F % 4 == 0 (a float4 of
+// kk never crosses a tap).
+// ---------------------------------------------------------------------------
+struct XaDgradArgs {
+  const float* dy;
+  const float* w;
+  const float* gate;
+  float* out;
+  int rows, P, k, s, C, F, W_in;
+};
+
+template <int BNT>
+__global__ __launch_bounds__(256) void conv1d_dgrad_kernel(XaDgradArgs d) {
+  constexpr int TBM = BNT == 64 ? 64 : 128;
+  constexpr int LA = TBM + 4, LB = BNT + 4;
+  constexpr int NAM = TBM / 64;  // A rows (m) per thread
+  __shared__ __attribute__((aligned(16))) float As[2][BK * LA];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BK * LB];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = BNT == 64 ? w >> 1 : w, wn = BNT == 64 ? w & 1 : 0;
+  const int phi = blockIdx.z;
+  const int Q = (d.W_in - phi + d.s - 1) / d.s;
+  const int J = phi < d.k ? (d.k - phi + d.s - 1) / d.s : 0;
+  const int Mp = d.rows * Q, Kt = J * d.F;
+  const int m0 = blockIdx.x * TBM, c0 = blockIdx.y * BNT;
+  if (m0 >= Mp) return;
+
+  // A slots: m_local = (tid >> 2) + 64 r, kk quad (tid & 3)
+  const int aq = (tid & 3) * 4;
+  int a_q[NAM];
+  int64_t a_base[NAM];
+  bool a_ok[NAM];
+#pragma unroll
+  for (int r = 0; r < NAM; ++r) {
+    const int m = m0 + (tid >> 2) + 64 * r;
+    a_ok[r] = m < Mp;
+    const unsigned row = a_ok[r] ? (unsigned)m / (unsigned)Q : 0u;
+    a_q[r] = a_ok[r] ? m - (int)row * Q : 0;
+    a_base[r] = (int64_t)row * d.P * d.F;
+  }
+  // B slots: channel (tid >> 2), kk quad (tid & 3); threads past the tile stay idle
+  const int bc = tid >> 2;
+  const bool b_on = bc < BNT && c0 + bc < d.C;
+
+  f32x4 ra[NAM], rb;
+  auto load = [&](int kt) {
+    const int kk = kt + aq;
+    const int j = kk / d.F, f = kk - j * d.F;
+#pragma unroll
+    for (int r = 0; r < NAM; ++r) {
+      const int p = a_q[r] - j;
+      f32x4 v = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+      if (a_ok[r] && kk < Kt && p >= 0 && p < d.P)
+        v = *reinterpret_cast<const f32x4*>(d.dy + a_base[r] + (int64_t)p * d.F + f);
+      ra[r] = v;
+    }
+    rb = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    if (b_on && kk < Kt) {
+      const int t = phi + j * d.s;
+      rb = *reinterpret_cast<const f32x4*>(d.w + ((int64_t)t * d.C + c0 + bc) * d.F + f);
+    }
+  };
+  auto stash = [&](int buf) {
+#pragma unroll
+    for (int r = 0; r < NAM; ++r)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) As[buf][(aq + i) * LA + (tid >> 2) + 64 * r] = ra[r][i];
+    if (bc < BNT)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) Bs[buf][(aq + i) * LB + bc] = rb[i];
+  };
+
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+
+  if (Kt > 0) {
+    load(0);
+    stash(0);
+    __syncthreads();
+    int buf = 0;
+    for (int kt = 0; kt < Kt; kt += BK) {
+      const bool more = kt + BK < Kt;
+      if (more) load(kt + BK);
+      const float* as = As[buf];
+      const float* bs = Bs[buf];
+#pragma unroll
+      for (int s4 = 0; s4 < BK / 4; ++s4) {
+        const int kk = 4 * s4 + (lane >> 4);
+        float av[2], bv[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) av[i] = as[kk * LA + wm * 32 + i * 16 + (lane & 15)];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) bv[j] = bs[kk * LB + wn * 32 + j * 16 + (lane & 15)];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[i][j] = mfma4(av[i], bv[j], acc[i][j]);
+      }
+      if (more) stash(buf ^ 1);
+      __syncthreads();
+      buf ^= 1;
+    }
+  }
+
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = m0 + wm * 32 + i * 16 + 4 * (lane >> 4) + r;
+      if (m >= Mp) continue;
+      const unsigned row = (unsigned)m / (unsigned)Q;
+      const int q = m - (int)row * Q;
+      const int64_t o = ((int64_t)row * d.W_in + (int64_t)q * d.s + phi) * d.C;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int c = c0 + wn * 32 + j * 16 + (lane & 15);
+        if (c >= d.C) continue;
+        float v = acc[i][j][r];
+        if (d.gate && !(d.gate[o + c] > 0.0f)) v = 0.0f;
+        d.out[o + c] = v;
+      }
+    }
+}
+
 template <bool AK, bool BNM, bool U8>
 void launch(const XaGemmArgs& g, dim3 grid, hipStream_t s) {
   hipLaunchKernelGGL((gemm_kernel<AK, BNM, U8>), grid, dim3(256), 0, s, g);
@@ -549,10 +720,46 @@ extern "C" int xa_gemm(const XaGemmArgs* p, void* stream) {
   XA_CHECK_LAUNCH("xa_gemm");
   if (g.splits > 1) {
     const int64_t total = (int64_t)g.M * g.N;
-    const int64_t want = (total + 255) / 256;
-    const int blocks = (int)(want < 4096 ? want : 4096);
-    hipLaunchKernelGGL(gemm_split_reduce_kernel, dim3(blocks), dim3(256), 0, s, g, g.splits);
+    if (total <= 65536 && g.splits >= 64) {
+      hipLaunchKernelGGL(gemm_split_reduce_wide_kernel, dim3((int)((total + 63) / 64)),
+                         dim3(1024), 0, s, g, g.splits);
+    } else {
+      const int64_t want = (total + 255) / 256;
+      const int blocks = (int)(want < 4096 ? want : 4096);
+      hipLaunchKernelGGL(gemm_split_reduce_kernel, dim3(blocks), dim3(256), 0, s, g, g.splits);
+    }
     XA_CHECK_LAUNCH("xa_gemm (split reduce)");
   }
+  return 0;
+}
+
+extern "C" int xa_conv1d_dgrad(const float* dy, const float* kernel, int rows, int positions,
+                               int ksize, int stride, int channels, int filters, int width_in,
+                               const float* gate, float* dinput, void* stream) {
+  XA_CHECK_ARG(dy && kernel && dinput && rows > 0 && positions > 0 && ksize > 0 && stride > 0 &&
+                   channels > 0 && filters > 0 &&
+                   width_in >= (positions - 1) * stride + ksize,
+               "xa_conv1d_dgrad: bad arguments");
+  XA_CHECK_ARG(filters % 4 == 0, "xa_conv1d_dgrad: filters must be a multiple of 4 (got %d)",
+               filters);
+  XA_CHECK_ARG(((uintptr_t)dy & 15) == 0 && ((uintptr_t)kernel & 15) == 0,
+               "xa_conv1d_dgrad: dY and the kernel must be 16-byte aligned");
+  XA_CHECK_ARG((int64_t)rows * width_in < (1ll << 31) &&
+                   (int64_t)rows * width_in * channels < (1ll << 40),
+               "xa_conv1d_dgrad: rows * width_in must stay below 2^31");
+  XaDgradArgs d{dy, kernel, gate, dinput, rows, positions, ksize, stride, channels, filters,
+                width_in};
+  const int q0 = (width_in + stride - 1) / stride;  // phase 0 has the most positions
+  const int64_t m0 = (int64_t)rows * q0;
+  const int nph = stride < width_in ? stride : width_in;
+  hipStream_t s = (hipStream_t)stream;
+  if (channels <= 32) {
+    dim3 grid((unsigned)((m0 + 127) / 128), 1, nph);
+    hipLaunchKernelGGL(conv1d_dgrad_kernel<32>, grid, dim3(256), 0, s, d);
+  } else {
+    dim3 grid((unsigned)((m0 + 63) / 64), (channels + 63) / 64, nph);
+    hipLaunchKernelGGL(conv1d_dgrad_kernel<64>, grid, dim3(256), 0, s, d);
+  }
+  XA_CHECK_LAUNCH("xa_conv1d_dgrad");
   return 0;
 }

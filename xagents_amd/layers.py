@@ -5,8 +5,9 @@ wide-MLP path of the off-policy agents and the CNN actor-critic
 Every layer runs as one `xa_gemm` (gemm.hip) with grouped-affine operand addressing:
 Conv1D on (B, H, W, C) input (conv along W, H folded into the batch)
 is an implicit-im2col GEMM, its weight gradient the same GEMM with the im2col moved to
-the reduction index, its input gradient a dY W^T GEMM followed by a fixed-order col2im
-gather (`xa_conv1d_input_grad`). Biases, ReLU / tanh and the ReLU gate of the backward
+the reduction index, its input gradient one implicit transposed-conv GEMM
+(`xa_conv1d_dgrad`; a dY W^T GEMM + fixed-order col2im gather, `xa_conv1d_input_grad`,
+when the filter count is not a multiple of 4). Biases, ReLU / tanh and the ReLU gate of the backward
 pass are GEMM epilogues. Image inputs stay uint8 in HBM and are scaled f32(x) / 255 in
 the GEMM loader (xagents/base.py:505-506).
 
@@ -99,11 +100,15 @@ class LayerExecutor:
             for (M, N, K) in self._gemm_shapes(i):
                 s = lib.xa_gemm_splits(M, N, K)
                 ws = max(ws, s * M * N if s > 1 else 0)
-            if l.kind == 'convolutional' and l.input_index != -1:
+            if l.kind == 'convolutional' and l.input_index != -1 and not self._dgrad_ok(i):
                 rows, P, kC = self._conv_dims(i)[0], self._conv_dims(i)[2], l.size * l.in_features
                 dcol = max(dcol, rows * P * kC)
         self.workspace = torch.empty(max(ws, 1), **f32)
         self.dcol = torch.empty(max(dcol, 1), **f32)
+
+    def _dgrad_ok(self, i):
+        """xa_conv1d_dgrad needs F % 4 == 0 and a 16-byte aligned kernel slice."""
+        return self.layers[i].filters % 4 == 0 and self.offsets[i][0] % 4 == 0
 
     # ---- shapes --------------------------------------------------------------
     def _src_shape(self, i):
@@ -251,9 +256,16 @@ class LayerExecutor:
                          workspace=self.workspace)
                 if j != -1:
                     assert not written[j], 'a conv input with two consumers is not supported'
-                    gemm(rows * P, k * C, F, d.data_ptr(), tp + 4 * w0, self.dcol.data_ptr(),
-                         a_m=(1, F, 0), b_ks=1, b_ns=F, ldc=k * C, workspace=self.workspace)
-                    call('xa_conv1d_input_grad', self.dcol.data_ptr(), rows, P, k, s, C, Win,
-                         gate_j, self.douts[j].data_ptr(), stream())
+                    if self._dgrad_ok(i):
+                        # implicit transposed-conv GEMM straight into dX (no im2col buffer)
+                        call('xa_conv1d_dgrad', d.data_ptr(), int(tp + 4 * w0), int(rows),
+                             int(P), int(k), int(s), int(C), int(F), int(Win), gate_j,
+                             self.douts[j].data_ptr(), stream())
+                    else:
+                        gemm(rows * P, k * C, F, d.data_ptr(), tp + 4 * w0,
+                             self.dcol.data_ptr(), a_m=(1, F, 0), b_ks=1, b_ns=F, ldc=k * C,
+                             workspace=self.workspace)
+                        call('xa_conv1d_input_grad', self.dcol.data_ptr(), rows, P, k, s, C,
+                             Win, gate_j, self.douts[j].data_ptr(), stream())
                     written[j] = True
         return grad
