@@ -55,10 +55,40 @@ XA_DEV void store_c(float v, int m, int n, const XaGemmArgs& g) {
   *c = g.beta ? *c + v : v;
 }
 
+// kernel argument: the public args plus the host's vectorisation verdicts. vec_a / vec_b:
+// every 4-run a thread loads (along k for k-major A, along m otherwise; along n for n-major
+// B, along k otherwise) is contiguous, aligned and entirely in or out of bounds, so it is
+// one 16-B (f32) or 4-B (u8) load
+struct XaGemmK {
+  XaGemmArgs g;
+  int vec_a, vec_b;
+};
+
+template <bool U8>
+XA_DEV void ld4(const void* base, int64_t off, float* d) {
+  if (U8) {
+    const uchar4 v = *reinterpret_cast<const uchar4*>(static_cast<const uint8_t*>(base) + off);
+    d[0] = (float)v.x / 255.0f;
+    d[1] = (float)v.y / 255.0f;
+    d[2] = (float)v.z / 255.0f;
+    d[3] = (float)v.w / 255.0f;
+  } else {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(static_cast<const float*>(base) + off);
+    d[0] = v[0];
+    d[1] = v[1];
+    d[2] = v[2];
+    d[3] = v[3];
+  }
+}
+
+XA_DEV void zero4(float* d) { d[0] = d[1] = d[2] = d[3] = 0.0f; }
+
 // A_KMAJOR: g(k) is unit stride (loader reads along k); otherwise along m.
 // B_NMAJOR: b_ns == 1 (loader reads along n); otherwise along k.
 template <bool A_KMAJOR, bool B_NMAJOR, bool A_U8>
-__global__ __launch_bounds__(256) void gemm_kernel(XaGemmArgs g) {
+__global__ __launch_bounds__(256) void gemm_kernel(XaGemmK kargs) {
+  const XaGemmArgs& g = kargs.g;
+  const bool vec_a = kargs.vec_a, vec_b = kargs.vec_b;
   __shared__ __attribute__((aligned(16))) float As[2][BK * LDA];
   __shared__ __attribute__((aligned(16))) float Bs[2][BK * LDB];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -87,6 +117,12 @@ __global__ __launch_bounds__(256) void gemm_kernel(XaGemmArgs g) {
 
   float ra[4], rb[4];
   auto load = [&](int kt) {
+    if (vec_a) {
+      // one run: 4 k of row a_m (k-major) or 4 m at column a_k
+      const int k = kt + a_k;
+      if (a_ok[0] && k < k_end) ld4<A_U8>(g.a, a_row[0] + grouped(k, (int)g.a_pk, g.a_rk, g.a_sk), ra);
+      else zero4(ra);
+    } else {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int k = kt + a_k + (A_KMAJOR ? i : 0);
@@ -102,11 +138,18 @@ __global__ __launch_bounds__(256) void gemm_kernel(XaGemmArgs g) {
       }
       ra[i] = v;
     }
+    }
+    if (vec_b) {
+      const int k = kt + b_k, n = n0 + b_n;
+      if (k < k_end && n < g.N) ld4<false>(g.b, (int64_t)k * g.b_ks + (int64_t)n * g.b_ns, rb);
+      else zero4(rb);
+    } else {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int k = kt + b_k + (B_NMAJOR ? 0 : i);
       const int n = n0 + b_n + (B_NMAJOR ? i : 0);
       rb[i] = (k < k_end && n < g.N) ? g.b[(int64_t)k * g.b_ks + (int64_t)n * g.b_ns] : 0.0f;
+    }
     }
   };
   auto stash = [&](int buf) {
@@ -184,7 +227,9 @@ XA_DEV f32x16 mfma32(float a, float b, f32x16 c) {
 }
 
 template <int WM, int WN, bool A_KMAJOR, bool B_NMAJOR, bool A_U8>
-__global__ __launch_bounds__(256) void gemm_tile_kernel(XaGemmArgs g) {
+__global__ __launch_bounds__(256) void gemm_tile_kernel(XaGemmK kargs) {
+  const XaGemmArgs& g = kargs.g;
+  const bool vec_a = kargs.vec_a, vec_b = kargs.vec_b;
   constexpr int TBM = 64 * WM, TBN = 64 * WN, TLA = TBM + 4, TLB = TBN + 4;
   constexpr int EA = TBM * TBK / 256, EB = TBN * TBK / 256;  // elements per thread
   __shared__ __attribute__((aligned(16))) float As[2][TBK * TLA];
@@ -215,6 +260,17 @@ __global__ __launch_bounds__(256) void gemm_tile_kernel(XaGemmArgs g) {
   float ra[EA], rb[EB];
 
   auto load = [&](int kt) {
+    if (vec_a) {
+#pragma unroll
+      for (int r = 0; r < EA / 4; ++r) {
+        // k-major: row r, k quad (tid & 7); m-major: 4 m from (tid % AQ) 4, k row r
+        const int mi = A_KMAJOR ? r : 0;
+        const int k = A_KMAJOR ? kt + (tid & 7) * 4 : kt + tid / AQ + AKR * r;
+        if (a_ok[mi] && k < k_end)
+          ld4<A_U8>(g.a, a_row[mi] + grouped(k, (int)g.a_pk, g.a_rk, g.a_sk), ra + 4 * r);
+        else zero4(ra + 4 * r);
+      }
+    } else {
 #pragma unroll
     for (int e = 0; e < EA; ++e) {
       int mi, k;
@@ -236,6 +292,16 @@ __global__ __launch_bounds__(256) void gemm_tile_kernel(XaGemmArgs g) {
       }
       ra[e] = v;
     }
+    }
+    if (vec_b) {
+#pragma unroll
+      for (int r = 0; r < EB / 4; ++r) {
+        const int n = B_NMAJOR ? n0 + (tid % BQ) * 4 : n0 + (tid >> 3) + 32 * r;
+        const int k = B_NMAJOR ? kt + tid / BQ + BKR * r : kt + (tid & 7) * 4;
+        if (k < k_end && n < g.N) ld4<false>(g.b, (int64_t)k * g.b_ks + (int64_t)n * g.b_ns, rb + 4 * r);
+        else zero4(rb + 4 * r);
+      }
+    } else {
 #pragma unroll
     for (int e = 0; e < EB; ++e) {
       int n, k;
@@ -247,6 +313,7 @@ __global__ __launch_bounds__(256) void gemm_tile_kernel(XaGemmArgs g) {
         k = kt + (tid & 7) * 4 + (e & 3);
       }
       rb[e] = (k < k_end && n < g.N) ? g.b[(int64_t)k * g.b_ks + (int64_t)n * g.b_ns] : 0.0f;
+    }
     }
   };
   auto stash = [&](int buf) {
@@ -609,28 +676,28 @@ __global__ __launch_bounds__(256) void conv1d_dgrad_kernel(XaDgradArgs d) {
 }
 
 template <bool AK, bool BNM, bool U8>
-void launch(const XaGemmArgs& g, dim3 grid, hipStream_t s) {
+void launch(const XaGemmK& g, dim3 grid, hipStream_t s) {
   hipLaunchKernelGGL((gemm_kernel<AK, BNM, U8>), grid, dim3(256), 0, s, g);
 }
 
 template <int WM, int WN, bool AK, bool BNM, bool U8>
-void launch_tile(const XaGemmArgs& g, int splits, hipStream_t s) {
-  dim3 grid((g.M + 64 * WM - 1) / (64 * WM), (g.N + 64 * WN - 1) / (64 * WN), splits);
+void launch_tile(const XaGemmK& g, int splits, hipStream_t s) {
+  dim3 grid((g.g.M + 64 * WM - 1) / (64 * WM), (g.g.N + 64 * WN - 1) / (64 * WN), splits);
   hipLaunchKernelGGL((gemm_tile_kernel<WM, WN, AK, BNM, U8>), grid, dim3(256), 0, s, g);
 }
 
 template <int WM, int WN>
-void dispatch_tile(const XaGemmArgs& g, bool ak, bool bn, bool u8, hipStream_t s) {
+void dispatch_tile(const XaGemmK& g, bool ak, bool bn, bool u8, hipStream_t s) {
   if (u8) {
-    if (ak && bn) launch_tile<WM, WN, true, true, true>(g, g.splits, s);
-    else if (ak) launch_tile<WM, WN, true, false, true>(g, g.splits, s);
-    else if (bn) launch_tile<WM, WN, false, true, true>(g, g.splits, s);
-    else launch_tile<WM, WN, false, false, true>(g, g.splits, s);
+    if (ak && bn) launch_tile<WM, WN, true, true, true>(g, g.g.splits, s);
+    else if (ak) launch_tile<WM, WN, true, false, true>(g, g.g.splits, s);
+    else if (bn) launch_tile<WM, WN, false, true, true>(g, g.g.splits, s);
+    else launch_tile<WM, WN, false, false, true>(g, g.g.splits, s);
   } else {
-    if (ak && bn) launch_tile<WM, WN, true, true, false>(g, g.splits, s);
-    else if (ak) launch_tile<WM, WN, true, false, false>(g, g.splits, s);
-    else if (bn) launch_tile<WM, WN, false, true, false>(g, g.splits, s);
-    else launch_tile<WM, WN, false, false, false>(g, g.splits, s);
+    if (ak && bn) launch_tile<WM, WN, true, true, false>(g, g.g.splits, s);
+    else if (ak) launch_tile<WM, WN, true, false, false>(g, g.g.splits, s);
+    else if (bn) launch_tile<WM, WN, false, true, false>(g, g.g.splits, s);
+    else launch_tile<WM, WN, false, false, false>(g, g.g.splits, s);
   }
 }
 
@@ -697,25 +764,35 @@ extern "C" int xa_gemm(const XaGemmArgs* p, void* stream) {
   const bool u8 = g.a_u8 != 0;
   const int per_split = (g.K + g.splits - 1) / g.splits;
   const int shape = g.force_small ? 0 : pick_shape(g.M, g.N, g.K, per_split, g.a == nullptr);
+  XaGemmK kg{g, 0, 0};
+  if (g.a != nullptr && ((uintptr_t)g.a & (u8 ? 3 : 15)) == 0) {
+    const bool rows4 = g.a_rm % 4 == 0 && (g.a_pm == 1 || g.a_sm % 4 == 0);
+    const bool cols4 = g.a_rk % 4 == 0 && (g.a_pk == 1 || g.a_sk % 4 == 0);
+    kg.vec_a = ak ? (g.K % 4 == 0 && rows4)
+                  : (g.a_pm == 1 && g.a_rm == 1 && g.M % 4 == 0 && cols4);
+  }
+  if (((uintptr_t)g.b & 15) == 0)
+    kg.vec_b = bn ? (g.b_ks % 4 == 0 && g.N % 4 == 0)
+                  : (g.b_ks == 1 && g.b_ns % 4 == 0 && g.K % 4 == 0);
   if (shape == 2) {
     hipLaunchKernelGGL(colsum_kernel, dim3(1, (g.N + 63) / 64, g.splits), dim3(256), 0, s, g);
   } else if (shape == 1) {
     dim3 gs((g.M + 31) / 32, (g.N + 31) / 32, g.splits);
     if (u8) hipLaunchKernelGGL(gemm_skinny_kernel<true>, gs, dim3(64), 0, s, g);
     else hipLaunchKernelGGL(gemm_skinny_kernel<false>, gs, dim3(64), 0, s, g);
-  } else if (shape == 22) dispatch_tile<2, 2>(g, ak, bn, u8, s);
-  else if (shape == 41) dispatch_tile<4, 1>(g, ak, bn, u8, s);
-  else if (shape == 14) dispatch_tile<1, 4>(g, ak, bn, u8, s);
+  } else if (shape == 22) dispatch_tile<2, 2>(kg, ak, bn, u8, s);
+  else if (shape == 41) dispatch_tile<4, 1>(kg, ak, bn, u8, s);
+  else if (shape == 14) dispatch_tile<1, 4>(kg, ak, bn, u8, s);
   else if (u8) {
-    if (ak && bn) launch<true, true, true>(g, grid, s);
-    else if (ak) launch<true, false, true>(g, grid, s);
-    else if (bn) launch<false, true, true>(g, grid, s);
-    else launch<false, false, true>(g, grid, s);
+    if (ak && bn) launch<true, true, true>(kg, grid, s);
+    else if (ak) launch<true, false, true>(kg, grid, s);
+    else if (bn) launch<false, true, true>(kg, grid, s);
+    else launch<false, false, true>(kg, grid, s);
   } else {
-    if (ak && bn) launch<true, true, false>(g, grid, s);
-    else if (ak) launch<true, false, false>(g, grid, s);
-    else if (bn) launch<false, true, false>(g, grid, s);
-    else launch<false, false, false>(g, grid, s);
+    if (ak && bn) launch<true, true, false>(kg, grid, s);
+    else if (ak) launch<true, false, false>(kg, grid, s);
+    else if (bn) launch<false, true, false>(kg, grid, s);
+    else launch<false, false, false>(kg, grid, s);
   }
   XA_CHECK_LAUNCH("xa_gemm");
   if (g.splits > 1) {
