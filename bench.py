@@ -44,6 +44,9 @@ def parse():
     p.add_argument('--no-graph', action='store_true')
     p.add_argument('--cpu-baseline-seconds', type=float, default=15.0)
     p.add_argument('--cpu-threads', type=int, default=0)
+    p.add_argument('--preprocess', action='store_true',
+                   help='c3 / c4: AtariWrapper on device (xa_atari_step: frame skip 4, '
+                        'gray + resize of synthetic raw 210x160 RGB frames) in every env step')
     p.add_argument('--config', default='c2', choices=['c2', 'c3', 'c4', 'c5'],
                    help='c2 (default, the BASELINE metric line); c3 DQN Pong-shaped, c4 PPO '
                         'CNN Breakout-shaped (global 1024 envs, strong scaling), c5 TD3')
@@ -133,6 +136,17 @@ def _timed(fn, steps, warmup, world):
     return el
 
 
+def _raw_kw(args, n):
+    return {'t_raw_frames': 64 if n <= 64 else 16} if args.preprocess else {}
+
+
+def _data_note(args, what):
+    if args.preprocess:
+        return ('synthetic: raw 210x160 RGB uint8 frames i.i.d. uniform (seed 55+rank) '
+                'through AtariWrapper on device (frame skip 4, gray, resize 84x84)')
+    return what
+
+
 def bench_offpolicy_and_cnn(args):
     """Secondary configs; one JSON line each, same fields."""
     import numpy as np
@@ -146,7 +160,8 @@ def bench_offpolicy_and_cnn(args):
     if args.config == 'c3':
         from xagents_amd import DQN
         n = 32
-        envs = create_envs('PongNoFrameskip-v4', n, device=device, seed=args.seed + rank)
+        envs = create_envs('PongNoFrameskip-v4', n, args.preprocess, device=device,
+                           seed=args.seed + rank, **_raw_kw(args, n))
         model = create_model(envs, 'dqn', 'model', seed=args.seed, device=device)
         bufs = create_buffers('dqn', 1_000_000, 64, n, initial_size=1_000_000)
         agent = DQN(envs, model, bufs, double=True, seed=args.seed, quiet=True,
@@ -161,8 +176,9 @@ def bench_offpolicy_and_cnn(args):
             agent.at_step_end()
         el = _timed(step, args.steps, args.warmup, world)
         env_steps = n * args.steps * world
-        line.update(scaling='weak', data='synthetic: Pong-shaped uint8 (84,84,1) frames '
-                    'i.i.d. uniform (seed 55+rank), replay buffers pre-filled by device env steps',
+        line.update(scaling='weak', data=_data_note(
+                        args, 'synthetic: Pong-shaped uint8 (84,84,1) frames i.i.d. uniform '
+                        '(seed 55+rank), replay buffers pre-filled by device env steps'),
                     config={'workload': 'DQN/DDQN PongNoFrameskip-v4-shaped, 32 envs, NatureCNN '
                                         '(Conv1D cfg), ReplayBuffer1 1M total, buffer batch 64, '
                                         'double, epsilon 0.02 (BASELINE configs[2])',
@@ -171,13 +187,15 @@ def bench_offpolicy_and_cnn(args):
     elif args.config == 'c4':
         from xagents_amd import PPO
         n = 1024 // world
-        envs = create_envs('BreakoutNoFrameskip-v4', n, device=device, seed=args.seed + rank)
+        envs = create_envs('BreakoutNoFrameskip-v4', n, args.preprocess, device=device,
+                           seed=args.seed + rank, **_raw_kw(args, n))
         model = create_model(envs, 'ppo', 'model', seed=args.seed, device=device)
         agent = PPO(envs, model, n_steps=128, seed=args.seed, quiet=True)
         el = _timed(agent.fused_train_step, args.steps, args.warmup, world)
         env_steps = n * 128 * args.steps * world
-        line.update(scaling='strong', data='synthetic: Breakout-shaped uint8 (84,84,1) frames '
-                    'i.i.d. uniform (seed 55+rank), random-init CNN',
+        line.update(scaling='strong', data=_data_note(
+                        args, 'synthetic: Breakout-shaped uint8 (84,84,1) frames i.i.d. '
+                        'uniform (seed 55+rank), random-init CNN'),
                     config={'workload': 'PPO BreakoutNoFrameskip-v4-shaped, 1024 envs global '
                                         'sharded over the GPUs, NatureCNN (Conv1D cfg), n_steps '
                                         '128, 4x4 minibatches (BASELINE configs[3])',

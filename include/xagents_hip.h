@@ -416,6 +416,36 @@ typedef struct XaReplayStepArgs {
 
 int xa_replay_env_step(const XaReplayStepArgs* args, void* stream);
 
+/* AtariWrapper.step / reset on device (xagents/utils/common.py:67-142, the per-env
+ * `env.step` + `env.reset` of BaseAgent.step_envs, base.py:388-426, for Atari envs).
+ * Raw RGB frames [n_envs, t_raw, height, width, 3] u8; stepping into frame t yields
+ * raw_rew[t], raw_done[t]; the frame after a done frame is the env.reset() frame.
+ * A step walks `skips` frames from raw_cursor (reward summed, stop at a done), takes the
+ * pixelwise max with the previous raw frame when max_frame (the 2-deep frame_buffer),
+ * then cv2.cvtColor(COLOR_BGR2GRAY) and cv2.resize(dsize = (out_w, out_h), INTER_LINEAR)
+ * in OpenCV's 8-bit fixed point (xofs / alpha / yofs / beta: cv::resize's tables, built by
+ * the host). out_step = frame returned by step (pre-reset), out_post = state after
+ * step_envs (the reset frame, processed alone, when done). reset_only = 1 processes
+ * frames[raw_cursor] alone into out_post (AtariWrapper.reset). */
+typedef struct XaAtariStepArgs {
+  int n_envs, t_raw, height, width, out_h, out_w;
+  const uint8_t* frames;
+  const float* raw_rew;
+  const float* raw_done;
+  int* raw_cursor;
+  int skips, max_frame, reset_only;
+  const int* xofs;
+  const short* alpha;
+  const int* yofs;
+  const short* beta;
+  uint8_t* out_step;
+  uint8_t* out_post;
+  float* out_rew;
+  float* out_done;
+} XaAtariStepArgs;
+
+int xa_atari_step(const XaAtariStepArgs* args, void* stream);
+
 /* tf.keras.losses.MSE(target, pred) per row, gradient of the batch sum (minimize on a
  * [B] loss): dpred = 2 (pred - target) / n_out; loss[b] (optional). */
 int xa_mse_grad(const float* pred, const float* target, int batch, int n_out, float* dpred,

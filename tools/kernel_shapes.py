@@ -9,7 +9,7 @@ rows = list(csv.DictReader(open(sys.argv[1])))
 top = int(sys.argv[2]) if len(sys.argv) > 2 else 25
 d = collections.defaultdict(list)
 for r in rows:
-    k = (r['Kernel_Name'].split('(')[0].replace('void ', '').replace('(anonymous namespace)::', '')[:48],
+    k = (r['Kernel_Name'].replace('void ', '').replace('(anonymous namespace)::', '').split('(')[0][:48],
          r['Grid_Size_X'], r['Grid_Size_Y'], r['Grid_Size_Z'], r['Workgroup_Size_X'])
     d[k].append(int(r['End_Timestamp']) - int(r['Start_Timestamp']))
 tot = sum(sum(v) for v in d.values())

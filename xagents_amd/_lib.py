@@ -167,6 +167,19 @@ class XaGemmArgs(Structure):
     ]
 
 
+class XaAtariStepArgs(Structure):
+    _fields_ = [
+        ('n_envs', c_int), ('t_raw', c_int), ('height', c_int), ('width', c_int),
+        ('out_h', c_int), ('out_w', c_int),
+        ('frames', c_void_p), ('raw_rew', c_void_p), ('raw_done', c_void_p),
+        ('raw_cursor', c_void_p),
+        ('skips', c_int), ('max_frame', c_int), ('reset_only', c_int),
+        ('xofs', c_void_p), ('alpha', c_void_p), ('yofs', c_void_p), ('beta', c_void_p),
+        ('out_step', c_void_p), ('out_post', c_void_p), ('out_rew', c_void_p),
+        ('out_done', c_void_p),
+    ]
+
+
 class XaReplayStepArgs(Structure):
     _fields_ = [
         ('n_envs', c_int), ('t_rec', c_int),
@@ -278,6 +291,7 @@ _SIGNATURES = {
     'xa_polyak': (c_int, [c_void_p, c_void_p, c_int64, c_float, c_void_p]),
     'xa_adam_step_bump': (c_int, [c_void_p, c_void_p]),
     'xa_replay_env_step': (c_int, [POINTER(XaReplayStepArgs), c_void_p]),
+    'xa_atari_step': (c_int, [POINTER(XaAtariStepArgs), c_void_p]),
     'xa_mse_grad': (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     'xa_copy_block': (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int, c_int, c_void_p]),
     'xa_categorical': (

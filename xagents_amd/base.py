@@ -457,6 +457,9 @@ class OffPolicy(BaseAgent, ABC):
         r = self._st_row
         a.out_dones = self._st_done[r].data_ptr()
         a.done_epret = self._st_epret[r].data_ptr()
+        pre_step = getattr(self.envs, 'pre_step', None)
+        if pre_step is not None:
+            pre_step()  # raw-frame env: AtariWrapper.step into the one-step record
         call('xa_replay_env_step', ctypes.byref(a), stream())
         if store:
             self.replay.appended()

@@ -321,6 +321,12 @@ def create_envs(env_name, n=1, preprocess=False, *args, mode='replay', seed=55, 
     Returns ONE vectorized env object of length n (the agents accept it wherever the
     reference takes a list of gym envs).
     """
+    if 'NoFrameskip' in env_name and preprocess:
+        # AtariWrapper on device over a synthetic raw RGB frame stream (atari.py)
+        from xagents_amd.atari import AtariFrameVecEnv
+        actions = {'PongNoFrameskip-v4': 6, 'BreakoutNoFrameskip-v4': 4}.get(env_name, 6)
+        return AtariFrameVecEnv(env_name, n, actions, *args, seed=seed, device=device,
+                                t_raw=kwargs.pop('t_raw_frames', 64), **kwargs)
     if 'NoFrameskip' in env_name:
         # Atari-shaped synthetic replay: frames as AtariWrapper emits them (84, 84, 1)
         # uint8 (xagents/utils/common.py:67-142); the wrapper itself is not rebuilt
@@ -330,8 +336,8 @@ def create_envs(env_name, n=1, preprocess=False, *args, mode='replay', seed=55, 
     if env_name.startswith('BipedalWalker'):
         return TransitionReplayVecEnv(env_name, n, (24,), Box(-1.0, 1.0, (4,)), np.float32,
                                       t_rec=t_rec, seed=seed, device=device)
-    assert not preprocess, ('Atari preprocessing on device is not implemented yet '
-                            '(SURVEY.md section 8f rank 1)')
+    assert not preprocess, (f'Cannot use AtariWrapper or --preprocess for non-atari '
+                            f'environment {env_name}')
     if env_name != 'CartPole-v1':
         raise NotImplementedError(f'No device environment for {env_name}')
     if mode == 'replay':

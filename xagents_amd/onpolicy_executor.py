@@ -111,6 +111,8 @@ class ExecutorActorCritic:
             a.out_dones = self.b_dstep.data_ptr() + 4 * t
             a.done_epret = self.b_epret.data_ptr() + 4 * t
             a.out_ld = T  # env-major [N, T] rows
+            if hasattr(env, 'pre_step'):
+                env.pre_step()  # raw-frame env: AtariWrapper.step into the one-step record
             call('xa_replay_env_step', ctypes.byref(a), stream())
         # dones[:, t + 1] = done of step t (dones[:, 0] is the carried-in flag)
         call('xa_copy_block', self.b_dstep.data_ptr(), T, self.b_done.data_ptr() + 4, T + 1, N,
