@@ -341,6 +341,20 @@ int xa_conv1d_dgrad(const float* dy, const float* kernel, int rows, int position
                     int stride, int channels, int filters, int width_in, const float* gate,
                     float* dinput, void* stream);
 
+/* Keras Conv1D weight and bias gradient of a narrow layer (ksize * channels <= 8, filters a
+ * power of two in [4, 64]; NatureCNN's first layer on single-channel frames) in one pass
+ * over dY (the gradient tape of common.py:231-237):
+ *   dw[t][c][f] (+)= sum_{row, p} x[row][p stride + t][c] dy[row][p][f],
+ *   db[f]       (+)= sum_{row, p} dy[row][p][f]
+ * x [rows, width_in, channels] f32 or uint8 (x_u8: scaled f32(x) / 255, base.py:505-506),
+ * dy [rows, positions, filters] (16-byte aligned). accumulate = 1 adds to dw / db.
+ * workspace: xa_conv1d_wgrad_workspace_floats(...) floats (0 = shape not supported). */
+size_t xa_conv1d_wgrad_workspace_floats(int ksize, int channels, int filters);
+int xa_conv1d_wgrad(const void* x, int x_u8, const float* dy, int rows, int width_in,
+                    int channels, int positions, int ksize, int stride, int filters, float* dw,
+                    float* db, int accumulate, float* workspace, size_t workspace_floats,
+                    void* stream);
+
 /* DQN.get_actions (xagents/dqn/agent.py:107-116): actions[i] = tf.argmax(q[i]) (first max),
  * or random_actions[i] when use_random (the host draws np.random.random() < epsilon and
  * np.random.randint(0, A, n) exactly as the reference). */

@@ -173,3 +173,38 @@ def test_conv1d_dgrad_vs_f64_and_col2im(device, rows, W, C, F, k, s):
              out2.data_ptr(), stream())
         torch.cuda.synchronize()
         _close(out.cpu().numpy(), out2.cpu().numpy().astype(np.float64))
+
+
+@pytest.mark.parametrize('u8', [False, True])
+@pytest.mark.parametrize('rows,W,C,k,s,F', [(50, 84, 1, 8, 4, 32), (7, 30, 2, 3, 2, 64),
+                                             (3, 9, 1, 1, 1, 4)])
+def test_conv1d_wgrad_small_vs_f64(device, rows, W, C, k, s, F, u8):
+    """xa_conv1d_wgrad: one-pass dW + db of a narrow Conv1D vs float64, plain and
+    accumulating."""
+    from xagents_amd._lib import call, load, stream
+    rng = np.random.default_rng(rows + F)
+    P = (W - k) // s + 1
+    if u8:
+        xh = rng.integers(0, 256, size=(rows, W, C), dtype=np.uint8)
+        x64 = (xh.astype(np.float32) / np.float32(255.0)).astype(np.float64)
+    else:
+        xh = rng.normal(size=(rows, W, C)).astype(np.float32)
+        x64 = xh.astype(np.float64)
+    dy = rng.normal(size=(rows, P, F)).astype(np.float32)
+    idx = np.arange(P)[:, None] * s + np.arange(k)[None, :]
+    cols = x64[:, idx, :].reshape(rows * P, k * C)
+    ref_w = cols.T @ dy.reshape(rows * P, F).astype(np.float64)
+    ref_b = dy.astype(np.float64).sum((0, 1))
+    n_ws = int(load().xa_conv1d_wgrad_workspace_floats(k, C, F))
+    assert n_ws > 0
+    ws = torch.empty(n_ws, device=device)
+    tx, tdy = torch.from_numpy(xh).to(device), torch.from_numpy(dy).to(device)
+    w0 = rng.normal(size=(k * C, F)).astype(np.float32)
+    b0 = rng.normal(size=F).astype(np.float32)
+    for acc in (0, 1):
+        dw, db = torch.from_numpy(w0.copy()).to(device), torch.from_numpy(b0.copy()).to(device)
+        call('xa_conv1d_wgrad', tx.data_ptr(), int(u8), tdy.data_ptr(), rows, W, C, P, k, s, F,
+             dw.data_ptr(), db.data_ptr(), acc, ws.data_ptr(), n_ws, stream())
+        torch.cuda.synchronize()
+        _close(dw.cpu().numpy(), ref_w + (w0 if acc else 0))
+        _close(db.cpu().numpy(), ref_b + (b0 if acc else 0))

@@ -280,6 +280,12 @@ _SIGNATURES = {
         [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p,
          c_void_p, c_void_p],
     ),
+    'xa_conv1d_wgrad_workspace_floats': (ctypes.c_size_t, [c_int, c_int, c_int]),
+    'xa_conv1d_wgrad': (
+        c_int,
+        [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p,
+         c_void_p, c_int, c_void_p, ctypes.c_size_t, c_void_p],
+    ),
     'xa_dqn_act': (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p]),
     'xa_dqn_td_grad': (
         c_int,

@@ -540,6 +540,105 @@ __global__ __launch_bounds__(1024) void gemm_split_reduce_wide_kernel(XaGemmArgs
 }
 
 // ---------------------------------------------------------------------------
+// Conv1D weight + bias gradient for a narrow im2col (k C <= 8, e.g. NatureCNN's first
+// layer on single-channel frames): dW[t][c][f] = sum_{row, p} x[row][p s + t][c] dY[row][p][f]
+// and db[f] = sum dY[row][p][f] in ONE pass over dY (the GEMM path reads dY twice, for dW
+// and for the bias column sums, and wastes 3/4 of a 32 x 32 MFMA tile on M = 8).
+// Block b owns a contiguous range of the rows x positions samples; thread = (filter quad,
+// sample lane); fixed-order LDS combine -> per-block partials [G][kC F] and [G][F], summed
+// in fixed order by the wide split reduce. Bound: reading dY (HBM).
+// ---------------------------------------------------------------------------
+constexpr int kWgMaxKC = 8;
+
+struct XaWgradArgs {
+  const void* x;
+  const float* dy;
+  float* ws;
+  int rows, W, C, P, k, s, F, kc;
+  int vec_x;  // kc % 4 == 0 and every im2col row start 4-element aligned
+};
+
+template <bool X_U8>
+__global__ __launch_bounds__(256) void conv_wgrad_small_kernel(XaWgradArgs a) {
+  const int FQ = a.F >> 2, nsub = 256 / FQ;
+  const int q = threadIdx.x % FQ, sub = threadIdx.x / FQ;
+  const int R = a.rows * a.P;
+  const int per = (R + (int)gridDim.x - 1) / (int)gridDim.x;
+  const int r0 = blockIdx.x * per, r1 = min(R, r0 + per);
+  const float* xf = static_cast<const float*>(a.x);
+  const uint8_t* xu = static_cast<const uint8_t*>(a.x);
+  float acc[kWgMaxKC][4], bacc[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    bacc[c] = 0.0f;
+#pragma unroll
+    for (int j = 0; j < kWgMaxKC; ++j) acc[j][c] = 0.0f;
+  }
+  // U samples per trip, all their loads issued before the first use
+  constexpr int U = 4;
+  for (int rb = r0 + sub; rb < r1; rb += U * nsub) {
+    f32x4 dz[U];
+    float xv[U][kWgMaxKC];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int r = rb + u * nsub;
+      const bool ok = r < r1;
+      const int rr = ok ? r : r0;
+      const unsigned row = (unsigned)rr / (unsigned)a.P;
+      const int p = rr - (int)row * a.P;
+      const int64_t xb = (int64_t)row * a.W * a.C + (int64_t)p * a.s * a.C;
+      dz[u] = ok ? *reinterpret_cast<const f32x4*>(a.dy + (int64_t)rr * a.F + 4 * q)
+                 : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+      if (!ok) {
+#pragma unroll
+        for (int j = 0; j < kWgMaxKC; ++j) xv[u][j] = 0.0f;
+      } else if (a.vec_x) {
+#pragma unroll
+        for (int j = 0; j < kWgMaxKC; j += 4) {
+          if (j < a.kc) ld4<X_U8>(a.x, xb + j, &xv[u][j]);
+          else zero4(&xv[u][j]);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < kWgMaxKC; ++j)
+          xv[u][j] = j < a.kc ? (X_U8 ? (float)xu[xb + j] / 255.0f : xf[xb + j]) : 0.0f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        bacc[c] = bacc[c] + dz[u][c];
+#pragma unroll
+        for (int j = 0; j < kWgMaxKC; ++j) acc[j][c] = fmaf(xv[u][j], dz[u][c], acc[j][c]);
+      }
+  }
+  // combine the nsub sample lanes of every (quad, value) in fixed order
+  constexpr int NV = 4 * (kWgMaxKC + 1);
+  __shared__ float red[256 * NV];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    red[(sub * FQ + q) * NV + kWgMaxKC * 4 + c] = bacc[c];
+#pragma unroll
+    for (int j = 0; j < kWgMaxKC; ++j) red[(sub * FQ + q) * NV + j * 4 + c] = acc[j][c];
+  }
+  __syncthreads();
+  const int nval = (a.kc + 1) * a.F;  // dW [kc][F] then db [F]
+  const int G = gridDim.x;
+  for (int v = threadIdx.x; v < nval; v += 256) {
+    const int j = v / a.F, f = v - j * a.F;
+    const int qq = f >> 2, c = f & 3;
+    const int slot = (j < a.kc ? j : kWgMaxKC) * 4 + c;
+    float sum = 0.0f;
+    for (int u = 0; u < nsub; ++u) sum = sum + red[(u * FQ + qq) * NV + slot];
+    if (j < a.kc) a.ws[(int64_t)blockIdx.x * a.kc * a.F + v] = sum;
+    else a.ws[(int64_t)G * a.kc * a.F + (int64_t)blockIdx.x * a.F + f] = sum;
+  }
+}
+
+constexpr int kWgBlocks = 1024;
+
+// ---------------------------------------------------------------------------
 // Keras Conv1D input gradient as one implicit GEMM (a transposed convolution), replacing
 // the dY W^T GEMM into an im2col buffer + col2im gather. For phase phi = w mod s
 // (blockIdx.z) and output position w = q s + phi:
@@ -838,5 +937,56 @@ extern "C" int xa_conv1d_dgrad(const float* dy, const float* kernel, int rows, i
     hipLaunchKernelGGL(conv1d_dgrad_kernel<64>, grid, dim3(256), 0, s, d);
   }
   XA_CHECK_LAUNCH("xa_conv1d_dgrad");
+  return 0;
+}
+
+extern "C" size_t xa_conv1d_wgrad_workspace_floats(int ksize, int channels, int filters) {
+  const int kc = ksize * channels;
+  const bool ok = kc >= 1 && kc <= kWgMaxKC && filters >= 4 && filters <= 64 &&
+                  (filters & (filters - 1)) == 0;
+  return ok ? (size_t)kWgBlocks * (kc + 1) * filters : 0;
+}
+
+extern "C" int xa_conv1d_wgrad(const void* x, int x_u8, const float* dy, int rows, int width_in,
+                               int channels, int positions, int ksize, int stride, int filters,
+                               float* dw, float* db, int accumulate, float* workspace,
+                               size_t workspace_floats, void* stream) {
+  const size_t need = xa_conv1d_wgrad_workspace_floats(ksize, channels, filters);
+  XA_CHECK_ARG(need > 0, "xa_conv1d_wgrad: needs ksize * channels <= 8 and filters a power of "
+                         "two in [4, 64] (got k %d, C %d, F %d)", ksize, channels, filters);
+  XA_CHECK_ARG(x && dy && dw && db && workspace && workspace_floats >= need,
+               "xa_conv1d_wgrad: null pointer or workspace below %zu floats", need);
+  XA_CHECK_ARG(rows > 0 && positions > 0 && stride > 0 &&
+                   width_in >= (positions - 1) * stride + ksize &&
+                   (int64_t)rows * positions < (1ll << 31) && ((uintptr_t)dy & 15) == 0,
+               "xa_conv1d_wgrad: bad sizes or unaligned dY");
+  hipStream_t s = (hipStream_t)stream;
+  const int kc = ksize * channels;
+  const int align = x_u8 ? 3 : 15;
+  const int vec_x = kc % 4 == 0 && (width_in * channels) % 4 == 0 &&
+                    (stride * channels) % 4 == 0 && ((uintptr_t)x & align) == 0;
+  XaWgradArgs a{x, dy, workspace, rows, width_in, channels, positions, ksize, stride, filters, kc,
+                vec_x};
+  if (x_u8) hipLaunchKernelGGL(conv_wgrad_small_kernel<true>, dim3(kWgBlocks), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(conv_wgrad_small_kernel<false>, dim3(kWgBlocks), dim3(256), 0, s, a);
+  XA_CHECK_LAUNCH("xa_conv1d_wgrad");
+  // fixed-order sums over the blocks: dW [kc][F], then db [F]
+  XaGemmArgs r{};
+  r.M = kc;
+  r.N = filters;
+  r.K = 1;
+  r.c = dw;
+  r.ldc = filters;
+  r.partials = workspace;
+  r.beta = accumulate;
+  r.act = XA_ACT_NONE;
+  hipLaunchKernelGGL(gemm_split_reduce_wide_kernel, dim3((kc * filters + 63) / 64), dim3(1024), 0,
+                     s, r, kWgBlocks);
+  r.M = 1;
+  r.c = db;
+  r.partials = workspace + (size_t)kWgBlocks * kc * filters;
+  hipLaunchKernelGGL(gemm_split_reduce_wide_kernel, dim3((filters + 63) / 64), dim3(1024), 0, s, r,
+                     kWgBlocks);
+  XA_CHECK_LAUNCH("xa_conv1d_wgrad (reduce)");
   return 0;
 }

@@ -92,7 +92,10 @@ def adv_stats(returns, values, batch, mb_size, epochs, shuffle: XaShuffle, stats
 
 
 def ac_grad_blocks(mb_size):
-    return _lib.load().xa_ac_grad_blocks(mb_size)
+    import os
+    cap = int(os.environ.get('XA_AC_BLOCKS', '0'))  # experiment knob: fewer, longer blocks
+    nb = _lib.load().xa_ac_grad_blocks(mb_size)
+    return min(nb, cap) if cap > 0 else nb
 
 
 def ac_grad(args: XaAcGradArgs):

@@ -105,6 +105,10 @@ class LayerExecutor:
                 dcol = max(dcol, rows * P * kC)
         self.workspace = torch.empty(max(ws, 1), **f32)
         self.dcol = torch.empty(max(dcol, 1), **f32)
+        # narrow convs (k C <= 8): weight + bias gradient in one pass (xa_conv1d_wgrad)
+        self.wg_floats = [int(lib.xa_conv1d_wgrad_workspace_floats(l.size, l.in_features, l.filters))
+                          if l.kind == 'convolutional' else 0 for l in self.layers]
+        self.wg_ws = torch.empty(max(self.wg_floats + [1]), **f32)
 
     def _dgrad_ok(self, i):
         """xa_conv1d_dgrad needs F % 4 == 0 and a 16-byte aligned kernel slice."""
@@ -247,7 +251,12 @@ class LayerExecutor:
             else:
                 rows, Win, P, C = self._conv_dims(i, Bb)
                 k, s, F = l.size, l.stride, l.filters
-                if gp is not None:
+                if gp is not None and self.wg_floats[i]:
+                    call('xa_conv1d_wgrad', src.data_ptr(), int(src_u8), d.data_ptr(),
+                         int(rows), int(Win), int(C), int(P), int(k), int(s), int(F),
+                         int(gp + 4 * w0), int(gp + 4 * b0), int(accumulate),
+                         self.wg_ws.data_ptr(), self.wg_floats[i], stream())
+                elif gp is not None:
                     gemm(k * C, F, rows * P, src.data_ptr(), d.data_ptr(), gp + 4 * w0,
                          a_u8=src_u8, a_m=(1, 1, 0), a_k=(P, Win * C, s * C), b_ks=F, b_ns=1,
                          ldc=F, beta=accumulate, workspace=self.workspace)

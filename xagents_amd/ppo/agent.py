@@ -52,6 +52,10 @@ class PPO(A2C):
         super(PPO, self).__init__(envs, model, **kwargs)
 
     def _setup_update(self):
+        import os
+        # optimizer step placement: 'prologue' (next minibatch's xa_ac_grad recomputes it
+        # in every block) or 'kernel' (a standalone xa_clip_adam launch per minibatch)
+        self._opt_kernel = os.environ.get('XA_PPO_OPT', 'prologue') == 'kernel'
         B, MB, E = self.batch_size, self.mini_batch_size, self.ppo_epochs
         # range(0, B, MB) slicing: a ragged last minibatch when MB does not divide B
         # (xagents/ppo/agent.py:152)
@@ -109,8 +113,10 @@ class PPO(A2C):
                 g.adv_in = None
                 g.loss_scale = 1.0 / (count * self.world_size)
                 src = slots[(k - 1) % 2] if k else slots[0]
+                if self._opt_kernel:
+                    src = slots[0]
                 g.theta = src[0].data_ptr()
-                if k:
+                if k and not self._opt_kernel:
                     dst = slots[k % 2]
                     g.pend_grad = self.grad.data_ptr()
                     g.pend_m, g.pend_v = src[1].data_ptr(), src[2].data_ptr()
@@ -118,17 +124,20 @@ class PPO(A2C):
                     g.adam_step = opt.iterations.data_ptr()
                     g.adam = adam
                 self._gargs_list.append(g)
-        self._final_src = slots[(len(self._gargs_list) - 1) % 2]
+        self._final_src = slots[0 if self._opt_kernel else (len(self._gargs_list) - 1) % 2]
         self._tail_bump, self._tail_nobump = self._adam_tail(True), self._adam_tail(False)
 
     def _update(self):
         kernels.minibatches(self._mbargs)
         self._all_reduce(self.adv_stats)
+        last = len(self._gargs_list) - 1
         for i, g in enumerate(self._gargs_list):
             self._kernel_event('ac_grad', i, 0)
             kernels.ac_grad(g)
             self._kernel_event('ac_grad', i, 1)
             self._reduce_gradients(self.partials)
+            if self._opt_kernel and i < last:
+                self._optimizer_step()  # standalone clip + Adam launch
         self._optimizer_step(self._final_src)
 
     def _on_lr_change(self):
