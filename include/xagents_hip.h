@@ -355,6 +355,46 @@ int xa_conv1d_wgrad(const void* x, int x_u8, const float* dy, int rows, int widt
                     float* db, int accumulate, float* workspace, size_t workspace_floats,
                     void* stream);
 
+/* TRPO (xagents/trpo/agent.py). xa_trpo_head: per sample of Categorical(logits_new) vs
+ * Categorical(logits_old) (calculate_losses / calculate_kl_divergence, trpo/agent.py:179-223):
+ * ratio = exp(logp_new(a) - logp_old(a)), KL(old || new), entropy H(new); with dlogits, the
+ * gradient of surrogate_loss = mean(ratio adv) + entropy_coef mean(H) w.r.t. logits_new
+ * (times inv_n = 1 / n). partials: [xa_trpo_head_blocks(n), 3] f64 block sums; out (optional)
+ * receives [surrogate_loss, mean KL, mean H] as f32. */
+typedef struct XaTrpoHeadArgs {
+  int n, n_actions;
+  const float* logits_new;
+  const float* logits_old;
+  int64_t ld_logits;
+  const int* actions;
+  const float* advantages;
+  float entropy_coef, inv_n;
+  float* dlogits;
+  int64_t ld_dlogits;
+  double* partials;
+} XaTrpoHeadArgs;
+
+int xa_trpo_head_blocks(int n);
+int xa_trpo_head(const XaTrpoHeadArgs* args, float* out, void* stream);
+
+/* out[i][a] = scale p_a (t_a - sum_b p_b t_b), p = softmax(logits[i]): the Categorical Fisher
+ * metric on a logit tangent, the middle factor of the Fisher-vector product
+ * (TRPO.calculate_fvp, trpo/agent.py:121-148, evaluated where actor == old actor). */
+int xa_categorical_fisher(const float* logits, int64_t ld_logits, const float* tangent,
+                          int64_t ld_tangent, int n, int n_actions, float scale, float* out,
+                          int64_t ld_out, void* stream);
+
+/* Conjugate-gradient vector algebra (TRPO.conjugate_gradients, trpo/agent.py:150-177):
+ * *out = sum x y (f64, fixed order); out = a x + b y (f32, out may alias x or y). */
+int xa_vec_dot(const float* x, const float* y, int64_t n, double* out, void* stream);
+int xa_axpby(float a, const float* x, float b, const float* y, float* out, int64_t n,
+             void* stream);
+
+/* adv = ((returns - values) - mean) / (std + eps) over the whole batch, population std
+ * (TRPO.train_step, trpo/agent.py:321-324: tf.reduce_mean / tf.math.reduce_std, eps 0). */
+int xa_normalized_advantages(const float* returns, const float* values, int n, float eps,
+                             float* adv, void* stream);
+
 /* DQN.get_actions (xagents/dqn/agent.py:107-116): actions[i] = tf.argmax(q[i]) (first max),
  * or random_actions[i] when use_random (the host draws np.random.random() < epsilon and
  * np.random.randint(0, A, n) exactly as the reference). */

@@ -3,13 +3,14 @@
 Agent registry and command table mirror xagents/__init__.py:18-40. Only the
 agents whose hot path is built are registered (see DESIGN.md for scope).
 """
-from xagents_amd import a2c, ddpg, dqn, ppo, td3
+from xagents_amd import a2c, ddpg, dqn, ppo, td3, trpo
 from xagents_amd.a2c.agent import A2C
 from xagents_amd.base import BaseAgent, OffPolicy, OnPolicy
 from xagents_amd.ddpg.agent import DDPG
 from xagents_amd.dqn.agent import DQN
 from xagents_amd.ppo.agent import PPO
 from xagents_amd.td3.agent import TD3
+from xagents_amd.trpo.agent import TRPO
 from xagents_amd.utils.common import register_models
 
 __version__ = '0.1.0'
@@ -20,7 +21,8 @@ agents = {
     'dqn': {'module': dqn, 'agent': DQN},
     'ddpg': {'module': ddpg, 'agent': DDPG},
     'td3': {'module': td3, 'agent': TD3},
+    'trpo': {'module': trpo, 'agent': TRPO},
 }
 register_models(agents)
 
-__all__ = ['A2C', 'DDPG', 'DQN', 'PPO', 'TD3', 'BaseAgent', 'OnPolicy', 'OffPolicy', 'agents']
+__all__ = ['A2C', 'DDPG', 'DQN', 'PPO', 'TD3', 'TRPO', 'BaseAgent', 'OnPolicy', 'OffPolicy', 'agents']

@@ -180,6 +180,17 @@ class XaAtariStepArgs(Structure):
     ]
 
 
+class XaTrpoHeadArgs(Structure):
+    _fields_ = [
+        ('n', c_int), ('n_actions', c_int),
+        ('logits_new', c_void_p), ('logits_old', c_void_p), ('ld_logits', c_int64),
+        ('actions', c_void_p), ('advantages', c_void_p),
+        ('entropy_coef', c_float), ('inv_n', c_float),
+        ('dlogits', c_void_p), ('ld_dlogits', c_int64),
+        ('partials', c_void_p),
+    ]
+
+
 class XaReplayStepArgs(Structure):
     _fields_ = [
         ('n_envs', c_int), ('t_rec', c_int),
@@ -286,6 +297,16 @@ _SIGNATURES = {
         [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p,
          c_void_p, c_int, c_void_p, ctypes.c_size_t, c_void_p],
     ),
+    'xa_trpo_head_blocks': (c_int, [c_int]),
+    'xa_trpo_head': (c_int, [POINTER(XaTrpoHeadArgs), c_void_p, c_void_p]),
+    'xa_categorical_fisher': (
+        c_int,
+        [c_void_p, c_int64, c_void_p, c_int64, c_int, c_int, c_float, c_void_p, c_int64,
+         c_void_p],
+    ),
+    'xa_vec_dot': (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
+    'xa_axpby': (c_int, [c_float, c_void_p, c_float, c_void_p, c_void_p, c_int64, c_void_p]),
+    'xa_normalized_advantages': (c_int, [c_void_p, c_void_p, c_int, c_float, c_void_p, c_void_p]),
     'xa_dqn_act': (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p]),
     'xa_dqn_td_grad': (
         c_int,

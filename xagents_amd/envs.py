@@ -344,4 +344,10 @@ def create_envs(env_name, n=1, preprocess=False, *args, mode='replay', seed=55, 
         return ReplayVecEnv(env_name, n, t_rec=t_rec, seed=seed, device=device)
     if mode == 'dynamics':
         return CartPoleVecEnv(n, seed=seed, device=device)
+    if mode == 'transitions':
+        # the same CartPole record behind the executor env step (models run by the layer
+        # executor, e.g. TRPO's separate actor and critic)
+        return TransitionReplayVecEnv(env_name, n, (4,), Discrete(2), np.float32, seed=seed,
+                                      device=device,
+                                      record=record_cartpole_replay(n, t_rec, seed))
     raise ValueError(f'Unknown env mode {mode}')

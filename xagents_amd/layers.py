@@ -179,6 +179,50 @@ class LayerExecutor:
                      act=act_code(l.activation), workspace=self.workspace)
         return [self.outs[i] for i in self.model.outputs]
 
+    # ---- forward-mode derivative ------------------------------------------------
+    def jvp(self, v):
+        """Tangents of the output layers along the flat parameter direction `v` (Keras
+        variable order) at the last forward's input: per layer dz = x dW + dx W + db,
+        dy = act'(y) dz, i.e. J v for TRPO's Fisher-vector product (the R-operator of the
+        double tape in xagents/trpo/agent.py:121-148). Returns [B, n] tensors."""
+        if getattr(self, 'touts', None) is None:
+            self.touts = [None if l.kind == 'flatten' else torch.empty_like(self.outs[i])
+                          for i, l in enumerate(self.layers)]
+            for i, l in enumerate(self.layers):
+                if l.kind == 'flatten':
+                    j = self._src_layer(i)
+                    self.touts[i] = None if j == -1 else self.touts[j].reshape(self.B, -1)
+        tp, vp = self.model.theta.data_ptr(), v.data_ptr()
+        u8 = self.x.dtype == torch.uint8
+        for i, l in enumerate(self.layers):
+            if l.kind == 'flatten':
+                continue
+            j = self._src_layer(i)
+            src = self.x if j == -1 else self.outs[j]
+            tsrc = None if j == -1 else self.touts[j]
+            src_u8 = u8 and j == -1
+            w0, b0 = self.offsets[i]
+            out = self.touts[i]
+            if l.kind == 'dense':
+                geo = dict(a_m=(1, l.in_features, 0), b_ks=l.units, b_ns=1, ldc=l.units)
+                M, N, K = self.B, l.units, l.in_features
+            else:
+                rows, Win, P, C = self._conv_dims(i)
+                geo = dict(a_m=(P, Win * C, l.stride * C), b_ks=l.filters, b_ns=1,
+                           ldc=l.filters)
+                M, N, K = rows * P, l.filters, l.size * C
+            # x dW + db, then + dx W (the input tangent, absent for the model input)
+            gemm(M, N, K, src.data_ptr(), vp + 4 * w0, out.data_ptr(), a_u8=src_u8,
+                 bias=vp + 4 * b0, workspace=self.workspace, **geo)
+            if tsrc is not None:
+                gemm(M, N, K, tsrc.data_ptr(), tp + 4 * w0, out.data_ptr(), beta=True,
+                     workspace=self.workspace, **geo)
+            a = act_code(l.activation)
+            if a != XA_ACT_NONE:
+                call('xa_activation_grad', self.outs[i].data_ptr(), out.data_ptr(), out.numel(),
+                     a, out.data_ptr(), stream())
+        return [self.touts[i] for i in self.model.outputs]
+
     # ---- backward ----------------------------------------------------------------
     def backward(self, d_outputs, grad, batch=None, dinput=None, accumulate=False):
         """d_outputs: gradients w.r.t. the output layers (model.outputs order, [b, n]).
