@@ -47,7 +47,7 @@ def parse():
     p.add_argument('--preprocess', action='store_true',
                    help='c3 / c4: AtariWrapper on device (xa_atari_step: frame skip 4, '
                         'gray + resize of synthetic raw 210x160 RGB frames) in every env step')
-    p.add_argument('--config', default='c2', choices=['c2', 'c3', 'c4', 'c5'],
+    p.add_argument('--config', default='c2', choices=['c2', 'c3', 'c4', 'c5', 'trpo'],
                    help='c2 (default, the BASELINE metric line); c3 DQN Pong-shaped, c4 PPO '
                         'CNN Breakout-shaped (global 1024 envs, strong scaling), c5 TD3')
     return p.parse_args()
@@ -200,6 +200,24 @@ def bench_offpolicy_and_cnn(args):
                                         'sharded over the GPUs, NatureCNN (Conv1D cfg), n_steps '
                                         '128, 4x4 minibatches (BASELINE configs[3])',
                             'n_envs_per_gpu': n, 'parallelism': f'dp{world}'})
+    elif args.config == 'trpo':
+        from xagents_amd import TRPO
+        if world > 1:
+            raise SystemExit('bench --config trpo runs on one GPU (TRPO is not data parallel)')
+        n, T = 16, 512  # the reference's headline env count; trpo/cli.py n-steps default
+        envs = create_envs('CartPole-v1', n, mode='transitions', device=device,
+                           seed=args.seed, t_rec=4096)
+        actor = create_model(envs, 'trpo', 'actor_model', seed=args.seed, device=device)
+        critic = create_model(envs, 'trpo', 'critic_model', seed=args.seed + 1, device=device)
+        agent = TRPO(envs, actor, critic, n_steps=T, seed=args.seed, quiet=True)
+        el = _timed(agent.train_step, args.steps, args.warmup, world)
+        env_steps = n * T * args.steps
+        line.update(scaling='weak', data='synthetic: CartPole-v1 observation replay recorded '
+                    'on the host (seed 55), random-init actor and critic', config={
+                        'workload': 'TRPO CartPole-v1, 16 envs, n_steps 512, MLP actor / critic '
+                                    '[64, 64] relu, CG 10 x FVP on every 5th state, line '
+                                    'search, 3 x 4 x 4 critic minibatches (SURVEY 8f rank 2)',
+                        'n_envs_per_gpu': n, 'parallelism': 'dp1'})
     else:
         from xagents_amd import TD3
         n = max(64 // world, 1)

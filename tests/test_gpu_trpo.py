@@ -98,6 +98,22 @@ def test_trpo_train_step_vs_f64(device):
     assert int(agent.critic.optimizer.iterations.cpu()[0]) == len(perms) * agent.mini_batches
 
 
+def test_trpo_rollout_graph_matches_eager(device):
+    """The captured rollout replays exactly what the eager launches compute."""
+    outs = []
+    for use_graph in (False, True):
+        agent = _agent(device, n_envs=4, n_steps=16, seed=5, use_graph=use_graph)
+        got = []
+        for _ in range(3):
+            agent.get_batch()
+            got.append([t.cpu().numpy().copy() for t in (agent.batch_states, agent.b_act,
+                                                         agent.b_logp, agent.b_ret)])
+        outs.append(got)
+    for a, b in zip(*outs):
+        for x, y in zip(a, b):
+            np.testing.assert_array_equal(x, y)
+
+
 def test_trpo_fit_runs(device):
     agent = _agent(device, n_envs=4, n_steps=64, seed=3)
     agent.fit(max_steps=4 * 64 * 3)

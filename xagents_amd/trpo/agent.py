@@ -78,7 +78,8 @@ class TRPO(PPO):
         self.entropy_coef = entropy_coef
         self.value_loss_coef = value_loss_coef
         self.grad_norm = grad_norm
-        self.use_graph = False
+        self.use_graph = use_graph  # rollout replayed from a hipGraph after one eager pass
+        self._rgraph = None
         self.executor_path = True
         if not isinstance(self.envs[0].action_space, Discrete):
             raise NotImplementedError('Only Categorical(logits) policies are supported')
@@ -155,7 +156,7 @@ class TRPO(PPO):
         self.w0 = torch.zeros(P, **f32)
         self.full_step = torch.zeros(P, **f32)
         # critic minibatch buffers
-        self.mb_slots = torch.zeros(mb, dtype=torch.int64, device=dev)
+        self.critic_slots = None
         self.mb_states = torch.zeros((mb,) + env.obs_shape, dtype=env.state.dtype, device=dev)
         self.mb_ret = torch.zeros(mb, **f32)
         self.dvalue = torch.zeros(mb, 1, **f32)
@@ -179,6 +180,25 @@ class TRPO(PPO):
                 self.b_val.reshape(B), self.b_logp.reshape(B)]
 
     def _rollout(self):
+        """The rollout launches (~11 per env step) are host-bound when launched one by one
+        from Python; after one eager pass they are captured once and replayed."""
+        if not self.use_graph:
+            self._rollout_kernels()
+        elif self._rgraph is not None:
+            self._rgraph.replay()
+        elif getattr(self, '_rollout_warm', False):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._rollout_kernels()
+            self._rgraph = g
+            g.replay()
+        else:
+            self._rollout_kernels()
+            self._rollout_warm = True
+        self.steps += self.n_envs * self.n_steps
+        self._queue_episode_stats(self.b_done, self.b_epret)
+
+    def _rollout_kernels(self):
         N, T = self.n_envs, self.n_steps
         env, a = self.envs, self._sa
         self.obs_buf[0].copy_(env.state)
@@ -213,8 +233,6 @@ class TRPO(PPO):
         # env-major batch of the states the reference concatenates (base.py:549-564)
         call('xa_ring_gather', self.obs_buf.data_ptr(), self.batch_states.data_ptr(),
              self._batch_slots.data_ptr(), self.batch_size, env.obs_bytes, stream())
-        self.steps += N * T
-        self._queue_episode_stats(self.b_done, self.b_epret)
 
     # ---- actor pieces ------------------------------------------------------------------
     def _head(self, logits_new, dlogits=None, out=None):
@@ -306,30 +324,52 @@ class TRPO(PPO):
 
     def update_critic_weights(self):
         """critic_iterations x PPO minibatches of mean((V - R)^2), Keras Adam
-        (trpo/agent.py:280-299)."""
+        (trpo/agent.py:280-299). Every epoch's permutation (numpy's global RNG, one per
+        epoch as get_mini_batches draws them) is uploaded in one copy; the minibatch
+        launches are captured once and replayed like the rollout."""
+        B = self.batch_size
+        n_perm = self.critic_iterations * self.ppo_epochs
+        perms = np.stack([np.random.permutation(B) for _ in range(n_perm)])
+        if getattr(self, 'critic_slots', None) is None or self.critic_slots.shape[0] != n_perm:
+            self.critic_slots = torch.zeros(n_perm, B, dtype=torch.int64, device=self.device)
+            self._cgraph = None
+        self.critic_slots.copy_(torch.from_numpy(perms), non_blocking=False)
+        if not self.use_graph:
+            self._critic_kernels()
+        elif self._cgraph is not None:
+            self._cgraph.replay()
+        elif getattr(self, '_critic_warm', False):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._critic_kernels()
+            self._cgraph = g
+            g.replay()
+        else:
+            self._critic_kernels()
+            self._critic_warm = True
+
+    def _critic_kernels(self):
         B, mb = self.batch_size, self.mini_batch_size
         opt = self.critic.optimizer
         ret = self.b_ret.reshape(B)
-        for _ in range(self.critic_iterations):
-            for _e in range(self.ppo_epochs):
-                perm = np.random.permutation(B)
-                for i in range(0, B, mb):  # a ragged last slice as ppo/agent.py:152
-                    n = min(mb, B - i)
-                    self.mb_slots[:n].copy_(torch.from_numpy(perm[i:i + n]))
-                    call('xa_ring_gather', self.batch_states.data_ptr(), self.mb_states.data_ptr(),
-                         self.mb_slots.data_ptr(), n, self.envs.obs_bytes, stream())
-                    call('xa_ring_gather', ret.data_ptr(), self.mb_ret.data_ptr(),
-                         self.mb_slots.data_ptr(), n, 4, stream())
-                    v = self.ex_critic.forward(self.mb_states)[0]
-                    # d mean((v - R)^2) / dv = 2 (v - R) / n: xa_mse_grad gives 2 (v - R),
-                    # the 1 / n rides on Adam's grad_scale (rows past n are never used)
-                    call('xa_mse_grad', v.data_ptr(), self.mb_ret.data_ptr(), n, 1,
-                         self.dvalue.data_ptr(), None, stream())
-                    self.ex_critic.backward([self.dvalue[:n]], self.critic_grad, batch=n)
-                    call('xa_adam_step_bump', opt.iterations.data_ptr(), stream())
-                    kernels.clip_adam(self.critic.theta, opt.m, opt.v, self.critic_grad,
-                                      opt.iterations, opt.learning_rate, opt.beta_1, opt.beta_2,
-                                      opt.epsilon, grad_scale=1.0 / n, workspace=self.adam_ws)
+        for k in range(self.critic_slots.shape[0]):
+            for i in range(0, B, mb):  # a ragged last slice as ppo/agent.py:152
+                n = min(mb, B - i)
+                slots = self.critic_slots.data_ptr() + 8 * (k * B + i)
+                call('xa_ring_gather', self.batch_states.data_ptr(), self.mb_states.data_ptr(),
+                     slots, n, self.envs.obs_bytes, stream())
+                call('xa_ring_gather', ret.data_ptr(), self.mb_ret.data_ptr(), slots, n, 4,
+                     stream())
+                v = self.ex_critic.forward(self.mb_states)[0]
+                # d mean((v - R)^2) / dv = 2 (v - R) / n: xa_mse_grad gives 2 (v - R),
+                # the 1 / n rides on Adam's grad_scale (rows past n are never used)
+                call('xa_mse_grad', v.data_ptr(), self.mb_ret.data_ptr(), n, 1,
+                     self.dvalue.data_ptr(), None, stream())
+                self.ex_critic.backward([self.dvalue[:n]], self.critic_grad, batch=n)
+                call('xa_adam_step_bump', opt.iterations.data_ptr(), stream())
+                kernels.clip_adam(self.critic.theta, opt.m, opt.v, self.critic_grad,
+                                  opt.iterations, opt.learning_rate, opt.beta_1, opt.beta_2,
+                                  opt.epsilon, grad_scale=1.0 / n, workspace=self.adam_ws)
 
     def train_step(self):
         """trpo/agent.py:301-348."""
