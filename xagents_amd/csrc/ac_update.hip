@@ -102,11 +102,15 @@ __host__ __device__ inline int stats_chunks(int mb_size) {
 }
 
 // ---------------------------------------------------------------------------
-// minibatch preparation: one block per (epoch, minibatch, 1024-sample chunk)
+// minibatch preparation: one block per (epoch, minibatch, 1024-sample chunk), one thread
+// per sample (the shuffle index -> scattered loads -> stores chain runs once per thread)
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void minibatch_kernel(XaMinibatchArgs a, int n_mb,
-                                                        int n_chunks) {
-  __shared__ double red[2][4];
+constexpr int kMbThreads = kStatsChunk;
+
+__global__ __launch_bounds__(kMbThreads) void minibatch_kernel(XaMinibatchArgs a, int n_mb,
+                                                               int n_chunks) {
+  constexpr int NW = kMbThreads / 64;
+  __shared__ double red[2][NW];
   const int sidx = blockIdx.x / n_chunks, chunk = blockIdx.x % n_chunks;
   const int e = sidx / n_mb, m = sidx % n_mb;
   const ShuffleKeys keys = shuffle_keys(a.shuffle, e, a.batch);
@@ -140,8 +144,14 @@ __global__ __launch_bounds__(256) void minibatch_kernel(XaMinibatchArgs a, int n
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    a.stats[(size_t)blockIdx.x * 2 + 0] = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
-    a.stats[(size_t)blockIdx.x * 2 + 1] = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+    double t1 = 0.0, t2 = 0.0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      t1 += red[0][w];
+      t2 += red[1][w];
+    }
+    a.stats[(size_t)blockIdx.x * 2 + 0] = t1;
+    a.stats[(size_t)blockIdx.x * 2 + 1] = t2;
   }
 }
 
@@ -784,7 +794,7 @@ extern "C" int xa_ppo_minibatches(const XaMinibatchArgs* a, void* stream) {
                "xa_ppo_minibatches: gather needs obs/actions/old_logp and every mb_* output");
   const int n_mb = (a->batch + a->mb_size - 1) / a->mb_size;
   const int nc = stats_chunks(a->mb_size);
-  hipLaunchKernelGGL(minibatch_kernel, dim3(a->epochs * n_mb * nc), dim3(256), 0,
+  hipLaunchKernelGGL(minibatch_kernel, dim3(a->epochs * n_mb * nc), dim3(kMbThreads), 0,
                      (hipStream_t)stream, *a, n_mb, nc);
   XA_CHECK_LAUNCH("xa_ppo_minibatches");
   return 0;
