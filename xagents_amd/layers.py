@@ -114,6 +114,22 @@ class LayerExecutor:
         """xa_conv1d_dgrad needs F % 4 == 0 and a 16-byte aligned kernel slice."""
         return self.layers[i].filters % 4 == 0 and self.offsets[i][0] % 4 == 0
 
+    # ---- optional per-launch timing (bench): HIP events on the launch stream ----
+    timing = None  # a list to collect (name, start event, end event, flops) into
+
+    def _timing_start(self):
+        if self.timing is None:
+            return None
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        return e
+
+    def _timing_end(self, e0, name, flops):
+        if e0 is not None:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            self.timing.append((name, e0, e1, flops))
+
     # ---- shapes --------------------------------------------------------------
     def _src_shape(self, i):
         l = self.layers[i]
@@ -287,10 +303,12 @@ class LayerExecutor:
                          workspace=self.workspace)
                 if j != -1:
                     # dX = dZ W^T (gated by the source layer's ReLU), accumulated over heads
+                    ev = self._timing_start()
                     gemm(Bb, n_in, n_out, d.data_ptr(), tp + 4 * w0,
                          self.douts[j].data_ptr(), a_m=(1, n_out, 0), b_ks=1, b_ns=n_out,
                          ldc=n_in, gate=gate_j, ld_gate=n_in if gate_j else 0,
                          beta=written[j], workspace=self.workspace)
+                    self._timing_end(ev, f'dense dX {Bb}x{n_in}x{n_out}', 2.0 * Bb * n_in * n_out)
                     written[j] = True
             else:
                 rows, Win, P, C = self._conv_dims(i, Bb)
