@@ -230,7 +230,11 @@ template <int WM, int WN, bool A_KMAJOR, bool B_NMAJOR, bool A_U8>
 __global__ __launch_bounds__(256) void gemm_tile_kernel(XaGemmK kargs) {
   const XaGemmArgs& g = kargs.g;
   const bool vec_a = kargs.vec_a, vec_b = kargs.vec_b;
-  constexpr int TBM = 64 * WM, TBN = 64 * WN, TLA = TBM + 4, TLB = TBN + 4;
+  // LDS row pitch: a k-major operand is stashed one float per row (4 rows per thread), so
+  // a pitch = 1 (mod 8) spreads a wave's 32-lane write group over all 32 banks; an m- /
+  // n-major operand is stashed as one 16-B write per thread (pitch a multiple of 4)
+  constexpr int TBM = 64 * WM, TBN = 64 * WN;
+  constexpr int TLA = A_KMAJOR ? TBM + 1 : TBM + 4, TLB = B_NMAJOR ? TBN + 4 : TBN + 1;
   constexpr int EA = TBM * TBK / 256, EB = TBN * TBK / 256;  // elements per thread
   __shared__ __attribute__((aligned(16))) float As[2][TBK * TLA];
   __shared__ __attribute__((aligned(16))) float Bs[2][TBK * TLB];
@@ -317,29 +321,25 @@ __global__ __launch_bounds__(256) void gemm_tile_kernel(XaGemmK kargs) {
     }
   };
   auto stash = [&](int buf) {
+    if (A_KMAJOR) {
 #pragma unroll
-    for (int e = 0; e < EA; ++e) {
-      int ml, kl;
-      if (A_KMAJOR) {
-        ml = (tid >> 3) + 32 * (e >> 2);
-        kl = (tid & 7) * 4 + (e & 3);
-      } else {
-        ml = (tid % AQ) * 4 + (e & 3);
-        kl = tid / AQ + AKR * (e >> 2);
-      }
-      As[buf][kl * TLA + ml] = ra[e];
+      for (int e = 0; e < EA; ++e)
+        As[buf][((tid & 7) * 4 + (e & 3)) * TLA + (tid >> 3) + 32 * (e >> 2)] = ra[e];
+    } else {
+#pragma unroll
+      for (int r = 0; r < EA / 4; ++r)
+        *reinterpret_cast<f32x4*>(&As[buf][(tid / AQ + AKR * r) * TLA + (tid % AQ) * 4]) =
+            f32x4{ra[4 * r], ra[4 * r + 1], ra[4 * r + 2], ra[4 * r + 3]};
     }
+    if (B_NMAJOR) {
 #pragma unroll
-    for (int e = 0; e < EB; ++e) {
-      int nl, kl;
-      if (B_NMAJOR) {
-        nl = (tid % BQ) * 4 + (e & 3);
-        kl = tid / BQ + BKR * (e >> 2);
-      } else {
-        nl = (tid >> 3) + 32 * (e >> 2);
-        kl = (tid & 7) * 4 + (e & 3);
-      }
-      Bs[buf][kl * TLB + nl] = rb[e];
+      for (int r = 0; r < EB / 4; ++r)
+        *reinterpret_cast<f32x4*>(&Bs[buf][(tid / BQ + BKR * r) * TLB + (tid % BQ) * 4]) =
+            f32x4{rb[4 * r], rb[4 * r + 1], rb[4 * r + 2], rb[4 * r + 3]};
+    } else {
+#pragma unroll
+      for (int e = 0; e < EB; ++e)
+        Bs[buf][((tid & 7) * 4 + (e & 3)) * TLB + (tid >> 3) + 32 * (e >> 2)] = rb[e];
     }
   };
 
