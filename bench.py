@@ -136,6 +136,36 @@ def _timed(fn, steps, warmup, world):
     return el
 
 
+def cnn_cpu_baseline(args, kind):
+    """Bounded CPU sample of the C3 / C4 workload (oracle/cpu_cnn.py, kind "port")."""
+    sys.path.insert(0, str(ROOT / 'oracle'))
+    import numpy as np
+    import torch
+    import cpu_cnn
+    from xagents_amd.envs import record_transitions
+    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    if kind == 'c4':
+        n, T = 16, 128
+        rec = record_transitions(n, 256, (84, 84, 1), np.uint8, seed=args.seed)
+        value, info = cpu_cnn.time_cnn_ppo(rec, n_steps=T, seconds=args.cpu_baseline_seconds,
+                                           threads=threads)
+        sample = (f"{info['train_steps']} PPO-CNN train steps of {n} envs x {T} steps (4x4 "
+                  f"minibatches of 512) in {info['seconds']:.1f} s: per-env Python step_envs "
+                  f"loop, torch-CPU f32 Conv1D/dense + autograd, numpy GAE, Keras Adam "
+                  f"(oracle/cpu_cnn.py); the GPU line runs 1024 envs")
+    else:
+        n = 32
+        rec = record_transitions(n, 256, (84, 84, 1), np.uint8, seed=args.seed)
+        value, info = cpu_cnn.time_dqn(rec, seconds=args.cpu_baseline_seconds, threads=threads)
+        sample = (f"{info['train_steps']} double-DQN train steps of {n} envs (batch 64 from "
+                  f"per-env deques of 1000) in {info['seconds']:.1f} s: per-env Python "
+                  f"step_envs loop, random.sample replay, torch-CPU f32 NatureCNN + autograd, "
+                  f"Keras Adam (oracle/cpu_cnn.py)")
+    torch.set_num_threads(threads)
+    return {'value': round(value, 2), 'unit': 'env-steps/s', 'cores': info['threads'],
+            'kind': 'port', 'sample': sample}
+
+
 def _raw_kw(args, n):
     return {'t_raw_frames': 64 if n <= 64 else 16} if args.preprocess else {}
 
@@ -262,6 +292,8 @@ def bench_offpolicy_and_cnn(args):
                     gradient_step_ms=round(g_el / args.steps * 1e3, 4))
     line['value'] = round(env_steps / el, 1)
     line['ms_per_step'] = round(el / args.steps * 1e3, 4)
+    if rank == 0 and world == 1 and args.config in ('c3', 'c4') and args.cpu_baseline_seconds > 0:
+        line['cpu_baseline'] = cnn_cpu_baseline(args, args.config)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
