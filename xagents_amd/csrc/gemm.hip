@@ -116,6 +116,21 @@ __global__ __launch_bounds__(256) void gemm_kernel(XaGemmK kargs) {
   const uint8_t* au = static_cast<const uint8_t*>(g.a);
 
   float ra[4], rb[4];
+
+  // interior fast path (as gemm_tile_kernel): fixed bases + k strides, no bounds tests
+  const bool fast = vec_a && vec_b && (A_KMAJOR || g.a_pk == 1) && m0 + BM <= g.M &&
+                    n0 + BN <= g.N && (k_end - k_begin) % BK == 0;
+  int64_t fa = 0, fb = 0;
+  const int64_t fa_k = A_KMAJOR ? 1 : g.a_rk, fb_k = g.b_ks;
+  if (fast) {
+    fa = A_KMAJOR ? a_row[0] + k_begin + a_k : a_row[0] + (int64_t)(k_begin + a_k) * g.a_rk;
+    fb = (int64_t)(k_begin + b_k) * g.b_ks + (int64_t)(n0 + b_n) * g.b_ns;
+  }
+  auto load_fast = [&](int kt) {
+    const int64_t dk = kt - k_begin;
+    ld4<A_U8>(g.a, fa + dk * fa_k, ra);
+    ld4<false>(g.b, fb + dk * fb_k, rb);
+  };
   auto load = [&](int kt) {
     if (vec_a) {
       // one run: 4 k of row a_m (k-major) or 4 m at column a_k
@@ -167,13 +182,17 @@ __global__ __launch_bounds__(256) void gemm_kernel(XaGemmK kargs) {
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
 
   if (k_begin < k_end) {
-    load(k_begin);
+    if (fast) load_fast(k_begin);
+    else load(k_begin);
     stash(0);
     __syncthreads();
     int buf = 0;
     for (int kt = k_begin; kt < k_end; kt += BK) {
       const bool more = kt + BK < k_end;
-      if (more) load(kt + BK);
+      if (more) {
+        if (fast) load_fast(kt + BK);
+        else load(kt + BK);
+      }
       const float* as = As[buf];
       const float* bs = Bs[buf];
 #pragma unroll
@@ -262,6 +281,41 @@ __global__ __launch_bounds__(256) void gemm_tile_kernel(XaGemmK kargs) {
   const float* af = static_cast<const float*>(g.a);
   const uint8_t* au = static_cast<const uint8_t*>(g.a);
   float ra[EA], rb[EB];
+
+  // Interior fast path: every row / column of the tile exists, the split's K range is whole
+  // K steps, both operands load as 16-B runs and A's k offset is linear (no im2col on k).
+  // Then each run's address is a base fixed at k_begin plus (kt - k_begin) x its k stride,
+  // and the loads need no bounds tests or index arithmetic per step.
+  const bool a_lin = A_KMAJOR || g.a_pk == 1;
+  const bool fast = vec_a && vec_b && a_lin && m0 + TBM <= g.M && n0 + TBN <= g.N &&
+                    (k_end - k_begin) % TBK == 0;
+  constexpr int RA = EA / 4, RB = EB / 4;
+  int64_t a_base[RA], b_base[RB];
+  int64_t a_kstride = 1, b_kstride = g.b_ks;
+  if (fast) {
+#pragma unroll
+    for (int r = 0; r < RA; ++r) {
+      if (A_KMAJOR) {
+        a_base[r] = a_row[r] + k_begin + (tid & 7) * 4;
+      } else {
+        a_base[r] = a_row[0] + (int64_t)(k_begin + tid / AQ + AKR * r) * g.a_rk;
+      }
+    }
+    a_kstride = A_KMAJOR ? 1 : g.a_rk;
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      const int n = B_NMAJOR ? n0 + (tid % BQ) * 4 : n0 + (tid >> 3) + 32 * r;
+      const int k = B_NMAJOR ? k_begin + tid / BQ + BKR * r : k_begin + (tid & 7) * 4;
+      b_base[r] = (int64_t)k * g.b_ks + (int64_t)n * g.b_ns;
+    }
+  }
+  auto load_fast = [&](int kt) {
+    const int64_t dk = kt - k_begin;
+#pragma unroll
+    for (int r = 0; r < RA; ++r) ld4<A_U8>(g.a, a_base[r] + dk * a_kstride, ra + 4 * r);
+#pragma unroll
+    for (int r = 0; r < RB; ++r) ld4<false>(g.b, b_base[r] + dk * b_kstride, rb + 4 * r);
+  };
 
   auto load = [&](int kt) {
     if (vec_a) {
@@ -352,13 +406,17 @@ __global__ __launch_bounds__(256) void gemm_tile_kernel(XaGemmK kargs) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
 
   if (k_begin < k_end) {
-    load(k_begin);
+    if (fast) load_fast(k_begin);
+    else load(k_begin);
     stash(0);
     __syncthreads();
     int buf = 0;
     for (int kt = k_begin; kt < k_end; kt += TBK) {
       const bool more = kt + TBK < k_end;
-      if (more) load(kt + TBK);
+      if (more) {
+        if (fast) load_fast(kt + TBK);
+        else load(kt + TBK);
+      }
       const float* as = As[buf] + wm * 64 + (lane & 31);
       const float* bs = Bs[buf] + wn * 64 + (lane & 31);
 #pragma unroll
