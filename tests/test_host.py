@@ -240,3 +240,15 @@ def test_replay_record_is_consistent():
     np.testing.assert_array_equal(obs[:, :-1][nd], post[:, :-1][nd])
     assert np.all(np.abs(post[:, :-1][done[:, :-1] == 1]) <= 0.05)
     assert 0.01 < done.mean() < 0.2 and np.all(rew == 1)
+
+
+def test_rb2_batched_randint_matches_per_buffer_calls():
+    """DeviceReplay.sample_slots draws all RB2 indices in one randint call when every
+    buffer has the same size: legacy numpy yields exactly the values of the reference's
+    per-buffer np.random.randint(0, size, k) calls in env order (buffers.py:137-148)."""
+    for size, n, k in ((5, 64, 2), (31250, 32, 2), (1000, 7, 3), (2 ** 20 + 7, 4, 1)):
+        np.random.seed(11)
+        ref = np.concatenate([np.random.randint(0, size, k) for _ in range(n)])
+        np.random.seed(11)
+        got = np.random.randint(0, size, n * k)
+        np.testing.assert_array_equal(ref, got)

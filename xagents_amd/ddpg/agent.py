@@ -155,13 +155,46 @@ class DDPG(OffPolicy):
         return [self.s, self.a, self.r, self.d, self.s2]
 
     def update_weights(self, gradient_steps):
-        """ddpg/agent.py:129-147"""
+        """ddpg/agent.py:129-147. The sample indices come from the host RNG exactly as
+        before; the device work of a gradient step (gather, critic update; actor update and
+        Polyak sync) is captured once per phase and replayed as hipGraphs, since at batch
+        sizes like 64 its ~40 small launches are launch-bound when issued from Python."""
         for gradient_step in range(int(gradient_steps)):
-            self.concat_buffer_samples()
-            self.update_critic_weights()
+            self.replay.upload_slots(self.replay.sample_slots())
+            self._run_phase('critic', self._critic_phase)
             if gradient_step % self.policy_delay == 0:
-                self.update_actor_weights()
-                self.sync_target_models()
+                self._run_phase('actor', self._actor_phase)
+
+    def _critic_phase(self):
+        self.replay.gather(self.replay.slots, self.s, self.a, self.r, self.d, self.s2)
+        self.update_critic_weights()
+
+    def _actor_phase(self):
+        self.update_actor_weights()
+        self.sync_target_models()
+
+    def _run_phase(self, name, fn):
+        """Eager once, then captured and replayed. Data-parallel steps stay eager (their
+        gradient all-reduce is a torch collective)."""
+        graphs = self.__dict__.setdefault('_graphs', {})
+        warm = self.__dict__.setdefault('_warm', set())
+        if not getattr(self, 'use_graph', True) or self.distributed:
+            fn()
+        elif name in graphs:
+            graphs[name].replay()
+        elif name in warm:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                fn()
+            graphs[name] = g
+            g.replay()
+        else:
+            fn()
+            warm.add(name)
+
+    def _on_lr_change(self):
+        self.__dict__['_graphs'] = {}  # the learning rates are baked into the launches
+        self.__dict__['_warm'] = set()
 
     def train_step(self):
         """ddpg/agent.py:149-166: step every env, then for each env that finished an

@@ -86,6 +86,12 @@ class DeviceReplay:
     def sample_slots(self):
         """Ring slots of one concat_buffer_samples batch (env-major), reference RNG."""
         out = np.empty(self.n * self.k, np.int64)
+        if self.kind == XA_RING_RB2 and (self.host_count == self.host_count[0]).all():
+            # equal sizes: one randint(0, size, n k) draws the same legacy-RNG values as the
+            # reference's n sequential randint(0, size, k) calls (tests/test_host.py)
+            size = min(int(self.host_count[0]), self.cap)
+            idx = np.random.randint(0, size, self.n * self.k).astype(np.int64)
+            return np.repeat(np.arange(self.n, dtype=np.int64) * self.cap, self.k) + idx
         for i in range(self.n):
             cnt = int(self.host_count[i])
             if self.kind == XA_RING_RB2:
