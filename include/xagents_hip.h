@@ -563,6 +563,44 @@ typedef struct XaHeadGradArgs {
 
 int xa_ac_head_grad(const XaHeadGradArgs* args, void* stream);
 
+/* ACER loss gradient of a batch of n_envs trajectories (ACER.update_gradients,
+ * xagents/acer/agent.py:295-347; calculate_returns 171-208; calculate_losses 210-260;
+ * calculate_grads 262-293). Rows are env-major [n_envs, n_steps + 1] (acer/agent.py:164-169):
+ * logits / q / avg_logits are the model's actor (pre-softmax) and critic outputs and the
+ * average model's actor output on every row; mu_logits [n_envs, n_steps, A] the behaviour
+ * policy's actor logits; actions / rewards / dones [n_envs, n_steps]. Writes dlogits
+ * (gradient w.r.t. the pre-softmax logits) and dq for every row (zero on the bootstrap row
+ * t = n_steps), the Retrace returns (optional) and per-env loss partials env_loss[n_envs][4]
+ * = [sum gain, sum entropy, sum 0.5 (R - Q_a)^2, trust-region adjustments] (optional).
+ * n_total = the batch's n_envs x n_steps over all ranks (the mean's denominator). */
+typedef struct XaAcerArgs {
+  int n_envs, n_steps, n_actions, n_total;
+  const float* logits;
+  int64_t ld_logits;
+  const float* q;
+  int64_t ld_q;
+  const float* avg_logits;
+  int64_t ld_avg;
+  const float* mu_logits;
+  const int* actions;
+  const float* rewards;
+  const float* dones;
+  float gamma, epsilon, importance_c, delta, entropy_coef, value_coef;
+  int trust_region;
+  float* dlogits;
+  int64_t ld_dlogits;
+  float* dq;
+  int64_t ld_dq;
+  float* returns;
+  float* env_loss;
+} XaAcerArgs;
+
+int xa_acer_grad(const XaAcerArgs* args, void* stream);
+
+/* shadow -= (shadow - var) (1 - decay): tf.train.ExponentialMovingAverage.apply without
+ * zero-debias (ACER average model, acer/agent.py:46,114-125,346). */
+int xa_ema(float* shadow, const float* var, int64_t n, float decay, void* stream);
+
 /* Keras OptimizerV2 `iterations += 1` on device (before xa_clip_adam reads t). */
 int xa_adam_step_bump(int* adam_step, void* stream);
 

@@ -5,7 +5,7 @@ reference's .cfg models are built from (xagents/utils/common.py:169-290):
 * Conv1D (valid padding, common.py:231-237) applied to rank-4 (B, H, W, C) input: the
   convolution runs along W with H folded into the batch; kernel (k, C_in, F);
 * Flatten: row-major over (H, W', F) (common.py:259-260);
-* activations relu / tanh / linear.
+* activations relu / tanh / linear (softmax outputs as logits).
 
 `forward` returns every layer output; `backward` takes d(loss)/d(output) for each
 output layer and returns the flat parameter gradient in Keras trainable_variables
@@ -20,7 +20,9 @@ def _act(name, z):
         return np.maximum(z, 0.0)
     if name == 'tanh':
         return np.tanh(z)
-    assert name in (None, 'linear'), name
+    # a softmax output layer yields its pre-softmax logits (the ACER actor): the loss
+    # restatement applies the softmax, as the device executor does
+    assert name in (None, 'linear', 'softmax'), name
     return z
 
 

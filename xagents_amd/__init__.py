@@ -3,8 +3,9 @@
 Agent registry and command table mirror xagents/__init__.py:18-40. Only the
 agents whose hot path is built are registered (see DESIGN.md for scope).
 """
-from xagents_amd import a2c, ddpg, dqn, ppo, td3, trpo
+from xagents_amd import a2c, acer, ddpg, dqn, ppo, td3, trpo
 from xagents_amd.a2c.agent import A2C
+from xagents_amd.acer.agent import ACER
 from xagents_amd.base import BaseAgent, OffPolicy, OnPolicy
 from xagents_amd.ddpg.agent import DDPG
 from xagents_amd.dqn.agent import DQN
@@ -17,6 +18,7 @@ __version__ = '0.1.0'
 
 agents = {
     'a2c': {'module': a2c, 'agent': A2C},
+    'acer': {'module': acer, 'agent': ACER},
     'ppo': {'module': ppo, 'agent': PPO},
     'dqn': {'module': dqn, 'agent': DQN},
     'ddpg': {'module': ddpg, 'agent': DDPG},
@@ -25,4 +27,4 @@ agents = {
 }
 register_models(agents)
 
-__all__ = ['A2C', 'DDPG', 'DQN', 'PPO', 'TD3', 'TRPO', 'BaseAgent', 'OnPolicy', 'OffPolicy', 'agents']
+__all__ = ['A2C', 'ACER', 'DDPG', 'DQN', 'PPO', 'TD3', 'TRPO', 'BaseAgent', 'OnPolicy', 'OffPolicy', 'agents']

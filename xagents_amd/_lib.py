@@ -221,6 +221,23 @@ class XaHeadGradArgs(Structure):
     ]
 
 
+class XaAcerArgs(Structure):
+    _fields_ = [
+        ('n_envs', c_int), ('n_steps', c_int), ('n_actions', c_int), ('n_total', c_int),
+        ('logits', c_void_p), ('ld_logits', c_int64),
+        ('q', c_void_p), ('ld_q', c_int64),
+        ('avg_logits', c_void_p), ('ld_avg', c_int64),
+        ('mu_logits', c_void_p), ('actions', c_void_p), ('rewards', c_void_p),
+        ('dones', c_void_p),
+        ('gamma', c_float), ('epsilon', c_float), ('importance_c', c_float), ('delta', c_float),
+        ('entropy_coef', c_float), ('value_coef', c_float),
+        ('trust_region', c_int),
+        ('dlogits', c_void_p), ('ld_dlogits', c_int64),
+        ('dq', c_void_p), ('ld_dq', c_int64),
+        ('returns', c_void_p), ('env_loss', c_void_p),
+    ]
+
+
 XA_PEER_MAX = 16
 XA_DTYPE_F32 = 0
 XA_DTYPE_F64 = 1
@@ -327,6 +344,8 @@ _SIGNATURES = {
          c_void_p, c_void_p, c_void_p, c_int64, c_void_p],
     ),
     'xa_ac_head_grad': (c_int, [POINTER(XaHeadGradArgs), c_void_p]),
+    'xa_acer_grad': (c_int, [POINTER(XaAcerArgs), c_void_p]),
+    'xa_ema': (c_int, [c_void_p, c_void_p, c_int64, c_float, c_void_p]),
     'xa_noisy_actions': (
         c_int,
         [c_void_p, c_int64, c_int, c_int, c_float, c_float, c_float, c_float, c_void_p,

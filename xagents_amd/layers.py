@@ -110,6 +110,15 @@ class LayerExecutor:
                           if l.kind == 'convolutional' else 0 for l in self.layers]
         self.wg_ws = torch.empty(max(self.wg_floats + [1]), **f32)
 
+    def _act(self, i):
+        """Epilogue of layer i. A softmax output layer (the ACER actor,
+        xagents/acer/models/cnn-actor-critic.cfg) yields its pre-softmax logits: the loss
+        head applies the softmax and returns the gradient w.r.t. the logits."""
+        name = self.layers[i].activation
+        if name == 'softmax' and i in self.model.outputs:
+            return XA_ACT_NONE
+        return act_code(name)
+
     def _dgrad_ok(self, i):
         """xa_conv1d_dgrad needs F % 4 == 0 and a 16-byte aligned kernel slice."""
         return self.layers[i].filters % 4 == 0 and self.offsets[i][0] % 4 == 0
@@ -186,13 +195,13 @@ class LayerExecutor:
                 gemm(self.B, l.units, l.in_features, src.data_ptr(), tp + 4 * w0,
                      self.outs[i].data_ptr(), a_u8=src_u8, a_m=(1, l.in_features, 0),
                      b_ks=l.units, b_ns=1, ldc=l.units, bias=tp + 4 * b0,
-                     act=act_code(l.activation), workspace=self.workspace)
+                     act=self._act(i), workspace=self.workspace)
             else:
                 rows, Win, P, C = self._conv_dims(i)
                 gemm(rows * P, l.filters, l.size * C, src.data_ptr(), tp + 4 * w0,
                      self.outs[i].data_ptr(), a_u8=src_u8, a_m=(P, Win * C, l.stride * C),
                      b_ks=l.filters, b_ns=1, ldc=l.filters, bias=tp + 4 * b0,
-                     act=act_code(l.activation), workspace=self.workspace)
+                     act=self._act(i), workspace=self.workspace)
         return [self.outs[i] for i in self.model.outputs]
 
     # ---- forward-mode derivative ------------------------------------------------
@@ -233,7 +242,7 @@ class LayerExecutor:
             if tsrc is not None:
                 gemm(M, N, K, tsrc.data_ptr(), tp + 4 * w0, out.data_ptr(), beta=True,
                      workspace=self.workspace, **geo)
-            a = act_code(l.activation)
+            a = self._act(i)
             if a != XA_ACT_NONE:
                 call('xa_activation_grad', self.outs[i].data_ptr(), out.data_ptr(), out.numel(),
                      a, out.data_ptr(), stream())
@@ -256,7 +265,7 @@ class LayerExecutor:
         dz = {}
         for i, d in zip(self.model.outputs, d_outputs):
             l = self.layers[i]
-            a = act_code(l.activation)
+            a = self._act(i)
             if a == XA_ACT_NONE:
                 dz[i] = d.contiguous()
             else:
@@ -274,7 +283,7 @@ class LayerExecutor:
                     continue
                 # hidden layer: its ReLU gate was applied by the consumers (gate=out);
                 # a tanh hidden layer takes the derivative here
-                if act_code(l.activation) == XA_ACT_TANH:
+                if self._act(i) == XA_ACT_TANH:
                     call('xa_activation_grad', self.outs[i].data_ptr(),
                          self.douts[i].data_ptr(), self.douts[i][:Bb].numel(), XA_ACT_TANH,
                          self.douts[i].data_ptr(), stream())
@@ -285,7 +294,7 @@ class LayerExecutor:
             src_u8 = u8 and j == -1
             w0, b0 = self.offsets[i]
             gate_j = None
-            if j != -1 and act_code(self.layers[j].activation) == XA_ACT_RELU:
+            if j != -1 and self._act(j) == XA_ACT_RELU:
                 gate_j = self.outs[j].data_ptr()
             if l.kind == 'dense':
                 n_in, n_out = l.in_features, l.units
