@@ -47,7 +47,7 @@ def parse():
     p.add_argument('--preprocess', action='store_true',
                    help='c3 / c4: AtariWrapper on device (xa_atari_step: frame skip 4, '
                         'gray + resize of synthetic raw 210x160 RGB frames) in every env step')
-    p.add_argument('--config', default='c2', choices=['c2', 'c3', 'c4', 'c5', 'trpo'],
+    p.add_argument('--config', default='c2', choices=['c2', 'c3', 'c4', 'c5', 'trpo', 'acer'],
                    help='c2 (default, the BASELINE metric line); c3 DQN Pong-shaped, c4 PPO '
                         'CNN Breakout-shaped (global 1024 envs, strong scaling), c5 TD3')
     return p.parse_args()
@@ -269,6 +269,28 @@ def bench_offpolicy_and_cnn(args):
                                     '[64, 64] relu, CG 10 x FVP on every 5th state, line '
                                     'search, 3 x 4 x 4 critic minibatches (SURVEY 8f rank 2)',
                         'n_envs_per_gpu': n, 'parallelism': 'dp1'})
+    elif args.config == 'acer':
+        from xagents_amd import ACER
+        n, T = 16, 20  # the headline env count; acer/cli.py n-steps default
+        envs = create_envs('PongNoFrameskip-v4', n, args.preprocess, device=device,
+                           seed=args.seed + rank, **_raw_kw(args, n))
+        model = create_model(envs, 'acer', 'model', seed=args.seed, device=device)
+        # 64 trajectories per env, replay from the first step (initial size 1 per env)
+        bufs = create_buffers('acer', 64 * n, 1, n, initial_size=n)
+        agent = ACER(envs, model, bufs, n_steps=T, seed=args.seed, quiet=True, grad_norm=10.0)
+        np.random.seed(args.seed)
+        el = _timed(agent.train_step, args.steps, args.warmup, world)
+        env_steps = n * T * args.steps * world
+        updates = int(agent.model.optimizer.iterations.item())
+        line.update(scaling='weak', data=_data_note(
+                        args, 'synthetic: Pong-shaped uint8 (84,84,1) frames i.i.d. uniform '
+                        '(seed 55+rank), random-init CNN'),
+                    config={'workload': 'ACER PongNoFrameskip-v4-shaped, 16 envs, n_steps 20, '
+                                        'NatureCNN (Conv1D cfg, softmax actor + Q critic), '
+                                        'trust region, replay ratio 4 (poisson), 64 '
+                                        'trajectories per env (SURVEY 8f rank 2)',
+                            'n_envs_per_gpu': n, 'parallelism': f'dp{world}',
+                            'updates_per_step': round(updates / (args.steps + args.warmup), 2)})
     else:
         from xagents_amd import TD3
         n = max(64 // world, 1)
