@@ -153,6 +153,17 @@ def cnn_cpu_baseline(args, kind):
                   f"minibatches of 512) in {info['seconds']:.1f} s: per-env Python step_envs "
                   f"loop, torch-CPU f32 Conv1D/dense + autograd, numpy GAE, Keras Adam "
                   f"(oracle/cpu_cnn.py); the GPU line runs 1024 envs")
+    elif kind == 'acer':
+        n, T = 16, 20
+        rec = record_transitions(n, 256, (84, 84, 1), np.uint8, seed=args.seed)
+        np.random.seed(args.seed)
+        value, info = cpu_cnn.time_acer(rec, seconds=args.cpu_baseline_seconds,
+                                        threads=threads, n_steps=T)
+        sample = (f"{info['train_steps']} ACER train steps of {n} envs x {T} steps (fresh "
+                  f"update + poisson(4) replays of random.sample'd trajectories) in "
+                  f"{info['seconds']:.1f} s: per-env Python step_envs loop, torch-CPU f32 "
+                  f"NatureCNN + autograd trust-region gradient, Python Retrace loop, Keras "
+                  f"Adam, weight EMA (oracle/cpu_cnn.py)")
     else:
         n = 32
         rec = record_transitions(n, 256, (84, 84, 1), np.uint8, seed=args.seed)
@@ -314,7 +325,8 @@ def bench_offpolicy_and_cnn(args):
                     gradient_step_ms=round(g_el / args.steps * 1e3, 4))
     line['value'] = round(env_steps / el, 1)
     line['ms_per_step'] = round(el / args.steps * 1e3, 4)
-    if rank == 0 and world == 1 and args.config in ('c3', 'c4') and args.cpu_baseline_seconds > 0:
+    if rank == 0 and world == 1 and args.config in ('c3', 'c4', 'acer') and \
+            args.cpu_baseline_seconds > 0:
         line['cpu_baseline'] = cnn_cpu_baseline(args, args.config)
     if rank == 0:
         print(json.dumps(line), flush=True)

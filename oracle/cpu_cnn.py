@@ -6,6 +6,7 @@ torch-CPU float32 ops stand in for the TF CPU kernels, in the reference's op ord
   of xagents/ppo/models/cnn-actor-critic.cfg. Keras Conv1D on (B, 84, 84, 1) convolves along
   W with H folded into the batch: conv1d on [B 84, C, W], channels-last
   flatten (common.py:231-260); frames scaled uint8 / 255 (base.py:505-506).
+* CpuACER (bench --config acer): see the class docstring.
 * CpuDQN (config C3): DQN.train_step (xagents/dqn/agent.py:178-209): epsilon-greedy acting
   on the CNN, per-env Python step_envs loop, ReplayBuffer1 deques + random.sample,
   concat_buffer_samples, double-DQN targets, MSE summed over the batch, Keras Adam.
@@ -208,6 +209,127 @@ class CpuDQN:
 def time_dqn(record, seconds=15.0, threads=None, min_steps=2):
     agent = CpuDQN(record, threads=threads)
     agent.fill(8)
+    agent.train_step()
+    steps0 = agent.steps
+    t0 = time.perf_counter()
+    k = 0
+    while k < min_steps or time.perf_counter() - t0 < seconds:
+        agent.train_step()
+        k += 1
+    dt = time.perf_counter() - t0
+    return (agent.steps - steps0) / dt, dict(train_steps=k, seconds=dt, threads=agent.threads,
+                                             n_envs=agent.n_envs)
+
+
+class CpuACER:
+    """ACER.train_step on the host (xagents/acer/agent.py:363-387): A2C.get_batch rollout
+    with the softmax actor, per-env Python step_envs loop, one trajectory per env per step
+    into ReplayBuffer1 deques, update_gradients on the fresh batch then poisson(replay_ratio)
+    updates on random.sample'd trajectories; Retrace returns as a reversed Python loop,
+    trust-region gradient through autograd, global-norm clip, Keras Adam, weight EMA."""
+
+    def __init__(self, record, n_steps=20, buffer_size=64, replay_ratio=4, gamma=0.99,
+                 lr=7e-4, threads=None, seed=55, n_actions=6):
+        if threads:
+            torch.set_num_threads(threads)
+        self.threads = torch.get_num_threads()
+        s0, obs, post, rew, done = record
+        self.envs = [ReplayEnv(s0[i], obs[i], post[i], rew[i], done[i]) for i in range(len(s0))]
+        self.n_envs, self.T, self.A = len(self.envs), n_steps, n_actions
+        self.states = [e.reset() for e in self.envs]
+        self.buffers = [deque(maxlen=buffer_size) for _ in self.envs]
+        self.replay_ratio, self.gamma, self.lr = replay_ratio, gamma, lr
+        self.eps, self.c, self.delta, self.ent, self.vcoef = 1e-6, 10.0, 1.0, 0.01, 0.5
+        gen = torch.Generator().manual_seed(seed)
+        self.params = cnn_params([n_actions, n_actions], gen)
+        self.avg = [p.detach().clone() for p in self.params]
+        self.m = [torch.zeros_like(p) for p in self.params]
+        self.v = [torch.zeros_like(p) for p in self.params]
+        self.t = 0
+        self.steps = 0
+
+    def get_batch(self):
+        N, T = self.n_envs, self.T
+        states, rewards, actions, dones, probs = [], [], [], [], []
+        for _ in range(T):
+            x = np.array(self.states)
+            with torch.no_grad():
+                p = torch.softmax(cnn_forward(self.params, x)[0], -1)
+            a = torch.multinomial(p, 1).squeeze(1).numpy()
+            states.append(x)
+            probs.append(p.numpy())
+            actions.append(a)
+            r, d = np.zeros(N, np.float32), np.zeros(N, np.float32)
+            for i, env in enumerate(self.envs):
+                ns, r[i], d[i], _ = env.step(a[i])
+                self.states[i] = env.reset() if d[i] else ns
+                self.steps += 1
+            rewards.append(r)
+            dones.append(d)
+        states.append(np.array(self.states))
+        batch = [np.asarray(b).swapaxes(0, 1) for b in (states, rewards, actions, dones, probs)]
+        for i in range(N):
+            self.buffers[i].append(tuple(b[i] for b in batch))
+        return batch
+
+    def update(self, batch):
+        states, rewards, actions, dones, mu = batch
+        N, T, A = self.n_envs, self.T, self.A
+        x = states.reshape(N * (T + 1), *states.shape[2:])
+        logits, q = cnn_forward(self.params, x)
+        p = torch.softmax(logits, -1)
+        with torch.no_grad():
+            avg_p = torch.softmax(cnn_forward(self.avg, x)[0], -1)
+        values = (p * q).sum(-1).reshape(N, T + 1)
+        pc = p.reshape(N, T + 1, A)[:, :T]
+        qc = q.reshape(N, T + 1, A)[:, :T]
+        avg_c = avg_p.reshape(N, T + 1, A)[:, :T]
+        a = torch.from_numpy(np.asarray(actions, np.int64))[..., None]
+        sel_p = pc.gather(2, a).squeeze(2)
+        sel_q = qc.gather(2, a).squeeze(2)
+        rho = (sel_p / (torch.from_numpy(np.asarray(mu, np.float32)).gather(2, a).squeeze(2)
+                        + self.eps)).detach()
+        r, d = torch.from_numpy(rewards), torch.from_numpy(dones)
+        ret, cur, rets = None, values[:, T].detach(), []
+        for i in reversed(range(T)):
+            cur = r[:, i] + self.gamma * cur * (1 - d[:, i])
+            rets.append(cur)
+            cur = torch.clamp(rho[:, i], max=1.0) * (cur - sel_q[:, i].detach()) \
+                + values[:, i].detach()
+        ret = torch.stack(rets[::-1], 1)
+        adv = (ret - values[:, :T]).detach()
+        ent = (-(pc * torch.log(pc + self.eps)).sum(-1)).mean()
+        gain = torch.log(sel_p + self.eps) * (adv * torch.clamp(rho, max=self.c))
+        loss = (gain.mean() + self.ent * ent) * N * T
+        vloss = (0.5 * (ret - sel_q) ** 2).mean() * self.vcoef
+        g = torch.autograd.grad(loss, pc, retain_graph=True)[0]
+        k = -avg_c / (pc.detach() + self.eps)
+        adj = torch.clamp(((k * g).sum(-1) - self.delta) / ((k * k).sum(-1) + self.eps), min=0)
+        g = -(g - adj[..., None] * k) / (N * T)
+        ga = torch.autograd.grad(pc, self.params, g, retain_graph=True, allow_unused=True)
+        gv = torch.autograd.grad(vloss, self.params, allow_unused=True)
+        grads = [x if y is None else (y if x is None else x + y) for x, y in zip(ga, gv)]
+        norm = torch.sqrt(sum((gi * gi).sum() for gi in grads))
+        scale = 10.0 / max(float(norm), 10.0)
+        self.t += 1
+        alpha = self.lr * np.sqrt(1 - 0.999 ** self.t) / (1 - 0.9 ** self.t)
+        with torch.no_grad():
+            for prm, gi, m, v, av in zip(self.params, grads, self.m, self.v, self.avg):
+                gi = gi * scale
+                m += (gi - m) * (1 - 0.9)
+                v += (gi * gi - v) * (1 - 0.999)
+                prm -= m * alpha / (torch.sqrt(v) + 1e-7)
+                av -= (av - prm) * (1 - 0.99)
+
+    def train_step(self):
+        self.update(self.get_batch())
+        for _ in range(np.random.poisson(self.replay_ratio)):
+            samples = [random.sample(b, 1)[0] for b in self.buffers]
+            self.update([np.stack(f) for f in zip(*samples)])
+
+
+def time_acer(record, seconds=15.0, threads=None, min_steps=1, n_steps=20):
+    agent = CpuACER(record, n_steps=n_steps, threads=threads)
     agent.train_step()
     steps0 = agent.steps
     t0 = time.perf_counter()
