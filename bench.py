@@ -136,8 +136,9 @@ def _timed(fn, steps, warmup, world):
     return el
 
 
-def cnn_cpu_baseline(args, kind):
-    """Bounded CPU sample of the C3 / C4 workload (oracle/cpu_cnn.py, kind "port")."""
+def secondary_cpu_baseline(args, kind):
+    """Bounded CPU sample of the C3 / C4 / C5 / ACER workload (oracle/cpu_cnn.py,
+    oracle/cpu_td3.py; kind "port")."""
     sys.path.insert(0, str(ROOT / 'oracle'))
     import numpy as np
     import torch
@@ -153,6 +154,16 @@ def cnn_cpu_baseline(args, kind):
                   f"minibatches of 512) in {info['seconds']:.1f} s: per-env Python step_envs "
                   f"loop, torch-CPU f32 Conv1D/dense + autograd, numpy GAE, Keras Adam "
                   f"(oracle/cpu_cnn.py); the GPU line runs 1024 envs")
+    elif kind == 'c5':
+        import cpu_td3
+        n = 64
+        rec = record_transitions(n, 4096, (24,), np.float32, seed=args.seed)
+        np.random.seed(args.seed)
+        value, info = cpu_td3.time_td3(rec, seconds=args.cpu_baseline_seconds, threads=threads)
+        sample = (f"{info['train_steps']} TD3 train steps of {n} envs (gradient_steps 1 per "
+                  f"finished episode, batch 64 from per-env ReplayBuffer2 rings) in "
+                  f"{info['seconds']:.1f} s: per-env Python step_envs loop, torch-CPU f32 "
+                  f"actor / twin critics + autograd, Keras Adam, Polyak (oracle/cpu_td3.py)")
     elif kind == 'acer':
         n, T = 16, 20
         rec = record_transitions(n, 256, (84, 84, 1), np.uint8, seed=args.seed)
@@ -188,6 +199,34 @@ def _data_note(args, what):
     return what
 
 
+def dense_dx_roofline(executors, step):
+    """Roofline of the CNN's dominant GEMM -- the dense 37632 x 512 layer's input gradient
+    dX = dZ W^T -- from HIP events recorded on the launch stream around each of its launches
+    during one more (eager) `step`."""
+    import torch
+    timing = []
+    for ex in executors:
+        ex.timing = timing
+    try:
+        step()
+        torch.cuda.synchronize()
+    finally:
+        for ex in executors:
+            ex.timing = None
+    top = max((fl for *_, fl in timing), default=0)
+    big = [x for x in timing if x[3] == top]
+    full = [(e0.elapsed_time(e1), fl) for _, e0, e1, fl in big]
+    if not full:
+        return None
+    ms = sum(t for t, _ in full) / len(full)
+    tf = full[0][1] / (ms * 1e-3) / 1e12
+    return {'kernel': f'xa_gemm {big[0][0]} (MFMA f32 tile GEMM, ReLU-gate epilogue)',
+            'bound': 'mfma', 'achieved': round(tf, 3), 'peak': 157.3, 'unit': 'TFLOP/s',
+            'frac': round(tf / 157.3, 4), 'traffic': None, 'launch_ms': round(ms, 4),
+            'note': f'2 M N K FLOP per launch, mean of {len(full)} launches; the 77 MB '
+                    f'kernel read alone bounds it at {77.07e6 / 8e12 * 1e3:.4f} ms (HBM)'}
+
+
 def bench_offpolicy_and_cnn(args):
     """Secondary configs; one JSON line each, same fields."""
     import numpy as np
@@ -217,6 +256,9 @@ def bench_offpolicy_and_cnn(args):
             agent.at_step_end()
         el = _timed(step, args.steps, args.warmup, world)
         env_steps = n * args.steps * world
+        rl = dense_dx_roofline([agent.ex_online], step)
+        if rl:
+            line['roofline'] = rl
         line.update(scaling='weak', data=_data_note(
                         args, 'synthetic: Pong-shaped uint8 (84,84,1) frames i.i.d. uniform '
                         '(seed 55+rank), replay buffers pre-filled by device env steps'),
@@ -235,26 +277,10 @@ def bench_offpolicy_and_cnn(args):
         el = _timed(agent.fused_train_step, args.steps, args.warmup, world)
         env_steps = n * 128 * args.steps * world
         # dominant kernel: the dense 37632 x 512 layer's input gradient (gemm_tile_kernel,
-        # 128 x 128 tiles on v_mfma_f32_32x32x2_f32), HIP events around each launch of one
-        # more train step on the launch stream
-        timing = []
-        for ex in agent.ex_chunks:
-            ex.timing = timing
-        agent.fused_train_step()
-        torch.cuda.synchronize()
-        for ex in agent.ex_chunks:
-            ex.timing = None
-        top = max((fl for *_, fl in timing), default=0)
-        big = [x for x in timing if x[3] == top]
-        full = [(e0.elapsed_time(e1), fl) for _, e0, e1, fl in big]
-        if full:
-            ms = sum(t for t, _ in full) / len(full)
-            tf = full[0][1] / (ms * 1e-3) / 1e12
-            line['roofline'] = {
-                'kernel': f'xa_gemm {big[0][0]} (gemm_tile_kernel<2,2>, ReLU-gate epilogue)',
-                'bound': 'mfma', 'achieved': round(tf, 3), 'peak': 157.3, 'unit': 'TFLOP/s',
-                'frac': round(tf / 157.3, 4), 'traffic': None, 'launch_ms': round(ms, 4),
-                'note': f'2 M N K FLOP per launch, mean of {len(full)} launches'}
+        # 128 x 128 tiles on v_mfma_f32_32x32x2_f32)
+        rl = dense_dx_roofline(agent.ex_chunks, agent.fused_train_step)
+        if rl:
+            line['roofline'] = rl
         line.update(scaling='strong', data=_data_note(
                         args, 'synthetic: Breakout-shaped uint8 (84,84,1) frames i.i.d. '
                         'uniform (seed 55+rank), random-init CNN'),
@@ -293,6 +319,9 @@ def bench_offpolicy_and_cnn(args):
         el = _timed(agent.train_step, args.steps, args.warmup, world)
         env_steps = n * T * args.steps * world
         updates = int(agent.model.optimizer.iterations.item())
+        rl = dense_dx_roofline(agent.ex_chunks, agent.train_step)
+        if rl:
+            line['roofline'] = rl
         line.update(scaling='weak', data=_data_note(
                         args, 'synthetic: Pong-shaped uint8 (84,84,1) frames i.i.d. uniform '
                         '(seed 55+rank), random-init CNN'),
@@ -325,9 +354,9 @@ def bench_offpolicy_and_cnn(args):
                     gradient_step_ms=round(g_el / args.steps * 1e3, 4))
     line['value'] = round(env_steps / el, 1)
     line['ms_per_step'] = round(el / args.steps * 1e3, 4)
-    if rank == 0 and world == 1 and args.config in ('c3', 'c4', 'acer') and \
+    if rank == 0 and world == 1 and args.config in ('c3', 'c4', 'c5', 'acer') and \
             args.cpu_baseline_seconds > 0:
-        line['cpu_baseline'] = cnn_cpu_baseline(args, args.config)
+        line['cpu_baseline'] = secondary_cpu_baseline(args, args.config)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

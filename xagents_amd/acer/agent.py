@@ -265,7 +265,7 @@ class ACER(A2C):
                      ex.B, A, stream())
         h = XaAcerArgs()
         h.n_envs, h.n_steps, h.n_actions = N, T, A
-        h.n_total = N * T * self.world_size
+        h.n_total = N * T  # local mean; the all-reduced sum is scaled by 1 / world in Adam
         h.logits, h.ld_logits = self.u_logits.data_ptr(), A
         h.q, h.ld_q = self.u_q.data_ptr(), A
         h.avg_logits, h.ld_avg = (self.u_avg.data_ptr() if self.trust_region else None), A
@@ -321,7 +321,12 @@ class ACER(A2C):
         self.buffer_current_size += 1
         self._acer_update(*self._slot_views(slot))
         if self.replay_ratio > 0 and self.buffer_current_size >= self.buffers[0].initial_size:
-            for _ in range(np.random.poisson(self.replay_ratio)):
+            n_replay = np.random.poisson(self.replay_ratio)
+            if self.distributed:  # every rank must run the same number of all-reduces
+                t = torch.tensor([n_replay], dtype=torch.int64, device=self.device)
+                dist.broadcast(t, 0)
+                n_replay = int(t.item())
+            for _ in range(n_replay):
                 self._acer_update(*self._gather(self.sample_slots()))
         rec(2)
         self.steps += self.n_envs * self.n_steps
