@@ -893,6 +893,11 @@ extern "C" int xa_gemm_splits(int M, int N, int K) {
   const int kt = (K + BK - 1) / BK;
   // skinny workgroups are one wave: 4096 of them keep 4 waves per SIMD streaming
   const int want = shape == 1 ? (M == 1 ? 512 : 4096) : 2048;
+  // two or more full-K tiles per CU already fill the chip: a split only adds partial
+  // traffic and, below 256 K per split, drops the 32x32-MFMA tile kernel (measured,
+  // tools/gemm_split_sweep.py: dense dX 336 x 37632 x 512 167 us unsplit vs 212 us at the
+  // former 4 splits; dense dW 37632 x 512 x 336 163 vs 180 us)
+  if (shape != 1 && tiles >= 512) return 1;
   int s = 1;
   while (tiles * s < want && kt / (s * 2) >= 8 && s < 4096) s *= 2;
   return s;
