@@ -137,8 +137,8 @@ def _timed(fn, steps, warmup, world):
 
 
 def secondary_cpu_baseline(args, kind):
-    """Bounded CPU sample of the C3 / C4 / C5 / ACER workload (oracle/cpu_cnn.py,
-    oracle/cpu_td3.py; kind "port")."""
+    """Bounded CPU sample of the C3 / C4 / C5 / TRPO / ACER workload (oracle/cpu_cnn.py,
+    oracle/cpu_td3.py, oracle/cpu_trpo.py; kind "port")."""
     sys.path.insert(0, str(ROOT / 'oracle'))
     import numpy as np
     import torch
@@ -164,6 +164,19 @@ def secondary_cpu_baseline(args, kind):
                   f"finished episode, batch 64 from per-env ReplayBuffer2 rings) in "
                   f"{info['seconds']:.1f} s: per-env Python step_envs loop, torch-CPU f32 "
                   f"actor / twin critics + autograd, Keras Adam, Polyak (oracle/cpu_td3.py)")
+    elif kind == 'trpo':
+        import cpu_trpo
+        n, T = 16, 512
+        rec = record_transitions(n, 4096, (4,), np.float32, seed=args.seed)
+        np.random.seed(args.seed)
+        value, info = cpu_trpo.time_trpo(rec, seconds=args.cpu_baseline_seconds,
+                                         threads=threads, n_steps=T)
+        sample = (f"{info['train_steps']} TRPO train steps of {n} envs x {T} steps in "
+                  f"{info['seconds']:.1f} s: per-env Python step_envs loop, numpy GAE, "
+                  f"torch-CPU f32 actor / critic, autograd surrogate gradient, 10 CG "
+                  f"iterations of double-backprop Fisher-vector products, line search, "
+                  f"3 x 4 x 4 critic minibatches with Keras Adam (oracle/cpu_trpo.py); "
+                  f"CartPole-shaped f32 transition replay")
     elif kind == 'acer':
         n, T = 16, 20
         rec = record_transitions(n, 256, (84, 84, 1), np.uint8, seed=args.seed)
@@ -354,7 +367,7 @@ def bench_offpolicy_and_cnn(args):
                     gradient_step_ms=round(g_el / args.steps * 1e3, 4))
     line['value'] = round(env_steps / el, 1)
     line['ms_per_step'] = round(el / args.steps * 1e3, 4)
-    if rank == 0 and world == 1 and args.config in ('c3', 'c4', 'c5', 'acer') and \
+    if rank == 0 and world == 1 and args.config in ('c3', 'c4', 'c5', 'trpo', 'acer') and \
             args.cpu_baseline_seconds > 0:
         line['cpu_baseline'] = secondary_cpu_baseline(args, args.config)
     if rank == 0:
