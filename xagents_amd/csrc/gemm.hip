@@ -898,6 +898,20 @@ extern "C" int xa_gemm_splits(int M, int N, int K) {
   // tools/gemm_split_sweep.py: dense dX 336 x 37632 x 512 167 us unsplit vs 212 us at the
   // former 4 splits; dense dW 37632 x 512 x 336 163 vs 180 us)
   if (shape != 1 && tiles >= 512) return 1;
+  if (shape >= 14) {
+    // few 32x32-MFMA tiles (the dense forward, K = 37632): split until the shape that is
+    // actually launched (it drops to 64x64 below 256 K per split) covers ~1024 workgroups
+    // (tools/gemm_split_sweep.py: 336 x 512 x 37632 187 us at 128 splits vs 227 us at 256;
+    // 4096 x 512 x 37632 1209 us at 8 vs 1246 us at 16)
+    int s = 1;
+    while (s < 4096 && kt / (s * 2) >= 8) {
+      int tm, tn;
+      tile_dims(pick_shape(M, N, K, (K + s - 1) / s, false), tm, tn);
+      if ((int64_t)((M + tm - 1) / tm) * ((N + tn - 1) / tn) * s >= 1024) break;
+      s *= 2;
+    }
+    return s;
+  }
   int s = 1;
   while (tiles * s < want && kt / (s * 2) >= 8 && s < 4096) s *= 2;
   return s;
