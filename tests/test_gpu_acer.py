@@ -169,3 +169,22 @@ def test_acer_train_steps_with_replay(device):
     # the average model moved towards the weights, not onto them
     th, av = agent.model.theta, agent.avg_model.theta
     assert not torch.equal(th, av)
+
+
+def test_acer_graph_rollout_matches_eager(device):
+    """The captured rollout (replayed from step 3 on) stores the same trajectories and
+    yields the same weights as eager launches."""
+    agents = []
+    for use_graph in (True, False):
+        ag = _acer(device, n=4, t=6)
+        ag.use_graph = use_graph
+        for _ in range(4):
+            ag.train_step()
+        torch.cuda.synchronize()
+        agents.append(ag)
+    g, e = agents
+    assert g._graph is not None and e._graph is None
+    for name in ('r_frames', 'r_act', 'r_mu', 'r_rew', 'r_done'):
+        assert torch.equal(getattr(g, name), getattr(e, name)), name
+    assert torch.equal(g.model.theta, e.model.theta)
+    assert torch.equal(g.avg_model.theta, e.avg_model.theta)

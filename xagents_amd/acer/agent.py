@@ -2,10 +2,12 @@
 
 Train step (ACER.train_step, acer/agent.py:363-387):
 
-    rollout, n_steps x [actor-critic forward, Categorical sample, env step], written
-    straight into the trajectory ring slot of this step (one RB1 entry per env:
-    frames [T + 1] incl. the get_states() bootstrap frame, behaviour logits [T, A],
-    actions, rewards, dones; ACER.get_batch / store_batch 127-169)
+    rollout, n_steps x [actor-critic forward, Categorical sample, env step] into fixed
+    staging buffers, captured once and replayed as a hipGraph (it is launch-bound at
+    batch n_envs); then stored as this step's trajectory ring slot (one RB1 entry per env:
+    frames [T + 1] incl. the get_states() bootstrap frame -- one xa_ring_gather turns the
+    time-major frames env-major --, behaviour logits [T, A], actions, rewards, dones;
+    ACER.get_batch / store_batch 127-169)
     update on the fresh trajectories
     once buffer_current_size >= initial_size: poisson(replay_ratio) more updates, each on
     one trajectory per env drawn with random.sample (RB1 batch size 1, buffers.py:59-98)
@@ -66,9 +68,9 @@ class ACER(A2C):
         entropy_coef=0.01,
         value_loss_coef=0.5,
         grad_norm=0.5,
+        use_graph=True,
         **kwargs,
     ):
-        kwargs.pop('use_graph', None)
         OnPolicy.__init__(self, envs, model, **kwargs)
         self.entropy_coef = entropy_coef
         self.value_loss_coef = value_loss_coef
@@ -92,8 +94,9 @@ class ACER(A2C):
         self.trust_region = trust_region
         self.ema_alpha = ema_alpha
         self.batch_dtypes = ['uint8', 'float32', 'int32', 'float32', 'float32']
-        self.use_graph = False
+        self.use_graph = use_graph
         self._graph = None
+        self._rollout_warm = False
         self.executor_path = True
         self.distributed = dist.is_available() and dist.is_initialized()
         self.world_size = dist.get_world_size() if self.distributed else 1
@@ -139,6 +142,14 @@ class ACER(A2C):
         self.s_act = torch.zeros(N, T, dtype=torch.int32, device=dev)
         self.s_rew, self.s_done = torch.zeros(N, T, **f32), torch.zeros(N, T, **f32)
         self.s_slots = torch.zeros(N, dtype=torch.int64, device=dev)
+        # rollout staging (fixed addresses: the rollout is captured once as a hipGraph and
+        # replayed; the ring-slot store runs after it)
+        self.g_act = torch.zeros(N, T, dtype=torch.int32, device=dev)
+        self.g_mu = torch.zeros(N, T, A, **f32)
+        self.g_rew, self.g_done = torch.zeros(N, T, **f32), torch.zeros(N, T, **f32)
+        # frame item j = env (T + 1) + t of a trajectory slot <- obs_buf item t N + env
+        j = np.arange(N * (T + 1))
+        self.frame_perm = torch.from_numpy((j % (T + 1)) * N + j // (T + 1)).to(dev)
         # rollout bookkeeping (episode statistics)
         self.b_logp, self.b_ent = torch.zeros(N, T, **f32), torch.zeros(N, T, **f32)
         self.b_done = torch.zeros(N, T + 1, **f32)
@@ -181,18 +192,18 @@ class ACER(A2C):
             self.avg_model.theta.copy_(self.model.theta)
 
     # ---- rollout (A2C.get_batch + ACER.get_batch / store_batch) -----------------------
-    def _acer_rollout(self):
+    def _rollout_kernels(self):
+        """n_steps x [forward, Categorical sample, behaviour logits, env step] into the
+        staging buffers; obs_buf[t] = the policy input of step t (step t + 1's input is the
+        pre-reset obs of step t), obs_buf[T] = get_states() (the bootstrap frame)."""
         N, T, A = self.n_envs, self.n_steps, self.n_actions
         env = self.envs
-        slot = self.count % self.capacity
         a = self._sa
         self.obs_buf[0].copy_(env.state)
         call('xa_copy_block', env.done.data_ptr(), 1, self.b_done.data_ptr(), T + 1, N, 1,
              stream())
-        act0 = self.r_act[slot].data_ptr()
-        mu0 = self.r_mu[slot].data_ptr()
-        rew0 = self.r_rew[slot].data_ptr()
-        done0 = self.r_done[slot].data_ptr()
+        act0, mu0 = self.g_act.data_ptr(), self.g_mu.data_ptr()
+        rew0, done0 = self.g_rew.data_ptr(), self.g_done.data_ptr()
         for t in range(T):
             outs = self.ex_roll.forward(self.obs_buf[t])
             logits = outs[self.actor_out]
@@ -209,16 +220,33 @@ class ACER(A2C):
                 env.pre_step()
             call('xa_replay_env_step', ctypes.byref(a), stream())
         call('xa_copy_block', done0, T, self.b_done.data_ptr() + 4, T + 1, N, T, stream())
-        # frames: the T policy inputs (step t + 1 input = pre-reset obs of step t) and the
-        # get_states() bootstrap frame, env-major
-        w = self.ob // 4
-        fr = self.r_frames[slot].data_ptr()
-        for t in range(T):
-            call('xa_copy_block', self.obs_buf[t].data_ptr(), w, fr + t * self.ob,
-                 (T + 1) * w, N, w, stream())
-        call('xa_copy_block', env.state.data_ptr(), w, fr + T * self.ob, (T + 1) * w, N, w,
-             stream())
+        self.obs_buf[T].copy_(env.state)
         kernels.counter_bump(self.rng_counter)
+
+    def _acer_rollout(self):
+        """One rollout (eager the first time, then a captured hipGraph; envs with a host-side
+        pre_step stay eager), stored as this step's trajectory ring slot."""
+        N, T = self.n_envs, self.n_steps
+        if not self.use_graph or hasattr(self.envs, 'pre_step'):
+            self._rollout_kernels()
+        elif self._graph is not None:
+            self._graph.replay()
+        elif self._rollout_warm:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._rollout_kernels()
+            self._graph = g
+            g.replay()
+        else:
+            self._rollout_kernels()
+            self._rollout_warm = True
+        slot = self.count % self.capacity
+        call('xa_ring_gather', self.obs_buf.data_ptr(), self.r_frames[slot].data_ptr(),
+             self.frame_perm.data_ptr(), N * (T + 1), self.ob, stream())
+        self.r_act[slot].copy_(self.g_act)
+        self.r_mu[slot].copy_(self.g_mu)
+        self.r_rew[slot].copy_(self.g_rew)
+        self.r_done[slot].copy_(self.g_done)
         self.count += 1
         for b in self.buffers:
             b.current_size = min(b.current_size + 1, b.size)
