@@ -75,7 +75,7 @@ def test_trust_region_projection():
     np.testing.assert_allclose(dz_tr, dz_pl, rtol=1e-12, atol=1e-15)
     np.testing.assert_allclose(dq_tr * 0.5, dq_pl, rtol=1e-12)  # coef vs coef^2
     assert l_tr['adjusted'] == 0
-    # a small delta: every adjusted row ends on k . g' ~= delta (calculate_grads 281-287)
+    # delta 0: rows whose k . g exceeds it get adjusted (calculate_grads 281-287)
     _, _, _, l = AO.acer_output_grads(logits, q, avg, mu, act, rew, done, trust_region=True,
                                       delta=0.0, **common)
     assert l['adjusted'] > 0
@@ -99,3 +99,21 @@ def test_sample_slots_follow_reference_deque_sampling():
         random.seed(count)
         ids = [random.sample(dq, 1)[0] for dq in deques]
         assert list(slots) == [i % 5 for i in ids]
+
+
+def test_acer_default_model_units_and_softmax_actor():
+    """create_model('acer') (common.py:447-487): the registered cnn-actor-critic.cfg, output
+    units [n_actions, n_actions], softmax actor output first, critic Q over the actions."""
+    import xagents_amd
+    from xagents_amd.envs import Box, Discrete
+    from xagents_amd.utils.common import create_model
+
+    class _Env:
+        observation_space = Box(0, 255, (84, 84, 1), np.uint8)
+        action_space = Discrete(6)
+
+    assert xagents_amd.agents['acer']['model']['cnn']
+    m = create_model(_Env(), 'acer', 'model', seed=1, device='cpu')
+    outs = [m.layers[i] for i in m.outputs]
+    assert [l.units for l in outs] == [6, 6]
+    assert outs[0].activation == 'softmax' and outs[1].activation in (None, 'linear')
