@@ -188,3 +188,25 @@ def test_acer_graph_rollout_matches_eager(device):
         assert torch.equal(getattr(g, name), getattr(e, name)), name
     assert torch.equal(g.model.theta, e.model.theta)
     assert torch.equal(g.avg_model.theta, e.avg_model.theta)
+
+
+@pytest.mark.parametrize('world', [2])
+def test_acer_data_parallel_processes_on_one_gpu(device, world):
+    """ACER's DP path (gradient all-reduce, replay count broadcast) with W processes sharing
+    the test GPU over a gloo group (tests/acer_dp_worker.py)."""
+    import os
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY='0', OMP_NUM_THREADS='1')
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1',
+           f'--nproc-per-node={world}', '--master-addr=127.0.0.1', f'--master-port={port}',
+           str(ROOT / 'tests' / 'acer_dp_worker.py')]
+    res = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=110,
+                         cwd=str(ROOT))
+    out = res.stdout + res.stderr
+    assert res.returncode == 0, out[-4000:]
+    for r in range(world):
+        assert f'ACER DP OK {r}' in out, out[-4000:]
