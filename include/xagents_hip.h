@@ -572,7 +572,7 @@ int xa_ac_head_grad(const XaHeadGradArgs* args, void* stream);
  * (gradient w.r.t. the pre-softmax logits) and dq for every row (zero on the bootstrap row
  * t = n_steps), the Retrace returns (optional) and per-env loss partials env_loss[n_envs][4]
  * = [sum gain, sum entropy, sum 0.5 (R - Q_a)^2, trust-region adjustments] (optional).
- * n_total = the batch's n_envs x n_steps over all ranks (the mean's denominator). */
+ * n_total = the mean's denominator (this rank's n_envs x n_steps). n_steps <= 4000. */
 typedef struct XaAcerArgs {
   int n_envs, n_steps, n_actions, n_total;
   const float* logits;

@@ -41,7 +41,7 @@ import torch
 import torch.distributed as dist
 
 from xagents_amd import kernels
-from xagents_amd._lib import XaAcerArgs, call, stream
+from xagents_amd._lib import XaAcerArgs, XaReplayStepArgs, call, stream
 from xagents_amd.a2c.agent import A2C
 from xagents_amd.base import OnPolicy
 from xagents_amd.envs import Discrete
@@ -158,7 +158,6 @@ class ACER(A2C):
         seed = self.seed if self.seed is not None else int(np.random.SeedSequence().entropy % 2**63)
         self.rng_seed = (int(seed) * 1000003 + self.rank * 7919 + 17) % 2**64
         self.ex_roll = LayerExecutor(self.model, N)
-        from xagents_amd._lib import XaReplayStepArgs
         self._sa = XaReplayStepArgs()
         env.fill_step_args(self._sa)
         self._sa.ring_states = None

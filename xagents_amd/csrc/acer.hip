@@ -152,7 +152,8 @@ __global__ void ema_kernel(float* __restrict__ shadow, const float* __restrict__
 }  // namespace
 
 extern "C" int xa_acer_grad(const XaAcerArgs* p, void* stream) {
-  XA_CHECK_ARG(p && p->n_envs > 0 && p->n_steps > 0 && p->n_steps <= 4096 &&
+  // LDS: (4 n_steps + 1) floats within the 64 KB dynamic default
+  XA_CHECK_ARG(p && p->n_envs > 0 && p->n_steps > 0 && p->n_steps <= 4000 &&
                    p->n_actions > 0 && p->n_actions <= kMaxA && p->n_total > 0 && p->logits &&
                    p->q && p->mu_logits && p->actions && p->rewards && p->dones &&
                    p->dlogits && p->dq && (!p->trust_region || p->avg_logits),
