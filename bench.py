@@ -455,8 +455,10 @@ def main():
             'data': 'synthetic: CartPole-v1 observation replay recorded on the host '
                     '(np.random.default_rng(55+rank)), random-init weights',
             'config': {
-                'workload': 'PPO CartPole-v1, 256 envs/GPU, MLP[64,64], n_steps=128, '
-                            'synthetic obs replay (BASELINE configs[1])',
+                'workload': (f'PPO CartPole-v1, {args.n_envs} envs/GPU, MLP[64,64], '
+                             f'n_steps={args.n_steps}, synthetic obs replay'
+                             + (' (BASELINE configs[1])' if (args.n_envs, args.n_steps)
+                                == (256, 128) else '')),
                 'n_envs_per_gpu': args.n_envs,
                 'n_steps': args.n_steps,
                 'batch_per_gpu': args.n_envs * args.n_steps,
