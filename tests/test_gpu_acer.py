@@ -210,3 +210,13 @@ def test_acer_data_parallel_processes_on_one_gpu(device, world):
     assert res.returncode == 0, out[-4000:]
     for r in range(world):
         assert f'ACER DP OK {r}' in out, out[-4000:]
+
+
+def test_acer_fit_runs(device):
+    """BaseAgent.fit (base.py:566-593) drives ACER.train_step until max_steps."""
+    np.random.seed(2)
+    agent = _acer(device, n=4, t=6, replay_ratio=1, initial=1)
+    agent.fit(max_steps=4 * 6 * 3)
+    assert agent.steps >= 4 * 6 * 3
+    assert np.isfinite(agent.model.theta.cpu().numpy()).all()
+    assert np.isfinite(agent.avg_model.theta.cpu().numpy()).all()
