@@ -32,6 +32,30 @@ def mlp_fwd_flops(obs_dim=4, n_actions=2, hidden=64):
     return 2 * (obs_dim * hidden + hidden * hidden + hidden * (n_actions + 1))
 
 
+def ac_grad_burst_ms(agent, rounds=3):
+    """xa_ac_grad duration, second estimate: the 16 launches of one update back-to-back (behind
+    a spin kernel, so the host is ahead) between ONE event pair on the launch stream. An event
+    pair around every launch adds its packets to each bracketed launch (~3 us here); this
+    includes only the 15 inter-kernel gaps. Each launch applies the pending optimizer step from
+    the slot the previous one wrote (ping-pong), as in the real chain minus the reduces."""
+    import numpy as np
+    import torch
+    from xagents_amd import kernels
+    args = agent._gargs_list
+    out = []
+    for _ in range(rounds):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        torch.cuda._sleep(20_000_000)
+        e0.record()
+        for g in args:
+            kernels.ac_grad(g)
+        e1.record()
+        torch.cuda.synchronize()
+        out.append(e0.elapsed_time(e1) / len(args))
+    return float(np.median(out))
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument('--gpus', type=int, default=1)
@@ -435,6 +459,7 @@ def main():
         # minibatch: forward + backward = 3F FLOPs per sample
         mb = args.n_envs * args.n_steps // 4
         grad_ms = float(np.mean(ktimes['ac_grad']))
+        grad_ms_burst = ac_grad_burst_ms(agent)
         grad_flops = 3 * mlp_fwd_flops() * mb
         grad_tflops = grad_flops / (grad_ms * 1e-3) / 1e12
         roll_kms = float(np.mean(ktimes['rollout']))
@@ -480,9 +505,15 @@ def main():
                 'frac': round(grad_tflops / F32_MFMA_PEAK_TFLOPS, 5),
                 'traffic': load_traffic('ac_grad'),
                 'launch_ms': round(grad_ms, 5),
+                'launch_ms_burst': round(grad_ms_burst, 5),
                 'note': f'3F = {3 * mlp_fwd_flops()} FLOP/sample (fwd + bwd) x {mb} samples '
                         'per launch; latency-bound (one 32-sample tile per workgroup); '
-                        'traffic = PMC FETCH_SIZE x 2 + WRITE_SIZE per launch',
+                        'launch_ms = an event pair around every launch of 3 eager train steps '
+                        '(conservative: includes the event packets); launch_ms_burst = one '
+                        'event pair around the 16 launches of an update back-to-back without '
+                        'the interleaved reduces (L2-warm, optimistic); the rocprofv3 average '
+                        'lies between the two; traffic = PMC FETCH_SIZE x 2 + WRITE_SIZE per '
+                        'launch',
             },
             'rollout_roofline': {
                 'kernel': 'xa_mlp_rollout (mlp_rollout_kernel<4,2,replay>)',
