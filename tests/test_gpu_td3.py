@@ -128,3 +128,29 @@ def test_captured_gradient_steps_match_eager(device, kind):
         out.append([_np(m.theta) for m in nets])
     for a, b in zip(*out):
         np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize('kind', ['td3', 'ddpg'])
+def test_captured_env_phase_matches_eager(device, kind):
+    """train_step's env phase (actor forward [+ noise] + ring append) replayed as a hipGraph
+    stores the same transitions, episode statistics and weights as eager launches."""
+    import random
+    out = []
+    for use_graph in (False, True):
+        np.random.seed(0)
+        random.seed(0)
+        agent = _agent(device, kind, n=4, gradient_steps=1)
+        agent.use_graph = use_graph
+        agent.fill_buffers()
+        for _ in range(70):
+            agent.train_step()
+        agent._drain_episode_stats()
+        torch.cuda.synchronize()
+        r = agent.replay
+        out.append(([_np(x) for x in (r.states, r.actions, r.rewards, r.dones, r.new_states,
+                                      agent.actor.theta, agent.critic.theta)],
+                    (agent.games, list(agent.total_rewards), agent.steps)))
+    for a, b in zip(out[0][0], out[1][0]):
+        np.testing.assert_array_equal(a, b)
+    assert out[0][1] == out[1][1]
+    assert out[1][1][0] > 0  # some episodes finished (gradient steps ran)

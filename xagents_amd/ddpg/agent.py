@@ -10,6 +10,8 @@ Per gradient step (ddpg/agent.py:129-147), all launches on device:
     sync_target_models      xa_polyak (1 - tau) target + tau online (every policy_delay)
 The MLPs run on xa_gemm through the layer executor (xagents_amd/layers.py).
 """
+import ctypes
+
 import numpy as np
 import torch
 
@@ -196,14 +198,42 @@ class DDPG(OffPolicy):
         self.__dict__['_graphs'] = {}  # the learning rates are baked into the launches
         self.__dict__['_warm'] = set()
 
+    def _step_phase(self):
+        """get_step_actions + one xa_replay_env_step (ring append) writing the step's
+        done / episode-return row into fixed staging rows (graph-capturable)."""
+        actions = self.get_step_actions()
+        a = self._step_args
+        self.replay.fill_step_args(a, actions)
+        a.out_dones = self._stage_done.data_ptr()
+        a.done_epret = self._stage_epret.data_ptr()
+        call('xa_replay_env_step', ctypes.byref(a), stream())
+
     def train_step(self):
         """ddpg/agent.py:149-166: step every env, then for each env that finished an
-        episode run gradient_steps (or that env's episode length) gradient steps."""
-        actions = self.get_step_actions()
-        row = self._st_row
-        self._env_step(actions)
-        self.steps += self.n_envs
-        dones = self._host_row_dones(row)
+        episode run gradient_steps (or that env's episode length) gradient steps.
+        The env phase is one hipGraph replay (a few small launches at batch n_envs);
+        envs with a host-side pre_step (raw-frame Atari) stay on the eager path."""
+        if hasattr(self.envs, 'pre_step'):
+            actions = self.get_step_actions()
+            row = self._st_row
+            self._env_step(actions)
+            self.steps += self.n_envs
+            dones = self._host_row_dones(row)
+        else:
+            if not hasattr(self, '_stage_done'):
+                f32 = dict(dtype=torch.float32, device=self.device)
+                self._stage_done = torch.zeros(self.n_envs, **f32)
+                self._stage_epret = torch.zeros(self.n_envs, **f32)
+            self._run_phase('step', self._step_phase)
+            r = self._st_row
+            self._st_done[r].copy_(self._stage_done)
+            self._st_epret[r].copy_(self._stage_epret)
+            self.replay.appended()
+            self._st_row += 1
+            if self._st_row == self._STATS_ROWS:
+                self._flush_offpolicy_stats()
+            self.steps += self.n_envs
+            dones = self._stage_done.cpu().numpy()
         for idx in np.nonzero(dones)[0]:
             steps = self.gradient_steps or self.episode_steps[idx]
             self.update_weights(steps)
