@@ -144,3 +144,34 @@ def test_dqn_fit_epsilon_and_target_sync(device):
                                   model.theta.cpu().numpy())
     assert len(agent.total_rewards) == agent.games
     assert int(model.optimizer.iterations.item()) == agent.steps // 4
+
+
+@pytest.mark.parametrize('double', [False, True])
+def test_dqn_captured_learner_matches_eager(device, double):
+    """The learner phase (gather -> TD gradient -> backward -> Adam) replayed as a hipGraph
+    from the third train step on gives bit-identical weights to eager launches."""
+    import random
+    from xagents_amd import DQN
+    from xagents_amd.envs import create_envs
+    from xagents_amd.utils.common import create_buffers, create_model
+    out = []
+    for use_graph in (False, True):
+        np.random.seed(4)
+        random.seed(4)
+        envs = create_envs('PongNoFrameskip-v4', 2, device=device, seed=3)
+        model = create_model(envs, 'dqn', 'model', seed=9, device=device)
+        agent = DQN(envs, model, create_buffers('dqn', 40, 4, 2, initial_size=20),
+                    double=double, seed=2, quiet=True, epsilon_decay_steps=20,
+                    target_sync_steps=6)
+        agent.use_graph = use_graph
+        agent.fill_buffers()
+        for _ in range(8):
+            agent.at_step_start()
+            agent.train_step()
+            agent.at_step_end()
+        torch.cuda.synchronize()
+        assert (getattr(agent, '_lgraph', None) is not None) == use_graph
+        out.append([model.theta.cpu().numpy(), agent.target_model.theta.cpu().numpy(),
+                    agent.model.optimizer.m.cpu().numpy(), agent.b_act.cpu().numpy()])
+    for a, b in zip(*out):
+        np.testing.assert_array_equal(a, b)

@@ -188,9 +188,38 @@ class DQN(OffPolicy):
         self.get_actions()
         self._env_step(self.actions)
         self.steps += self.n_envs
-        self.concat_buffer_samples()
+        # host index draw in the reference's order, then the device learner phase
+        self.replay.upload_slots(self.replay.sample_slots())
+        self._run_learn()
+
+    def _learn_phase(self):
+        """gather the sampled batch -> TD gradient -> CNN backward -> Keras Adam."""
+        B = self.batch_size
+        self.replay.gather(self.replay.slots, self.xb[:B], self.b_act, self.b_rew, self.b_done,
+                           self.xb[B:])
         self._td_grad()
         self._apply()
+
+    def _run_learn(self):
+        """Eager once, then captured and replayed as a hipGraph (the sample slots live in a
+        fixed device buffer); data-parallel steps stay eager (torch collective)."""
+        if not getattr(self, 'use_graph', True) or self.distributed:
+            self._learn_phase()
+        elif getattr(self, '_lgraph', None) is not None:
+            self._lgraph.replay()
+        elif getattr(self, '_lwarm', False):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._learn_phase()
+            self._lgraph = g
+            g.replay()
+        else:
+            self._learn_phase()
+            self._lwarm = True
+
+    def _on_lr_change(self):
+        self._lgraph = None  # the learning rate is baked into the Adam launch
+        self._lwarm = False
 
     def at_step_end(self):
         self.sync_target_model()
