@@ -1,13 +1,15 @@
-"""Benchmark: PPO train steps on BASELINE config 2 (PPO CartPole-v1, 256 envs per GPU,
-MLP[64,64], n_steps=128, synthetic observation replay), one process per GPU.
+"""Benchmark: PPO train steps on PPO CartPole-v1 (MLP[64,64], n_steps=128, synthetic
+observation replay), one process per GPU.
 
     python bench.py --gpus N --steps K --warmup W
     (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
 
-A step = one PPO train_step: fused rollout of 256 envs x 128 steps (+GAE) and
-4 epochs x 4 minibatches of 8192 (shuffle-gather, forward, clipped loss, backward,
-global-norm clip, Keras Adam; RCCL all-reduce of the gradient when N>1).
-Weak scaling: every rank owns 256 envs. Rank 0 prints ONE JSON line.
+A step = one PPO train_step: fused rollout of n_envs x 128 steps (+GAE) and 4 epochs x 4
+minibatches (shuffle, forward, clipped loss, backward, global-norm clip, Keras Adam; one
+persistent launch on one GPU, all-reduce of the gradient when N>1).
+`value` = the metric's 16-env workload (BASELINE metric "PPO 16-env"); the line's `c2`
+object = BASELINE configs[1] (256 envs per GPU). Weak scaling: every rank owns its envs.
+Rank 0 prints ONE JSON line.
 """
 import argparse
 import json
@@ -32,36 +34,15 @@ def mlp_fwd_flops(obs_dim=4, n_actions=2, hidden=64):
     return 2 * (obs_dim * hidden + hidden * hidden + hidden * (n_actions + 1))
 
 
-def ac_grad_burst_ms(agent, rounds=3):
-    """xa_ac_grad duration, second estimate: the 16 launches of one update back-to-back (behind
-    a spin kernel, so the host is ahead) between ONE event pair on the launch stream. An event
-    pair around every launch adds its packets to each bracketed launch (~3 us here); this
-    includes only the 15 inter-kernel gaps. Each launch applies the pending optimizer step from
-    the slot the previous one wrote (ping-pong), as in the real chain minus the reduces."""
-    import numpy as np
-    import torch
-    from xagents_amd import kernels
-    args = agent._gargs_list
-    out = []
-    for _ in range(rounds):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        torch.cuda.synchronize()
-        torch.cuda._sleep(20_000_000)
-        e0.record()
-        for g in args:
-            kernels.ac_grad(g)
-        e1.record()
-        torch.cuda.synchronize()
-        out.append(e0.elapsed_time(e1) / len(args))
-    return float(np.median(out))
-
-
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument('--gpus', type=int, default=1)
     p.add_argument('--steps', type=int, default=20)
     p.add_argument('--warmup', type=int, default=5)
-    p.add_argument('--n-envs', type=int, default=256)
+    p.add_argument('--n-envs', type=int, default=16,
+                   help='envs per GPU of the headline line (the metric is quoted on 16)')
+    p.add_argument('--no-c2', dest='c2', action='store_false',
+                   help='skip the secondary BASELINE configs[1] (256 envs per GPU) measurement')
     p.add_argument('--n-steps', type=int, default=128)
     p.add_argument('--t-rec', type=int, default=4096)
     p.add_argument('--seed', type=int, default=55)
@@ -401,28 +382,23 @@ def bench_offpolicy_and_cnn(args):
         dist.destroy_process_group()
 
 
-def main():
-    args = parse()
-    if args.config != 'c2':
-        return bench_offpolicy_and_cnn(args)
+def bench_ppo(args, world, rank, device, n_envs):
+    """Time PPO train steps on n_envs CartPole replay envs per rank; returns the
+    measurements and the per-kernel roofline of this workload."""
     import numpy as np
     import torch
     import torch.distributed as dist
-
-    world, rank, device = _dist_setup()
-
     from xagents_amd import PPO
     from xagents_amd.envs import ReplayVecEnv, record_cartpole_replay
     from xagents_amd.utils.common import create_model
 
-    record = record_cartpole_replay(args.n_envs, args.t_rec, seed=args.seed + rank)
-    envs = ReplayVecEnv('CartPole-v1', args.n_envs, device=device, record=record)
+    record = record_cartpole_replay(n_envs, args.t_rec, seed=args.seed + rank)
+    envs = ReplayVecEnv('CartPole-v1', n_envs, device=device, record=record)
     model = create_model(envs, 'ppo', 'model', optimizer_kwargs=dict(learning_rate=7e-4),
                          seed=args.seed, device=device)
     theta0 = model.theta.cpu().numpy().copy()
     agent = PPO(envs, model, n_steps=args.n_steps, seed=args.seed, quiet=True,
                 use_graph=not args.no_graph)
-
     for _ in range(args.warmup):
         agent.train_step()
     transport = agent.check_peer_all_reduce()
@@ -440,39 +416,92 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    # per-kernel durations: HIP events around the rollout launch and the 16 xa_ac_grad
-    # launches of 3 eagerly launched train steps right after the timed region
-    ktimes = {'rollout': [], 'ac_grad': []}
+    # per-kernel durations: HIP events on the launch stream around the rollout and the
+    # update launches of 3 eagerly launched train steps right after the timed region
+    ktimes = {}
     for _ in range(3):
         for k, v in agent.timed_train_step().items():
-            ktimes[k] += v
+            ktimes.setdefault(k, []).extend(v)
     if world > 1:
         elapsed = _max_over_ranks(elapsed, device)
-    rollout_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in events]))
-    update_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in events]))
-    env_steps = args.n_envs * args.n_steps * args.steps * world
-    value = env_steps / elapsed
     agent._drain_episode_stats()
+    T = args.n_steps
+    B = n_envs * T
+    mb = B // agent.mini_batches
+    K = agent.ppo_epochs * agent.n_mb
+    flops_sample = 3 * mlp_fwd_flops()  # forward + backward per sample
+    out = {
+        'n_envs': n_envs,
+        'value': n_envs * T * args.steps * world / elapsed,
+        'ms_per_step': elapsed / args.steps * 1e3,
+        'rollout_ms': float(np.mean([e[0].elapsed_time(e[1]) for e in events])),
+        'update_ms': float(np.mean([e[1].elapsed_time(e[2]) for e in events])),
+        'transport': transport, 'graph': bool(agent.use_graph and agent._graph is not None),
+        'update_mode': agent.update_mode, 'record': record, 'theta0': theta0, 'agent': agent,
+    }
+    roll_ms = float(np.mean(ktimes['rollout']))
+    roll_bytes = ROLLOUT_BYTES_PER_ENV_STEP * B
+    roll_gbs = roll_bytes / (roll_ms * 1e-3) / 1e9
+    out['rollout_roofline'] = {
+        'kernel': 'xa_mlp_rollout (mlp_rollout_kernel<4,2,replay>)', 'bound': 'hbm',
+        'achieved': round(roll_gbs, 3), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+        'frac': round(roll_gbs / HBM_PEAK_GBS, 6),
+        'traffic': load_traffic(f'rollout_n{n_envs}'), 'launch_ms': round(roll_ms, 5),
+        'note': f'latency-bound: {T} dependent policy steps per env (one wave64 per env); '
+                f'{ROLLOUT_BYTES_PER_ENV_STEP} algorithmic B/env-step x {B} env-steps per launch'}
+    if agent.update_mode == 'persistent':
+        upd_ms = float(np.mean(ktimes['ppo_update']))
+        flops = flops_sample * B * agent.ppo_epochs  # every sample once per epoch
+        tf = flops / (upd_ms * 1e-3) / 1e12
+        out['update_roofline'] = {
+            'kernel': 'xa_ppo_update (ppo_update_kernel<4,2>, persistent)', 'bound': 'mfma',
+            'achieved': round(tf, 3), 'peak': F32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
+            'frac': round(tf / F32_MFMA_PEAK_TFLOPS, 5),
+            'traffic': load_traffic(f'ppo_update_n{n_envs}'), 'launch_ms': round(upd_ms, 5),
+            'note': f'3F = {flops_sample} FLOP/sample (fwd + bwd) x {B} samples x '
+                    f'{agent.ppo_epochs} epochs = {K} optimizer steps of {mb} in ONE launch '
+                    f'on {agent.update_blocks} workgroups; latency-bound (2 in-launch '
+                    f'exchanges per optimizer step); launch_ms = HIP event pair on the launch '
+                    f'stream around each launch of 3 eager train steps'}
+    else:
+        grad_ms = float(np.mean(ktimes['ac_grad']))
+        tf = flops_sample * mb / (grad_ms * 1e-3) / 1e12
+        out['update_roofline'] = {
+            'kernel': 'xa_ac_grad (ac_grad_kernel<4,2>, per-minibatch chain)', 'bound': 'mfma',
+            'achieved': round(tf, 3), 'peak': F32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
+            'frac': round(tf / F32_MFMA_PEAK_TFLOPS, 5),
+            'traffic': load_traffic(f'ac_grad_n{n_envs}'), 'launch_ms': round(grad_ms, 5),
+            'note': f'3F = {flops_sample} FLOP/sample x {mb} samples per launch, {K} launches '
+                    f'per train step (data-parallel chain)'}
+    return out
+
+
+def main():
+    args = parse()
+    if args.config != 'c2':
+        return bench_offpolicy_and_cnn(args)
+    import torch.distributed as dist
+
+    world, rank, device = _dist_setup()
+    # headline: the metric's PPO CartPole-v1 16-env workload (BASELINE metric / configs[0]
+    # shape) on the GPU; secondary: BASELINE configs[1] (256 envs per GPU)
+    head = bench_ppo(args, world, rank, device, args.n_envs)
+    c2 = bench_ppo(args, world, rank, device, 256) if args.c2 and args.n_envs != 256 else None
 
     if rank == 0:
-        # dominant kernel: xa_ac_grad (16 launches per step); one launch processes one
-        # minibatch: forward + backward = 3F FLOPs per sample
-        mb = args.n_envs * args.n_steps // 4
-        grad_ms = float(np.mean(ktimes['ac_grad']))
-        grad_ms_burst = ac_grad_burst_ms(agent)
-        grad_flops = 3 * mlp_fwd_flops() * mb
-        grad_tflops = grad_flops / (grad_ms * 1e-3) / 1e12
-        roll_kms = float(np.mean(ktimes['rollout']))
-        roll_bytes = ROLLOUT_BYTES_PER_ENV_STEP * args.n_envs * args.n_steps
-        roll_gbs = roll_bytes / (roll_kms * 1e-3) / 1e9
+        def dominant(r):
+            # the kernel with the larger share of the step carries the line's roofline
+            u, ro = r['update_roofline'], r['rollout_roofline']
+            return dict(u) if u['launch_ms'] >= ro['launch_ms'] else dict(ro)
+
         line = {
             'metric': METRIC,
-            'value': round(value, 1),
+            'value': round(head['value'], 1),
             'unit': 'env-steps/s',
             'n_gpus': world,
             'steps': args.steps,
             'warmup': args.warmup,
-            'ms_per_step': round(elapsed / args.steps * 1e3, 4),
+            'ms_per_step': round(head['ms_per_step'], 4),
             'higher_is_better': True,
             'scaling': 'weak',
             'vs_baseline': None,
@@ -481,62 +510,47 @@ def main():
                     '(np.random.default_rng(55+rank)), random-init weights',
             'config': {
                 'workload': (f'PPO CartPole-v1, {args.n_envs} envs/GPU, MLP[64,64], '
-                             f'n_steps={args.n_steps}, synthetic obs replay'
-                             + (' (BASELINE configs[1])' if (args.n_envs, args.n_steps)
-                                == (256, 128) else '')),
+                             f'n_steps={args.n_steps}, 4 epochs x 4 minibatches, synthetic obs '
+                             f'replay' + (' (the metric\'s 16-env configuration)'
+                                          if args.n_envs == 16 else '')),
                 'n_envs_per_gpu': args.n_envs,
                 'n_steps': args.n_steps,
                 'batch_per_gpu': args.n_envs * args.n_steps,
                 'minibatch_per_gpu': args.n_envs * args.n_steps // 4,
                 'ppo_epochs': 4,
                 'parallelism': f'dp{world}',
-                'graph': bool(agent.use_graph and agent._graph is not None),
-                'allreduce': transport,
+                'graph': head['graph'],
+                'update': head['update_mode'],
+                'allreduce': head['transport'],
             },
-            'update_ms': round(update_ms, 4),
-            'rollout_ms': round(rollout_ms, 4),
-            'env_steps_per_sec_per_gpu': round(value / world, 1),
-            'roofline': {
-                'kernel': 'xa_ac_grad (ac_grad_kernel<4,2>)',
-                'bound': 'mfma',
-                'achieved': round(grad_tflops, 3),
-                'peak': F32_MFMA_PEAK_TFLOPS,
-                'unit': 'TFLOP/s',
-                'frac': round(grad_tflops / F32_MFMA_PEAK_TFLOPS, 5),
-                'traffic': load_traffic('ac_grad'),
-                'launch_ms': round(grad_ms, 5),
-                'launch_ms_burst': round(grad_ms_burst, 5),
-                'note': f'3F = {3 * mlp_fwd_flops()} FLOP/sample (fwd + bwd) x {mb} samples '
-                        'per launch; latency-bound (one 32-sample tile per workgroup); '
-                        'launch_ms = an event pair around every launch of 3 eager train steps '
-                        '(conservative: includes the event packets); launch_ms_burst = one '
-                        'event pair around the 16 launches of an update back-to-back without '
-                        'the interleaved reduces (L2-warm, optimistic); the rocprofv3 average '
-                        'lies between the two; traffic = PMC FETCH_SIZE x 2 + WRITE_SIZE per '
-                        'launch',
-            },
-            'rollout_roofline': {
-                'kernel': 'xa_mlp_rollout (mlp_rollout_kernel<4,2,replay>)',
-                'bound': 'hbm',
-                'achieved': round(roll_gbs, 3),
-                'peak': HBM_PEAK_GBS,
-                'unit': 'GB/s',
-                'frac': round(roll_gbs / HBM_PEAK_GBS, 6),
-                'traffic': load_traffic('rollout'),
-                'launch_ms': round(roll_kms, 5),
-                'note': 'latency-bound: 128 dependent policy steps per env; '
-                        f'{ROLLOUT_BYTES_PER_ENV_STEP} algorithmic B/env-step x '
-                        f'{args.n_envs * args.n_steps} env-steps per launch',
-            },
+            'update_ms': round(head['update_ms'], 4),
+            'rollout_ms': round(head['rollout_ms'], 4),
+            'env_steps_per_sec_per_gpu': round(head['value'] / world, 1),
+            'roofline': dominant(head),
+            'update_roofline': head['update_roofline'],
+            'rollout_roofline': head['rollout_roofline'],
         }
+        if c2 is not None:
+            line['c2'] = {
+                'workload': 'PPO CartPole-v1, 256 envs/GPU, MLP[64,64], n_steps=128, 4x4 '
+                            'minibatches of 8192, synthetic obs replay (BASELINE configs[1])',
+                'value': round(c2['value'], 1), 'unit': 'env-steps/s',
+                'ms_per_step': round(c2['ms_per_step'], 4),
+                'update_ms': round(c2['update_ms'], 4), 'rollout_ms': round(c2['rollout_ms'], 4),
+                'update': c2['update_mode'],
+                'roofline': dominant(c2),
+                'update_roofline': c2['update_roofline'],
+                'rollout_roofline': c2['rollout_roofline'],
+            }
         if world == 1 and args.cpu_baseline_seconds > 0:
-            line['cpu_baseline'] = cpu_baseline(args, record, theta0)
+            line['cpu_baseline'] = cpu_baseline(args, head['record'], head['theta0'])
         else:
             line['cpu_baseline'] = None
         print(json.dumps(line), flush=True)
     if world > 1:
-        if agent.peer is not None:
-            agent.peer.close()
+        for r in (head, c2):
+            if r is not None and r['agent'].peer is not None:
+                r['agent'].peer.close()
         dist.destroy_process_group()
 
 

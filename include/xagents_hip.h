@@ -278,6 +278,56 @@ int xa_clip_adam(float* theta, float* adam_m, float* adam_v, const float* grad, 
                  float eps, const int* adam_step, double* workspace, float* gnorm_out,
                  float* theta_out, float* m_out, float* v_out, void* stream);
 
+/*
+ * Persistent PPO update: EVERY optimizer step of one train step in ONE launch.
+ * Replaces PPO.get_mini_batches + run_ppo_epochs + update_gradients
+ * (xagents/ppo/agent.py:96-191): for epoch e, minibatch m (k = e*n_mb + m, n_mb =
+ * ceil(batch/mb_size), ragged last minibatch as range(0, batch, mb_size) slices it):
+ * the shuffled samples (XaShuffle, the same permutation as xa_ppo_minibatches),
+ * advantage normalisation with the minibatch's mean / population std
+ * (ppo/agent.py:180-183), clipped PPO loss + backward (as xa_ac_grad), global-norm clip
+ * and Keras Adam with t = *adam_step + k + 1 -- the arithmetic of the per-minibatch
+ * chain xa_ppo_minibatches -> [xa_ac_grad -> xa_grad_reduce] x E*M -> xa_clip_adam,
+ * up to the f64 summation order of the gradient and advantage sums.
+ * In place on theta / adam_m / adam_v; *adam_step += E*M. One process (no
+ * cross-rank exchange inside; data-parallel steps use the chain).
+ * n_blocks: xa_ppo_update_blocks(obs_dim, n_actions, mb_size) (every block must be
+ * resident at once: the blocks exchange gradient rows inside the launch).
+ * workspace: device memory, 256-byte aligned, >= xa_ppo_update_workspace_bytes(...),
+ * owned by the caller; the launch zeroes its first 256 bytes (a memset node).
+ * loss_out (optional) [E*n_mb, n_blocks, 4]: per-block (pg, value, entropy, count) sums.
+ * grad_out (optional) [P]: the last optimizer step's reduced gradient (before the clip).
+ * status (optional device int): set to 1 if an in-launch exchange timed out (2 s);
+ * the parameters are then invalid. adam.grad_scale is not used (must be 1).
+ */
+typedef struct XaPpoUpdateArgs {
+  int obs_dim, n_actions;
+  int batch, mb_size, epochs;
+  XaShuffle shuffle;
+  const float* obs;        /* [batch, obs] env-major rollout (concat_step_batches order) */
+  const int* actions;      /* [batch] */
+  const float* old_logp;   /* [batch] */
+  const float* old_values; /* [batch] */
+  const float* returns;    /* [batch] */
+  float clip_norm, entropy_coef, value_coef, adv_eps;
+  float* theta;
+  float* adam_m;
+  float* adam_v;
+  int* adam_step;
+  XaAdam adam;
+  void* workspace;
+  size_t workspace_bytes;
+  float* loss_out;
+  float* grad_out;
+  int* status;
+  int n_blocks;
+} XaPpoUpdateArgs;
+
+int xa_ppo_update_blocks(int obs_dim, int n_actions, int mb_size);
+size_t xa_ppo_update_workspace_bytes(int obs_dim, int n_actions, int batch, int mb_size,
+                                     int epochs, int n_blocks);
+int xa_ppo_update(const XaPpoUpdateArgs* args, void* stream);
+
 /* ------------------------------------------------------------------------- */
 /* Dense / Conv1D building blocks (CNN cfgs: xagents/dqn/models/cnn.cfg,      */
 /* xagents/ppo/models/cnn-actor-critic.cfg; TD3/DDPG MLPs in td3/models)     */

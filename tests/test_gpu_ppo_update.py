@@ -1,0 +1,196 @@
+"""GPU tests of the persistent PPO update (xa_ppo_update): every optimizer step of a train
+step in one launch (xagents/ppo/agent.py:96-191), against the float64 restatement
+(oracle/oracle.py) and against the per-minibatch launch chain."""
+import ctypes
+
+import numpy as np
+import oracle
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+OBS, A = 4, 2
+LR, B1, B2, EPS, CLIP_G = 7e-4, 0.9, 0.999, 1e-7, 0.5
+
+
+def _rollout_buffers(B, seed):
+    """Synthetic rollout buffers shaped like a CartPole rollout (env-major flat)."""
+    rng = np.random.default_rng(seed)
+    obs = rng.standard_normal((B, OBS)).astype(np.float32)
+    act = rng.integers(0, A, B).astype(np.int32)
+    val = (rng.standard_normal(B) * 0.5).astype(np.float32)
+    ret = (val + rng.standard_normal(B)).astype(np.float32)
+    logp = np.log(rng.uniform(0.2, 0.8, B)).astype(np.float32)
+    return obs, act, logp, val, ret
+
+
+def _theta0(seed):
+    rng = np.random.default_rng(seed + 100)
+    return (rng.standard_normal(4675) * 0.2).astype(np.float32)
+
+
+def run_update(theta0, bufs, mb_size, epochs, perm=None, n_blocks=None, want=True):
+    """Call xa_ppo_update directly; returns theta, m, v, step, grad_out, loss_out, status."""
+    from xagents_amd import kernels
+    from xagents_amd._lib import XaPpoUpdateArgs, XaShuffle
+    obs, act, logp, val, ret = (torch.as_tensor(x, device='cuda') for x in bufs)
+    B = obs.shape[0]
+    n_mb = (B + mb_size - 1) // mb_size
+    K = epochs * n_mb
+    G = kernels.ppo_update_blocks(OBS, A, mb_size)
+    assert G > 0
+    if n_blocks is not None:
+        G = min(G, n_blocks)
+    theta = torch.as_tensor(theta0, device='cuda').clone()
+    m, v = torch.zeros_like(theta), torch.zeros_like(theta)
+    step = torch.zeros(1, dtype=torch.int32, device='cuda')
+    nbytes = kernels.ppo_update_workspace_bytes(OBS, A, B, mb_size, epochs, G)
+    ws = torch.full((nbytes,), 0xA5, dtype=torch.uint8, device='cuda')  # poisoned
+    grad = torch.zeros_like(theta)
+    loss = torch.zeros(K, G, 4, dtype=torch.float32, device='cuda')
+    status = torch.zeros(1, dtype=torch.int32, device='cuda')
+    sh = XaShuffle()
+    perm_t = None
+    if perm is not None:
+        perm_t = torch.as_tensor(np.asarray(perm, np.int32).ravel(), device='cuda')
+        sh.perm = perm_t.data_ptr()
+    else:
+        sh.perm = None
+    sh.seed, sh.rng_counter = 12345, None
+    u = XaPpoUpdateArgs()
+    u.obs_dim, u.n_actions, u.batch, u.mb_size, u.epochs = OBS, A, B, mb_size, epochs
+    u.shuffle = sh
+    u.obs, u.actions, u.old_logp = obs.data_ptr(), act.data_ptr(), logp.data_ptr()
+    u.old_values, u.returns = val.data_ptr(), ret.data_ptr()
+    u.clip_norm, u.entropy_coef, u.value_coef, u.adv_eps = 0.1, 0.01, 0.5, 1e-8
+    u.theta, u.adam_m, u.adam_v, u.adam_step = (theta.data_ptr(), m.data_ptr(), v.data_ptr(),
+                                                step.data_ptr())
+    u.adam = kernels.adam_struct(LR, B1, B2, EPS, clip_norm=CLIP_G)
+    u.workspace, u.workspace_bytes = ws.data_ptr(), nbytes
+    u.loss_out = loss.data_ptr() if want else None
+    u.grad_out = grad.data_ptr() if want else None
+    u.status = status.data_ptr()
+    u.n_blocks = G
+    kernels.ppo_update(u)
+    torch.cuda.synchronize()
+    return dict(theta=theta.cpu().numpy(), m=m.cpu().numpy(), v=v.cpu().numpy(),
+                step=int(step.item()), grad=grad.cpu().numpy(), loss=loss.cpu().numpy(),
+                status=int(status.item()), G=G, K=K)
+
+
+def f64_trajectory(theta0, bufs, mb_size, perms):
+    """The reference update (ppo/agent.py:139-191) in float64 for given permutations."""
+    obs, act, logp, val, ret = bufs
+    B = obs.shape[0]
+    th = theta0.astype(np.float64)
+    m, v = np.zeros_like(th), np.zeros_like(th)
+    t = 0
+    grads, terms = [], []
+    for perm in perms:
+        for start in range(0, B, mb_size):
+            idx = perm[start:start + mb_size]
+            adv = oracle.normalize_advantages(ret[idx], val[idx])
+            tm, g = oracle.ac_loss_grad_f64(th, obs[idx], act[idx], ret[idx], val[idx], A, 'ppo',
+                                            logp[idx], adv)
+            grads.append(g)
+            terms.append(tm)
+            g, _ = oracle.clip_by_global_norm_f64(g, CLIP_G)
+            t += 1
+            th, m, v = oracle.keras_adam_f64(th, m, v, g, t, LR, B1, B2, EPS)
+    return th, m, v, grads, terms
+
+
+def _rel(a, b):
+    return float(np.linalg.norm(np.asarray(a, np.float64) - b) / np.linalg.norm(b))
+
+
+@pytest.mark.parametrize('B,mb', [(512, 512), (8192, 8192), (600, 600)])
+def test_single_step_gradient_and_losses_vs_f64(device, B, mb):
+    """One optimizer step (E = M = 1): the raw reduced gradient and the per-minibatch loss
+    sums are scale-sensitive checks of the fused loss / backward (1e-5 rel)."""
+    bufs = _rollout_buffers(B, seed=B)
+    theta0 = _theta0(1)
+    rng = np.random.default_rng(7)
+    perm = rng.permutation(B).astype(np.int32)[None]
+    out = run_update(theta0, bufs, mb, 1, perm=perm)
+    assert out['status'] == 0 and out['step'] == 1
+    th, m, v, grads, terms = f64_trajectory(theta0, bufs, mb, perm)
+    assert _rel(out['grad'], grads[0]) < 1e-5
+    ls = out['loss'].sum(axis=1)[0]
+    assert ls[3] == B
+    np.testing.assert_allclose(ls[0], terms[0]['pg_sum'], rtol=1e-5, atol=1e-5 * B)
+    np.testing.assert_allclose(ls[1], terms[0]['vl_sum'], rtol=1e-5)
+    np.testing.assert_allclose(ls[2], terms[0]['ent_sum'], rtol=1e-5)
+    # the first Adam moments carry the clipped gradient's scale: m = (1 - b1) g_clip
+    g64, _ = oracle.clip_by_global_norm_f64(grads[0], CLIP_G)
+    assert _rel(out['m'], (1 - B1) * g64) < 1e-5
+    assert _rel(out['v'], (1 - B2) * g64 * g64) < 2e-5
+
+
+def test_multi_step_ragged_trajectory_vs_f64(device):
+    """2 epochs x 4 minibatches of a 600-sample batch with mb 198, the 4th ragged (the
+    reference slices range(0, B, mb): 600 = 3 x 198 + 6): host permutations, Adam moments
+    non-zero after the first step."""
+    B, mb, E = 600, 198, 2
+    bufs = _rollout_buffers(B, seed=11)
+    theta0 = _theta0(2)
+    rng = np.random.default_rng(3)
+    perms = np.stack([rng.permutation(B) for _ in range(E)]).astype(np.int32)
+    out = run_update(theta0, bufs, mb, E, perm=perms)
+    n_mb = 4
+    assert out['status'] == 0 and out['step'] == E * n_mb
+    th, m, v, grads, terms = f64_trajectory(theta0, bufs, mb, perms)
+    assert _rel(out['theta'] - theta0, th - theta0) < 2e-3
+    assert _rel(out['m'], m) < 2e-3
+    # every minibatch's sample count (the ragged one has 6)
+    counts = out['loss'].sum(axis=1)[:, 3]
+    np.testing.assert_array_equal(counts, [198, 198, 198, 6] * E)
+
+
+def test_fewer_blocks_than_tiles_is_the_same_update(device):
+    """With fewer resident blocks than tiles each block walks several tiles; only the f64
+    summation order of the gradient changes."""
+    B = 4096
+    bufs = _rollout_buffers(B, seed=5)
+    theta0 = _theta0(3)
+    full = run_update(theta0, bufs, 1024, 2)
+    few = run_update(theta0, bufs, 1024, 2, n_blocks=5)
+    assert full['G'] == 32 and few['G'] == 5
+    assert few['status'] == 0 and few['step'] == 8
+    assert _rel(few['grad'], full['grad'].astype(np.float64)) < 1e-5
+    assert _rel(few['theta'] - theta0, (full['theta'] - theta0).astype(np.float64)) < 1e-4
+
+
+def test_feistel_shuffle_matches_oracle_permutation(device):
+    """No host permutation: the device Feistel shuffle is oracle.shuffle_perm's."""
+    B, mb = 1024, 256
+    bufs = _rollout_buffers(B, seed=9)
+    theta0 = _theta0(4)
+    out = run_update(theta0, bufs, mb, 2)
+    perms = np.stack([oracle.shuffle_perm(B, e, 12345, 0) for e in range(2)])
+    th, m, v, grads, _ = f64_trajectory(theta0, bufs, mb, perms)
+    assert out['status'] == 0 and out['step'] == 8
+    assert _rel(out['theta'] - theta0, th - theta0) < 2e-3
+
+
+def test_agent_persistent_update_matches_chain(device, monkeypatch):
+    """Same rollout, one train step: the persistent launch and the per-minibatch chain
+    give the same parameters up to the f64 reduction order."""
+    from test_gpu_agent import make_agent
+    monkeypatch.setenv('XA_PPO_UPDATE', 'persistent')
+    a = make_agent(n_envs=32, n_steps=64, seed=5, use_graph=False)
+    monkeypatch.setenv('XA_PPO_UPDATE', 'chain')
+    b = make_agent(n_envs=32, n_steps=64, seed=5, use_graph=False)
+    assert a.update_mode == 'persistent' and b.update_mode == 'chain'
+    theta0 = a.model.theta.cpu().numpy().astype(np.float64)
+    np.testing.assert_array_equal(theta0, b.model.theta.cpu().numpy())
+    a.train_step()
+    b.train_step()
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(a.b_act.cpu().numpy(), b.b_act.cpu().numpy())
+    ta = a.model.theta.cpu().numpy().astype(np.float64)
+    tb = b.model.theta.cpu().numpy().astype(np.float64)
+    assert np.linalg.norm(ta - tb) / np.linalg.norm(tb - theta0) < 1e-4
+    assert int(a.model.optimizer.iterations.item()) == int(b.model.optimizer.iterations.item()) == 16
+    assert int(a.device_status.item()) == 0

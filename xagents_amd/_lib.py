@@ -131,6 +131,25 @@ class XaAcGradArgs(Structure):
     ]
 
 
+class XaPpoUpdateArgs(Structure):
+    _fields_ = [
+        ('obs_dim', c_int), ('n_actions', c_int),
+        ('batch', c_int), ('mb_size', c_int), ('epochs', c_int),
+        ('shuffle', XaShuffle),
+        ('obs', c_void_p), ('actions', c_void_p), ('old_logp', c_void_p),
+        ('old_values', c_void_p), ('returns', c_void_p),
+        ('clip_norm', c_float), ('entropy_coef', c_float), ('value_coef', c_float),
+        ('adv_eps', c_float),
+        ('theta', c_void_p), ('adam_m', c_void_p), ('adam_v', c_void_p), ('adam_step', c_void_p),
+        ('adam', XaAdam),
+        ('workspace', c_void_p), ('workspace_bytes', ctypes.c_size_t),
+        ('loss_out', c_void_p),
+        ('grad_out', c_void_p),
+        ('status', c_void_p),
+        ('n_blocks', c_int),
+    ]
+
+
 class XaAdamTail(Structure):
     _fields_ = [
         ('theta', c_void_p), ('m', c_void_p), ('v', c_void_p),
@@ -297,6 +316,9 @@ _SIGNATURES = {
          c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
          c_void_p],
     ),
+    'xa_ppo_update_blocks': (c_int, [c_int, c_int, c_int]),
+    'xa_ppo_update_workspace_bytes': (ctypes.c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int]),
+    'xa_ppo_update': (c_int, [POINTER(XaPpoUpdateArgs), c_void_p]),
     'xa_gemm': (c_int, [POINTER(XaGemmArgs), c_void_p]),
     'xa_gemm_splits': (c_int, [c_int, c_int, c_int]),
     'xa_gemm_workspace_floats': (ctypes.c_size_t, [c_int, c_int, c_int, c_int]),

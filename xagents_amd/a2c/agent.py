@@ -230,11 +230,10 @@ class A2C(ExecutorActorCritic, OnPolicy):
     # external events inside graph capture, so captured steps record none) --------
     def timed_train_step(self):
         """One eager train step with events around the hot launches; returns
-        {'rollout': [ms], 'ac_grad': [ms per launch]} (synchronizes)."""
+        {name: [ms per launch]} for _timed_kernels() (synchronizes)."""
         ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
-        n_grad = len(getattr(self, '_gargs_list', [None]))
-        self._kernel_events = {'rollout': [(ev(), ev())],
-                               'ac_grad': [(ev(), ev()) for _ in range(n_grad)]}
+        self._kernel_events = {name: [(ev(), ev()) for _ in range(n)]
+                               for name, n in self._timed_kernels().items()}
         try:
             # park the stream on a spin kernel so the host enqueues the whole step behind
             # it: the event pairs then bracket GPU execution, not host launch gaps
@@ -246,6 +245,10 @@ class A2C(ExecutorActorCritic, OnPolicy):
             return {k: [a.elapsed_time(b) for a, b in v] for k, v in self._kernel_events.items()}
         finally:
             self._kernel_events = None
+
+    def _timed_kernels(self):
+        """Event-bracketed launches of one eager train step: name -> count."""
+        return {'rollout': 1, 'ac_grad': 1}
 
     def _kernel_event(self, name, i, j):
         evs = getattr(self, '_kernel_events', None)

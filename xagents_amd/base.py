@@ -347,6 +347,12 @@ class BaseAgent(ABC):
         slot = self._stats_slot
         self._host_done[slot].copy_(done_out, non_blocking=True)
         self._host_epret[slot].copy_(epret_out, non_blocking=True)
+        status = getattr(self, 'device_status', None)
+        if status is not None:
+            if getattr(self, '_host_status', None) is None:
+                self._host_status = [torch.zeros(status.shape, dtype=status.dtype).pin_memory()
+                                     for _ in range(2)]
+            self._host_status[slot].copy_(status, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
         self._stats_queue.append((slot, ev))
@@ -358,6 +364,10 @@ class BaseAgent(ABC):
 
     def _fold_stats(self, slot, ev):
         ev.synchronize()
+        if getattr(self, 'device_status', None) is not None and int(self._host_status[slot].max()):
+            raise RuntimeError(
+                f'{self.__class__.__name__}: an in-launch exchange of the persistent update '
+                f'timed out (device status word set); the parameters are invalid')
         done = self._host_done[slot].numpy()[:, 1:]
         epret = self._host_epret[slot].numpy()
         t_idx, env_idx = np.nonzero(done.T)  # step-major, env-minor like step_envs

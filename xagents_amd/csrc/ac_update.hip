@@ -20,55 +20,23 @@
 // clip + Adam (measured: for PPO's 16 chained steps the redundant per-block prologue is
 // faster than a one-block tail, whose loads all miss the freshly invalidated L2).
 //
-// xa_ac_grad tile schedule (256 threads = 4 waves, 32 samples):
-//   H1 = tanh(X W1 + b1)                (VALU, K = obs)
-//   Z2 = H1 W2                          (MFMA f32 16x16x4, K = 64)
-//   heads + loss + dL/dz                (8 lanes per sample, xor shuffles)
-//   dA2 = (dZ W34^T) * (1 - H2^2)       (VALU, K = A + 1)
-//   dW2 += H1^T dA2 ; dH1 = dA2 W2^T    (MFMA f32 16x16x4, K = 32 / 64)
-//   dW1 += X^T dA1                      (VALU, K = 32)
-// MFMA operands are read from LDS as contiguous 16-byte rows: the K index lane
-// group q feeds is remapped to a contiguous block (k = 16q + kk), which only
-// reorders the f32 accumulation (tolerance-checked against float64).
+// The tile arithmetic (forward, loss, backward of 32 samples) lives in ac_tile.hpp, shared
+// with the persistent whole-train-step update (ppo_update.hip).
 #include <math.h>
 
 #include "../../include/xagents_hip.h"
+#include "ac_tile.hpp"
 #include "xa_adam.hpp"
 #include "xa_common.hpp"
 
 namespace {
 
-constexpr int H = XA_MLP_HIDDEN;
-constexpr int S = 32;    // samples per tile
-constexpr int LDW = 68;  // LDS row stride of [*][64] tiles (16-B aligned, conflict-spreading)
-constexpr int LDT = 36;  // LDS row stride of transposed [64][32] tiles
+using xa_ac::H;
+using xa_ac::S;
+using xa_ac::Offs;
+using xa_ac::offs;
 constexpr int kStatsChunk = 1024;
 constexpr int kRedThreads = 1024, kRedBatch = 16, kRedPB = 32;  // reduce: 32 row streams, one batch for <= 512 rows
-
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-// D = A B + C on a 16x16 tile, K = 4: lane l feeds A[l&15][k=l>>4], B[k=l>>4][l&15];
-// D[row = 4*(l>>4) + r][col = l&15] lands in register r (exact f32 fma chain).
-XA_DEV f32x4 mfma4(float a, float b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-}
-
-struct Offs {
-  int w1, b1, w2, b2, w3, b3, w4, b4, P;
-};
-__host__ __device__ inline Offs offs(int obs, int A) {
-  Offs o;
-  o.w1 = 0;
-  o.b1 = obs * H;
-  o.w2 = o.b1 + H;
-  o.b2 = o.w2 + H * H;
-  o.w3 = o.b2 + H;
-  o.b3 = o.w3 + H * A;
-  o.w4 = o.b3 + A;
-  o.b4 = o.w4 + H;
-  o.P = o.b4 + 1;
-  return o;
-}
 
 struct ShuffleKeys {
   uint32_t k[4];
@@ -160,30 +128,13 @@ __global__ __launch_bounds__(kMbThreads) void minibatch_kernel(XaMinibatchArgs a
 // ---------------------------------------------------------------------------
 template <int OBS, int A>
 __global__ __launch_bounds__(256) void ac_grad_kernel(XaAcGradArgs p) {
-  constexpr int AH = A + 1;            // logits + value head
-  constexpr int NSLOT = AH + 2 + OBS;  // per-feature partial sums combined at the end
-  constexpr int NREST = OBS * H + H + H + H * A + A + H + 1;  // parameters outside W2
-  constexpr int RPT = (NREST + 255) / 256;                    // of them per thread
-  __shared__ __attribute__((aligned(16))) float sW2[H * LDW];   // [i][j]
-  __shared__ __attribute__((aligned(16))) float sW2T[H * LDW];  // [j][k] = W2[k][j]
-  __shared__ __attribute__((aligned(16))) float sH1[S * LDW];   // [s][i]
-  __shared__ __attribute__((aligned(16))) float sH1T[H * LDT];  // [i][s]
-  __shared__ __attribute__((aligned(16))) float sH2[S * LDW];   // [s][j]; then dA1 [s][i]
-  __shared__ __attribute__((aligned(16))) float sdA2[S * LDW];  // [s][j]
-  __shared__ __attribute__((aligned(16))) float sdA2T[H * LDT]; // [j][s]
-  __shared__ float sW1[OBS * H], sb1[H], sb2[H], sW34[H * AH], sb34[AH];
-  __shared__ float sX[S * OBS], sdZ[S * AH];
-  __shared__ float sAct[S], sOldLp[S], sOldV[S], sRet[S], sAdvIn[S];
-  __shared__ int sValid[S];
-  __shared__ float sRed[4 * H * NSLOT];
-  __shared__ float sLoss[4][4];
-  __shared__ double sNorm[4];
+  using namespace xa_ac;
+  constexpr int RPT = Dims<OBS, A>::RPT;
+  __shared__ __attribute__((aligned(16))) TileLds<OBS, A> L;
 
   const Offs o = offs(OBS, A);
   const int tid = threadIdx.x;
   const int lane = tid & 63, w = tid >> 6;
-  const int li = lane & 15, lq = lane >> 4;     // MFMA lane coordinates
-  const int f = tid & 63, c8 = (tid >> 6) * 8;  // element-wise phases: feature, 8-sample chunk
   XA_STAMP_DECL
   XA_STAMP(10);
 
@@ -233,422 +184,97 @@ __global__ __launch_bounds__(256) void ac_grad_kernel(XaAcGradArgs p) {
 
   // ---- parameters (optionally after the pending clip + Keras Adam step) ----
   {
-    const int k0 = 4 * (tid >> 4), j0 = 4 * (tid & 15);  // this thread's 4x4 block of W2
+    ParamSlice<OBS, A> ps;
+    ps.init(tid);
     float wv[16], rv[RPT];
-    int ri[RPT];
-#pragma unroll
-    for (int q = 0; q < RPT; ++q) {
-      const int r = tid + 256 * q;
-      ri[q] = r < NREST ? (r < o.w2 ? r : r + H * H) : -1;
-    }
-    auto w2_at = [&](const float* base, int rr) {
-      return *reinterpret_cast<const float4*>(&base[o.w2 + (k0 + rr) * H + j0]);
-    };
     if (p.pend_grad == nullptr) {
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const float4 t4 = w2_at(p.theta, rr);
-        wv[4 * rr] = t4.x; wv[4 * rr + 1] = t4.y; wv[4 * rr + 2] = t4.z; wv[4 * rr + 3] = t4.w;
-      }
-#pragma unroll
-      for (int q = 0; q < RPT; ++q) rv[q] = ri[q] >= 0 ? p.theta[ri[q]] : 0.0f;
+      ps.load(p.theta, wv, rv);
     } else {
-      float gw[16], gr[RPT];
-      // every load of the step (g, theta, m, v) is issued before the first use
-      float4 tw4[4], mw4[4], vw4[4];
-      float tr[RPT], mr[RPT], vr[RPT];
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        tw4[rr] = w2_at(p.theta, rr);
-        mw4[rr] = w2_at(p.pend_m, rr);
-        vw4[rr] = w2_at(p.pend_v, rr);
-      }
-#pragma unroll
-      for (int q = 0; q < RPT; ++q) {
-        const int e = ri[q] >= 0 ? ri[q] : 0;
-        tr[q] = p.theta[e];
-        mr[q] = p.pend_m[e];
-        vr[q] = p.pend_v[e];
-      }
+      // every load of the step (theta, m, v, g) is issued before the first use
+      float mw[16], vw[16], gw[16], mr[RPT], vr[RPT], gr[RPT];
+      ps.load(p.theta, wv, rv);
+      ps.load(p.pend_m, mw, mr);
+      ps.load(p.pend_v, vw, vr);
+      ps.load(p.pend_grad, gw, gr);
       double sq = 0.0;
       const float gs = p.adam.grad_scale;
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const float4 t4 = w2_at(p.pend_grad, rr);
-        gw[4 * rr] = t4.x * gs; gw[4 * rr + 1] = t4.y * gs;
-        gw[4 * rr + 2] = t4.z * gs; gw[4 * rr + 3] = t4.w * gs;
-      }
+      for (int i = 0; i < 16; ++i) gw[i] = gw[i] * gs;
 #pragma unroll
-      for (int q = 0; q < RPT; ++q) gr[q] = ri[q] >= 0 ? p.pend_grad[ri[q]] * gs : 0.0f;
+      for (int q = 0; q < RPT; ++q) gr[q] = ps.ri[q] >= 0 ? gr[q] * gs : 0.0f;
 #pragma unroll
       for (int i = 0; i < 16; ++i) sq += (double)gw[i] * (double)gw[i];
 #pragma unroll
       for (int q = 0; q < RPT; ++q) sq += (double)gr[q] * (double)gr[q];
       XA_STAMP(20);
       sq = xa_wave_sum_f64(sq);
-      if (lane == 0) sNorm[w] = sq;
+      if (lane == 0) L.sNorm[w] = sq;
       const float alpha = adam_alpha(p.adam.lr, p.adam.beta1, p.adam.beta2, pend_t);
       __syncthreads();
       XA_STAMP(21);
       // every block forms the identical norm and step (fixed assignment and order)
-      const double tot = (sNorm[0] + sNorm[1]) + (sNorm[2] + sNorm[3]);
+      const double tot = (L.sNorm[0] + L.sNorm[1]) + (L.sNorm[2] + L.sNorm[3]);
       const float sc = clip_scale(tot, p.adam.clip_norm);
       const float omb1 = 1.0f - p.adam.beta1, omb2 = 1.0f - p.adam.beta2, eps = p.adam.eps;
-      const bool writer = blockIdx.x == 0;
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const float4 t4 = tw4[rr], m4 = mw4[rr], v4 = vw4[rr];
-        float th[4] = {t4.x, t4.y, t4.z, t4.w}, mm[4] = {m4.x, m4.y, m4.z, m4.w},
-              vv[4] = {v4.x, v4.y, v4.z, v4.w};
+      for (int i = 0; i < 16; ++i) adam_elem(gw[i] * sc, wv[i], mw[i], vw[i], alpha, omb1, omb2, eps);
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          adam_elem(gw[4 * rr + c] * sc, th[c], mm[c], vv[c], alpha, omb1, omb2, eps);
-          wv[4 * rr + c] = th[c];
-        }
-        if (writer) {
-          const size_t off = o.w2 + (k0 + rr) * H + j0;
-          *reinterpret_cast<float4*>(&p.theta_out[off]) = make_float4(th[0], th[1], th[2], th[3]);
-          *reinterpret_cast<float4*>(&p.m_out[off]) = make_float4(mm[0], mm[1], mm[2], mm[3]);
-          *reinterpret_cast<float4*>(&p.v_out[off]) = make_float4(vv[0], vv[1], vv[2], vv[3]);
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < RPT; ++q) {
-        if (ri[q] < 0) continue;
-        float th = tr[q], mm = mr[q], vv = vr[q];
-        adam_elem(gr[q] * sc, th, mm, vv, alpha, omb1, omb2, eps);
-        rv[q] = th;
-        if (writer) {
-          p.theta_out[ri[q]] = th;
-          p.m_out[ri[q]] = mm;
-          p.v_out[ri[q]] = vv;
-        }
+      for (int q = 0; q < RPT; ++q) adam_elem(gr[q] * sc, rv[q], mr[q], vr[q], alpha, omb1, omb2, eps);
+      if (blockIdx.x == 0) {
+        ps.store(p.theta_out, wv, rv);
+        ps.store(p.m_out, mw, mr);
+        ps.store(p.v_out, vw, vr);
       }
     }
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-      *reinterpret_cast<float4*>(&sW2[(k0 + rr) * LDW + j0]) =
-          make_float4(wv[4 * rr], wv[4 * rr + 1], wv[4 * rr + 2], wv[4 * rr + 3]);
-      *reinterpret_cast<float4*>(&sW2T[(j0 + rr) * LDW + k0]) =
-          make_float4(wv[rr], wv[4 + rr], wv[8 + rr], wv[12 + rr]);
-    }
-#pragma unroll
-    for (int q = 0; q < RPT; ++q) {
-      const int e = ri[q];
-      if (e < 0) continue;
-      const float x = rv[q];
-      if (e < o.b1) sW1[e] = x;
-      else if (e < o.w2) sb1[e - o.b1] = x;
-      else if (e < o.w3) sb2[e - o.b2] = x;
-      else if (e < o.b3) {
-        const int jj = (e - o.w3) / A, a = (e - o.w3) - jj * A;
-        sW34[jj * AH + a] = x;
-      } else if (e < o.w4) sb34[e - o.b3] = x;
-      else if (e < o.b4) sW34[(e - o.w4) * AH + A] = x;
-      else sb34[A] = x;
-    }
+    ps.to_lds(L, wv, rv);
   }
 
   XA_STAMP(22);
-  float adv_mean = 0.0f, adv_std = 0.0f;
+  LossCfg cfg;
+  cfg.is_ppo = is_ppo;
+  cfg.has_adv_in = p.adv_in != nullptr;
+  cfg.loss_scale = p.loss_scale;
+  cfg.clip_norm = p.clip_norm;
+  cfg.value_coef = p.value_coef;
+  cfg.entropy_coef = p.entropy_coef;
+  cfg.adv_eps = p.adv_eps;
+  cfg.adv_mean = cfg.adv_std = 0.0f;
   if (is_ppo && p.adv_in == nullptr) {
     const double n = p.adv_count;
     const double mean = st1 / n;
     const double var = fmax(st2 / n - mean * mean, 0.0);
-    adv_mean = (float)mean;
-    adv_std = (float)sqrt(var);
+    cfg.adv_mean = (float)mean;
+    cfg.adv_std = (float)sqrt(var);
   }
 
-  // register accumulators
-  f32x4 gW2[4];
-#pragma unroll
-  for (int jt = 0; jt < 4; ++jt) gW2[jt] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-  float gW34[AH], gW1[OBS];
-#pragma unroll
-  for (int a = 0; a < AH; ++a) gW34[a] = 0.0f;
-#pragma unroll
-  for (int k = 0; k < OBS; ++k) gW1[k] = 0.0f;
-  float gb1 = 0.0f, gb2 = 0.0f, gb34 = 0.0f;
-  float l_pg = 0.0f, l_v = 0.0f, l_ent = 0.0f, l_cnt = 0.0f;
-
+  TileAcc<OBS, A> acc;
+  acc.zero();
   for (int tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
     __syncthreads();
     XA_STAMP(11);
     // ---- gather: the prefetched samples into LDS, next tile's loads issued ----
     if (tid < S) {
-      sValid[tid] = n_valid;
+      L.sValid[tid] = n_valid;
 #pragma unroll
-      for (int k = 0; k < OBS; ++k) sX[tid * OBS + k] = nx[k];
-      sAct[tid] = n_act;
-      sRet[tid] = n_ret;
-      sOldV[tid] = n_oldv;
-      sOldLp[tid] = n_oldlp;
-      sAdvIn[tid] = n_adv;
+      for (int k = 0; k < OBS; ++k) L.sX[tid * OBS + k] = nx[k];
+      L.sAct[tid] = n_act;
+      L.sRet[tid] = n_ret;
+      L.sOldV[tid] = n_oldv;
+      L.sOldLp[tid] = n_oldlp;
+      L.sAdvIn[tid] = n_adv;
     }
     if (tile + (int)gridDim.x < n_tiles) fetch_tile(tile + gridDim.x);
     __syncthreads();
     XA_STAMP(12);
-    // ---- H1 = tanh(X W1 + b1): feature f, samples c8..c8+7 ----
-    {
-      float hv[8];
-#pragma unroll
-      for (int ss = 0; ss < 8; ++ss) {
-        const int s = c8 + ss;
-        float z = 0.0f;
-#pragma unroll
-        for (int k = 0; k < OBS; ++k) z = fmaf(sX[s * OBS + k], sW1[k * H + f], z);
-        hv[ss] = xa_tanhf(z + sb1[f]);
-        sH1[s * LDW + f] = hv[ss];
-      }
-      *reinterpret_cast<float4*>(&sH1T[f * LDT + c8]) = make_float4(hv[0], hv[1], hv[2], hv[3]);
-      *reinterpret_cast<float4*>(&sH1T[f * LDT + c8 + 4]) = make_float4(hv[4], hv[5], hv[6], hv[7]);
-    }
-    __syncthreads();
-    XA_STAMP(13);
-    // ---- Z2 = H1 W2 (MFMA): wave w owns hidden columns 16w..16w+15 ----
-    {
-      float bv[16];
-#pragma unroll
-      for (int v4 = 0; v4 < 4; ++v4) {
-        const float4 t4 = *reinterpret_cast<const float4*>(&sW2T[(16 * w + li) * LDW + 16 * lq + 4 * v4]);
-        bv[4 * v4] = t4.x; bv[4 * v4 + 1] = t4.y; bv[4 * v4 + 2] = t4.z; bv[4 * v4 + 3] = t4.w;
-      }
-      const float bias = sb2[16 * w + li];
-#pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        float av[16];
-#pragma unroll
-        for (int v4 = 0; v4 < 4; ++v4) {
-          const float4 t4 = *reinterpret_cast<const float4*>(&sH1[(16 * st + li) * LDW + 16 * lq + 4 * v4]);
-          av[4 * v4] = t4.x; av[4 * v4 + 1] = t4.y; av[4 * v4 + 2] = t4.z; av[4 * v4 + 3] = t4.w;
-        }
-        f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-        for (int kk = 0; kk < 16; ++kk) acc = mfma4(av[kk], bv[kk], acc);
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          sH2[(16 * st + 4 * lq + r) * LDW + 16 * w + li] = xa_tanhf(acc[r] + bias);
-      }
-    }
-    __syncthreads();
-    XA_STAMP(14);
-    // ---- heads + loss + dL/dz: 8 lanes per sample ----
-    {
-      const int s = tid >> 3, pp = tid & 7;
-      float z[AH];
-#pragma unroll
-      for (int a = 0; a < AH; ++a) z[a] = 0.0f;
-#pragma unroll
-      for (int jj = 0; jj < 8; ++jj) {
-        const int j = 8 * pp + jj;
-        const float hj = sH2[s * LDW + j];
-#pragma unroll
-        for (int a = 0; a < AH; ++a) z[a] = fmaf(hj, sW34[j * AH + a], z[a]);
-      }
-#pragma unroll
-      for (int a = 0; a < AH; ++a) z[a] = xa_sum8(z[a]) + sb34[a];
-      if (pp == 0) {
-        float dz[AH];
-#pragma unroll
-        for (int a = 0; a < AH; ++a) dz[a] = 0.0f;
-        if (sValid[s]) {
-          const int act = (int)sAct[s];
-          float m = z[0];
-#pragma unroll
-          for (int a = 1; a < A; ++a) m = fmaxf(m, z[a]);
-          float e[A], ssum = 0.0f;
-#pragma unroll
-          for (int a = 0; a < A; ++a) {
-            e[a] = xa_expf(z[a] - m);
-            ssum = ssum + e[a];
-          }
-          const float ls = xa_logf(ssum);
-          float lp[A], pr[A], ent = 0.0f, logp = 0.0f;
-#pragma unroll
-          for (int a = 0; a < A; ++a) {
-            lp[a] = (z[a] - m) - ls;
-            pr[a] = e[a] / ssum;
-            ent = ent - pr[a] * lp[a];
-            if (a == act) logp = lp[a];
-          }
-          const float v = z[A];
-          const float R = sRet[s];
-          const float oldv = sOldV[s];
-          const float adv_raw = R - oldv;
-          const float sc = p.loss_scale;
-          float dlogp, dv, pg, vl;
-          if (is_ppo) {
-            const float adv =
-                p.adv_in ? sAdvIn[s] : (adv_raw - adv_mean) / (adv_std + p.adv_eps);
-            const float ratio = xa_expf(logp - sOldLp[s]);
-            const float c = p.clip_norm;
-            const float pg1 = -adv * ratio;
-            const float pg2 = -adv * fminf(fmaxf(ratio, 1.0f - c), 1.0f + c);
-            pg = fmaxf(pg1, pg2);
-            // tf.maximum routes the gradient to its first input when x >= y; the
-            // second input's gradient passes tf.clip_by_value only inside [lo, hi]
-            const bool r_in = ratio >= 1.0f - c && ratio <= 1.0f + c;
-            dlogp = (pg1 >= pg2 || r_in) ? (sc * -adv) * ratio : 0.0f;
-            const float dvo = v - oldv;
-            const float vclip = oldv + fminf(fmaxf(dvo, -c), c);
-            const float vl1 = (v - R) * (v - R);
-            const float vl2 = (vclip - R) * (vclip - R);
-            vl = fmaxf(vl1, vl2);
-            // rounding can make oldv + (v - oldv) != v inside the clip range: the
-            // clipped branch then still carries the gradient 2 (v_clip - R)
-            const float kv = sc * p.value_coef * 0.5f * 2.0f;
-            if (vl1 >= vl2) dv = kv * (v - R);
-            else dv = (dvo >= -c && dvo <= c) ? kv * (vclip - R) : 0.0f;
-          } else {
-            pg = -(adv_raw * logp);
-            dlogp = -sc * adv_raw;
-            vl = (v - R) * (v - R);
-            dv = sc * p.value_coef * 2.0f * (v - R);
-          }
-          const float ec = sc * p.entropy_coef;
-#pragma unroll
-          for (int a = 0; a < A; ++a)
-            dz[a] = dlogp * ((a == act ? 1.0f : 0.0f) - pr[a]) + ec * pr[a] * (lp[a] + ent);
-          dz[A] = dv;
-          l_pg += pg;
-          l_v += vl;
-          l_ent += ent;
-          l_cnt += 1.0f;
-        }
-#pragma unroll
-        for (int a = 0; a < AH; ++a) sdZ[s * AH + a] = dz[a];
-      }
-    }
-    __syncthreads();
-    XA_STAMP(15);
-    // ---- dA2 = (dZ W34^T) * (1 - H2^2); head / b2 partial grads ----
-    {
-      float dv8[8];
-#pragma unroll
-      for (int ss = 0; ss < 8; ++ss) {
-        const int s = c8 + ss;
-        float dh = 0.0f;
-#pragma unroll
-        for (int a = 0; a < AH; ++a) dh = fmaf(sdZ[s * AH + a], sW34[f * AH + a], dh);
-        const float hv = sH2[s * LDW + f];
-#pragma unroll
-        for (int a = 0; a < AH; ++a) gW34[a] = fmaf(hv, sdZ[s * AH + a], gW34[a]);
-        const float d = dh * (1.0f - hv * hv);
-        gb2 = gb2 + d;
-        sdA2[s * LDW + f] = d;
-        dv8[ss] = d;
-      }
-      *reinterpret_cast<float4*>(&sdA2T[f * LDT + c8]) = make_float4(dv8[0], dv8[1], dv8[2], dv8[3]);
-      *reinterpret_cast<float4*>(&sdA2T[f * LDT + c8 + 4]) = make_float4(dv8[4], dv8[5], dv8[6], dv8[7]);
-      if (tid < AH) {
-        float acc = gb34;
-        for (int s = 0; s < S; ++s) acc = acc + sdZ[s * AH + tid];
-        gb34 = acc;
-      }
-    }
-    __syncthreads();
-    XA_STAMP(16);
-    // ---- dW2 += H1^T dA2 (rows 16w.., K = samples 8q+kk) and dH1 = dA2 W2^T ----
-    {
-      float av[8];
-      {
-        const float4 t0 = *reinterpret_cast<const float4*>(&sH1T[(16 * w + li) * LDT + 8 * lq]);
-        const float4 t1 = *reinterpret_cast<const float4*>(&sH1T[(16 * w + li) * LDT + 8 * lq + 4]);
-        av[0] = t0.x; av[1] = t0.y; av[2] = t0.z; av[3] = t0.w;
-        av[4] = t1.x; av[5] = t1.y; av[6] = t1.z; av[7] = t1.w;
-      }
-#pragma unroll
-      for (int jt = 0; jt < 4; ++jt) {
-        const float4 t0 = *reinterpret_cast<const float4*>(&sdA2T[(16 * jt + li) * LDT + 8 * lq]);
-        const float4 t1 = *reinterpret_cast<const float4*>(&sdA2T[(16 * jt + li) * LDT + 8 * lq + 4]);
-        const float bv[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
-#pragma unroll
-        for (int kk = 0; kk < 8; ++kk) gW2[jt] = mfma4(av[kk], bv[kk], gW2[jt]);
-      }
-      float wv[16];
-#pragma unroll
-      for (int v4 = 0; v4 < 4; ++v4) {
-        const float4 t4 = *reinterpret_cast<const float4*>(&sW2[(16 * w + li) * LDW + 16 * lq + 4 * v4]);
-        wv[4 * v4] = t4.x; wv[4 * v4 + 1] = t4.y; wv[4 * v4 + 2] = t4.z; wv[4 * v4 + 3] = t4.w;
-      }
-#pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        float dv16[16];
-#pragma unroll
-        for (int v4 = 0; v4 < 4; ++v4) {
-          const float4 t4 = *reinterpret_cast<const float4*>(&sdA2[(16 * st + li) * LDW + 16 * lq + 4 * v4]);
-          dv16[4 * v4] = t4.x; dv16[4 * v4 + 1] = t4.y; dv16[4 * v4 + 2] = t4.z; dv16[4 * v4 + 3] = t4.w;
-        }
-        f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-        for (int kk = 0; kk < 16; ++kk) acc = mfma4(dv16[kk], wv[kk], acc);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int s = 16 * st + 4 * lq + r;
-          const float h1 = sH1[s * LDW + 16 * w + li];
-          sH2[s * LDW + 16 * w + li] = acc[r] * (1.0f - h1 * h1);  // dA1
-        }
-      }
-    }
-    __syncthreads();
-    XA_STAMP(17);
-    // ---- dW1 += X^T dA1 ; db1 ----
-#pragma unroll
-    for (int ss = 0; ss < 8; ++ss) {
-      const int s = c8 + ss;
-      const float d = sH2[s * LDW + f];
-      gb1 = gb1 + d;
-#pragma unroll
-      for (int k = 0; k < OBS; ++k) gW1[k] = fmaf(sX[s * OBS + k], d, gW1[k]);
-    }
+    tile_compute<OBS, A>(L, acc, cfg);
   }
 
   XA_STAMP(18);
-  // ---- combine the 4 sample-chunk partials per feature, write the partial row ----
   float* part = p.partials + (size_t)blockIdx.x * o.P;
-  {
-    float* r = sRed + ((tid >> 6) * H + f) * NSLOT;
-#pragma unroll
-    for (int a = 0; a < AH; ++a) r[a] = gW34[a];
-    r[AH] = gb2;
-    r[AH + 1] = gb1;
-#pragma unroll
-    for (int k = 0; k < OBS; ++k) r[AH + 2 + k] = gW1[k];
-  }
-#pragma unroll
-  for (int jt = 0; jt < 4; ++jt)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) part[o.w2 + (16 * w + 4 * lq + r) * H + 16 * jt + li] = gW2[jt][r];
-  if (tid < AH) {
-    if (tid < A) part[o.b3 + tid] = gb34;
-    else part[o.b4] = gb34;
-  }
-  __syncthreads();
-  for (int e = tid; e < H * NSLOT; e += 256) {
-    const int ff = e / NSLOT, slot = e - ff * NSLOT;
-    const float v = ((sRed[(0 * H + ff) * NSLOT + slot] + sRed[(1 * H + ff) * NSLOT + slot]) +
-                     (sRed[(2 * H + ff) * NSLOT + slot] + sRed[(3 * H + ff) * NSLOT + slot]));
-    if (slot < A) part[o.w3 + ff * A + slot] = v;
-    else if (slot == A) part[o.w4 + ff] = v;
-    else if (slot == AH) part[o.b2 + ff] = v;
-    else if (slot == AH + 1) part[o.b1 + ff] = v;
-    else part[o.w1 + (slot - AH - 2) * H + ff] = v;
-  }
+  tile_write_row<OBS, A>(L, acc, [&](int i, float v) { part[i] = v; });
   if (p.loss_partials) {
-    l_pg = xa_wave_sum(l_pg);
-    l_v = xa_wave_sum(l_v);
-    l_ent = xa_wave_sum(l_ent);
-    l_cnt = xa_wave_sum(l_cnt);
-    if (lane == 0) {
-      sLoss[w][0] = l_pg;
-      sLoss[w][1] = l_v;
-      sLoss[w][2] = l_ent;
-      sLoss[w][3] = l_cnt;
-    }
-    __syncthreads();
-    if (tid < 4)
-      p.loss_partials[(size_t)blockIdx.x * 4 + tid] =
-          (sLoss[0][tid] + sLoss[1][tid]) + (sLoss[2][tid] + sLoss[3][tid]);
+    const float ls = tile_loss_sums<OBS, A>(L, acc);
+    if (tid < 4) p.loss_partials[(size_t)blockIdx.x * 4 + tid] = ls;
   }
   XA_STAMP(19);
 }

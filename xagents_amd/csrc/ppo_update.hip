@@ -1,0 +1,528 @@
+// Persistent PPO update: every optimizer step of one train step -- E epochs x M
+// minibatches of shuffle, per-minibatch advantage normalisation, forward, clipped loss,
+// backward, tf.clip_by_global_norm and Keras Adam -- in ONE launch.
+// Replaces PPO.get_mini_batches + run_ppo_epochs + update_gradients
+// (xagents/ppo/agent.py:96-191); same arithmetic as the per-minibatch chain
+// (xa_ppo_minibatches -> E*M x [xa_ac_grad -> xa_grad_reduce] -> xa_clip_adam), minus
+// its 2 E*M + 2 launches and its partial-row round trips through separate kernels.
+//
+// G resident workgroups (one per CU, G = min(32-sample tiles per minibatch, resident
+// capacity)); workgroup b owns tiles b, b + G, ... of every minibatch.
+//   phase 0   advantage sums of every (minibatch, workgroup) -> hop -> per-minibatch
+//             mean / population std in LDS (ppo/agent.py:180-183)
+//   per minibatch k:
+//     A  forward + loss + backward of the block's tiles (ac_tile.hpp) -> the block's
+//        gradient row [P] -> hop
+//     B  block b reduces parameters [b PB, (b+1) PB) over the G rows in a fixed order
+//        (f64) -> g slice + its f64 sum of squares -> hop
+//     C  every block: global norm from the G sums (fixed order, identical in every
+//        block), clip + Keras Adam with t = t0 + k + 1 on its register-resident slice
+//        of theta / m / v (ac_tile.hpp ParamSlice), refresh the LDS weight tiles
+//   block 0 stores theta / m / v and the Adam step count at the end.
+// Hops follow the write-through hand-off (cdna_hip_programming.md Guideline 16,
+// MI355X_MICROARCH.md visibility table row 1): every handed-off word is stored with a
+// write-through (sc1) store, every storing wave drains (s_waitcnt vmcnt(0)), a barrier,
+// ONE lane adds 1 to an agent-scope counter; the consumer's ONE lane polls the counter
+// relaxed (sc1 load), a barrier, then every load of the handed-off words is an sc1
+// load. Counters are zeroed by a memset node in front of every launch and count
+// arrivals within the call. Spins are bounded (wall clock); a timeout raises the
+// abort word and `status`, and every block leaves.
+#include <math.h>
+
+#include "../../include/xagents_hip.h"
+#include "ac_tile.hpp"
+#include "xa_adam.hpp"
+#include "xa_common.hpp"
+
+namespace {
+
+using namespace xa_ac;
+
+typedef __attribute__((address_space(1))) unsigned gu32;
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+
+constexpr int kMaxSteps = 512;              // E * M optimizer steps per launch
+constexpr int kCtlBytes = 256;              // control words at the workspace start
+constexpr uint64_t kSpinTicks = 200000000;  // 2 s of the 100 MHz wall clock per hop
+enum { kCntStats = 0, kCntRows = 1, kCntGrad = 2, kAbort = 3 };
+
+// ---- write-through hand-off primitives (global address space, agent scope) ----
+XA_DEV void st_wt(float* p, float v) {
+  __hip_atomic_store((gu32*)p, __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+XA_DEV void st_wt(double* p, double v) {
+  __hip_atomic_store((gu64*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+XA_DEV float ld_wt(const float* p) {
+  return __uint_as_float(__hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+XA_DEV double ld_wt(const double* p) {
+  return __longlong_as_double(
+      (long long)__hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+constexpr int kRsrcWord3 = 0x00020000;  // raw buffer, gfx9-family resource word 3
+constexpr int kAuxSc1 = 16;             // buffer instruction aux bits: write-through (sc1)
+
+XA_DEV __amdgpu_buffer_rsrc_t rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, bytes, kRsrcWord3);
+}
+XA_DEV void st_wt4(__amdgpu_buffer_rsrc_t r, uint32_t byte_off, float4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(f32x4v{v.x, v.y, v.z, v.w}, r, byte_off, 0, kAuxSc1);
+}
+XA_DEV float4 ld_wt4(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
+  const f32x4v v = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, kAuxSc1);
+  return make_float4(v[0], v[1], v[2], v[3]);
+}
+
+struct Ws {
+  unsigned* ctl;    // [kCtlBytes / 4], zeroed per launch
+  float* rows;      // [G, PP] per-block gradient rows, PP = P rounded up to 4 floats
+  float* g;         // [PP] reduced gradient
+  double* sumsq;    // [G] f64 sums of squares of the g slices
+  double* adv;      // [K, G, 2] f64 advantage sums
+};
+
+__host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+__host__ __device__ inline int padded(int P) { return (P + 3) & ~3; }
+
+__host__ __device__ inline Ws carve(void* base, int G, int P, int K) {
+  Ws w;
+  char* c = (char*)base;
+  size_t off = 0;
+  w.ctl = (unsigned*)(c + off);
+  off += kCtlBytes;
+  w.rows = (float*)(c + off);
+  off = align_up(off + (size_t)G * padded(P) * sizeof(float), 256);
+  w.g = (float*)(c + off);
+  off = align_up(off + (size_t)padded(P) * sizeof(float), 256);
+  w.sumsq = (double*)(c + off);
+  off = align_up(off + (size_t)G * sizeof(double), 256);
+  w.adv = (double*)(c + off);
+  return w;
+}
+
+__host__ __device__ inline size_t ws_bytes(int G, int P, int K) {
+  size_t off = kCtlBytes;
+  off = align_up(off + (size_t)G * padded(P) * sizeof(float), 256);
+  off = align_up(off + (size_t)padded(P) * sizeof(float), 256);
+  off = align_up(off + (size_t)G * sizeof(double), 256);
+  off += (size_t)K * G * 2 * sizeof(double);
+  return align_up(off, 256);
+}
+
+struct ShufKeys {
+  uint32_t k[4];
+  uint32_t half_bits;
+};
+
+// same keys / permutation as xa_ppo_minibatches (ac_update.hip)
+XA_DEV ShufKeys shuf_keys(const XaShuffle& sh, uint64_t ctr, int epoch, int batch) {
+  ShufKeys s;
+  const xa_u4 r = xa_philox((uint32_t)epoch, 0x5u, (uint32_t)ctr, (uint32_t)(ctr >> 32),
+                            (uint32_t)sh.seed, (uint32_t)(sh.seed >> 32));
+  s.k[0] = r.x;
+  s.k[1] = r.y;
+  s.k[2] = r.z;
+  s.k[3] = r.w;
+  const uint32_t bits = batch <= 1 ? 1u : 32u - __clz((uint32_t)(batch - 1));
+  s.half_bits = (bits + 1u) / 2u;
+  if (s.half_bits == 0) s.half_bits = 1;
+  return s;
+}
+
+XA_DEV int shuf_index(const XaShuffle& sh, const ShufKeys& keys, int epoch, int batch, int g) {
+  if (sh.perm) return sh.perm[(size_t)epoch * batch + g];
+  return (int)xa_permute((uint32_t)g, (uint32_t)batch, keys.half_bits, keys.k[0], keys.k[1],
+                         keys.k[2], keys.k[3]);
+}
+
+template <int OBS, int A>
+struct UpdLds {
+  TileLds<OBS, A> t;
+  alignas(16) float row[(offs(OBS, A).P + 3) & ~3];  // the block's gradient row, staged
+  float stat[kMaxSteps][2];  // per optimizer step: advantage mean, population std
+  double red[256 * 4];
+  double wsum[4];
+  int flag;
+};
+
+// Publish: every wave drained its write-through stores, then ONE lane counts the
+// block in. Contains a __syncthreads().
+XA_DEV void hop_signal(unsigned* ctl, int which) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    __hip_atomic_fetch_add((gu32*)(ctl + which), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Consume: ONE lane polls the counter (relaxed sc1 loads, bounded by the wall clock and
+// the abort word); the block then leaves the barrier together. Returns false on abort.
+XA_DEV bool hop_wait(unsigned* ctl, int which, unsigned target, int* status, int& lds_flag) {
+  if (threadIdx.x == 0) {
+    int ok = 1;
+    const uint64_t t0 = wall_clock64();
+    while (__hip_atomic_load((gu32*)(ctl + which), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+           target) {
+      if (__hip_atomic_load((gu32*)(ctl + kAbort), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+        ok = 0;
+        break;
+      }
+      if (wall_clock64() - t0 > kSpinTicks) {
+        __hip_atomic_store((gu32*)(ctl + kAbort), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (status) __hip_atomic_store((gu32*)status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    lds_flag = ok;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no load moves above the poll
+  __syncthreads();
+  return lds_flag != 0;
+}
+
+template <int OBS, int A>
+__global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws ws, int K,
+                                                          int n_mb) {
+  constexpr int RPT = Dims<OBS, A>::RPT;
+  __shared__ __attribute__((aligned(16))) UpdLds<OBS, A> U;
+  TileLds<OBS, A>& L = U.t;
+  const Offs o = offs(OBS, A);
+  const int P = o.P;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int G = gridDim.x, b = blockIdx.x;
+  const int B = p.batch, MB = p.mb_size;
+  const uint64_t ctr = p.shuffle.rng_counter ? *p.shuffle.rng_counter : 0ull;
+  XA_STAMP_DECL
+  XA_STAMP(30);
+
+  // ---- phase 0: advantage sums of this block's samples of every minibatch ----
+  for (int k = w; k < K; k += 4) {
+    const int e = k / n_mb, m = k - e * n_mb;
+    const int start = m * MB, cnt = min(MB, B - start);
+    const int n_tiles = (cnt + S - 1) / S;
+    const ShufKeys keys = shuf_keys(p.shuffle, ctr, e, B);
+    const int mine = n_tiles > b ? (n_tiles - b + G - 1) / G : 0;  // tiles of this block
+    double s1 = 0.0, s2 = 0.0;
+    for (int j = lane; j < mine * S; j += 64) {
+      const int q = (b + (j / S) * G) * S + (j % S);
+      if (q >= cnt) continue;
+      const int idx = shuf_index(p.shuffle, keys, e, B, start + q);
+      const float adv = p.returns[idx] - p.old_values[idx];
+      s1 += (double)adv;
+      s2 += (double)adv * (double)adv;
+    }
+    s1 = xa_wave_sum_f64(s1);
+    s2 = xa_wave_sum_f64(s2);
+    if (lane == 0) {
+      st_wt(ws.adv + ((size_t)k * G + b) * 2, s1);
+      st_wt(ws.adv + ((size_t)k * G + b) * 2 + 1, s2);
+    }
+  }
+  hop_signal(ws.ctl, kCntStats);
+  XA_STAMP(31);
+
+  // parameters: theta / m / v slices in registers for the whole launch
+  ParamSlice<OBS, A> ps;
+  ps.init(tid);
+  float wv[16], rv[RPT], mw[16], mr[RPT], vw[16], vr[RPT];
+  ps.load(p.theta, wv, rv);
+  ps.load(p.adam_m, mw, mr);
+  ps.load(p.adam_v, vw, vr);
+  const int t0 = *p.adam_step;
+  ps.to_lds(L, wv, rv);
+
+  XA_STAMP(32);
+  if (!hop_wait(ws.ctl, kCntStats, (unsigned)G, p.status, U.flag)) return;
+  XA_STAMP(33);
+  for (int k = w; k < K; k += 4) {
+    const int m = k % n_mb;
+    const double n = (double)min(MB, B - m * MB);
+    double s1 = 0.0, s2 = 0.0;
+    for (int gi = lane; gi < G; gi += 64) {
+      s1 += ld_wt(ws.adv + ((size_t)k * G + gi) * 2);
+      s2 += ld_wt(ws.adv + ((size_t)k * G + gi) * 2 + 1);
+    }
+    s1 = xa_wave_sum_f64(s1);
+    s2 = xa_wave_sum_f64(s2);
+    if (lane == 0) {
+      const double mean = s1 / n;
+      const double var = fmax(s2 / n - mean * mean, 0.0);
+      U.stat[k][0] = (float)mean;
+      U.stat[k][1] = (float)sqrt(var);
+    }
+  }
+
+  // per-sample inputs of the next tile (threads < S), fetched one tile ahead -- across
+  // minibatch boundaries too: they do not depend on the parameters. The next step's
+  // first tile is fetched between the row hop's signal and wait (off the critical path).
+  float nx[OBS], n_act = 0.0f, n_ret = 0.0f, n_oldv = 0.0f, n_oldlp = 0.0f;
+  int n_valid = 0;
+  auto fetch_tile = [&](int k, int tile) {
+    if (tid >= S) return;
+    long idx = -1;
+    if (k < K) {
+      const int e = k / n_mb, m = k - e * n_mb;
+      const int start = m * MB, cnt = min(MB, B - start);
+      const int q = tile * S + tid;
+      if (q < cnt) {
+        const ShufKeys keys = shuf_keys(p.shuffle, ctr, e, B);
+        idx = shuf_index(p.shuffle, keys, e, B, start + q);
+      }
+    }
+    n_valid = idx >= 0;
+    const size_t ix = idx >= 0 ? (size_t)idx : 0;
+#pragma unroll
+    for (int kk = 0; kk < OBS; ++kk) nx[kk] = idx >= 0 ? p.obs[ix * OBS + kk] : 0.0f;
+    n_act = idx >= 0 ? (float)p.actions[ix] : 0.0f;
+    n_ret = idx >= 0 ? p.returns[ix] : 0.0f;
+    n_oldv = idx >= 0 ? p.old_values[ix] : 0.0f;
+    n_oldlp = idx >= 0 ? p.old_logp[ix] : 0.0f;
+  };
+  fetch_tile(0, b);
+
+  LossCfg cfg;
+  cfg.is_ppo = true;
+  cfg.has_adv_in = false;
+  cfg.clip_norm = p.clip_norm;
+  cfg.value_coef = p.value_coef;
+  cfg.entropy_coef = p.entropy_coef;
+  cfg.adv_eps = p.adv_eps;
+  const float omb1 = 1.0f - p.adam.beta1, omb2 = 1.0f - p.adam.beta2;
+  // rows are PP = P rounded up to 4 floats; block b reduces float4 columns [c0, c0 + nc)
+  const int PP = padded(P), C4 = PP / 4;
+  const int CB = (C4 + G - 1) / G;
+  const int c0 = min(C4, b * CB), nc = min(C4, c0 + CB) - c0;
+  const __amdgpu_buffer_rsrc_t rows_r = rsrc(ws.rows, (uint32_t)((size_t)G * PP * 4));
+  const __amdgpu_buffer_rsrc_t g_r = rsrc(ws.g, (uint32_t)(PP * 4));
+  float* srow = U.row;
+  for (int i = P + tid; i < PP; i += 256) srow[i] = 0.0f;  // the pad stays zero
+
+  TileAcc<OBS, A> acc;
+  for (int k = 0; k < K; ++k) {
+    const int m = k % n_mb;
+    const int cnt = min(MB, B - m * MB);
+    const int n_tiles = (cnt + S - 1) / S;
+    __syncthreads();  // U.stat, the LDS weights of the previous step
+    cfg.adv_mean = U.stat[k][0];
+    cfg.adv_std = U.stat[k][1];
+    cfg.loss_scale = 1.0f / (float)cnt;
+    acc.zero();
+    XA_STAMP(34);
+    // ---- A: forward + loss + backward of this block's tiles ----
+    for (int tile = b; tile < n_tiles; tile += G) {
+      __syncthreads();
+      if (tid < S) {
+        L.sValid[tid] = n_valid;
+#pragma unroll
+        for (int kk = 0; kk < OBS; ++kk) L.sX[tid * OBS + kk] = nx[kk];
+        L.sAct[tid] = n_act;
+        L.sRet[tid] = n_ret;
+        L.sOldV[tid] = n_oldv;
+        L.sOldLp[tid] = n_oldlp;
+        L.sAdvIn[tid] = 0.0f;
+      }
+      if (tile + G < n_tiles) fetch_tile(k, tile + G);
+      __syncthreads();
+      XA_STAMP(35);
+      tile_compute<OBS, A>(L, acc, cfg, [&](int slot) { XA_STAMP(slot); });
+      XA_STAMP(36);
+    }
+    // ---- the block's gradient row: staged in LDS, published with 16-B write-through ----
+    tile_write_row<OBS, A>(L, acc, [&](int i, float v) { srow[i] = v; });
+    if (p.loss_out) {
+      const float ls = tile_loss_sums<OBS, A>(L, acc);
+      if (tid < 4) p.loss_out[((size_t)k * G + b) * 4 + tid] = ls;
+    }
+    __syncthreads();
+    for (int c = tid; c < C4; c += 256)
+      st_wt4(rows_r, (uint32_t)(((size_t)b * PP + 4 * c) * 4),
+             *reinterpret_cast<const float4*>(&srow[4 * c]));
+    XA_STAMP(37);
+    hop_signal(ws.ctl, kCntRows);
+    fetch_tile(k + 1, b);  // the next step's first tile, while the other blocks finish
+    XA_STAMP(38);
+    if (!hop_wait(ws.ctl, kCntRows, (unsigned)(G * (k + 1)), p.status, U.flag)) return;
+    XA_STAMP(39);
+
+    // ---- B: fixed-order reduction of float4 columns [c0, c0 + nc) over the G rows ----
+    double sq = 0.0;
+    if (nc > 0) {
+      const int ncol = min(nc, 256), RG = 256 / ncol;
+      const int rg = tid / ncol, cq = tid - rg * ncol;
+      for (int cb = 0; cb < nc; cb += ncol) {  // one pass unless G < 5
+        const int c = c0 + cb + cq;
+        if (rg < RG && cb + cq < nc) {
+          double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+          constexpr int kB = 8;  // every load of a batch in flight together
+          for (int r0 = rg; r0 < G; r0 += RG * kB) {
+            float4 x[kB];
+#pragma unroll
+            for (int u = 0; u < kB; ++u) {
+              const int r = r0 + u * RG;
+              x[u] = r < G ? ld_wt4(rows_r, (uint32_t)(((size_t)r * PP + 4 * c) * 4))
+                           : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            }
+#pragma unroll
+            for (int u = 0; u < kB; ++u) {
+              a0 += (double)x[u].x;
+              a1 += (double)x[u].y;
+              a2 += (double)x[u].z;
+              a3 += (double)x[u].w;
+            }
+          }
+          double* red = U.red + (rg * ncol + cq) * 4;
+          red[0] = a0;
+          red[1] = a1;
+          red[2] = a2;
+          red[3] = a3;
+        }
+        __syncthreads();
+        if (tid < ncol && cb + tid < nc) {
+          double t4[4] = {0.0, 0.0, 0.0, 0.0};
+          for (int r = 0; r < RG; ++r)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) t4[j] += U.red[(r * ncol + tid) * 4 + j];
+          const float4 gv = make_float4((float)t4[0], (float)t4[1], (float)t4[2], (float)t4[3]);
+          const int cc = c0 + cb + tid;
+          st_wt4(g_r, (uint32_t)(16 * cc), gv);
+          if (p.grad_out && k == K - 1) {
+            const float gg[4] = {gv.x, gv.y, gv.z, gv.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (4 * cc + j < P) p.grad_out[4 * cc + j] = gg[j];
+          }
+          sq += ((double)gv.x * (double)gv.x + (double)gv.y * (double)gv.y) +
+                ((double)gv.z * (double)gv.z + (double)gv.w * (double)gv.w);
+        }
+        __syncthreads();  // U.red is reused by the next pass
+      }
+    }
+    sq = xa_wave_sum_f64(sq);
+    if (lane == 0) U.wsum[w] = sq;
+    __syncthreads();
+    if (tid == 0) st_wt(ws.sumsq + b, (U.wsum[0] + U.wsum[1]) + (U.wsum[2] + U.wsum[3]));
+    XA_STAMP(40);
+    hop_signal(ws.ctl, kCntGrad);
+    XA_STAMP(41);
+    if (!hop_wait(ws.ctl, kCntGrad, (unsigned)(G * (k + 1)), p.status, U.flag)) return;
+    XA_STAMP(42);
+
+    // ---- C: global norm (identical in every wave of every block) + clip + Adam ----
+    float gw[16], gr[RPT];
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const float4 t4 = ld_wt4(g_r, (uint32_t)(ps.w2_off(rr) * 4));
+      gw[4 * rr] = t4.x; gw[4 * rr + 1] = t4.y; gw[4 * rr + 2] = t4.z; gw[4 * rr + 3] = t4.w;
+    }
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) gr[q] = ps.ri[q] >= 0 ? ld_wt(ws.g + ps.ri[q]) : 0.0f;
+    double tot = 0.0;
+    for (int gi = lane; gi < G; gi += 64) tot += ld_wt(ws.sumsq + gi);
+    tot = xa_wave_sum_f64(tot);
+    const float sc = clip_scale(tot, p.adam.clip_norm);
+    const float alpha = adam_alpha(p.adam.lr, p.adam.beta1, p.adam.beta2, t0 + k + 1);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) adam_elem(gw[i] * sc, wv[i], mw[i], vw[i], alpha, omb1, omb2, p.adam.eps);
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) adam_elem(gr[q] * sc, rv[q], mr[q], vr[q], alpha, omb1, omb2, p.adam.eps);
+    ps.to_lds(L, wv, rv);
+    XA_STAMP(43);
+  }
+  if (b == 0) {
+    ps.store(p.theta, wv, rv);
+    ps.store(p.adam_m, mw, mr);
+    ps.store(p.adam_v, vw, vr);
+    if (tid == 0) *p.adam_step = t0 + K;
+  }
+}
+
+// resident capacity (blocks of one launch that are co-resident), per device
+template <int OBS, int A>
+int capacity() {
+  static int cap[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  if (cap[dev] == 0) {
+    int cus = 0, occ = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, ppo_update_kernel<OBS, A>, 256, 0) !=
+        hipSuccess)
+      return 0;
+    cap[dev] = cus * occ;
+  }
+  return cap[dev];
+}
+
+int capacity_for(int obs_dim, int n_actions) {
+  if (obs_dim == 4 && n_actions == 2) return capacity<4, 2>();
+  if (obs_dim == 6 && n_actions == 3) return capacity<6, 3>();
+  if (obs_dim == 8 && n_actions == 4) return capacity<8, 4>();
+  if (obs_dim == 2 && n_actions == 3) return capacity<2, 3>();
+  return -1;
+}
+
+template <int OBS, int A>
+int launch(const XaPpoUpdateArgs* a, int G, int K, int n_mb, hipStream_t s) {
+  const int P = offs(OBS, A).P;
+  const Ws ws = carve(a->workspace, G, P, K);
+  if (hipMemsetAsync(ws.ctl, 0, kCtlBytes, s) != hipSuccess) {
+    xa_set_error("xa_ppo_update: control-word memset failed");
+    return -2;
+  }
+  hipLaunchKernelGGL((ppo_update_kernel<OBS, A>), dim3(G), dim3(256), 0, s, *a, ws, K, n_mb);
+  XA_CHECK_LAUNCH("xa_ppo_update");
+  return 0;
+}
+
+}  // namespace
+
+extern "C" int xa_ppo_update_blocks(int obs_dim, int n_actions, int mb_size) {
+  const int cap = capacity_for(obs_dim, n_actions);
+  if (cap <= 0 || mb_size <= 0) return 0;
+  const int tiles = (mb_size + S - 1) / S;
+  return tiles < cap ? tiles : cap;
+}
+
+extern "C" size_t xa_ppo_update_workspace_bytes(int obs_dim, int n_actions, int batch,
+                                                int mb_size, int epochs, int n_blocks) {
+  if (batch <= 0 || mb_size <= 0 || epochs <= 0 || n_blocks <= 0) return 0;
+  const int n_mb = (batch + mb_size - 1) / mb_size;
+  return ws_bytes(n_blocks, offs(obs_dim, n_actions).P, epochs * n_mb);
+}
+
+extern "C" int xa_ppo_update(const XaPpoUpdateArgs* a, void* stream) {
+  XA_CHECK_ARG(a && a->obs && a->actions && a->old_logp && a->old_values && a->returns &&
+                   a->theta && a->adam_m && a->adam_v && a->adam_step && a->workspace,
+               "xa_ppo_update: null pointer");
+  XA_CHECK_ARG(a->batch > 0 && a->mb_size > 0 && a->epochs > 0, "xa_ppo_update: bad sizes");
+  const int n_mb = (a->batch + a->mb_size - 1) / a->mb_size;
+  const int K = a->epochs * n_mb;
+  XA_CHECK_ARG(K <= kMaxSteps, "xa_ppo_update: %d optimizer steps per launch > %d", K, kMaxSteps);
+  XA_CHECK_ARG(((uintptr_t)a->theta & 15) == 0 && ((uintptr_t)a->adam_m & 15) == 0 &&
+                   ((uintptr_t)a->adam_v & 15) == 0 && ((uintptr_t)a->workspace & 255) == 0,
+               "xa_ppo_update: theta/m/v need 16-byte and the workspace 256-byte alignment");
+  const int cap = capacity_for(a->obs_dim, a->n_actions);
+  XA_CHECK_ARG(cap != -1, "xa_ppo_update: unsupported (obs_dim, n_actions) = (%d, %d)",
+               a->obs_dim, a->n_actions);
+  XA_CHECK_ARG(cap > 0, "xa_ppo_update: could not query the resident capacity");
+  const int G = a->n_blocks;
+  XA_CHECK_ARG(G > 0 && G <= cap && G <= (a->mb_size + S - 1) / S,
+               "xa_ppo_update: n_blocks %d must be in [1, min(resident capacity %d, tiles per "
+               "minibatch)] (xa_ppo_update_blocks)", G, cap);
+  const size_t need = ws_bytes(G, offs(a->obs_dim, a->n_actions).P, K);
+  XA_CHECK_ARG(a->workspace_bytes >= need, "xa_ppo_update: workspace %zu bytes < %zu needed",
+               a->workspace_bytes, need);
+  hipStream_t s = (hipStream_t)stream;
+  if (a->obs_dim == 4 && a->n_actions == 2) return launch<4, 2>(a, G, K, n_mb, s);
+  if (a->obs_dim == 6 && a->n_actions == 3) return launch<6, 3>(a, G, K, n_mb, s);
+  if (a->obs_dim == 8 && a->n_actions == 4) return launch<8, 4>(a, G, K, n_mb, s);
+  return launch<2, 3>(a, G, K, n_mb, s);
+}
+XA_DIAG_READER(xa_diag_read_stamps_ppo)

@@ -10,7 +10,8 @@ import torch
 
 from xagents_amd import _lib
 from xagents_amd._lib import (XA_LOSS_A2C, XA_LOSS_PPO, XaAcGradArgs, XaAdam, XaAdamTail,
-                              XaMinibatchArgs, XaRolloutArgs, XaShuffle, call, ptr, stream)
+                              XaMinibatchArgs, XaPpoUpdateArgs, XaRolloutArgs, XaShuffle, call,
+                              ptr, stream)
 
 
 def _f32(x):
@@ -102,6 +103,23 @@ def ac_grad(args: XaAcGradArgs):
     call('xa_ac_grad', ctypes.byref(args), stream())
 
 
+def ppo_update_blocks(obs_dim, n_actions, mb_size):
+    """Workgroups of the persistent PPO update: one per 32-sample tile of a minibatch, at most
+    as many as can be resident at once (0 if the device cannot be queried)."""
+    return _lib.load().xa_ppo_update_blocks(obs_dim, n_actions, mb_size)
+
+
+def ppo_update_workspace_bytes(obs_dim, n_actions, batch, mb_size, epochs, n_blocks):
+    return _lib.load().xa_ppo_update_workspace_bytes(obs_dim, n_actions, batch, mb_size, epochs,
+                                                     n_blocks)
+
+
+def ppo_update(args: XaPpoUpdateArgs):
+    """Every optimizer step of a PPO train step in one persistent launch
+    (xagents/ppo/agent.py:96-191)."""
+    call('xa_ppo_update', ctypes.byref(args), stream())
+
+
 def adv_stats_size(batch, mb_size, epochs):
     return _lib.load().xa_ppo_adv_stats_size(batch, mb_size, epochs)
 
@@ -151,5 +169,5 @@ def clip_adam(theta, m, v, grad, adam_step, lr, beta1, beta2, eps, clip_norm=Non
 __all__ = [
     'XA_LOSS_A2C', 'XA_LOSS_PPO', 'XaAcGradArgs', 'XaRolloutArgs', 'XaShuffle', 'gae',
     'nstep_returns', 'mlp_forward', 'rollout', 'counter_bump', 'adv_stats', 'ac_grad',
-    'ac_grad_blocks', 'grad_reduce', 'grad_reduce_adam', 'adam_tail', 'clip_adam', 'mlp_param_count', 'gamma_lam_f32',
+    'ac_grad_blocks', 'ppo_update', 'ppo_update_blocks', 'ppo_update_workspace_bytes', 'grad_reduce', 'grad_reduce_adam', 'adam_tail', 'clip_adam', 'mlp_param_count', 'gamma_lam_f32',
 ]

@@ -3,10 +3,14 @@ MI355X path.
 
 train_step = one hipGraph replay of:
     xa_mlp_rollout (n_steps x [forward, sample, env step, store] + GAE)
-    xa_ppo_adv_stats (per-minibatch adv sums, all epochs)  -> [RCCL all_reduce]
-    ppo_epochs x mini_batches x:
-        xa_ac_grad (shuffle-gather + fwd + clipped PPO loss + bwd, partial grads)
-        -> xa_grad_reduce -> [RCCL all_reduce] -> xa_clip_adam
+    one process:   xa_ppo_update (every optimizer step of the train step in ONE
+                   persistent launch: shuffle, adv normalisation, fwd + clipped PPO loss
+                   + bwd, in-launch gradient reduction, clip + Keras Adam)
+    data parallel: xa_ppo_minibatches (shuffle-gather, adv sums) -> [all_reduce]
+                   ppo_epochs x mini_batches x:
+                       xa_ac_grad (prologue: the previous step's clip + Adam; fwd + loss +
+                       bwd -> partial rows) -> xa_grad_reduce -> [all_reduce]
+                   -> xa_clip_adam
     xa_counter_bump
 Multi-GPU: every rank owns n_envs envs (weak scaling); the minibatch of a step is the
 union of the ranks' local minibatches, advantage normalisation and the loss mean use
@@ -16,7 +20,7 @@ import numpy as np
 import torch
 
 from xagents_amd import kernels
-from xagents_amd._lib import XA_RETURNS_GAE, XaShuffle
+from xagents_amd._lib import XA_RETURNS_GAE, XaPpoUpdateArgs, XaShuffle
 from xagents_amd.a2c.agent import A2C
 
 
@@ -53,23 +57,35 @@ class PPO(A2C):
 
     def _setup_update(self):
         import os
-        # optimizer step placement: 'prologue' (next minibatch's xa_ac_grad recomputes it
-        # in every block) or 'kernel' (a standalone xa_clip_adam launch per minibatch)
+        # optimizer step placement of the chain: 'prologue' (next minibatch's xa_ac_grad
+        # recomputes it in every block) or 'kernel' (a standalone xa_clip_adam launch)
         self._opt_kernel = os.environ.get('XA_PPO_OPT', 'prologue') == 'kernel'
         B, MB, E = self.batch_size, self.mini_batch_size, self.ppo_epochs
         # range(0, B, MB) slicing: a ragged last minibatch when MB does not divide B
         # (xagents/ppo/agent.py:152)
         self.n_mb = (B + MB - 1) // MB
-        nb = kernels.ac_grad_blocks(MB)
         dev = self.device
-        self.partials = torch.zeros(nb, self.model.n_params, dtype=torch.float32, device=dev)
-        self.loss_partials = torch.zeros(nb, 4, dtype=torch.float32, device=dev)
-        self.adv_stats = torch.zeros(kernels.adv_stats_size(B, MB, E), dtype=torch.float64,
-                                     device=dev)
         self.shuffle = XaShuffle()
         self.shuffle.perm = None
         self.shuffle.seed = self.rng_seed ^ 0x9E3779B97F4A7C15
         self.shuffle.rng_counter = self.rng_counter.data_ptr()
+        self._tail_bump, self._tail_nobump = self._adam_tail(True), self._adam_tail(False)
+        # one process: every optimizer step of the train step in ONE persistent launch
+        # (xa_ppo_update); data parallel (a cross-rank exchange per step) or
+        # XA_PPO_UPDATE=chain: the per-minibatch launch chain below
+        self.update_mode = 'chain'
+        if os.environ.get('XA_PPO_UPDATE', 'persistent') == 'persistent' and \
+                not self.distributed and E * self.n_mb <= 512:
+            G = kernels.ppo_update_blocks(self.model.obs_dim, self.n_actions, MB)
+            if G > 0:
+                self._setup_persistent(G)
+                return
+        self.device_status = None
+        nb = kernels.ac_grad_blocks(MB)
+        self.partials = torch.zeros(nb, self.model.n_params, dtype=torch.float32, device=dev)
+        self.loss_partials = torch.zeros(nb, 4, dtype=torch.float32, device=dev)
+        self.adv_stats = torch.zeros(kernels.adv_stats_size(B, MB, E), dtype=torch.float64,
+                                     device=dev)
         # every minibatch of the train step materialised up front (ppo/agent.py:139-155)
         obs_dim = self.model.obs_dim
         f32 = dict(dtype=torch.float32, device=dev)
@@ -125,9 +141,51 @@ class PPO(A2C):
                     g.adam = adam
                 self._gargs_list.append(g)
         self._final_src = slots[0 if self._opt_kernel else (len(self._gargs_list) - 1) % 2]
-        self._tail_bump, self._tail_nobump = self._adam_tail(True), self._adam_tail(False)
+
+    def _setup_persistent(self, n_blocks):
+        """Arguments of the persistent update (xa_ppo_update): the rollout buffers in place,
+        theta / Adam moments / iterations of the model in place, a workspace for the
+        in-launch gradient exchange and a device status word (checked with the episode
+        statistics)."""
+        B, MB, E = self.batch_size, self.mini_batch_size, self.ppo_epochs
+        dev, opt = self.device, self.model.optimizer
+        obs_dim, A = self.model.obs_dim, self.n_actions
+        nbytes = kernels.ppo_update_workspace_bytes(obs_dim, A, B, MB, E, n_blocks)
+        self.update_ws = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
+        self.device_status = torch.zeros(1, dtype=torch.int32, device=dev)
+        u = XaPpoUpdateArgs()
+        u.obs_dim, u.n_actions = obs_dim, A
+        u.batch, u.mb_size, u.epochs = B, MB, E
+        u.shuffle = self.shuffle
+        u.obs, u.actions = self.b_obs.data_ptr(), self.b_act.data_ptr()
+        u.old_logp, u.old_values = self.b_logp.data_ptr(), self.b_val.data_ptr()
+        u.returns = self.b_ret.data_ptr()
+        u.clip_norm, u.entropy_coef = float(self.clip_norm), float(self.entropy_coef)
+        u.value_coef, u.adv_eps = float(self.value_loss_coef), float(self.advantage_epsilon)
+        u.theta, u.adam_m, u.adam_v = (self.model.theta.data_ptr(), opt.m.data_ptr(),
+                                       opt.v.data_ptr())
+        u.adam_step = opt.iterations.data_ptr()
+        u.adam = kernels.adam_struct(opt.learning_rate, opt.beta_1, opt.beta_2, opt.epsilon,
+                                     clip_norm=self.grad_norm)
+        u.workspace, u.workspace_bytes = self.update_ws.data_ptr(), nbytes
+        u.loss_out = u.grad_out = None
+        u.status = self.device_status.data_ptr()
+        u.n_blocks = n_blocks
+        self._uargs = u
+        self.update_mode = 'persistent'
+        self.update_blocks = n_blocks
+
+    def _timed_kernels(self):
+        if self.update_mode == 'persistent':
+            return {'rollout': 1, 'ppo_update': 1}
+        return {'rollout': 1, 'ac_grad': len(self._gargs_list)}
 
     def _update(self):
+        if self.update_mode == 'persistent':
+            self._kernel_event('ppo_update', 0, 0)
+            kernels.ppo_update(self._uargs)
+            self._kernel_event('ppo_update', 0, 1)
+            return
         kernels.minibatches(self._mbargs)
         self._all_reduce(self.adv_stats)
         last = len(self._gargs_list) - 1
