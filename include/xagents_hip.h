@@ -454,10 +454,14 @@ int xa_dqn_act(const float* q, int n, int n_actions, const int* random_actions, 
 /* DQN.get_targets + update_gradients loss (dqn/agent.py:118-171): y = v' gamma + r with
  * v' = max_a Qt(s') (or Qt(s')[argmax Q(s')] when q_next_online != NULL), 0 where done;
  * MSE over actions, summed over the batch by minimize: dq[b][a_b] = -2 (y - q[b][a_b]) / A,
- * 0 elsewhere; loss[b] (optional) = (y - q[b][a_b])^2 / A. */
+ * 0 elsewhere; loss[b] (optional) = (y - q[b][a_b])^2 / A.
+ * huber_delta > 0 (opt-in, not in the reference -- BASELINE north_star's Huber-TD loss):
+ * tf.keras.losses.Huber(delta) in place of MSE, x = y - q[b][a_b]:
+ * dq[b][a_b] = -clip(x, -delta, delta) / A, loss[b] = huber(x) / A. <= 0: MSE (parity). */
 int xa_dqn_td_grad(const float* q, const float* q_next_target, const float* q_next_online,
                    const int* actions, const float* rewards, const float* dones, int batch,
-                   int n_actions, float gamma, float* dq, float* loss, void* stream);
+                   int n_actions, float gamma, float huber_delta, float* dq, float* loss,
+                   void* stream);
 
 /* Replay rings (ReplayBuffer1 xagents/utils/buffers.py:59-98, ReplayBuffer2 101-148):
  * ring[slots[i]] = src[i] / dst[i] = ring[slots[i]] for items of item_bytes. The host
@@ -571,10 +575,12 @@ int xa_noisy_actions(const float* x, int64_t ld_x, int rows, int cols, float sig
 
 /* Critic targets + MSE gradients (ddpg/agent.py:104-127; TD3 twin critics
  * td3/agent.py:66-110 when v2/tv2 != NULL): y = r + ((1 - d) gamma) min(tv1, tv2),
- * dv_i = 2 (v_i - y), loss[b] = sum_i (v_i - y)^2. */
+ * dv_i = 2 (v_i - y), loss[b] = sum_i (v_i - y)^2.
+ * huber_delta > 0 (opt-in Huber-TD, not in the reference): dv_i = clip(v_i - y, +-delta),
+ * loss[b] = sum_i huber(v_i - y). <= 0: MSE (parity). */
 int xa_critic_td_grad(const float* v1, const float* v2, const float* tv1, const float* tv2,
                       const float* rewards, const float* dones, int batch, float gamma,
-                      float* dv1, float* dv2, float* loss, void* stream);
+                      float huber_delta, float* dv1, float* dv2, float* loss, void* stream);
 
 /* TFP Categorical(logits) over n logit rows (A2C.get_model_outputs, a2c/agent.py:65-94):
  * log-prob and entropy of the given actions (actions_in) or of an inverse-CDF sample

@@ -1,0 +1,50 @@
+"""Data-parallel paths with W processes sharing the one test GPU over a gloo group
+(SURVEY.md 8e): the fused PPO step equals one process on the union of the shards, TD3 /
+DDPG ranks with different done patterns run the same gradient steps (no collective
+mismatch), and a stalled peer exchange falls back to the process group's all-reduce."""
+import os
+import socket
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+pytestmark = pytest.mark.gpu
+
+
+def _run(worker, world, tag, extra_env=None, timeout=110):
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY='0', OMP_NUM_THREADS='1',
+               **(extra_env or {}))
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1',
+           f'--nproc-per-node={world}', '--master-addr=127.0.0.1', f'--master-port={port}',
+           str(ROOT / 'tests' / worker)]
+    res = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout,
+                         cwd=str(ROOT))
+    out = res.stdout + res.stderr
+    assert res.returncode == 0, out[-4000:]
+    for r in range(world):
+        assert f'{tag} {r}' in out, out[-4000:]
+
+
+def test_ppo_data_parallel_equals_union(device):
+    """xagents/ppo/agent.py:157-191 on the union of 2 shards vs the W = 2 data-parallel
+    step (advantage sums and gradients exchanged), tests/ppo_dp_worker.py."""
+    _run('ppo_dp_worker.py', 2, 'PPO DP OK')
+
+
+def test_td3_data_parallel_done_patterns(device):
+    """TD3 and DDPG at W = 2 with different per-rank done patterns (ddpg/agent.py:157-166),
+    tests/td3_dp_worker.py."""
+    _run('td3_dp_worker.py', 2, 'TD3 DP OK')
+
+
+def test_peer_stall_falls_back_to_rccl(device):
+    """A rank stalling past the peer-exchange timeout in the middle of training is detected
+    by the periodic health check on every rank (tests/peer_stall_worker.py)."""
+    _run('peer_stall_worker.py', 2, 'STALL OK',
+         extra_env={'XA_PEER_TIMEOUT_S': '0.5', 'XA_PEER_CHECK_STEPS': '4'})

@@ -350,7 +350,7 @@ _SIGNATURES = {
     'xa_dqn_td_grad': (
         c_int,
         [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float,
-         c_void_p, c_void_p, c_void_p],
+         c_float, c_void_p, c_void_p, c_void_p],
     ),
     'xa_ring_scatter': (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int64, c_void_p]),
     'xa_ring_gather': (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int64, c_void_p]),
@@ -375,8 +375,8 @@ _SIGNATURES = {
     ),
     'xa_critic_td_grad': (
         c_int,
-        [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_float, c_void_p,
-         c_void_p, c_void_p, c_void_p],
+        [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_float, c_float,
+         c_void_p, c_void_p, c_void_p, c_void_p],
     ),
     'xa_activation_grad': (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p, c_void_p]),
     'xa_peer_block_bytes': (ctypes.c_size_t, [ctypes.c_size_t, c_int]),

@@ -7,6 +7,7 @@ train_step = one hipGraph replay of:
     -> xa_clip_adam (tf.clip_by_global_norm + Keras Adam) -> xa_counter_bump
 """
 import ctypes
+import os
 import warnings
 
 import numpy as np
@@ -37,8 +38,12 @@ class A2C(ExecutorActorCritic, OnPolicy):
         value_loss_coef=0.5,
         grad_norm=0.5,
         use_graph=True,
+        data_parallel=None,
         **kwargs,
     ):
+        # data_parallel: None = data parallel over the default process group when one is
+        # initialised; False = a single-process agent even inside a process group
+        self.data_parallel = data_parallel
         super(A2C, self).__init__(envs, model, **kwargs)
         self.entropy_coef = entropy_coef
         self.value_loss_coef = value_loss_coef
@@ -60,18 +65,20 @@ class A2C(ExecutorActorCritic, OnPolicy):
         # (the CNN) on the layer executor (xagents_amd/onpolicy_executor.py)
         self.executor_path = getattr(model, 'fused_kind', None) != 'actor_critic_mlp'
         if self.executor_path:
-            self.distributed = dist.is_available() and dist.is_initialized()
-            self.world_size = dist.get_world_size() if self.distributed else 1
-            self.rank = dist.get_rank() if self.distributed else 0
+            self._detect_distributed()
             self._setup_executor_path()
         else:
             self._setup_device()
 
     # ---- device state ------------------------------------------------------
-    def _setup_device(self):
-        self.distributed = dist.is_available() and dist.is_initialized()
+    def _detect_distributed(self):
+        dp = getattr(self, 'data_parallel', None)
+        self.distributed = (dist.is_available() and dist.is_initialized() and dp is not False)
         self.world_size = dist.get_world_size() if self.distributed else 1
         self.rank = dist.get_rank() if self.distributed else 0
+
+    def _setup_device(self):
+        self._detect_distributed()
         N, T, obs = self.n_envs, self.n_steps, self.model.obs_dim
         dev = self.device
         f32 = dict(dtype=torch.float32, device=dev)
@@ -118,6 +125,18 @@ class A2C(ExecutorActorCritic, OnPolicy):
         a.gamma_lam = kernels.gamma_lam_f32(self.gamma, getattr(self, 'lam', 0.0))
         self._rargs = a
         self._setup_update()
+
+    def set_rollout_uniforms(self, uniforms):
+        """Parity mode: the fused rollout samples every action by inverse CDF from these
+        [n_envs, n_steps] f32 device uniforms (held, not copied) instead of the Philox
+        stream; None restores Philox."""
+        if uniforms is not None:
+            assert uniforms.dtype == torch.float32 and uniforms.is_contiguous() and \
+                tuple(uniforms.shape) == (self.n_envs, self.n_steps), \
+                f'Expected f32 [{self.n_envs}, {self.n_steps}] uniforms'
+        self._rollout_uniforms = uniforms
+        self._rargs.uniforms = None if uniforms is None else uniforms.data_ptr()
+        self._graph = None
 
     def _grad_args(self, mb_size, n_blocks, partials, loss_partials):
         g = XaAcGradArgs()
@@ -320,6 +339,22 @@ class A2C(ExecutorActorCritic, OnPolicy):
                 self._capture()
         self.steps += self.n_envs * self.n_steps
         self._queue_episode_stats(self.b_done, self.b_epret)
+        self._maybe_check_peer()
+
+    # every rank reaches the same train-step count, so this collective check lines up
+    PEER_CHECK_STEPS = 64
+
+    def _maybe_check_peer(self):
+        """A timed-out peer exchange leaves a sticky error after which every exchange
+        returns local values: check every PEER_CHECK_STEPS train steps (a collective on a
+        schedule identical on all ranks) and, if any rank failed, fall back to RCCL after
+        re-broadcasting rank 0's parameters and optimizer state (check_peer_all_reduce)."""
+        if not self.distributed or getattr(self, 'peer', None) is None:
+            return
+        self._fused_steps = getattr(self, '_fused_steps', 0) + 1
+        every = int(os.environ.get('XA_PEER_CHECK_STEPS', self.PEER_CHECK_STEPS))
+        if self._fused_steps % every == 0:
+            self.check_peer_all_reduce()
 
     def train_step(self):
         self.fused_train_step()

@@ -516,13 +516,24 @@ class OffPolicy(BaseAgent, ABC):
             for m in models:
                 dist.broadcast(m.theta, 0)
 
-    def _reduce_grad(self, grad):
-        """All-reduce a gradient over the data-parallel ranks; returns Adam's grad_scale."""
+    def _reduce_grad(self, grad, mean=False):
+        """All-reduce (sum) a gradient over the data-parallel ranks; returns Adam's
+        grad_scale so the step equals one process on the union of the ranks' batches:
+        1 for losses summed over the batch (Keras MSE + minimize: DQN, the critics,
+        dqn/agent.py:170-171, ddpg/agent.py:126-127), 1 / world for batch means (the
+        actor's -mean Q, ddpg/agent.py:97-100) when every rank samples the same count."""
         if not self.distributed:
             return 1.0
         import torch.distributed as dist
         dist.all_reduce(grad)
-        return 1.0 / self.world_size
+        return 1.0 / self.world_size if mean else 1.0
+
+    def _all_gather_host(self, arr):
+        """Concatenation over the ranks (rank-major) of a small host array."""
+        import torch.distributed as dist
+        parts = [None] * self.world_size
+        dist.all_gather_object(parts, np.asarray(arr))
+        return np.concatenate(parts)
 
     def _random_actions(self):
         """env.action_space.sample() per env (OffPolicy.fill_buffers, base.py:702-730)."""

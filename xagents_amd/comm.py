@@ -124,7 +124,7 @@ def maybe_peer_all_reduce(world_size):
     if not torch.cuda.is_available():
         return None
     try:
-        return PeerAllReduce()
+        return PeerAllReduce(timeout_s=float(os.environ.get('XA_PEER_TIMEOUT_S', '30')))
     except Exception as exc:  # IPC unavailable on this node: RCCL carries the exchange
         warnings.warn(f'peer all-reduce unavailable ({exc}); using RCCL all_reduce')
         return None

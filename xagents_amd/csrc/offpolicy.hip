@@ -70,7 +70,7 @@ __global__ void dqn_act_kernel(const float* __restrict__ q, int n, int A,
 __global__ void dqn_td_kernel(const float* __restrict__ q, const float* __restrict__ q_next_t,
                               const float* __restrict__ q_next_o, const int* __restrict__ act,
                               const float* __restrict__ rew, const float* __restrict__ done,
-                              int B, int A, float gamma, float* __restrict__ dq,
+                              int B, int A, float gamma, float huber, float* __restrict__ dq,
                               float* __restrict__ loss) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
@@ -94,8 +94,18 @@ __global__ void dqn_td_kernel(const float* __restrict__ q, const float* __restri
   const float y = v * gamma + rew[b];
   const int ab = act[b];
   const float diff = y - q[(size_t)b * A + ab];
-  for (int a = 0; a < A; ++a) dq[(size_t)b * A + a] = a == ab ? (-2.0f * diff) / (float)A : 0.0f;
-  if (loss) loss[b] = (diff * diff) / (float)A;
+  float dqa, l;
+  if (huber > 0.0f) {
+    // tf.keras.losses.Huber(delta): 0.5 x^2 if |x| <= delta else delta (|x| - 0.5 delta)
+    const float ad = fabsf(diff);
+    dqa = -fminf(fmaxf(diff, -huber), huber) / (float)A;
+    l = (ad <= huber ? 0.5f * (diff * diff) : huber * (ad - 0.5f * huber)) / (float)A;
+  } else {
+    dqa = (-2.0f * diff) / (float)A;
+    l = (diff * diff) / (float)A;
+  }
+  for (int a = 0; a < A; ++a) dq[(size_t)b * A + a] = a == ab ? dqa : 0.0f;
+  if (loss) loss[b] = l;
 }
 
 // ring[slot[i]] <- src[i] for n_items items of item_bytes each (append)
@@ -289,19 +299,30 @@ __global__ void noisy_actions_kernel(const float* __restrict__ x, int64_t ld_x, 
 __global__ void critic_td_kernel(const float* __restrict__ v1, const float* __restrict__ v2,
                                  const float* __restrict__ tv1, const float* __restrict__ tv2,
                                  const float* __restrict__ rew, const float* __restrict__ done,
-                                 int B, float gamma, float* __restrict__ dv1,
+                                 int B, float gamma, float huber, float* __restrict__ dv1,
                                  float* __restrict__ dv2, float* __restrict__ loss) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   const float tv = tv2 ? fminf(tv1[b], tv2[b]) : tv1[b];
   const float y = rew[b] + ((1.0f - done[b]) * gamma) * tv;
-  const float e1 = v1[b] - y;
-  dv1[b] = 2.0f * e1;
-  float l = e1 * e1;
+  // MSE (the reference): d = 2 e, l = e^2; Huber(delta) opt-in: d = clip(e, +-delta),
+  // l = 0.5 e^2 if |e| <= delta else delta (|e| - 0.5 delta)
+  auto term = [huber](float e, float& d) {
+    if (huber > 0.0f) {
+      d = fminf(fmaxf(e, -huber), huber);
+      const float ae = fabsf(e);
+      return ae <= huber ? 0.5f * (e * e) : huber * (ae - 0.5f * huber);
+    }
+    d = 2.0f * e;
+    return e * e;
+  };
+  float d1;
+  float l = term(v1[b] - y, d1);
+  dv1[b] = d1;
   if (v2) {
-    const float e2 = v2[b] - y;
-    dv2[b] = 2.0f * e2;
-    l = l + e2 * e2;
+    float d2;
+    l = l + term(v2[b] - y, d2);
+    dv2[b] = d2;
   }
   if (loss) loss[b] = l;
 }
@@ -346,13 +367,14 @@ extern "C" int xa_dqn_act(const float* q, int n, int n_actions, const int* rando
 extern "C" int xa_dqn_td_grad(const float* q, const float* q_next_target,
                               const float* q_next_online, const int* actions,
                               const float* rewards, const float* dones, int batch, int n_actions,
-                              float gamma, float* dq, float* loss, void* stream) {
+                              float gamma, float huber_delta, float* dq, float* loss,
+                              void* stream) {
   XA_CHECK_ARG(q && q_next_target && actions && rewards && dones && dq && batch > 0 &&
                    n_actions > 0,
                "xa_dqn_td_grad: bad arguments");
   hipLaunchKernelGGL(dqn_td_kernel, dim3((batch + 63) / 64), dim3(64), 0, (hipStream_t)stream, q,
                      q_next_target, q_next_online, actions, rewards, dones, batch, n_actions,
-                     gamma, dq, loss);
+                     gamma, huber_delta, dq, loss);
   XA_CHECK_LAUNCH("xa_dqn_td_grad");
   return 0;
 }
@@ -471,12 +493,12 @@ extern "C" int xa_noisy_actions(const float* x, int64_t ld_x, int rows, int cols
 
 extern "C" int xa_critic_td_grad(const float* v1, const float* v2, const float* tv1,
                                  const float* tv2, const float* rewards, const float* dones,
-                                 int batch, float gamma, float* dv1, float* dv2, float* loss,
-                                 void* stream) {
+                                 int batch, float gamma, float huber_delta, float* dv1,
+                                 float* dv2, float* loss, void* stream) {
   XA_CHECK_ARG(v1 && tv1 && rewards && dones && dv1 && batch > 0 && (!v2 || dv2),
                "xa_critic_td_grad: bad arguments");
   hipLaunchKernelGGL(critic_td_kernel, dim3((batch + 63) / 64), dim3(64), 0, (hipStream_t)stream,
-                     v1, v2, tv1, tv2, rewards, dones, batch, gamma, dv1, dv2, loss);
+                     v1, v2, tv1, tv2, rewards, dones, batch, gamma, huber_delta, dv1, dv2, loss);
   XA_CHECK_LAUNCH("xa_critic_td_grad");
   return 0;
 }

@@ -34,9 +34,13 @@ class DDPG(OffPolicy):
         gradient_steps=None,
         tau=0.05,
         step_noise_coef=0.1,
+        huber_delta=None,
         **kwargs,
     ):
         super(DDPG, self).__init__(envs, actor_model, buffers, **kwargs)
+        # opt-in Huber-TD critic loss (BASELINE north_star; the reference uses MSE,
+        # ddpg/agent.py:126, td3/agent.py:102-104): None keeps the reference's MSE
+        self.huber_delta = huber_delta
         self.assert_valid_env(envs[0], Box)
         self.actor = actor_model
         self.critic = critic_model
@@ -94,9 +98,9 @@ class DDPG(OffPolicy):
         call('xa_copy_block', right.data_ptr(), right.shape[1], out.data_ptr() + 4 * left.shape[1],
              out.shape[1], B, right.shape[1], stream())
 
-    def _adam(self, model, grad):
+    def _adam(self, model, grad, mean=False):
         opt = model.optimizer
-        scale = self._reduce_grad(grad)
+        scale = self._reduce_grad(grad, mean=mean)
         call('xa_adam_step_bump', opt.iterations.data_ptr(), stream())
         kernels.clip_adam(model.theta, opt.m, opt.v, grad, opt.iterations, opt.learning_rate,
                           opt.beta_1, opt.beta_2, opt.epsilon, clip_norm=0.0,
@@ -135,8 +139,9 @@ class DDPG(OffPolicy):
         self._concat(self.s, self.a, self.sa)
         v = self.ex_critic.forward(self.sa)[0]
         call('xa_critic_td_grad', v.data_ptr(), None, tv.data_ptr(), None, self.r.data_ptr(),
-             self.d.data_ptr(), self.batch_size, kernels._f32(self.gamma), self.dv1.data_ptr(),
-             None, self.critic_loss.data_ptr(), stream())
+             self.d.data_ptr(), self.batch_size, kernels._f32(self.gamma),
+             kernels._f32(self.huber_delta or 0.0), self.dv1.data_ptr(), None,
+             self.critic_loss.data_ptr(), stream())
         self.ex_critic.backward([self.dv1], self.g_critic)
         self._adam(self.critic, self.g_critic)
 
@@ -149,7 +154,7 @@ class DDPG(OffPolicy):
         call('xa_copy_block', self.dspa.data_ptr() + 4 * self.S, self.S + self.A,
              self.da.data_ptr(), self.A, self.batch_size, self.A, stream())
         self.ex_actor.backward([self.da], self.g_actor)
-        self._adam(self.actor, self.g_actor)
+        self._adam(self.actor, self.g_actor, mean=True)
 
     def concat_buffer_samples(self):
         slots = self.replay.upload_slots(self.replay.sample_slots())
@@ -234,8 +239,17 @@ class DDPG(OffPolicy):
                 self._flush_offpolicy_stats()
             self.steps += self.n_envs
             dones = self._stage_done.cpu().numpy()
-        for idx in np.nonzero(dones)[0]:
-            steps = self.gradient_steps or self.episode_steps[idx]
+        if self.distributed:
+            # every rank runs the gradient steps of the union of the ranks' finished
+            # episodes, in global (rank-major) env order -- what one process stepping all
+            # envs would run (ddpg/agent.py:157-166) -- so every rank issues the same
+            # sequence of gradient all-reduces
+            all_dones = self._all_gather_host(dones)
+            all_steps = self._all_gather_host(self.episode_steps)
+        else:
+            all_dones, all_steps = dones, self.episode_steps
+        for idx in np.nonzero(all_dones)[0]:
+            steps = self.gradient_steps or all_steps[idx]
             self.update_weights(steps)
         self.episode_steps = (self.episode_steps + 1.0) * (1.0 - dones)
 

@@ -36,9 +36,13 @@ class DQN(OffPolicy):
         epsilon_end=0.02,
         epsilon_decay_steps=150000,
         target_sync_steps=1000,
+        huber_delta=None,
         **kwargs,
     ):
         super(DQN, self).__init__(envs, model, buffers, **kwargs)
+        # opt-in Huber-TD loss (BASELINE north_star; the reference uses MSE,
+        # dqn/agent.py:170): None keeps the reference's MSE
+        self.huber_delta = huber_delta
         self.assert_valid_env(envs[0], Discrete)
         self.target_model = self.model.clone()
         self.double = double
@@ -127,8 +131,8 @@ class DQN(OffPolicy):
         q_next_o = q_all[B:].data_ptr() if self.double else None
         call('xa_dqn_td_grad', q_all.data_ptr(), q_next_t.data_ptr(), q_next_o,
              self.b_act.data_ptr(), self.b_rew.data_ptr(), self.b_done.data_ptr(), B,
-             self.n_actions, kernels._f32(self.gamma), self.dq.data_ptr(),
-             self.td_loss.data_ptr(), stream())
+             self.n_actions, kernels._f32(self.gamma), kernels._f32(self.huber_delta or 0.0),
+             self.dq.data_ptr(), self.td_loss.data_ptr(), stream())
 
     def _apply(self):
         opt = self.model.optimizer

@@ -66,7 +66,8 @@ class PPO(A2C):
         self.n_mb = (B + MB - 1) // MB
         dev = self.device
         self.shuffle = XaShuffle()
-        self.shuffle.perm = None
+        perm = getattr(self, '_host_perm', None)
+        self.shuffle.perm = None if perm is None else perm.data_ptr()
         self.shuffle.seed = self.rng_seed ^ 0x9E3779B97F4A7C15
         self.shuffle.rng_counter = self.rng_counter.data_ptr()
         self._tail_bump, self._tail_nobump = self._adam_tail(True), self._adam_tail(False)
@@ -174,6 +175,21 @@ class PPO(A2C):
         self._uargs = u
         self.update_mode = 'persistent'
         self.update_blocks = n_blocks
+
+    def set_minibatch_permutation(self, perm):
+        """Parity mode: the fused update takes every epoch's shuffle from `perm`, an
+        [ppo_epochs, batch] int32 device tensor of permutations of the env-major batch
+        (what tf.random.shuffle produced in the reference, ppo/agent.py:149-151), instead
+        of the device Feistel shuffle; None restores the device shuffle. The tensor is read
+        at every train step (update it in place for a new draw)."""
+        if perm is not None:
+            assert perm.dtype == torch.int32 and perm.is_contiguous() and \
+                tuple(perm.shape) == (self.ppo_epochs, self.batch_size), \
+                f'Expected an int32 [{self.ppo_epochs}, {self.batch_size}] permutation tensor'
+        self._host_perm = perm
+        if not self.executor_path:
+            self._setup_update()
+        self._graph = None
 
     def _timed_kernels(self):
         if self.update_mode == 'persistent':

@@ -81,7 +81,8 @@ class TD3(DDPG):
         v2 = self.ex_critic2.forward(self.sa)[0]
         call('xa_critic_td_grad', v1.data_ptr(), v2.data_ptr(), tv1.data_ptr(), tv2.data_ptr(),
              self.r.data_ptr(), self.d.data_ptr(), self.batch_size, kernels._f32(self.gamma),
-             self.dv1.data_ptr(), self.dv2.data_ptr(), self.critic_loss.data_ptr(), stream())
+             kernels._f32(self.huber_delta or 0.0), self.dv1.data_ptr(), self.dv2.data_ptr(),
+             self.critic_loss.data_ptr(), stream())
         self.ex_critic.backward([self.dv1], self.g_critic)
         self.ex_critic2.backward([self.dv2], self.g_critic2)
         self._adam(self.critic1, self.g_critic)

@@ -348,6 +348,14 @@ class TRPO(PPO):
             self._critic_kernels()
             self._critic_warm = True
 
+    def _on_lr_change(self):
+        """The plateau reducer changes the LAST output model's learning rate (the critic,
+        base.py:277-284); it is a launch argument of the captured critic minibatches, so
+        drop the capture (the next update re-warms and re-captures)."""
+        super()._on_lr_change()
+        self._cgraph = None
+        self._critic_warm = False
+
     def _critic_kernels(self):
         B, mb = self.batch_size, self.mini_batch_size
         opt = self.critic.optimizer
