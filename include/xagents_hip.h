@@ -294,7 +294,9 @@ int xa_clip_adam(float* theta, float* adam_m, float* adam_v, const float* grad, 
  * n_blocks: xa_ppo_update_blocks(obs_dim, n_actions, mb_size) (every block must be
  * resident at once: the blocks exchange gradient rows inside the launch).
  * workspace: device memory, 256-byte aligned, >= xa_ppo_update_workspace_bytes(...),
- * owned by the caller; the launch zeroes its first 256 bytes (a memset node).
+ * owned by the caller, ZEROED ONCE at allocation and then reused by every launch (its
+ * first 256 bytes are re-zeroed by a memset node in front of each launch; the rest holds
+ * tagged exchange words whose tags advance with a launch counter kept in it).
  * loss_out (optional) [E*n_mb, n_blocks, 4]: per-block (pg, value, entropy, count) sums.
  * grad_out (optional) [P]: the last optimizer step's reduced gradient (before the clip).
  * status (optional device int): set to 1 if an in-launch exchange timed out (2 s);

@@ -46,7 +46,7 @@ def run_update(theta0, bufs, mb_size, epochs, perm=None, n_blocks=None, want=Tru
     m, v = torch.zeros_like(theta), torch.zeros_like(theta)
     step = torch.zeros(1, dtype=torch.int32, device='cuda')
     nbytes = kernels.ppo_update_workspace_bytes(OBS, A, B, mb_size, epochs, G)
-    ws = torch.full((nbytes,), 0xA5, dtype=torch.uint8, device='cuda')  # poisoned
+    ws = torch.zeros(nbytes, dtype=torch.uint8, device='cuda')  # zeroed once, as required
     grad = torch.zeros_like(theta)
     loss = torch.zeros(K, G, 4, dtype=torch.float32, device='cuda')
     status = torch.zeros(1, dtype=torch.int32, device='cuda')
@@ -148,18 +148,20 @@ def test_multi_step_ragged_trajectory_vs_f64(device):
     np.testing.assert_array_equal(counts, [198, 198, 198, 6] * E)
 
 
-def test_fewer_blocks_than_tiles_is_the_same_update(device):
-    """With fewer resident blocks than tiles each block walks several tiles; only the f64
-    summation order of the gradient changes."""
-    B = 4096
+@pytest.mark.parametrize('B,mb,blocks', [(4096, 1024, (32, 5)), (16384, 8192, (256, 64, 40, 7))])
+def test_block_count_changes_only_the_summation_order(device, B, mb, blocks):
+    """Fewer resident blocks than tiles: each block walks several tiles. 64 and more
+    blocks reduce the gradient rows inside each XCD's L2 first (two-level), fewer in one
+    level. Only the f64 summation order of the gradient changes."""
     bufs = _rollout_buffers(B, seed=5)
     theta0 = _theta0(3)
-    full = run_update(theta0, bufs, 1024, 2)
-    few = run_update(theta0, bufs, 1024, 2, n_blocks=5)
-    assert full['G'] == 32 and few['G'] == 5
-    assert few['status'] == 0 and few['step'] == 8
-    assert _rel(few['grad'], full['grad'].astype(np.float64)) < 1e-5
-    assert _rel(few['theta'] - theta0, (full['theta'] - theta0).astype(np.float64)) < 1e-4
+    runs = [run_update(theta0, bufs, mb, 2, n_blocks=g) for g in blocks]
+    ref = runs[0]
+    assert ref['G'] == blocks[0]
+    for r, g in zip(runs, blocks):
+        assert r['G'] == g and r['status'] == 0 and r['step'] == 2 * (B // mb)
+        assert _rel(r['grad'], ref['grad'].astype(np.float64)) < 1e-5, g
+        assert _rel(r['theta'] - theta0, (ref['theta'] - theta0).astype(np.float64)) < 1e-4, g
 
 
 def test_feistel_shuffle_matches_oracle_permutation(device):

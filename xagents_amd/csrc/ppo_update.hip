@@ -44,7 +44,11 @@ typedef __attribute__((address_space(1))) unsigned long long gu64;
 constexpr int kMaxSteps = 512;              // E * M optimizer steps per launch
 constexpr int kCtlBytes = 256;              // control words at the workspace start
 constexpr uint64_t kSpinTicks = 200000000;  // 2 s of the 100 MHz wall clock per hop
-enum { kCntStats = 0, kCntRows = 1, kCntGrad = 2, kAbort = 3 };
+// control words (zeroed per launch): global hop counters, the abort word, and per XCD
+// the census count and the XCD-local row hop counter
+enum { kCntStats = 0, kCntRows = 1, kCntGrad = 2, kAbort = 3, kCntX = 4, kXcnt = 8, kXrows = 16 };
+constexpr int kXcds = 8;            // MI355X: 8 XCDs, each with its own L2
+constexpr int kTwoLevelMinG = 64;   // >= 8 blocks per XCD: reduce inside each XCD's L2 first
 
 // ---- write-through hand-off primitives (global address space, agent scope) ----
 XA_DEV void st_wt(float* p, float v) {
@@ -76,13 +80,91 @@ XA_DEV float4 ld_wt4(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
   const f32x4v v = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, kAuxSc1);
   return make_float4(v[0], v[1], v[2], v[3]);
 }
+// two f64 in one 16-B write-through access
+XA_DEV void st_wt_d2(__amdgpu_buffer_rsrc_t r, uint32_t byte_off, double a, double b) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(f32x4v, make_double2(a, b)), r,
+                                         byte_off, 0, kAuxSc1);
+}
+XA_DEV double2 ld_wt_d2(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
+  return __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, kAuxSc1));
+}
+// {v0, tag} {v1, tag} as one 16-byte store, write-through (cross-XCD readers) or plain
+// (readers on this XCD: the line stays in the shared L2)
+XA_DEV void st_gran2(__amdgpu_buffer_rsrc_t r, uint32_t off, float v0, float v1, unsigned tag,
+                     bool wt) {
+  const f32x4v v = {v0, __uint_as_float(tag), v1, __uint_as_float(tag)};
+  if (wt) __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, kAuxSc1);
+  else __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 0);
+}
+XA_DEV void st_gran_f64(__amdgpu_buffer_rsrc_t r, uint32_t off, double d, unsigned tag) {
+  const unsigned long long u = (unsigned long long)__double_as_longlong(d);
+  st_gran2(r, off, __uint_as_float((unsigned)u), __uint_as_float((unsigned)(u >> 32)), tag, true);
+}
+XA_DEV bool gran_ok(const f32x4v& v, unsigned tag) {
+  return __float_as_uint(v[1]) == tag && __float_as_uint(v[3]) == tag;
+}
+XA_DEV double gran_f64(const f32x4v& v) {
+  return __longlong_as_double((long long)(((unsigned long long)__float_as_uint(v[2]) << 32) |
+                                          __float_as_uint(v[0])));
+}
 
+// Poll n (<= N) granule pairs (write-through loads) until every tag equals `tag`. Bounded
+// by the wall clock and the abort word; false on timeout / abort (the caller leaves).
+template <int N>
+XA_DEV bool poll_gran(__amdgpu_buffer_rsrc_t r, const uint32_t (&off)[N], int n, unsigned tag,
+                      f32x4v (&v)[N], unsigned* ctl, int* status) {
+  uint64_t t0 = 0;
+  for (;;) {
+#pragma unroll
+    for (int u = 0; u < N; ++u)
+      if (u < n) v[u] = __builtin_amdgcn_raw_buffer_load_b128(r, off[u], 0, kAuxSc1);
+    bool ok = true;
+#pragma unroll
+    for (int u = 0; u < N; ++u)
+      if (u < n) ok = ok && gran_ok(v[u], tag);
+    if (ok) return true;
+    const uint64_t now = wall_clock64();
+    if (t0 == 0) t0 = now;
+    else if (now - t0 > kSpinTicks) {
+      __hip_atomic_store((gu32*)(ctl + kAbort), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (status) __hip_atomic_store((gu32*)status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    if (__hip_atomic_load((gu32*)(ctl + kAbort), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+      return false;
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+// this workgroup's XCD (MI355X_MICROARCH.md: read placement from HW_REG_XCC_ID)
+XA_DEV int xcc_id() {
+  unsigned x;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+  return (int)(x & (kXcds - 1));
+}
+
+// Workspace (device memory, zeroed once by the caller at allocation):
+//   ctl      control words, zeroed by a memset node in front of every launch
+//   persist  the launch generation (NOT reset: the granule tags of every launch differ)
+//   rows_g   [G, PP/2] granule pairs: the blocks' gradient rows
+//   g_g      [PP/2] granule pairs: the reduced gradient
+//   sumsq_g  [G] granule pairs: f64 sums of squares of the g slices (lo, hi words)
+//   adv      [K, G, 2] f64 advantage sums (phase-0 hop)
+//   members  [kXcds, G] census of the blocks of every XCD (two-level)
+//   xpart_g  [kXcds, PP] granule pairs: f64 per-XCD partial sums of the rows (two-level)
+// A granule is 8 bytes {32-bit value, 32-bit tag}; two of them travel in one 16-byte
+// access (MI355X_MICROARCH.md: 16-B write-through halves observed untorn), and the tag
+// is the step's epoch, so the data is its own flag: consumers poll the data.
 struct Ws {
-  unsigned* ctl;    // [kCtlBytes / 4], zeroed per launch
-  float* rows;      // [G, PP] per-block gradient rows, PP = P rounded up to 4 floats
-  float* g;         // [PP] reduced gradient
-  double* sumsq;    // [G] f64 sums of squares of the g slices
-  double* adv;      // [K, G, 2] f64 advantage sums
+  unsigned* ctl;
+  unsigned* persist;
+  void* rows_g;
+  void* g_g;
+  void* sumsq_g;
+  double* adv;
+  int* members;
+  void* xpart_g;
+  size_t total;
 };
 
 __host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
@@ -93,25 +175,26 @@ __host__ __device__ inline Ws carve(void* base, int G, int P, int K) {
   Ws w;
   char* c = (char*)base;
   size_t off = 0;
-  w.ctl = (unsigned*)(c + off);
-  off += kCtlBytes;
-  w.rows = (float*)(c + off);
-  off = align_up(off + (size_t)G * padded(P) * sizeof(float), 256);
-  w.g = (float*)(c + off);
-  off = align_up(off + (size_t)padded(P) * sizeof(float), 256);
-  w.sumsq = (double*)(c + off);
-  off = align_up(off + (size_t)G * sizeof(double), 256);
-  w.adv = (double*)(c + off);
+  auto take = [&](size_t bytes) {
+    char* q = c + off;
+    off = align_up(off + bytes, 256);
+    return q;
+  };
+  const size_t PP = padded(P);
+  w.ctl = (unsigned*)take(kCtlBytes);
+  w.persist = (unsigned*)take(256);
+  w.rows_g = take((size_t)G * PP * 8);
+  w.g_g = take(PP * 8);
+  w.sumsq_g = take((size_t)G * 16);
+  w.adv = (double*)take((size_t)K * G * 2 * sizeof(double));
+  w.members = (int*)take((size_t)kXcds * G * sizeof(int));
+  w.xpart_g = take((size_t)kXcds * PP * 16);
+  w.total = off;
   return w;
 }
 
 __host__ __device__ inline size_t ws_bytes(int G, int P, int K) {
-  size_t off = kCtlBytes;
-  off = align_up(off + (size_t)G * padded(P) * sizeof(float), 256);
-  off = align_up(off + (size_t)padded(P) * sizeof(float), 256);
-  off = align_up(off + (size_t)G * sizeof(double), 256);
-  off += (size_t)K * G * 2 * sizeof(double);
-  return align_up(off, 256);
+  return carve(nullptr, G, P, K).total;
 }
 
 struct ShufKeys {
@@ -148,6 +231,9 @@ struct UpdLds {
   double red[256 * 4];
   double wsum[4];
   int flag;
+  int xn[kXcds];   // blocks per XCD (census)
+  int xmem[256];   // this XCD's blocks, ascending block id (two-level)
+  int xrank;       // this block's position among them
 };
 
 // Publish: every wave drained its write-through stores, then ONE lane counts the
@@ -201,6 +287,16 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
   XA_STAMP_DECL
   XA_STAMP(30);
 
+  // ---- census: which XCD this block runs on (published by the phase-0 hop) ----
+  const bool two_level = G >= kTwoLevelMinG;
+  const int xcc = xcc_id();
+  if (two_level && tid == 0) {
+    const unsigned slot = __hip_atomic_fetch_add((gu32*)(ws.ctl + kXcnt + xcc), 1u,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((gu32*)(ws.members + xcc * G + slot), (unsigned)b, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+
   // ---- phase 0: advantage sums of this block's samples of every minibatch ----
   for (int k = w; k < K; k += 4) {
     const int e = k / n_mb, m = k - e * n_mb;
@@ -239,6 +335,27 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
 
   XA_STAMP(32);
   if (!hop_wait(ws.ctl, kCntStats, (unsigned)G, p.status, U.flag)) return;
+  if (two_level) {
+    // this XCD's member blocks in ascending id: fixed reduction order and column split
+    if (tid < kXcds)
+      U.xn[tid] = (int)__hip_atomic_load((gu32*)(ws.ctl + kXcnt + tid), __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const int ng = U.xn[xcc];
+    int mb_id = -1;
+    if (tid < ng)
+      mb_id = (int)__hip_atomic_load((gu32*)(ws.members + xcc * G + tid), __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+    U.red[tid] = (double)mb_id;  // scratch: the unsorted list
+    __syncthreads();
+    if (tid < ng) {
+      int rank = 0;
+      for (int j = 0; j < ng; ++j) rank += (int)U.red[j] < mb_id;
+      U.xmem[rank] = mb_id;
+      if (mb_id == b) U.xrank = rank;
+    }
+    __syncthreads();
+  }
   XA_STAMP(33);
   for (int k = w; k < K; k += 4) {
     const int m = k % n_mb;
@@ -294,20 +411,28 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
   cfg.entropy_coef = p.entropy_coef;
   cfg.adv_eps = p.adv_eps;
   const float omb1 = 1.0f - p.adam.beta1, omb2 = 1.0f - p.adam.beta2;
-  // rows are PP = P rounded up to 4 floats; block b reduces float4 columns [c0, c0 + nc)
-  const int PP = padded(P), C4 = PP / 4;
-  const int CB = (C4 + G - 1) / G;
-  const int c0 = min(C4, b * CB), nc = min(C4, c0 + CB) - c0;
-  const __amdgpu_buffer_rsrc_t rows_r = rsrc(ws.rows, (uint32_t)((size_t)G * PP * 4));
-  const __amdgpu_buffer_rsrc_t g_r = rsrc(ws.g, (uint32_t)(PP * 4));
+  // rows are PP = P rounded up to 4 floats = PP/2 granule pairs (one pair per 16 B)
+  const int PP = padded(P), NP2 = PP / 2;
+  // phase B: block b reduces pair columns [c0, c0 + nc) of the gradient
+  const int CB = (NP2 + G - 1) / G;
+  const int c0 = min(NP2, b * CB), nc = min(NP2, c0 + CB) - c0;
+  const __amdgpu_buffer_rsrc_t rows_r = rsrc(ws.rows_g, (uint32_t)((size_t)G * PP * 8));
+  const __amdgpu_buffer_rsrc_t g_r = rsrc(ws.g_g, (uint32_t)(PP * 8));
+  const __amdgpu_buffer_rsrc_t sq_r = rsrc(ws.sumsq_g, (uint32_t)(G * 16));
+  const __amdgpu_buffer_rsrc_t xp_r = rsrc(ws.xpart_g, (uint32_t)(kXcds * PP * 16));
   float* srow = U.row;
   for (int i = P + tid; i < PP; i += 256) srow[i] = 0.0f;  // the pad stays zero
+  // granule tags: unique per (launch, step); the generation word is bumped at the end
+  const unsigned gen = *ws.persist;
+  auto tag_of = [&](int k) { return gen * (unsigned)K + (unsigned)k + 1u; };
+  int* const fail = &U.flag;
 
   TileAcc<OBS, A> acc;
   for (int k = 0; k < K; ++k) {
     const int m = k % n_mb;
     const int cnt = min(MB, B - m * MB);
     const int n_tiles = (cnt + S - 1) / S;
+    const unsigned tag = tag_of(k);
     __syncthreads();  // U.stat, the LDS weights of the previous step
     cfg.adv_mean = U.stat[k][0];
     cfg.adv_std = U.stat[k][1];
@@ -333,97 +458,194 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
       tile_compute<OBS, A>(L, acc, cfg, [&](int slot) { XA_STAMP(slot); });
       XA_STAMP(36);
     }
-    // ---- the block's gradient row: staged in LDS, published with 16-B write-through ----
+    // ---- the block's gradient row, staged in LDS, published as granule pairs ----
     tile_write_row<OBS, A>(L, acc, [&](int i, float v) { srow[i] = v; });
     if (p.loss_out) {
       const float ls = tile_loss_sums<OBS, A>(L, acc);
       if (tid < 4) p.loss_out[((size_t)k * G + b) * 4 + tid] = ls;
     }
     __syncthreads();
-    for (int c = tid; c < C4; c += 256)
-      st_wt4(rows_r, (uint32_t)(((size_t)b * PP + 4 * c) * 4),
-             *reinterpret_cast<const float4*>(&srow[4 * c]));
-    XA_STAMP(37);
-    hop_signal(ws.ctl, kCntRows);
+    for (int c = tid; c < NP2; c += 256)
+      st_gran2(rows_r, (uint32_t)(((size_t)b * NP2 + c) * 16), srow[2 * c], srow[2 * c + 1], tag,
+               !two_level);
     fetch_tile(k + 1, b);  // the next step's first tile, while the other blocks finish
-    XA_STAMP(38);
-    if (!hop_wait(ws.ctl, kCntRows, (unsigned)(G * (k + 1)), p.status, U.flag)) return;
-    XA_STAMP(39);
-
-    // ---- B: fixed-order reduction of float4 columns [c0, c0 + nc) over the G rows ----
-    double sq = 0.0;
-    if (nc > 0) {
-      const int ncol = min(nc, 256), RG = 256 / ncol;
+    XA_STAMP(37);
+    if (tid == 0) *fail = 0;
+    if (two_level) {
+      // ---- level 1, inside the XCD: its members' rows (in this XCD's L2) -> this XCD's
+      // f64 partial of pair columns [xc0, xc0 + xnc), published write-through ----
+      const int ng = U.xn[xcc];
+      const int CBx = (NP2 + ng - 1) / ng;
+      const int xc0 = min(NP2, U.xrank * CBx), xnc = min(NP2, xc0 + CBx) - xc0;
+      const int ncol = max(1, min(xnc, 256)), RG = 256 / ncol;
       const int rg = tid / ncol, cq = tid - rg * ncol;
-      for (int cb = 0; cb < nc; cb += ncol) {  // one pass unless G < 5
-        const int c = c0 + cb + cq;
-        if (rg < RG && cb + cq < nc) {
-          double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-          constexpr int kB = 8;  // every load of a batch in flight together
-          for (int r0 = rg; r0 < G; r0 += RG * kB) {
-            float4 x[kB];
+      for (int cb = 0; cb < xnc; cb += ncol) {
+        bool bad = false;
+        if (rg < RG && cb + cq < xnc) {
+          const int c = xc0 + cb + cq;
+          double a0 = 0.0, a1 = 0.0;
+          constexpr int kB = 8;
+          for (int j0 = rg; j0 < ng && !bad; j0 += RG * kB) {
+            uint32_t off[kB];
+            f32x4v x[kB];
+            int n = 0;
 #pragma unroll
             for (int u = 0; u < kB; ++u) {
-              const int r = r0 + u * RG;
-              x[u] = r < G ? ld_wt4(rows_r, (uint32_t)(((size_t)r * PP + 4 * c) * 4))
-                           : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+              const int j = j0 + u * RG;
+              off[u] = j < ng ? (uint32_t)(((size_t)U.xmem[j] * NP2 + c) * 16) : 0u;
+              n += j < ng;
             }
+            bad = !poll_gran<kB>(rows_r, off, n, tag, x, ws.ctl, p.status);
 #pragma unroll
-            for (int u = 0; u < kB; ++u) {
-              a0 += (double)x[u].x;
-              a1 += (double)x[u].y;
-              a2 += (double)x[u].z;
-              a3 += (double)x[u].w;
-            }
+            for (int u = 0; u < kB; ++u)
+              if (u < n) {
+                a0 += (double)x[u][0];
+                a1 += (double)x[u][2];
+              }
           }
-          double* red = U.red + (rg * ncol + cq) * 4;
-          red[0] = a0;
-          red[1] = a1;
-          red[2] = a2;
-          red[3] = a3;
+          U.red[(rg * ncol + cq) * 2] = a0;
+          U.red[(rg * ncol + cq) * 2 + 1] = a1;
+        }
+        if (__syncthreads_or(bad)) return;
+        if (tid < ncol && cb + tid < xnc) {
+          double t0 = 0.0, t1 = 0.0;
+          for (int r = 0; r < RG; ++r) {
+            t0 += U.red[(r * ncol + tid) * 2];
+            t1 += U.red[(r * ncol + tid) * 2 + 1];
+          }
+          const uint32_t off = (uint32_t)(((size_t)xcc * NP2 + xc0 + cb + tid) * 32);
+          st_gran_f64(xp_r, off, t0, tag);
+          st_gran_f64(xp_r, off + 16, t1, tag);
         }
         __syncthreads();
-        if (tid < ncol && cb + tid < nc) {
-          double t4[4] = {0.0, 0.0, 0.0, 0.0};
-          for (int r = 0; r < RG; ++r)
+      }
+    }
+    XA_STAMP(38);
+
+    // ---- B: pair columns [c0, c0 + nc): the fixed-order sum over the G rows, or
+    // (two-level) over the XCD partials in XCD order -> g (granules) + f64 sum of squares ----
+    double sq = 0.0;
+    if (nc > 0) {
+      const int SRC = two_level ? kXcds : G;  // sources summed per column
+      const int ncol = min(nc, 256), RG = min(SRC, 256 / ncol);
+      const int rg = tid / ncol, cq = tid - rg * ncol;
+      for (int cb = 0; cb < nc; cb += ncol) {
+        bool bad = false;
+        if (rg < RG && cb + cq < nc) {
+          const int c = c0 + cb + cq;
+          double a0 = 0.0, a1 = 0.0;
+          constexpr int kB = 8;
+          for (int j0 = rg; j0 < SRC && !bad; j0 += RG * kB) {
+            uint32_t off[kB];
+            f32x4v x[kB];
+            int n = 0;
+            if (two_level) {
+              // two granule pairs (one f64 each) per pair column and XCD
 #pragma unroll
-            for (int j = 0; j < 4; ++j) t4[j] += U.red[(r * ncol + tid) * 4 + j];
-          const float4 gv = make_float4((float)t4[0], (float)t4[1], (float)t4[2], (float)t4[3]);
-          const int cc = c0 + cb + tid;
-          st_wt4(g_r, (uint32_t)(16 * cc), gv);
-          if (p.grad_out && k == K - 1) {
-            const float gg[4] = {gv.x, gv.y, gv.z, gv.w};
+              for (int u = 0; u < kB; ++u) off[u] = 0u;
+              for (int u = 0; u < kB / 2; ++u) {
+                const int xx = j0 + u * RG;
+                if (xx < kXcds && U.xn[xx] > 0) {
+                  const uint32_t o2 = (uint32_t)(((size_t)xx * NP2 + c) * 32);
+                  off[n] = o2;
+                  off[n + 1] = o2 + 16;
+                  n += 2;
+                }
+              }
+              bad = !poll_gran<kB>(xp_r, off, n, tag, x, ws.ctl, p.status);
+              for (int u = 0; u + 1 < n; u += 2) {
+                a0 += gran_f64(x[u]);
+                a1 += gran_f64(x[u + 1]);
+              }
+            } else {
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
-              if (4 * cc + j < P) p.grad_out[4 * cc + j] = gg[j];
+              for (int u = 0; u < kB; ++u) {
+                const int r = j0 + u * RG;
+                off[u] = r < G ? (uint32_t)(((size_t)r * NP2 + c) * 16) : 0u;
+                n += r < G;
+              }
+              bad = !poll_gran<kB>(rows_r, off, n, tag, x, ws.ctl, p.status);
+#pragma unroll
+              for (int u = 0; u < kB; ++u)
+                if (u < n) {
+                  a0 += (double)x[u][0];
+                  a1 += (double)x[u][2];
+                }
+            }
           }
-          sq += ((double)gv.x * (double)gv.x + (double)gv.y * (double)gv.y) +
-                ((double)gv.z * (double)gv.z + (double)gv.w * (double)gv.w);
+          U.red[(rg * ncol + cq) * 2] = a0;
+          U.red[(rg * ncol + cq) * 2 + 1] = a1;
         }
-        __syncthreads();  // U.red is reused by the next pass
+        if (__syncthreads_or(bad)) return;
+        if (tid < ncol && cb + tid < nc) {
+          double t0 = 0.0, t1 = 0.0;
+          for (int r = 0; r < RG; ++r) {
+            t0 += U.red[(r * ncol + tid) * 2];
+            t1 += U.red[(r * ncol + tid) * 2 + 1];
+          }
+          const float g0 = (float)t0, g1 = (float)t1;
+          const int cc = c0 + cb + tid;
+          st_gran2(g_r, (uint32_t)(16 * cc), g0, g1, tag, true);
+          if (p.grad_out && k == K - 1) {
+            if (2 * cc < P) p.grad_out[2 * cc] = g0;
+            if (2 * cc + 1 < P) p.grad_out[2 * cc + 1] = g1;
+          }
+          sq += (double)g0 * (double)g0 + (double)g1 * (double)g1;
+        }
+        __syncthreads();
       }
     }
     sq = xa_wave_sum_f64(sq);
     if (lane == 0) U.wsum[w] = sq;
     __syncthreads();
-    if (tid == 0) st_wt(ws.sumsq + b, (U.wsum[0] + U.wsum[1]) + (U.wsum[2] + U.wsum[3]));
+    if (tid == 0)
+      st_gran_f64(sq_r, (uint32_t)(16 * b), (U.wsum[0] + U.wsum[1]) + (U.wsum[2] + U.wsum[3]), tag);
     XA_STAMP(40);
-    hop_signal(ws.ctl, kCntGrad);
-    XA_STAMP(41);
-    if (!hop_wait(ws.ctl, kCntGrad, (unsigned)(G * (k + 1)), p.status, U.flag)) return;
-    XA_STAMP(42);
 
-    // ---- C: global norm (identical in every wave of every block) + clip + Adam ----
+    // ---- C: the g slice of this thread's parameters and the G norm partials (granules),
+    // global norm (identical in every wave of every block), clip + Keras Adam ----
     float gw[16], gr[RPT];
+    bool bad = false;
+    {
+      constexpr int NG = 8 + RPT;
+      uint32_t off[NG];
+      f32x4v x[NG];
 #pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-      const float4 t4 = ld_wt4(g_r, (uint32_t)(ps.w2_off(rr) * 4));
-      gw[4 * rr] = t4.x; gw[4 * rr + 1] = t4.y; gw[4 * rr + 2] = t4.z; gw[4 * rr + 3] = t4.w;
+      for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) off[2 * rr + h] = (uint32_t)((ps.w2_off(rr) / 2 + h) * 16);
+#pragma unroll
+      for (int q = 0; q < RPT; ++q) off[8 + q] = (uint32_t)((ps.ri[q] >= 0 ? ps.ri[q] / 2 : 0) * 16);
+      bad = !poll_gran<NG>(g_r, off, NG, tag, x, ws.ctl, p.status);
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        gw[4 * rr] = x[2 * rr][0];
+        gw[4 * rr + 1] = x[2 * rr][2];
+        gw[4 * rr + 2] = x[2 * rr + 1][0];
+        gw[4 * rr + 3] = x[2 * rr + 1][2];
+      }
+#pragma unroll
+      for (int q = 0; q < RPT; ++q)
+        gr[q] = ps.ri[q] >= 0 ? ((ps.ri[q] & 1) ? x[8 + q][2] : x[8 + q][0]) : 0.0f;
     }
-#pragma unroll
-    for (int q = 0; q < RPT; ++q) gr[q] = ps.ri[q] >= 0 ? ld_wt(ws.g + ps.ri[q]) : 0.0f;
     double tot = 0.0;
-    for (int gi = lane; gi < G; gi += 64) tot += ld_wt(ws.sumsq + gi);
+    for (int gi0 = 0; gi0 < G && !bad; gi0 += 64 * 4) {
+      uint32_t off[4];
+      f32x4v x[4];
+      int n = 0;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int gi = gi0 + u * 64 + lane;
+        off[u] = gi < G ? (uint32_t)(16 * gi) : 0u;
+        n += gi < G;
+      }
+      // lanes past G poll nothing (n counts this lane's valid granules in order)
+      bad = !poll_gran<4>(sq_r, off, n, tag, x, ws.ctl, p.status);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (u < n) tot += gran_f64(x[u]);
+    }
+    if (__syncthreads_or(bad)) return;
     tot = xa_wave_sum_f64(tot);
     const float sc = clip_scale(tot, p.adam.clip_norm);
     const float alpha = adam_alpha(p.adam.lr, p.adam.beta1, p.adam.beta2, t0 + k + 1);
@@ -438,7 +660,10 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
     ps.store(p.theta, wv, rv);
     ps.store(p.adam_m, mw, mr);
     ps.store(p.adam_v, vw, vr);
-    if (tid == 0) *p.adam_step = t0 + K;
+    if (tid == 0) {
+      *p.adam_step = t0 + K;
+      *ws.persist = gen + 1u;  // the next launch's tags (read at its start)
+    }
   }
 }
 
