@@ -42,6 +42,10 @@ extern "C" {
 #define XA_RETURNS_GAE 1   /* PPO.calculate_returns, xagents/ppo/agent.py:48-94 */
 #define XA_RETURNS_NSTEP 2 /* A2C.calculate_returns, xagents/a2c/agent.py:141-171 */
 
+/* action distributions of the actor-critic heads (A2C.get_distribution, a2c/agent.py:54-63) */
+#define XA_DIST_CATEGORICAL 0
+#define XA_DIST_DIAG_GAUSSIAN 1
+
 /* loss kinds of the fused actor-critic gradient */
 #define XA_LOSS_PPO 0 /* PPO.update_gradients, xagents/ppo/agent.py:96-137 */
 #define XA_LOSS_A2C 1 /* A2C.train_step, xagents/a2c/agent.py:190-218 */
@@ -617,9 +621,26 @@ typedef struct XaHeadGradArgs {
    * 2 = use the all-reduced adv_stats (the union minibatch's mean / population std) */
   int stats_mode;
   double* adv_stats;
+  /* XA_DIST_CATEGORICAL (logits rows, `actions` int) or XA_DIST_DIAG_GAUSSIAN (`logits`
+   * rows are the mean of MultivariateNormalDiag(loc) with unit scale, a2c/agent.py:59-60;
+   * actions_f [n, ld_actions] f32; dlogits is then d loss / d mean) */
+  int dist_kind;
+  const float* actions_f;
+  int64_t ld_actions;
 } XaHeadGradArgs;
 
 int xa_ac_head_grad(const XaHeadGradArgs* args, void* stream);
+
+/* MultivariateNormalDiag(loc = mu) with unit scale, the reference's distribution for Box
+ * action spaces (A2C.get_distribution, a2c/agent.py:54-63): per row i of mu [n, d],
+ * actions_out[i] = mu[i] + N(0, I) (noise [n, d] if given, else Philox4x32-10 Box-Muller
+ * at (i, step, *rng_counter), key seed; TF's stream is not reproduced), or the log-prob of
+ * actions_in; logp[i] = -0.5 |a - mu|^2 - 0.5 d log(2 pi), entropy[i] = 0.5 d (1 +
+ * log(2 pi)). Outputs at i * ld_out (optional). */
+int xa_diag_gaussian(const float* mu, int64_t ld_mu, int n, int d, const float* noise,
+                     const uint64_t* rng_counter, uint64_t seed, int step,
+                     const float* actions_in, int64_t ld_act, float* actions_out, float* logp,
+                     float* entropy, int64_t ld_out, void* stream);
 
 /* ACER loss gradient of a batch of n_envs trajectories (ACER.update_gradients,
  * xagents/acer/agent.py:295-347; calculate_returns 171-208; calculate_losses 210-260;

@@ -252,3 +252,25 @@ def test_rb2_batched_randint_matches_per_buffer_calls():
         np.random.seed(11)
         got = np.random.randint(0, size, n * k)
         np.testing.assert_array_equal(ref, got)
+
+
+# ---- LazyFrames and the per-env states view (xagents/utils/common.py:23-64) --------------
+def test_lazyframes_and_states_view():
+    import torch
+    from xagents_amd.utils.common import DeviceStates, LazyFrames
+    frames = np.arange(84 * 84, dtype=np.uint8).reshape(84, 84, 1)
+    lf = LazyFrames(frames)
+    assert lf.dtype == np.uint8 and lf.shape == (84, 84, 1)
+    np.testing.assert_array_equal(np.asarray(lf), frames)
+    assert lf.frames is None  # materialised once
+    assert len(lf) == 84 and lf.count() == 1
+    np.testing.assert_array_equal(lf[3], frames[3])
+    assert np.asarray(lf, dtype=np.float32).dtype == np.float32
+    images = torch.from_numpy(np.stack([frames, frames + 1]))
+    view = DeviceStates(images)
+    assert len(view) == 2 and isinstance(view[1], LazyFrames)
+    np.testing.assert_array_equal(np.asarray(view[1]), frames + 1)
+    np.testing.assert_array_equal(np.asarray(view), images.numpy())
+    vec = DeviceStates(torch.zeros(3, 4))
+    assert isinstance(vec[0], np.ndarray) and vec[0].shape == (4,)
+    assert [s.shape for s in vec] == [(4,)] * 3

@@ -21,6 +21,8 @@ XA_RETURNS_GAE = 1
 XA_RETURNS_NSTEP = 2
 XA_LOSS_PPO = 0
 XA_LOSS_A2C = 1
+XA_DIST_CATEGORICAL = 0
+XA_DIST_DIAG_GAUSSIAN = 1
 MLP_HIDDEN = 64
 
 
@@ -237,6 +239,7 @@ class XaHeadGradArgs(Structure):
         ('adv_eps', c_float),
         ('dlogits', c_void_p), ('dvalues', c_void_p), ('loss', c_void_p),
         ('stats_mode', c_int), ('adv_stats', c_void_p),
+        ('dist_kind', c_int), ('actions_f', c_void_p), ('ld_actions', c_int64),
     ]
 
 
@@ -366,6 +369,11 @@ _SIGNATURES = {
          c_void_p, c_void_p, c_void_p, c_int64, c_void_p],
     ),
     'xa_ac_head_grad': (c_int, [POINTER(XaHeadGradArgs), c_void_p]),
+    'xa_diag_gaussian': (
+        c_int,
+        [c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_uint64, c_int, c_void_p, c_int64,
+         c_void_p, c_void_p, c_void_p, c_int64, c_void_p],
+    ),
     'xa_acer_grad': (c_int, [POINTER(XaAcerArgs), c_void_p]),
     'xa_ema': (c_int, [c_void_p, c_void_p, c_int64, c_float, c_void_p]),
     'xa_noisy_actions': (

@@ -53,17 +53,23 @@ class A2C(ExecutorActorCritic, OnPolicy):
             len(model.layers) + 1 > 2
         ), f'Expected a model that has at least 3 layers, got {len(model.layers) + 1}'
         activations = [layer.activation for layer in model.layers[-2:]]
+        # A2C.get_distribution (a2c/agent.py:54-63): Categorical(probs) after a softmax
+        # output layer (its log-prob is the log-softmax of the layer's pre-activation,
+        # which the executor returns), Categorical(logits) otherwise, and
+        # MultivariateNormalDiag(loc = actor output) for Box action spaces
         self.output_is_softmax = 'softmax' in activations
         self.distribution_type = (
             'Categorical' if isinstance(self.envs[0].action_space, Discrete)
             else 'MultivariateNormalDiag')
-        if self.output_is_softmax or self.distribution_type != 'Categorical':
-            raise NotImplementedError('Only Categorical(logits) policies are supported')
         self.use_graph = use_graph
         self._graph = None
-        # the actor-critic MLP runs on the fused kernels; any other .cfg actor-critic
-        # (the CNN) on the layer executor (xagents_amd/onpolicy_executor.py)
-        self.executor_path = getattr(model, 'fused_kind', None) != 'actor_critic_mlp'
+        # the Categorical actor-critic MLP of the fused kernels' shapes runs fused; any other
+        # .cfg actor-critic (the CNN, a softmax actor, a Gaussian policy, other sizes) on the
+        # layer executor (xagents_amd/onpolicy_executor.py)
+        self.executor_path = not (
+            getattr(model, 'fused_kind', None) == 'actor_critic_mlp'
+            and self.distribution_type == 'Categorical'
+            and (getattr(model, 'obs_dim', None), self.n_actions) in kernels.FUSED_MLP_SHAPES)
         if self.executor_path:
             self._detect_distributed()
             self._setup_executor_path()
@@ -130,6 +136,8 @@ class A2C(ExecutorActorCritic, OnPolicy):
         """Parity mode: the fused rollout samples every action by inverse CDF from these
         [n_envs, n_steps] f32 device uniforms (held, not copied) instead of the Philox
         stream; None restores Philox."""
+        if self.executor_path:
+            raise NotImplementedError('rollout uniforms are injected on the fused MLP path')
         if uniforms is not None:
             assert uniforms.dtype == torch.float32 and uniforms.is_contiguous() and \
                 tuple(uniforms.shape) == (self.n_envs, self.n_steps), \
@@ -356,7 +364,52 @@ class A2C(ExecutorActorCritic, OnPolicy):
         if self._fused_steps % every == 0:
             self.check_peer_all_reduce()
 
+    def np_train_step(self):
+        """Batching and returns (xagents/a2c/agent.py:173-186): get_batch ->
+        calculate_returns -> concat_step_batches; env-major flat [states, returns,
+        actions, critic_output]."""
+        (states, rewards, actions, critic_output, dones, log_probs, entropies,
+         actor_output) = self.get_batch()
+        returns = self.calculate_returns(rewards, dones)
+        return self.concat_step_batches(states, returns, actions, critic_output)
+
+    def update_gradients(self, states, returns, actions, old_values):
+        """The A2C loss of a batch (xagents/a2c/agent.py:188-218): adv = R - V_old,
+        -mean(adv logp) - entropy_coef mean(H) + value_loss_coef mean((v - R)^2),
+        tf.clip_by_global_norm, Keras Adam -- xa_ac_grad + the reduce's optimizer tail."""
+        n = states.shape[0]
+        dev = self.device
+        c = lambda x, dt=torch.float32: torch.as_tensor(  # noqa: E731
+            x, device=dev).to(dt).reshape(n, -1).squeeze(-1).contiguous()
+        obs = torch.as_tensor(states, device=dev).float().reshape(n, -1).contiguous()
+        act, ret, oldv = c(actions, torch.int32), c(returns), c(old_values)
+        nb = kernels.ac_grad_blocks(n)
+        partials = torch.zeros(nb, self.model.n_params, dtype=torch.float32, device=dev)
+        lossp = torch.zeros(nb, 4, dtype=torch.float32, device=dev)
+        g = self._grad_args(n, nb, partials, lossp)
+        g.loss_kind = kernels.XA_LOSS_A2C
+        g.batch = n
+        g.epoch = g.mb_index = 0
+        g.obs, g.actions = obs.data_ptr(), act.data_ptr()
+        g.old_values, g.returns = oldv.data_ptr(), ret.data_ptr()
+        g.old_logp = None
+        g.adv_stats, g.adv_count, g.adv_in = None, 0.0, None
+        g.loss_scale = 1.0 / (n * self.world_size)
+        kernels.ac_grad(g)
+        self._apply_gradients(partials)
+        lp = lossp.sum(0)
+        return {'pg_loss': lp[0] / lp[3], 'value_loss': lp[1] / lp[3],
+                'entropy': lp[2] / lp[3]}
+
+    _A2C_HOOKS = ('get_batch', 'calculate_returns', 'np_train_step', 'update_gradients')
+
     def train_step(self):
+        if type(self).loss_kind == kernels.XA_LOSS_A2C and any(
+                getattr(type(self), h) is not getattr(A2C, h) for h in self._A2C_HOOKS):
+            # a subclass overrode a reference hook: compose the pieces (the reference's
+            # np_train_step + gradient step) so the override is honoured
+            self.update_gradients(*self.np_train_step())
+            return
         self.fused_train_step()
 
     # ---- reference-level pieces (composable, not used by the fused step) -----

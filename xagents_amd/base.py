@@ -58,7 +58,10 @@ class BaseAgent(ABC):
         self.seed = seed
         self.output_models = [self.model]
         self.log_frequency = log_frequency or self.n_envs
-        self.id = self.__module__.split('.')[1]
+        # the agent package (xagents/base.py:88); a user subclass defined outside the
+        # package (the reference would fail here) takes its nearest agent base class's id
+        self.id = next((c.__module__.split('.')[1] for c in type(self).__mro__
+                        if c.__module__.startswith('xagents_amd.')), self.__module__)
         self.history_checkpoint = history_checkpoint
         self.plateau_reduce_factor = plateau_reduce_factor
         self.plateau_reduce_patience = plateau_reduce_patience
@@ -124,7 +127,11 @@ class BaseAgent(ABC):
 
     @property
     def states(self):
-        return self.envs.state
+        """Per-env view of the current (post-reset) observations, as the reference's list
+        (LazyFrames for Atari frames, xagents/base.py:105-113); the device path reads
+        self.envs.state directly."""
+        from xagents_amd.utils.common import DeviceStates
+        return DeviceStates(self.envs.state)
 
     def set_action_count(self):
         action_space = self.envs[0].action_space

@@ -3,8 +3,10 @@
 //   * xa_categorical: TFP Categorical(logits) sample / log-prob / entropy over a batch of
 //     logit rows (A2C.get_model_outputs, xagents/a2c/agent.py:65-94), same arithmetic
 //     and inverse-CDF sampling as the fused MLP rollout (mlp_rollout.hip);
+//   * xa_diag_gaussian: MultivariateNormalDiag(loc) sample / log-prob / entropy for Box
+//     action spaces (a2c/agent.py:59-60);
 //   * xa_ac_head_grad: the PPO / A2C loss of a minibatch and its gradient w.r.t. the
-//     logits and the value head (PPO.update_gradients ppo/agent.py:96-137 with the
+//     logits (or the Gaussian mean) and the value head (PPO.update_gradients ppo/agent.py:96-137 with the
 //     per-minibatch advantage normalisation of run_ppo_epochs 180-183; A2C.train_step
 //     a2c/agent.py:190-218), TF tie semantics as in ac_update.hip.
 #include "../../include/xagents_hip.h"
@@ -13,6 +15,48 @@
 namespace {
 
 constexpr int kMaxA = 64;
+constexpr float kLog2Pi = 1.83787706640934548f;  // log(2 pi)
+
+// MultivariateNormalDiag(loc = mu) with unit scale (a2c/agent.py:59-60, 86-92): sample
+// a = mu + N(0, I) (Philox4x32-10 Box-Muller at counter (i, step, *rng_counter), or given
+// noise / actions), log-prob and entropy. One thread per row.
+__global__ void diag_gaussian_kernel(const float* __restrict__ mu, int64_t ld_mu, int n, int d,
+                                     const float* __restrict__ noise,
+                                     const uint64_t* __restrict__ ctr, uint64_t seed, int step,
+                                     const float* __restrict__ actions_in, int64_t ld_act,
+                                     float* __restrict__ act_out, float* __restrict__ logp,
+                                     float* __restrict__ ent, int64_t ld_out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float* m = mu + (int64_t)i * ld_mu;
+  const uint64_t c = ctr ? *ctr : 0ull;
+  float ss = 0.0f;
+  for (int j = 0; j < d; ++j) {
+    float a;
+    if (actions_in) {
+      a = actions_in[(int64_t)i * ld_act + j];
+    } else {
+      float e;
+      if (noise) {
+        e = noise[(int64_t)i * d + j];
+      } else {
+        // one Philox draw per pair of dimensions, Box-Muller
+        const xa_u4 r = xa_philox((uint32_t)i, (uint32_t)step, (uint32_t)(j >> 1) ^ (uint32_t)c,
+                                  (uint32_t)(c >> 32), (uint32_t)seed, (uint32_t)(seed >> 32));
+        const float u1 = fmaxf(xa_u01(r.x), 1.0e-7f), u2 = xa_u01(r.y);
+        const float rad = sqrtf(-2.0f * xa_logf(u1));
+        e = rad * ((j & 1) ? sinf(6.283185307179586f * u2) : cosf(6.283185307179586f * u2));
+      }
+      a = m[j] + e;
+      if (act_out) act_out[(int64_t)i * ld_act + j] = a;
+    }
+    const float dj = a - m[j];
+    ss = fmaf(dj, dj, ss);
+  }
+  const int64_t o = (int64_t)i * ld_out;
+  if (logp) logp[o] = -0.5f * ss - 0.5f * (float)d * kLog2Pi;
+  if (ent) ent[o] = 0.5f * (float)d * (1.0f + kLog2Pi);
+}
 
 __global__ void categorical_kernel(const float* __restrict__ logits, int64_t ld, int n, int A,
                                    const float* __restrict__ uniforms,
@@ -116,7 +160,54 @@ __global__ __launch_bounds__(1024) void ac_head_grad_kernel(XaHeadGradArgs p) {
   const float adv_std = (float)sqrt(fmax(t2 / cnt - mean * mean, 0.0));
   const float sc = 1.0f / (float)n;
   float l_pg = 0.0f, l_v = 0.0f, l_ent = 0.0f;
-  for (int i = tid; i < n; i += blockDim.x) {
+  const bool gauss = p.dist_kind == XA_DIST_DIAG_GAUSSIAN;
+  for (int i = tid; i < n && gauss; i += blockDim.x) {
+    // MultivariateNormalDiag(loc = z) with unit scale (a2c/agent.py:59-60):
+    // log p(a) = -0.5 |a - z|^2 - 0.5 d log(2 pi), entropy 0.5 d (1 + log(2 pi)) is
+    // constant (no gradient), d log p / d z = a - z
+    const float* z = p.logits + (int64_t)i * p.ld_logits;
+    const float* a = p.actions_f + (int64_t)i * p.ld_actions;
+    float ss = 0.0f;
+    for (int j = 0; j < A; ++j) {
+      const float dj = a[j] - z[j];
+      ss = fmaf(dj, dj, ss);
+    }
+    const float logp = -0.5f * ss - 0.5f * (float)A * kLog2Pi;
+    const float ent = 0.5f * (float)A * (1.0f + kLog2Pi);
+    const float v = p.values[(int64_t)i * p.ld_values];
+    const float R = p.returns[i], oldv = p.old_values[i];
+    const float adv_raw = R - oldv;
+    float dlogp, dv, pg, vl;
+    if (ppo) {
+      const float adv = (adv_raw - adv_mean) / (adv_std + p.adv_eps);
+      const float ratio = xa_expf(logp - p.old_logp[i]);
+      const float c = p.clip_norm;
+      const float pg1 = -adv * ratio;
+      const float pg2 = -adv * fminf(fmaxf(ratio, 1.0f - c), 1.0f + c);
+      pg = fmaxf(pg1, pg2);
+      const bool r_in = ratio >= 1.0f - c && ratio <= 1.0f + c;
+      dlogp = (pg1 >= pg2 || r_in) ? (sc * -adv) * ratio : 0.0f;
+      const float dvo = v - oldv;
+      const float vclip = oldv + fminf(fmaxf(dvo, -c), c);
+      const float vl1 = (v - R) * (v - R), vl2 = (vclip - R) * (vclip - R);
+      vl = fmaxf(vl1, vl2);
+      const float kv = sc * p.value_coef * 0.5f * 2.0f;
+      if (vl1 >= vl2) dv = kv * (v - R);
+      else dv = (dvo >= -c && dvo <= c) ? kv * (vclip - R) : 0.0f;
+    } else {
+      pg = -(adv_raw * logp);
+      dlogp = -sc * adv_raw;
+      vl = (v - R) * (v - R);
+      dv = sc * p.value_coef * 2.0f * (v - R);
+    }
+    float* dz = p.dlogits + (int64_t)i * A;
+    for (int j = 0; j < A; ++j) dz[j] = dlogp * (a[j] - z[j]);
+    p.dvalues[i] = dv;
+    l_pg += pg;
+    l_v += vl;
+    l_ent += ent;
+  }
+  for (int i = tid; i < n && !gauss; i += blockDim.x) {
     const float* z = p.logits + (int64_t)i * p.ld_logits;
     const int act = p.actions[i];
     float m = z[0];
@@ -206,9 +297,28 @@ extern "C" int xa_categorical(const float* logits, int64_t ld_logits, int n, int
   return 0;
 }
 
+extern "C" int xa_diag_gaussian(const float* mu, int64_t ld_mu, int n, int d, const float* noise,
+                                const uint64_t* rng_counter, uint64_t seed, int step,
+                                const float* actions_in, int64_t ld_act, float* actions_out,
+                                float* logp, float* entropy, int64_t ld_out, void* stream) {
+  XA_CHECK_ARG(mu && n > 0 && d > 0 && ld_mu >= d && (actions_in || actions_out) &&
+                   ld_act >= d,
+               "xa_diag_gaussian: bad arguments");
+  XA_CHECK_ARG(actions_in || noise || rng_counter,
+               "xa_diag_gaussian: sampling needs noise or rng_counter");
+  hipLaunchKernelGGL(diag_gaussian_kernel, dim3((n + 63) / 64), dim3(64), 0, (hipStream_t)stream,
+                     mu, ld_mu, n, d, noise, rng_counter, seed, step, actions_in, ld_act,
+                     actions_out, logp, entropy, ld_out > 0 ? ld_out : 1);
+  XA_CHECK_LAUNCH("xa_diag_gaussian");
+  return 0;
+}
+
 extern "C" int xa_ac_head_grad(const XaHeadGradArgs* p, void* stream) {
+  XA_CHECK_ARG(p && (p->dist_kind != XA_DIST_DIAG_GAUSSIAN || (p->actions_f && p->ld_actions >= p->n_actions)),
+               "xa_ac_head_grad: a Gaussian head needs actions_f [n, >= n_actions]");
   XA_CHECK_ARG(p && p->n > 0 && p->n_actions > 0 && p->n_actions <= kMaxA && p->logits &&
-                   p->values && p->actions && p->returns && p->old_values && p->dlogits &&
+                   p->values && (p->actions || p->dist_kind == XA_DIST_DIAG_GAUSSIAN) &&
+                   p->returns && p->old_values && p->dlogits &&
                    p->dvalues && (p->loss_kind != XA_LOSS_PPO || p->old_logp) &&
                    (p->stats_mode == 0 || p->adv_stats),
                "xa_ac_head_grad: bad arguments");

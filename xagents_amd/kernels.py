@@ -24,6 +24,11 @@ def gamma_lam_f32(gamma, lam):
     return float(np.float32(float(gamma) * float(lam)))
 
 
+# (obs_dim, n_actions) instantiations of the fused MLP kernels (mlp_rollout.hip,
+# ac_update.hip, ppo_update.hip)
+FUSED_MLP_SHAPES = frozenset({(4, 2), (6, 3), (8, 4), (2, 3)})
+
+
 def mlp_param_count(obs_dim, n_actions):
     return _lib.load().xa_mlp_param_count(obs_dim, n_actions)
 

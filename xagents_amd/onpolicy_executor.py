@@ -5,6 +5,7 @@ counterpart of the fused MLP kernels for any .cfg actor-critic.
 Rollout (A2C.get_batch, xagents/a2c/agent.py:96-139), per step t:
     CNN forward of obs[t] (uint8 frames, scaled in the GEMM loader)   xa_gemm x layers
     Categorical sample / log-prob / entropy (Philox uniforms)          xa_categorical
+    (Box action spaces: MultivariateNormalDiag(loc) sample / log-prob  xa_diag_gaussian)
     value -> values[:, t]                                              xa_copy_block
     env step: reward / done rows, obs[t+1] = the pre-reset obs (the
     terminal-obs feed-through of a2c/agent.py:132-136)                 xa_replay_env_step
@@ -22,8 +23,8 @@ import numpy as np
 import torch
 
 from xagents_amd import kernels
-from xagents_amd._lib import (XA_LOSS_PPO, XA_RETURNS_GAE, XaHeadGradArgs, XaReplayStepArgs,
-                              call, stream)
+from xagents_amd._lib import (XA_DIST_DIAG_GAUSSIAN, XA_LOSS_PPO, XA_RETURNS_GAE,
+                              XaHeadGradArgs, XaReplayStepArgs, call, stream)
 from xagents_amd.layers import LayerExecutor
 
 
@@ -44,7 +45,13 @@ class ExecutorActorCritic:
         f32 = dict(dtype=torch.float32, device=dev)
         self.obs_buf = torch.zeros((T + 1, N) + env.obs_shape,
                                    dtype=env.state.dtype, device=dev)
-        self.b_act = torch.zeros(N, T, dtype=torch.int32, device=dev)
+        # Box action spaces: MultivariateNormalDiag(loc = actor output), f32 action rows
+        self.gaussian = getattr(self, 'distribution_type', 'Categorical') != 'Categorical'
+        A = self.n_actions
+        if self.gaussian:
+            self.b_act = torch.zeros(N, T, A, dtype=torch.float32, device=dev)
+        else:
+            self.b_act = torch.zeros(N, T, dtype=torch.int32, device=dev)
         self.b_logp, self.b_val = torch.zeros(N, T, **f32), torch.zeros(N, T, **f32)
         self.b_ent, self.b_rew = torch.zeros(N, T, **f32), torch.zeros(N, T, **f32)
         self.b_done = torch.zeros(N, T + 1, **f32)
@@ -75,7 +82,8 @@ class ExecutorActorCritic:
         self.mb_logits = torch.zeros(mb, self.n_actions, **f32)
         self.mb_value = torch.zeros(mb, 1, **f32)
         self.mb_obs = torch.zeros((mb,) + env.obs_shape, dtype=env.state.dtype, device=dev)
-        self.mb_act = torch.zeros(mb, dtype=torch.int32, device=dev)
+        self.mb_act = (torch.zeros(mb, A, dtype=torch.float32, device=dev) if self.gaussian
+                       else torch.zeros(mb, dtype=torch.int32, device=dev))
         self.mb_logp, self.mb_val = torch.zeros(mb, **f32), torch.zeros(mb, **f32)
         self.mb_ret = torch.zeros(mb, **f32)
         self.dlogits = torch.zeros(mb, self.n_actions, **f32)
@@ -100,10 +108,17 @@ class ExecutorActorCritic:
         ob = env.obs_bytes
         for t in range(T):
             logits, value = self.ex_roll.forward(self.obs_buf[t])
-            call('xa_categorical', logits.data_ptr(), self.n_actions, N, self.n_actions, None,
-                 self.rng_counter.data_ptr(), self.rng_seed, t, None,
-                 self.b_act.data_ptr() + 4 * t, self.b_logp.data_ptr() + 4 * t,
-                 self.b_ent.data_ptr() + 4 * t, T, stream())
+            A = self.n_actions
+            if self.gaussian:
+                call('xa_diag_gaussian', logits.data_ptr(), A, N, A, None,
+                     self.rng_counter.data_ptr(), self.rng_seed, t, None, T * A,
+                     self.b_act.data_ptr() + 4 * t * A, self.b_logp.data_ptr() + 4 * t,
+                     self.b_ent.data_ptr() + 4 * t, T, stream())
+            else:
+                call('xa_categorical', logits.data_ptr(), A, N, A, None,
+                     self.rng_counter.data_ptr(), self.rng_seed, t, None,
+                     self.b_act.data_ptr() + 4 * t, self.b_logp.data_ptr() + 4 * t,
+                     self.b_ent.data_ptr() + 4 * t, T, stream())
             call('xa_copy_block', value.data_ptr(), 1, self.b_val.data_ptr() + 4 * t, T, N, 1,
                  stream())
             a.out_new_states = self.obs_buf.data_ptr() + (t + 1) * N * ob
@@ -141,9 +156,10 @@ class ExecutorActorCritic:
         so, sf = self._slots_obs.data_ptr(), self._slots_flat.data_ptr()
         call('xa_ring_gather', self.obs_buf.data_ptr(), self.mb_obs.data_ptr(), so, n,
              self.envs.obs_bytes, stream())
-        for src, dst in ((self.b_act, self.mb_act), (self.b_logp, self.mb_logp),
-                         (self.b_val, self.mb_val), (self.b_ret, self.mb_ret)):
-            call('xa_ring_gather', src.data_ptr(), dst.data_ptr(), sf, n, 4, stream())
+        act_bytes = 4 * self.n_actions if self.gaussian else 4
+        for src, dst, nb in ((self.b_act, self.mb_act, act_bytes), (self.b_logp, self.mb_logp, 4),
+                             (self.b_val, self.mb_val, 4), (self.b_ret, self.mb_ret, 4)):
+            call('xa_ring_gather', src.data_ptr(), dst.data_ptr(), sf, n, nb, stream())
 
     def _minibatch_step(self, n):
         A = self.n_actions
@@ -162,7 +178,12 @@ class ExecutorActorCritic:
         h.n, h.n_actions, h.loss_kind = n, self.n_actions, self.loss_kind
         h.logits, h.ld_logits = logits.data_ptr(), self.n_actions
         h.values, h.ld_values = value.data_ptr(), 1
-        h.actions, h.old_logp = self.mb_act.data_ptr(), self.mb_logp.data_ptr()
+        if self.gaussian:
+            h.dist_kind, h.actions = XA_DIST_DIAG_GAUSSIAN, None
+            h.actions_f, h.ld_actions = self.mb_act.data_ptr(), A
+        else:
+            h.actions = self.mb_act.data_ptr()
+        h.old_logp = self.mb_logp.data_ptr()
         h.old_values, h.returns = self.mb_val.data_ptr(), self.mb_ret.data_ptr()
         h.clip_norm = float(getattr(self, 'clip_norm', 0.0))
         h.entropy_coef, h.value_coef = float(self.entropy_coef), float(self.value_loss_coef)

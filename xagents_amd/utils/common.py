@@ -8,6 +8,69 @@ from pathlib import Path
 from xagents_amd.utils.buffers import ReplayBuffer1, ReplayBuffer2
 
 
+class LazyFrames:
+    """The reference's Atari frame container (xagents/utils/common.py:23-64): wraps a
+    uint8 frame array, materialised once on first use; np.asarray / len / indexing /
+    count() behave as there. Here frames live in HBM rings, so agent.states hands out
+    LazyFrames over host copies for user code; the device path never builds them."""
+
+    def __init__(self, frames):
+        self.frames = frames
+        self.out = None
+        self.dtype = frames.dtype
+        self.shape = frames.shape
+
+    def process_frame(self):
+        if self.out is None:
+            import numpy as np
+            self.out = np.array(self.frames)
+            self.frames = None
+        return self.out
+
+    def __array__(self, dtype=None, copy=None):
+        out = self.process_frame()
+        return out if dtype is None else out.astype(dtype)
+
+    def __len__(self):
+        return len(self.process_frame())
+
+    def __getitem__(self, i):
+        return self.process_frame()[i]
+
+    def count(self):
+        frames = self.process_frame()
+        return frames.shape[frames.ndim - 1]
+
+
+class DeviceStates:
+    """BaseAgent.states as the reference exposes it -- a per-env sequence (base.py:105,
+    407-424) -- over the device env's [n_envs, *obs] state tensor: states[i] is a host
+    copy (LazyFrames for image observations, a numpy array otherwise), np.asarray(states)
+    the stacked host array; `.tensor` is the device tensor itself."""
+
+    def __init__(self, tensor):
+        self.tensor = tensor
+
+    def __len__(self):
+        return self.tensor.shape[0]
+
+    def _host(self, x):
+        a = x.detach().cpu().numpy()
+        return LazyFrames(a) if a.ndim >= 2 else a
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return [self._host(x) for x in self.tensor[i]]
+        return self._host(self.tensor[i])
+
+    def __iter__(self):
+        return (self[i] for i in range(len(self)))
+
+    def __array__(self, dtype=None, copy=None):
+        a = self.tensor.detach().cpu().numpy()
+        return a if dtype is None else a.astype(dtype)
+
+
 def write_from_dict(_dict, path):
     """Append one row to a parquet dataset (training history)."""
     import pyarrow as pa
