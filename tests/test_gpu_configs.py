@@ -1,0 +1,152 @@
+"""BASELINE configs C3 / C4 / C5 at their single-GPU size: a few train
+steps each with the counters and ring bookkeeping checked, plus one sampled minibatch's
+raw gradient against the float64 restatement (oracle/nets_f64.py) at the full batch."""
+import random
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT / 'oracle'))
+pytestmark = pytest.mark.gpu
+
+
+def _np(t):
+    return t.detach().cpu().numpy().astype(np.float64)
+
+
+def _rel(got, want):
+    want = np.asarray(want, np.float64)
+    return float(np.linalg.norm(np.asarray(got, np.float64) - want) / np.linalg.norm(want))
+
+
+def test_c3_dqn_32_envs_rb1_1m_batch_64(device):
+    """C3: double DQN, 32 Pong-shaped envs, ReplayBuffer1 1M total (31,250 per env, the
+    full 14 GB uint8 ring allocated), buffer batch 64 (2 per env)."""
+    import nets_f64 as O
+    from test_gpu_scale import _dqn_f64
+    from xagents_amd import DQN
+    from xagents_amd.envs import create_envs
+    from xagents_amd.utils.common import create_buffers, create_model
+    n = 32
+    np.random.seed(3)
+    random.seed(3)
+    envs = create_envs('PongNoFrameskip-v4', n, device=device, seed=55)
+    model = create_model(envs, 'dqn', 'model', seed=55, device=device,
+                         optimizer_kwargs=dict(learning_rate=1e-4))
+    bufs = create_buffers('dqn', 1_000_000, 64, n, initial_size=64 * n)
+    assert [b.size for b in bufs] == [31250] * n and bufs[0].batch_size == 2
+    agent = DQN(envs, model, bufs, double=True, seed=55, quiet=True, epsilon_start=0.5,
+                epsilon_end=0.02)
+    assert agent.replay.states.shape[:2] == (n, 31250) and agent.batch_size == 64
+    agent.fill_buffers()
+    assert [b.current_size for b in bufs] == [64] * n
+    th0, tt0 = _np(model.theta), _np(agent.target_model.theta)
+    agent.at_step_start()
+    agent.train_step()
+    torch.cuda.synchronize()
+    _, loss64, g64 = _dqn_f64(agent, th0, tt0)
+    assert _rel(_np(agent.grad), g64) < 1e-4
+    assert _rel(_np(agent.td_loss), loss64) < 1e-5
+    for _ in range(5):
+        agent.at_step_start()
+        agent.train_step()
+        agent.at_step_end()
+    torch.cuda.synchronize()
+    assert agent.steps == 6 * n
+    assert [b.current_size for b in bufs] == [64 + 6] * n
+    assert int(model.optimizer.iterations.item()) == 6
+    assert np.isfinite(_np(model.theta)).all()
+
+
+def test_c4_ppo_cnn_128_env_shard(device):
+    """C4, one rank's shard: PPO with the CNN actor-critic on 128 Breakout-shaped envs x 128
+    steps (batch 16,384), 4 epochs x 4 minibatches of 4,096."""
+    import nets_f64 as O
+    import oracle as OR
+    from test_gpu_cnn_onpolicy import _heads_grad_f64
+    from xagents_amd import PPO
+    from xagents_amd.envs import create_envs
+    from xagents_amd.utils.common import create_model
+    n, T = 128, 128
+    envs = create_envs('BreakoutNoFrameskip-v4', n, device=device, seed=55)
+    model = create_model(envs, 'ppo', 'model', seed=55, device=device)
+    agent = PPO(envs, model, n_steps=T, seed=55, quiet=True)
+    assert agent.executor_path and agent.mb == 4096 and agent.n_mb == 4
+    th0 = _np(model.theta)
+    agent._executor_rollout()
+    # one minibatch of the update at full size vs float64
+    np.random.seed(9)
+    perm = np.random.permutation(n * T)[:agent.mb]
+    k = agent._upload_slots(perm)
+    agent._gather_minibatch(k)
+    agent._minibatch_step(k)
+    torch.cuda.synchronize()
+    obs = agent.obs_buf[:T].cpu().numpy()
+    idx = perm
+    x = obs[idx % T, idx // T]  # flat env-major index i = env * T + t
+    act = agent.b_act.cpu().numpy().reshape(-1)[idx]
+    oldlp, oldv, ret = (_np(t).reshape(-1)[idx] for t in (agent.b_logp, agent.b_val, agent.b_ret))
+    x64, outs = O.forward(model.layers, th0, x, model.input_shape)
+    logits, v = outs[model.outputs[0]], outs[model.outputs[1]][:, 0]
+    dz, dv = _heads_grad_f64(logits, v, act, oldlp, oldv, ret, 'ppo')
+    g = O.backward(model.layers, th0, x64, outs, {model.outputs[0]: dz, model.outputs[1]: dv[:, None]})
+    assert _rel(_np(agent.grad), g) < 1e-4
+    # full train steps
+    it0 = int(model.optimizer.iterations.item())
+    for _ in range(2):
+        agent.fused_train_step()
+    agent._drain_episode_stats()
+    torch.cuda.synchronize()
+    assert int(model.optimizer.iterations.item()) - it0 == 2 * 16
+    assert agent.steps == 2 * n * T
+    assert np.isfinite(_np(model.theta)).all()
+
+
+def test_c5_td3_64_envs_rb2(device):
+    """C5 on one GPU: TD3, 64 BipedalWalker-shaped envs, ReplayBuffer2 (1M total, per-buffer
+    batch 100 // 64 = 1), gradient_steps 1; one gradient step vs float64."""
+    from test_gpu_scale import _critic_head_f64
+    import nets_f64 as O
+    from xagents_amd import TD3
+    from xagents_amd.envs import create_envs
+    from xagents_amd.utils.common import create_buffers, create_model
+    n = 64
+    np.random.seed(4)
+    random.seed(4)
+    envs = create_envs('BipedalWalker-v3', n, device=device, seed=55)
+    kw = dict(seed=55, device=device)
+    actor = create_model(envs, 'td3', 'actor_model', **kw)
+    critic = create_model(envs, 'td3', 'critic_model', **kw)
+    bufs = create_buffers('td3', 1_000_000, 100, n, initial_size=n * 64)
+    assert bufs[0].batch_size == 1 and bufs[0].size == 1_000_000 // n
+    agent = TD3(envs, actor, critic, bufs, gradient_steps=1, seed=55, quiet=True)
+    assert agent.batch_size == 64
+    agent.fill_buffers()
+    c1 = _np(agent.critic.theta)
+    tt = [_np(m.theta) for m in (agent.target_actor, agent.target_critic, agent.target_critic2)]
+    agent.update_weights(1)
+    torch.cuda.synchronize()
+    s, a, r, d, s2 = (_np(x) for x in (agent.s, agent.a, agent.r, agent.d, agent.s2))
+    fw = lambda m, th, x: O.forward(m.layers, th, x, m.input_shape)  # noqa: E731
+    ta = fw(agent.target_actor, tt[0], s2)[1][agent.target_actor.outputs[0]]
+    ta = np.clip(ta + _np(agent.noise), -1, 1)
+    s2a2 = np.concatenate([s2, ta], 1)
+    tv = np.minimum(*[fw(c, th, s2a2)[1][c.outputs[0]]
+                      for c, th in zip((agent.target_critic, agent.target_critic2), tt[1:])])
+    y = r[:, None] + (1 - d[:, None]) * np.float64(np.float32(0.99)) * tv
+    x64, o = fw(agent.critic, c1, np.concatenate([s, a], 1))
+    dv, _ = _critic_head_f64(o[agent.critic.outputs[0]], y, None)
+    g = O.backward(agent.critic.layers, c1, x64, o, {agent.critic.outputs[0]: dv})
+    assert _rel(_np(agent.g_critic), g) < 1e-4
+    for _ in range(100):
+        agent.train_step()
+    agent._drain_episode_stats()
+    torch.cuda.synchronize()
+    it = int(agent.critic.optimizer.iterations.item())
+    assert it == 1 + agent.games and agent.games > 0
+    assert agent.steps == 100 * n
+    assert np.isfinite(_np(agent.actor.theta)).all()
