@@ -274,3 +274,25 @@ def test_lazyframes_and_states_view():
     vec = DeviceStates(torch.zeros(3, 4))
     assert isinstance(vec[0], np.ndarray) and vec[0].shape == (4,)
     assert [s.shape for s in vec] == [(4,)] * 3
+
+
+def test_fill_buffers_draws_actions_env_by_env():
+    """OffPolicy.fill_buffers draws env 0's random actions first, then env 1's
+    (xagents/base.py:702-730)."""
+    from types import SimpleNamespace
+    from xagents_amd.base import OffPolicy
+    from xagents_amd.envs import Discrete
+    from xagents_amd.utils.buffers import ReplayBuffer2
+    space = Discrete(6)
+    space.seed(3)
+    bufs = [ReplayBuffer2(10, 5, initial_size=4, batch_size=2) for _ in range(3)]
+    bufs[1].current_size = 1  # env 1 needs only 3 more
+    stub = SimpleNamespace(envs=[SimpleNamespace(action_space=space)], buffers=bufs, n_envs=3)
+    plan, need = OffPolicy._fill_action_plan(stub)
+    assert need == [4, 3, 4] and plan.shape == (4, 3)
+    ref = Discrete(6)
+    ref.seed(3)
+    draws = [int(ref.sample()) for _ in range(11)]
+    assert list(plan[:, 0]) == draws[0:4]
+    assert list(plan[:3, 1]) == draws[4:7]
+    assert list(plan[:, 2]) == draws[7:11]

@@ -32,6 +32,11 @@ Differences from the reference, by design:
   clone_model re-runs the seeded initializers, which give the same values);
 * float observations are refused: ACER.get_batch casts states to uint8
   (acer/agent.py:60,167), which only makes sense for image frames.
+
+Reference behaviour kept: the number of replays per train step is drawn ONCE,
+np.random.poisson(replay_ratio) at the first step that replays (the reference draws it
+while tracing its tf.function train_step, acer/agent.py:363-387); redraw_replays=True
+draws it every step (the per-step ACER of the paper).
 """
 import ctypes
 import random
@@ -69,9 +74,12 @@ class ACER(A2C):
         value_loss_coef=0.5,
         grad_norm=0.5,
         use_graph=True,
+        redraw_replays=False,
         **kwargs,
     ):
         OnPolicy.__init__(self, envs, model, **kwargs)
+        self.redraw_replays = redraw_replays
+        self._replay_count = None
         self.entropy_coef = entropy_coef
         self.value_loss_coef = value_loss_coef
         self.grad_norm = grad_norm
@@ -348,11 +356,17 @@ class ACER(A2C):
         self.buffer_current_size += 1
         self._acer_update(*self._slot_views(slot))
         if self.replay_ratio > 0 and self.buffer_current_size >= self.buffers[0].initial_size:
-            n_replay = np.random.poisson(self.replay_ratio)
-            if self.distributed:  # every rank must run the same number of all-reduces
-                t = torch.tensor([n_replay], dtype=torch.int64, device=self.device)
-                dist.broadcast(t, 0)
-                n_replay = int(t.item())
+            n_replay = self._replay_count
+            if n_replay is None or self.redraw_replays:
+                # the reference's train_step is a tf.function: range(np.random.poisson(...))
+                # runs once, at trace time, so ONE draw fixes the replay count of the whole
+                # run (acer/agent.py:376-380); redraw_replays=True draws every step instead
+                n_replay = np.random.poisson(self.replay_ratio)
+                if self.distributed:  # every rank must run the same number of all-reduces
+                    t = torch.tensor([n_replay], dtype=torch.int64, device=self.device)
+                    dist.broadcast(t, 0)
+                    n_replay = int(t.item())
+                self._replay_count = n_replay
             for _ in range(n_replay):
                 self._acer_update(*self._gather(self.sample_slots()))
         rec(2)

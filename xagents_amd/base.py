@@ -542,19 +542,37 @@ class OffPolicy(BaseAgent, ABC):
         dist.all_gather_object(parts, np.asarray(arr))
         return np.concatenate(parts)
 
-    def _random_actions(self):
-        """env.action_space.sample() per env (OffPolicy.fill_buffers, base.py:702-730)."""
+    def _fill_action_plan(self):
+        """The random actions of fill_buffers in the reference's draw order: env 0's
+        action_space.sample() calls until its buffer is full, then env 1's, ...
+        (xagents/base.py:702-730); [max missing, n_envs, *act] plus each env's count."""
         space = self.envs[0].action_space
-        return np.stack([np.asarray(space.sample()) for _ in range(self.n_envs)])
+        need = [max(b.initial_size - b.current_size, 0) for b in self.buffers]
+        seqs = [[np.asarray(space.sample()) for _ in range(k)] for k in need]
+        width = max(need) if need else 0
+        proto = np.asarray(space.sample()) if width else None
+        plan = None
+        if width:
+            plan = np.zeros((width, self.n_envs) + proto.shape, proto.dtype)
+            for i, seq in enumerate(seqs):
+                if seq:
+                    plan[:len(seq), i] = np.stack(seq)
+        return plan, need
 
     def fill_buffers(self):
-        """Step every env with random actions until each buffer holds initial_size
-        transitions (xagents/base.py:702-730), then reset the envs."""
+        """Random actions until each buffer holds initial_size transitions
+        (xagents/base.py:702-730), then reset the envs. The actions are drawn env by env
+        in the reference's order (_fill_action_plan); the device then steps every env
+        together (an env that needed fewer than another takes action 0 on the extra
+        steps, which leaves the draw order unchanged)."""
         total = sum(b.initial_size for b in self.buffers)
+        plan, need = self._fill_action_plan()
+        step = 0
         while min(b.current_size - b.initial_size for b in self.buffers) < 0:
-            acts = torch.as_tensor(self._random_actions(), device=self.device)
+            acts = torch.as_tensor(plan[min(step, len(plan) - 1)], device=self.device)
             acts = acts.to(self.replay.act_t).contiguous()
             self._env_step(acts)
+            step += 1
             filled = sum(min(b.current_size, b.initial_size) for b in self.buffers)
             complete = round((filled / total) * 100, self.display_precision)
             self.display_message(
