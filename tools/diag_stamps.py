@@ -30,7 +30,7 @@ def build():
 
 def main():
     lib_path = build() if not (len(sys.argv) > 1 and sys.argv[1] == '--no-build') else (
-        OUT / 'libxagents_hip_diag.so')
+        ROOT / 'tools' / 'diag_lib' / 'libxagents_hip_diag.so')  # built here, travels to the box
     if len(sys.argv) > 1 and sys.argv[1] == '--build-only':
         return
     import torch
