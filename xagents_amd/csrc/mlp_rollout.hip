@@ -12,9 +12,11 @@
 //   h1 -> LDS (wave-private row), 16 x ds_read_b128 broadcast back
 //   h2_j = tanh(sum of 8 interleaved 8-long fma chains + b2_j)
 //   logit_a = butterfly_sum_j(h2_j * W3[j][a]) + b3_a ;  value likewise
-//   softmax / log-prob / entropy / inverse-CDF sample on every lane (wave-uniform)
 //   env step (replay: records of 64 steps fetched a chunk ahead, one lane per step,
-//   read back with readlane; cartpole: f64 dynamics)
+//   read back with readlane; cartpole: inverse-CDF sample, then f64 dynamics)
+//   logits / value parked in lane (t & 63)
+// and once per 64-step chunk, lane j on step t0 + j: softmax, log-prob, entropy and
+// (replay env, whose record stream ignores the action) the sample.
 // Envs are independent, so no inter-wave synchronisation exists anywhere.
 // The arithmetic order above is restated exactly by oracle/xa_oracle.c.
 #include "../../include/xagents_hip.h"
@@ -130,34 +132,54 @@ struct CatOut {
   float logp, entropy;
 };
 
+// max, shifted exponentials and their sum: the part both the sample and the
+// log-prob / entropy need (the same operations in both, so a sample drawn on the
+// step's critical path and a log-prob computed later agree bit for bit)
 template <int A>
-XA_DEV CatOut<A> categorical(const float (&l)[A], float u, int given_action) {
+XA_DEV float cat_exp(const float (&l)[A], float (&e)[A], float& s) {
   float m = l[0];
 #pragma unroll
   for (int a = 1; a < A; ++a) m = fmaxf(m, l[a]);
-  float e[A];
-  float s = 0.0f;
+  s = 0.0f;
 #pragma unroll
   for (int a = 0; a < A; ++a) {
     e[a] = xa_expf(l[a] - m);
     s = s + e[a];
   }
-  const float ls = xa_logf(s);
-  int act = given_action;
-  if (act < 0) {
-    const float target = u * s;
-    act = A - 1;
-    float c = 0.0f;
-    bool found = false;
+  return m;
+}
+
+// inverse-CDF sample: the first a with u * s < e_0 + ... + e_a (A - 1 if none)
+template <int A>
+XA_DEV int cat_pick(const float (&e)[A], float s, float u) {
+  const float target = u * s;
+  int act = A - 1;
+  float c = 0.0f;
+  bool found = false;
 #pragma unroll
-    for (int a = 0; a < A; ++a) {
-      c = c + e[a];
-      if (!found && target < c) {
-        act = a;
-        found = true;
-      }
+  for (int a = 0; a < A; ++a) {
+    c = c + e[a];
+    if (!found && target < c) {
+      act = a;
+      found = true;
     }
   }
+  return act;
+}
+
+template <int A>
+XA_DEV int cat_sample(const float (&l)[A], float u) {
+  float e[A], s;
+  cat_exp<A>(l, e, s);
+  return cat_pick<A>(e, s, u);
+}
+
+template <int A>
+XA_DEV CatOut<A> categorical(const float (&l)[A], float u, int given_action) {
+  float e[A], s;
+  const float m = cat_exp<A>(l, e, s);
+  const float ls = xa_logf(s);
+  const int act = given_action < 0 ? cat_pick<A>(e, s, u) : given_action;
   float ent = 0.0f, logp = 0.0f;
   const float inv_s = 1.0f / s;
 #pragma unroll
@@ -260,13 +282,20 @@ __global__ __launch_bounds__(256) void mlp_rollout_kernel(XaRolloutArgs p) {
   if (lane == 0) p.done_out[(size_t)env * (T + 1)] = d_last;
 
   // per-step scalars park in lane (t & 63) and leave as one coalesced store per
-  // output after each 64-step chunk (no stores inside the step loop)
-  float b_obs[OBS] = {};
-  int b_act = 0;
-  float b_logp = 0.0f, b_val = 0.0f, b_ent = 0.0f, b_rew = 0.0f, b_done = 0.0f, b_epret = 0.0f;
+  // output after each 64-step chunk (no stores inside the step loop). What the next
+  // step does not read -- log-prob and entropy always, the sample too for the replay
+  // env, whose record stream ignores the action -- is computed once per chunk with
+  // lane j on step t0 + j (the same operations as in-step, so bit for bit the same).
+  float b_obs[OBS] = {};  // CartPole only: replay inputs are the shifted record obs
+  int b_act = 0;          // CartPole only: the replay action is drawn in the chunk pass
+  float b_l[A] = {};
+  float b_val = 0.0f, b_rew = 0.0f, b_done = 0.0f, b_epret = 0.0f;
 
   auto run_chunk = [&](const StepChunk<OBS>& c, int t0) {
     const int n = min(64, T - t0);
+    float x0[OBS];  // the chunk's first policy input
+#pragma unroll
+    for (int k = 0; k < OBS; ++k) x0[k] = x[k];
     for (int j = 0; j < n; ++j) {
       XA_STAMP(0);
       float logits[A], value;
@@ -279,28 +308,31 @@ __global__ __launch_bounds__(256) void mlp_rollout_kernel(XaRolloutArgs p) {
         net.heads(h2, logits, value);
       }
       XA_STAMP(3);
-      const float u = p.uniforms ? xa_readlane(c.u_given, j) : xa_readlane(c.u_philox, j);
-      const CatOut<A> cat = categorical<A>(logits, u, -1);
-      XA_STAMP(4);
-      // env step
+      const bool mine = lane == j;
       float r, d;
-      float o_obs[OBS];
       if constexpr (REPLAY) {
         r = xa_readlane(c.r, j);
         d = xa_readlane(c.d, j);
 #pragma unroll
-        for (int k = 0; k < OBS; ++k) {
-          o_obs[k] = xa_readlane(c.obs[k], j);
-          st[k] = xa_readlane(c.st[k], j);
-        }
+        for (int k = 0; k < OBS; ++k) x[k] = xa_readlane(c.obs[k], j);  // pre-reset obs
       } else {
-        bool done = cartpole_step(cp, cat.action);
+        const float u = p.uniforms ? xa_readlane(c.u_given, j) : xa_readlane(c.u_philox, j);
+        const int act = cat_sample<A>(logits, u);
+        XA_STAMP(4);
+        bool done = cartpole_step(cp, act);
         cur = cur + 1;
         if (cur >= p.max_episode_steps) done = true;  // gym TimeLimit
         r = 1.0f;
         d = done ? 1.0f : 0.0f;
+        if (mine) {
 #pragma unroll
-        for (int k = 0; k < OBS; ++k) o_obs[k] = (float)cp[k < 4 ? k : 3];
+          for (int k = 0; k < OBS; ++k) b_obs[k] = x[k];
+          b_act = act;
+          b_rew = r;
+          b_done = d;
+        }
+#pragma unroll
+        for (int k = 0; k < OBS; ++k) x[k] = (float)cp[k < 4 ? k : 3];  // pre-reset obs
         if (done) {
           // reset: np_random.uniform(-0.05, 0.05, size=(4,))
           const xa_u4 rr = xa_philox((uint32_t)env, (uint32_t)(t0 + j), (uint32_t)ctr,
@@ -312,35 +344,47 @@ __global__ __launch_bounds__(256) void mlp_rollout_kernel(XaRolloutArgs p) {
             cp[k] = -0.05 + 0.1 * ((double)rv[k] * 2.3283064365386963e-10);
           cur = 0;
         }
+      }
+      if (mine) {
 #pragma unroll
-        for (int k = 0; k < OBS; ++k) st[k] = (float)cp[k < 4 ? k : 3];
+        for (int a = 0; a < A; ++a) b_l[a] = logits[a];
+        b_val = value;
       }
       ep_ret = ep_ret + r;
-      if (lane == j) {
-#pragma unroll
-        for (int k = 0; k < OBS; ++k) b_obs[k] = x[k];
-        b_act = cat.action;
-        b_logp = cat.logp;
-        b_val = value;
-        b_ent = cat.entropy;
-        b_rew = r;
-        b_done = d;
-        b_epret = ep_ret;
-      }
+      if (mine) b_epret = ep_ret;
       if (d != 0.0f) ep_ret = 0.0f;
       d_last = d;
-#pragma unroll
-      for (int k = 0; k < OBS; ++k) x[k] = o_obs[k];  // pre-reset obs feeds the next step
       XA_STAMP(6);
     }
+    // chunk pass: lane j finishes step t0 + j
+    const float u = p.uniforms ? c.u_given : c.u_philox;
+    const CatOut<A> cat = categorical<A>(b_l, u, REPLAY ? -1 : b_act);
+    float o_obs[OBS];
+    if constexpr (REPLAY) {
+#pragma unroll
+      for (int k = 0; k < OBS; ++k) {
+        const float prev = __shfl_up(c.obs[k], 1);  // step j's input = record obs of j - 1
+        o_obs[k] = lane == 0 ? x0[k] : prev;
+        st[k] = xa_readlane(c.st[k], n - 1);
+      }
+      b_rew = c.r;
+      b_done = c.d;
+    } else {
+#pragma unroll
+      for (int k = 0; k < OBS; ++k) {
+        o_obs[k] = b_obs[k];
+        st[k] = (float)cp[k < 4 ? k : 3];  // post-reset state
+      }
+    }
+    XA_STAMP(7);
     if (lane < n) {
       const size_t o = (size_t)env * T + t0 + lane;
 #pragma unroll
-      for (int k = 0; k < OBS; ++k) p.obs_out[o * OBS + k] = b_obs[k];
-      p.act_out[o] = b_act;
-      p.logp_out[o] = b_logp;
+      for (int k = 0; k < OBS; ++k) p.obs_out[o * OBS + k] = o_obs[k];
+      p.act_out[o] = cat.action;
+      p.logp_out[o] = cat.logp;
       p.val_out[o] = b_val;
-      if (p.ent_out) p.ent_out[o] = b_ent;
+      if (p.ent_out) p.ent_out[o] = cat.entropy;
       p.rew_out[o] = b_rew;
       p.done_out[(size_t)env * (T + 1) + 1 + t0 + lane] = b_done;
       if (p.epret_out) p.epret_out[o] = b_epret;
