@@ -196,3 +196,58 @@ def test_agent_persistent_update_matches_chain(device, monkeypatch):
     assert np.linalg.norm(ta - tb) / np.linalg.norm(tb - theta0) < 1e-4
     assert int(a.model.optimizer.iterations.item()) == int(b.model.optimizer.iterations.item()) == 16
     assert int(a.device_status.item()) == 0
+
+
+@pytest.mark.parametrize('n_envs', [16, 64])
+def test_graph_replays_back_to_back_equal_eager(device, n_envs):
+    """The bench's pattern: hipGraph replays of the persistent update back to back (no
+    eager launch in between, 16 blocks / 64 blocks two-level) give the eager result bit
+    for bit, with no hand-off timeout."""
+    from test_gpu_agent import make_agent
+    a = make_agent(n_envs=n_envs, n_steps=128, seed=11, use_graph=True, t_rec=512)
+    for _ in range(6):
+        a.train_step()
+    torch.cuda.synchronize()
+    b = make_agent(n_envs=n_envs, n_steps=128, seed=11, use_graph=False, t_rec=512)
+    for _ in range(6):
+        b.train_step()
+    torch.cuda.synchronize()
+    assert a._graph is not None and a.update_mode == 'persistent'
+    assert int(a.device_status.item()) == 0 and int(b.device_status.item()) == 0
+    np.testing.assert_array_equal(a.b_act.cpu().numpy(), b.b_act.cpu().numpy())
+    np.testing.assert_array_equal(a.model.theta.cpu().numpy(), b.model.theta.cpu().numpy())
+    np.testing.assert_array_equal(a.model.optimizer.v.cpu().numpy(),
+                                  b.model.optimizer.v.cpu().numpy())
+
+
+def test_bench_loop_graph_replays_equal_eager(device):
+    """The bench's exact loop -- fused_train_step with events, host running ahead, the
+    per-step episode-statistics copies -- for 40 steps gives the eager replica's
+    parameters bit for bit. (A memset node in front of the update once let the runtime's
+    copy-kernel arguments land on the control words after ~16 such steps: the launch
+    then left early without a timeout.)"""
+    from xagents_amd import PPO
+    from xagents_amd.envs import ReplayVecEnv, record_cartpole_replay
+    from xagents_amd.utils.common import create_model
+    n = 16
+    rec = record_cartpole_replay(n, 1024, seed=55)
+    agents = []
+    for g in (True, False):
+        envs = ReplayVecEnv('CartPole-v1', n, device='cuda', record=rec)
+        model = create_model(envs, 'ppo', 'model', optimizer_kwargs=dict(learning_rate=7e-4),
+                             seed=55, device='cuda')
+        agents.append(PPO(envs, model, n_steps=128, seed=55, quiet=True, use_graph=g))
+    a, b = agents
+    for _ in range(5):
+        a.train_step()
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(35)]
+    for k in range(35):
+        a.fused_train_step(events[k])
+    torch.cuda.synchronize()
+    for _ in range(40):
+        b.train_step()
+    torch.cuda.synchronize()
+    assert a._graph is not None
+    assert int(a.device_status.item()) == 0
+    assert int(a.model.optimizer.iterations.item()) == 40 * 16
+    np.testing.assert_array_equal(a.model.theta.cpu().numpy(), b.model.theta.cpu().numpy())

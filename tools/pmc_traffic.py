@@ -1,5 +1,6 @@
-"""Turn the two rocprofv3 PMC passes (tools/gpurun_pmc.sh) into profiles/traffic.json:
-HBM bytes per launch of the hot kernels. FETCH_SIZE / WRITE_SIZE are in KB; on gfx950
+"""Turn the rocprofv3 PMC passes (tools/gpurun_pmc.sh, tools/gpurun_r02n.sh) into
+profiles/traffic.json: HBM bytes per launch of the hot kernels, keyed per workload shape
+(`<kernel>_<tag>`, e.g. ppo_update_n16) when the passes ran per shape. FETCH_SIZE / WRITE_SIZE are in KB; on gfx950
 FETCH_SIZE counts half the bytes of wide coalesced reads (MI355X_MICROARCH.md, HBM), so
 it is doubled; WRITE_SIZE is exact for 16-B-per-lane stores."""
 import csv
@@ -10,7 +11,8 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
 KERNELS = {'ac_grad': 'ac_grad_kernel<4, 2>', 'rollout': 'mlp_rollout_kernel<4, 2, true>',
-           'grad_reduce': 'grad_reduce_kernel', 'minibatch': 'minibatch_kernel'}
+           'grad_reduce': 'grad_reduce_kernel', 'minibatch': 'minibatch_kernel',
+           'ppo_update': 'ppo_update_kernel<4, 2>'}
 
 
 def per_kernel(counter, src):
@@ -29,27 +31,46 @@ def per_kernel(counter, src):
     return {k: (sum(v) / len(v), len(v)) for k, v in vals.items()}
 
 
-def main(out_dir='gpurun_out'):
-    fetch = per_kernel('FETCH_SIZE', Path(out_dir) / 'pmc_FETCH_SIZE')
-    write = per_kernel('WRITE_SIZE', Path(out_dir) / 'pmc_WRITE_SIZE')
+def entries(fetch_dir, write_dir, suffix=''):
+    fetch = per_kernel('FETCH_SIZE', fetch_dir)
+    write = per_kernel('WRITE_SIZE', write_dir)
     res = {}
     for k in KERNELS:
         if k in fetch and k in write:
             f_kb, n = fetch[k]
             w_kb, _ = write[k]
-            res[k] = {'bytes_per_launch': round((2 * f_kb + w_kb) * 1024),
-                      'fetch_size_kb_raw': round(f_kb, 1), 'write_size_kb': round(w_kb, 1),
-                      'dispatches': n,
-                      'correction': 'FETCH_SIZE x 2 (gfx950 wide-read tally), KB = 1024 B'}
-    if 'grad_reduce' in res:
-        # calibration on a known byte count (MI355X_MICROARCH.md: other access widths are
-        # uncalibrated): xa_grad_reduce reads exactly 256 rows x 4675 f32 with 4-B lanes
-        known = 256 * 4675 * 4
-        res['calibration'] = {'kernel': 'grad_reduce', 'known_read_bytes': known,
-                              'fetch_raw_bytes': round(fetch['grad_reduce'][0] * 1024),
-                              'factor': round(known / (fetch['grad_reduce'][0] * 1024), 3)}
-    (ROOT / 'profiles').mkdir(exist_ok=True)
-    (ROOT / 'profiles' / 'traffic.json').write_text(json.dumps(res, indent=1) + '\n')
+            res[k + suffix] = {'bytes_per_launch': round((2 * f_kb + w_kb) * 1024),
+                               'fetch_size_kb_raw': round(f_kb, 1), 'write_size_kb': round(w_kb, 1),
+                               'dispatches': n,
+                               'correction': 'FETCH_SIZE x 2 (gfx950 wide-read tally), KB = 1024 B'}
+    return res, fetch
+
+
+def main(out_dir='gpurun_out', *tags):
+    """No tags: gpurun_out/pmc_{FETCH_SIZE,WRITE_SIZE} -> unsuffixed keys (round 1 layout).
+    Tags (e.g. r02n_n16): gpurun_out/pmc_<tag>_{FETCH_SIZE,WRITE_SIZE} -> keys suffixed
+    with the tag's last '_' field (ppo_update_n16). Merges into the existing file."""
+    f_out = ROOT / 'profiles' / 'traffic.json'
+    res = json.loads(f_out.read_text()) if f_out.exists() else {}
+    if not tags:
+        new, fetch = entries(Path(out_dir) / 'pmc_FETCH_SIZE', Path(out_dir) / 'pmc_WRITE_SIZE')
+        res.update(new)
+        if 'grad_reduce' in new:
+            # calibration on a known byte count (MI355X_MICROARCH.md: other access widths
+            # are uncalibrated): xa_grad_reduce reads exactly 256 rows x 4675 f32 with 4-B lanes
+            known = 256 * 4675 * 4
+            res['calibration'] = {'kernel': 'grad_reduce', 'known_read_bytes': known,
+                                  'fetch_raw_bytes': round(fetch['grad_reduce'][0] * 1024),
+                                  'factor': round(known / (fetch['grad_reduce'][0] * 1024), 3)}
+    for tag in tags:
+        suffix = '_' + tag.split('_')[-1]
+        new, _ = entries(Path(out_dir) / f'pmc_{tag}_FETCH_SIZE',
+                         Path(out_dir) / f'pmc_{tag}_WRITE_SIZE', suffix)
+        for v in new.values():
+            v['source'] = f'rocprofv3 --pmc passes {tag} (tools/gpurun_r02n.sh)'
+        res.update(new)
+    f_out.parent.mkdir(exist_ok=True)
+    f_out.write_text(json.dumps(res, indent=1) + '\n')
     print(json.dumps(res, indent=1))
 
 

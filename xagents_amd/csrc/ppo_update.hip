@@ -19,14 +19,17 @@
 //        block), clip + Keras Adam with t = t0 + k + 1 on its register-resident slice
 //        of theta / m / v (ac_tile.hpp ParamSlice), refresh the LDS weight tiles
 //   block 0 stores theta / m / v and the Adam step count at the end.
-// Hops follow the write-through hand-off (cdna_hip_programming.md Guideline 16,
-// MI355X_MICROARCH.md visibility table row 1): every handed-off word is stored with a
-// write-through (sc1) store, every storing wave drains (s_waitcnt vmcnt(0)), a barrier,
-// ONE lane adds 1 to an agent-scope counter; the consumer's ONE lane polls the counter
-// relaxed (sc1 load), a barrier, then every load of the handed-off words is an sc1
-// load. Counters are zeroed by a memset node in front of every launch and count
-// arrivals within the call. Spins are bounded (wall clock); a timeout raises the
-// abort word and `status`, and every block leaves.
+// Hand-offs follow the write-through protocol (cdna_hip_programming.md Guideline 16,
+// MI355X_MICROARCH.md visibility table row 1): handed-off words are stored write-through
+// (sc1) and loaded with sc1 loads. Inside the step loop the data is its own flag (tagged
+// granules, below); the one counter hop (phase 0) drains (s_waitcnt vmcnt(0)), barriers,
+// and ONE lane adds 1 to an agent-scope counter that ONE lane of every block polls.
+// Nothing is reset between launches (no memset node in front of the kernel): the launch
+// generation `gen` in the workspace numbers the launches, the counter target is
+// (gen + 1) G, granule tags are unique per (launch, step), and the abort word holds the
+// number of the launch that aborted. Spins are bounded (wall clock); a timeout raises the
+// abort word and `status` (after which the workspace must be re-zeroed), and every block
+// leaves.
 #include <math.h>
 
 #include "../../include/xagents_hip.h"
@@ -44,9 +47,9 @@ typedef __attribute__((address_space(1))) unsigned long long gu64;
 constexpr int kMaxSteps = 512;              // E * M optimizer steps per launch
 constexpr int kCtlBytes = 256;              // control words at the workspace start
 constexpr uint64_t kSpinTicks = 200000000;  // 2 s of the 100 MHz wall clock per hop
-// control words (zeroed per launch): global hop counters, the abort word, and per XCD
-// the census count and the XCD-local row hop counter
-enum { kCntStats = 0, kCntRows = 1, kCntGrad = 2, kAbort = 3, kCntX = 4, kXcnt = 8, kXrows = 16 };
+// control words (never reset): the phase-0 arrival counter ((gen + 1) G after launch gen)
+// and the abort word (the number gen + 1 of a launch that timed out)
+enum { kCntStats = 0, kAbort = 1 };
 constexpr int kXcds = 8;            // MI355X: 8 XCDs, each with its own L2
 constexpr int kTwoLevelMinG = 64;   // >= 8 blocks per XCD: reduce inside each XCD's L2 first
 
@@ -112,7 +115,7 @@ XA_DEV double gran_f64(const f32x4v& v) {
 // by the wall clock and the abort word; false on timeout / abort (the caller leaves).
 template <int N>
 XA_DEV bool poll_gran(__amdgpu_buffer_rsrc_t r, const uint32_t (&off)[N], int n, unsigned tag,
-                      f32x4v (&v)[N], unsigned* ctl, int* status) {
+                      f32x4v (&v)[N], unsigned* ctl, unsigned epoch, int* status) {
   uint64_t t0 = 0;
   for (;;) {
 #pragma unroll
@@ -126,11 +129,12 @@ XA_DEV bool poll_gran(__amdgpu_buffer_rsrc_t r, const uint32_t (&off)[N], int n,
     const uint64_t now = wall_clock64();
     if (t0 == 0) t0 = now;
     else if (now - t0 > kSpinTicks) {
-      __hip_atomic_store((gu32*)(ctl + kAbort), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store((gu32*)(ctl + kAbort), epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (status) __hip_atomic_store((gu32*)status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return false;
     }
-    if (__hip_atomic_load((gu32*)(ctl + kAbort), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+    if (__hip_atomic_load((gu32*)(ctl + kAbort), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+        epoch)
       return false;
     __builtin_amdgcn_s_sleep(1);
   }
@@ -143,14 +147,15 @@ XA_DEV int xcc_id() {
   return (int)(x & (kXcds - 1));
 }
 
-// Workspace (device memory, zeroed once by the caller at allocation):
-//   ctl      control words, zeroed by a memset node in front of every launch
-//   persist  the launch generation (NOT reset: the granule tags of every launch differ)
+// Workspace (device memory, zeroed once by the caller at allocation; nothing in it is
+// reset between launches):
+//   ctl      control words (phase-0 counter, abort word)
+//   persist  the launch generation gen (the granule tags of every launch differ)
 //   rows_g   [G, PP/2] granule pairs: the blocks' gradient rows
 //   g_g      [PP/2] granule pairs: the reduced gradient
 //   sumsq_g  [G] granule pairs: f64 sums of squares of the g slices (lo, hi words)
 //   adv      [K, G, 2] f64 advantage sums (phase-0 hop)
-//   members  [kXcds, G] census of the blocks of every XCD (two-level)
+//   cen_g    [G] granule pairs: the XCD each block runs on (two-level census)
 //   xpart_g  [kXcds, PP] granule pairs: f64 per-XCD partial sums of the rows (two-level)
 // A granule is 8 bytes {32-bit value, 32-bit tag}; two of them travel in one 16-byte
 // access (MI355X_MICROARCH.md: 16-B write-through halves observed untorn), and the tag
@@ -162,7 +167,7 @@ struct Ws {
   void* g_g;
   void* sumsq_g;
   double* adv;
-  int* members;
+  void* cen_g;
   void* xpart_g;
   size_t total;
 };
@@ -187,7 +192,7 @@ __host__ __device__ inline Ws carve(void* base, int G, int P, int K) {
   w.g_g = take(PP * 8);
   w.sumsq_g = take((size_t)G * 16);
   w.adv = (double*)take((size_t)K * G * 2 * sizeof(double));
-  w.members = (int*)take((size_t)kXcds * G * sizeof(int));
+  w.cen_g = take((size_t)G * 16);
   w.xpart_g = take((size_t)kXcds * PP * 16);
   w.total = off;
   return w;
@@ -231,9 +236,10 @@ struct UpdLds {
   double red[256 * 4];
   double wsum[4];
   int flag;
-  int xn[kXcds];   // blocks per XCD (census)
-  int xmem[256];   // this XCD's blocks, ascending block id (two-level)
-  int xrank;       // this block's position among them
+  int xn[kXcds];      // blocks per XCD (census)
+  int wx[4][kXcds];   // census: blocks per (wave of block ids, XCD)
+  int xmem[256];      // this XCD's blocks, ascending block id (two-level)
+  int xrank;          // this block's position among them
 };
 
 // Publish: every wave drained its write-through stores, then ONE lane counts the
@@ -245,20 +251,24 @@ XA_DEV void hop_signal(unsigned* ctl, int which) {
     __hip_atomic_fetch_add((gu32*)(ctl + which), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Consume: ONE lane polls the counter (relaxed sc1 loads, bounded by the wall clock and
-// the abort word); the block then leaves the barrier together. Returns false on abort.
-XA_DEV bool hop_wait(unsigned* ctl, int which, unsigned target, int* status, int& lds_flag) {
+// Consume: ONE lane polls the counter until it reaches `target` (relaxed sc1 loads,
+// bounded by the wall clock and the abort word); the block then leaves the barrier
+// together. Returns false on abort.
+XA_DEV bool hop_wait(unsigned* ctl, int which, unsigned target, unsigned epoch, int* status,
+                     int& lds_flag) {
   if (threadIdx.x == 0) {
     int ok = 1;
     const uint64_t t0 = wall_clock64();
-    while (__hip_atomic_load((gu32*)(ctl + which), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
-           target) {
-      if (__hip_atomic_load((gu32*)(ctl + kAbort), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+    // wrap-safe: the counter only grows
+    while ((int)(__hip_atomic_load((gu32*)(ctl + which), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
+      if (__hip_atomic_load((gu32*)(ctl + kAbort), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+          epoch) {
         ok = 0;
         break;
       }
       if (wall_clock64() - t0 > kSpinTicks) {
-        __hip_atomic_store((gu32*)(ctl + kAbort), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store((gu32*)(ctl + kAbort), epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (status) __hip_atomic_store((gu32*)status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         ok = 0;
         break;
@@ -287,15 +297,18 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
   XA_STAMP_DECL
   XA_STAMP(30);
 
-  // ---- census: which XCD this block runs on (published by the phase-0 hop) ----
+  // the launch generation (written write-through by block 0 of the previous launch, which
+  // cannot finish before every block of this launch has passed phase 0)
+  const unsigned gen =
+      __hip_atomic_load((gu32*)ws.persist, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned epoch = gen + 1u;
+
+  // ---- census: which XCD this block runs on (a granule, read after the phase-0 hop) ----
   const bool two_level = G >= kTwoLevelMinG;
   const int xcc = xcc_id();
-  if (two_level && tid == 0) {
-    const unsigned slot = __hip_atomic_fetch_add((gu32*)(ws.ctl + kXcnt + xcc), 1u,
-                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store((gu32*)(ws.members + xcc * G + slot), (unsigned)b, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-  }
+  const __amdgpu_buffer_rsrc_t cen_r = rsrc(ws.cen_g, (uint32_t)(G * 16));
+  if (two_level && tid == 0) st_gran2(cen_r, (uint32_t)(16 * b), __uint_as_float((unsigned)xcc),
+                                      __uint_as_float((unsigned)xcc), epoch, true);
 
   // ---- phase 0: advantage sums of this block's samples of every minibatch ----
   for (int k = w; k < K; k += 4) {
@@ -334,25 +347,33 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
   ps.to_lds(L, wv, rv);
 
   XA_STAMP(32);
-  if (!hop_wait(ws.ctl, kCntStats, (unsigned)G, p.status, U.flag)) return;
+  if (!hop_wait(ws.ctl, kCntStats, epoch * (unsigned)G, epoch, p.status, U.flag)) return;
   if (two_level) {
-    // this XCD's member blocks in ascending id: fixed reduction order and column split
-    if (tid < kXcds)
-      U.xn[tid] = (int)__hip_atomic_load((gu32*)(ws.ctl + kXcnt + tid), __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT);
+    // thread t reads block t's census granule; per XCD, the member blocks in ascending id
+    // (fixed reduction order and column split) from wave ballots
+    int xt = -1;
+    bool bad = false;
+    if (tid < G) {
+      const uint32_t off[1] = {(uint32_t)(16 * tid)};
+      f32x4v v[1];
+      bad = !poll_gran<1>(cen_r, off, 1, epoch, v, ws.ctl, epoch, p.status);
+      xt = (int)__float_as_uint(v[0][0]);
+    }
+    if (__syncthreads_or(bad)) return;
+    int below = 0;  // lanes of this wave below this one on the same XCD
+#pragma unroll
+    for (int x = 0; x < kXcds; ++x) {
+      const unsigned long long m = __ballot(xt == x);
+      if (lane == 0) U.wx[w][x] = __popcll(m);
+      if (xt == x) below = __popcll(m & ((1ull << lane) - 1ull));
+    }
     __syncthreads();
-    const int ng = U.xn[xcc];
-    int mb_id = -1;
-    if (tid < ng)
-      mb_id = (int)__hip_atomic_load((gu32*)(ws.members + xcc * G + tid), __ATOMIC_RELAXED,
-                                     __HIP_MEMORY_SCOPE_AGENT);
-    U.red[tid] = (double)mb_id;  // scratch: the unsorted list
-    __syncthreads();
-    if (tid < ng) {
-      int rank = 0;
-      for (int j = 0; j < ng; ++j) rank += (int)U.red[j] < mb_id;
-      U.xmem[rank] = mb_id;
-      if (mb_id == b) U.xrank = rank;
+    if (tid < kXcds) U.xn[tid] = (U.wx[0][tid] + U.wx[1][tid]) + (U.wx[2][tid] + U.wx[3][tid]);
+    if (xt == xcc) {
+      int rank = below;
+      for (int ww = 0; ww < w; ++ww) rank += U.wx[ww][xt];
+      U.xmem[rank] = tid;
+      if (tid == b) U.xrank = rank;
     }
     __syncthreads();
   }
@@ -422,8 +443,7 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
   const __amdgpu_buffer_rsrc_t xp_r = rsrc(ws.xpart_g, (uint32_t)(kXcds * PP * 16));
   float* srow = U.row;
   for (int i = P + tid; i < PP; i += 256) srow[i] = 0.0f;  // the pad stays zero
-  // granule tags: unique per (launch, step); the generation word is bumped at the end
-  const unsigned gen = *ws.persist;
+  // granule tags: unique per (launch, step)
   auto tag_of = [&](int k) { return gen * (unsigned)K + (unsigned)k + 1u; };
   int* const fail = &U.flag;
 
@@ -495,7 +515,7 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
               off[u] = j < ng ? (uint32_t)(((size_t)U.xmem[j] * NP2 + c) * 16) : 0u;
               n += j < ng;
             }
-            bad = !poll_gran<kB>(rows_r, off, n, tag, x, ws.ctl, p.status);
+            bad = !poll_gran<kB>(rows_r, off, n, tag, x, ws.ctl, epoch, p.status);
 #pragma unroll
             for (int u = 0; u < kB; ++u)
               if (u < n) {
@@ -552,7 +572,7 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
                   n += 2;
                 }
               }
-              bad = !poll_gran<kB>(xp_r, off, n, tag, x, ws.ctl, p.status);
+              bad = !poll_gran<kB>(xp_r, off, n, tag, x, ws.ctl, epoch, p.status);
               for (int u = 0; u + 1 < n; u += 2) {
                 a0 += gran_f64(x[u]);
                 a1 += gran_f64(x[u + 1]);
@@ -564,7 +584,7 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
                 off[u] = r < G ? (uint32_t)(((size_t)r * NP2 + c) * 16) : 0u;
                 n += r < G;
               }
-              bad = !poll_gran<kB>(rows_r, off, n, tag, x, ws.ctl, p.status);
+              bad = !poll_gran<kB>(rows_r, off, n, tag, x, ws.ctl, epoch, p.status);
 #pragma unroll
               for (int u = 0; u < kB; ++u)
                 if (u < n) {
@@ -616,7 +636,7 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
         for (int h = 0; h < 2; ++h) off[2 * rr + h] = (uint32_t)((ps.w2_off(rr) / 2 + h) * 16);
 #pragma unroll
       for (int q = 0; q < RPT; ++q) off[8 + q] = (uint32_t)((ps.ri[q] >= 0 ? ps.ri[q] / 2 : 0) * 16);
-      bad = !poll_gran<NG>(g_r, off, NG, tag, x, ws.ctl, p.status);
+      bad = !poll_gran<NG>(g_r, off, NG, tag, x, ws.ctl, epoch, p.status);
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
         gw[4 * rr] = x[2 * rr][0];
@@ -640,7 +660,7 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
         n += gi < G;
       }
       // lanes past G poll nothing (n counts this lane's valid granules in order)
-      bad = !poll_gran<4>(sq_r, off, n, tag, x, ws.ctl, p.status);
+      bad = !poll_gran<4>(sq_r, off, n, tag, x, ws.ctl, epoch, p.status);
 #pragma unroll
       for (int u = 0; u < 4; ++u)
         if (u < n) tot += gran_f64(x[u]);
@@ -662,7 +682,8 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
     ps.store(p.adam_v, vw, vr);
     if (tid == 0) {
       *p.adam_step = t0 + K;
-      *ws.persist = gen + 1u;  // the next launch's tags (read at its start)
+      // the next launch's generation, write-through (read at its start on every XCD)
+      __hip_atomic_store((gu32*)ws.persist, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
@@ -697,10 +718,6 @@ template <int OBS, int A>
 int launch(const XaPpoUpdateArgs* a, int G, int K, int n_mb, hipStream_t s) {
   const int P = offs(OBS, A).P;
   const Ws ws = carve(a->workspace, G, P, K);
-  if (hipMemsetAsync(ws.ctl, 0, kCtlBytes, s) != hipSuccess) {
-    xa_set_error("xa_ppo_update: control-word memset failed");
-    return -2;
-  }
   hipLaunchKernelGGL((ppo_update_kernel<OBS, A>), dim3(G), dim3(256), 0, s, *a, ws, K, n_mb);
   XA_CHECK_LAUNCH("xa_ppo_update");
   return 0;
