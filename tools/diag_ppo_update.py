@@ -14,8 +14,10 @@ SLOTS = {30: 'phase 0: adv sums', 31: 'hop 0 signal', 32: 'param loads', 33: 'ho
          50: ' tile: H1 (VALU tanh)', 51: ' tile: Z2 = H1 W2 (MFMA) + tanh',
          52: ' tile: heads + loss + dz', 53: ' tile: dA2 + head grads',
          54: ' tile: dW2, dH1 (MFMA)', 55: ' tile: dW1', 36: 'tile end',
-         37: 'row write (write-through)', 38: 'hop 1 signal (drain + add)', 39: 'hop 1 wait',
-         40: 'phase B reduce', 41: 'hop 2 signal', 42: 'hop 2 wait', 43: 'phase C norm+Adam'}
+         44: 'row: combine partials (LDS)', 45: 'row: loss sums + granule stores',
+         37: 'row: next tile prefetch', 38: 'XCD level-1 reduce (two-level)',
+         40: 'phase B reduce', 46: 'phase C: g slice poll', 47: 'phase C: norm partial poll',
+         43: 'phase C: norm + Adam + LDS'}
 
 
 def main():
@@ -35,7 +37,7 @@ def main():
     from xagents_amd.utils.common import create_model
     L = _lib._lib
     buf = (ctypes.c_ulonglong * 64)()
-    for n in (16, 256):
+    for n in [int(a) for a in sys.argv[1:] if a.isdigit()] or (16, 256):
         envs = ReplayVecEnv('CartPole-v1', n, t_rec=4096, seed=55, device='cuda')
         model = create_model(envs, 'ppo', 'model', seed=55, device='cuda')
         agent = PPO(envs, model, n_steps=128, seed=55, quiet=True, use_graph=False)

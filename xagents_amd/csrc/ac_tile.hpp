@@ -34,6 +34,35 @@ constexpr int LDT = 36;  // LDS row stride of transposed [64][32] tiles
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// Update-path math on the hardware transcendental units (v_exp_f32 / v_log_f32 /
+// v_rcp_f32, about 1 ulp): the update's outputs are floating-point gradients checked
+// against float64 with a tolerance, so it does not need the rollout's restated
+// bit-exact sequences (xa_expf / xa_logf / xa_tanhf, whose integer action indices the C
+// oracle must reproduce). tanh keeps xa_tanhf's rational form, with the division by a
+// refined reciprocal.
+XA_DEV float fexp(float x) { return __builtin_amdgcn_exp2f(x * 1.44269504088896341f); }
+XA_DEV float flog(float x) { return __builtin_amdgcn_logf(x) * 0.693147180559945309f; }
+XA_DEV float frcp(float x) {
+  const float r = __builtin_amdgcn_rcpf(x);
+  return fmaf(fmaf(-x, r, 1.0f), r, r);  // one Newton step
+}
+XA_DEV float ftanh(float x) {
+  const float c = 7.90531110763549805f;
+  const float xc = fminf(fmaxf(x, -c), c);
+  const float x2 = xc * xc;
+  float p = fmaf(x2, -2.76076847742355e-16f, 2.00018790482477e-13f);
+  p = fmaf(x2, p, -8.60467152213735e-11f);
+  p = fmaf(x2, p, 5.12229709037114e-08f);
+  p = fmaf(x2, p, 1.48572235717979e-05f);
+  p = fmaf(x2, p, 6.37261928875436e-04f);
+  p = fmaf(x2, p, 4.89352455891786e-03f);
+  p = xc * p;
+  float q = fmaf(x2, 1.19825839466702e-06f, 1.18534705686654e-04f);
+  q = fmaf(x2, q, 2.26843463243900e-03f);
+  q = fmaf(x2, q, 4.89352518554385e-03f);
+  return p * frcp(q);
+}
+
 // D = A B + C on a 16x16 tile, K = 4: lane l feeds A[l&15][k=l>>4], B[k=l>>4][l&15];
 // D[row = 4*(l>>4) + r][col = l&15] lands in register r (exact f32 fma chain).
 XA_DEV f32x4 mfma4(float a, float b, f32x4 c) {
@@ -109,6 +138,7 @@ struct LossCfg {
   bool is_ppo, has_adv_in;
   float loss_scale, clip_norm, value_coef, entropy_coef, adv_eps;
   float adv_mean, adv_std;
+  float adv_rstd;  // 1 / (adv_std + adv_eps), set with adv_std
 };
 
 // A thread's slice of the flat parameter vector (see the file comment).
@@ -201,7 +231,7 @@ XA_DEV void tile_compute(TileLds<OBS, A>& L, TileAcc<OBS, A>& acc, const LossCfg
       float z = 0.0f;
 #pragma unroll
       for (int k = 0; k < OBS; ++k) z = fmaf(L.sX[s * OBS + k], L.sW1[k * H + f], z);
-      hv[ss] = xa_tanhf(z + L.sb1[f]);
+      hv[ss] = ftanh(z + L.sb1[f]);
       L.sH1[s * LDW + f] = hv[ss];
     }
     *reinterpret_cast<float4*>(&L.sH1T[f * LDT + c8]) = make_float4(hv[0], hv[1], hv[2], hv[3]);
@@ -231,7 +261,7 @@ XA_DEV void tile_compute(TileLds<OBS, A>& L, TileAcc<OBS, A>& acc, const LossCfg
       for (int kk = 0; kk < 16; ++kk) d = mfma4(av[kk], bv[kk], d);
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        L.sH2[(16 * st + 4 * lq + r) * LDW + 16 * w + li] = xa_tanhf(d[r] + bias);
+        L.sH2[(16 * st + 4 * lq + r) * LDW + 16 * w + li] = ftanh(d[r] + bias);
     }
   }
   __syncthreads();
@@ -263,15 +293,15 @@ XA_DEV void tile_compute(TileLds<OBS, A>& L, TileAcc<OBS, A>& acc, const LossCfg
         float e[A], ssum = 0.0f;
 #pragma unroll
         for (int a = 0; a < A; ++a) {
-          e[a] = xa_expf(z[a] - m);
+          e[a] = fexp(z[a] - m);
           ssum = ssum + e[a];
         }
-        const float ls = xa_logf(ssum);
+        const float ls = flog(ssum), rs = frcp(ssum);
         float lp[A], pr[A], ent = 0.0f, logp = 0.0f;
 #pragma unroll
         for (int a = 0; a < A; ++a) {
           lp[a] = (z[a] - m) - ls;
-          pr[a] = e[a] / ssum;
+          pr[a] = e[a] * rs;
           ent = ent - pr[a] * lp[a];
           if (a == act) logp = lp[a];
         }
@@ -283,8 +313,8 @@ XA_DEV void tile_compute(TileLds<OBS, A>& L, TileAcc<OBS, A>& acc, const LossCfg
         float dlogp, dv, pg, vl;
         if (cfg.is_ppo) {
           const float adv =
-              cfg.has_adv_in ? L.sAdvIn[s] : (adv_raw - cfg.adv_mean) / (cfg.adv_std + cfg.adv_eps);
-          const float ratio = xa_expf(logp - L.sOldLp[s]);
+              cfg.has_adv_in ? L.sAdvIn[s] : (adv_raw - cfg.adv_mean) * cfg.adv_rstd;
+          const float ratio = fexp(logp - L.sOldLp[s]);
           const float c = cfg.clip_norm;
           const float pg1 = -adv * ratio;
           const float pg2 = -adv * fminf(fmaxf(ratio, 1.0f - c), 1.0f + c);

@@ -246,6 +246,7 @@ __global__ __launch_bounds__(256) void ac_grad_kernel(XaAcGradArgs p) {
     cfg.adv_mean = (float)mean;
     cfg.adv_std = (float)sqrt(var);
   }
+  cfg.adv_rstd = 1.0f / (cfg.adv_std + cfg.adv_eps);
 
   TileAcc<OBS, A> acc;
   acc.zero();

@@ -152,8 +152,8 @@ XA_DEV int xcc_id() {
 //   ctl      control words (phase-0 counter, abort word)
 //   persist  the launch generation gen (the granule tags of every launch differ)
 //   rows_g   [G, PP/2] granule pairs: the blocks' gradient rows
-//   g_g      [PP/2] granule pairs: the reduced gradient
-//   sumsq_g  [G] granule pairs: f64 sums of squares of the g slices (lo, hi words)
+//   g_g      [PP/2] granule pairs: the reduced gradient, then [G] granule pairs: the f64
+//            sums of squares of the g slices (lo, hi words) -- one buffer, one poll
 //   adv      [K, G, 2] f64 advantage sums (phase-0 hop)
 //   cen_g    [G] granule pairs: the XCD each block runs on (two-level census)
 //   xpart_g  [kXcds, PP] granule pairs: f64 per-XCD partial sums of the rows (two-level)
@@ -165,7 +165,6 @@ struct Ws {
   unsigned* persist;
   void* rows_g;
   void* g_g;
-  void* sumsq_g;
   double* adv;
   void* cen_g;
   void* xpart_g;
@@ -189,8 +188,7 @@ __host__ __device__ inline Ws carve(void* base, int G, int P, int K) {
   w.ctl = (unsigned*)take(kCtlBytes);
   w.persist = (unsigned*)take(256);
   w.rows_g = take((size_t)G * PP * 8);
-  w.g_g = take(PP * 8);
-  w.sumsq_g = take((size_t)G * 16);
+  w.g_g = take(PP * 8 + (size_t)G * 16);
   w.adv = (double*)take((size_t)K * G * 2 * sizeof(double));
   w.cen_g = take((size_t)G * 16);
   w.xpart_g = take((size_t)kXcds * PP * 16);
@@ -228,11 +226,19 @@ XA_DEV int shuf_index(const XaShuffle& sh, const ShufKeys& keys, int epoch, int 
                          keys.k[2], keys.k[3]);
 }
 
+// Per-sample inputs of every tile a block processes in the launch, gathered in phase 0
+// when they fit: {obs[OBS], action (-1 = padding), return, old value, old log-prob}.
+constexpr int kPreBytes = 16384;
+template <int OBS>
+constexpr int pre_max() { return kPreBytes / ((OBS + 4) * 4); }
+
 template <int OBS, int A>
 struct UpdLds {
   TileLds<OBS, A> t;
   alignas(16) float row[(offs(OBS, A).P + 3) & ~3];  // the block's gradient row, staged
-  float stat[kMaxSteps][2];  // per optimizer step: advantage mean, population std
+  float pre[pre_max<OBS>() * (OBS + 4)];             // preloaded tile inputs
+  float alpha[kMaxSteps];    // per optimizer step: the Adam step size
+  float stat[kMaxSteps][3];  // per optimizer step: advantage mean, population std, 1 / (std + eps)
   double red[256 * 4];
   double wsum[4];
   int flag;
@@ -310,7 +316,14 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
   if (two_level && tid == 0) st_gran2(cen_r, (uint32_t)(16 * b), __uint_as_float((unsigned)xcc),
                                       __uint_as_float((unsigned)xcc), epoch, true);
 
-  // ---- phase 0: advantage sums of this block's samples of every minibatch ----
+  // ---- phase 0: advantage sums of this block's samples of every minibatch; their
+  // inputs into LDS when all of them fit; the Adam step size of every step ----
+  const int n_tiles_max = (min(MB, B) + S - 1) / S;
+  const int TPB = (n_tiles_max + G - 1) / G;  // tiles per block per step (at most)
+  const bool pre = K * TPB * S <= pre_max<OBS>();
+  const int t0 = *p.adam_step;
+  for (int k = tid; k < K; k += 256)
+    U.alpha[k] = adam_alpha(p.adam.lr, p.adam.beta1, p.adam.beta2, t0 + k + 1);
   for (int k = w; k < K; k += 4) {
     const int e = k / n_mb, m = k - e * n_mb;
     const int start = m * MB, cnt = min(MB, B - start);
@@ -318,13 +331,27 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
     const ShufKeys keys = shuf_keys(p.shuffle, ctr, e, B);
     const int mine = n_tiles > b ? (n_tiles - b + G - 1) / G : 0;  // tiles of this block
     double s1 = 0.0, s2 = 0.0;
-    for (int j = lane; j < mine * S; j += 64) {
+    for (int j = lane; j < (pre ? TPB : mine) * S; j += 64) {
       const int q = (b + (j / S) * G) * S + (j % S);
-      if (q >= cnt) continue;
+      const bool valid = j < mine * S && q < cnt;
+      float* slot = &U.pre[((size_t)k * TPB * S + j) * (OBS + 4)];
+      if (!valid) {
+        if (pre) slot[OBS] = -1.0f;  // padding
+        continue;
+      }
       const int idx = shuf_index(p.shuffle, keys, e, B, start + q);
-      const float adv = p.returns[idx] - p.old_values[idx];
+      const float ret = p.returns[idx], oldv = p.old_values[idx];
+      const float adv = ret - oldv;
       s1 += (double)adv;
       s2 += (double)adv * (double)adv;
+      if (pre) {
+#pragma unroll
+        for (int kk = 0; kk < OBS; ++kk) slot[kk] = p.obs[(size_t)idx * OBS + kk];
+        slot[OBS] = (float)p.actions[idx];
+        slot[OBS + 1] = ret;
+        slot[OBS + 2] = oldv;
+        slot[OBS + 3] = p.old_logp[idx];
+      }
     }
     s1 = xa_wave_sum_f64(s1);
     s2 = xa_wave_sum_f64(s2);
@@ -343,7 +370,6 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
   ps.load(p.theta, wv, rv);
   ps.load(p.adam_m, mw, mr);
   ps.load(p.adam_v, vw, vr);
-  const int t0 = *p.adam_step;
   ps.to_lds(L, wv, rv);
 
   XA_STAMP(32);
@@ -393,6 +419,7 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
       const double var = fmax(s2 / n - mean * mean, 0.0);
       U.stat[k][0] = (float)mean;
       U.stat[k][1] = (float)sqrt(var);
+      U.stat[k][2] = 1.0f / (U.stat[k][1] + p.adv_eps);
     }
   }
 
@@ -402,7 +429,7 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
   float nx[OBS], n_act = 0.0f, n_ret = 0.0f, n_oldv = 0.0f, n_oldlp = 0.0f;
   int n_valid = 0;
   auto fetch_tile = [&](int k, int tile) {
-    if (tid >= S) return;
+    if (pre || tid >= S) return;
     long idx = -1;
     if (k < K) {
       const int e = k / n_mb, m = k - e * n_mb;
@@ -438,14 +465,44 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
   const int CB = (NP2 + G - 1) / G;
   const int c0 = min(NP2, b * CB), nc = min(NP2, c0 + CB) - c0;
   const __amdgpu_buffer_rsrc_t rows_r = rsrc(ws.rows_g, (uint32_t)((size_t)G * PP * 8));
-  const __amdgpu_buffer_rsrc_t g_r = rsrc(ws.g_g, (uint32_t)(PP * 8));
-  const __amdgpu_buffer_rsrc_t sq_r = rsrc(ws.sumsq_g, (uint32_t)(G * 16));
+  const __amdgpu_buffer_rsrc_t g_r = rsrc(ws.g_g, (uint32_t)(PP * 8 + G * 16));
+  const uint32_t sq0 = (uint32_t)(PP * 8);  // the sums of squares follow g
   const __amdgpu_buffer_rsrc_t xp_r = rsrc(ws.xpart_g, (uint32_t)(kXcds * PP * 16));
   float* srow = U.row;
   for (int i = P + tid; i < PP; i += 256) srow[i] = 0.0f;  // the pad stays zero
   // granule tags: unique per (launch, step)
   auto tag_of = [&](int k) { return gen * (unsigned)K + (unsigned)k + 1u; };
   int* const fail = &U.flag;
+  // Flat gather of nrow rows x ncol pair columns in ONE poll round (row r's pair column c
+  // at byte offset base(r) + 16 c of `r`), staged as f32 pairs in LDS scratch (the W2
+  // tiles: dead between the row write and phase C's refresh); summed afterwards in
+  // ascending row order. Used when the rows x columns fit kBF granules per thread.
+  constexpr int kBF = 11;
+  float* const scr = L.sW2;  // spans sW2 and sW2T (2 H LDW floats >= 2 * 256 kBF)
+  static_assert(2 * H * LDW >= 2 * 256 * kBF, "gather scratch");
+  auto gather_rows = [&](__amdgpu_buffer_rsrc_t r, int nrow, int ncol, auto base,
+                         unsigned tg) -> bool {
+    const int total = nrow * ncol;
+    uint32_t off[kBF];
+    f32x4v x[kBF];
+    int n = 0;
+#pragma unroll
+    for (int u = 0; u < kBF; ++u) {
+      const int f = tid + 256 * u;
+      const int rr = f / ncol;
+      off[u] = f < total ? base(rr) + (uint32_t)(16 * (f - rr * ncol)) : 0u;
+      n += f < total;
+    }
+    const bool bad = !poll_gran<kBF>(r, off, n, tg, x, ws.ctl, epoch, p.status);
+#pragma unroll
+    for (int u = 0; u < kBF; ++u)
+      if (u < n) {
+        const int f = tid + 256 * u;
+        scr[2 * f] = x[u][0];
+        scr[2 * f + 1] = x[u][2];
+      }
+    return bad;
+  };
 
   TileAcc<OBS, A> acc;
   for (int k = 0; k < K; ++k) {
@@ -456,13 +513,25 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
     __syncthreads();  // U.stat, the LDS weights of the previous step
     cfg.adv_mean = U.stat[k][0];
     cfg.adv_std = U.stat[k][1];
+    cfg.adv_rstd = U.stat[k][2];
     cfg.loss_scale = 1.0f / (float)cnt;
     acc.zero();
     XA_STAMP(34);
     // ---- A: forward + loss + backward of this block's tiles ----
     for (int tile = b; tile < n_tiles; tile += G) {
       __syncthreads();
-      if (tid < S) {
+      if (tid < S && pre) {
+        const float* slot = &U.pre[((size_t)k * TPB * S + ((tile - b) / G) * S + tid) * (OBS + 4)];
+        const float act = slot[OBS];
+        L.sValid[tid] = act >= 0.0f;
+#pragma unroll
+        for (int kk = 0; kk < OBS; ++kk) L.sX[tid * OBS + kk] = act >= 0.0f ? slot[kk] : 0.0f;
+        L.sAct[tid] = act >= 0.0f ? act : 0.0f;
+        L.sRet[tid] = act >= 0.0f ? slot[OBS + 1] : 0.0f;
+        L.sOldV[tid] = act >= 0.0f ? slot[OBS + 2] : 0.0f;
+        L.sOldLp[tid] = act >= 0.0f ? slot[OBS + 3] : 0.0f;
+        L.sAdvIn[tid] = 0.0f;
+      } else if (tid < S) {
         L.sValid[tid] = n_valid;
 #pragma unroll
         for (int kk = 0; kk < OBS; ++kk) L.sX[tid * OBS + kk] = nx[kk];
@@ -480,6 +549,7 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
     }
     // ---- the block's gradient row, staged in LDS, published as granule pairs ----
     tile_write_row<OBS, A>(L, acc, [&](int i, float v) { srow[i] = v; });
+    XA_STAMP(44);
     if (p.loss_out) {
       const float ls = tile_loss_sums<OBS, A>(L, acc);
       if (tid < 4) p.loss_out[((size_t)k * G + b) * 4 + tid] = ls;
@@ -488,6 +558,7 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
     for (int c = tid; c < NP2; c += 256)
       st_gran2(rows_r, (uint32_t)(((size_t)b * NP2 + c) * 16), srow[2 * c], srow[2 * c + 1], tag,
                !two_level);
+    XA_STAMP(45);
     fetch_tile(k + 1, b);  // the next step's first tile, while the other blocks finish
     XA_STAMP(37);
     if (tid == 0) *fail = 0;
@@ -497,9 +568,27 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
       const int ng = U.xn[xcc];
       const int CBx = (NP2 + ng - 1) / ng;
       const int xc0 = min(NP2, U.xrank * CBx), xnc = min(NP2, xc0 + CBx) - xc0;
+      const bool flat = false && ng * xnc <= 256 * kBF;  // measured slower at 32 rows (C2)
+      if (flat && xnc > 0) {
+        const bool bad = gather_rows(rows_r, ng, xnc, [&](int j) {
+          return (uint32_t)(((size_t)U.xmem[j] * NP2 + xc0) * 16);
+        }, tag);
+        if (__syncthreads_or(bad)) return;
+        for (int c = tid; c < xnc; c += 256) {
+          double t0 = 0.0, t1 = 0.0;
+          for (int j = 0; j < ng; ++j) {
+            t0 += (double)scr[2 * (j * xnc + c)];
+            t1 += (double)scr[2 * (j * xnc + c) + 1];
+          }
+          const uint32_t off = (uint32_t)(((size_t)xcc * NP2 + xc0 + c) * 32);
+          st_gran_f64(xp_r, off, t0, tag);
+          st_gran_f64(xp_r, off + 16, t1, tag);
+        }
+        __syncthreads();
+      }
       const int ncol = max(1, min(xnc, 256)), RG = 256 / ncol;
       const int rg = tid / ncol, cq = tid - rg * ncol;
-      for (int cb = 0; cb < xnc; cb += ncol) {
+      for (int cb = 0; !flat && cb < xnc; cb += ncol) {
         bool bad = false;
         if (rg < RG && cb + cq < xnc) {
           const int c = xc0 + cb + cq;
@@ -545,7 +634,29 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
     // ---- B: pair columns [c0, c0 + nc): the fixed-order sum over the G rows, or
     // (two-level) over the XCD partials in XCD order -> g (granules) + f64 sum of squares ----
     double sq = 0.0;
-    if (nc > 0) {
+    const bool flat_b = !two_level && G * nc <= 256 * kBF;
+    if (nc > 0 && flat_b) {
+      const bool bad = gather_rows(rows_r, G, nc, [&](int r) {
+        return (uint32_t)(((size_t)r * NP2 + c0) * 16);
+      }, tag);
+      if (__syncthreads_or(bad)) return;
+      for (int c = tid; c < nc; c += 256) {
+        double t0 = 0.0, t1 = 0.0;
+        for (int r = 0; r < G; ++r) {
+          t0 += (double)scr[2 * (r * nc + c)];
+          t1 += (double)scr[2 * (r * nc + c) + 1];
+        }
+        const float g0 = (float)t0, g1 = (float)t1;
+        const int cc = c0 + c;
+        st_gran2(g_r, (uint32_t)(16 * cc), g0, g1, tag, true);
+        if (p.grad_out && k == K - 1) {
+          if (2 * cc < P) p.grad_out[2 * cc] = g0;
+          if (2 * cc + 1 < P) p.grad_out[2 * cc + 1] = g1;
+        }
+        sq += (double)g0 * (double)g0 + (double)g1 * (double)g1;
+      }
+    }
+    if (nc > 0 && !flat_b) {
       const int SRC = two_level ? kXcds : G;  // sources summed per column
       const int ncol = min(nc, 256), RG = min(SRC, 256 / ncol);
       const int rg = tid / ncol, cq = tid - rg * ncol;
@@ -619,24 +730,53 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
     if (lane == 0) U.wsum[w] = sq;
     __syncthreads();
     if (tid == 0)
-      st_gran_f64(sq_r, (uint32_t)(16 * b), (U.wsum[0] + U.wsum[1]) + (U.wsum[2] + U.wsum[3]), tag);
+      st_gran_f64(g_r, sq0 + (uint32_t)(16 * b), (U.wsum[0] + U.wsum[1]) + (U.wsum[2] + U.wsum[3]),
+                  tag);
     XA_STAMP(40);
 
-    // ---- C: the g slice of this thread's parameters and the G norm partials (granules),
-    // global norm (identical in every wave of every block), clip + Keras Adam ----
+    // ---- C: the g slice of this thread's parameters and the G norm partials (granules of
+    // one buffer, one poll), global norm (identical in every wave of every block), clip +
+    // Keras Adam ----
     float gw[16], gr[RPT];
+    double tot = 0.0;
     bool bad = false;
     {
-      constexpr int NG = 8 + RPT;
-      uint32_t off[NG];
-      f32x4v x[NG];
+      constexpr int NG = 8 + RPT, NQ = 4;  // g slice pairs; norm partials per lane (G <= 256)
+      uint32_t off[NG + NQ];
+      f32x4v x[NG + NQ];
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr)
 #pragma unroll
         for (int h = 0; h < 2; ++h) off[2 * rr + h] = (uint32_t)((ps.w2_off(rr) / 2 + h) * 16);
 #pragma unroll
       for (int q = 0; q < RPT; ++q) off[8 + q] = (uint32_t)((ps.ri[q] >= 0 ? ps.ri[q] / 2 : 0) * 16);
-      bad = !poll_gran<NG>(g_r, off, NG, tag, x, ws.ctl, epoch, p.status);
+      int n = NG;  // lanes past G poll fewer norm partials (valid ones first)
+#pragma unroll
+      for (int u = 0; u < NQ; ++u) {
+        const int gi = u * 64 + lane;
+        off[NG + u] = gi < G ? sq0 + (uint32_t)(16 * gi) : 0u;
+        n += gi < G;
+      }
+      if (G <= 32) {
+        // few blocks: one round trip for both
+        bad = !poll_gran<NG + NQ>(g_r, off, n, tag, x, ws.ctl, epoch, p.status);
+      } else {
+        // many blocks: the g slice, then the norm partials (a failed poll re-reads only
+        // its own granules)
+        uint32_t offg[NG], offq[NQ];
+        f32x4v xg[NG], xq[NQ];
+#pragma unroll
+        for (int u = 0; u < NG; ++u) offg[u] = off[u];
+#pragma unroll
+        for (int u = 0; u < NQ; ++u) offq[u] = off[NG + u];
+        bad = !poll_gran<NG>(g_r, offg, NG, tag, xg, ws.ctl, epoch, p.status);
+        if (!bad) bad = !poll_gran<NQ>(g_r, offq, n - NG, tag, xq, ws.ctl, epoch, p.status);
+#pragma unroll
+        for (int u = 0; u < NG; ++u) x[u] = xg[u];
+#pragma unroll
+        for (int u = 0; u < NQ; ++u) x[NG + u] = xq[u];
+      }
+      XA_STAMP(46);
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
         gw[4 * rr] = x[2 * rr][0];
@@ -647,28 +787,15 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
 #pragma unroll
       for (int q = 0; q < RPT; ++q)
         gr[q] = ps.ri[q] >= 0 ? ((ps.ri[q] & 1) ? x[8 + q][2] : x[8 + q][0]) : 0.0f;
-    }
-    double tot = 0.0;
-    for (int gi0 = 0; gi0 < G && !bad; gi0 += 64 * 4) {
-      uint32_t off[4];
-      f32x4v x[4];
-      int n = 0;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int gi = gi0 + u * 64 + lane;
-        off[u] = gi < G ? (uint32_t)(16 * gi) : 0u;
-        n += gi < G;
-      }
-      // lanes past G poll nothing (n counts this lane's valid granules in order)
-      bad = !poll_gran<4>(sq_r, off, n, tag, x, ws.ctl, epoch, p.status);
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (u < n) tot += gran_f64(x[u]);
+      for (int u = 0; u < NQ; ++u)
+        if (NG + u < n) tot += gran_f64(x[NG + u]);
     }
     if (__syncthreads_or(bad)) return;
+    XA_STAMP(47);
     tot = xa_wave_sum_f64(tot);
     const float sc = clip_scale(tot, p.adam.clip_norm);
-    const float alpha = adam_alpha(p.adam.lr, p.adam.beta1, p.adam.beta2, t0 + k + 1);
+    const float alpha = U.alpha[k];
 #pragma unroll
     for (int i = 0; i < 16; ++i) adam_elem(gw[i] * sc, wv[i], mw[i], vw[i], alpha, omb1, omb2, p.adam.eps);
 #pragma unroll
@@ -726,7 +853,7 @@ int launch(const XaPpoUpdateArgs* a, int G, int K, int n_mb, hipStream_t s) {
 }  // namespace
 
 extern "C" int xa_ppo_update_blocks(int obs_dim, int n_actions, int mb_size) {
-  const int cap = capacity_for(obs_dim, n_actions);
+  const int cap = min(capacity_for(obs_dim, n_actions), 256);  // one block per thread in phase C
   if (cap <= 0 || mb_size <= 0) return 0;
   const int tiles = (mb_size + S - 1) / S;
   return tiles < cap ? tiles : cap;
@@ -755,7 +882,7 @@ extern "C" int xa_ppo_update(const XaPpoUpdateArgs* a, void* stream) {
                a->obs_dim, a->n_actions);
   XA_CHECK_ARG(cap > 0, "xa_ppo_update: could not query the resident capacity");
   const int G = a->n_blocks;
-  XA_CHECK_ARG(G > 0 && G <= cap && G <= (a->mb_size + S - 1) / S,
+  XA_CHECK_ARG(G > 0 && G <= cap && G <= 256 && G <= (a->mb_size + S - 1) / S,
                "xa_ppo_update: n_blocks %d must be in [1, min(resident capacity %d, tiles per "
                "minibatch)] (xa_ppo_update_blocks)", G, cap);
   const size_t need = ws_bytes(G, offs(a->obs_dim, a->n_actions).P, K);
