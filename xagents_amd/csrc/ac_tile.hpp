@@ -213,10 +213,46 @@ struct NoStamp {
   XA_DEV void operator()(int) const {}
 };
 
+// Where a tile's per-sample inputs come from: the TileLds staging arrays, or packed LDS
+// records {obs[OBS], action (< 0: padding, obs zero), return, old value, old log-prob}.
+template <int OBS, int A>
+struct StagedIn {
+  const TileLds<OBS, A>& L;
+  XA_DEV float x(int s, int k) const { return L.sX[s * OBS + k]; }
+  XA_DEV bool valid(int s) const { return L.sValid[s] != 0; }
+  XA_DEV float act(int s) const { return L.sAct[s]; }
+  XA_DEV float ret(int s) const { return L.sRet[s]; }
+  XA_DEV float oldv(int s) const { return L.sOldV[s]; }
+  XA_DEV float oldlp(int s) const { return L.sOldLp[s]; }
+  XA_DEV float advin(int s) const { return L.sAdvIn[s]; }
+};
+template <int OBS>
+struct PackedIn {
+  static constexpr int R = OBS + 4;
+  const float* rec;  // [S][R]
+  XA_DEV float x(int s, int k) const { return rec[s * R + k]; }
+  XA_DEV bool valid(int s) const { return rec[s * R + OBS] >= 0.0f; }
+  XA_DEV float act(int s) const { return rec[s * R + OBS]; }
+  XA_DEV float ret(int s) const { return rec[s * R + OBS + 1]; }
+  XA_DEV float oldv(int s) const { return rec[s * R + OBS + 2]; }
+  XA_DEV float oldlp(int s) const { return rec[s * R + OBS + 3]; }
+  XA_DEV float advin(int) const { return 0.0f; }
+};
+
 // Forward + loss + backward; stamp(slot) marks the phase ends (diagnostic builds).
+template <int OBS, int A, class Stamp, class In>
+XA_DEV void tile_compute(TileLds<OBS, A>& L, TileAcc<OBS, A>& acc, const LossCfg& cfg,
+                         Stamp stamp, const In& in);
+
 template <int OBS, int A, class Stamp = NoStamp>
 XA_DEV void tile_compute(TileLds<OBS, A>& L, TileAcc<OBS, A>& acc, const LossCfg& cfg,
                          Stamp stamp = Stamp()) {
+  tile_compute<OBS, A>(L, acc, cfg, stamp, StagedIn<OBS, A>{L});
+}
+
+template <int OBS, int A, class Stamp, class In>
+XA_DEV void tile_compute(TileLds<OBS, A>& L, TileAcc<OBS, A>& acc, const LossCfg& cfg,
+                         Stamp stamp, const In& in) {
   constexpr int AH = A + 1;
   const int tid = threadIdx.x;
   const int w = tid >> 6, lane = tid & 63;
@@ -230,7 +266,7 @@ XA_DEV void tile_compute(TileLds<OBS, A>& L, TileAcc<OBS, A>& acc, const LossCfg
       const int s = c8 + ss;
       float z = 0.0f;
 #pragma unroll
-      for (int k = 0; k < OBS; ++k) z = fmaf(L.sX[s * OBS + k], L.sW1[k * H + f], z);
+      for (int k = 0; k < OBS; ++k) z = fmaf(in.x(s, k), L.sW1[k * H + f], z);
       hv[ss] = ftanh(z + L.sb1[f]);
       L.sH1[s * LDW + f] = hv[ss];
     }
@@ -285,8 +321,8 @@ XA_DEV void tile_compute(TileLds<OBS, A>& L, TileAcc<OBS, A>& acc, const LossCfg
       float dz[AH];
 #pragma unroll
       for (int a = 0; a < AH; ++a) dz[a] = 0.0f;
-      if (L.sValid[s]) {
-        const int act = (int)L.sAct[s];
+      if (in.valid(s)) {
+        const int act = (int)in.act(s);
         float m = z[0];
 #pragma unroll
         for (int a = 1; a < A; ++a) m = fmaxf(m, z[a]);
@@ -306,15 +342,15 @@ XA_DEV void tile_compute(TileLds<OBS, A>& L, TileAcc<OBS, A>& acc, const LossCfg
           if (a == act) logp = lp[a];
         }
         const float v = z[A];
-        const float R = L.sRet[s];
-        const float oldv = L.sOldV[s];
+        const float R = in.ret(s);
+        const float oldv = in.oldv(s);
         const float adv_raw = R - oldv;
         const float sc = cfg.loss_scale;
         float dlogp, dv, pg, vl;
         if (cfg.is_ppo) {
           const float adv =
-              cfg.has_adv_in ? L.sAdvIn[s] : (adv_raw - cfg.adv_mean) * cfg.adv_rstd;
-          const float ratio = fexp(logp - L.sOldLp[s]);
+              cfg.has_adv_in ? in.advin(s) : (adv_raw - cfg.adv_mean) * cfg.adv_rstd;
+          const float ratio = fexp(logp - in.oldlp(s));
           const float c = cfg.clip_norm;
           const float pg1 = -adv * ratio;
           const float pg2 = -adv * fminf(fmaxf(ratio, 1.0f - c), 1.0f + c);
@@ -433,7 +469,7 @@ XA_DEV void tile_compute(TileLds<OBS, A>& L, TileAcc<OBS, A>& acc, const LossCfg
     const float d = L.sH2[s * LDW + f];
     acc.gb1 = acc.gb1 + d;
 #pragma unroll
-    for (int k = 0; k < OBS; ++k) acc.gW1[k] = fmaf(L.sX[s * OBS + k], d, acc.gW1[k]);
+    for (int k = 0; k < OBS; ++k) acc.gW1[k] = fmaf(in.x(s, k), d, acc.gW1[k]);
   }
   stamp(55);
 }

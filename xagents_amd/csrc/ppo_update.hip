@@ -336,7 +336,11 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
       const bool valid = j < mine * S && q < cnt;
       float* slot = &U.pre[((size_t)k * TPB * S + j) * (OBS + 4)];
       if (!valid) {
-        if (pre) slot[OBS] = -1.0f;  // padding
+        if (pre) {  // padding: zero inputs (they meet zero gradients, never NaNs)
+#pragma unroll
+          for (int kk = 0; kk < OBS + 4; ++kk) slot[kk] = 0.0f;
+          slot[OBS] = -1.0f;
+        }
         continue;
       }
       const int idx = shuf_index(p.shuffle, keys, e, B, start + q);
@@ -519,19 +523,16 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
     XA_STAMP(34);
     // ---- A: forward + loss + backward of this block's tiles ----
     for (int tile = b; tile < n_tiles; tile += G) {
+      if (pre) {
+        // inputs straight from the phase-0 records (read-only: no staging, no barrier)
+        XA_STAMP(35);
+        const PackedIn<OBS> in{&U.pre[((size_t)k * TPB * S + ((tile - b) / G) * S) * (OBS + 4)]};
+        tile_compute<OBS, A>(L, acc, cfg, [&](int slot) { XA_STAMP(slot); }, in);
+        XA_STAMP(36);
+        continue;
+      }
       __syncthreads();
-      if (tid < S && pre) {
-        const float* slot = &U.pre[((size_t)k * TPB * S + ((tile - b) / G) * S + tid) * (OBS + 4)];
-        const float act = slot[OBS];
-        L.sValid[tid] = act >= 0.0f;
-#pragma unroll
-        for (int kk = 0; kk < OBS; ++kk) L.sX[tid * OBS + kk] = act >= 0.0f ? slot[kk] : 0.0f;
-        L.sAct[tid] = act >= 0.0f ? act : 0.0f;
-        L.sRet[tid] = act >= 0.0f ? slot[OBS + 1] : 0.0f;
-        L.sOldV[tid] = act >= 0.0f ? slot[OBS + 2] : 0.0f;
-        L.sOldLp[tid] = act >= 0.0f ? slot[OBS + 3] : 0.0f;
-        L.sAdvIn[tid] = 0.0f;
-      } else if (tid < S) {
+      if (tid < S) {
         L.sValid[tid] = n_valid;
 #pragma unroll
         for (int kk = 0; kk < OBS; ++kk) L.sX[tid * OBS + kk] = nx[kk];
@@ -547,7 +548,9 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
       tile_compute<OBS, A>(L, acc, cfg, [&](int slot) { XA_STAMP(slot); });
       XA_STAMP(36);
     }
-    // ---- the block's gradient row, staged in LDS, published as granule pairs ----
+    // ---- the block's gradient row, staged in LDS, published as granule pairs (measured:
+    // storing W2's pairs straight from the MFMA accumulators with a lane swap was slower,
+    // the write-through stores then stall the combine below) ----
     tile_write_row<OBS, A>(L, acc, [&](int i, float v) { srow[i] = v; });
     XA_STAMP(44);
     if (p.loss_out) {
