@@ -94,9 +94,13 @@ def forward(layers, theta, x, input_shape):
     return x, outs
 
 
-def backward(layers, theta, x_in, outs, d_outputs, want_input_grad=False):
+def backward(layers, theta, x_in, outs, d_outputs, want_input_grad=False, abs_terms=None,
+             d_layers=None):
     """d_outputs: {layer index: d(loss)/d(layer output)} for the output layers.
-    Returns the flat gradient, and d(loss)/d(input) too when want_input_grad."""
+    Returns the flat gradient, and d(loss)/d(input) too when want_input_grad.
+    abs_terms: an optional [P] array that receives, per parameter, the sum of the absolute
+    values of the terms its gradient sums (|x|^T |dz|, sum |dz|) -- the scale of the
+    rounding error an f32 reduction of those terms can carry when they cancel."""
     sls, P = param_slices(layers)
     grad = np.zeros(P)
     B = x_in.shape[0]
@@ -106,6 +110,8 @@ def backward(layers, theta, x_in, outs, d_outputs, want_input_grad=False):
         if i not in dys:
             continue
         l = layers[i]
+        if d_layers is not None:  # d(loss)/d(output) of every layer, for diagnostics
+            d_layers[i] = dys[i]
         src = x_in if l.input_index == -1 else outs[l.input_index]
         if l.kind == 'flatten':
             dsrc = dys[i].reshape(src.shape)
@@ -116,6 +122,9 @@ def backward(layers, theta, x_in, outs, d_outputs, want_input_grad=False):
             (o1, s1), (o2, s2) = sls[i]
             grad[o1:o1 + W.size] += (xs.T @ dz).ravel()
             grad[o2:o2 + s2[0]] += dz.sum(0)
+            if abs_terms is not None:
+                abs_terms[o1:o1 + W.size] += (np.abs(xs).T @ np.abs(dz)).ravel()
+                abs_terms[o2:o2 + s2[0]] += np.abs(dz).sum(0)
             dsrc = (dz @ W.T).reshape(src.shape)
         else:
             W, _ = _weights(theta, sls[i])
@@ -129,6 +138,9 @@ def backward(layers, theta, x_in, outs, d_outputs, want_input_grad=False):
             (o1, s1), (o2, s2) = sls[i]
             grad[o1:o1 + W.size] += (cols.T @ dz2).ravel()
             grad[o2:o2 + s2[0]] += dz2.sum(0)
+            if abs_terms is not None:
+                abs_terms[o1:o1 + W.size] += (np.abs(cols).T @ np.abs(dz2)).ravel()
+                abs_terms[o2:o2 + s2[0]] += np.abs(dz2).sum(0)
             dcol = (dz2 @ W.reshape(k * C, l.filters).T).reshape(R, Pn, k, C)
             dsrc = np.zeros((R, Win, C))
             for p in range(Pn):
@@ -140,3 +152,31 @@ def backward(layers, theta, x_in, outs, d_outputs, want_input_grad=False):
         else:
             dx = dsrc if dx is None else dx + dsrc
     return (grad, dx) if want_input_grad else grad
+
+
+def adopt_gates(layers, outs, device_outs, tol=1e-5):
+    """Return a copy of the f64 layer outputs whose ReLU gates follow the device's f32
+    forward (device_outs: {layer: array}), and the number of gates that differed. An
+    f32 and an f64 forward disagree on a gate only where the pre-activation is ~0; each
+    such flip moves one gradient element by its full value, so backward parity is checked
+    with the device's own gates. Asserts that every flip sits within tol x the layer's
+    largest output of zero."""
+    outs = list(outs)
+    flips = 0
+    for i, l in enumerate(layers):
+        if getattr(l, 'activation', None) != 'relu' or i not in device_outs:
+            continue
+        dev = np.asarray(device_outs[i]).reshape(outs[i].shape) > 0
+        ref = outs[i] > 0
+        bad = dev != ref
+        if bad.any():
+            scale = np.abs(outs[i]).max()
+            assert (np.abs(np.asarray(device_outs[i], np.float64).reshape(outs[i].shape))[bad]
+                    <= tol * scale).all(), f'layer {i}: a gate differs away from zero'
+            flips += int(bad.sum())
+            o = outs[i].copy()
+            o[bad & dev] = np.finfo(np.float64).tiny
+            o[bad & ~dev] = 0.0
+            outs[i] = o
+    return outs, flips
+

@@ -154,7 +154,9 @@ def test_acer_train_steps_with_replay(device):
     torch.cuda.synchronize()
     assert agent.steps == 5 * 4 * 6
     np.random.seed(1)
-    expected = 5 + sum(np.random.poisson(3) for _ in range(4))  # replays from step 2 on
+    # replays from step 2 on; the count is drawn once per run (the reference draws it
+    # while tracing its tf.function train_step, acer/agent.py:376-380)
+    expected = 5 + 4 * np.random.poisson(3)
     assert int(agent.model.optimizer.iterations.item()) == expected
     assert np.isfinite(agent.model.theta.cpu().numpy()).all()
     # a gathered batch holds each env's sampled trajectory

@@ -78,6 +78,29 @@ def test_gemm_transposes_gate_beta_u8(device, M, N, K):
     _close(out.cpu().numpy(), cols @ Wt)
 
 
+@pytest.mark.parametrize('M', [4, 64, 336])
+def test_gemm_dense_input_gradient_shape(device, M):
+    """dX = dZ W^T of the 37632 x 512 dense layer (B read k-major), split as the executor
+    splits it, gated; relative to each row's scale."""
+    from xagents_amd.layers import gemm
+    from xagents_amd._lib import load
+    N, K = 37632, 512
+    rng = np.random.default_rng(M)
+    dz = rng.normal(size=(M, K)).astype(np.float32)
+    W = (rng.normal(size=(N, K)) * 0.01).astype(np.float32)   # (in, out) = Keras layout
+    gate = rng.normal(size=(M, N)).astype(np.float32)
+    s = load().xa_gemm_splits(M, N, K)
+    tdz, tw, tg = (torch.from_numpy(x).to(device) for x in (dz, W, gate))
+    C = torch.empty(M, N, device=device)
+    ws = torch.empty(max(s, 1) * M * N + 1, device=device)
+    gemm(M, N, K, tdz.data_ptr(), tw.data_ptr(), C.data_ptr(), a_m=(1, K, 0), b_ks=1,
+         b_ns=K, ldc=N, gate=tg.data_ptr(), ld_gate=N, workspace=ws)
+    ref = (dz.astype(np.float64) @ W.T.astype(np.float64)) * (gate > 0)
+    got = C.cpu().numpy().astype(np.float64)
+    err = np.linalg.norm(got - ref) / np.linalg.norm(ref)
+    assert err < 1e-6, f'splits {s}: relative error {err:.3g}'
+
+
 def _model(cfg, units, input_shape, device, seed=5):
     from xagents_amd.nets import Adam, ModelReader
     return ModelReader(str(cfg), units, input_shape, Adam(), seed=seed,
@@ -86,6 +109,7 @@ def _model(cfg, units, input_shape, device, seed=5):
 
 @pytest.mark.parametrize('cfg,units,shape,B', [
     ('dqn/models/cnn.cfg', [6], (84, 84, 1), 2),
+    ('dqn/models/cnn.cfg', [6], (84, 84, 1), 64),   # C3's batch: dense dX at M = 64
     ('ppo/models/cnn-actor-critic.cfg', [4, 1], (84, 84, 1), 3),
     ('td3/models/ann-actor.cfg', [4], (24,), 9),
     ('td3/models/ann-critic.cfg', [1], (28,), 9),
@@ -211,3 +235,55 @@ def test_conv1d_wgrad_small_vs_f64(device, rows, W, C, k, s, F, u8):
         torch.cuda.synchronize()
         _close(dw.cpu().numpy(), ref_w + (w0 if acc else 0))
         _close(db.cpu().numpy(), ref_b + (b0 if acc else 0))
+
+
+@pytest.mark.parametrize('B,half', [(64, False), (64, True), (4, True)])
+def test_layer_executor_cnn_backward_on_leading_rows(device, B, half):
+    """The DQN learner's pattern (dqn/agent.py: one forward over [s; s'] of 2B rows, the
+    backward over the first B): per-tensor norm-relative error vs float64."""
+    import sys
+    sys.path.insert(0, str(ROOT / 'oracle'))
+    import nets_f64 as O
+    from xagents_amd.layers import LayerExecutor
+    model = _model(ROOT / 'xagents_amd' / 'dqn/models/cnn.cfg', [6], (84, 84, 1), device)
+    rng = np.random.default_rng(5)
+    R = 2 * B if half else B
+    x = rng.integers(0, 256, size=(R, 84, 84, 1), dtype=np.uint8)
+    ex = LayerExecutor(model, R)
+    ex.forward(torch.from_numpy(x).to(device))
+    dq = np.zeros((B, 6), np.float32)
+    dq[np.arange(B), rng.integers(0, 6, size=B)] = rng.normal(size=B).astype(np.float32)
+    grad = torch.zeros(model.n_params, device=device)
+    ex.backward([torch.from_numpy(dq).to(device)], grad, batch=B)
+    theta = model.theta.cpu().numpy()
+    x64, ref_outs = O.forward(model.layers, theta, x[:B], (84, 84, 1))
+    dev = {i: ex.outs[i][:B].cpu().numpy() for i, l in enumerate(model.layers)
+           if l.kind != 'flatten'}
+    ref_outs, flips = O.adopt_gates(model.layers, ref_outs, dev)
+    S = np.zeros(model.n_params)
+    dl = {}
+    ref_g = O.backward(model.layers, theta, x64, ref_outs, {model.outputs[0]: dq}, abs_terms=S,
+                       d_layers=dl)
+    dz_msgs = []
+    for i, l in enumerate(model.layers):
+        if l.kind == 'flatten' or i not in dl or ex.douts[i] is None or i in model.outputs:
+            continue
+        want = dl[i] * (ref_outs[i] > 0)
+        got = ex.douts[i][:B].cpu().numpy().reshape(want.shape)
+        dz_msgs.append(f'dz[{i}] {_rel_err(got, want):.2e} worst@'
+                       f'{np.unravel_index(np.argmax(np.abs(got - want)), want.shape)}')
+    sls, _ = O.param_slices(model.layers)
+    g = grad.cpu().numpy().astype(np.float64)
+    msgs, worst = [], 0.0
+    for sl in sls:
+        for off, s in sl or ():
+            n = int(np.prod(s))
+            d = np.linalg.norm(g[off:off + n] - ref_g[off:off + n])
+            r = d / np.linalg.norm(ref_g[off:off + n])
+            worst = max(worst, r)
+            msgs.append(f'{s}: {r:.2e} (|S|/|g| {np.linalg.norm(S[off:off + n]) / np.linalg.norm(ref_g[off:off + n]):.1f})')
+    assert worst < 1e-4, '; '.join(msgs + dz_msgs + [f'{flips} gate flips'])
+
+
+def _rel_err(got, want):
+    return float(np.linalg.norm(np.asarray(got, np.float64) - want) / np.linalg.norm(want))
