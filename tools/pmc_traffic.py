@@ -67,7 +67,7 @@ def main(out_dir='gpurun_out', *tags):
         new, _ = entries(Path(out_dir) / f'pmc_{tag}_FETCH_SIZE',
                          Path(out_dir) / f'pmc_{tag}_WRITE_SIZE', suffix)
         for v in new.values():
-            v['source'] = f'rocprofv3 --pmc passes {tag} (tools/gpurun_r02n.sh)'
+            v['source'] = f'rocprofv3 --pmc passes {tag} (tools/gpurun_r02n.sh, tools/gpurun_pmc_shapes.sh)'
         res.update(new)
     f_out.parent.mkdir(exist_ok=True)
     f_out.write_text(json.dumps(res, indent=1) + '\n')
