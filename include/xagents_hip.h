@@ -296,11 +296,13 @@ int xa_clip_adam(float* theta, float* adam_m, float* adam_v, const float* grad, 
  * In place on theta / adam_m / adam_v; *adam_step += E*M. One process (no
  * cross-rank exchange inside; data-parallel steps use the chain).
  * n_blocks: xa_ppo_update_blocks(obs_dim, n_actions, mb_size) (every block must be
- * resident at once: the blocks exchange gradient rows inside the launch).
+ * resident at once: the blocks exchange gradient rows inside the launch), at most one
+ * per 16 samples of a minibatch. More blocks than 32-sample tiles select 16-sample
+ * tiles (the default for minibatches of <= 512 samples).
  * workspace: device memory, 256-byte aligned, >= xa_ppo_update_workspace_bytes(...),
- * owned by the caller, ZEROED ONCE at allocation and then reused by every launch (its
- * first 256 bytes are re-zeroed by a memset node in front of each launch; the rest holds
- * tagged exchange words whose tags advance with a launch counter kept in it).
+ * owned by the caller, ZEROED ONCE at allocation and then reused by every launch
+ * (nothing in it is reset between launches: a launch counter kept in it numbers the
+ * launches, and the exchange words carry tags unique per launch and step).
  * loss_out (optional) [E*n_mb, n_blocks, 4]: per-block (pg, value, entropy, count) sums.
  * grad_out (optional) [P]: the last optimizer step's reduced gradient (before the clip).
  * status (optional device int): set to 1 if an in-launch exchange timed out (2 s);

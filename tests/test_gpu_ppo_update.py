@@ -148,11 +148,13 @@ def test_multi_step_ragged_trajectory_vs_f64(device):
     np.testing.assert_array_equal(counts, [198, 198, 198, 6] * E)
 
 
-@pytest.mark.parametrize('B,mb,blocks', [(4096, 1024, (32, 5)), (16384, 8192, (256, 64, 40, 7))])
+@pytest.mark.parametrize('B,mb,blocks', [(4096, 1024, (32, 5)), (16384, 8192, (256, 64, 40, 7)),
+                                         (2048, 512, (16, 32, 23))])
 def test_block_count_changes_only_the_summation_order(device, B, mb, blocks):
     """Fewer resident blocks than tiles: each block walks several tiles. 64 and more
     blocks reduce the gradient rows inside each XCD's L2 first (two-level), fewer in one
-    level. Only the f64 summation order of the gradient changes."""
+    level; more blocks than 32-sample tiles run 16-sample tiles (mb 512: 32 and 23
+    blocks). Only the f32 / f64 summation order of the gradient changes."""
     bufs = _rollout_buffers(B, seed=5)
     theta0 = _theta0(3)
     runs = [run_update(theta0, bufs, mb, 2, n_blocks=g) for g in blocks]

@@ -240,7 +240,9 @@ struct PackedIn {
 };
 
 // Forward + loss + backward; stamp(slot) marks the phase ends (diagnostic builds).
-template <int OBS, int A, class Stamp, class In>
+// TS = samples per tile: S (32), or 16 for small minibatches, where more blocks with half
+// the element-wise work each shorten the latency-bound step (the persistent update).
+template <int OBS, int A, class Stamp, class In, int TS = S>
 XA_DEV void tile_compute(TileLds<OBS, A>& L, TileAcc<OBS, A>& acc, const LossCfg& cfg,
                          Stamp stamp, const In& in);
 
@@ -250,19 +252,22 @@ XA_DEV void tile_compute(TileLds<OBS, A>& L, TileAcc<OBS, A>& acc, const LossCfg
   tile_compute<OBS, A>(L, acc, cfg, stamp, StagedIn<OBS, A>{L});
 }
 
-template <int OBS, int A, class Stamp, class In>
+template <int OBS, int A, class Stamp, class In, int TS>
 XA_DEV void tile_compute(TileLds<OBS, A>& L, TileAcc<OBS, A>& acc, const LossCfg& cfg,
                          Stamp stamp, const In& in) {
+  static_assert(TS == 16 || TS == 32, "tile sizes: 16 or 32 samples");
   constexpr int AH = A + 1;
+  constexpr int SPW = TS / 4;  // samples per wave in the element-wise phases
+  constexpr int KQ = TS / 4;   // dW2: samples per MFMA lane group (K = TS)
   const int tid = threadIdx.x;
   const int w = tid >> 6, lane = tid & 63;
-  const int li = lane & 15, lq = lane >> 4;     // MFMA lane coordinates
-  const int f = tid & 63, c8 = (tid >> 6) * 8;  // element-wise phases: feature, 8-sample chunk
-  // ---- H1 = tanh(X W1 + b1): feature f, samples c8..c8+7 ----
+  const int li = lane & 15, lq = lane >> 4;      // MFMA lane coordinates
+  const int f = tid & 63, c8 = (tid >> 6) * SPW;  // element-wise phases: feature, sample chunk
+  // ---- H1 = tanh(X W1 + b1): feature f, samples c8..c8+SPW-1 ----
   {
-    float hv[8];
+    float hv[SPW];
 #pragma unroll
-    for (int ss = 0; ss < 8; ++ss) {
+    for (int ss = 0; ss < SPW; ++ss) {
       const int s = c8 + ss;
       float z = 0.0f;
 #pragma unroll
@@ -270,8 +275,10 @@ XA_DEV void tile_compute(TileLds<OBS, A>& L, TileAcc<OBS, A>& acc, const LossCfg
       hv[ss] = ftanh(z + L.sb1[f]);
       L.sH1[s * LDW + f] = hv[ss];
     }
-    *reinterpret_cast<float4*>(&L.sH1T[f * LDT + c8]) = make_float4(hv[0], hv[1], hv[2], hv[3]);
-    *reinterpret_cast<float4*>(&L.sH1T[f * LDT + c8 + 4]) = make_float4(hv[4], hv[5], hv[6], hv[7]);
+#pragma unroll
+    for (int q = 0; q < SPW / 4; ++q)
+      *reinterpret_cast<float4*>(&L.sH1T[f * LDT + c8 + 4 * q]) =
+          make_float4(hv[4 * q], hv[4 * q + 1], hv[4 * q + 2], hv[4 * q + 3]);
   }
   __syncthreads();
   stamp(50);
@@ -285,7 +292,7 @@ XA_DEV void tile_compute(TileLds<OBS, A>& L, TileAcc<OBS, A>& acc, const LossCfg
     }
     const float bias = L.sb2[16 * w + li];
 #pragma unroll
-    for (int st = 0; st < 2; ++st) {
+    for (int st = 0; st < TS / 16; ++st) {
       float av[16];
 #pragma unroll
       for (int v4 = 0; v4 < 4; ++v4) {
@@ -302,8 +309,8 @@ XA_DEV void tile_compute(TileLds<OBS, A>& L, TileAcc<OBS, A>& acc, const LossCfg
   }
   __syncthreads();
   stamp(51);
-  // ---- heads + loss + dL/dz: 8 lanes per sample ----
-  {
+  // ---- heads + loss + dL/dz: 8 lanes per sample (threads past TS x 8 idle) ----
+  if (tid < TS * 8) {
     const int s = tid >> 3, pp = tid & 7;
     float z[AH];
 #pragma unroll
@@ -393,9 +400,9 @@ XA_DEV void tile_compute(TileLds<OBS, A>& L, TileAcc<OBS, A>& acc, const LossCfg
   stamp(52);
   // ---- dA2 = (dZ W34^T) * (1 - H2^2); head / b2 partial grads ----
   {
-    float dv8[8];
+    float dv8[SPW];
 #pragma unroll
-    for (int ss = 0; ss < 8; ++ss) {
+    for (int ss = 0; ss < SPW; ++ss) {
       const int s = c8 + ss;
       float dh = 0.0f;
 #pragma unroll
@@ -408,32 +415,36 @@ XA_DEV void tile_compute(TileLds<OBS, A>& L, TileAcc<OBS, A>& acc, const LossCfg
       L.sdA2[s * LDW + f] = d;
       dv8[ss] = d;
     }
-    *reinterpret_cast<float4*>(&L.sdA2T[f * LDT + c8]) = make_float4(dv8[0], dv8[1], dv8[2], dv8[3]);
-    *reinterpret_cast<float4*>(&L.sdA2T[f * LDT + c8 + 4]) = make_float4(dv8[4], dv8[5], dv8[6], dv8[7]);
+#pragma unroll
+    for (int q = 0; q < SPW / 4; ++q)
+      *reinterpret_cast<float4*>(&L.sdA2T[f * LDT + c8 + 4 * q]) =
+          make_float4(dv8[4 * q], dv8[4 * q + 1], dv8[4 * q + 2], dv8[4 * q + 3]);
     if (tid < AH) {
       float t = acc.gb34;
-      for (int s = 0; s < S; ++s) t = t + L.sdZ[s * AH + tid];
+      for (int s = 0; s < TS; ++s) t = t + L.sdZ[s * AH + tid];
       acc.gb34 = t;
     }
   }
   __syncthreads();
   stamp(53);
-  // ---- dW2 += H1^T dA2 (rows 16w.., K = samples 8q+kk) and dH1 = dA2 W2^T ----
+  // ---- dW2 += H1^T dA2 (rows 16w.., K = samples KQ q + kk) and dH1 = dA2 W2^T ----
   {
-    float av[8];
-    {
-      const float4 t0 = *reinterpret_cast<const float4*>(&L.sH1T[(16 * w + li) * LDT + 8 * lq]);
-      const float4 t1 = *reinterpret_cast<const float4*>(&L.sH1T[(16 * w + li) * LDT + 8 * lq + 4]);
-      av[0] = t0.x; av[1] = t0.y; av[2] = t0.z; av[3] = t0.w;
-      av[4] = t1.x; av[5] = t1.y; av[6] = t1.z; av[7] = t1.w;
+    float av[KQ];
+#pragma unroll
+    for (int q = 0; q < KQ / 4; ++q) {
+      const float4 t = *reinterpret_cast<const float4*>(&L.sH1T[(16 * w + li) * LDT + KQ * lq + 4 * q]);
+      av[4 * q] = t.x; av[4 * q + 1] = t.y; av[4 * q + 2] = t.z; av[4 * q + 3] = t.w;
     }
 #pragma unroll
     for (int jt = 0; jt < 4; ++jt) {
-      const float4 t0 = *reinterpret_cast<const float4*>(&L.sdA2T[(16 * jt + li) * LDT + 8 * lq]);
-      const float4 t1 = *reinterpret_cast<const float4*>(&L.sdA2T[(16 * jt + li) * LDT + 8 * lq + 4]);
-      const float bv[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
+      float bv[KQ];
 #pragma unroll
-      for (int kk = 0; kk < 8; ++kk) acc.gW2[jt] = mfma4(av[kk], bv[kk], acc.gW2[jt]);
+      for (int q = 0; q < KQ / 4; ++q) {
+        const float4 t = *reinterpret_cast<const float4*>(&L.sdA2T[(16 * jt + li) * LDT + KQ * lq + 4 * q]);
+        bv[4 * q] = t.x; bv[4 * q + 1] = t.y; bv[4 * q + 2] = t.z; bv[4 * q + 3] = t.w;
+      }
+#pragma unroll
+      for (int kk = 0; kk < KQ; ++kk) acc.gW2[jt] = mfma4(av[kk], bv[kk], acc.gW2[jt]);
     }
     float wv[16];
 #pragma unroll
@@ -442,7 +453,7 @@ XA_DEV void tile_compute(TileLds<OBS, A>& L, TileAcc<OBS, A>& acc, const LossCfg
       wv[4 * v4] = t4.x; wv[4 * v4 + 1] = t4.y; wv[4 * v4 + 2] = t4.z; wv[4 * v4 + 3] = t4.w;
     }
 #pragma unroll
-    for (int st = 0; st < 2; ++st) {
+    for (int st = 0; st < TS / 16; ++st) {
       float dv16[16];
 #pragma unroll
       for (int v4 = 0; v4 < 4; ++v4) {
@@ -464,7 +475,7 @@ XA_DEV void tile_compute(TileLds<OBS, A>& L, TileAcc<OBS, A>& acc, const LossCfg
   stamp(54);
   // ---- dW1 += X^T dA1 ; db1 ----
 #pragma unroll
-  for (int ss = 0; ss < 8; ++ss) {
+  for (int ss = 0; ss < SPW; ++ss) {
     const int s = c8 + ss;
     const float d = L.sH2[s * LDW + f];
     acc.gb1 = acc.gb1 + d;

@@ -288,7 +288,9 @@ XA_DEV bool hop_wait(unsigned* ctl, int which, unsigned target, unsigned epoch, 
   return lds_flag != 0;
 }
 
-template <int OBS, int A>
+// TS = samples per tile (32; 16 when the minibatch has at most 16 tiles of 32: twice the
+// blocks, half the element-wise work per block and step)
+template <int OBS, int A, int TS>
 __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws ws, int K,
                                                           int n_mb) {
   constexpr int RPT = Dims<OBS, A>::RPT;
@@ -318,23 +320,23 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
 
   // ---- phase 0: advantage sums of this block's samples of every minibatch; their
   // inputs into LDS when all of them fit; the Adam step size of every step ----
-  const int n_tiles_max = (min(MB, B) + S - 1) / S;
+  const int n_tiles_max = (min(MB, B) + TS - 1) / TS;
   const int TPB = (n_tiles_max + G - 1) / G;  // tiles per block per step (at most)
-  const bool pre = K * TPB * S <= pre_max<OBS>();
+  const bool pre = K * TPB * TS <= pre_max<OBS>();
   const int t0 = *p.adam_step;
   for (int k = tid; k < K; k += 256)
     U.alpha[k] = adam_alpha(p.adam.lr, p.adam.beta1, p.adam.beta2, t0 + k + 1);
   for (int k = w; k < K; k += 4) {
     const int e = k / n_mb, m = k - e * n_mb;
     const int start = m * MB, cnt = min(MB, B - start);
-    const int n_tiles = (cnt + S - 1) / S;
+    const int n_tiles = (cnt + TS - 1) / TS;
     const ShufKeys keys = shuf_keys(p.shuffle, ctr, e, B);
     const int mine = n_tiles > b ? (n_tiles - b + G - 1) / G : 0;  // tiles of this block
     double s1 = 0.0, s2 = 0.0;
-    for (int j = lane; j < (pre ? TPB : mine) * S; j += 64) {
-      const int q = (b + (j / S) * G) * S + (j % S);
-      const bool valid = j < mine * S && q < cnt;
-      float* slot = &U.pre[((size_t)k * TPB * S + j) * (OBS + 4)];
+    for (int j = lane; j < (pre ? TPB : mine) * TS; j += 64) {
+      const int q = (b + (j / TS) * G) * TS + (j % TS);
+      const bool valid = j < mine * TS && q < cnt;
+      float* slot = &U.pre[((size_t)k * TPB * TS + j) * (OBS + 4)];
       if (!valid) {
         if (pre) {  // padding: zero inputs (they meet zero gradients, never NaNs)
 #pragma unroll
@@ -427,18 +429,18 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
     }
   }
 
-  // per-sample inputs of the next tile (threads < S), fetched one tile ahead -- across
+  // per-sample inputs of the next tile (threads < TS), fetched one tile ahead -- across
   // minibatch boundaries too: they do not depend on the parameters. The next step's
   // first tile is fetched between the row hop's signal and wait (off the critical path).
   float nx[OBS], n_act = 0.0f, n_ret = 0.0f, n_oldv = 0.0f, n_oldlp = 0.0f;
   int n_valid = 0;
   auto fetch_tile = [&](int k, int tile) {
-    if (pre || tid >= S) return;
+    if (pre || tid >= TS) return;
     long idx = -1;
     if (k < K) {
       const int e = k / n_mb, m = k - e * n_mb;
       const int start = m * MB, cnt = min(MB, B - start);
-      const int q = tile * S + tid;
+      const int q = tile * TS + tid;
       if (q < cnt) {
         const ShufKeys keys = shuf_keys(p.shuffle, ctr, e, B);
         idx = shuf_index(p.shuffle, keys, e, B, start + q);
@@ -509,10 +511,12 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
   };
 
   TileAcc<OBS, A> acc;
+  auto stampf = [&](int slot) { XA_STAMP(slot); };
+  (void)stampf;
   for (int k = 0; k < K; ++k) {
     const int m = k % n_mb;
     const int cnt = min(MB, B - m * MB);
-    const int n_tiles = (cnt + S - 1) / S;
+    const int n_tiles = (cnt + TS - 1) / TS;
     const unsigned tag = tag_of(k);
     __syncthreads();  // U.stat, the LDS weights of the previous step
     cfg.adv_mean = U.stat[k][0];
@@ -526,13 +530,13 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
       if (pre) {
         // inputs straight from the phase-0 records (read-only: no staging, no barrier)
         XA_STAMP(35);
-        const PackedIn<OBS> in{&U.pre[((size_t)k * TPB * S + ((tile - b) / G) * S) * (OBS + 4)]};
-        tile_compute<OBS, A>(L, acc, cfg, [&](int slot) { XA_STAMP(slot); }, in);
+        const PackedIn<OBS> in{&U.pre[((size_t)k * TPB * TS + ((tile - b) / G) * TS) * (OBS + 4)]};
+        tile_compute<OBS, A, decltype(stampf), PackedIn<OBS>, TS>(L, acc, cfg, stampf, in);
         XA_STAMP(36);
         continue;
       }
       __syncthreads();
-      if (tid < S) {
+      if (tid < TS) {
         L.sValid[tid] = n_valid;
 #pragma unroll
         for (int kk = 0; kk < OBS; ++kk) L.sX[tid * OBS + kk] = nx[kk];
@@ -545,7 +549,8 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
       if (tile + G < n_tiles) fetch_tile(k, tile + G);
       __syncthreads();
       XA_STAMP(35);
-      tile_compute<OBS, A>(L, acc, cfg, [&](int slot) { XA_STAMP(slot); });
+      tile_compute<OBS, A, decltype(stampf), StagedIn<OBS, A>, TS>(L, acc, cfg, stampf,
+                                                                 StagedIn<OBS, A>{L});
       XA_STAMP(36);
     }
     // ---- the block's gradient row, staged in LDS, published as granule pairs (measured:
@@ -828,7 +833,7 @@ int capacity() {
     int cus = 0, occ = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       return 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, ppo_update_kernel<OBS, A>, 256, 0) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, ppo_update_kernel<OBS, A, S>, 256, 0) !=
         hipSuccess)
       return 0;
     cap[dev] = cus * occ;
@@ -844,11 +849,18 @@ int capacity_for(int obs_dim, int n_actions) {
   return -1;
 }
 
+// samples per tile: 16 when there are more blocks than 32-sample tiles of a minibatch
+// (xa_ppo_update_blocks picks that for minibatches of <= 16 such tiles), else 32
+int tile_samples(int mb_size, int G) { return G > (mb_size + S - 1) / S ? 16 : S; }
+
 template <int OBS, int A>
 int launch(const XaPpoUpdateArgs* a, int G, int K, int n_mb, hipStream_t s) {
   const int P = offs(OBS, A).P;
   const Ws ws = carve(a->workspace, G, P, K);
-  hipLaunchKernelGGL((ppo_update_kernel<OBS, A>), dim3(G), dim3(256), 0, s, *a, ws, K, n_mb);
+  if (tile_samples(a->mb_size, G) == 16)
+    hipLaunchKernelGGL((ppo_update_kernel<OBS, A, 16>), dim3(G), dim3(256), 0, s, *a, ws, K, n_mb);
+  else
+    hipLaunchKernelGGL((ppo_update_kernel<OBS, A, S>), dim3(G), dim3(256), 0, s, *a, ws, K, n_mb);
   XA_CHECK_LAUNCH("xa_ppo_update");
   return 0;
 }
@@ -859,6 +871,10 @@ extern "C" int xa_ppo_update_blocks(int obs_dim, int n_actions, int mb_size) {
   const int cap = min(capacity_for(obs_dim, n_actions), 256);  // one block per thread in phase C
   if (cap <= 0 || mb_size <= 0) return 0;
   const int tiles = (mb_size + S - 1) / S;
+  // small minibatches (<= 16 tiles of 32): 16-sample tiles on twice the blocks -- the step
+  // is latency-bound, and the element-wise tile phases halve
+  const int tiles16 = (mb_size + 15) / 16;
+  if (tiles <= 16 && tiles16 <= cap) return tiles16;
   return tiles < cap ? tiles : cap;
 }
 
@@ -885,9 +901,9 @@ extern "C" int xa_ppo_update(const XaPpoUpdateArgs* a, void* stream) {
                a->obs_dim, a->n_actions);
   XA_CHECK_ARG(cap > 0, "xa_ppo_update: could not query the resident capacity");
   const int G = a->n_blocks;
-  XA_CHECK_ARG(G > 0 && G <= cap && G <= 256 && G <= (a->mb_size + S - 1) / S,
-               "xa_ppo_update: n_blocks %d must be in [1, min(resident capacity %d, tiles per "
-               "minibatch)] (xa_ppo_update_blocks)", G, cap);
+  XA_CHECK_ARG(G > 0 && G <= cap && G <= 256 && G <= (a->mb_size + 15) / 16,
+               "xa_ppo_update: n_blocks %d must be in [1, min(resident capacity %d, 16-sample "
+               "tiles per minibatch)] (xa_ppo_update_blocks)", G, cap);
   const size_t need = ws_bytes(G, offs(a->obs_dim, a->n_actions).P, K);
   XA_CHECK_ARG(a->workspace_bytes >= need, "xa_ppo_update: workspace %zu bytes < %zu needed",
                a->workspace_bytes, need);
