@@ -140,6 +140,16 @@ XA_DEV bool poll_gran(__amdgpu_buffer_rsrc_t r, const uint32_t (&off)[N], int n,
   }
 }
 
+// Keras ApplyAdam element (xa_adam.hpp adam_elem) with sqrt and the division on the
+// hardware units (v_sqrt_f32, v_rcp_f32 + one Newton step): the update is checked
+// against float64 with a tolerance, and this runs for every parameter in every block
+XA_DEV void adam_fast(float g, float& th, float& m, float& v, float alpha, float omb1,
+                      float omb2, float eps) {
+  m = m + (g - m) * omb1;
+  v = v + (g * g - v) * omb2;
+  th = th - (m * alpha) * frcp(__builtin_amdgcn_sqrtf(v) + eps);
+}
+
 // this workgroup's XCD (MI355X_MICROARCH.md: read placement from HW_REG_XCC_ID)
 XA_DEV int xcc_id() {
   unsigned x;
@@ -648,11 +658,34 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
         return (uint32_t)(((size_t)r * NP2 + c0) * 16);
       }, tag);
       if (__syncthreads_or(bad)) return;
+      // few columns: `parts` threads per column sum interleaved rows, combined in part
+      // order (a shorter dependent f64 chain; fixed order)
+      const int parts = nc <= 128 ? min(4, 256 / nc) : 1;
+      if (parts > 1) {
+        if (tid < parts * nc) {
+          const int part = tid / nc, c = tid - part * nc;
+          double t0 = 0.0, t1 = 0.0;
+          for (int r = part; r < G; r += parts) {
+            t0 += (double)scr[2 * (r * nc + c)];
+            t1 += (double)scr[2 * (r * nc + c) + 1];
+          }
+          U.red[(part * nc + c) * 2] = t0;
+          U.red[(part * nc + c) * 2 + 1] = t1;
+        }
+        __syncthreads();
+      }
       for (int c = tid; c < nc; c += 256) {
         double t0 = 0.0, t1 = 0.0;
-        for (int r = 0; r < G; ++r) {
-          t0 += (double)scr[2 * (r * nc + c)];
-          t1 += (double)scr[2 * (r * nc + c) + 1];
+        if (parts > 1) {
+          for (int part = 0; part < parts; ++part) {
+            t0 += U.red[(part * nc + c) * 2];
+            t1 += U.red[(part * nc + c) * 2 + 1];
+          }
+        } else {
+          for (int r = 0; r < G; ++r) {
+            t0 += (double)scr[2 * (r * nc + c)];
+            t1 += (double)scr[2 * (r * nc + c) + 1];
+          }
         }
         const float g0 = (float)t0, g1 = (float)t1;
         const int cc = c0 + c;
@@ -805,9 +838,9 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
     const float sc = clip_scale(tot, p.adam.clip_norm);
     const float alpha = U.alpha[k];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) adam_elem(gw[i] * sc, wv[i], mw[i], vw[i], alpha, omb1, omb2, p.adam.eps);
+    for (int i = 0; i < 16; ++i) adam_fast(gw[i] * sc, wv[i], mw[i], vw[i], alpha, omb1, omb2, p.adam.eps);
 #pragma unroll
-    for (int q = 0; q < RPT; ++q) adam_elem(gr[q] * sc, rv[q], mr[q], vr[q], alpha, omb1, omb2, p.adam.eps);
+    for (int q = 0; q < RPT; ++q) adam_fast(gr[q] * sc, rv[q], mr[q], vr[q], alpha, omb1, omb2, p.adam.eps);
     ps.to_lds(L, wv, rv);
     XA_STAMP(43);
   }
