@@ -322,7 +322,8 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
   const unsigned epoch = gen + 1u;
 
   // ---- census: which XCD this block runs on (a granule, read after the phase-0 hop) ----
-  const bool two_level = G >= kTwoLevelMinG;
+  // 16-sample tiles run only on small grids (<= 32 blocks): one level, known at compile time
+  const bool two_level = TS == S && G >= kTwoLevelMinG;
   const int xcc = xcc_id();
   const __amdgpu_buffer_rsrc_t cen_r = rsrc(ws.cen_g, (uint32_t)(G * 16));
   if (two_level && tid == 0) st_gran2(cen_r, (uint32_t)(16 * b), __uint_as_float((unsigned)xcc),
