@@ -405,17 +405,22 @@ def bench_ppo(args, world, rank, device, n_envs):
     if transport == 'rccl' and world > 1:
         agent.train_step()  # re-capture on RCCL after a peer-path fallback
     torch.cuda.synchronize()
-    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        agent.fused_train_step(events[k])
+        agent.fused_train_step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    # the rollout / update split: the same K steps again with HIP events between the
+    # phases, outside the timed region (an event record costs ~3 us of stream time)
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    for k in range(args.steps):
+        agent.fused_train_step(events[k])
+    torch.cuda.synchronize()
     # per-kernel durations: HIP events on the launch stream around the rollout and the
     # update launches of 3 eagerly launched train steps right after the timed region
     ktimes = {}

@@ -329,6 +329,8 @@ typedef struct XaPpoUpdateArgs {
   float* grad_out;
   int* status;
   int n_blocks;
+  int bump_counter; /* nonzero: the launch ends with *shuffle.rng_counter += 1 (the
+                       xa_counter_bump that follows the update in a train step) */
 } XaPpoUpdateArgs;
 
 int xa_ppo_update_blocks(int obs_dim, int n_actions, int mb_size);

@@ -149,6 +149,7 @@ class XaPpoUpdateArgs(Structure):
         ('grad_out', c_void_p),
         ('status', c_void_p),
         ('n_blocks', c_int),
+        ('bump_counter', c_int),
     ]
 
 

@@ -94,11 +94,26 @@ class A2C(ExecutorActorCritic, OnPolicy):
         self.b_val = torch.zeros(N, T, **f32)
         self.b_ent = torch.zeros(N, T, **f32)
         self.b_rew = torch.zeros(N, T, **f32)
-        self.b_done = torch.zeros(N, T + 1, **f32)
-        self.b_epret = torch.zeros(N, T, **f32)
+        # done flags, running episode returns and a device status word in ONE buffer, so
+        # the per-step episode statistics leave the device in one D2H copy
+        al = lambda x: (x + 63) // 64 * 64  # noqa: E731  (256-B aligned views)
+        o_ep = al(N * (T + 1))
+        o_st = o_ep + al(N * T)
+        self._stats_pack = torch.zeros(o_st + 64, **f32)
+        self.b_done = self._stats_pack[:N * (T + 1)].view(N, T + 1)
+        self.b_epret = self._stats_pack[o_ep:o_ep + N * T].view(N, T)
+        self._stats_status = self._stats_pack[o_st:o_st + 1].view(torch.int32)
+        self._stats_views = (N * (T + 1), (N, T + 1), o_ep, (N, T), o_st)
         self.b_ret = torch.zeros(N, T, **f32)
         self.next_val = torch.zeros(N, **f32)
         self.rng_counter = torch.zeros(1, dtype=torch.int64, device=dev)
+        self._rollout_ev = None
+        # Episode statistics leave the device after every train step. On the launch stream
+        # (default) they cost ~4 us per copy; on a side stream behind the rollout they
+        # overlap the update (C2: 0.43 -> 0.41 ms per step), but the first copies of a
+        # process's side stream stall the host ~7 ms twice at a random early step
+        # (tools/diag_bench_steps.py), which a 20-step timed loop cannot absorb.
+        self.stats_side_stream = False
         seed = self.seed if self.seed is not None else int(np.random.SeedSequence().entropy % 2**63)
         self.rng_seed = (int(seed) * 1000003 + self.rank * 7919 + 17) % 2**64
         P = self.model.n_params
@@ -264,6 +279,7 @@ class A2C(ExecutorActorCritic, OnPolicy):
         try:
             # park the stream on a spin kernel so the host enqueues the whole step behind
             # it: the event pairs then bracket GPU execution, not host launch gaps
+            self._sync_stats_copy()
             torch.cuda._sleep(20_000_000)
             self._step_impl()
             self.steps += self.n_envs * self.n_steps
@@ -331,22 +347,31 @@ class A2C(ExecutorActorCritic, OnPolicy):
             self.steps += self.n_envs * self.n_steps
             self._queue_episode_stats(self.b_done, self.b_epret)
             return
+        self._sync_stats_copy()
+        if self._rollout_ev is None and self.stats_side_stream:
+            self._rollout_ev = torch.cuda.Event()
         if self.use_graph and self._graph is not None:
             rec(0)
             self._graph[0].replay()
+            if self.stats_side_stream:
+                self._rollout_ev.record()
             rec(1)
             self._graph[1].replay()
             rec(2)
         else:
             rec(0)
             self._rollout_impl()
+            if self.stats_side_stream:
+                self._rollout_ev.record()
             rec(1)
             self._update_impl()
             rec(2)
             if self.use_graph:
                 self._capture()
         self.steps += self.n_envs * self.n_steps
-        self._queue_episode_stats(self.b_done, self.b_epret)
+        # opt-in: the statistics copy overlaps the update (side stream behind the rollout)
+        self._queue_episode_stats(self.b_done, self.b_epret,
+                                  after=self._rollout_ev if self.stats_side_stream else None)
         self._maybe_check_peer()
 
     # every rank reaches the same train-step count, so this collective check lines up
@@ -437,6 +462,7 @@ class A2C(ExecutorActorCritic, OnPolicy):
         saved = a.return_kind
         a.return_kind = return_kind
         try:
+            self._sync_stats_copy()
             kernels.rollout(a)
             kernels.counter_bump(self.rng_counter)
         finally:

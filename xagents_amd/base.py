@@ -15,6 +15,7 @@ import os
 import random
 from abc import ABC
 from collections import deque
+from contextlib import nullcontext as _nullcontext
 from datetime import timedelta
 from pathlib import Path
 from time import perf_counter
@@ -342,32 +343,85 @@ class BaseAgent(ABC):
         return concatenated
 
     # ---- device episode bookkeeping ----------------------------------------
-    def _queue_episode_stats(self, done_out, epret_out):
-        """Async D2H copy of one rollout's done flags [N,T+1] and running returns [N,T]."""
+    def _queue_episode_stats(self, done_out, epret_out, after=None):
+        """Async D2H copy of one rollout's done flags [N,T+1] and running returns [N,T]
+        (with the persistent update's status word). `after`: an event recorded on the
+        launch stream right after the rollout -- the copy then runs on a side stream
+        behind it, overlapping the update, and the next rollout waits for it
+        (_sync_stats_copy)."""
         if self._pending_stats is None or self._pending_stats[0].shape != done_out.shape:
+            self._drain_episode_stats()
             self._host_done = [torch.empty(done_out.shape, dtype=done_out.dtype).pin_memory()
                                for _ in range(2)]
             self._host_epret = [torch.empty(epret_out.shape, dtype=epret_out.dtype).pin_memory()
                                 for _ in range(2)]
+            self._host_pack = None
+            # one completion event per host slot, reused (a slot is re-recorded only after
+            # its previous copy was folded): no event creation on the step path
+            self._stats_events = [torch.cuda.Event(), torch.cuda.Event()]
             self._stats_slot = 0
             self._stats_queue = []
         slot = self._stats_slot
-        self._host_done[slot].copy_(done_out, non_blocking=True)
-        self._host_epret[slot].copy_(epret_out, non_blocking=True)
-        status = getattr(self, 'device_status', None)
-        if status is not None:
-            if getattr(self, '_host_status', None) is None:
-                self._host_status = [torch.zeros(status.shape, dtype=status.dtype).pin_memory()
-                                     for _ in range(2)]
-            self._host_status[slot].copy_(status, non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record()
+        side = None
+        if after is not None:
+            if getattr(self, '_stats_stream', None) is None:
+                self._stats_stream = torch.cuda.Stream(device=done_out.device)
+                self._stats_warm = False
+            side = self._stats_stream
+            side.wait_event(after)
+        with torch.cuda.stream(side) if side is not None else _nullcontext():
+            pack = getattr(self, '_stats_pack', None)
+            # one copy of the whole pack pays off for large rollouts (256 envs: 0.432 vs
+            # 0.439 ms per step); at 16 envs three small copies measured faster (0.323 vs
+            # 0.333 ms; tools/ab_ppo_step.py)
+            if pack is not None and pack.numel() >= 65536 and \
+                    done_out.data_ptr() == self.b_done.data_ptr():
+                # done, episode returns and the status word in one copy (a2c/agent.py)
+                if self._host_pack is None:
+                    nd, sd, oe, se, os_ = self._stats_views
+                    self._host_pack = [torch.zeros(pack.shape, dtype=pack.dtype).pin_memory()
+                                       for _ in range(2)]
+                    self._host_done = [h[:nd].view(sd) for h in self._host_pack]
+                    self._host_epret = [h[oe:oe + se[0] * se[1]].view(se)
+                                        for h in self._host_pack]
+                    self._host_status = [h[os_:os_ + 1].view(torch.int32)
+                                         for h in self._host_pack]
+                if side is not None and not self._stats_warm:
+                    # the first device-to-pinned-host copies of a side stream block the
+                    # host for ~7 ms each (MI355X / ROCm 7.2, tools/diag_d2h_side.py): pay
+                    # them here, once, not inside a later step
+                    for _ in range(4):
+                        for h in self._host_pack:
+                            h.copy_(pack, non_blocking=True)
+                    side.synchronize()
+                    self._stats_warm = True
+                self._host_pack[slot].copy_(pack, non_blocking=True)
+            else:
+                self._host_done[slot].copy_(done_out, non_blocking=True)
+                self._host_epret[slot].copy_(epret_out, non_blocking=True)
+                status = getattr(self, 'device_status', None)
+                if status is not None:
+                    if getattr(self, '_host_status', None) is None:
+                        self._host_status = [torch.zeros(status.shape, dtype=status.dtype)
+                                             .pin_memory() for _ in range(2)]
+                    self._host_status[slot].copy_(status, non_blocking=True)
+            ev = self._stats_events[slot]
+            ev.record()
+        self._stats_guard = ev if side is not None else None
         self._stats_queue.append((slot, ev))
         self._stats_slot ^= 1
         self._pending_stats = (done_out, epret_out)
         # keep at most one rollout in flight: fold the previous one now
         while len(self._stats_queue) > 1:
             self._fold_stats(*self._stats_queue.pop(0))
+
+    def _sync_stats_copy(self):
+        """The launch stream waits for a side-stream statistics copy still reading the
+        rollout buffers (call before every rollout launch)."""
+        ev = getattr(self, '_stats_guard', None)
+        if ev is not None:
+            torch.cuda.current_stream().wait_event(ev)
+            self._stats_guard = None
 
     def _fold_stats(self, slot, ev):
         ev.synchronize()
@@ -391,6 +445,14 @@ class BaseAgent(ABC):
     def _drain_episode_stats(self):
         while getattr(self, '_stats_queue', None):
             self._fold_stats(*self._stats_queue.pop(0))
+        # a side-stream copy reads the status word before the step's update ends: the
+        # last update's status is read here
+        status = getattr(self, 'device_status', None)
+        if status is not None and getattr(self, '_stats_stream', None) is not None and \
+                int(status.max().item()):
+            raise RuntimeError(
+                f'{self.__class__.__name__}: an in-launch exchange of the persistent update '
+                f'timed out (device status word set); the parameters are invalid')
 
     def fit(
         self,

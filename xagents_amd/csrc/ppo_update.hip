@@ -851,6 +851,10 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
     ps.store(p.adam_v, vw, vr);
     if (tid == 0) {
       *p.adam_step = t0 + K;
+      // every block read the counter before its last gradient row, which block 0 has
+      // consumed by now (phase B of the last step)
+      if (p.bump_counter && p.shuffle.rng_counter)
+        *const_cast<uint64_t*>(p.shuffle.rng_counter) = ctr + 1;
       // the next launch's generation, write-through (read at its start on every XCD)
       __hip_atomic_store((gu32*)ws.persist, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }

@@ -153,7 +153,9 @@ class PPO(A2C):
         obs_dim, A = self.model.obs_dim, self.n_actions
         nbytes = kernels.ppo_update_workspace_bytes(obs_dim, A, B, MB, E, n_blocks)
         self.update_ws = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
-        self.device_status = torch.zeros(1, dtype=torch.int32, device=dev)
+        # the status word rides in the packed episode-statistics buffer (one D2H copy)
+        self.device_status = self._stats_status
+        self.device_status.zero_()
         u = XaPpoUpdateArgs()
         u.obs_dim, u.n_actions = obs_dim, A
         u.batch, u.mb_size, u.epochs = B, MB, E
@@ -172,6 +174,8 @@ class PPO(A2C):
         u.loss_out = u.grad_out = None
         u.status = self.device_status.data_ptr()
         u.n_blocks = n_blocks
+        # the Philox counter bump that ends a train step runs in the launch's last block
+        u.bump_counter = int(bool(self.shuffle.rng_counter))
         self._uargs = u
         self.update_mode = 'persistent'
         self.update_blocks = n_blocks
@@ -190,6 +194,11 @@ class PPO(A2C):
         if not self.executor_path:
             self._setup_update()
         self._graph = None
+
+    def _update_impl(self):
+        self._update()
+        if not (self.update_mode == 'persistent' and self._uargs.bump_counter):
+            kernels.counter_bump(self.rng_counter)
 
     def _timed_kernels(self):
         if self.update_mode == 'persistent':
@@ -236,6 +245,7 @@ class PPO(A2C):
         log_probs] exactly as concat_step_batches lays them out
         (xagents/ppo/agent.py:193-213, xagents/base.py:549-564)."""
         a = self._rargs
+        self._sync_stats_copy()
         kernels.rollout(a)
         kernels.counter_bump(self.rng_counter)
         self.steps += self.n_envs * self.n_steps
