@@ -39,7 +39,8 @@ def main():
     from xagents_amd import PPO
     from xagents_amd.envs import ReplayVecEnv
     from xagents_amd.utils.common import create_model
-    envs = ReplayVecEnv('CartPole-v1', 256, t_rec=4096, seed=55, device='cuda')
+    n_envs = next((int(a) for a in sys.argv[1:] if a.isdigit()), 256)
+    envs = ReplayVecEnv('CartPole-v1', n_envs, t_rec=4096, seed=55, device='cuda')
     model = create_model(envs, 'ppo', 'model', seed=55, device='cuda')
     agent = PPO(envs, model, n_steps=128, seed=55, quiet=True, use_graph=False)
     L = _lib._lib
@@ -50,9 +51,9 @@ def main():
         agent.train_step()
     torch.cuda.synchronize()
     for name, slots in (('xa_diag_read_stamps_rollout',
-                         {0: 'loop-top->layer1 (stores/env of prev step)', 1: 'layer1+LDS bcast',
+                         {0: 'loop top', 1: 'layer1+LDS bcast',
                           2: 'layer2+tanh', 3: 'heads (3 wave sums)', 4: 'categorical',
-                          6: 'env step + stores', 5: 'tail'}),
+                          6: 'env step (record readlanes)', 7: 'chunk pass', 5: 'tail'}),
                         ('xa_diag_read_stamps_update',
                          {20: 'prologue: param/grad loads', 21: 'prologue: norm + barrier',
                           22: 'prologue: Adam + LDS stores', 11: 'adv stats + tile-loop barrier',

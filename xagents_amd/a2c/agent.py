@@ -437,6 +437,18 @@ class A2C(ExecutorActorCritic, OnPolicy):
             return
         self.fused_train_step()
 
+    def _play_chunk(self):
+        """play(): one rollout of n_steps with the actor's Categorical / Gaussian samples
+        (the reference's play samples through get_model_outputs, a2c/agent.py:65-94);
+        env 0's rewards and step dones. The rollout's episode statistics are not queued."""
+        self._sync_stats_copy()
+        if self.executor_path:
+            self._executor_rollout()
+        else:
+            kernels.rollout(self._rargs)
+            kernels.counter_bump(self.rng_counter)
+        return self.b_rew[0].cpu().numpy(), self.b_done[0, 1:].cpu().numpy()
+
     # ---- reference-level pieces (composable, not used by the fused step) -----
     def get_model_outputs(self, inputs, models, training=True, actions=None):
         """[actions, log probs, critic output, entropy, actor output]

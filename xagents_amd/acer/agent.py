@@ -230,6 +230,13 @@ class ACER(A2C):
         self.obs_buf[T].copy_(env.state)
         kernels.counter_bump(self.rng_counter)
 
+    def _play_chunk(self):
+        """play(): one eager rollout into the staging buffers (not stored in the ring);
+        env 0's rewards and step dones."""
+        self._sync_stats_copy()
+        self._rollout_kernels()
+        return self.g_rew[0].cpu().numpy(), self.g_done[0].cpu().numpy()
+
     def _acer_rollout(self):
         """One rollout (eager the first time, then a captured hipGraph; envs with a host-side
         pre_step stay eager), stored as this step's trajectory ring slot."""

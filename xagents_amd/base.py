@@ -473,8 +473,42 @@ class BaseAgent(ABC):
             self.at_step_end()
         self._drain_episode_stats()
 
-    def play(self, *args, **kwargs):
-        raise NotImplementedError('play() renders gym frames; no gym in this build')
+    def play(self, video_dir=None, render=False, frame_dir=None, frame_delay=0.0,
+             max_steps=None, action_idx=0, frame_frequency=1):
+        """Play one game of env 0 with the current policy (xagents/base.py:595-653): reset
+        the envs, act with the agent's play policy (A2C / PPO: a Categorical sample of the
+        actor, DQN: argmax Q, DDPG / TD3: the noise-free actor), stop at env 0's first done
+        or after max_steps steps, display the total reward.
+
+        The envs are device envs, stepped together in chunks (_play_chunk); env 0's
+        rewards and dones are read back per chunk and the reference's per-step loop runs
+        over them. Nothing is rendered: video_dir / render / frame_dir need gym's renderer
+        and cv2, which this build has no counterpart of. Training counters (steps, games,
+        total_rewards) are left untouched, as the reference's play leaves them. Returns the
+        total reward (the reference returns None)."""
+        if video_dir or render or frame_dir:
+            raise NotImplementedError(
+                'play(): device envs have no renderer (video_dir / render / frame_dir need '
+                'gym and cv2)')
+        del frame_delay, action_idx, frame_frequency  # rendering / multi-output options
+        self.reset_envs()
+        total_reward, steps = 0.0, 0
+        while True:
+            rewards, dones = self._play_chunk()
+            for r, d in zip(rewards, dones):
+                if max_steps and steps >= max_steps:
+                    self.display_message(f'Maximum steps {max_steps} exceeded')
+                    return total_reward
+                total_reward += float(r)
+                if d:
+                    self.display_message(f'Total reward: {total_reward}')
+                    return total_reward
+                steps += 1
+
+    def _play_chunk(self):
+        """Step every env with the play policy for one or more steps; env 0's rewards and
+        dones (host arrays, one entry per step, in step order)."""
+        raise NotImplementedError(f'play() is not available for {type(self).__name__}')
 
 
 class OnPolicy(BaseAgent, ABC):
@@ -545,6 +579,36 @@ class OffPolicy(BaseAgent, ABC):
         self._st_row += 1
         if self._st_row == self._STATS_ROWS:
             self._flush_offpolicy_stats()
+
+    def _play_actions(self):
+        """Device actions of the play policy for every env (subclasses)."""
+        raise NotImplementedError(f'play() is not available for {type(self).__name__}')
+
+    def _play_chunk(self):
+        """One xa_replay_env_step with the play policy's actions and no replay append;
+        reward / done rows go to play-only buffers, so the training statistics rows and
+        the rings are untouched."""
+        from xagents_amd._lib import XaReplayStepArgs, call, stream
+        import ctypes
+        if getattr(self, '_play_args', None) is None:
+            n = self.n_envs
+            self._play_out = torch.zeros(3, n, dtype=torch.float32, device=self.device)
+            a = XaReplayStepArgs()
+            self.envs.fill_step_args(a)
+            a.ring_states = None
+            o = self._play_out
+            a.out_rewards, a.out_dones = o[0].data_ptr(), o[1].data_ptr()
+            a.done_epret = o[2].data_ptr()
+            self._play_args = a
+        a = self._play_args
+        actions = self._play_actions()
+        a.actions, a.act_bytes = actions.data_ptr(), self.replay.act_bytes
+        pre_step = getattr(self.envs, 'pre_step', None)
+        if pre_step is not None:
+            pre_step()
+        call('xa_replay_env_step', ctypes.byref(a), stream())
+        out = self._play_out[:2, 0].cpu().numpy()
+        return out[:1], out[1:]
 
     def _flush_offpolicy_stats(self):
         rows = self._st_row

@@ -121,6 +121,11 @@ class DDPG(OffPolicy):
         self._noisy(a, self.step_noise_coef, float('inf'), self.step_actions)
         return self.step_actions
 
+    def _play_actions(self):
+        """play(): the actor's output without exploration noise (self.actor(states),
+        xagents/base.py:639-640)."""
+        return self.ex_step.forward(self.envs.state)[0]
+
     def sync_target_models(self):
         """target = (1 - tau) target + tau online, every model group (ddpg/agent.py:73-85)."""
         for model, target in self.model_groups:

@@ -115,6 +115,14 @@ class DQN(OffPolicy):
                  self.actions.data_ptr(), stream())
         return self.actions
 
+    def _play_actions(self):
+        """play(): greedy argmax Q for every env (get_model_outputs(...)[0],
+        xagents/base.py:641-644 with dqn/agent.py:70-84)."""
+        q = self.ex_act.forward(self.envs.state)[0]
+        call('xa_dqn_act', q.data_ptr(), self.n_envs, self.n_actions, None, 0,
+             self.actions.data_ptr(), stream())
+        return self.actions
+
     def concat_buffer_samples(self):
         """One sampled batch gathered from the device rings in the reference's index
         order: [states, actions, rewards, dones, new_states] (base.py:344-368)."""

@@ -198,6 +198,12 @@ class TRPO(PPO):
         self.steps += self.n_envs * self.n_steps
         self._queue_episode_stats(self.b_done, self.b_epret)
 
+    def _play_chunk(self):
+        """play(): one eager rollout (actor samples); env 0's rewards and step dones."""
+        self._sync_stats_copy()
+        self._rollout_kernels()
+        return self.b_rew[0].cpu().numpy(), self.b_done[0, 1:].cpu().numpy()
+
     def _rollout_kernels(self):
         N, T = self.n_envs, self.n_steps
         env, a = self.envs, self._sa
