@@ -374,7 +374,8 @@ typedef struct XaGemmArgs {
   const float* gate;
   int64_t ld_gate;
   int beta;
-  int force_small; /* 1: always the 64 x 64 small-tile kernel (tests) */
+  int force_small; /* 1: always the 64 x 64 small-tile kernel; 2: the generic tile kernels,
+                     never the small-M ones (tests / A-B timing) */
 } XaGemmArgs;
 
 int xa_gemm(const XaGemmArgs* args, void* stream);

@@ -101,6 +101,30 @@ def test_gemm_dense_input_gradient_shape(device, M):
     assert err < 1e-6, f'splits {s}: relative error {err:.3g}'
 
 
+@pytest.mark.parametrize('M,N,K', [(1, 2048, 256), (17, 2050, 768), (64, 4100, 512),
+                                   (100, 2048, 256), (128, 3000, 1024), (200, 2064, 256),
+                                   (384, 2048, 512), (336, 2100, 512), (33, 2048, 128),
+                                   (64, 2064, 256)])
+def test_gemm_small_m_kmajor(device, M, N, K):
+    """The small-M kernel (both operands k-major, dX = dY W^T shapes): ragged M / N, K with
+    and without the 2-wave K split, bias + ReLU, gate and beta accumulation vs float64."""
+    from xagents_amd.layers import gemm
+    from xagents_amd._lib import XA_ACT_RELU
+    rng = np.random.default_rng(M * 7 + K)
+    A = rng.normal(size=(M, K)).astype(np.float32)
+    W = rng.normal(size=(N, K)).astype(np.float32)      # B(k, n) = W[n][k]
+    bias = rng.normal(size=N).astype(np.float32)
+    gate = rng.normal(size=(M, N)).astype(np.float32)
+    C0 = rng.normal(size=(M, N)).astype(np.float32)
+    ta, tw, tb, tg = (torch.from_numpy(x).to(device) for x in (A, W, bias, gate))
+    C = torch.from_numpy(C0.copy()).to(device)
+    gemm(M, N, K, ta.data_ptr(), tw.data_ptr(), C.data_ptr(), a_m=(1, K, 0), b_ks=1, b_ns=K,
+         ldc=N, bias=tb.data_ptr(), act=XA_ACT_RELU, gate=tg.data_ptr(), ld_gate=N, beta=True,
+         splits=1)
+    z = np.maximum(A.astype(np.float64) @ W.T.astype(np.float64) + bias, 0)
+    _close(C.cpu().numpy(), C0 + z * (gate > 0))
+
+
 def _model(cfg, units, input_shape, device, seed=5):
     from xagents_amd.nets import Adam, ModelReader
     return ModelReader(str(cfg), units, input_shape, Adam(), seed=seed,

@@ -20,6 +20,8 @@
 // K in steps of 16 staged through double-buffered LDS. K may be split over
 // blockIdx.z; split partial sums are reduced in fixed order by a second kernel that
 // applies the epilogue (deterministic, no atomics).
+#include <algorithm>
+
 #include "../../include/xagents_hip.h"
 #include "xa_common.hpp"
 
@@ -453,6 +455,138 @@ __global__ __launch_bounds__(256) void gemm_tile_kernel(XaGemmK kargs) {
 }
 
 // ---------------------------------------------------------------------------
+// Small-M path, both operands k-major: C[M, N] = A[M, K] B[K, N] with A(m, k) = a[m lda + k]
+// and B(k, n) = b[n ldb + k] -- the dense layer's input gradient dX = dY W^T at batch
+// M <= 64 (DQN's 64), where 64-row M tiles leave most CUs idle. K = 128 CH.
+// A unit is a strip of 16 columns n x every row m; the wave that owns a unit's K part
+// streams its 16 rows of b along k from HBM straight into MFMA operand registers (lane
+// (q = l >> 4, i = l & 15) loads b[n0 + i][k0 + 4q .. 4q + 3], one float4 that feeds the 4
+// MFMAs of a 16-k step in a permuted k order: no LDS staging, no transpose) and reads A, in
+// the same k order, from LDS, where ALL of A stays resident: no A load sits in the K loop,
+// so nothing queues behind the B prefetches in the in-order memory counter. 512 threads = 8 waves = 2 units x 4 K parts; the grid is
+// persistent (<= one workgroup per CU) and walks rounds of 2 units per workgroup; each
+// wave's B ring holds the next round's CH chunks while it computes this round's. At a
+// round's end the 4 K parts are combined through LDS in part order and wave p finishes m
+// tile p (gate values fetched when the round started, ahead of the prefetches).
+// ---------------------------------------------------------------------------
+constexpr int RS_KP = 4, RS_UPR = 2;
+
+template <int MT, int CH, bool GATE>
+__global__ __launch_bounds__(512) void gemm_smallm_res_kernel(XaGemmArgs g, int rounds) {
+  constexpr int K = 128 * CH, KQ = K / RS_KP, PA = K + 4;
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* As = sm;                       // [MT 16][PA]
+  float* red = sm + MT * 16 * PA;       // [RS_UPR][MT][RS_KP - 1][256] (a tile's own part stays in registers)
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int kp = w % RS_KP, us = w / RS_KP;
+  const int li = lane & 15, lq = lane >> 4;
+  const int M = g.M, N = g.N;
+  const int units = (N + 15) / 16;
+  const float* af = static_cast<const float*>(g.a);
+  for (int sl = tid; sl < MT * 16 * (K / 4); sl += 512) {
+    const int m = sl / (K / 4), q = sl - m * (K / 4);
+    const f32x4 z = {0.0f, 0.0f, 0.0f, 0.0f};
+    *reinterpret_cast<f32x4*>(As + m * PA + 4 * q) =
+        m < M ? *reinterpret_cast<const f32x4*>(af + (int64_t)m * g.a_rm + 4 * q) : z;
+  }
+  auto unit_of = [&](int r) { return (r * (int)gridDim.x + (int)blockIdx.x) * RS_UPR + us; };
+  auto brow = [&](int r) {
+    const int n = min(unit_of(r) * 16 + li, N - 1);
+    return g.b + (int64_t)n * g.b_ns + kp * KQ + 4 * lq;
+  };
+  // B ring over the flattened chunk sequence gi = r CH + c of this wave's rounds: RS_R slots
+  // (two rounds), chunk gi + RS_R - 1 fetched while chunk gi is computed
+  constexpr int RS_R = 2 * CH;
+  f32x4 rb[RS_R][2];
+  auto load_b = [&](int gi, f32x4 (&dst)[2]) {
+    const float* p = brow(gi / CH) + 32 * (gi % CH);
+    dst[0] = *reinterpret_cast<const f32x4*>(p);
+    dst[1] = *reinterpret_cast<const f32x4*>(p + 16);
+  };
+#pragma unroll
+  for (int gi = 0; gi < RS_R - 1; ++gi) load_b(gi, rb[gi]);
+  __syncthreads();
+  const float* as = As + li * PA + kp * KQ + 4 * lq;
+  const int mt_fin = min(kp, MT - 1);  // the m tile this wave finishes (kp < MT)
+  for (int r0 = 0; r0 < rounds; r0 += 2) {
+#pragma unroll
+    for (int par = 0; par < 2; ++par) {
+      const int r = r0 + par;
+      const int unit = unit_of(r);
+      const bool live = unit < units;
+      const int n = unit * 16 + li;
+      float gt[4] = {1.0f, 1.0f, 1.0f, 1.0f};
+      if (GATE) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int m = min(16 * mt_fin + 4 * lq + q, M - 1);
+          gt[q] = g.gate[(int64_t)m * g.ld_gate + min(n, N - 1)];
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      f32x4 acc[MT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int c = 0; c < CH; ++c) {
+        const int u = par * CH + c;  // this chunk's slot
+        // chunk gi + RS_R - 1 (clamped rows past the last round; unused) into the slot
+        // the previous chunk freed
+        load_b(r * CH + c + RS_R - 1, rb[(u + RS_R - 1) % RS_R]);
+        __builtin_amdgcn_sched_barrier(0);
+        if (live) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            f32x4 aq[MT];
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+              aq[mt] = *reinterpret_cast<const f32x4*>(as + mt * 16 * PA + 32 * c + 16 * h);
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+              for (int mt = 0; mt < MT; ++mt)
+                acc[mt] = mfma4(aq[mt][j], rb[u][h][j], acc[mt]);
+          }
+        }
+      }
+      // slot of part p in m tile mt's scratch: p, or p - 1 past the finishing wave mt
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        if (mt == kp) continue;
+        const int slot = kp < mt ? kp : kp - 1;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          red[((us * MT + mt) * (RS_KP - 1) + slot) * 256 + q * 64 + lane] = acc[mt][q];
+      }
+      __syncthreads();
+      if (kp < MT && live && n < N) {
+        f32x4 own = acc[0];
+#pragma unroll
+        for (int mt = 1; mt < MT; ++mt)
+          if (mt == kp) own = acc[mt];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float v = 0.0f;
+#pragma unroll
+          for (int p = 0; p < RS_KP; ++p)
+            v += p == kp ? own[q]
+                         : red[((us * MT + kp) * (RS_KP - 1) + (p < kp ? p : p - 1)) * 256 +
+                               q * 64 + lane];
+          const int m = 16 * kp + 4 * lq + q;
+          if (m < M) {
+            v = epilogue(v, n, g);
+            if (GATE && !(gt[q] > 0.0f)) v = 0.0f;
+            float* cp = g.c + (int64_t)m * g.ldc + n;
+            *cp = g.beta ? *cp + v : v;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Skinny path (weight gradients of the convs: M, N <= 256 / 64, K = rows x positions in
 // the millions): one wave per workgroup owns a 32 x 32 output tile and a K range; the
 // operands come straight from global memory (A rows / B rows are contiguous along m / n
@@ -881,6 +1015,30 @@ void tile_dims(int shape, int& bm, int& bn) {
   else if (shape > 2) bm = 64 * (shape / 10), bn = 64 * (shape % 10);
 }
 
+template <int MT, int CH, bool GATE>
+void launch_res1(const XaGemmArgs& g, int G, int rounds, hipStream_t s) {
+  const size_t lds =
+      sizeof(float) * ((size_t)MT * 16 * (128 * CH + 4) + (size_t)RS_UPR * MT * (RS_KP - 1) * 256);
+  hipLaunchKernelGGL((gemm_smallm_res_kernel<MT, CH, GATE>), dim3(G), dim3(512), lds, s, g, rounds);
+}
+
+template <int MT>
+void launch_res(const XaGemmArgs& g, int ch, bool gate, int G, int rounds, hipStream_t s) {
+  if (ch == 4) gate ? launch_res1<MT, 4, true>(g, G, rounds, s) : launch_res1<MT, 4, false>(g, G, rounds, s);
+  else if (ch == 2) gate ? launch_res1<MT, 2, true>(g, G, rounds, s) : launch_res1<MT, 2, false>(g, G, rounds, s);
+  else gate ? launch_res1<MT, 1, true>(g, G, rounds, s) : launch_res1<MT, 1, false>(g, G, rounds, s);
+}
+
+// the small-M kernel's contract: f32 A(m, k) = a[m lda + k], B(k, n) = b[n ldb + k], both
+// 16-B aligned with lda, ldb multiples of 4, M <= 64, K in {128, 256, 512} (all of A in
+// LDS), and enough 16-column units (N >= 2048) to cover the chip
+bool smallm_res_ok(const XaGemmArgs& g) {
+  return !g.force_small && g.a != nullptr && !g.a_u8 && g.a_pm == 1 && g.a_pk == 1 &&
+         g.a_rk == 1 && g.a_rm % 4 == 0 && ((uintptr_t)g.a & 15) == 0 && g.b_ks == 1 &&
+         g.b_ns % 4 == 0 && ((uintptr_t)g.b & 15) == 0 && g.M <= 64 &&
+         (g.K == 128 || g.K == 256 || g.K == 512) && g.N >= 2048;
+}
+
 }  // namespace
 
 extern "C" int xa_gemm_splits(int M, int N, int K) {
@@ -934,12 +1092,30 @@ extern "C" int xa_gemm(const XaGemmArgs* p, void* stream) {
   XA_CHECK_ARG((int64_t)g.M * g.N < (1ll << 31) && g.a_pm < (1ll << 31) && g.a_pk < (1ll << 31),
                "xa_gemm: M * N and group sizes must stay below 2^31");
   hipStream_t s = (hipStream_t)stream;
+  if (smallm_res_ok(g)) {
+    const int units = (g.N + 15) / 16;
+    int cus = 256;
+    int dev = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 256;
+    const int G = std::min(cus, (units + RS_UPR - 1) / RS_UPR);
+    int rounds = (units + RS_UPR * G - 1) / (RS_UPR * G);
+    rounds += rounds & 1;  // the round loop is unrolled by 2
+    const int mt = (g.M + 15) / 16, ch = g.K / 128;
+    const bool gate = g.gate != nullptr;
+    if (mt <= 1) launch_res<1>(g, ch, gate, G, rounds, s);
+    else if (mt <= 2) launch_res<2>(g, ch, gate, G, rounds, s);
+    else launch_res<4>(g, ch, gate, G, rounds, s);
+    XA_CHECK_LAUNCH("xa_gemm (small M, resident A)");
+    return 0;
+  }
   dim3 grid((g.M + BM - 1) / BM, (g.N + BN - 1) / BN, g.splits);
   const bool ak = g.a_pk == 1 && g.a_rk == 1;
   const bool bn = g.b_ns == 1;
   const bool u8 = g.a_u8 != 0;
   const int per_split = (g.K + g.splits - 1) / g.splits;
-  const int shape = g.force_small ? 0 : pick_shape(g.M, g.N, g.K, per_split, g.a == nullptr);
+  const int shape = g.force_small == 1 ? 0 : pick_shape(g.M, g.N, g.K, per_split, g.a == nullptr);
   XaGemmK kg{g, 0, 0};
   if (g.a != nullptr && ((uintptr_t)g.a & (u8 ? 3 : 15)) == 0) {
     const bool rows4 = g.a_rm % 4 == 0 && (g.a_pm == 1 || g.a_sm % 4 == 0);
