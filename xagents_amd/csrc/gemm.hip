@@ -463,10 +463,10 @@ __global__ __launch_bounds__(256) void gemm_tile_kernel(XaGemmK kargs) {
 // (q = l >> 4, i = l & 15) loads b[n0 + i][k0 + 4q .. 4q + 3], one float4 that feeds the 4
 // MFMAs of a 16-k step in a permuted k order: no LDS staging, no transpose) and reads A, in
 // the same k order, from LDS, where ALL of A stays resident: no A load sits in the K loop,
-// so nothing queues behind the B prefetches in the in-order memory counter. 512 threads = 8 waves = 2 units x 4 K parts; the grid is
-// persistent (<= one workgroup per CU) and walks rounds of 2 units per workgroup; each
-// wave's B ring holds the next round's CH chunks while it computes this round's. At a
-// round's end the 4 K parts are combined through LDS in part order and wave p finishes m
+// so nothing queues behind the B prefetches in the in-order memory counter.
+// 512 threads = 8 waves = 2 units x 4 K parts; the grid is persistent (<= one workgroup
+// per CU) and walks rounds of 2 units per workgroup; each wave's B ring spans two rounds'
+// chunks and runs 2 CH - 1 chunks ahead. At a round's end the 4 K parts are combined through LDS in part order and wave p finishes m
 // tile p (gate values fetched when the round started, ahead of the prefetches).
 // ---------------------------------------------------------------------------
 constexpr int RS_KP = 4, RS_UPR = 2;
