@@ -565,6 +565,33 @@ typedef struct XaAtariStepArgs {
 
 int xa_atari_step(const XaAtariStepArgs* args, void* stream);
 
+/* BipedalWalker-v3 device stand-in: gym's env.step / env.reset of
+ * BaseAgent.step_envs (xagents/base.py:388-426, gym call base.py:408) for BipedalWalker ids,
+ * with the real env's 24-value observation, 4 motor commands in [-1, 1], reward formula and
+ * termination, over a planar kinematic walker on flat ground (not Box2D; csrc/walker.hip).
+ * state [n_envs][XA_WALKER_STATE] f32 and episode [n_envs] int are the env's own memory
+ * (zeroed, then one reset_only call). A step reads actions [n_envs] rows of 4 f32 at row
+ * stride act_ld floats and writes the returned obs (pre-reset) to out_obs, reward and done,
+ * and the post-step state's obs (the reset obs when done) to out_post -- the one-step
+ * record xa_replay_env_step consumes. reset_only = 1 resets every env into out_post. */
+#define XA_WALKER_STATE 18
+#define XA_WALKER_OBS 24
+typedef struct XaWalkerStepArgs {
+  int n_envs;
+  float* state;
+  int* episode;
+  const float* actions;
+  int64_t act_ld;
+  uint64_t seed;
+  int reset_only;
+  float* out_obs;
+  float* out_post;
+  float* out_rew;
+  float* out_done;
+} XaWalkerStepArgs;
+
+int xa_walker_step(const XaWalkerStepArgs* args, void* stream);
+
 /* tf.keras.losses.MSE(target, pred) per row, gradient of the batch sum (minimize on a
  * [B] loss): dpred = 2 (pred - target) / n_out; loss[b] (optional). */
 int xa_mse_grad(const float* pred, const float* target, int batch, int n_out, float* dpred,

@@ -54,6 +54,8 @@ def lib():
         _lib.xo_nstep.argtypes = [c_void_p] * 4 + [c_int, c_int, c_float]
         _lib.xo_philox.argtypes = [c_uint32] * 6 + [c_void_p]
         _lib.xo_shuffle_perm.argtypes = [c_int, c_int, c_uint64, c_uint64, c_void_p]
+        _lib.xo_walker_step.argtypes = ([c_int, c_void_p, c_void_p, c_void_p, ctypes.c_long,
+                                         c_uint64, c_int] + [c_void_p] * 4)
     return _lib
 
 
@@ -103,6 +105,28 @@ def mlp_forward(theta, obs, n_actions, actions=None, uniforms=None):
     lib().xo_mlp_forward(_p(theta), _p(obs), c_int(b), c_int(obs_dim), c_int(n_actions),
                          _p(a_in), _p(u), _p(act), _p(logp), _p(value), _p(ent), _p(logits))
     return (act if actions is None else a_in), logp, value, ent, logits
+
+
+def walker_step(state, episode, actions, seed, reset_only=False):
+    """Mirror of xa_walker_step (the BipedalWalker-v3 device stand-in): state [N, 18] f32
+    and episode [N] i32 are mutated in place; actions [N, 4] f32 (ignored on reset).
+    Returns (obs [N, 24], post [N, 24], reward [N], done [N]) (obs / reward / done are
+    None on reset)."""
+    n = state.shape[0]
+    assert state.dtype == np.float32 and state.flags.c_contiguous and state.shape[1] == 18
+    assert episode.dtype == np.int32 and episode.flags.c_contiguous
+    post = np.empty((n, 24), np.float32)
+    if reset_only:
+        lib().xo_walker_step(c_int(n), _p(state), _p(episode), None, 4, c_uint64(seed), 1,
+                             None, _p(post), None, None)
+        return None, post, None, None
+    act = _f32(actions).reshape(n, 4)
+    obs = np.empty((n, 24), np.float32)
+    rew = np.empty(n, np.float32)
+    done = np.empty(n, np.float32)
+    lib().xo_walker_step(c_int(n), _p(state), _p(episode), _p(act), 4, c_uint64(seed), 0,
+                         _p(obs), _p(post), _p(rew), _p(done))
+    return obs, post, rew, done
 
 
 def mlp_rollout(theta, n_actions, env, n_steps, uniforms=None, seed=0, ctr=0,

@@ -465,3 +465,176 @@ void xo_clip_adam(float* theta, float* m, float* v, const float* g, int P, float
     theta[i] = theta[i] - (mm * alpha) / (sqrtf(vv) + eps);
   }
 }
+
+/* ---- BipedalWalker-v3 device stand-in (xagents_amd/csrc/walker.hip) ----------------
+ * The f32 restatement of walker_step_kernel, operation for operation (explicit fmaf, the
+ * same sin / cos polynomials, the same Philox reset draw). The stand-in replaces gym's
+ * BipedalWalker inside BaseAgent.step_envs (xagents/base.py:388-426); gym / Box2D are
+ * absent, so its dynamics are parity-unpinned -- this pins the device kernel to its own
+ * CPU statement. */
+#define WK_STATE 18
+#define WK_OBS 24
+enum { WS_X, WS_Y, WS_TH, WS_VX, WS_VY, WS_W, WS_Q, WS_DQ = WS_Q + 4, WS_SHAPE = WS_DQ + 4,
+       WS_STEPS, WS_FX0, WS_FX1 };
+static const float wk_scale = 30.0f, wk_fps = 50.0f, wk_dt = 1.0f / 50.0f;
+static const float wk_torque = 80.0f, wk_speed_hip = 4.0f, wk_speed_knee = 6.0f;
+static const float wk_leg_h = 34.0f / 30.0f, wk_hip_dy = 0.2f, wk_hull_half_h = 0.25f;
+static const float wk_lidar_range = 160.0f / 30.0f;
+static const float wk_gravity = 10.0f, wk_gain = 40.0f, wk_jdamp = 2.0f;
+static const float wk_react = 2.0f, wk_restore = 3.0f, wk_pdamp = 1.0f, wk_drag = 0.5f;
+static const float wk_terrain_end = (200.0f - 10.0f) * (14.0f / 30.0f);
+static const float wk_start_x = 20.0f * (14.0f / 30.0f) * 0.5f;
+static const float wk_lidar_cos[10] = {1.0f,        0.98877108f, 0.95533649f, 0.90044710f,
+                                       0.82533561f, 0.73168887f, 0.62160997f, 0.49757105f,
+                                       0.36235775f, 0.21901920f};
+static const float wk_hip_lo = -0.8f, wk_hip_hi = 1.1f, wk_knee_lo = -1.6f, wk_knee_hi = -0.1f;
+
+static float wk_reduce(float x) {
+  const float k = rintf(x * 0.159154943f);
+  return fmaf(-k, 6.28318548f, x);
+}
+static float wk_sin(float x) {
+  const float r = wk_reduce(x), r2 = r * r;
+  float p = fmaf(r2, -7.6471637e-13f, 1.6059044e-10f);
+  p = fmaf(r2, p, -2.5052108e-08f);
+  p = fmaf(r2, p, 2.7557319e-06f);
+  p = fmaf(r2, p, -1.9841270e-04f);
+  p = fmaf(r2, p, 8.3333333e-03f);
+  p = fmaf(r2, p, -1.6666667e-01f);
+  p = fmaf(r2, p, 1.0f);
+  return r * p;
+}
+static float wk_cos(float x) {
+  const float r = wk_reduce(x), r2 = r * r;
+  float p = fmaf(r2, 4.7794773e-14f, -1.1470746e-11f);
+  p = fmaf(r2, p, 2.0876757e-09f);
+  p = fmaf(r2, p, -2.7557319e-07f);
+  p = fmaf(r2, p, 2.4801587e-05f);
+  p = fmaf(r2, p, -1.3888889e-03f);
+  p = fmaf(r2, p, 4.1666667e-02f);
+  p = fmaf(r2, p, -0.5f);
+  return fmaf(r2, p, 1.0f);
+}
+static float wk_clip(float v, float lo, float hi) { return fminf(fmaxf(v, lo), hi); }
+
+static void wk_feet(const float* s, float* fx, float* fy) {
+  for (int j = 0; j < 2; ++j) {
+    const float a1 = s[WS_TH] + s[WS_Q + 2 * j];
+    const float a2 = a1 + s[WS_Q + 2 * j + 1];
+    fx[j] = fmaf(wk_leg_h, wk_sin(a1), wk_leg_h * wk_sin(a2));
+    fy[j] = (-wk_hip_dy - wk_leg_h * wk_cos(a1)) - wk_leg_h * wk_cos(a2);
+  }
+}
+
+static void wk_observe(const float* s, const float* contact, float* o) {
+  o[0] = s[WS_TH];
+  o[1] = 2.0f * s[WS_W] / wk_fps;
+  o[2] = 0.3f * s[WS_VX] * (600.0f / wk_scale) / wk_fps;
+  o[3] = 0.3f * s[WS_VY] * (400.0f / wk_scale) / wk_fps;
+  for (int j = 0; j < 2; ++j) {
+    o[4 + 5 * j] = s[WS_Q + 2 * j];
+    o[5 + 5 * j] = s[WS_DQ + 2 * j] / wk_speed_hip;
+    o[6 + 5 * j] = s[WS_Q + 2 * j + 1] + 1.0f;
+    o[7 + 5 * j] = s[WS_DQ + 2 * j + 1] / wk_speed_knee;
+    o[8 + 5 * j] = contact[j];
+  }
+  for (int i = 0; i < 10; ++i)
+    o[14 + i] = fminf(1.0f, s[WS_Y] / (wk_lidar_range * wk_lidar_cos[i]));
+}
+
+static void wk_reset(float* s, int env, int episode, uint64_t seed, float* contact) {
+  uint32_t r[4];
+  xo_philox((uint32_t)env, (uint32_t)episode, 0x3a1cu, 0u, (uint32_t)seed,
+            (uint32_t)(seed >> 32), r);
+  for (int k = 0; k < WK_STATE; ++k) s[k] = 0.0f;
+  s[WS_X] = wk_start_x;
+  s[WS_VX] = (u01(r[0]) * 2.0f - 1.0f) * 0.2f;
+  s[WS_Q + 1] = wk_knee_hi;
+  s[WS_Q + 3] = wk_knee_hi;
+  float fx[2], fy[2];
+  wk_feet(s, fx, fy);
+  s[WS_Y] = -fminf(fy[0], fy[1]);
+  s[WS_FX0] = fx[0];
+  s[WS_FX1] = fx[1];
+  s[WS_SHAPE] = 130.0f * s[WS_X] / wk_scale;
+  contact[0] = contact[1] = 1.0f;
+}
+
+void xo_walker_step(int n_envs, float* state, int* episode, const float* actions, long act_ld,
+                    uint64_t seed, int reset_only, float* out_obs, float* out_post,
+                    float* out_rew, float* out_done) {
+  for (int e = 0; e < n_envs; ++e) {
+    float* s = state + (size_t)e * WK_STATE;
+    float contact[2];
+    if (reset_only) {
+      wk_reset(s, e, episode[e], seed, contact);
+      wk_observe(s, contact, out_post + (size_t)e * WK_OBS);
+      continue;
+    }
+    const float* act = actions + (size_t)e * act_ld;
+    float u[4], cost = 0.0f;
+    for (int i = 0; i < 4; ++i) {
+      u[i] = wk_clip(act[i], -1.0f, 1.0f);
+      cost = cost + fabsf(u[i]);
+    }
+    for (int i = 0; i < 4; ++i) {
+      const int hip = (i & 1) == 0;
+      const float vmax = hip ? wk_speed_hip : wk_speed_knee;
+      float dq = s[WS_DQ + i];
+      dq = dq + wk_dt * fmaf(wk_gain, u[i], -wk_jdamp * dq);
+      dq = wk_clip(dq, -vmax, vmax);
+      float q = fmaf(wk_dt, dq, s[WS_Q + i]);
+      const float lo = hip ? wk_hip_lo : wk_knee_lo, hi = hip ? wk_hip_hi : wk_knee_hi;
+      if (q < lo || q > hi) dq = 0.0f;
+      s[WS_Q + i] = wk_clip(q, lo, hi);
+      s[WS_DQ + i] = dq;
+    }
+    s[WS_W] = s[WS_W] +
+              wk_dt * ((-wk_react * (u[0] + u[2]) - wk_restore * s[WS_TH]) - wk_pdamp * s[WS_W]);
+    s[WS_TH] = fmaf(wk_dt, s[WS_W], s[WS_TH]);
+    float fx[2], fy[2];
+    wk_feet(s, fx, fy);
+    const float support = -fminf(fy[0], fy[1]);
+    s[WS_VY] = s[WS_VY] - wk_gravity * wk_dt;
+    float y = fmaf(wk_dt, s[WS_VY], s[WS_Y]);
+    int grounded = 0;
+    if (y <= support) {
+      y = support;
+      s[WS_VY] = fmaxf(s[WS_VY], 0.0f);
+      grounded = 1;
+    }
+    s[WS_Y] = y;
+    float push = 0.0f, n_st = 0.0f;
+    for (int j = 0; j < 2; ++j) {
+      contact[j] = grounded && fy[j] <= fminf(fy[0], fy[1]) + 0.02f ? 1.0f : 0.0f;
+      if (contact[j] > 0.0f) {
+        push = push - (fx[j] - s[WS_FX0 + j]);
+        n_st = n_st + 1.0f;
+      }
+    }
+    s[WS_VX] = n_st > 0.0f ? push / (n_st * wk_dt) : s[WS_VX] * (1.0f - wk_drag * wk_dt);
+    s[WS_X] = fmaf(wk_dt, s[WS_VX], s[WS_X]);
+    s[WS_FX0] = fx[0];
+    s[WS_FX1] = fx[1];
+    s[WS_STEPS] = s[WS_STEPS] + 1.0f;
+    const float shaping = 130.0f * s[WS_X] / wk_scale - 5.0f * fabsf(s[WS_TH]);
+    float reward = shaping - s[WS_SHAPE];
+    s[WS_SHAPE] = shaping;
+    reward = reward - 0.00035f * wk_torque * cost;
+    const int game_over = s[WS_Y] - wk_hull_half_h < 0.0f || fabsf(s[WS_TH]) > 1.0f;
+    int done = 0;
+    if (game_over || s[WS_X] < 0.0f) {
+      reward = -100.0f;
+      done = 1;
+    }
+    if (s[WS_X] > wk_terrain_end || s[WS_STEPS] >= 1600.0f) done = 1;
+    wk_observe(s, contact, out_obs + (size_t)e * WK_OBS);
+    out_rew[e] = reward;
+    out_done[e] = done ? 1.0f : 0.0f;
+    if (done) {
+      episode[e] = episode[e] + 1;
+      wk_reset(s, e, episode[e], seed, contact);
+    }
+    wk_observe(s, contact, out_post + (size_t)e * WK_OBS);
+  }
+}

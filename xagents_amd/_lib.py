@@ -202,6 +202,15 @@ class XaAtariStepArgs(Structure):
     ]
 
 
+class XaWalkerStepArgs(Structure):
+    _fields_ = [
+        ('n_envs', c_int), ('state', c_void_p), ('episode', c_void_p), ('actions', c_void_p),
+        ('act_ld', c_int64), ('seed', c_uint64), ('reset_only', c_int),
+        ('out_obs', c_void_p), ('out_post', c_void_p), ('out_rew', c_void_p),
+        ('out_done', c_void_p),
+    ]
+
+
 class XaTrpoHeadArgs(Structure):
     _fields_ = [
         ('n', c_int), ('n_actions', c_int),
@@ -362,6 +371,7 @@ _SIGNATURES = {
     'xa_adam_step_bump': (c_int, [c_void_p, c_void_p]),
     'xa_replay_env_step': (c_int, [POINTER(XaReplayStepArgs), c_void_p]),
     'xa_atari_step': (c_int, [POINTER(XaAtariStepArgs), c_void_p]),
+    'xa_walker_step': (c_int, [POINTER(XaWalkerStepArgs), c_void_p]),
     'xa_mse_grad': (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     'xa_copy_block': (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int, c_int, c_void_p]),
     'xa_categorical': (

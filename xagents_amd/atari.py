@@ -137,9 +137,10 @@ class AtariFrameVecEnv(TransitionReplayVecEnv):
         call('xa_atari_step', ctypes.byref(a), stream())
         return self.state
 
-    def pre_step(self):
+    def pre_step(self, actions=None, act_ld=None):
         """AtariWrapper.step (frame skip + preprocessing) of every env into the one-step
-        record that the following xa_replay_env_step consumes."""
+        record that the following xa_replay_env_step consumes (the synthetic raw stream
+        does not depend on the actions)."""
         a = self._args
         a.reset_only = 0
         a.out_step, a.out_post = self.rep_obs.data_ptr(), self.rep_state.data_ptr()

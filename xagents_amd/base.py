@@ -572,7 +572,9 @@ class OffPolicy(BaseAgent, ABC):
         a.done_epret = self._st_epret[r].data_ptr()
         pre_step = getattr(self.envs, 'pre_step', None)
         if pre_step is not None:
-            pre_step()  # raw-frame env: AtariWrapper.step into the one-step record
+            # raw-frame env (AtariWrapper.step) / dynamics env (env.step with the actions)
+            # into the one-step record
+            pre_step(actions)
         call('xa_replay_env_step', ctypes.byref(a), stream())
         if store:
             self.replay.appended()
@@ -605,7 +607,7 @@ class OffPolicy(BaseAgent, ABC):
         a.actions, a.act_bytes = actions.data_ptr(), self.replay.act_bytes
         pre_step = getattr(self.envs, 'pre_step', None)
         if pre_step is not None:
-            pre_step()
+            pre_step(actions)
         call('xa_replay_env_step', ctypes.byref(a), stream())
         out = self._play_out[:2, 0].cpu().numpy()
         return out[:1], out[1:]

@@ -314,6 +314,67 @@ class TransitionReplayVecEnv:
         a.ep_return, a.done = self.ep_return.data_ptr(), self.done.data_ptr()
 
 
+class WalkerVecEnv(TransitionReplayVecEnv):
+    """BipedalWalker-v3 device stand-in (csrc/walker.hip): real
+    action-dependent dynamics with BipedalWalker's 24-value observation, 4 motor commands
+    in [-1, 1], reward formula and termination (not Box2D: a planar kinematic walker on flat
+    ground). Each env step is one xa_walker_step launch (pre_step, given the step's actions)
+    into the one-step record that xa_replay_env_step then turns into the agent's state,
+    rewards, dones and replay-ring append, as for the other transition envs."""
+
+    def __init__(self, env_id='BipedalWalker-v3', n_envs=1, seed=55, device=None):
+        n = int(n_envs)
+        z = np.zeros((n, 1, 24), np.float32)
+        record = (np.zeros((n, 24), np.float32), z, z.copy(), np.zeros((n, 1), np.float32),
+                  np.zeros((n, 1), np.float32))
+        self._ready = False
+        super().__init__(env_id, n, (24,), Box(-1.0, 1.0, (4,)), np.float32, seed=seed,
+                         device=device, record=record)
+        self.walker_seed = int(seed if seed is not None else 0) % 2**64
+        self.walker_state = torch.zeros(n, 18, dtype=torch.float32, device=self.device)
+        self.episode = torch.zeros(n, dtype=torch.int32, device=self.device)
+        self._ready = True
+        self.reset()
+
+    def _args(self, reset_only, actions=0, act_ld=4):
+        from xagents_amd._lib import XaWalkerStepArgs
+        a = XaWalkerStepArgs()
+        a.n_envs, a.state, a.episode = self.n_envs, self.walker_state.data_ptr(), \
+            self.episode.data_ptr()
+        a.actions, a.act_ld, a.seed, a.reset_only = actions, act_ld, self.walker_seed, \
+            int(reset_only)
+        return a
+
+    def reset(self):
+        """BipedalWalker.reset of every env into the state (the episode counters keep
+        counting, so every reset draws a fresh initial push)."""
+        super().reset()
+        if not self._ready:
+            return self.state
+        import ctypes
+        from xagents_amd._lib import call, stream
+        a = self._args(True)
+        a.out_post = self.state.data_ptr()
+        call('xa_walker_step', ctypes.byref(a), stream())
+        return self.state
+
+    def pre_step(self, actions=None, act_ld=4):
+        """env.step of every env with `actions` (a device tensor [N, 4] f32, or a pointer
+        to rows of 4 f32 at row stride act_ld) into the one-step record."""
+        import ctypes
+        from xagents_amd._lib import call, stream
+        if actions is None:
+            raise ValueError('WalkerVecEnv.pre_step needs the step\'s actions')
+        ptr = actions if isinstance(actions, int) else actions.data_ptr()
+        if not isinstance(actions, int):
+            assert actions.dtype == torch.float32 and actions.is_contiguous()
+            act_ld = actions.shape[-1]
+        a = self._args(False, ptr, act_ld)
+        a.out_obs, a.out_post = self.rep_obs.data_ptr(), self.rep_state.data_ptr()
+        a.out_rew, a.out_done = self.rep_rew.data_ptr(), self.rep_done.data_ptr()
+        call('xa_walker_step', ctypes.byref(a), stream())
+
+
 def create_envs(env_name, n=1, preprocess=False, *args, mode='replay', seed=55, device=None,
                 t_rec=4096, **kwargs):
     """Device counterpart of xagents.utils.common.create_envs (common.py:145-166).
@@ -334,6 +395,8 @@ def create_envs(env_name, n=1, preprocess=False, *args, mode='replay', seed=55, 
         return TransitionReplayVecEnv(env_name, n, (84, 84, 1), Discrete(actions), np.uint8,
                                       t_rec=min(t_rec, 256), seed=seed, device=device)
     if env_name.startswith('BipedalWalker'):
+        if mode == 'dynamics':
+            return WalkerVecEnv(env_name, n, seed=seed, device=device)
         return TransitionReplayVecEnv(env_name, n, (24,), Box(-1.0, 1.0, (4,)), np.float32,
                                       t_rec=t_rec, seed=seed, device=device)
     assert not preprocess, (f'Cannot use AtariWrapper or --preprocess for non-atari '

@@ -127,7 +127,12 @@ class ExecutorActorCritic:
             a.done_epret = self.b_epret.data_ptr() + 4 * t
             a.out_ld = T  # env-major [N, T] rows
             if hasattr(env, 'pre_step'):
-                env.pre_step()  # raw-frame env: AtariWrapper.step into the one-step record
+                # raw-frame env (AtariWrapper.step) / dynamics env (env.step with step t's
+                # actions: env-major rows of b_act, stride T A) into the one-step record
+                if self.gaussian:
+                    env.pre_step(self.b_act.data_ptr() + 4 * t * A, T * A)
+                else:
+                    env.pre_step(self.b_act.data_ptr() + 4 * t, T)
             call('xa_replay_env_step', ctypes.byref(a), stream())
         # dones[:, t + 1] = done of step t (dones[:, 0] is the carried-in flag)
         call('xa_copy_block', self.b_dstep.data_ptr(), T, self.b_done.data_ptr() + 4, T + 1, N,
