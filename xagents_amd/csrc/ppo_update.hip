@@ -337,7 +337,11 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
   const int t0 = *p.adam_step;
   for (int k = tid; k < K; k += 256)
     U.alpha[k] = adam_alpha(p.adam.lr, p.adam.beta1, p.adam.beta2, t0 + k + 1);
+#ifndef XA_ABL_P0
   for (int k = w; k < K; k += 4) {
+#else
+  for (int k = w; k < 0; k += 4) {
+#endif
     const int e = k / n_mb, m = k - e * n_mb;
     const int start = m * MB, cnt = min(MB, B - start);
     const int n_tiles = (cnt + TS - 1) / TS;
@@ -542,7 +546,9 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
         // inputs straight from the phase-0 records (read-only: no staging, no barrier)
         XA_STAMP(35);
         const PackedIn<OBS> in{&U.pre[((size_t)k * TPB * TS + ((tile - b) / G) * TS) * (OBS + 4)]};
+#ifndef XA_ABL_TILE  // diagnostic ablation builds (tools/ablate_update.py) only
         tile_compute<OBS, A, decltype(stampf), PackedIn<OBS>, TS>(L, acc, cfg, stampf, in);
+#endif
         XA_STAMP(36);
         continue;
       }
@@ -567,7 +573,9 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
     // ---- the block's gradient row, staged in LDS, published as granule pairs (measured:
     // storing W2's pairs straight from the MFMA accumulators with a lane swap was slower,
     // the write-through stores then stall the combine below) ----
+#ifndef XA_ABL_ROW
     tile_write_row<OBS, A>(L, acc, [&](int i, float v) { srow[i] = v; });
+#endif
     XA_STAMP(44);
     if (p.loss_out) {
       const float ls = tile_loss_sums<OBS, A>(L, acc);
@@ -653,7 +661,53 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
     // ---- B: pair columns [c0, c0 + nc): the fixed-order sum over the G rows, or
     // (two-level) over the XCD partials in XCD order -> g (granules) + f64 sum of squares ----
     double sq = 0.0;
-    const bool flat_b = !two_level && G * nc <= 256 * kBF;
+    // few columns, few rows per part: thread (part, c) polls its own column's rows part,
+    // part + parts, ... (<= kBF granules, one round trip) and sums them in registers in
+    // that order -- the flat path's arithmetic without its LDS staging pass
+    const int parts_b = nc <= 128 ? min(4, 256 / max(nc, 1)) : 1;
+    const bool col_b = !two_level && nc > 0 && parts_b > 1 && (G + parts_b - 1) / parts_b <= kBF;
+    if (col_b) {
+      double t0 = 0.0, t1 = 0.0;
+      bool bad = false;
+      if (tid < parts_b * nc) {
+        const int part = tid / nc, c = tid - part * nc;
+        uint32_t off[kBF];
+        f32x4v x[kBF];
+        int n = 0;
+#pragma unroll
+        for (int u = 0; u < kBF; ++u) {
+          const int r = part + parts_b * u;
+          off[u] = r < G ? (uint32_t)(((size_t)r * NP2 + c0 + c) * 16) : 0u;
+          n += r < G;
+        }
+        bad = !poll_gran<kBF>(rows_r, off, n, tag, x, ws.ctl, epoch, p.status);
+#pragma unroll
+        for (int u = 0; u < kBF; ++u)
+          if (u < n) {
+            t0 += (double)x[u][0];
+            t1 += (double)x[u][2];
+          }
+        U.red[(part * nc + c) * 2] = t0;
+        U.red[(part * nc + c) * 2 + 1] = t1;
+      }
+      if (__syncthreads_or(bad)) return;
+      for (int c = tid; c < nc; c += 256) {
+        double s0 = 0.0, s1 = 0.0;
+        for (int part = 0; part < parts_b; ++part) {
+          s0 += U.red[(part * nc + c) * 2];
+          s1 += U.red[(part * nc + c) * 2 + 1];
+        }
+        const float g0 = (float)s0, g1 = (float)s1;
+        const int cc = c0 + c;
+        st_gran2(g_r, (uint32_t)(16 * cc), g0, g1, tag, true);
+        if (p.grad_out && k == K - 1) {
+          if (2 * cc < P) p.grad_out[2 * cc] = g0;
+          if (2 * cc + 1 < P) p.grad_out[2 * cc + 1] = g1;
+        }
+        sq += (double)g0 * (double)g0 + (double)g1 * (double)g1;
+      }
+    }
+    const bool flat_b = !col_b && !two_level && G * nc <= 256 * kBF;
     if (nc > 0 && flat_b) {
       const bool bad = gather_rows(rows_r, G, nc, [&](int r) {
         return (uint32_t)(((size_t)r * NP2 + c0) * 16);
@@ -662,7 +716,11 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
       // few columns: `parts` threads per column sum interleaved rows, combined in part
       // order (a shorter dependent f64 chain; fixed order)
       const int parts = nc <= 128 ? min(4, 256 / nc) : 1;
+#ifdef XA_ABL_BSUM
+      if (false) {
+#else
       if (parts > 1) {
+#endif
         if (tid < parts * nc) {
           const int part = tid / nc, c = tid - part * nc;
           double t0 = 0.0, t1 = 0.0;
@@ -677,6 +735,11 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
       }
       for (int c = tid; c < nc; c += 256) {
         double t0 = 0.0, t1 = 0.0;
+#ifdef XA_ABL_BSUM
+        if (true) {
+          t0 = scr[2 * c]; t1 = scr[2 * c + 1];
+        } else
+#endif
         if (parts > 1) {
           for (int part = 0; part < parts; ++part) {
             t0 += U.red[(part * nc + c) * 2];
@@ -698,7 +761,7 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
         sq += (double)g0 * (double)g0 + (double)g1 * (double)g1;
       }
     }
-    if (nc > 0 && !flat_b) {
+    if (nc > 0 && !flat_b && !col_b) {
       const int SRC = two_level ? kXcds : G;  // sources summed per column
       const int ncol = min(nc, 256), RG = min(SRC, 256 / ncol);
       const int rg = tid / ncol, cq = tid - rg * ncol;
@@ -835,14 +898,22 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
     }
     if (__syncthreads_or(bad)) return;
     XA_STAMP(47);
+#ifndef XA_ABL_CNORM
     tot = xa_wave_sum_f64(tot);
     const float sc = clip_scale(tot, p.adam.clip_norm);
+#else
+    const float sc = (float)tot;
+#endif
     const float alpha = U.alpha[k];
+#ifndef XA_ABL_ADAM
 #pragma unroll
     for (int i = 0; i < 16; ++i) adam_fast(gw[i] * sc, wv[i], mw[i], vw[i], alpha, omb1, omb2, p.adam.eps);
 #pragma unroll
     for (int q = 0; q < RPT; ++q) adam_fast(gr[q] * sc, rv[q], mr[q], vr[q], alpha, omb1, omb2, p.adam.eps);
+#endif
+#ifndef XA_ABL_LDS
     ps.to_lds(L, wv, rv);
+#endif
     XA_STAMP(43);
   }
   if (b == 0) {
