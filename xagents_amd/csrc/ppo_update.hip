@@ -150,6 +150,23 @@ XA_DEV void adam_fast(float g, float& th, float& m, float& v, float alpha, float
   th = th - (m * alpha) * frcp(__builtin_amdgcn_sqrtf(v) + eps);
 }
 
+// the same on two parameters at once: the moment updates as packed f32 (v_pk_fma_f32 /
+// v_pk_mul_f32), sqrt and the reciprocal on the hardware units without a Newton step (the
+// update is checked against float64 with a tolerance)
+XA_DEV void adam_fast2(xa_f2 g, float& th0, float& th1, float& m0, float& m1, float& v0,
+                       float& v1, float alpha, float omb1, float omb2, float eps) {
+  const xa_f2 m = {m0, m1}, v = {v0, v1};
+  const xa_f2 mn = xa_fma2(g - m, xa_f2{omb1, omb1}, m);
+  const xa_f2 vn = xa_fma2(g * g - v, xa_f2{omb2, omb2}, v);
+  const xa_f2 step = mn * xa_f2{alpha, alpha};
+  th0 = th0 - step.x * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(vn.x) + eps);
+  th1 = th1 - step.y * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(vn.y) + eps);
+  m0 = mn.x;
+  m1 = mn.y;
+  v0 = vn.x;
+  v1 = vn.y;
+}
+
 // this workgroup's XCD (MI355X_MICROARCH.md: read placement from HW_REG_XCC_ID)
 XA_DEV int xcc_id() {
   unsigned x;
@@ -906,10 +923,20 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
 #endif
     const float alpha = U.alpha[k];
 #ifndef XA_ABL_ADAM
+    {
+      const xa_f2 sc2 = {sc, sc};
 #pragma unroll
-    for (int i = 0; i < 16; ++i) adam_fast(gw[i] * sc, wv[i], mw[i], vw[i], alpha, omb1, omb2, p.adam.eps);
+      for (int i = 0; i < 16; i += 2)
+        adam_fast2(xa_f2{gw[i], gw[i + 1]} * sc2, wv[i], wv[i + 1], mw[i], mw[i + 1], vw[i],
+                   vw[i + 1], alpha, omb1, omb2, p.adam.eps);
 #pragma unroll
-    for (int q = 0; q < RPT; ++q) adam_fast(gr[q] * sc, rv[q], mr[q], vr[q], alpha, omb1, omb2, p.adam.eps);
+      for (int q = 0; q + 1 < RPT; q += 2)
+        adam_fast2(xa_f2{gr[q], gr[q + 1]} * sc2, rv[q], rv[q + 1], mr[q], mr[q + 1], vr[q],
+                   vr[q + 1], alpha, omb1, omb2, p.adam.eps);
+      if (RPT % 2)
+        adam_fast(gr[RPT - 1] * sc, rv[RPT - 1], mr[RPT - 1], vr[RPT - 1], alpha, omb1, omb2,
+                  p.adam.eps);
+    }
 #endif
 #ifndef XA_ABL_LDS
     ps.to_lds(L, wv, rv);
