@@ -20,6 +20,7 @@
 // optimizer step runs on these slices and they fill the LDS weight tiles.
 #pragma once
 #include <math.h>
+#include <stddef.h>
 
 #include "../../include/xagents_hip.h"
 #include "xa_adam.hpp"
@@ -146,15 +147,31 @@ template <int OBS, int A>
 struct ParamSlice {
   static constexpr int RPT = Dims<OBS, A>::RPT, NREST = Dims<OBS, A>::NREST;
   int k0, j0;
-  int ri[RPT];  // flat index of rest value q, -1 past the end
+  int ri[RPT];    // flat index of rest value q, -1 past the end
+  int rdst[RPT];  // its float offset inside TileLds (the LDS weight tiles), -1 past the end
   XA_DEV void init(int tid) {
+    typedef TileLds<OBS, A> T;
+    constexpr int AH = A + 1;
     const Offs o = offs(OBS, A);
     k0 = 4 * (tid >> 4);
     j0 = 4 * (tid & 15);
 #pragma unroll
     for (int q = 0; q < RPT; ++q) {
       const int r = tid + 256 * q;
-      ri[q] = r < NREST ? (r < o.w2 ? r : r + H * H) : -1;
+      const int e = r < NREST ? (r < o.w2 ? r : r + H * H) : -1;
+      ri[q] = e;
+      int d = -1;
+      if (e < 0) d = -1;
+      else if (e < o.b1) d = (int)(offsetof(T, sW1) / 4) + e;
+      else if (e < o.w2) d = (int)(offsetof(T, sb1) / 4) + (e - o.b1);
+      else if (e < o.w3) d = (int)(offsetof(T, sb2) / 4) + (e - o.b2);
+      else if (e < o.b3) {
+        const int jj = (e - o.w3) / A, a = (e - o.w3) - jj * A;
+        d = (int)(offsetof(T, sW34) / 4) + jj * AH + a;
+      } else if (e < o.w4) d = (int)(offsetof(T, sb34) / 4) + (e - o.b3);
+      else if (e < o.b4) d = (int)(offsetof(T, sW34) / 4) + (e - o.w4) * AH + A;
+      else d = (int)(offsetof(T, sb34) / 4) + A;
+      rdst[q] = d;
     }
   }
   XA_DEV size_t w2_off(int rr) const { return (size_t)offs(OBS, A).w2 + (k0 + rr) * H + j0; }
@@ -179,8 +196,6 @@ struct ParamSlice {
   }
   // the slice into the LDS weight tiles (W2 and its transpose, W1, biases, heads)
   XA_DEV void to_lds(TileLds<OBS, A>& L, const float (&w)[16], const float (&r)[RPT]) const {
-    constexpr int AH = A + 1;
-    const Offs o = offs(OBS, A);
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) {
       *reinterpret_cast<float4*>(&L.sW2[(k0 + rr) * LDW + j0]) =
@@ -188,21 +203,10 @@ struct ParamSlice {
       *reinterpret_cast<float4*>(&L.sW2T[(j0 + rr) * LDW + k0]) =
           make_float4(w[rr], w[4 + rr], w[8 + rr], w[12 + rr]);
     }
+    // the rest values through their precomputed LDS offsets (no per-lane range branches)
 #pragma unroll
-    for (int q = 0; q < RPT; ++q) {
-      const int e = ri[q];
-      if (e < 0) continue;
-      const float x = r[q];
-      if (e < o.b1) L.sW1[e] = x;
-      else if (e < o.w2) L.sb1[e - o.b1] = x;
-      else if (e < o.w3) L.sb2[e - o.b2] = x;
-      else if (e < o.b3) {
-        const int jj = (e - o.w3) / A, a = (e - o.w3) - jj * A;
-        L.sW34[jj * AH + a] = x;
-      } else if (e < o.w4) L.sb34[e - o.b3] = x;
-      else if (e < o.b4) L.sW34[(e - o.w4) * AH + A] = x;
-      else L.sb34[A] = x;
-    }
+    for (int q = 0; q < RPT; ++q)
+      if (rdst[q] >= 0) reinterpret_cast<float*>(&L)[rdst[q]] = r[q];
   }
 };
 
