@@ -274,7 +274,10 @@ def bench_offpolicy_and_cnn(args):
             agent.at_step_end()
         el = _timed(step, args.steps, args.warmup, world)
         env_steps = n * args.steps * world
+        # one eager learner phase for the event pairs (the timed steps replay it as a graph)
+        agent.use_graph = False
         rl = dense_dx_roofline([agent.ex_online], step)
+        agent.use_graph = True
         if rl:
             line['roofline'] = rl
         line.update(scaling='weak', data=_data_note(
