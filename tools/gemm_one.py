@@ -1,5 +1,6 @@
 """Run one CNN GEMM shape repeatedly (for rocprofv3 PMC passes): dense dX of the
-NatureCNN dense layer at B = 4096 by default.  usage: python tools/gemm_one.py [name] [reps]"""
+NatureCNN dense layer at B = 4096 by default.
+usage: python tools/gemm_one.py [name] [reps] [B]"""
 import sys
 from pathlib import Path
 
@@ -16,7 +17,7 @@ def main():
     from xagents_amd.layers import gemm
     name = sys.argv[1] if len(sys.argv) > 1 else 'dense dX'
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
-    B = 4096
+    B = int(sys.argv[3]) if len(sys.argv) > 3 else 4096
     lib = _lib.load()
     dev = torch.device('cuda')
     (_, M, N, K, am, ak, bks, bns, is_u8), = [s for s in shapes(B) if s[0] == name]
