@@ -402,6 +402,8 @@ def bench_ppo(args, world, rank, device, n_envs):
     theta0 = model.theta.cpu().numpy().copy()
     agent = PPO(envs, model, n_steps=args.n_steps, seed=args.seed, quiet=True,
                 use_graph=not args.no_graph)
+    if world > 1:
+        dist.barrier()  # the data-parallel update's in-launch exchanges wait for every rank
     for _ in range(args.warmup):
         agent.train_step()
     transport = agent.check_peer_all_reduce()

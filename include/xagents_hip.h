@@ -308,6 +308,7 @@ int xa_clip_adam(float* theta, float* adam_m, float* adam_v, const float* grad, 
  * status (optional device int): set to 1 if an in-launch exchange timed out (2 s);
  * the parameters are then invalid. adam.grad_scale is not used (must be 1).
  */
+#define XA_PPO_DP_MAX 16
 typedef struct XaPpoUpdateArgs {
   int obs_dim, n_actions;
   int batch, mb_size, epochs;
@@ -331,11 +332,23 @@ typedef struct XaPpoUpdateArgs {
   int n_blocks;
   int bump_counter; /* nonzero: the launch ends with *shuffle.rng_counter += 1 (the
                        xa_counter_bump that follows the update in a train step) */
+  /* data parallel (dp_world > 1; one process per GPU, each with its own env shard and
+   * batch): per minibatch the advantage sums, and per optimizer step every workgroup's
+   * reduced gradient slice, are exchanged inside the launch through the ranks' exchange
+   * blocks (uncached, IPC-mapped into every rank, zeroed once; dp_blocks[r] = rank r's,
+   * each >= xa_ppo_update_dp_block_bytes) and summed in rank order, so every rank applies
+   * the step of the union of the ranks' minibatches (the all_reduce(SUM) of SURVEY 8e).
+   * Every rank must launch with the same shapes and n_blocks, and all ranks' workgroups
+   * must be resident at once. */
+  int dp_world, dp_rank;
+  void* dp_blocks[XA_PPO_DP_MAX];
 } XaPpoUpdateArgs;
 
 int xa_ppo_update_blocks(int obs_dim, int n_actions, int mb_size);
 size_t xa_ppo_update_workspace_bytes(int obs_dim, int n_actions, int batch, int mb_size,
                                      int epochs, int n_blocks);
+size_t xa_ppo_update_dp_block_bytes(int obs_dim, int n_actions, int batch, int mb_size,
+                                    int epochs, int n_blocks, int world);
 int xa_ppo_update(const XaPpoUpdateArgs* args, void* stream);
 
 /* ------------------------------------------------------------------------- */

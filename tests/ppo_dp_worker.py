@@ -42,7 +42,9 @@ def main():
     perms = [np.stack([np.random.default_rng(200 + 10 * r + e).permutation(B)
                        for e in range(E)]).astype(np.int32) for r in range(world)]
     dp = make(records[rank], N)
-    assert dp.distributed and dp.world_size == world and dp.update_mode == 'chain'
+    import os
+    want = os.environ.get('XA_PPO_UPDATE', 'persistent')
+    assert dp.distributed and dp.world_size == world and dp.update_mode == want, dp.update_mode
     theta0 = dp.model.theta.cpu().numpy().astype(np.float64)
     u_dp = torch.from_numpy(uniforms[rank]).cuda()
     p_dp = torch.from_numpy(perms[rank]).cuda()
@@ -62,7 +64,7 @@ def main():
     if rank == 0:
         union_rec = tuple(np.concatenate([r[i] for r in records]) for i in range(5))
         un = make(union_rec, world * N, data_parallel=False)
-        assert not un.distributed and un.update_mode == 'persistent'
+        assert not un.distributed and un.update_mode == want
         np.testing.assert_array_equal(un.model.theta.cpu().numpy(), theta0)
         un.set_rollout_uniforms(torch.from_numpy(np.concatenate(uniforms)).cuda())
         # union minibatch m = the ranks' minibatch m slices, rank-major, global indices
@@ -82,6 +84,8 @@ def main():
         assert int(un.model.optimizer.iterations.item()) == E * M
     assert int(dp.model.optimizer.iterations.item()) == E * M
     dist.barrier()
+    if getattr(dp, 'dp_blocks', None) is not None:
+        dp.dp_blocks.close()
     if dp.peer is not None:
         dp.peer.close()
     print(f'PPO DP OK {rank}', flush=True)

@@ -31,10 +31,12 @@ def _run(worker, world, tag, extra_env=None, timeout=110):
         assert f'{tag} {r}' in out, out[-4000:]
 
 
-def test_ppo_data_parallel_equals_union(device):
+@pytest.mark.parametrize('mode', ['persistent', 'chain'])
+def test_ppo_data_parallel_equals_union(device, mode):
     """xagents/ppo/agent.py:157-191 on the union of 2 shards vs the W = 2 data-parallel
-    step (advantage sums and gradients exchanged), tests/ppo_dp_worker.py."""
-    _run('ppo_dp_worker.py', 2, 'PPO DP OK')
+    step (advantage sums and gradients exchanged), tests/ppo_dp_worker.py: the persistent
+    update exchanging inside its launch, and the per-minibatch chain."""
+    _run('ppo_dp_worker.py', 2, 'PPO DP OK', extra_env={'XA_PPO_UPDATE': mode})
 
 
 def test_td3_data_parallel_done_patterns(device):
@@ -47,4 +49,5 @@ def test_peer_stall_falls_back_to_rccl(device):
     """A rank stalling past the peer-exchange timeout in the middle of training is detected
     by the periodic health check on every rank (tests/peer_stall_worker.py)."""
     _run('peer_stall_worker.py', 2, 'STALL OK',
-         extra_env={'XA_PEER_TIMEOUT_S': '0.5', 'XA_PEER_CHECK_STEPS': '4'})
+         extra_env={'XA_PEER_TIMEOUT_S': '0.5', 'XA_PEER_CHECK_STEPS': '4',
+                    'XA_PPO_UPDATE': 'chain'})

@@ -150,6 +150,8 @@ class XaPpoUpdateArgs(Structure):
         ('status', c_void_p),
         ('n_blocks', c_int),
         ('bump_counter', c_int),
+        ('dp_world', c_int), ('dp_rank', c_int),
+        ('dp_blocks', c_void_p * 16),
     ]
 
 
@@ -371,6 +373,7 @@ _SIGNATURES = {
     'xa_adam_step_bump': (c_int, [c_void_p, c_void_p]),
     'xa_replay_env_step': (c_int, [POINTER(XaReplayStepArgs), c_void_p]),
     'xa_atari_step': (c_int, [POINTER(XaAtariStepArgs), c_void_p]),
+    'xa_ppo_update_dp_block_bytes': (ctypes.c_size_t, [c_int] * 7),
     'xa_walker_step': (c_int, [POINTER(XaWalkerStepArgs), c_void_p]),
     'xa_mse_grad': (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     'xa_copy_block': (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int, c_int, c_void_p]),

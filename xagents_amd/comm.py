@@ -116,6 +116,55 @@ class PeerAllReduce:
         self._own = None
 
 
+class PeerBlocks:
+    """One uncached HBM block per rank of the default group, IPC-mapped into every rank
+    (the exchange memory of the data-parallel persistent PPO update, csrc/ppo_update.hip);
+    `pointers[r]` is rank r's block as this process addresses it. Zeroed at allocation."""
+
+    def __init__(self, nbytes, group=None):
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self._own = ctypes.c_void_p()
+        self._opened = []
+        call('xa_peer_block_alloc', int(nbytes), ctypes.byref(self._own))
+        handle = (ctypes.c_char * 64)()
+        call('xa_peer_ipc_handle', self._own, handle)
+        handles = [None] * self.world
+        dist.all_gather_object(handles, bytes(handle), group=group)
+        self.pointers = []
+        for p, h in enumerate(handles):
+            if p == self.rank:
+                self.pointers.append(self._own.value)
+                continue
+            blk = ctypes.c_void_p()
+            call('xa_peer_ipc_open', (ctypes.c_char * 64).from_buffer_copy(h), ctypes.byref(blk))
+            self._opened.append(blk)
+            self.pointers.append(blk.value)
+        dist.barrier(group=group)
+
+    def close(self):
+        if self._own is None:
+            return
+        torch.cuda.synchronize()
+        for blk in self._opened:
+            call('xa_peer_ipc_close', blk)
+        self._opened = []
+        dist.barrier(group=self.group)
+        call('xa_peer_block_free', self._own)
+        self._own = None
+
+
+def ranks_per_device(group=None):
+    """The largest number of ranks of the group that share one physical device (1 on a
+    node with one process per GPU; > 1 when ranks share a GPU, as the tests do)."""
+    import socket
+    key = (socket.gethostname(), torch.cuda.current_device())
+    keys = [None] * dist.get_world_size(group)
+    dist.all_gather_object(keys, key, group=group)
+    return max(keys.count(k) for k in keys)
+
+
 def maybe_peer_all_reduce(world_size):
     """A PeerAllReduce for the default group when data-parallel on HIP devices and not
     disabled (XA_PEER_ALLREDUCE=0); None (use RCCL) if the IPC setup fails."""

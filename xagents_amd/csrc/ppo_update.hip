@@ -19,6 +19,12 @@
 //        block), clip + Keras Adam with t = t0 + k + 1 on its register-resident slice
 //        of theta / m / v (ac_tile.hpp ParamSlice), refresh the LDS weight tiles
 //   block 0 stores theta / m / v and the Adam step count at the end.
+// Data parallel (dp_world = W > 1, the DP template variant): phase 0's per-minibatch
+// advantage totals and, in every step, each block's phase-B slice are pushed to every
+// rank's IPC-mapped exchange block and summed in rank order from the own block (system-
+// scope 8-byte {word, tag} pairs, the xa_peer_allreduce protocol) -- so every rank applies
+// the optimizer step of the union of the ranks' minibatches with one cross-GPU hop per step
+// and no launch or collective outside the kernel.
 // Hand-offs follow the write-through protocol (cdna_hip_programming.md Guideline 16,
 // MI355X_MICROARCH.md visibility table row 1): handed-off words are stored write-through
 // (sc1) and loaded with sc1 loads. Inside the step loop the data is its own flag (tagged
@@ -46,7 +52,9 @@ typedef __attribute__((address_space(1))) unsigned long long gu64;
 
 constexpr int kMaxSteps = 512;              // E * M optimizer steps per launch
 constexpr int kCtlBytes = 256;              // control words at the workspace start
-constexpr uint64_t kSpinTicks = 200000000;  // 2 s of the 100 MHz wall clock per hop
+// 10 s of the 100 MHz wall clock per hop: data parallel, a hop also absorbs the other ranks'
+// host-side skew (one process per GPU)
+constexpr uint64_t kSpinTicks = 1000000000;
 // control words (never reset): the phase-0 arrival counter ((gen + 1) G after launch gen)
 // and the abort word (the number gen + 1 of a launch that timed out)
 enum { kCntStats = 0, kAbort = 1 };
@@ -227,6 +235,62 @@ __host__ __device__ inline size_t ws_bytes(int G, int P, int K) {
   return carve(nullptr, G, P, K).total;
 }
 
+// Data-parallel exchange block (one per rank, uncached, IPC-mapped into every rank,
+// zeroed once): (32-bit word, 32-bit tag) pairs written with system-scope 8-byte stores
+// by the pushing rank and polled by the owner (the xa_peer_allreduce protocol, comm.hip)
+//   adv [G][W][K] x 4 pairs: block b's copy of rank r's minibatch-k advantage sums (2 f64)
+//   gsl [2 parity][G][W][CB] x 2 pairs: rank r's reduced slice b (pair column c) at step
+//       parity k & 1 (a rank runs at most one step ahead of any other: step k + 1 needs
+//       every rank's step-(k + 1) slice, pushed only after that rank consumed step k)
+struct DpLayout {
+  size_t adv, gsl, total;
+};
+__host__ __device__ inline DpLayout dp_layout(int G, int W, int K, int CB) {
+  DpLayout d;
+  d.adv = 0;
+  d.gsl = align_up((size_t)G * W * K * 32, 256);
+  d.total = d.gsl + (size_t)2 * G * W * CB * 16;
+  return d;
+}
+XA_DEV void dp_st(void* base, size_t off, uint32_t word, unsigned tag) {
+  __hip_atomic_store((unsigned long long*)((char*)base + off),
+                     (unsigned long long)word | ((unsigned long long)tag << 32), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_SYSTEM);
+}
+XA_DEV unsigned long long dp_ld(const void* base, size_t off) {
+  return __hip_atomic_load((unsigned long long*)((char*)base + off), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// Poll n (<= N) pairs of the own block until every tag equals `tag` (bounded by the wall
+// clock and the abort word, like poll_gran); the words land in w.
+template <int N>
+XA_DEV bool dp_poll(const void* base, const size_t (&off)[N], int n, unsigned tag,
+                    uint32_t (&w)[N], unsigned* ctl, unsigned epoch, int* status) {
+  uint64_t t0 = 0;
+  for (;;) {
+    bool ok = true;
+#pragma unroll
+    for (int u = 0; u < N; ++u)
+      if (u < n) {
+        const unsigned long long v = dp_ld(base, off[u]);
+        w[u] = (uint32_t)v;
+        ok = ok && (unsigned)(v >> 32) == tag;
+      }
+    if (ok) return true;
+    const uint64_t now = wall_clock64();
+    if (t0 == 0) t0 = now;
+    else if (now - t0 > kSpinTicks) {
+      __hip_atomic_store((gu32*)(ctl + kAbort), epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (status) __hip_atomic_store((gu32*)status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    if (__hip_atomic_load((gu32*)(ctl + kAbort), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+        epoch)
+      return false;
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
 struct ShufKeys {
   uint32_t k[4];
   uint32_t half_bits;
@@ -317,7 +381,7 @@ XA_DEV bool hop_wait(unsigned* ctl, int which, unsigned target, unsigned epoch, 
 
 // TS = samples per tile (32; 16 when the minibatch has at most 16 tiles of 32: twice the
 // blocks, half the element-wise work per block and step)
-template <int OBS, int A, int TS>
+template <int OBS, int A, int TS, bool DP>
 __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws ws, int K,
                                                           int n_mb) {
   constexpr int RPT = Dims<OBS, A>::RPT;
@@ -442,9 +506,13 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
     __syncthreads();
   }
   XA_STAMP(33);
+  const int W = DP ? p.dp_world : 1;  // DP: compiled only into the data-parallel kernels
+  const int CB0 = (padded(P) / 2 + G - 1) / G;
+  const DpLayout dl = dp_layout(G, W, K, CB0);
+  bool dp_bad = false;
   for (int k = w; k < K; k += 4) {
     const int m = k % n_mb;
-    const double n = (double)min(MB, B - m * MB);
+    const double n = (double)min(MB, B - m * MB) * (double)W;
     double s1 = 0.0, s2 = 0.0;
     for (int gi = lane; gi < G; gi += 64) {
       s1 += ld_wt(ws.adv + ((size_t)k * G + gi) * 2);
@@ -452,6 +520,36 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
     }
     s1 = xa_wave_sum_f64(s1);
     s2 = xa_wave_sum_f64(s2);
+    if constexpr (DP) {
+      // lane q pushes this rank's totals to rank q (block b's slot); lane r then reads rank
+      // r's totals from the own block; the sums run in rank order
+      const unsigned long long u1 = (unsigned long long)__double_as_longlong(s1);
+      const unsigned long long u2 = (unsigned long long)__double_as_longlong(s2);
+      const size_t o_me = dl.adv + (((size_t)b * W + p.dp_rank) * K + k) * 32;
+      if (lane < W) {
+        void* blk = p.dp_blocks[lane];
+        dp_st(blk, o_me, (uint32_t)u1, epoch);
+        dp_st(blk, o_me + 8, (uint32_t)(u1 >> 32), epoch);
+        dp_st(blk, o_me + 16, (uint32_t)u2, epoch);
+        dp_st(blk, o_me + 24, (uint32_t)(u2 >> 32), epoch);
+      }
+      double v1 = 0.0, v2 = 0.0;
+      if (lane < W) {
+        const size_t o = dl.adv + (((size_t)b * W + lane) * K + k) * 32;
+        const size_t off[4] = {o, o + 8, o + 16, o + 24};
+        uint32_t x[4];
+        dp_bad = dp_bad || !dp_poll<4>(p.dp_blocks[p.dp_rank], off, 4, epoch, x, ws.ctl, epoch,
+                                       p.status);
+        v1 = __longlong_as_double((long long)(((unsigned long long)x[1] << 32) | x[0]));
+        v2 = __longlong_as_double((long long)(((unsigned long long)x[3] << 32) | x[2]));
+      }
+      s1 = 0.0;
+      s2 = 0.0;
+      for (int r = 0; r < W; ++r) {
+        s1 += __shfl(v1, r);
+        s2 += __shfl(v2, r);
+      }
+    }
     if (lane == 0) {
       const double mean = s1 / n;
       const double var = fmax(s2 / n - mean * mean, 0.0);
@@ -460,6 +558,8 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
       U.stat[k][2] = 1.0f / (U.stat[k][1] + p.adv_eps);
     }
   }
+
+  if (__syncthreads_or(dp_bad)) return;
 
   // per-sample inputs of the next tile (threads < TS), fetched one tile ahead -- across
   // minibatch boundaries too: they do not depend on the parameters. The next step's
@@ -554,7 +654,7 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
     cfg.adv_mean = U.stat[k][0];
     cfg.adv_std = U.stat[k][1];
     cfg.adv_rstd = U.stat[k][2];
-    cfg.loss_scale = 1.0f / (float)cnt;
+    cfg.loss_scale = 1.0f / (float)(cnt * W);
     acc.zero();
     XA_STAMP(34);
     // ---- A: forward + loss + backward of this block's tiles ----
@@ -678,6 +778,26 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
     // ---- B: pair columns [c0, c0 + nc): the fixed-order sum over the G rows, or
     // (two-level) over the XCD partials in XCD order -> g (granules) + f64 sum of squares ----
     double sq = 0.0;
+    // pair column c of this block's slice: publish the final value (g granules, the last
+    // step's raw gradient, the sum of squares), or -- data parallel -- stage the rank's local
+    // value in srow for the cross-rank exchange below
+    auto publish = [&](int c, float g0, float g1) {
+      const int cc = c0 + c;
+      st_gran2(g_r, (uint32_t)(16 * cc), g0, g1, tag, true);
+      if (p.grad_out && k == K - 1) {
+        if (2 * cc < P) p.grad_out[2 * cc] = g0;
+        if (2 * cc + 1 < P) p.grad_out[2 * cc + 1] = g1;
+      }
+      sq += (double)g0 * (double)g0 + (double)g1 * (double)g1;
+    };
+    auto emit = [&](int c, float g0, float g1) {
+      if constexpr (DP) {
+        srow[2 * c] = g0;
+        srow[2 * c + 1] = g1;
+      } else {
+        publish(c, g0, g1);
+      }
+    };
     // few columns, few rows per part: thread (part, c) polls its own column's rows part,
     // part + parts, ... (<= kBF granules, one round trip) and sums them in registers in
     // that order -- the flat path's arithmetic without its LDS staging pass
@@ -715,13 +835,7 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
           s1 += U.red[(part * nc + c) * 2 + 1];
         }
         const float g0 = (float)s0, g1 = (float)s1;
-        const int cc = c0 + c;
-        st_gran2(g_r, (uint32_t)(16 * cc), g0, g1, tag, true);
-        if (p.grad_out && k == K - 1) {
-          if (2 * cc < P) p.grad_out[2 * cc] = g0;
-          if (2 * cc + 1 < P) p.grad_out[2 * cc + 1] = g1;
-        }
-        sq += (double)g0 * (double)g0 + (double)g1 * (double)g1;
+        emit(c, g0, g1);
       }
     }
     const bool flat_b = !col_b && !two_level && G * nc <= 256 * kBF;
@@ -769,13 +883,7 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
           }
         }
         const float g0 = (float)t0, g1 = (float)t1;
-        const int cc = c0 + c;
-        st_gran2(g_r, (uint32_t)(16 * cc), g0, g1, tag, true);
-        if (p.grad_out && k == K - 1) {
-          if (2 * cc < P) p.grad_out[2 * cc] = g0;
-          if (2 * cc + 1 < P) p.grad_out[2 * cc + 1] = g1;
-        }
-        sq += (double)g0 * (double)g0 + (double)g1 * (double)g1;
+        emit(c, g0, g1);
       }
     }
     if (nc > 0 && !flat_b && !col_b) {
@@ -837,16 +945,45 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
             t1 += U.red[(r * ncol + tid) * 2 + 1];
           }
           const float g0 = (float)t0, g1 = (float)t1;
-          const int cc = c0 + cb + tid;
-          st_gran2(g_r, (uint32_t)(16 * cc), g0, g1, tag, true);
-          if (p.grad_out && k == K - 1) {
-            if (2 * cc < P) p.grad_out[2 * cc] = g0;
-            if (2 * cc + 1 < P) p.grad_out[2 * cc + 1] = g1;
-          }
-          sq += (double)g0 * (double)g0 + (double)g1 * (double)g1;
+          emit(cb + tid, g0, g1);
         }
         __syncthreads();
       }
+    }
+    if constexpr (DP) {
+      // push this rank's slice to every rank (parity k & 1), then read every rank's slice
+      // from the own block and sum in rank order (f64) -> the union's gradient slice
+      __syncthreads();  // srow holds the local slice
+      const int par = k & 1;
+      for (int c = tid; c < nc; c += 256) {
+        const size_t o = dl.gsl + ((((size_t)par * G + b) * W + p.dp_rank) * CB0 + c) * 16;
+        const uint32_t w0 = __float_as_uint(srow[2 * c]), w1 = __float_as_uint(srow[2 * c + 1]);
+        for (int q = 0; q < W; ++q) {
+          dp_st(p.dp_blocks[q], o, w0, tag);
+          dp_st(p.dp_blocks[q], o + 8, w1, tag);
+        }
+      }
+      bool bad = false;
+      for (int c = tid; c < nc; c += 256) {
+        constexpr int kW2 = 2 * XA_PPO_DP_MAX;
+        size_t off[kW2];
+        uint32_t x[kW2];
+#pragma unroll
+        for (int u = 0; u < kW2; ++u) {
+          const int r = u >> 1;
+          off[u] = r < W ? dl.gsl + ((((size_t)par * G + b) * W + r) * CB0 + c) * 16 + 8 * (u & 1)
+                         : 0;
+        }
+        bad = bad || !dp_poll<kW2>(p.dp_blocks[p.dp_rank], off, 2 * W, tag, x, ws.ctl, epoch,
+                                   p.status);
+        double s0 = 0.0, s1 = 0.0;
+        for (int r = 0; r < W; ++r) {
+          s0 += (double)__uint_as_float(x[2 * r]);
+          s1 += (double)__uint_as_float(x[2 * r + 1]);
+        }
+        publish(c, (float)s0, (float)s1);
+      }
+      if (__syncthreads_or(bad)) return;
     }
     sq = xa_wave_sum_f64(sq);
     if (lane == 0) U.wsum[w] = sq;
@@ -969,7 +1106,7 @@ int capacity() {
     int cus = 0, occ = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       return 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, ppo_update_kernel<OBS, A, S>, 256, 0) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, ppo_update_kernel<OBS, A, S, false>, 256, 0) !=
         hipSuccess)
       return 0;
     cap[dev] = cus * occ;
@@ -993,10 +1130,17 @@ template <int OBS, int A>
 int launch(const XaPpoUpdateArgs* a, int G, int K, int n_mb, hipStream_t s) {
   const int P = offs(OBS, A).P;
   const Ws ws = carve(a->workspace, G, P, K);
-  if (tile_samples(a->mb_size, G) == 16)
-    hipLaunchKernelGGL((ppo_update_kernel<OBS, A, 16>), dim3(G), dim3(256), 0, s, *a, ws, K, n_mb);
-  else
-    hipLaunchKernelGGL((ppo_update_kernel<OBS, A, S>), dim3(G), dim3(256), 0, s, *a, ws, K, n_mb);
+  const bool ts16 = tile_samples(a->mb_size, G) == 16;
+  if (a->dp_world > 1) {
+    if (ts16)
+      hipLaunchKernelGGL((ppo_update_kernel<OBS, A, 16, true>), dim3(G), dim3(256), 0, s, *a, ws, K, n_mb);
+    else
+      hipLaunchKernelGGL((ppo_update_kernel<OBS, A, S, true>), dim3(G), dim3(256), 0, s, *a, ws, K, n_mb);
+  } else if (ts16) {
+    hipLaunchKernelGGL((ppo_update_kernel<OBS, A, 16, false>), dim3(G), dim3(256), 0, s, *a, ws, K, n_mb);
+  } else {
+    hipLaunchKernelGGL((ppo_update_kernel<OBS, A, S, false>), dim3(G), dim3(256), 0, s, *a, ws, K, n_mb);
+  }
   XA_CHECK_LAUNCH("xa_ppo_update");
   return 0;
 }
@@ -1021,6 +1165,15 @@ extern "C" size_t xa_ppo_update_workspace_bytes(int obs_dim, int n_actions, int 
   return ws_bytes(n_blocks, offs(obs_dim, n_actions).P, epochs * n_mb);
 }
 
+extern "C" size_t xa_ppo_update_dp_block_bytes(int obs_dim, int n_actions, int batch,
+                                               int mb_size, int epochs, int n_blocks,
+                                               int world) {
+  if (batch <= 0 || mb_size <= 0 || epochs <= 0 || n_blocks <= 0 || world <= 1) return 0;
+  const int n_mb = (batch + mb_size - 1) / mb_size;
+  const int NP2 = padded(offs(obs_dim, n_actions).P) / 2;
+  return dp_layout(n_blocks, world, epochs * n_mb, (NP2 + n_blocks - 1) / n_blocks).total;
+}
+
 extern "C" int xa_ppo_update(const XaPpoUpdateArgs* a, void* stream) {
   XA_CHECK_ARG(a && a->obs && a->actions && a->old_logp && a->old_values && a->returns &&
                    a->theta && a->adam_m && a->adam_v && a->adam_step && a->workspace,
@@ -1040,6 +1193,12 @@ extern "C" int xa_ppo_update(const XaPpoUpdateArgs* a, void* stream) {
   XA_CHECK_ARG(G > 0 && G <= cap && G <= 256 && G <= (a->mb_size + 15) / 16,
                "xa_ppo_update: n_blocks %d must be in [1, min(resident capacity %d, 16-sample "
                "tiles per minibatch)] (xa_ppo_update_blocks)", G, cap);
+  XA_CHECK_ARG(a->dp_world <= 1 ||
+                   (a->dp_world <= XA_PPO_DP_MAX && a->dp_rank >= 0 && a->dp_rank < a->dp_world),
+               "xa_ppo_update: bad data-parallel rank %d / world %d", a->dp_rank, a->dp_world);
+  for (int r = 0; a->dp_world > 1 && r < a->dp_world; ++r)
+    XA_CHECK_ARG(a->dp_blocks[r] != nullptr && ((uintptr_t)a->dp_blocks[r] & 255) == 0,
+                 "xa_ppo_update: data-parallel exchange block %d is null or not 256-B aligned", r);
   const size_t need = ws_bytes(G, offs(a->obs_dim, a->n_actions).P, K);
   XA_CHECK_ARG(a->workspace_bytes >= need, "xa_ppo_update: workspace %zu bytes < %zu needed",
                a->workspace_bytes, need);

@@ -19,8 +19,9 @@ the global statistics/count, so the update equals a single-GPU update on the uni
 import numpy as np
 import torch
 
-from xagents_amd import kernels
+from xagents_amd import _lib, kernels
 from xagents_amd._lib import XA_RETURNS_GAE, XaPpoUpdateArgs, XaShuffle
+from xagents_amd.comm import PeerBlocks, ranks_per_device
 from xagents_amd.a2c.agent import A2C
 
 
@@ -74,10 +75,25 @@ class PPO(A2C):
         # one process: every optimizer step of the train step in ONE persistent launch
         # (xa_ppo_update); data parallel (a cross-rank exchange per step) or
         # XA_PPO_UPDATE=chain: the per-minibatch launch chain below
+        # data parallel: the persistent launch exchanges the advantage sums and the
+        # gradient slices between ranks itself, over IPC-mapped exchange blocks (needs the
+        # peer path: ranks of one node); otherwise (RCCL only) the chain below
         self.update_mode = 'chain'
-        if os.environ.get('XA_PPO_UPDATE', 'persistent') == 'persistent' and \
-                not self.distributed and E * self.n_mb <= 512:
-            G = kernels.ppo_update_blocks(self.model.obs_dim, self.n_actions, MB)
+        dp_ok = not self.distributed or (getattr(self, 'peer', None) is not None and
+                                         self.world_size <= 16)
+        if os.environ.get('XA_PPO_UPDATE', 'persistent') == 'persistent' and dp_ok and \
+                E * self.n_mb <= 512:
+            obs_dim, A = self.model.obs_dim, self.n_actions
+            G = kernels.ppo_update_blocks(obs_dim, A, MB)
+            if G > 0 and self.distributed:
+                # every rank's workgroups must be resident together: ranks sharing a GPU
+                # split its capacity
+                # (collective: computed once, so a later re-setup stays rank-local)
+                if getattr(self, '_ranks_share', None) is None:
+                    self._ranks_share = ranks_per_device()
+                share = self._ranks_share
+                if share > 1:
+                    G = min(G, kernels.ppo_update_blocks(obs_dim, A, 1 << 24) // share)
             if G > 0:
                 self._setup_persistent(G)
                 return
@@ -176,6 +192,17 @@ class PPO(A2C):
         u.n_blocks = n_blocks
         # the Philox counter bump that ends a train step runs in the launch's last block
         u.bump_counter = int(bool(self.shuffle.rng_counter))
+        u.dp_world, u.dp_rank = 1, 0
+        if self.distributed:
+            if getattr(self, 'dp_blocks', None) is None or self._dp_blocks_key != (B, MB, E,
+                                                                                  n_blocks):
+                nbytes = _lib.load().xa_ppo_update_dp_block_bytes(obs_dim, A, B, MB, E,
+                                                                  n_blocks, self.world_size)
+                self.dp_blocks = PeerBlocks(nbytes)
+                self._dp_blocks_key = (B, MB, E, n_blocks)
+            u.dp_world, u.dp_rank = self.world_size, self.rank
+            for r, ptr in enumerate(self.dp_blocks.pointers):
+                u.dp_blocks[r] = ptr
         self._uargs = u
         self.update_mode = 'persistent'
         self.update_blocks = n_blocks
