@@ -296,3 +296,39 @@ def test_fill_buffers_draws_actions_env_by_env():
     assert list(plan[:, 0]) == draws[0:4]
     assert list(plan[:3, 1]) == draws[4:7]
     assert list(plan[:, 2]) == draws[7:11]
+
+
+def test_ctypes_structs_match_the_c_abi(tmp_path):
+    """Every argument struct the ctypes binding mirrors has the C header's size and field
+    offsets (gcc on include/xagents_hip.h): a drifted mirror would hand kernels shifted
+    pointers."""
+    import ctypes
+    import shutil
+    import subprocess
+    from xagents_amd import _lib
+    if shutil.which('gcc') is None:
+        pytest.skip('gcc not available')
+    structs = [v for k, v in vars(_lib).items() if k.startswith('Xa') and isinstance(v, type)
+               and issubclass(v, ctypes.Structure)]
+    assert len(structs) >= 10
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "xagents_hip.h"',
+             'int main(void) {']
+    for s in structs:
+        lines.append(f'  printf("{s.__name__} size %zu\\n", sizeof({s.__name__}));')
+        for f in s._fields_:
+            lines.append(f'  printf("{s.__name__} {f[0]} %zu\\n", offsetof({s.__name__}, {f[0]}));')
+    lines += ['  return 0;', '}']
+    src = tmp_path / 'abi.c'
+    src.write_text('\n'.join(lines) + '\n')
+    exe = tmp_path / 'abi'
+    subprocess.run(['gcc', '-std=c11', '-I', str(ROOT / 'include'), str(src), '-o', str(exe)],
+                   check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout
+    got = {}
+    for line in out.splitlines():
+        name, field, val = line.split()
+        got[(name, field)] = int(val)
+    for s in structs:
+        assert got[(s.__name__, 'size')] == ctypes.sizeof(s), s.__name__
+        for f in s._fields_:
+            assert got[(s.__name__, f[0])] == getattr(s, f[0]).offset, (s.__name__, f[0])
