@@ -238,7 +238,7 @@ def dense_dx_roofline(executors, step):
         return None
     ms = sum(t for t, _ in full) / len(full)
     tf = full[0][1] / (ms * 1e-3) / 1e12
-    return {'kernel': f'xa_gemm {big[0][0]} (MFMA f32 tile GEMM, ReLU-gate epilogue)',
+    return {'kernel': f'xa_gemm {big[0][0]} (MFMA f32; small-M resident-A kernel at M <= 64, tile kernels above; ReLU-gate epilogue)',
             'bound': 'mfma', 'achieved': round(tf, 3), 'peak': 157.3, 'unit': 'TFLOP/s',
             'frac': round(tf / 157.3, 4), 'traffic': None, 'launch_ms': round(ms, 4),
             'note': f'2 M N K FLOP per launch, mean of {len(full)} launches; the 77 MB '
