@@ -418,11 +418,61 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
   const int t0 = *p.adam_step;
   for (int k = tid; k < K; k += 256)
     U.alpha[k] = adam_alpha(p.adam.lr, p.adam.beta1, p.adam.beta2, t0 + k + 1);
+  // with the inputs preloaded: all 256 threads gather the (step, sample) items and park each
+  // advantage in LDS (U.red, free until phase B), then a wave per step sums them in the
+  // lane-strided order of the loop below (bit-identical sums, all lanes busy in the gather)
+  float* const advs = reinterpret_cast<float*>(U.red);
+  const int per_k = TPB * TS;
+  if (pre) {
+    for (int i = tid; i < K * per_k; i += 256) {
+      const int k = i / per_k, j = i - k * per_k;
+      const int e = k / n_mb, m = k - e * n_mb;
+      const int start = m * MB, cnt = min(MB, B - start);
+      const int n_tiles = (cnt + TS - 1) / TS;
+      const int mine = n_tiles > b ? (n_tiles - b + G - 1) / G : 0;
+      const int q = (b + (j / TS) * G) * TS + (j % TS);
+      float* slot = &U.pre[(size_t)i * (OBS + 4)];
+      if (!(j < mine * TS && q < cnt)) {
+        // padding: zero inputs (they meet zero gradients, never NaNs)
+#pragma unroll
+        for (int kk = 0; kk < OBS + 4; ++kk) slot[kk] = 0.0f;
+        slot[OBS] = -1.0f;
+        advs[i] = 0.0f;
+        continue;
+      }
+      const ShufKeys keys = shuf_keys(p.shuffle, ctr, e, B);
+      const int idx = shuf_index(p.shuffle, keys, e, B, start + q);
+      const float ret = p.returns[idx], oldv = p.old_values[idx];
+      advs[i] = ret - oldv;
+#pragma unroll
+      for (int kk = 0; kk < OBS; ++kk) slot[kk] = p.obs[(size_t)idx * OBS + kk];
+      slot[OBS] = (float)p.actions[idx];
+      slot[OBS + 1] = ret;
+      slot[OBS + 2] = oldv;
+      slot[OBS + 3] = p.old_logp[idx];
+    }
+    __syncthreads();
+  }
 #ifndef XA_ABL_P0
   for (int k = w; k < K; k += 4) {
 #else
   for (int k = w; k < 0; k += 4) {
 #endif
+    if (pre) {
+      double s1 = 0.0, s2 = 0.0;
+      for (int j = lane; j < per_k; j += 64) {
+        const double a = (double)advs[k * per_k + j];
+        s1 += a;
+        s2 += a * a;
+      }
+      s1 = xa_wave_sum_f64(s1);
+      s2 = xa_wave_sum_f64(s2);
+      if (lane == 0) {
+        st_wt(ws.adv + ((size_t)k * G + b) * 2, s1);
+        st_wt(ws.adv + ((size_t)k * G + b) * 2 + 1, s2);
+      }
+      continue;
+    }
     const int e = k / n_mb, m = k - e * n_mb;
     const int start = m * MB, cnt = min(MB, B - start);
     const int n_tiles = (cnt + TS - 1) / TS;
