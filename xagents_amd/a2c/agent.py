@@ -307,8 +307,9 @@ class A2C(ExecutorActorCritic, OnPolicy):
         self._update_impl()
 
     def _capture(self):
-        """Capture the rollout and the update as two hipGraphs (replayed back to back;
-        two graphs so the update can be timed on its own). Data-parallel steps are
+        """Capture the rollout, the update, and the two back to back as hipGraphs (a
+        train step replays the combined graph; the per-phase graphs serve the event-timed
+        pass, so the update can be timed on its own). Data-parallel steps are
         captured only when every exchange goes through the peer kernel: a torch
         collective inside a capture (gloo, or RCCL where capture is unsupported)
         invalidates the capture and the stream, so those steps run eagerly."""
@@ -318,10 +319,14 @@ class A2C(ExecutorActorCritic, OnPolicy):
             return
         try:
             graphs = []
-            for fn in (self._rollout_impl, self._update_impl):
+            # rollout, update, and both back to back: the timed loop replays the third (one
+            # graph launch per train step), the per-phase event pass the first two
+            for fns in ((self._rollout_impl,), (self._update_impl,),
+                        (self._rollout_impl, self._update_impl)):
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
-                    fn()
+                    for fn in fns:
+                        fn()
                 graphs.append(g)
             self._graph = graphs
         except Exception as exc:  # collectives that refuse capture -> eager launches
@@ -350,7 +355,10 @@ class A2C(ExecutorActorCritic, OnPolicy):
         self._sync_stats_copy()
         if self._rollout_ev is None and self.stats_side_stream:
             self._rollout_ev = torch.cuda.Event()
-        if self.use_graph and self._graph is not None:
+        if self.use_graph and self._graph is not None and not events and \
+                not self.stats_side_stream:
+            self._graph[2].replay()
+        elif self.use_graph and self._graph is not None:
             rec(0)
             self._graph[0].replay()
             if self.stats_side_stream:
