@@ -787,7 +787,7 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
         if (rg < RG && cb + cq < xnc) {
           const int c = xc0 + cb + cq;
           double a0 = 0.0, a1 = 0.0;
-          constexpr int kB = 8;
+          constexpr int kB = kBF;  // 32 XCD members over 3 row groups: one poll round
           for (int j0 = rg; j0 < ng && !bad; j0 += RG * kB) {
             uint32_t off[kB];
             f32x4v x[kB];
