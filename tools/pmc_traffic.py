@@ -12,7 +12,7 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parents[1]
 KERNELS = {'ac_grad': 'ac_grad_kernel<4, 2>', 'rollout': 'mlp_rollout_kernel<4, 2, true>',
            'grad_reduce': 'grad_reduce_kernel', 'minibatch': 'minibatch_kernel',
-           'ppo_update': 'ppo_update_kernel<4, 2>'}
+           'ppo_update': 'ppo_update_kernel<4, 2,'}
 
 
 def per_kernel(counter, src):
