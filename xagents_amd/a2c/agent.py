@@ -113,7 +113,7 @@ class A2C(ExecutorActorCritic, OnPolicy):
         # overlap the update (C2: 0.43 -> 0.41 ms per step), but the first copies of a
         # process's side stream stall the host ~7 ms twice at a random early step
         # (tools/diag_bench_steps.py), which a 20-step timed loop cannot absorb.
-        self.stats_side_stream = False
+        self.stats_side_stream = os.environ.get('XA_STATS_SIDE_STREAM', '0') == '1'
         seed = self.seed if self.seed is not None else int(np.random.SeedSequence().entropy % 2**63)
         self.rng_seed = (int(seed) * 1000003 + self.rank * 7919 + 17) % 2**64
         P = self.model.n_params
