@@ -104,7 +104,17 @@ float xo_tanhf(float x) {
   float q = fmaf(x2, 1.19825839466702e-06f, 1.18534705686654e-04f);
   q = fmaf(x2, q, 2.26843463243900e-03f);
   q = fmaf(x2, q, 4.89352518554385e-03f);
-  return p / q;
+  /* the quotient as the kernels form it: bit-trick seed, two Newton steps, one residual
+     correction (xa_common.hpp xa_tanhf) */
+  int32_t qi;
+  memcpy(&qi, &q, 4);
+  qi = 0x7EF311C3 - qi;
+  float r;
+  memcpy(&r, &qi, 4);
+  r = fmaf(r, fmaf(-q, r, 1.0f), r);
+  r = fmaf(r, fmaf(-q, r, 1.0f), r);
+  float t = p * r;
+  return fmaf(r, fmaf(-q, t, p), t);
 }
 
 /* b^t by binary exponentiation in f64 (the kernels' xa_powi) */

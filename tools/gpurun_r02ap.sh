@@ -1,0 +1,13 @@
+#!/bin/bash
+# division-free tanh: every -m gpu test (the rollout / oracle bit-exact ones included),
+# then two bench lines (16-env headline + C2) (no CPU baseline)
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-.}"
+mkdir -p gpurun_out
+T=${TAG:-r02ap}
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+  > gpurun_out/${T}_pytest.log 2>&1 &&
+for i in 1 2; do
+timeout -k 10 200 python bench.py --steps 30 --warmup 5 --cpu-baseline-seconds 0 \
+  > gpurun_out/${T}_bench$i.json 2> gpurun_out/${T}_bench$i.err || exit 5
+done
