@@ -605,6 +605,23 @@ typedef struct XaWalkerStepArgs {
 
 int xa_walker_step(const XaWalkerStepArgs* args, void* stream);
 
+/* Episode statistics to the host (BaseAgent.step_envs bookkeeping, xagents/base.py:388-426):
+ * copies n_segments device buffers (bytes a multiple of 4) into pinned host memory in ONE
+ * launch on `stream`. dst[i] are the DEVICE addresses of the pinned host buffers, from
+ * xa_host_device_pointer. Completion = the stream's next event. */
+#define XA_HOST_COPY_MAX 4
+typedef struct XaHostCopyArgs {
+  int n_segments;
+  const void* src[XA_HOST_COPY_MAX];
+  void* dst[XA_HOST_COPY_MAX];
+  int64_t bytes[XA_HOST_COPY_MAX];
+} XaHostCopyArgs;
+
+int xa_copy_to_host(const XaHostCopyArgs* args, void* stream);
+
+/* *dev = the device address of pinned host memory `host` (hipHostGetDevicePointer). */
+int xa_host_device_pointer(void* host, void** dev);
+
 /* tf.keras.losses.MSE(target, pred) per row, gradient of the batch sum (minimize on a
  * [B] loss): dpred = 2 (pred - target) / n_out; loss[b] (optional). */
 int xa_mse_grad(const float* pred, const float* target, int batch, int n_out, float* dpred,

@@ -440,3 +440,34 @@ def test_pending_optimizer_step_in_ac_grad_prologue(device):
     for got, ref, name in zip(outs, (th_r, m_r, v_r), ('theta', 'm', 'v')):
         np.testing.assert_array_equal(N(got), N(ref), err_msg=name)
     np.testing.assert_array_equal(N(part_got), N(part_ref))
+
+
+@pytest.mark.parametrize('sizes', [(16 * 129, 16 * 128, 1), (256 * 129, 256 * 128), (1,), (3, 5)])
+def test_copy_to_host_segments_bit_exact(device, sizes):
+    """xa_copy_to_host (episode statistics, base.py _copy_to_host): every segment lands in
+    its pinned host buffer word for word (f32 bit patterns incl. NaN payloads, int32)."""
+    import ctypes
+    g = torch.Generator().manual_seed(len(sizes))
+    src, dst = [], []
+    for i, n in enumerate(sizes):
+        if i == 2:
+            h = torch.randint(-2**31, 2**31 - 1, (n,), dtype=torch.int32, generator=g)
+        else:
+            h = torch.randn(n, generator=g)
+            if n:
+                h.view(torch.int32)[::7] = 0x7fc01234  # quiet NaN with a payload
+        src.append(h.to(device))
+        dst.append(torch.full_like(h, 0).pin_memory())
+    a = _lib.XaHostCopyArgs()
+    a.n_segments = len(sizes)
+    for i, (d, h) in enumerate(zip(src, dst)):
+        dev = ctypes.c_void_p()
+        _lib.call('xa_host_device_pointer', ctypes.c_void_p(h.data_ptr()), ctypes.byref(dev))
+        a.src[i], a.dst[i], a.bytes[i] = d.data_ptr(), dev.value, d.numel() * d.element_size()
+    _lib.call('xa_copy_to_host', ctypes.byref(a), _lib.stream())
+    torch.cuda.synchronize()
+    for d, h in zip(src, dst):
+        assert torch.equal(d.cpu().view(torch.int32), h.view(torch.int32))
+    a.bytes[0] = 6  # not a multiple of 4
+    with pytest.raises(_lib.HipLibraryError, match='multiple of 4'):
+        _lib.call('xa_copy_to_host', ctypes.byref(a), _lib.stream())

@@ -213,6 +213,13 @@ class XaWalkerStepArgs(Structure):
     ]
 
 
+class XaHostCopyArgs(Structure):
+    _fields_ = [
+        ('n_segments', c_int), ('src', c_void_p * 4), ('dst', c_void_p * 4),
+        ('bytes', c_int64 * 4),
+    ]
+
+
 class XaTrpoHeadArgs(Structure):
     _fields_ = [
         ('n', c_int), ('n_actions', c_int),
@@ -375,6 +382,8 @@ _SIGNATURES = {
     'xa_atari_step': (c_int, [POINTER(XaAtariStepArgs), c_void_p]),
     'xa_ppo_update_dp_block_bytes': (ctypes.c_size_t, [c_int] * 7),
     'xa_walker_step': (c_int, [POINTER(XaWalkerStepArgs), c_void_p]),
+    'xa_copy_to_host': (c_int, [POINTER(XaHostCopyArgs), c_void_p]),
+    'xa_host_device_pointer': (c_int, [c_void_p, POINTER(c_void_p)]),
     'xa_mse_grad': (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     'xa_copy_block': (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int, c_int, c_void_p]),
     'xa_categorical': (
