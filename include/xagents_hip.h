@@ -293,22 +293,31 @@ int xa_clip_adam(float* theta, float* adam_m, float* adam_v, const float* grad, 
  * and Keras Adam with t = *adam_step + k + 1 -- the arithmetic of the per-minibatch
  * chain xa_ppo_minibatches -> [xa_ac_grad -> xa_grad_reduce] x E*M -> xa_clip_adam,
  * up to the f64 summation order of the gradient and advantage sums.
- * In place on theta / adam_m / adam_v; *adam_step += E*M. One process (no
- * cross-rank exchange inside; data-parallel steps use the chain).
+ * In place on theta / adam_m / adam_v; *adam_step += E*M. Data parallel (dp_world > 1,
+ * below): the cross-rank exchange runs inside the launch.
  * n_blocks: xa_ppo_update_blocks(obs_dim, n_actions, mb_size) (every block must be
  * resident at once: the blocks exchange gradient rows inside the launch), at most one
  * per 16 samples of a minibatch. More blocks than 32-sample tiles select 16-sample
- * tiles (the default for minibatches of <= 512 samples).
+ * tiles (the default for minibatches of <= 512 samples). Grids of < 64 blocks run
+ * XCD-local when 8 x n_blocks blocks fit the device: 8 x n_blocks workgroups are
+ * launched, the n_blocks that land first on one XCD do the update and keep every
+ * hand-off in that XCD's L2, the rest leave at once (placement: XA_PPO_PLACE_*).
  * workspace: device memory, 256-byte aligned, >= xa_ppo_update_workspace_bytes(...),
  * owned by the caller, ZEROED ONCE at allocation and then reused by every launch
  * (nothing in it is reset between launches: a launch counter kept in it numbers the
  * launches, and the exchange words carry tags unique per launch and step).
  * loss_out (optional) [E*n_mb, n_blocks, 4]: per-block (pg, value, entropy, count) sums.
  * grad_out (optional) [P]: the last optimizer step's reduced gradient (before the clip).
- * status (optional device int): set to 1 if an in-launch exchange timed out (2 s);
- * the parameters are then invalid. adam.grad_scale is not used (must be 1).
+ * status (optional device int): set to 1 if an in-launch exchange timed out (10 s per
+ * hop); the parameters are then invalid. adam.grad_scale is not used (must be 1).
+ * theta_trace / grad_trace (optional, diagnostic) [E*n_mb, P]: theta at the start of
+ * every optimizer step k and step k's reduced gradient (before the clip).
  */
 #define XA_PPO_DP_MAX 16
+#define XA_PPO_PLACE_AUTO 0   /* XCD-local when eligible; not for data-parallel launches */
+#define XA_PPO_PLACE_SPREAD 1 /* never XCD-local */
+#define XA_PPO_PLACE_LOCAL 2  /* XCD-local when eligible, data parallel included (every
+                                 rank on its own GPU) */
 typedef struct XaPpoUpdateArgs {
   int obs_dim, n_actions;
   int batch, mb_size, epochs;
@@ -342,6 +351,9 @@ typedef struct XaPpoUpdateArgs {
    * must be resident at once. */
   int dp_world, dp_rank;
   void* dp_blocks[XA_PPO_DP_MAX];
+  int placement;      /* XA_PPO_PLACE_* */
+  float* theta_trace; /* optional diagnostic outputs (above) */
+  float* grad_trace;
 } XaPpoUpdateArgs;
 
 int xa_ppo_update_blocks(int obs_dim, int n_actions, int mb_size);

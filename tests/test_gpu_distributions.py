@@ -59,6 +59,23 @@ def test_diag_gaussian_kernel(device):
     x = out.cpu().numpy()
     assert abs(x.mean()) < 0.02 and abs(x.std() - 1.0) < 0.02
     assert abs(np.corrcoef(x[:, 0], x[:, 1])[0, 1]) < 0.03
+    # consecutive train-step counters draw independent noise: no dimension of counter c + 1
+    # repeats (or correlates with) any dimension of counter c (a 4-D action, as the
+    # BipedalWalker stand-in's)
+    ctr.fill_(6)
+    out2 = torch.empty(N, d, device=device)
+    call('xa_diag_gaussian', zero.data_ptr(), d, N, d, None, ctr.data_ptr(), 1234, 3, None, d,
+         out2.data_ptr(), None, None, 1, stream())
+    ctr.fill_(7)
+    out3 = torch.empty(N, d, device=device)
+    call('xa_diag_gaussian', zero.data_ptr(), d, N, d, None, ctr.data_ptr(), 1234, 3, None, d,
+         out3.data_ptr(), None, None, 1, stream())
+    y, z = out2.cpu().numpy(), out3.cpu().numpy()
+    for j in range(d):
+        for jj in range(d):
+            assert abs(np.corrcoef(y[:, j], z[:, jj])[0, 1]) < 0.03, (j, jj)
+            if j != jj:
+                assert abs(np.corrcoef(y[:, j], y[:, jj])[0, 1]) < 0.03, (j, jj)
 
 
 def _heads_f64(out_a, v, act, oldlp, oldv, ret, kind, dist, clip=0.1, ent_coef=0.01,

@@ -30,8 +30,11 @@ def _theta0(seed):
     return (rng.standard_normal(4675) * 0.2).astype(np.float32)
 
 
-def run_update(theta0, bufs, mb_size, epochs, perm=None, n_blocks=None, want=True):
-    """Call xa_ppo_update directly; returns theta, m, v, step, grad_out, loss_out, status."""
+def run_update(theta0, bufs, mb_size, epochs, perm=None, n_blocks=None, want=True, trace=False,
+               placement=0):
+    """Call xa_ppo_update directly; returns theta, m, v, step, grad_out, loss_out, status
+    (and, with trace, theta at the start of every optimizer step and every step's
+    reduced gradient)."""
     from xagents_amd import kernels
     from xagents_amd._lib import XaPpoUpdateArgs, XaShuffle
     obs, act, logp, val, ret = (torch.as_tensor(x, device='cuda') for x in bufs)
@@ -72,11 +75,19 @@ def run_update(theta0, bufs, mb_size, epochs, perm=None, n_blocks=None, want=Tru
     u.grad_out = grad.data_ptr() if want else None
     u.status = status.data_ptr()
     u.n_blocks = G
+    u.placement = placement
+    if trace:
+        th_tr = torch.zeros(K, theta.numel(), dtype=torch.float32, device='cuda')
+        g_tr = torch.zeros_like(th_tr)
+        u.theta_trace, u.grad_trace = th_tr.data_ptr(), g_tr.data_ptr()
     kernels.ppo_update(u)
     torch.cuda.synchronize()
-    return dict(theta=theta.cpu().numpy(), m=m.cpu().numpy(), v=v.cpu().numpy(),
-                step=int(step.item()), grad=grad.cpu().numpy(), loss=loss.cpu().numpy(),
-                status=int(status.item()), G=G, K=K)
+    out = dict(theta=theta.cpu().numpy(), m=m.cpu().numpy(), v=v.cpu().numpy(),
+               step=int(step.item()), grad=grad.cpu().numpy(), loss=loss.cpu().numpy(),
+               status=int(status.item()), G=G, K=K)
+    if trace:
+        out['theta_trace'], out['grad_trace'] = th_tr.cpu().numpy(), g_tr.cpu().numpy()
+    return out
 
 
 def f64_trajectory(theta0, bufs, mb_size, perms):
@@ -253,3 +264,53 @@ def test_bench_loop_graph_replays_equal_eager(device):
     assert int(a.device_status.item()) == 0
     assert int(a.model.optimizer.iterations.item()) == 40 * 16
     np.testing.assert_array_equal(a.model.theta.cpu().numpy(), b.model.theta.cpu().numpy())
+
+
+@pytest.mark.parametrize('B,mb,placement', [(2048, 512, 0), (2048, 512, 1), (32768, 8192, 0)])
+def test_every_optimizer_step_teacher_forced_vs_f64(device, B, mb, placement):
+    """All E x M = 16 optimizer steps of one launch at the headline shape (16 envs x 128
+    steps, minibatches of 512, XCD-local (placement 0) and spread (1)) and at C2 (32768 /
+    8192), teacher-forced: step k's reduced gradient and loss sums are checked against the
+    float64 restatement evaluated at the device's own theta_k (1e-5 rel), and
+    theta_{k+1} against Keras Adam applied in float64 to theta_k with the device's
+    gradient (moments carried in f64). This pins every step the headline runs, not only
+    the first (ppo/agent.py:157-191 calling update_gradients, 96-137)."""
+    E = 4
+    bufs = _rollout_buffers(B, seed=B + 17)
+    obs, act, logp, val, ret = bufs
+    theta0 = _theta0(6)
+    out = run_update(theta0, bufs, mb, E, trace=True, placement=placement)
+    K = out['K']
+    assert out['status'] == 0 and out['step'] == K == 16
+    th_tr, g_tr = out['theta_trace'].astype(np.float64), out['grad_trace'].astype(np.float64)
+    np.testing.assert_array_equal(out['theta_trace'][0], theta0)
+    perms = [oracle.shuffle_perm(B, e, 12345, 0) for e in range(E)]
+    n_mb = B // mb
+    m64, v64 = np.zeros(theta0.size), np.zeros(theta0.size)
+    worst = dict(grad=0.0, pg=0.0, vl=0.0, ent=0.0, step=0.0)
+    for k in range(K):
+        e, mi = divmod(k, n_mb)
+        idx = perms[e][mi * mb:(mi + 1) * mb]
+        adv = oracle.normalize_advantages(ret[idx], val[idx])
+        tm, g = oracle.ac_loss_grad_f64(th_tr[k], obs[idx], act[idx], ret[idx], val[idx], A,
+                                        'ppo', logp[idx], adv)
+        worst['grad'] = max(worst['grad'], _rel(g_tr[k], g))
+        ls = out['loss'][k].astype(np.float64).sum(axis=0)
+        assert ls[3] == mb
+        worst['pg'] = max(worst['pg'], abs(ls[0] - tm['pg_sum']) / max(abs(tm['pg_sum']), mb))
+        worst['vl'] = max(worst['vl'], abs(ls[1] - tm['vl_sum']) / abs(tm['vl_sum']))
+        worst['ent'] = max(worst['ent'], abs(ls[2] - tm['ent_sum']) / abs(tm['ent_sum']))
+        # the optimizer step with the device's own gradient
+        gc, _ = oracle.clip_by_global_norm_f64(g_tr[k], CLIP_G)
+        th_next, m64, v64 = oracle.keras_adam_f64(th_tr[k], m64, v64, gc, k + 1, LR, B1, B2, EPS)
+        dev_next = th_tr[k + 1] if k + 1 < K else out['theta'].astype(np.float64)
+        # theta is f32: the step (~lr) is resolved only to f32's spacing at |theta|, so the
+        # bound is that rounding plus 1e-5 of the step itself, element by element
+        step = th_next - th_tr[k]
+        bound = np.spacing(np.abs(th_next).astype(np.float32)).astype(np.float64) + \
+            1e-5 * np.abs(step)
+        worst['step'] = max(worst['step'], float(np.max(np.abs(dev_next - th_next) / bound)))
+    print('worst relative errors over the 16 steps (step: in units of its bound):', worst)
+    assert worst['grad'] < 1e-5
+    assert worst['pg'] < 1e-5 and worst['vl'] < 1e-5 and worst['ent'] < 1e-5
+    assert worst['step'] <= 1.0

@@ -1,0 +1,79 @@
+#!/bin/bash
+# One GPU session on the gpurun box, as a list of named steps (outputs under gpurun_out/,
+# prefixed with $TAG). Every GPU step has its own time limit; pytest exit 1 (test
+# failures) lets the session go on, any other failure (fault, abort, time limit) ends it.
+#   usage: TAG=r03a bash tools/gpu_steps.sh update bench prof ...
+# steps:
+#   update   tests/test_gpu_ppo_update.py
+#   dp       tests/test_gpu_dp.py + tests/test_gpu_peer.py
+#   gpu      the whole -m gpu suite
+#   smoke    __graft_entry__.smoke()
+#   bench    the default bench line (with the CPU baseline)
+#   ab       bench lines without the CPU baseline: XCD-local vs spread persistent update
+#   prof     rocprofv3 --kernel-trace --stats of the default bench (no CPU baseline)
+#   pmc      FETCH_SIZE / WRITE_SIZE passes per shape (tools/gpurun_pmc_shapes.sh)
+#   c3 c4 c5 secondary bench lines
+#   stamps   per-phase stamp shares of the persistent update (tools/diag_ppo_update.py)
+#   trace    per-block phase timeline of the persistent update (tools/trace_ppo_update.py)
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-.}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+T=${TAG:-r03}
+R=$PWD
+PYT="python -u -m pytest -v --timeout 180 --timeout-method thread"
+
+run_pytest() {  # name, limit, args...
+  local name=$1 lim=$2
+  shift 2
+  timeout -k 10 "$lim" $PYT "$@" > gpurun_out/${T}_${name}.log 2>&1
+  local rc=$?
+  tail -3 gpurun_out/${T}_${name}.log
+  case $rc in 0|1) return 0 ;; *) echo "step $name: exit $rc"; exit $rc ;; esac
+}
+
+run() {  # name, limit, command... (stdout -> .json / .log, stderr -> .err)
+  local name=$1 lim=$2
+  shift 2
+  timeout -k 10 "$lim" "$@" > gpurun_out/${T}_${name}.out 2> gpurun_out/${T}_${name}.err
+  local rc=$?
+  tail -2 gpurun_out/${T}_${name}.out
+  if [ $rc -ne 0 ]; then echo "step $name: exit $rc"; tail -5 gpurun_out/${T}_${name}.err; exit $rc; fi
+}
+
+for step in "$@"; do
+  echo "== $step $(date +%T)"
+  case $step in
+    update) run_pytest update 400 tests/test_gpu_ppo_update.py ;;
+    dp) run_pytest dp 500 tests/test_gpu_dp.py tests/test_gpu_peer.py ;;
+    gpu) run_pytest gpu 1000 tests -m gpu ;;
+    smoke) run smoke 180 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 300 python bench.py --steps 20 --warmup 5 ;;
+    ab)
+      run ab_local 200 python bench.py --steps 40 --warmup 5 --cpu-baseline-seconds 0
+      XA_PPO_LOCAL=0 run ab_spread 200 python bench.py --steps 40 --warmup 5 --cpu-baseline-seconds 0
+      run ab_local2 200 python bench.py --steps 40 --warmup 5 --cpu-baseline-seconds 0 ;;
+    prof)
+      (cd /tmp && timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/${T}_prof \
+        -o run --output-format csv -- python $R/bench.py --steps 20 --warmup 5 \
+        --cpu-baseline-seconds 0 > $R/gpurun_out/${T}_prof_bench.json 2>&1) || exit $? ;;
+    pmc) TAG=${T} timeout -k 10 600 bash tools/gpurun_pmc_shapes.sh > gpurun_out/${T}_pmc.log 2>&1 || exit $? ;;
+    c3) run c3 300 python bench.py --config c3 --steps 30 --warmup 5 ;;
+    c4) run c4 400 python bench.py --config c4 --steps 4 --warmup 1 ;;
+    c5) run c5 300 python bench.py --config c5 --steps 30 --warmup 5 ;;
+    stamps) run stamps 200 python tools/diag_ppo_update.py --no-build ;;
+    trace)
+      run trace 200 python tools/trace_ppo_update.py --no-build 16 256
+      run trace_spread 200 python tools/trace_ppo_update.py --no-build --spread 16 ;;
+    icache)
+      # instruction-cache counters of the 16-env update (one counter per pass)
+      (cd /tmp && rocprofv3 -L > $R/gpurun_out/${T}_counters.txt 2>&1) || true
+      for c in $(grep -oE '\bSQC?_(ICACHE|IFETCH|INST_CACHE)[A-Z_]*' gpurun_out/${T}_counters.txt | sort -u | head -4); do
+        (cd /tmp && timeout -s KILL 90 rocprofv3 --pmc $c -d $R/gpurun_out/${T}_pmc_$c -o run \
+          --output-format csv -- python $R/bench.py --n-envs 16 --no-c2 --steps 2 --warmup 1 \
+          --cpu-baseline-seconds 0 --no-graph > $R/gpurun_out/${T}_pmc_$c.log 2>&1) || exit $?
+      done ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "== done $(date +%T)"

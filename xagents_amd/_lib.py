@@ -24,6 +24,9 @@ XA_LOSS_A2C = 1
 XA_DIST_CATEGORICAL = 0
 XA_DIST_DIAG_GAUSSIAN = 1
 MLP_HIDDEN = 64
+XA_PPO_PLACE_AUTO = 0
+XA_PPO_PLACE_SPREAD = 1
+XA_PPO_PLACE_LOCAL = 2
 
 
 class XaRolloutArgs(Structure):
@@ -152,6 +155,8 @@ class XaPpoUpdateArgs(Structure):
         ('bump_counter', c_int),
         ('dp_world', c_int), ('dp_rank', c_int),
         ('dp_blocks', c_void_p * 16),
+        ('placement', c_int),
+        ('theta_trace', c_void_p), ('grad_trace', c_void_p),
     ]
 
 

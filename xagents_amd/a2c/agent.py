@@ -217,6 +217,10 @@ class A2C(ExecutorActorCritic, OnPolicy):
         for t in (self.model.theta, opt.m, opt.v, opt.iterations):
             dist.broadcast(t, 0)
         self._graph = None
+        if not self.executor_path:
+            # PPO's persistent update exchanges through IPC blocks too: re-plan the update
+            # without the peer path (the per-minibatch chain over RCCL)
+            self._setup_update()
         return 'rccl'
 
     def _adam_tail(self, bump):

@@ -22,6 +22,7 @@ from time import perf_counter
 
 import numpy as np
 import torch
+import torch.distributed as dist
 
 from xagents_amd.envs import Box, Discrete
 from xagents_amd.utils.common import write_from_dict
@@ -193,9 +194,15 @@ class BaseAgent(ABC):
                 current_lr = model.optimizer.learning_rate
                 new_lr = current_lr * self.plateau_reduce_factor
             self.display_message(f'Learning rate reduced {current_lr} -> {new_lr}')
-            # the reference only updates the LAST output model (xagents/base.py:277-284)
-            self.output_models[-1].optimizer.learning_rate = new_lr
-            self._on_lr_change()
+            if getattr(self, 'distributed', False):
+                # data parallel: rank 0 decides, every rank applies it at the same train
+                # step (_dp_sync), so learning rates and launch state stay identical
+                if self.rank == 0:
+                    self._pending_lr = new_lr
+            else:
+                # the reference only updates the LAST output model (xagents/base.py:277-284)
+                self.output_models[-1].optimizer.learning_rate = new_lr
+                self._on_lr_change()
             self.plateau_count = 0
             self.early_stop_count += 1
         self.frame_speed = (self.steps - self.last_reset_step) / (
@@ -208,6 +215,42 @@ class BaseAgent(ABC):
 
     def _on_lr_change(self):
         """Subclasses holding captured graphs re-capture them (lr is a kernel arg)."""
+
+    # data parallel: the host decisions that must agree across ranks -- plateau learning-
+    # rate reductions and stopping on the target reward / early-stop patience, which the
+    # reference's one process takes from its own rewards -- are rank 0's, exchanged every
+    # DP_SYNC_STEPS train steps of fit() and applied by every rank at the same step
+    DP_SYNC_STEPS = 64
+
+    def _dp_sync(self, stop_local):
+        """One small collective (MAX over ranks): rank 0's pending learning rate and stop
+        decision. Returns the agreed stop decision."""
+        lr0 = getattr(self, '_pending_lr', None)
+        t = torch.tensor([lr0 if (self.rank == 0 and lr0 is not None) else -1.0,
+                          1.0 if (self.rank == 0 and stop_local) else 0.0], dtype=torch.float64)
+        if dist.get_backend() != 'gloo':
+            t = t.to(self.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        lr, stop = float(t[0].item()), bool(t[1].item() > 0)
+        self._pending_lr = None
+        if lr > 0:
+            self.output_models[-1].optimizer.learning_rate = lr
+            self._on_lr_change()
+        return stop
+
+    def _fit_done(self):
+        """training_done(), collective in data-parallel runs: max_steps is identical on every
+        rank (equal step counts); the reward-based decisions are rank 0's (_dp_sync)."""
+        done = self.training_done()
+        if not getattr(self, 'distributed', False):
+            return done
+        if self.max_steps and self.steps >= self.max_steps:
+            return True
+        self._fit_steps = getattr(self, '_fit_steps', 0) + 1
+        every = int(os.environ.get('XA_DP_SYNC_STEPS', self.DP_SYNC_STEPS))
+        if self._fit_steps % every:
+            return False
+        return self._dp_sync(done)
 
     def report_rewards(self):
         self.trial.report(np.mean(self.total_rewards), self.reported_rewards)
@@ -495,7 +538,7 @@ class BaseAgent(ABC):
         self.init_training(target_reward, max_steps, monitor_session)
         while True:
             self.check_episodes()
-            if self.training_done():
+            if self._fit_done():
                 break
             self.at_step_start()
             self.train_step()

@@ -31,6 +31,7 @@ __global__ void diag_gaussian_kernel(const float* __restrict__ mu, int64_t ld_mu
   const float* m = mu + (int64_t)i * ld_mu;
   const uint64_t c = ctr ? *ctr : 0ull;
   float ss = 0.0f;
+  xa_u4 r = {0u, 0u, 0u, 0u};
   for (int j = 0; j < d; ++j) {
     float a;
     if (actions_in) {
@@ -40,10 +41,14 @@ __global__ void diag_gaussian_kernel(const float* __restrict__ mu, int64_t ld_mu
       if (noise) {
         e = noise[(int64_t)i * d + j];
       } else {
-        // one Philox draw per pair of dimensions, Box-Muller
-        const xa_u4 r = xa_philox((uint32_t)i, (uint32_t)step, (uint32_t)(j >> 1) ^ (uint32_t)c,
-                                  (uint32_t)(c >> 32), (uint32_t)seed, (uint32_t)(seed >> 32));
-        const float u1 = fmaxf(xa_u01(r.x), 1.0e-7f), u2 = xa_u01(r.y);
+        // one Philox draw per 4 dimensions (two Box-Muller pairs: r.x r.y, r.z r.w); the
+        // counter is (row, step, *rng_counter) whole, the draw index j / 4 goes into the
+        // key (Weyl step), so no (counter, dimension) pair repeats another's draw
+        if ((j & 3) == 0)
+          r = xa_philox((uint32_t)i, (uint32_t)step, (uint32_t)c, (uint32_t)(c >> 32),
+                        (uint32_t)seed + (uint32_t)(j >> 2) * 0x9E3779B9u, (uint32_t)(seed >> 32));
+        const uint32_t w1 = (j & 2) ? r.z : r.x, w2 = (j & 2) ? r.w : r.y;
+        const float u1 = fmaxf(xa_u01(w1), 1.0e-7f), u2 = xa_u01(w2);
         const float rad = sqrtf(-2.0f * xa_logf(u1));
         e = rad * ((j & 1) ? sinf(6.283185307179586f * u2) : cosf(6.283185307179586f * u2));
       }

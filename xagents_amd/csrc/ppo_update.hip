@@ -37,6 +37,7 @@
 // abort word and `status` (after which the workspace must be re-zeroed), and every block
 // leaves.
 #include <math.h>
+#include <stdlib.h>
 
 #include "../../include/xagents_hip.h"
 #include "ac_tile.hpp"
@@ -55,10 +56,12 @@ constexpr int kCtlBytes = 256;              // control words at the workspace st
 // 10 s of the 100 MHz wall clock per hop: data parallel, a hop also absorbs the other ranks'
 // host-side skew (one process per GPU)
 constexpr uint64_t kSpinTicks = 1000000000;
-// control words (never reset): the phase-0 arrival counter ((gen + 1) G after launch gen)
-// and the abort word (the number gen + 1 of a launch that timed out)
-enum { kCntStats = 0, kAbort = 1 };
 constexpr int kXcds = 8;            // MI355X: 8 XCDs, each with its own L2
+// control words: the phase-0 arrival counter ((gen + 1) G after launch gen) and the abort
+// word (the number gen + 1 of a launch that timed out), never reset; the XCD election of
+// the XCD-local mode (below) in two parity slots -- launch gen uses slot gen & 1, which
+// launch gen - 1 (of either mode) zeroed at its end
+enum { kCntStats = 0, kAbort = 1, kWin = 2 /* [2] */, kElect = 4 /* [2][kXcds] */ };
 constexpr int kTwoLevelMinG = 64;   // >= 8 blocks per XCD: reduce inside each XCD's L2 first
 
 // ---- write-through hand-off primitives (global address space, agent scope) ----
@@ -107,9 +110,10 @@ XA_DEV void st_gran2(__amdgpu_buffer_rsrc_t r, uint32_t off, float v0, float v1,
   if (wt) __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, kAuxSc1);
   else __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 0);
 }
-XA_DEV void st_gran_f64(__amdgpu_buffer_rsrc_t r, uint32_t off, double d, unsigned tag) {
+XA_DEV void st_gran_f64(__amdgpu_buffer_rsrc_t r, uint32_t off, double d, unsigned tag,
+                        bool wt = true) {
   const unsigned long long u = (unsigned long long)__double_as_longlong(d);
-  st_gran2(r, off, __uint_as_float((unsigned)u), __uint_as_float((unsigned)(u >> 32)), tag, true);
+  st_gran2(r, off, __uint_as_float((unsigned)u), __uint_as_float((unsigned)(u >> 32)), tag, wt);
 }
 XA_DEV bool gran_ok(const f32x4v& v, unsigned tag) {
   return __float_as_uint(v[1]) == tag && __float_as_uint(v[3]) == tag;
@@ -181,6 +185,26 @@ XA_DEV int xcc_id() {
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
   return (int)(x & (kXcds - 1));
 }
+
+// Per-block phase trace (diagnostic -DXA_TRACE builds only, tools/trace_ppo_update.py):
+// thread 0 of every logical block records the 100 MHz real-time clock at 8 points of
+// every optimizer step of the last launch.
+constexpr int kTraceSteps = 64, kTracePts = 16;
+#ifdef XA_TRACE
+__device__ unsigned long long xa_ppo_trace[256 * kTraceSteps * kTracePts];
+#define XA_TRACE_PT(blk, k, i)                                                            \
+  do {                                                                                    \
+    if (threadIdx.x == 0 && (k) < kTraceSteps) {                                          \
+      unsigned long long t_;                                                              \
+      asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");     \
+      xa_ppo_trace[((size_t)(blk) * kTraceSteps + (k)) * kTracePts + (i)] = t_;           \
+    }                                                                                     \
+  } while (0)
+#else
+#define XA_TRACE_PT(blk, k, i) \
+  do {                         \
+  } while (0)
+#endif
 
 // Workspace (device memory, zeroed once by the caller at allocation; nothing in it is
 // reset between launches):
@@ -379,9 +403,51 @@ XA_DEV bool hop_wait(unsigned* ctl, int which, unsigned target, unsigned epoch, 
   return lds_flag != 0;
 }
 
+// XCD-local mode: the launch has kXcds x G workgroups; the G that run on the XCD whose
+// G-th workgroup arrives first do the update (logical block ids = their arrival ranks),
+// every other workgroup leaves at once. A winner always exists once every XCD's first G
+// arrivals are resident (the host launches this mode only when kXcds G fit), and every
+// hand-off of the launch then stays inside one L2: plain stores (the lines stay in the
+// shared L2) and L1-bypassing sc1 loads, no write-through round trip to the fabric.
+// Placement decides speed, never correctness: a workgroup learns its XCD from
+// HW_REG_XCC_ID and only workgroups of the elected XCD exchange data.
+// Returns the logical block id, or -1 (leave). Contains a __syncthreads().
+XA_DEV int elect_local(unsigned* ctl, int G, unsigned par, int xcc, unsigned epoch, int* status,
+                       int& lds) {
+  if (threadIdx.x == 0) {
+    int id = -1;
+    const unsigned r = __hip_atomic_fetch_add((gu32*)(ctl + kElect + par * kXcds + xcc), 1u,
+                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (r < (unsigned)G) {
+      gu32* win_w = (gu32*)(ctl + kWin + par);
+      if (r == (unsigned)G - 1u) {
+        unsigned expect = 0u;
+        __hip_atomic_compare_exchange_strong(win_w, &expect, (unsigned)xcc + 1u, __ATOMIC_RELAXED,
+                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      const uint64_t t0 = wall_clock64();
+      unsigned win;
+      while ((win = __hip_atomic_load(win_w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0u) {
+        if (wall_clock64() - t0 > kSpinTicks) {
+          __hip_atomic_store((gu32*)(ctl + kAbort), epoch, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+          if (status)
+            __hip_atomic_store((gu32*)status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (win == (unsigned)xcc + 1u) id = (int)r;
+    }
+    lds = id;
+  }
+  __syncthreads();
+  return lds;
+}
+
 // TS = samples per tile (32; 16 when the minibatch has at most 16 tiles of 32: twice the
-// blocks, half the element-wise work per block and step)
-template <int OBS, int A, int TS, bool DP>
+// blocks, half the element-wise work per block and step); LOC = XCD-local mode
+template <int OBS, int A, int TS, bool DP, bool LOC>
 __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws ws, int K,
                                                           int n_mb) {
   constexpr int RPT = Dims<OBS, A>::RPT;
@@ -390,22 +456,29 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
   const Offs o = offs(OBS, A);
   const int P = o.P;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int G = gridDim.x, b = blockIdx.x;
-  const int B = p.batch, MB = p.mb_size;
-  const uint64_t ctr = p.shuffle.rng_counter ? *p.shuffle.rng_counter : 0ull;
   XA_STAMP_DECL
-  XA_STAMP(30);
 
   // the launch generation (written write-through by block 0 of the previous launch, which
   // cannot finish before every block of this launch has passed phase 0)
   const unsigned gen =
       __hip_atomic_load((gu32*)ws.persist, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const unsigned epoch = gen + 1u;
+  const unsigned par = gen & 1u;
+  const int xcc = xcc_id();
+  const int G = LOC ? p.n_blocks : (int)gridDim.x;
+  const int b = LOC ? elect_local(ws.ctl, G, par, xcc, epoch, p.status, U.flag) : (int)blockIdx.x;
+  if (b < 0) return;
+  XA_STAMP_BLOCK(b == 0)
+  XA_STAMP(30);
+  XA_TRACE_PT(b, kTraceSteps - 1, 6);  // launch start (after the election)
+  const int B = p.batch, MB = p.mb_size;
+  const uint64_t ctr = p.shuffle.rng_counter ? *p.shuffle.rng_counter : 0ull;
+  // hand-off stores: write-through across XCDs, plain inside the elected XCD's L2
+  constexpr bool kWt = !LOC;
 
   // ---- census: which XCD this block runs on (a granule, read after the phase-0 hop) ----
   // 16-sample tiles run only on small grids (<= 32 blocks): one level, known at compile time
-  const bool two_level = TS == S && G >= kTwoLevelMinG;
-  const int xcc = xcc_id();
+  const bool two_level = !LOC && TS == S && G >= kTwoLevelMinG;
   const __amdgpu_buffer_rsrc_t cen_r = rsrc(ws.cen_g, (uint32_t)(G * 16));
   if (two_level && tid == 0) st_gran2(cen_r, (uint32_t)(16 * b), __uint_as_float((unsigned)xcc),
                                       __uint_as_float((unsigned)xcc), epoch, true);
@@ -556,6 +629,7 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
     __syncthreads();
   }
   XA_STAMP(33);
+  XA_TRACE_PT(b, kTraceSteps - 1, 7);  // after the phase-0 hop
   const int W = DP ? p.dp_world : 1;  // DP: compiled only into the data-parallel kernels
   const int CB0 = (padded(P) / 2 + G - 1) / G;
   const DpLayout dl = dp_layout(G, W, K, CB0);
@@ -693,7 +767,12 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
   };
 
   TileAcc<OBS, A> acc;
-  auto stampf = [&](int slot) { XA_STAMP(slot); };
+  int k_tr = 0;  // the step the tile trace points belong to
+  auto stampf = [&](int slot) {
+    XA_STAMP(slot);
+    XA_TRACE_PT(b, k_tr, 8 + (slot - 50));  // tile phases 50..55 -> points 8..13
+  };
+  (void)k_tr;
   (void)stampf;
   for (int k = 0; k < K; ++k) {
     const int m = k % n_mb;
@@ -706,7 +785,10 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
     cfg.adv_rstd = U.stat[k][2];
     cfg.loss_scale = 1.0f / (float)(cnt * W);
     acc.zero();
+    if (p.theta_trace && b == 0) ps.store(p.theta_trace + (size_t)k * P, wv, rv);  // diagnostic
     XA_STAMP(34);
+    XA_TRACE_PT(b, k, 0);
+    k_tr = k;
     // ---- A: forward + loss + backward of this block's tiles ----
     for (int tile = b; tile < n_tiles; tile += G) {
       if (pre) {
@@ -717,6 +799,7 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
         tile_compute<OBS, A, decltype(stampf), PackedIn<OBS>, TS>(L, acc, cfg, stampf, in);
 #endif
         XA_STAMP(36);
+        XA_TRACE_PT(b, k, 14);
         continue;
       }
       __syncthreads();
@@ -744,6 +827,7 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
     tile_write_row<OBS, A>(L, acc, [&](int i, float v) { srow[i] = v; });
 #endif
     XA_STAMP(44);
+    XA_TRACE_PT(b, k, 1);
     if (p.loss_out) {
       const float ls = tile_loss_sums<OBS, A>(L, acc);
       if (tid < 4) p.loss_out[((size_t)k * G + b) * 4 + tid] = ls;
@@ -751,8 +835,9 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
     __syncthreads();
     for (int c = tid; c < NP2; c += 256)
       st_gran2(rows_r, (uint32_t)(((size_t)b * NP2 + c) * 16), srow[2 * c], srow[2 * c + 1], tag,
-               !two_level);
+               kWt && !two_level);
     XA_STAMP(45);
+    XA_TRACE_PT(b, k, 2);
     fetch_tile(k + 1, b);  // the next step's first tile, while the other blocks finish
     XA_STAMP(37);
     if (tid == 0) *fail = 0;
@@ -833,10 +918,15 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
     // value in srow for the cross-rank exchange below
     auto publish = [&](int c, float g0, float g1) {
       const int cc = c0 + c;
-      st_gran2(g_r, (uint32_t)(16 * cc), g0, g1, tag, true);
+      st_gran2(g_r, (uint32_t)(16 * cc), g0, g1, tag, kWt);
       if (p.grad_out && k == K - 1) {
         if (2 * cc < P) p.grad_out[2 * cc] = g0;
         if (2 * cc + 1 < P) p.grad_out[2 * cc + 1] = g1;
+      }
+      if (p.grad_trace) {  // diagnostic: every step's reduced gradient
+        float* gt = p.grad_trace + (size_t)k * P;
+        if (2 * cc < P) gt[2 * cc] = g0;
+        if (2 * cc + 1 < P) gt[2 * cc + 1] = g1;
       }
       sq += (double)g0 * (double)g0 + (double)g1 * (double)g1;
     };
@@ -1040,8 +1130,9 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
     __syncthreads();
     if (tid == 0)
       st_gran_f64(g_r, sq0 + (uint32_t)(16 * b), (U.wsum[0] + U.wsum[1]) + (U.wsum[2] + U.wsum[3]),
-                  tag);
+                  tag, kWt);
     XA_STAMP(40);
+    XA_TRACE_PT(b, k, 3);
 
     // ---- C: the g slice of this thread's parameters and the G norm partials (granules of
     // one buffer, one poll), global norm (identical in every wave of every block), clip +
@@ -1102,6 +1193,7 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
     }
     if (__syncthreads_or(bad)) return;
     XA_STAMP(47);
+    XA_TRACE_PT(b, k, 4);
 #ifndef XA_ABL_CNORM
     tot = xa_wave_sum_f64(tot);
     const float sc = clip_scale(tot, p.adam.clip_norm);
@@ -1129,6 +1221,16 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
     ps.to_lds(L, wv, rv);
 #endif
     XA_STAMP(43);
+    XA_TRACE_PT(b, k, 5);
+  }
+  if (b == 0 && tid == 0) {
+    // zero the election slot of the next launch (this launch's slot is par; launch
+    // gen + 1 uses par ^ 1, which launch gen - 1 used and nothing touches now)
+    for (int x = 0; x < kXcds; ++x)
+      __hip_atomic_store((gu32*)(ws.ctl + kElect + (par ^ 1u) * kXcds + x), 0u, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((gu32*)(ws.ctl + kWin + (par ^ 1u)), 0u, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
   }
   if (b == 0) {
     ps.store(p.theta, wv, rv);
@@ -1146,20 +1248,34 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
   }
 }
 
-// resident capacity (blocks of one launch that are co-resident), per device
+// resident capacity (blocks of one launch that are co-resident), per device: the
+// minimum occupancy over every variant launch() may pick
+template <int OBS, int A>
+int occupancy_min() {
+  void* const kernels[] = {
+      (void*)ppo_update_kernel<OBS, A, S, false, false>, (void*)ppo_update_kernel<OBS, A, 16, false, false>,
+      (void*)ppo_update_kernel<OBS, A, S, true, false>, (void*)ppo_update_kernel<OBS, A, 16, true, false>,
+      (void*)ppo_update_kernel<OBS, A, S, false, true>, (void*)ppo_update_kernel<OBS, A, 16, false, true>,
+      (void*)ppo_update_kernel<OBS, A, S, true, true>, (void*)ppo_update_kernel<OBS, A, 16, true, true>};
+  int occ = 1 << 30;
+  for (void* k : kernels) {
+    int o = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, k, 256, 0) != hipSuccess) return 0;
+    occ = min(occ, o);
+  }
+  return occ;
+}
+
 template <int OBS, int A>
 int capacity() {
   static int cap[64] = {0};
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
   if (cap[dev] == 0) {
-    int cus = 0, occ = 0;
+    int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       return 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, ppo_update_kernel<OBS, A, S, false>, 256, 0) !=
-        hipSuccess)
-      return 0;
-    cap[dev] = cus * occ;
+    cap[dev] = cus * occupancy_min<OBS, A>();
   }
   return cap[dev];
 }
@@ -1176,21 +1292,42 @@ int capacity_for(int obs_dim, int n_actions) {
 // (xa_ppo_update_blocks picks that for minibatches of <= 16 such tiles), else 32
 int tile_samples(int mb_size, int G) { return G > (mb_size + S - 1) / S ? 16 : S; }
 
+// XCD-local mode (elect_local): small grids (one level, G <= 32 at one block per CU), when
+// kXcds G blocks are co-resident; data-parallel launches only when every rank owns its GPU
+// (ranks sharing one GPU could strand each other's elections). XA_PPO_LOCAL=0 disables it.
+bool use_local(const XaPpoUpdateArgs* a, int G, int cap) {
+  static const int env = [] {
+    const char* e = getenv("XA_PPO_LOCAL");
+    return e && e[0] == '0' ? 0 : 1;
+  }();
+  if (!env || a->placement == XA_PPO_PLACE_SPREAD) return false;
+  if (a->dp_world > 1 && a->placement != XA_PPO_PLACE_LOCAL) return false;
+  return G < kTwoLevelMinG && (long)G * kXcds <= (long)cap;
+}
+
+template <int OBS, int A, int TS>
+void launch_ts(const XaPpoUpdateArgs* a, int G, bool dp, bool loc, const Ws& ws, int K, int n_mb,
+               hipStream_t s) {
+  const dim3 grid(loc ? G * kXcds : G);
+  if (dp && loc)
+    hipLaunchKernelGGL((ppo_update_kernel<OBS, A, TS, true, true>), grid, dim3(256), 0, s, *a, ws, K, n_mb);
+  else if (dp)
+    hipLaunchKernelGGL((ppo_update_kernel<OBS, A, TS, true, false>), grid, dim3(256), 0, s, *a, ws, K, n_mb);
+  else if (loc)
+    hipLaunchKernelGGL((ppo_update_kernel<OBS, A, TS, false, true>), grid, dim3(256), 0, s, *a, ws, K, n_mb);
+  else
+    hipLaunchKernelGGL((ppo_update_kernel<OBS, A, TS, false, false>), grid, dim3(256), 0, s, *a, ws, K, n_mb);
+}
+
 template <int OBS, int A>
 int launch(const XaPpoUpdateArgs* a, int G, int K, int n_mb, hipStream_t s) {
   const int P = offs(OBS, A).P;
   const Ws ws = carve(a->workspace, G, P, K);
-  const bool ts16 = tile_samples(a->mb_size, G) == 16;
-  if (a->dp_world > 1) {
-    if (ts16)
-      hipLaunchKernelGGL((ppo_update_kernel<OBS, A, 16, true>), dim3(G), dim3(256), 0, s, *a, ws, K, n_mb);
-    else
-      hipLaunchKernelGGL((ppo_update_kernel<OBS, A, S, true>), dim3(G), dim3(256), 0, s, *a, ws, K, n_mb);
-  } else if (ts16) {
-    hipLaunchKernelGGL((ppo_update_kernel<OBS, A, 16, false>), dim3(G), dim3(256), 0, s, *a, ws, K, n_mb);
-  } else {
-    hipLaunchKernelGGL((ppo_update_kernel<OBS, A, S, false>), dim3(G), dim3(256), 0, s, *a, ws, K, n_mb);
-  }
+  const bool loc = use_local(a, G, capacity<OBS, A>());
+  if (tile_samples(a->mb_size, G) == 16)
+    launch_ts<OBS, A, 16>(a, G, a->dp_world > 1, loc, ws, K, n_mb, s);
+  else
+    launch_ts<OBS, A, S>(a, G, a->dp_world > 1, loc, ws, K, n_mb, s);
   XA_CHECK_LAUNCH("xa_ppo_update");
   return 0;
 }
@@ -1259,3 +1396,9 @@ extern "C" int xa_ppo_update(const XaPpoUpdateArgs* a, void* stream) {
   return launch<2, 3>(a, G, K, n_mb, s);
 }
 XA_DIAG_READER(xa_diag_read_stamps_ppo)
+#ifdef XA_TRACE
+extern "C" int xa_diag_read_trace_ppo(unsigned long long* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(xa_ppo_trace), sizeof(xa_ppo_trace)) == hipSuccess
+             ? 0 : -1;
+}
+#endif

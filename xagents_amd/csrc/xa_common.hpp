@@ -52,10 +52,14 @@ static __device__ unsigned long long xa_stamp_acc[64];
       return -1;                                                                     \
     return hipMemcpyToSymbol(HIP_SYMBOL(xa_stamp_acc), zero, sizeof(zero)) == hipSuccess ? 0 : -1; \
   }
-#define XA_STAMP_DECL unsigned long long xa_t_last_ = 0;
+#define XA_STAMP_DECL \
+  unsigned long long xa_t_last_ = 0; \
+  bool xa_stamp_on_ = threadIdx.x == 0 && blockIdx.x == 0;
+// a kernel whose logical block ids differ from blockIdx.x names the stamping block
+#define XA_STAMP_BLOCK(is_zero) xa_stamp_on_ = threadIdx.x == 0 && (is_zero);
 #define XA_STAMP(slot)                                                              \
   do {                                                                              \
-    if (threadIdx.x == 0 && blockIdx.x == 0) {                                      \
+    if (xa_stamp_on_) {                                                             \
       unsigned long long t_;                                                        \
       __builtin_amdgcn_sched_barrier(0);                                            \
       asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");    \
@@ -67,6 +71,7 @@ static __device__ unsigned long long xa_stamp_acc[64];
 #else
 #define XA_DIAG_READER(name)
 #define XA_STAMP_DECL
+#define XA_STAMP_BLOCK(is_zero)
 #define XA_STAMP(slot) \
   do {                 \
   } while (0)

@@ -3,19 +3,24 @@ MI355X path.
 
 train_step = one hipGraph replay of:
     xa_mlp_rollout (n_steps x [forward, sample, env step, store] + GAE)
-    one process:   xa_ppo_update (every optimizer step of the train step in ONE
-                   persistent launch: shuffle, adv normalisation, fwd + clipped PPO loss
-                   + bwd, in-launch gradient reduction, clip + Keras Adam)
-    data parallel: xa_ppo_minibatches (shuffle-gather, adv sums) -> [all_reduce]
+    xa_ppo_update  (every optimizer step of the train step in ONE persistent launch:
+                   shuffle, adv normalisation, fwd + clipped PPO loss + bwd, in-launch
+                   gradient reduction, clip + Keras Adam; data parallel over the peer
+                   path: the advantage sums and gradient slices are exchanged between the
+                   ranks inside the same launch)
+    chain (XA_PPO_UPDATE=chain, or data parallel without the peer path, i.e. RCCL only):
+                   xa_ppo_minibatches (shuffle-gather, adv sums) -> [all_reduce]
                    ppo_epochs x mini_batches x:
                        xa_ac_grad (prologue: the previous step's clip + Adam; fwd + loss +
                        bwd -> partial rows) -> xa_grad_reduce -> [all_reduce]
                    -> xa_clip_adam
-    xa_counter_bump
+    xa_counter_bump (inside xa_ppo_update's last block on the persistent path)
 Multi-GPU: every rank owns n_envs envs (weak scaling); the minibatch of a step is the
 union of the ranks' local minibatches, advantage normalisation and the loss mean use
 the global statistics/count, so the update equals a single-GPU update on the union.
 """
+import os
+
 import numpy as np
 import torch
 
@@ -57,7 +62,6 @@ class PPO(A2C):
         super(PPO, self).__init__(envs, model, **kwargs)
 
     def _setup_update(self):
-        import os
         # optimizer step placement of the chain: 'prologue' (next minibatch's xa_ac_grad
         # recomputes it in every block) or 'kernel' (a standalone xa_clip_adam launch)
         self._opt_kernel = os.environ.get('XA_PPO_OPT', 'prologue') == 'kernel'
@@ -168,7 +172,12 @@ class PPO(A2C):
         dev, opt = self.device, self.model.optimizer
         obs_dim, A = self.model.obs_dim, self.n_actions
         nbytes = kernels.ppo_update_workspace_bytes(obs_dim, A, B, MB, E, n_blocks)
-        self.update_ws = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
+        # zeroed once: a re-setup with the same shapes (a learning-rate change) keeps the
+        # workspace and with it the launch generation, which data-parallel ranks must share
+        key = (B, MB, E, n_blocks)
+        if getattr(self, 'update_ws', None) is None or getattr(self, '_ws_key', None) != key:
+            self.update_ws = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
+            self._ws_key = key
         # the status word rides in the packed episode-statistics buffer (one D2H copy)
         self.device_status = self._stats_status
         self.device_status.zero_()
@@ -193,6 +202,16 @@ class PPO(A2C):
         # the Philox counter bump that ends a train step runs in the launch's last block
         u.bump_counter = int(bool(self.shuffle.rng_counter))
         u.dp_world, u.dp_rank = 1, 0
+        # XCD-local placement of small grids (xa_ppo_update): automatic in one process; data
+        # parallel only when every rank owns its GPU (ranks sharing one could strand each
+        # other's XCD elections). XA_PPO_PLACE=spread|local overrides.
+        place = os.environ.get('XA_PPO_PLACE', 'auto')
+        if place == 'spread':
+            u.placement = _lib.XA_PPO_PLACE_SPREAD
+        elif place == 'local' or (self.distributed and getattr(self, '_ranks_share', 1) == 1):
+            u.placement = _lib.XA_PPO_PLACE_LOCAL
+        else:
+            u.placement = _lib.XA_PPO_PLACE_AUTO
         if self.distributed:
             if getattr(self, 'dp_blocks', None) is None or self._dp_blocks_key != (B, MB, E,
                                                                                   n_blocks):
@@ -249,11 +268,6 @@ class PPO(A2C):
             if self._opt_kernel and i < last:
                 self._optimizer_step()  # standalone clip + Adam launch
         self._optimizer_step(self._final_src)
-
-    def _on_lr_change(self):
-        super()._on_lr_change()
-        if not self.executor_path:
-            self._setup_update()  # the learning rate is baked into the launch arguments
 
     # ---- reference-level pieces --------------------------------------------
     def calculate_returns(self, rewards, dones, values=None, selected_critic_logits=None,
