@@ -8,8 +8,11 @@ A step = one PPO train_step: fused rollout of n_envs x 128 steps (+GAE) and 4 ep
 minibatches (shuffle, forward, clipped loss, backward, global-norm clip, Keras Adam; one
 persistent launch on one GPU, all-reduce of the gradient when N>1).
 `value` = the metric's 16-env workload (BASELINE metric "PPO 16-env"); the line's `c2`
-object = BASELINE configs[1] (256 envs per GPU). Weak scaling: every rank owns its envs.
-Rank 0 prints ONE JSON line.
+object = BASELINE configs[1] (256 envs per GPU). Weak scaling: every rank owns its envs;
+--global-envs N splits N envs over the ranks instead (strong scaling). At N = 1 the same
+line also carries compact `c3` / `c4` / `c5` objects (BASELINE configs[2..4]: value, ms per
+step, dominant-kernel roofline, a few-second CPU-port baseline); --config c3|c4|c5|trpo|acer
+prints a full line for one of them. Rank 0 prints ONE JSON line.
 """
 import argparse
 import json
@@ -41,6 +44,11 @@ def parse():
     p.add_argument('--warmup', type=int, default=5)
     p.add_argument('--n-envs', type=int, default=16,
                    help='envs per GPU of the headline line (the metric is quoted on 16)')
+    p.add_argument('--global-envs', type=int, default=0,
+                   help='strong scaling: this many envs in all, split over the ranks (the '
+                        'headline line then reports scaling "strong"; default: --n-envs per GPU)')
+    p.add_argument('--no-secondary', dest='secondary', action='store_false',
+                   help='skip the compact C3 / C4 / C5 objects of the default one-GPU line')
     p.add_argument('--no-c2', dest='c2', action='store_false',
                    help='skip the secondary BASELINE configs[1] (256 envs per GPU) measurement')
     p.add_argument('--n-steps', type=int, default=128)
@@ -59,23 +67,37 @@ def parse():
 
 
 def cpu_baseline(args, record, theta0):
+    """The CPU port timed at 1 thread and at up to 16 threads (the box's share), the median
+    of 3 windows for each; the faster setting is the baseline, both are in `sample`."""
     sys.path.insert(0, str(ROOT / 'oracle'))
+    import numpy as np
     import torch
     from cpu_ppo import time_cpu_baseline
 
-    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-    value, info = time_cpu_baseline(record, theta0, n_steps=args.n_steps,
-                                    seconds=args.cpu_baseline_seconds, threads=threads)
-    torch.set_num_threads(threads)
+    t_before = torch.get_num_threads()
+    many = args.cpu_threads or min(16, os.cpu_count() or 1)
+    window = max(args.cpu_baseline_seconds / 6.0, 1.0)
+    res = {}
+    for threads in sorted({1, many}):
+        runs = [time_cpu_baseline(record, theta0, n_steps=args.n_steps, seconds=window,
+                                  threads=threads) for _ in range(3)]
+        vals = [v for v, _ in runs]
+        res[threads] = (float(np.median(vals)), vals, runs[0][1])
+    torch.set_num_threads(t_before)
+    best = max(res, key=lambda t: res[t][0])
+    value, _, info = res[best]
+    per = '; '.join(f"{t} thread{'s' if t > 1 else ''}: median {res[t][0]:.0f} of "
+                    f"[{', '.join(f'{v:.0f}' for v in res[t][1])}]" for t in sorted(res))
     return {
         'value': round(value, 1),
         'unit': 'env-steps/s',
-        'cores': info['threads'],
+        'cores': best,
         'kind': 'port',
-        'sample': (f"{info['train_steps']} PPO train steps of the same workload "
-                   f"({info['n_envs']} envs x {args.n_steps} steps, 4x4 minibatches) in "
-                   f"{info['seconds']:.1f} s: per-env Python step_envs loop, torch-CPU f32 "
-                   f"MLP + autograd, numpy GAE, Keras Adam (oracle/cpu_ppo.py)"),
+        'sample': (f"PPO train steps of the same workload ({info['n_envs']} envs x "
+                   f"{args.n_steps} steps, 4x4 minibatches) in 3 windows of {window:.1f} s per "
+                   f"thread count ({per} env-steps/s; the faster is reported): per-env Python "
+                   f"step_envs loop, torch-CPU f32 MLP + autograd, numpy GAE, Keras Adam "
+                   f"(oracle/cpu_ppo.py)"),
     }
 
 
@@ -141,9 +163,11 @@ def _timed(fn, steps, warmup, world):
     return el
 
 
-def secondary_cpu_baseline(args, kind):
+def secondary_cpu_baseline(args, kind, seconds=None, compact=False):
     """Bounded CPU sample of the C3 / C4 / C5 / TRPO / ACER workload (oracle/cpu_cnn.py,
-    oracle/cpu_td3.py, oracle/cpu_trpo.py; kind "port")."""
+    oracle/cpu_td3.py, oracle/cpu_trpo.py; kind "port"). compact: the few-second samples of
+    the default line's c3 / c4 / c5 objects (C4: 16 steps per env instead of 128)."""
+    seconds = args.cpu_baseline_seconds if seconds is None else seconds
     sys.path.insert(0, str(ROOT / 'oracle'))
     import numpy as np
     import torch
@@ -151,12 +175,11 @@ def secondary_cpu_baseline(args, kind):
     from xagents_amd.envs import record_transitions
     threads = args.cpu_threads or min(16, os.cpu_count() or 1)
     if kind == 'c4':
-        n, T = 16, 128
+        n, T = 16, (16 if compact else 128)
         rec = record_transitions(n, 256, (84, 84, 1), np.uint8, seed=args.seed)
-        value, info = cpu_cnn.time_cnn_ppo(rec, n_steps=T, seconds=args.cpu_baseline_seconds,
-                                           threads=threads)
+        value, info = cpu_cnn.time_cnn_ppo(rec, n_steps=T, seconds=seconds, threads=threads)
         sample = (f"{info['train_steps']} PPO-CNN train steps of {n} envs x {T} steps (4x4 "
-                  f"minibatches of 512) in {info['seconds']:.1f} s: per-env Python step_envs "
+                  f"minibatches of {n * T // 4}) in {info['seconds']:.1f} s: per-env Python step_envs "
                   f"loop, torch-CPU f32 Conv1D/dense + autograd, numpy GAE, Keras Adam "
                   f"(oracle/cpu_cnn.py); the GPU line runs 1024 envs")
     elif kind == 'c5':
@@ -164,7 +187,7 @@ def secondary_cpu_baseline(args, kind):
         n = 64
         rec = record_transitions(n, 4096, (24,), np.float32, seed=args.seed)
         np.random.seed(args.seed)
-        value, info = cpu_td3.time_td3(rec, seconds=args.cpu_baseline_seconds, threads=threads)
+        value, info = cpu_td3.time_td3(rec, seconds=seconds, threads=threads)
         sample = (f"{info['train_steps']} TD3 train steps of {n} envs (gradient_steps 1 per "
                   f"finished episode, batch 64 from per-env ReplayBuffer2 rings) in "
                   f"{info['seconds']:.1f} s: per-env Python step_envs loop, torch-CPU f32 "
@@ -174,8 +197,7 @@ def secondary_cpu_baseline(args, kind):
         n, T = 16, 512
         rec = record_transitions(n, 4096, (4,), np.float32, seed=args.seed)
         np.random.seed(args.seed)
-        value, info = cpu_trpo.time_trpo(rec, seconds=args.cpu_baseline_seconds,
-                                         threads=threads, n_steps=T)
+        value, info = cpu_trpo.time_trpo(rec, seconds=seconds, threads=threads, n_steps=T)
         sample = (f"{info['train_steps']} TRPO train steps of {n} envs x {T} steps in "
                   f"{info['seconds']:.1f} s: per-env Python step_envs loop, numpy GAE, "
                   f"torch-CPU f32 actor / critic, autograd surrogate gradient, 10 CG "
@@ -186,8 +208,7 @@ def secondary_cpu_baseline(args, kind):
         n, T = 16, 20
         rec = record_transitions(n, 256, (84, 84, 1), np.uint8, seed=args.seed)
         np.random.seed(args.seed)
-        value, info = cpu_cnn.time_acer(rec, seconds=args.cpu_baseline_seconds,
-                                        threads=threads, n_steps=T)
+        value, info = cpu_cnn.time_acer(rec, seconds=seconds, threads=threads, n_steps=T)
         sample = (f"{info['train_steps']} ACER train steps of {n} envs x {T} steps (fresh "
                   f"update + poisson(4) replays of random.sample'd trajectories) in "
                   f"{info['seconds']:.1f} s: per-env Python step_envs loop, torch-CPU f32 "
@@ -196,7 +217,7 @@ def secondary_cpu_baseline(args, kind):
     else:
         n = 32
         rec = record_transitions(n, 256, (84, 84, 1), np.uint8, seed=args.seed)
-        value, info = cpu_cnn.time_dqn(rec, seconds=args.cpu_baseline_seconds, threads=threads)
+        value, info = cpu_cnn.time_dqn(rec, seconds=seconds, threads=threads)
         sample = (f"{info['train_steps']} double-DQN train steps of {n} envs (batch 64 from "
                   f"per-env deques of 1000) in {info['seconds']:.1f} s: per-env Python "
                   f"step_envs loop, random.sample replay, torch-CPU f32 NatureCNN + autograd, "
@@ -245,17 +266,61 @@ def dense_dx_roofline(executors, step):
                     f'kernel read alone bounds it at {77.07e6 / 8e12 * 1e3:.4f} ms (HBM)'}
 
 
+def dominant_gemm_roofline(executors, step):
+    """Roofline of the GEMM launch shape with the largest total time in one more (eager)
+    `step` (the layer executors' HIP event pairs on the launch stream)."""
+    import torch
+    timing = []
+    for ex in executors:
+        ex.timing = timing
+    try:
+        step()
+        torch.cuda.synchronize()
+    finally:
+        for ex in executors:
+            ex.timing = None
+    tot = {}
+    for name, e0, e1, fl in timing:
+        t = tot.setdefault((name, fl), [0.0, 0])
+        t[0] += e0.elapsed_time(e1)
+        t[1] += 1
+    if not tot:
+        return None
+    (name, fl), (ms_sum, cnt) = max(tot.items(), key=lambda kv: kv[1][0])
+    ms = ms_sum / cnt
+    tf = fl / (ms * 1e-3) / 1e12
+    share = ms_sum / sum(v[0] for v in tot.values())
+    return {'kernel': f'xa_gemm {name} (MFMA f32)', 'bound': 'mfma', 'achieved': round(tf, 4),
+            'peak': F32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
+            'frac': round(tf / F32_MFMA_PEAK_TFLOPS, 5), 'traffic': None,
+            'launch_ms': round(ms, 5),
+            'note': f'2 M N K FLOP per launch, mean of {cnt} launches; the largest total time '
+                    f'of the GEMM shapes in a gradient step ({share:.0%} of the GEMM time; the '
+                    f'step is launch-bound at batch 64)'}
+
+
 def bench_offpolicy_and_cnn(args):
-    """Secondary configs; one JSON line each, same fields."""
+    """Secondary configs (TRPO, ACER); one JSON line each."""
+    world, rank, device = _dist_setup()
+    line = run_secondary(args, args.config, world, rank, device, args.steps, args.warmup,
+                         args.cpu_baseline_seconds)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+def run_secondary(args, config, world, rank, device, steps, warmup, cpu_seconds, compact=False):
+    """One secondary config's measurement (its JSON line as a dict)."""
     import numpy as np
     import torch
-    world, rank, device = _dist_setup()
     from xagents_amd.envs import create_envs
     from xagents_amd.utils.common import create_buffers, create_model
-    line = {'metric': METRIC, 'unit': 'env-steps/s', 'n_gpus': world, 'steps': args.steps,
-            'warmup': args.warmup, 'higher_is_better': True, 'vs_baseline': None,
+    line = {'metric': METRIC, 'unit': 'env-steps/s', 'n_gpus': world, 'steps': steps,
+            'warmup': warmup, 'higher_is_better': True, 'vs_baseline': None,
             'dtype': 'f32', 'cpu_baseline': None}
-    if args.config == 'c3':
+    if config == 'c3':
         from xagents_amd import DQN
         n = 32
         envs = create_envs('PongNoFrameskip-v4', n, args.preprocess, device=device,
@@ -272,8 +337,8 @@ def bench_offpolicy_and_cnn(args):
             agent.at_step_start()
             agent.train_step()
             agent.at_step_end()
-        el = _timed(step, args.steps, args.warmup, world)
-        env_steps = n * args.steps * world
+        el = _timed(step, steps, warmup, world)
+        env_steps = n * steps * world
         # one eager learner phase for the event pairs (the timed steps replay it as a graph)
         agent.use_graph = False
         rl = dense_dx_roofline([agent.ex_online], step)
@@ -288,15 +353,15 @@ def bench_offpolicy_and_cnn(args):
                                         'double, epsilon 0.02 (BASELINE configs[2])',
                             'n_envs_per_gpu': n, 'batch': 64, 'replay_fill_s': round(t_fill, 2),
                             'parallelism': f'dp{world}'})
-    elif args.config == 'c4':
+    elif config == 'c4':
         from xagents_amd import PPO
         n = 1024 // world
         envs = create_envs('BreakoutNoFrameskip-v4', n, args.preprocess, device=device,
                            seed=args.seed + rank, **_raw_kw(args, n))
         model = create_model(envs, 'ppo', 'model', seed=args.seed, device=device)
         agent = PPO(envs, model, n_steps=128, seed=args.seed, quiet=True)
-        el = _timed(agent.fused_train_step, args.steps, args.warmup, world)
-        env_steps = n * 128 * args.steps * world
+        el = _timed(agent.fused_train_step, steps, warmup, world)
+        env_steps = n * 128 * steps * world
         # dominant kernel: the dense 37632 x 512 layer's input gradient (gemm_tile_kernel,
         # 128 x 128 tiles on v_mfma_f32_32x32x2_f32)
         rl = dense_dx_roofline(agent.ex_chunks, agent.fused_train_step)
@@ -309,7 +374,7 @@ def bench_offpolicy_and_cnn(args):
                                         'sharded over the GPUs, NatureCNN (Conv1D cfg), n_steps '
                                         '128, 4x4 minibatches (BASELINE configs[3])',
                             'n_envs_per_gpu': n, 'parallelism': f'dp{world}'})
-    elif args.config == 'trpo':
+    elif config == 'trpo':
         from xagents_amd import TRPO
         if world > 1:
             raise SystemExit('bench --config trpo runs on one GPU (TRPO is not data parallel)')
@@ -319,15 +384,15 @@ def bench_offpolicy_and_cnn(args):
         actor = create_model(envs, 'trpo', 'actor_model', seed=args.seed, device=device)
         critic = create_model(envs, 'trpo', 'critic_model', seed=args.seed + 1, device=device)
         agent = TRPO(envs, actor, critic, n_steps=T, seed=args.seed, quiet=True)
-        el = _timed(agent.train_step, args.steps, args.warmup, world)
-        env_steps = n * T * args.steps
+        el = _timed(agent.train_step, steps, warmup, world)
+        env_steps = n * T * steps
         line.update(scaling='weak', data='synthetic: CartPole-v1 observation replay recorded '
                     'on the host (seed 55), random-init actor and critic', config={
                         'workload': 'TRPO CartPole-v1, 16 envs, n_steps 512, MLP actor / critic '
                                     '[64, 64] relu, CG 10 x FVP on every 5th state, line '
                                     'search, 3 x 4 x 4 critic minibatches (SURVEY 8f rank 2)',
                         'n_envs_per_gpu': n, 'parallelism': 'dp1'})
-    elif args.config == 'acer':
+    elif config == 'acer':
         from xagents_amd import ACER
         n, T = 16, 20  # the headline env count; acer/cli.py n-steps default
         envs = create_envs('PongNoFrameskip-v4', n, args.preprocess, device=device,
@@ -337,8 +402,8 @@ def bench_offpolicy_and_cnn(args):
         bufs = create_buffers('acer', 64 * n, 1, n, initial_size=n)
         agent = ACER(envs, model, bufs, n_steps=T, seed=args.seed, quiet=True, grad_norm=10.0)
         np.random.seed(args.seed)
-        el = _timed(agent.train_step, args.steps, args.warmup, world)
-        env_steps = n * T * args.steps * world
+        el = _timed(agent.train_step, steps, warmup, world)
+        env_steps = n * T * steps * world
         updates = int(agent.model.optimizer.iterations.item())
         rl = dense_dx_roofline(agent.ex_chunks, agent.train_step)
         if rl:
@@ -351,7 +416,7 @@ def bench_offpolicy_and_cnn(args):
                                         'trust region, replay ratio 4 (poisson), 64 '
                                         'trajectories per env (SURVEY 8f rank 2)',
                             'n_envs_per_gpu': n, 'parallelism': f'dp{world}',
-                            'updates_per_step': round(updates / (args.steps + args.warmup), 2)})
+                            'updates_per_step': round(updates / (steps + warmup), 2)})
     else:
         from xagents_amd import TD3
         n = max(64 // world, 1)
@@ -363,26 +428,59 @@ def bench_offpolicy_and_cnn(args):
         agent = TD3(envs, actor, critic, bufs, gradient_steps=1, seed=args.seed, quiet=True)
         agent.fill_buffers()
         # env steps with their done-triggered gradient steps, and one gradient step alone
-        el = _timed(agent.train_step, args.steps, args.warmup, world)
-        g_el = _timed(lambda: agent.update_weights(1), args.steps, args.warmup, world)
-        env_steps = n * args.steps * world
+        el = _timed(agent.train_step, steps, warmup, world)
+        g_el = _timed(lambda: agent.update_weights(1), steps, warmup, world)
+        env_steps = n * steps * world
+        rl = dominant_gemm_roofline(
+            [agent.ex_actor, agent.ex_target_actor, agent.ex_critic, agent.ex_critic2,
+             agent.ex_target_critic, agent.ex_target_critic2, agent.ex_critic_pi],
+            lambda: agent.update_weights(1))
+        if rl:
+            line['roofline'] = rl
         line.update(scaling='weak', data='synthetic: BipedalWalker-shaped f32 obs ~N(0,1) '
                     '(seed 55+rank)', config={
                         'workload': 'TD3 BipedalWalker-v3-shaped, 64 envs, ReplayBuffer2, '
                                     'per-buffer batch 1 (100 // 64), gradient_steps 1 '
                                     '(BASELINE configs[4])',
                         'n_envs_per_gpu': n, 'parallelism': f'dp{world}'},
-                    gradient_step_ms=round(g_el / args.steps * 1e3, 4))
+                    gradient_step_ms=round(g_el / steps * 1e3, 4))
     line['value'] = round(env_steps / el, 1)
-    line['ms_per_step'] = round(el / args.steps * 1e3, 4)
-    if rank == 0 and world == 1 and args.config in ('c3', 'c4', 'c5', 'trpo', 'acer') and \
-            args.cpu_baseline_seconds > 0:
-        line['cpu_baseline'] = secondary_cpu_baseline(args, args.config)
-    if rank == 0:
-        print(json.dumps(line), flush=True)
-    if world > 1:
-        import torch.distributed as dist
-        dist.destroy_process_group()
+    line['ms_per_step'] = round(el / steps * 1e3, 4)
+    if rank == 0 and world == 1 and config in ('c3', 'c4', 'c5', 'trpo', 'acer') and \
+            cpu_seconds > 0:
+        line['cpu_baseline'] = secondary_cpu_baseline(args, config, cpu_seconds, compact)
+    return line
+
+
+# the default one-GPU line's compact secondary objects: (config, steps, warmup, CPU seconds)
+SECONDARY = (('c3', 30, 5, 4.0), ('c4', 3, 1, 3.0), ('c5', 30, 5, 3.0))
+
+
+def compact_secondaries(args, device):
+    """C3 / C4 / C5 (BASELINE configs[2..4]) measured in the same run as the headline, each
+    as a compact object: value, ms per step, the dominant kernel's roofline, a few-second
+    CPU-port baseline. A failing config is reported as an error in its object."""
+    import gc
+
+    import torch
+    out = {}
+    for cfg, steps, warmup, cpu_s in SECONDARY:
+        try:
+            r = run_secondary(args, cfg, 1, 0, device, steps, warmup,
+                              cpu_s if args.cpu_baseline_seconds > 0 else 0.0, compact=True)
+            out[cfg] = {k: r[k] for k in ('value', 'unit', 'ms_per_step', 'scaling', 'steps',
+                                          'warmup') if k in r}
+            out[cfg]['workload'] = r['config']['workload']
+            out[cfg]['roofline'] = r.get('roofline')
+            out[cfg]['cpu_baseline'] = r.get('cpu_baseline')
+            if 'gradient_step_ms' in r:
+                out[cfg]['gradient_step_ms'] = r['gradient_step_ms']
+        except Exception as exc:  # noqa: BLE001 -- reported in the line, never hidden
+            out[cfg] = {'error': f'{type(exc).__name__}: {exc}'}
+        gc.collect()
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+    return out
 
 
 def bench_ppo(args, world, rank, device, n_envs):
@@ -494,9 +592,15 @@ def main():
 
     world, rank, device = _dist_setup()
     # headline: the metric's PPO CartPole-v1 16-env workload (BASELINE metric / configs[0]
-    # shape) on the GPU; secondary: BASELINE configs[1] (256 envs per GPU)
-    head = bench_ppo(args, world, rank, device, args.n_envs)
-    c2 = bench_ppo(args, world, rank, device, 256) if args.c2 and args.n_envs != 256 else None
+    # shape) on the GPU; secondary: BASELINE configs[1] (256 envs per GPU); strong scaling
+    # (--global-envs): the given env count split over the ranks
+    if args.global_envs and args.global_envs % world:
+        raise SystemExit(f'--global-envs {args.global_envs} is not divisible by {world} ranks')
+    n_head = args.global_envs // world if args.global_envs else args.n_envs
+    head = bench_ppo(args, world, rank, device, n_head)
+    c2 = bench_ppo(args, world, rank, device, 256) if args.c2 and n_head != 256 else None
+    # BASELINE configs[2..4] as compact objects of the same one-GPU line
+    sec = compact_secondaries(args, device) if world == 1 and args.secondary else {}
 
     if rank == 0:
         def dominant(r):
@@ -513,20 +617,23 @@ def main():
             'warmup': args.warmup,
             'ms_per_step': round(head['ms_per_step'], 4),
             'higher_is_better': True,
-            'scaling': 'weak',
+            'scaling': 'strong' if args.global_envs else 'weak',
             'vs_baseline': None,
             'dtype': 'f32',
             'data': 'synthetic: CartPole-v1 observation replay recorded on the host '
                     '(np.random.default_rng(55+rank)), random-init weights',
             'config': {
-                'workload': (f'PPO CartPole-v1, {args.n_envs} envs/GPU, MLP[64,64], '
-                             f'n_steps={args.n_steps}, 4 epochs x 4 minibatches, synthetic obs '
-                             f'replay' + (' (the metric\'s 16-env configuration)'
-                                          if args.n_envs == 16 else '')),
-                'n_envs_per_gpu': args.n_envs,
+                'workload': (f'PPO CartPole-v1, {n_head} envs/GPU'
+                             + (f' ({args.global_envs} in all)' if args.global_envs else '')
+                             + f', MLP[64,64], n_steps={args.n_steps}, 4 epochs x 4 minibatches, '
+                             f'synthetic obs replay' + (' (the metric\'s 16-env configuration)'
+                                                        if n_head * world == 16 or
+                                                        (n_head == 16 and not args.global_envs)
+                                                        else '')),
+                'n_envs_per_gpu': n_head,
                 'n_steps': args.n_steps,
-                'batch_per_gpu': args.n_envs * args.n_steps,
-                'minibatch_per_gpu': args.n_envs * args.n_steps // 4,
+                'batch_per_gpu': n_head * args.n_steps,
+                'minibatch_per_gpu': n_head * args.n_steps // 4,
                 'ppo_epochs': 4,
                 'parallelism': f'dp{world}',
                 'graph': head['graph'],
@@ -552,6 +659,7 @@ def main():
                 'update_roofline': c2['update_roofline'],
                 'rollout_roofline': c2['rollout_roofline'],
             }
+        line.update(sec)
         if world == 1 and args.cpu_baseline_seconds > 0:
             line['cpu_baseline'] = cpu_baseline(args, head['record'], head['theta0'])
         else:

@@ -52,6 +52,8 @@ extern "C" {
 
 int xa_abi_version(void);
 const char* xa_last_error(void);
+/* Hash of the sources the library was built from (xagents_amd/_build.py source_hash()). */
+const char* xa_build_hash(void);
 
 /* Number of parameters of the actor-critic MLP (obs -> 64 -> 64 -> {A, 1}). */
 int xa_mlp_param_count(int obs_dim, int n_actions);
@@ -286,7 +288,8 @@ int xa_clip_adam(float* theta, float* adam_m, float* adam_v, const float* grad, 
  * Persistent PPO update: EVERY optimizer step of one train step in ONE launch.
  * Replaces PPO.get_mini_batches + run_ppo_epochs + update_gradients
  * (xagents/ppo/agent.py:96-191): for epoch e, minibatch m (k = e*n_mb + m, n_mb =
- * ceil(batch/mb_size), ragged last minibatch as range(0, batch, mb_size) slices it):
+ * ceil(batch/mb_size), ragged last minibatch as range(0, batch, mb_size) slices it;
+ * E*n_mb <= 128):
  * the shuffled samples (XaShuffle, the same permutation as xa_ppo_minibatches),
  * advantage normalisation with the minibatch's mean / population std
  * (ppo/agent.py:180-183), clipped PPO loss + backward (as xa_ac_grad), global-norm clip

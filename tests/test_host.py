@@ -200,6 +200,18 @@ def test_library_exports_every_header_symbol():
     assert lib.xa_ppo_adv_stats_size(32768, 8192, 4) == 2 * 4 * 4 * 8
 
 
+def test_library_is_built_from_this_tree(monkeypatch):
+    """The library carries the hash of the sources it was built from; the loader refuses a
+    stale one (a build from other sources) with a message, never a silent mismatch."""
+    from xagents_amd import _build, _lib
+    assert _build.library_hash() == _build.source_hash()
+    assert _lib.load().xa_build_hash().decode() == _build.source_hash()
+    monkeypatch.setattr(_lib, '_lib', None)
+    monkeypatch.setattr(_build, 'source_hash', lambda: '0' * 16)
+    with pytest.raises(_lib.HipLibraryError, match='stale'):
+        _lib.load()
+
+
 def test_product_never_imports_oracle():
     for p in (ROOT / 'xagents_amd').rglob('*.py'):
         src = p.read_text()

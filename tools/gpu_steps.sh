@@ -15,6 +15,7 @@
 #   c3 c4 c5 secondary bench lines
 #   stamps   per-phase stamp shares of the persistent update (tools/diag_ppo_update.py)
 #   trace    per-block phase timeline of the persistent update (tools/trace_ppo_update.py)
+#   probe    tools/probe/tile_probe (the per-step block work in isolation, old vs new tile)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out
@@ -52,7 +53,8 @@ for step in "$@"; do
     ab)
       run ab_local 200 python bench.py --steps 40 --warmup 5 --cpu-baseline-seconds 0
       XA_PPO_LOCAL=0 run ab_spread 200 python bench.py --steps 40 --warmup 5 --cpu-baseline-seconds 0
-      run ab_local2 200 python bench.py --steps 40 --warmup 5 --cpu-baseline-seconds 0 ;;
+      run ab_local2 200 python bench.py --steps 40 --warmup 5 --cpu-baseline-seconds 0
+      python tools/bench_brief.py gpurun_out/${T}_ab_*.out ;;
     prof)
       (cd /tmp && timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/${T}_prof \
         -o run --output-format csv -- python $R/bench.py --steps 20 --warmup 5 \
@@ -73,6 +75,7 @@ for step in "$@"; do
           --output-format csv -- python $R/bench.py --n-envs 16 --no-c2 --steps 2 --warmup 1 \
           --cpu-baseline-seconds 0 --no-graph > $R/gpurun_out/${T}_pmc_$c.log 2>&1) || exit $?
       done ;;
+    probe) run probe 120 ./tools/probe/tile_probe 200 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -16,7 +16,7 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 OUT = ROOT / 'tools' / 'diag_lib'
 LIB = OUT / 'libxa_trace.so'
-STEPS, PTS = 64, 16
+STEPS, PTS = 32, 16
 
 
 def build():
@@ -33,7 +33,11 @@ def build():
 
 
 def analyse(tr, G, K):
-    t = tr[:G, :K, :6].astype(np.int64)  # [block, step, point] in 10-ns ticks
+    # [block, step, point] in 10-ns ticks: low 32 bits, re-based (wrap-safe within a launch)
+    base = int(tr[0, 0, 0])
+    tr = ((tr.astype(np.int64) - base) & 0xFFFFFFFF).astype(np.int64)
+    tr[tr > 0x7FFFFFFF] -= 1 << 32
+    t = tr[:G, :K, :6]
     us = lambda x: x / 100.0  # noqa: E731
     names = ['A: tile (+row into LDS)', 'row granule stores', 'B: wait rows + reduce + publish',
              'C: poll g + norm partials', 'norm + Adam + LDS refresh']
@@ -41,14 +45,18 @@ def analyse(tr, G, K):
     for i, nm in enumerate(names):
         d = t[:, :, i + 1] - t[:, :, i]
         print(f'  {nm:34s} {us(np.median(d.mean(0))):8.3f} {us(np.median(d.max(0))):8.3f}')
-    tt = tr[:G, :K].astype(np.int64)
-    if (tt[:, :, 8] > 0).all():
+    tt = tr[:G, :K]
+    if (tt[:, :, 8] != 0).all():
         tile = ['H1 (VALU tanh)', 'Z2 = H1 W2 (MFMA) + tanh', 'heads + loss + dz',
                 'dA2 + head grads', 'dW2, dH1 (MFMA)', 'dW1', 'tile end -> row combine done']
         seq = [0, 8, 9, 10, 11, 12, 13, 14]
         for i, nm in enumerate(tile[:-1]):
             d = tt[:, :, seq[i + 1]] - tt[:, :, seq[i]]
             print(f'    tile: {nm:28s} {us(np.median(d.mean(0))):8.3f} {us(np.median(d.max(0))):8.3f}')
+        for a_, b_, nm in ((0, 6, 'loop top -> W1 in registers'), (6, 7, 'H1 computed'),
+                           (7, 15, 'H1 stored (wave 0)'), (15, 8, 'B1 barrier wait')):
+            d = tt[:, :, b_] - tt[:, :, a_]
+            print(f'      H1 {nm:30s} {us(np.median(d.mean(0))):8.3f}')
         d = tt[:, :, 1] - tt[:, :, 14]
         print(f'    row combine into LDS (+loss sums) {us(np.median(d.mean(0))):8.3f} '
               f'{us(np.median(d.max(0))):8.3f}')
@@ -86,7 +94,7 @@ def main():
     from xagents_amd.utils.common import create_model
     L = _lib._lib
     L.xa_diag_read_trace_ppo.argtypes = [ctypes.c_void_p]
-    buf = np.zeros(256 * STEPS * PTS, np.uint64)
+    buf = np.zeros(256 * STEPS * PTS, np.uint32)
     for n in [int(a) for a in sys.argv[1:] if a.isdigit()] or (16, 256):
         envs = ReplayVecEnv('CartPole-v1', n, t_rec=4096, seed=55, device='cuda')
         model = create_model(envs, 'ppo', 'model', seed=55, device='cuda')
@@ -97,7 +105,10 @@ def main():
         assert L.xa_diag_read_trace_ppo(buf.ctypes.data) == 0
         tr = buf.reshape(256, STEPS, PTS)
         G, K = agent.update_blocks, agent.ppo_epochs * agent.n_mb
-        print(f'n_envs {n}: placement {agent._uargs.placement}, {G} blocks, {K} steps')
+        clk = tr[:G, STEPS - 1, 8:12].astype(np.int64)
+        ghz = (clk[:, 3] - clk[:, 1]) / np.maximum(clk[:, 2] - clk[:, 0], 1) * 0.1
+        print(f'n_envs {n}: placement {agent._uargs.placement}, {G} blocks, {K} steps, '
+              f'shader clock {np.median(ghz):.2f} GHz (min {ghz.min():.2f})')
         analyse(tr, G, K)
 
 

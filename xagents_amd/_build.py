@@ -2,7 +2,9 @@
 
 The library is plain C-ABI (include/xagents_hip.h); no torch headers are involved.
 """
+import hashlib
 import os
+import re
 import subprocess
 from concurrent.futures import ThreadPoolExecutor
 from pathlib import Path
@@ -30,14 +32,31 @@ def sources():
     return sorted(CSRC.glob('*.hip'))
 
 
-def _newest_input_mtime():
-    files = list(sources()) + list(CSRC.glob('*.hpp'))
-    files.append(PKG_DIR.parent / 'include' / 'xagents_hip.h')
-    return max(f.stat().st_mtime for f in files)
+def _inputs():
+    return sorted(list(sources()) + list(CSRC.glob('*.hpp'))) + [
+        PKG_DIR.parent / 'include' / 'xagents_hip.h']
+
+
+def source_hash():
+    """16 hex digits of SHA-256 over every library input (name + bytes): baked into the
+    library as xa_build_hash(), compared by needs_build() and _lib.load()."""
+    h = hashlib.sha256()
+    for f in _inputs():
+        h.update(f.name.encode() + b'\0' + f.read_bytes() + b'\0')
+    return h.hexdigest()[:16]
+
+
+def library_hash(path=LIB_PATH):
+    """The source hash baked into a built library (read from its bytes, no load)."""
+    try:
+        m = re.search(rb'XA_BUILD_HASH:([0-9a-f]{16})', Path(path).read_bytes())
+    except OSError:
+        return None
+    return m.group(1).decode() if m else None
 
 
 def needs_build():
-    return not LIB_PATH.exists() or LIB_PATH.stat().st_mtime < _newest_input_mtime()
+    return not LIB_PATH.exists() or library_hash() != source_hash()
 
 
 def build_library(force=False, verbose=False):
@@ -45,10 +64,11 @@ def build_library(force=False, verbose=False):
     if not force and not needs_build():
         return LIB_PATH
     BUILD_DIR.mkdir(parents=True, exist_ok=True)
+    digest = source_hash()
 
     def compile_one(src):
         obj = BUILD_DIR / (src.stem + '.o')
-        cmd = [HIPCC, *CFLAGS, '-c', str(src), '-o', str(obj)]
+        cmd = [HIPCC, *CFLAGS, f'-DXA_BUILD_HASH="{digest}"', '-c', str(src), '-o', str(obj)]
         if verbose:
             print(' '.join(cmd))
         res = subprocess.run(cmd, capture_output=True, text=True)

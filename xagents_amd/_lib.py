@@ -313,6 +313,7 @@ XA_ACT_TANH = 2
 _SIGNATURES = {
     'xa_abi_version': (c_int, []),
     'xa_last_error': (ctypes.c_char_p, []),
+    'xa_build_hash': (ctypes.c_char_p, []),
     'xa_mlp_param_count': (c_int, [c_int, c_int]),
     'xa_counter_bump': (c_int, [c_void_p, c_void_p]),
     'xa_gae': (
@@ -451,6 +452,14 @@ def load(path=None):
         fn.restype = res
         fn.argtypes = args
     if path is None:
+        # the product library must be built from the sources in this tree (diagnostic
+        # builds loaded by path are exempt)
+        from xagents_amd._build import source_hash
+        built, want = lib.xa_build_hash().decode(), source_hash()
+        if built != want:
+            raise HipLibraryError(
+                f'{p} is stale: built from sources {built}, this tree is {want}; rebuild with '
+                f'`python -m xagents_amd._build` (or __graft_entry__.build())')
         _lib = lib
     return lib
 

@@ -40,18 +40,19 @@
 #include <stdlib.h>
 
 #include "../../include/xagents_hip.h"
-#include "ac_tile.hpp"
+#include "ppo_tile.hpp"
 #include "xa_adam.hpp"
 #include "xa_common.hpp"
 
 namespace {
 
 using namespace xa_ac;
+using namespace xa_pt;
 
 typedef __attribute__((address_space(1))) unsigned gu32;
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 
-constexpr int kMaxSteps = 512;              // E * M optimizer steps per launch
+constexpr int kMaxSteps = 128;              // E * M optimizer steps per launch (xagents: 16)
 constexpr int kCtlBytes = 256;              // control words at the workspace start
 // 10 s of the 100 MHz wall clock per hop: data parallel, a hop also absorbs the other ranks'
 // host-side skew (one process per GPU)
@@ -152,33 +153,6 @@ XA_DEV bool poll_gran(__amdgpu_buffer_rsrc_t r, const uint32_t (&off)[N], int n,
   }
 }
 
-// Keras ApplyAdam element (xa_adam.hpp adam_elem) with sqrt and the division on the
-// hardware units (v_sqrt_f32, v_rcp_f32 + one Newton step): the update is checked
-// against float64 with a tolerance, and this runs for every parameter in every block
-XA_DEV void adam_fast(float g, float& th, float& m, float& v, float alpha, float omb1,
-                      float omb2, float eps) {
-  m = m + (g - m) * omb1;
-  v = v + (g * g - v) * omb2;
-  th = th - (m * alpha) * frcp(__builtin_amdgcn_sqrtf(v) + eps);
-}
-
-// the same on two parameters at once: the moment updates as packed f32 (v_pk_fma_f32 /
-// v_pk_mul_f32), sqrt and the reciprocal on the hardware units without a Newton step (the
-// update is checked against float64 with a tolerance)
-XA_DEV void adam_fast2(xa_f2 g, float& th0, float& th1, float& m0, float& m1, float& v0,
-                       float& v1, float alpha, float omb1, float omb2, float eps) {
-  const xa_f2 m = {m0, m1}, v = {v0, v1};
-  const xa_f2 mn = xa_fma2(g - m, xa_f2{omb1, omb1}, m);
-  const xa_f2 vn = xa_fma2(g * g - v, xa_f2{omb2, omb2}, v);
-  const xa_f2 step = mn * xa_f2{alpha, alpha};
-  th0 = th0 - step.x * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(vn.x) + eps);
-  th1 = th1 - step.y * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(vn.y) + eps);
-  m0 = mn.x;
-  m1 = mn.y;
-  v0 = vn.x;
-  v1 = vn.y;
-}
-
 // this workgroup's XCD (MI355X_MICROARCH.md: read placement from HW_REG_XCC_ID)
 XA_DEV int xcc_id() {
   unsigned x;
@@ -187,22 +161,47 @@ XA_DEV int xcc_id() {
 }
 
 // Per-block phase trace (diagnostic -DXA_TRACE builds only, tools/trace_ppo_update.py):
-// thread 0 of every logical block records the 100 MHz real-time clock at 8 points of
-// every optimizer step of the last launch.
-constexpr int kTraceSteps = 64, kTracePts = 16;
+// thread 0 of every logical block records the low 32 bits of the 100 MHz real-time clock
+// at 16 points of every optimizer step into LDS (a global store there would hold up the
+// next barrier until it is acknowledged) and copies them out at the end of the launch;
+// slot kTraceSteps - 1 holds the launch start / phase-0 hop and the shader clock pairs.
 #ifdef XA_TRACE
-__device__ unsigned long long xa_ppo_trace[256 * kTraceSteps * kTracePts];
-#define XA_TRACE_PT(blk, k, i)                                                            \
-  do {                                                                                    \
-    if (threadIdx.x == 0 && (k) < kTraceSteps) {                                          \
-      unsigned long long t_;                                                              \
-      asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");     \
-      xa_ppo_trace[((size_t)(blk) * kTraceSteps + (k)) * kTracePts + (i)] = t_;           \
-    }                                                                                     \
+constexpr int kTraceSteps = 32, kTracePts = 16;
+__device__ unsigned xa_ppo_trace[256 * kTraceSteps * kTracePts];
+#define XA_TRACE_PT(blk, k, i)                                                        \
+  do {                                                                                \
+    if (threadIdx.x == 0 && (k) < kTraceSteps) {                                      \
+      unsigned long long t_;                                                          \
+      asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");  \
+      U.trace[(k) * kTracePts + (i)] = (unsigned)t_;                                  \
+    }                                                                                 \
+  } while (0)
+// the shader clock beside the real-time clock (the clock rate the launch ran at)
+#define XA_TRACE_CLK(blk, i)                                                          \
+  do {                                                                                \
+    if (threadIdx.x == 0) {                                                           \
+      unsigned long long t_, c_;                                                      \
+      asm volatile("s_memrealtime %0\n\ts_memtime %1\n\ts_waitcnt lgkmcnt(0)"        \
+                   : "=s"(t_), "=s"(c_)::"memory");                                   \
+      U.trace[(kTraceSteps - 1) * kTracePts + 8 + 2 * (i)] = (unsigned)t_;            \
+      U.trace[(kTraceSteps - 1) * kTracePts + 9 + 2 * (i)] = (unsigned)c_;            \
+    }                                                                                 \
+  } while (0)
+#define XA_TRACE_FLUSH(blk)                                                           \
+  do {                                                                                \
+    __syncthreads();                                                                  \
+    for (int i_ = threadIdx.x; i_ < kTraceSteps * kTracePts; i_ += 256)              \
+      xa_ppo_trace[(size_t)(blk) * kTraceSteps * kTracePts + i_] = U.trace[i_];      \
   } while (0)
 #else
 #define XA_TRACE_PT(blk, k, i) \
   do {                         \
+  } while (0)
+#define XA_TRACE_CLK(blk, i) \
+  do {                       \
+  } while (0)
+#define XA_TRACE_FLUSH(blk) \
+  do {                      \
   } while (0)
 #endif
 
@@ -347,13 +346,29 @@ constexpr int kPreBytes = 16384;
 template <int OBS>
 constexpr int pre_max() { return kPreBytes / ((OBS + 4) * 4); }
 
-template <int OBS, int A>
+constexpr int kBF = 11;  // granules per thread of a one-round flat gather
+template <int OBS, int A, int TS>
 struct UpdLds {
-  TileLds<OBS, A> t;
-  alignas(16) float row[(offs(OBS, A).P + 3) & ~3];  // the block's gradient row, staged
-  float pre[pre_max<OBS>() * (OBS + 4)];             // preloaded tile inputs
+  PtLds<OBS, A, TS> t;
+  alignas(16) float row[(offs(OBS, A).P + 3) & ~3];  // the gradient row's non-W2 part, staged
+  alignas(16) float pre[pre_max<OBS>() * (OBS + 4)]; // preloaded tile inputs
+  alignas(16) float stage[TS * (OBS + 4)];           // one tile's inputs (when not preloaded)
+  // flat-gather scratch of phase B: its own array at TS = 16; at TS = 32 the tile's
+  // activation buffers sH1 .. sdA2 (dead between the row write and the next step's tile)
+  alignas(16) float scr_own[TS == 32 ? 4 : 2 * 256 * kBF];
+  XA_DEV float* scr() {
+    static_assert(TS != 32 || (H + 2 * TS) * LDW + H * PtLds<OBS, A, TS>::LDT >= 2 * 256 * kBF,
+                  "gather scratch");
+    return TS == 32 ? t.sH1 : scr_own;
+  }
+  // Adam moments of the thread's parameter slice (16 W2 values, then the rest: NS slots),
+  // four slots per 16-byte word, thread-major (lane-consecutive, no bank conflicts):
+  // mv4[0][q / 4][t] holds m of slots q .. q + 3, mv4[1] the same for v
+  static constexpr int NS = 16 + Dims<OBS, A>::RPT, NQ4 = (NS + 3) / 4;
+  float4 mv4[2][NQ4][256];
   float alpha[kMaxSteps];    // per optimizer step: the Adam step size
-  float stat[kMaxSteps][3];  // per optimizer step: advantage mean, population std, 1 / (std + eps)
+  // per optimizer step: advantage mean, population std, 1 / (std + eps), loss scale
+  float stat[kMaxSteps][4];
   double red[256 * 4];
   double wsum[4];
   int flag;
@@ -361,6 +376,9 @@ struct UpdLds {
   int wx[4][kXcds];   // census: blocks per (wave of block ids, XCD)
   int xmem[256];      // this XCD's blocks, ascending block id (two-level)
   int xrank;          // this block's position among them
+#ifdef XA_TRACE
+  unsigned trace[kTraceSteps * kTracePts];
+#endif
 };
 
 // Publish: every wave drained its write-through stores, then ONE lane counts the
@@ -446,13 +464,14 @@ XA_DEV int elect_local(unsigned* ctl, int G, unsigned par, int xcc, unsigned epo
 }
 
 // TS = samples per tile (32; 16 when the minibatch has at most 16 tiles of 32: twice the
-// blocks, half the element-wise work per block and step); LOC = XCD-local mode
-template <int OBS, int A, int TS, bool DP, bool LOC>
+// blocks, half the element-wise work per block and step); PRE = every tile input of the
+// launch fits the block's LDS records (gathered once in phase 0); loc = XCD-local mode
+template <int OBS, int A, int TS, bool DP, bool PRE>
 __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws ws, int K,
-                                                          int n_mb) {
+                                                          int n_mb, int loc) {
   constexpr int RPT = Dims<OBS, A>::RPT;
-  __shared__ __attribute__((aligned(16))) UpdLds<OBS, A> U;
-  TileLds<OBS, A>& L = U.t;
+  __shared__ __attribute__((aligned(16))) UpdLds<OBS, A, TS> U;
+  PtLds<OBS, A, TS>& L = U.t;
   const Offs o = offs(OBS, A);
   const int P = o.P;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -465,20 +484,21 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
   const unsigned epoch = gen + 1u;
   const unsigned par = gen & 1u;
   const int xcc = xcc_id();
-  const int G = LOC ? p.n_blocks : (int)gridDim.x;
-  const int b = LOC ? elect_local(ws.ctl, G, par, xcc, epoch, p.status, U.flag) : (int)blockIdx.x;
+  const int G = loc ? p.n_blocks : (int)gridDim.x;
+  const int b = loc ? elect_local(ws.ctl, G, par, xcc, epoch, p.status, U.flag) : (int)blockIdx.x;
   if (b < 0) return;
   XA_STAMP_BLOCK(b == 0)
   XA_STAMP(30);
   XA_TRACE_PT(b, kTraceSteps - 1, 6);  // launch start (after the election)
+  XA_TRACE_CLK(b, 0);
   const int B = p.batch, MB = p.mb_size;
   const uint64_t ctr = p.shuffle.rng_counter ? *p.shuffle.rng_counter : 0ull;
   // hand-off stores: write-through across XCDs, plain inside the elected XCD's L2
-  constexpr bool kWt = !LOC;
+  const bool kWt = !loc;
 
   // ---- census: which XCD this block runs on (a granule, read after the phase-0 hop) ----
   // 16-sample tiles run only on small grids (<= 32 blocks): one level, known at compile time
-  const bool two_level = !LOC && TS == S && G >= kTwoLevelMinG;
+  const bool two_level = !loc && TS == S && G >= kTwoLevelMinG;
   const __amdgpu_buffer_rsrc_t cen_r = rsrc(ws.cen_g, (uint32_t)(G * 16));
   if (two_level && tid == 0) st_gran2(cen_r, (uint32_t)(16 * b), __uint_as_float((unsigned)xcc),
                                       __uint_as_float((unsigned)xcc), epoch, true);
@@ -487,7 +507,7 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
   // inputs into LDS when all of them fit; the Adam step size of every step ----
   const int n_tiles_max = (min(MB, B) + TS - 1) / TS;
   const int TPB = (n_tiles_max + G - 1) / G;  // tiles per block per step (at most)
-  const bool pre = K * TPB * TS <= pre_max<OBS>();
+  constexpr bool pre = PRE;  // the host checked K * TPB * TS <= pre_max
   const int t0 = *p.adam_step;
   for (int k = tid; k < K; k += 256)
     U.alpha[k] = adam_alpha(p.adam.lr, p.adam.beta1, p.adam.beta2, t0 + k + 1);
@@ -589,12 +609,26 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
   XA_STAMP(31);
 
   // parameters: theta / m / v slices in registers for the whole launch
-  ParamSlice<OBS, A> ps;
+  PSlice<OBS, A, TS> ps;
   ps.init(tid);
-  float wv[16], rv[RPT], mw[16], mr[RPT], vw[16], vr[RPT];
+  float wv[16], rv[RPT];
   ps.load(p.theta, wv, rv);
-  ps.load(p.adam_m, mw, mr);
-  ps.load(p.adam_v, vw, vr);
+  constexpr int NS = UpdLds<OBS, A, TS>::NS, NQ4 = UpdLds<OBS, A, TS>::NQ4;
+  {  // the Adam moments live in LDS (register pressure of the step loop)
+    float mw[16], mr[RPT], vw[16], vr[RPT], mm[4 * NQ4], vv[4 * NQ4];
+    ps.load(p.adam_m, mw, mr);
+    ps.load(p.adam_v, vw, vr);
+#pragma unroll
+    for (int q = 0; q < 4 * NQ4; ++q) {
+      mm[q] = q < 16 ? mw[q] : q < NS ? mr[q - 16] : 0.0f;
+      vv[q] = q < 16 ? vw[q] : q < NS ? vr[q - 16] : 0.0f;
+    }
+#pragma unroll
+    for (int q4 = 0; q4 < NQ4; ++q4) {
+      U.mv4[0][q4][tid] = make_float4(mm[4 * q4], mm[4 * q4 + 1], mm[4 * q4 + 2], mm[4 * q4 + 3]);
+      U.mv4[1][q4][tid] = make_float4(vv[4 * q4], vv[4 * q4 + 1], vv[4 * q4 + 2], vv[4 * q4 + 3]);
+    }
+  }
   ps.to_lds(L, wv, rv);
 
   XA_STAMP(32);
@@ -680,6 +714,7 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
       U.stat[k][0] = (float)mean;
       U.stat[k][1] = (float)sqrt(var);
       U.stat[k][2] = 1.0f / (U.stat[k][1] + p.adv_eps);
+      U.stat[k][3] = 1.0f / (float)(min(MB, B - m * MB) * W);
     }
   }
 
@@ -739,9 +774,7 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
   // at byte offset base(r) + 16 c of `r`), staged as f32 pairs in LDS scratch (the W2
   // tiles: dead between the row write and phase C's refresh); summed afterwards in
   // ascending row order. Used when the rows x columns fit kBF granules per thread.
-  constexpr int kBF = 11;
-  float* const scr = L.sW2;  // spans sW2 and sW2T (2 H LDW floats >= 2 * 256 kBF)
-  static_assert(2 * H * LDW >= 2 * 256 * kBF, "gather scratch");
+  float* const scr = U.scr();
   auto gather_rows = [&](__amdgpu_buffer_rsrc_t r, int nrow, int ncol, auto base,
                          unsigned tg) -> bool {
     const int total = nrow * ncol;
@@ -766,11 +799,13 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
     return bad;
   };
 
-  TileAcc<OBS, A> acc;
+  PtAcc<OBS, A> acc;
+  float w2r[16];  // dH1's B operand: W2 row 16 w + li, columns 16 lq .. (load_w2_rows)
   int k_tr = 0;  // the step the tile trace points belong to
   auto stampf = [&](int slot) {
     XA_STAMP(slot);
-    XA_TRACE_PT(b, k_tr, 8 + (slot - 50));  // tile phases 50..55 -> points 8..13
+    // tile phases 50..55 -> points 8..13; H1 sub-points 47, 48, 49 -> 6, 7, 15
+    XA_TRACE_PT(b, k_tr, slot == 49 ? 15 : slot == 48 ? 7 : slot == 47 ? 6 : 8 + (slot - 50));
   };
   (void)k_tr;
   (void)stampf;
@@ -783,59 +818,73 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
     cfg.adv_mean = U.stat[k][0];
     cfg.adv_std = U.stat[k][1];
     cfg.adv_rstd = U.stat[k][2];
-    cfg.loss_scale = 1.0f / (float)(cnt * W);
+    cfg.loss_scale = U.stat[k][3];
     acc.zero();
+    load_w2_rows(L, w2r);
     if (p.theta_trace && b == 0) ps.store(p.theta_trace + (size_t)k * P, wv, rv);  // diagnostic
     XA_STAMP(34);
     XA_TRACE_PT(b, k, 0);
     k_tr = k;
+    // the block's gradient row in exchange order: the W2 part straight from the MFMA
+    // accumulators as granule pairs (from the last tile, overlapping its dH1 phase), the
+    // other parameters through LDS below
+    const bool row_wt = kWt && !two_level;
+    auto w2_out = [&](const PtAcc<OBS, A>& a) {
+#ifndef XA_ABL_ROW
+      pt_write_row_w2<OBS, A>(a, [&](int pr, float v0, float v1) {
+        st_gran2(rows_r, (uint32_t)(((size_t)b * NP2 + pr) * 16), v0, v1, tag, row_wt);
+      });
+#endif
+    };
     // ---- A: forward + loss + backward of this block's tiles ----
     for (int tile = b; tile < n_tiles; tile += G) {
+      const bool last = tile + G >= n_tiles;
       if (pre) {
         // inputs straight from the phase-0 records (read-only: no staging, no barrier)
         XA_STAMP(35);
-        const PackedIn<OBS> in{&U.pre[((size_t)k * TPB * TS + ((tile - b) / G) * TS) * (OBS + 4)]};
+        const float* in = &U.pre[((size_t)k * TPB * TS + ((tile - b) / G) * TS) * (OBS + 4)];
 #ifndef XA_ABL_TILE  // diagnostic ablation builds (tools/ablate_update.py) only
-        tile_compute<OBS, A, decltype(stampf), PackedIn<OBS>, TS>(L, acc, cfg, stampf, in);
+        pt_tile<OBS, A, TS>(L, acc, cfg, in, wv, w2r, stampf, last, w2_out);
+#else
+        if (last) w2_out(acc);
 #endif
         XA_STAMP(36);
         XA_TRACE_PT(b, k, 14);
         continue;
       }
-      __syncthreads();
+      __syncthreads();  // the previous tile's reads of the staged records are done
       if (tid < TS) {
-        L.sValid[tid] = n_valid;
+        float* rec = &U.stage[tid * (OBS + 4)];
 #pragma unroll
-        for (int kk = 0; kk < OBS; ++kk) L.sX[tid * OBS + kk] = nx[kk];
-        L.sAct[tid] = n_act;
-        L.sRet[tid] = n_ret;
-        L.sOldV[tid] = n_oldv;
-        L.sOldLp[tid] = n_oldlp;
-        L.sAdvIn[tid] = 0.0f;
+        for (int kk = 0; kk < OBS; ++kk) rec[kk] = nx[kk];
+        rec[OBS] = n_valid ? n_act : -1.0f;
+        rec[OBS + 1] = n_ret;
+        rec[OBS + 2] = n_oldv;
+        rec[OBS + 3] = n_oldlp;
       }
       if (tile + G < n_tiles) fetch_tile(k, tile + G);
       __syncthreads();
       XA_STAMP(35);
-      tile_compute<OBS, A, decltype(stampf), StagedIn<OBS, A>, TS>(L, acc, cfg, stampf,
-                                                                 StagedIn<OBS, A>{L});
+      pt_tile<OBS, A, TS>(L, acc, cfg, U.stage, wv, w2r, stampf, last, w2_out);
       XA_STAMP(36);
     }
-    // ---- the block's gradient row, staged in LDS, published as granule pairs (measured:
-    // storing W2's pairs straight from the MFMA accumulators with a lane swap was slower,
-    // the write-through stores then stall the combine below) ----
+    if (b >= n_tiles) w2_out(acc);  // no tile of this minibatch: a zero row
 #ifndef XA_ABL_ROW
-    tile_write_row<OBS, A>(L, acc, [&](int i, float v) { srow[i] = v; });
+    pt_write_row_rest<OBS, A>(acc, [&](int x, float v) { srow[x] = v; });
 #endif
     XA_STAMP(44);
     XA_TRACE_PT(b, k, 1);
-    if (p.loss_out) {
-      const float ls = tile_loss_sums<OBS, A>(L, acc);
-      if (tid < 4) p.loss_out[((size_t)k * G + b) * 4 + tid] = ls;
+    if (p.loss_out && tid == 0) {
+      float* lo = p.loss_out + ((size_t)k * G + b) * 4;
+      lo[0] = acc.l_pg;
+      lo[1] = acc.l_v;
+      lo[2] = acc.l_ent;
+      lo[3] = acc.l_cnt;
     }
     __syncthreads();
-    for (int c = tid; c < NP2; c += 256)
+    for (int c = H * H / 2 + tid; c < NP2; c += 256)
       st_gran2(rows_r, (uint32_t)(((size_t)b * NP2 + c) * 16), srow[2 * c], srow[2 * c + 1], tag,
-               kWt && !two_level);
+               row_wt);
     XA_STAMP(45);
     XA_TRACE_PT(b, k, 2);
     fetch_tile(k + 1, b);  // the next step's first tile, while the other blocks finish
@@ -919,14 +968,15 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
     auto publish = [&](int c, float g0, float g1) {
       const int cc = c0 + c;
       st_gran2(g_r, (uint32_t)(16 * cc), g0, g1, tag, kWt);
+      // canonical order for the caller (exchange index -> flat parameter index)
       if (p.grad_out && k == K - 1) {
-        if (2 * cc < P) p.grad_out[2 * cc] = g0;
-        if (2 * cc + 1 < P) p.grad_out[2 * cc + 1] = g1;
+        if (2 * cc < P) p.grad_out[canon_of_exchange<OBS, A>(2 * cc)] = g0;
+        if (2 * cc + 1 < P) p.grad_out[canon_of_exchange<OBS, A>(2 * cc + 1)] = g1;
       }
       if (p.grad_trace) {  // diagnostic: every step's reduced gradient
         float* gt = p.grad_trace + (size_t)k * P;
-        if (2 * cc < P) gt[2 * cc] = g0;
-        if (2 * cc + 1 < P) gt[2 * cc + 1] = g1;
+        if (2 * cc < P) gt[canon_of_exchange<OBS, A>(2 * cc)] = g0;
+        if (2 * cc + 1 < P) gt[canon_of_exchange<OBS, A>(2 * cc + 1)] = g1;
       }
       sq += (double)g0 * (double)g0 + (double)g1 * (double)g1;
     };
@@ -1144,12 +1194,11 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
       constexpr int NG = 8 + RPT, NQ = 4;  // g slice pairs; norm partials per lane (G <= 256)
       uint32_t off[NG + NQ];
       f32x4v x[NG + NQ];
+      // exchange order: the thread's 16 W2 values are pairs 256 h + tid (coalesced)
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr)
+      for (int h = 0; h < 8; ++h) off[h] = (uint32_t)((256 * h + tid) * 16);
 #pragma unroll
-        for (int h = 0; h < 2; ++h) off[2 * rr + h] = (uint32_t)((ps.w2_off(rr) / 2 + h) * 16);
-#pragma unroll
-      for (int q = 0; q < RPT; ++q) off[8 + q] = (uint32_t)((ps.ri[q] >= 0 ? ps.ri[q] / 2 : 0) * 16);
+      for (int q = 0; q < RPT; ++q) off[8 + q] = (uint32_t)((ps.rx[q] >= 0 ? ps.rx[q] / 2 : 0) * 16);
       int n = NG;  // lanes past G poll fewer norm partials (valid ones first)
 #pragma unroll
       for (int u = 0; u < NQ; ++u) {
@@ -1178,15 +1227,13 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
       }
       XA_STAMP(46);
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        gw[4 * rr] = x[2 * rr][0];
-        gw[4 * rr + 1] = x[2 * rr][2];
-        gw[4 * rr + 2] = x[2 * rr + 1][0];
-        gw[4 * rr + 3] = x[2 * rr + 1][2];
+      for (int h = 0; h < 8; ++h) {
+        gw[2 * h] = x[h][0];
+        gw[2 * h + 1] = x[h][2];
       }
 #pragma unroll
       for (int q = 0; q < RPT; ++q)
-        gr[q] = ps.ri[q] >= 0 ? ((ps.ri[q] & 1) ? x[8 + q][2] : x[8 + q][0]) : 0.0f;
+        gr[q] = ps.rx[q] >= 0 ? ((ps.rx[q] & 1) ? x[8 + q][2] : x[8 + q][0]) : 0.0f;
 #pragma unroll
       for (int u = 0; u < NQ; ++u)
         if (NG + u < n) tot += gran_f64(x[NG + u]);
@@ -1196,7 +1243,11 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
     XA_TRACE_PT(b, k, 4);
 #ifndef XA_ABL_CNORM
     tot = xa_wave_sum_f64(tot);
-    const float sc = clip_scale(tot, p.adam.clip_norm);
+    // tf.clip_by_global_norm's scale clip * min(1 / norm, 1 / clip), on the hardware sqrt /
+    // reciprocal units (the update is checked against float64 with a tolerance)
+    const float gn = __builtin_amdgcn_sqrtf((float)tot);
+    const float sc = p.adam.clip_norm > 0.0f
+                         ? p.adam.clip_norm * fminf(frcp(gn), frcp(p.adam.clip_norm)) : 1.0f;
 #else
     const float sc = (float)tot;
 #endif
@@ -1204,17 +1255,31 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
 #ifndef XA_ABL_ADAM
     {
       const xa_f2 sc2 = {sc, sc};
+      float mm[4 * NQ4], vv[4 * NQ4], gg[4 * NQ4], th[4 * NQ4];
 #pragma unroll
-      for (int i = 0; i < 16; i += 2)
-        adam_fast2(xa_f2{gw[i], gw[i + 1]} * sc2, wv[i], wv[i + 1], mw[i], mw[i + 1], vw[i],
-                   vw[i + 1], alpha, omb1, omb2, p.adam.eps);
+      for (int q4 = 0; q4 < NQ4; ++q4) {
+        const float4 a = U.mv4[0][q4][tid], c = U.mv4[1][q4][tid];
+        mm[4 * q4] = a.x; mm[4 * q4 + 1] = a.y; mm[4 * q4 + 2] = a.z; mm[4 * q4 + 3] = a.w;
+        vv[4 * q4] = c.x; vv[4 * q4 + 1] = c.y; vv[4 * q4 + 2] = c.z; vv[4 * q4 + 3] = c.w;
+      }
 #pragma unroll
-      for (int q = 0; q + 1 < RPT; q += 2)
-        adam_fast2(xa_f2{gr[q], gr[q + 1]} * sc2, rv[q], rv[q + 1], mr[q], mr[q + 1], vr[q],
-                   vr[q + 1], alpha, omb1, omb2, p.adam.eps);
-      if (RPT % 2)
-        adam_fast(gr[RPT - 1] * sc, rv[RPT - 1], mr[RPT - 1], vr[RPT - 1], alpha, omb1, omb2,
-                  p.adam.eps);
+      for (int q = 0; q < 4 * NQ4; ++q) {
+        gg[q] = q < 16 ? gw[q] : q < NS ? gr[q - 16] : 0.0f;
+        th[q] = q < 16 ? wv[q] : q < NS ? rv[q - 16] : 0.0f;
+      }
+#pragma unroll
+      for (int q = 0; q < NS; q += 2)  // pairs (the pad slot past NS rides along, unused)
+        adam_pk(xa_f2{gg[q], gg[q + 1]} * sc2, th[q], th[q + 1], mm[q], mm[q + 1], vv[q],
+                vv[q + 1], alpha, omb1, omb2, p.adam.eps);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) wv[q] = th[q];
+#pragma unroll
+      for (int q = 0; q < RPT; ++q) rv[q] = th[16 + q];
+#pragma unroll
+      for (int q4 = 0; q4 < NQ4; ++q4) {
+        U.mv4[0][q4][tid] = make_float4(mm[4 * q4], mm[4 * q4 + 1], mm[4 * q4 + 2], mm[4 * q4 + 3]);
+        U.mv4[1][q4][tid] = make_float4(vv[4 * q4], vv[4 * q4 + 1], vv[4 * q4 + 2], vv[4 * q4 + 3]);
+      }
     }
 #endif
 #ifndef XA_ABL_LDS
@@ -1223,6 +1288,8 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
     XA_STAMP(43);
     XA_TRACE_PT(b, k, 5);
   }
+  XA_TRACE_CLK(b, 1);
+  XA_TRACE_FLUSH(b);
   if (b == 0 && tid == 0) {
     // zero the election slot of the next launch (this launch's slot is par; launch
     // gen + 1 uses par ^ 1, which launch gen - 1 used and nothing touches now)
@@ -1234,6 +1301,20 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
   }
   if (b == 0) {
     ps.store(p.theta, wv, rv);
+    float mw[16], mr[RPT], vw[16], vr[RPT];
+#pragma unroll
+    for (int q = 0; q < NS; ++q) {
+      const float4 a = U.mv4[0][q >> 2][tid], c = U.mv4[1][q >> 2][tid];
+      const float mq = (q & 3) == 0 ? a.x : (q & 3) == 1 ? a.y : (q & 3) == 2 ? a.z : a.w;
+      const float vq = (q & 3) == 0 ? c.x : (q & 3) == 1 ? c.y : (q & 3) == 2 ? c.z : c.w;
+      if (q < 16) {
+        mw[q] = mq;
+        vw[q] = vq;
+      } else {
+        mr[q - 16] = mq;
+        vr[q - 16] = vq;
+      }
+    }
     ps.store(p.adam_m, mw, mr);
     ps.store(p.adam_v, vw, vr);
     if (tid == 0) {
@@ -1257,6 +1338,7 @@ int occupancy_min() {
       (void*)ppo_update_kernel<OBS, A, S, true, false>, (void*)ppo_update_kernel<OBS, A, 16, true, false>,
       (void*)ppo_update_kernel<OBS, A, S, false, true>, (void*)ppo_update_kernel<OBS, A, 16, false, true>,
       (void*)ppo_update_kernel<OBS, A, S, true, true>, (void*)ppo_update_kernel<OBS, A, 16, true, true>};
+  // (template flags: DP, PRE)
   int occ = 1 << 30;
   for (void* k : kernels) {
     int o = 0;
@@ -1309,14 +1391,19 @@ template <int OBS, int A, int TS>
 void launch_ts(const XaPpoUpdateArgs* a, int G, bool dp, bool loc, const Ws& ws, int K, int n_mb,
                hipStream_t s) {
   const dim3 grid(loc ? G * kXcds : G);
-  if (dp && loc)
-    hipLaunchKernelGGL((ppo_update_kernel<OBS, A, TS, true, true>), grid, dim3(256), 0, s, *a, ws, K, n_mb);
+  // the tile inputs of every step fit the block's LDS records (same test as the kernel's)
+  const int n_tiles_max = (min(a->mb_size, a->batch) + TS - 1) / TS;
+  const int TPB = (n_tiles_max + G - 1) / G;
+  const bool pre = K * TPB * TS <= pre_max<OBS>();
+  const int l = loc ? 1 : 0;
+  if (dp && pre)
+    hipLaunchKernelGGL((ppo_update_kernel<OBS, A, TS, true, true>), grid, dim3(256), 0, s, *a, ws, K, n_mb, l);
   else if (dp)
-    hipLaunchKernelGGL((ppo_update_kernel<OBS, A, TS, true, false>), grid, dim3(256), 0, s, *a, ws, K, n_mb);
-  else if (loc)
-    hipLaunchKernelGGL((ppo_update_kernel<OBS, A, TS, false, true>), grid, dim3(256), 0, s, *a, ws, K, n_mb);
+    hipLaunchKernelGGL((ppo_update_kernel<OBS, A, TS, true, false>), grid, dim3(256), 0, s, *a, ws, K, n_mb, l);
+  else if (pre)
+    hipLaunchKernelGGL((ppo_update_kernel<OBS, A, TS, false, true>), grid, dim3(256), 0, s, *a, ws, K, n_mb, l);
   else
-    hipLaunchKernelGGL((ppo_update_kernel<OBS, A, TS, false, false>), grid, dim3(256), 0, s, *a, ws, K, n_mb);
+    hipLaunchKernelGGL((ppo_update_kernel<OBS, A, TS, false, false>), grid, dim3(256), 0, s, *a, ws, K, n_mb, l);
 }
 
 template <int OBS, int A>
@@ -1397,7 +1484,7 @@ extern "C" int xa_ppo_update(const XaPpoUpdateArgs* a, void* stream) {
 }
 XA_DIAG_READER(xa_diag_read_stamps_ppo)
 #ifdef XA_TRACE
-extern "C" int xa_diag_read_trace_ppo(unsigned long long* host) {
+extern "C" int xa_diag_read_trace_ppo(unsigned* host) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(xa_ppo_trace), sizeof(xa_ppo_trace)) == hipSuccess
              ? 0 : -1;
 }

@@ -17,6 +17,14 @@ void xa_set_error(const char* fmt, ...) {
 extern "C" const char* xa_last_error(void) { return g_xa_err; }
 extern "C" int xa_abi_version(void) { return XA_ABI_VERSION; }
 
+// the SHA-256 prefix of the sources this library was built from (xagents_amd/_build.py
+// passes it; the marker lets the loader find it in the file without loading it)
+#ifndef XA_BUILD_HASH
+#define XA_BUILD_HASH "unknown"
+#endif
+static const char kXaBuildHash[] = "XA_BUILD_HASH:" XA_BUILD_HASH;
+extern "C" const char* xa_build_hash(void) { return kXaBuildHash + 14; }
+
 extern "C" int xa_mlp_param_count(int obs_dim, int n_actions) {
   const int H = XA_MLP_HIDDEN;
   return obs_dim * H + H + H * H + H + H * n_actions + n_actions + H + 1;

@@ -86,7 +86,7 @@ class PPO(A2C):
         dp_ok = not self.distributed or (getattr(self, 'peer', None) is not None and
                                          self.world_size <= 16)
         if os.environ.get('XA_PPO_UPDATE', 'persistent') == 'persistent' and dp_ok and \
-                E * self.n_mb <= 512:
+                E * self.n_mb <= 128:
             obs_dim, A = self.model.obs_dim, self.n_actions
             G = kernels.ppo_update_blocks(obs_dim, A, MB)
             if G > 0 and self.distributed:
