@@ -5,8 +5,14 @@ rank 0 also runs a single-process agent on the union of the shards (data_paralle
 fed the same rollout uniforms and the rank-major union of the ranks' minibatch
 permutations. The data-parallel step must equal the union step: rollout buffers bit for
 bit, parameters up to the summation order of the gradient (xagents/ppo/agent.py:157-191).
+With XA_TEST_SKEW_S > 0 (launch-skew mode) every rank but 0 sleeps that long on the host
+before each of XA_TEST_STEPS train steps, so the persistent update's in-launch exchange
+waits for a late peer: the step must still equal the union step (first step) and every
+later step must leave the ranks' parameters identical with the device status word clean.
 Prints 'PPO DP OK <rank>'."""
+import os
 import sys
+import time
 from pathlib import Path
 
 import numpy as np
@@ -42,7 +48,6 @@ def main():
     perms = [np.stack([np.random.default_rng(200 + 10 * r + e).permutation(B)
                        for e in range(E)]).astype(np.int32) for r in range(world)]
     dp = make(records[rank], N)
-    import os
     want = os.environ.get('XA_PPO_UPDATE', 'persistent')
     assert dp.distributed and dp.world_size == world and dp.update_mode == want, dp.update_mode
     theta0 = dp.model.theta.cpu().numpy().astype(np.float64)
@@ -50,8 +55,18 @@ def main():
     p_dp = torch.from_numpy(perms[rank]).cuda()
     dp.set_rollout_uniforms(u_dp)
     dp.set_minibatch_permutation(p_dp)
-    dp.train_step()
-    torch.cuda.synchronize()
+    skew = float(os.environ.get('XA_TEST_SKEW_S', '0'))
+    n_steps = int(os.environ.get('XA_TEST_STEPS', '1'))
+
+    def step():
+        if skew > 0 and rank > 0:
+            time.sleep(skew * rank)  # this rank launches late: the others' launches wait
+        dp.train_step()
+        torch.cuda.synchronize()
+        if dp.update_mode == 'persistent':
+            assert int(dp._stats_status.item()) == 0, 'persistent update aborted (status word)'
+
+    step()
     got = {k: getattr(dp, k).cpu() for k in ('b_act', 'b_logp', 'b_val', 'b_ret')}
     got['theta'] = dp.model.theta.cpu()
     gathered = {}
@@ -83,6 +98,15 @@ def main():
         assert rel < 1e-4, f'data-parallel update deviates from the union update: {rel:.2e}'
         assert int(un.model.optimizer.iterations.item()) == E * M
     assert int(dp.model.optimizer.iterations.item()) == E * M
+    for _ in range(n_steps - 1):
+        step()
+        theta = dp.model.theta.cpu()
+        parts = [torch.empty_like(theta) for _ in range(world)]
+        dist.all_gather(parts, theta)
+        for p in parts[1:]:
+            assert torch.equal(p, parts[0]), 'ranks disagree on theta after a skewed step'
+        assert torch.isfinite(theta).all()
+    assert int(dp.model.optimizer.iterations.item()) == E * M * n_steps
     dist.barrier()
     if getattr(dp, 'dp_blocks', None) is not None:
         dp.dp_blocks.close()

@@ -31,12 +31,23 @@ def _run(worker, world, tag, extra_env=None, timeout=110):
         assert f'{tag} {r}' in out, out[-4000:]
 
 
-@pytest.mark.parametrize('mode', ['persistent', 'chain'])
-def test_ppo_data_parallel_equals_union(device, mode):
-    """xagents/ppo/agent.py:157-191 on the union of 2 shards vs the W = 2 data-parallel
+@pytest.mark.parametrize('mode,world', [('persistent', 2), ('chain', 2), ('persistent', 4)])
+def test_ppo_data_parallel_equals_union(device, mode, world):
+    """xagents/ppo/agent.py:157-191 on the union of W shards vs the W-rank data-parallel
     step (advantage sums and gradients exchanged), tests/ppo_dp_worker.py: the persistent
-    update exchanging inside its launch, and the per-minibatch chain."""
-    _run('ppo_dp_worker.py', 2, 'PPO DP OK', extra_env={'XA_PPO_UPDATE': mode})
+    update exchanging inside its launch (W = 2 and 4), and the per-minibatch chain."""
+    _run('ppo_dp_worker.py', world, 'PPO DP OK', extra_env={'XA_PPO_UPDATE': mode})
+
+
+def test_ppo_persistent_update_waits_for_late_ranks(device):
+    """Launch skew between ranks (one process per GPU launches with its own host-side
+    delay): rank 1 sleeps 0.5 s on the host before each of 3 train steps, so rank 0's
+    persistent update spins inside its launch until rank 1's pushes arrive. Every step
+    must complete without the timeout abort (status word 0), equal the union step, and
+    leave both ranks with identical parameters."""
+    _run('ppo_dp_worker.py', 2, 'PPO DP OK',
+         extra_env={'XA_PPO_UPDATE': 'persistent', 'XA_TEST_SKEW_S': '0.5',
+                    'XA_TEST_STEPS': '3'})
 
 
 def test_td3_data_parallel_done_patterns(device):

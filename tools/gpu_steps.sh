@@ -23,6 +23,9 @@ export TMPDIR=/tmp
 T=${TAG:-r03}
 R=$PWD
 PYT="python -u -m pytest -v --timeout 180 --timeout-method thread"
+# gpurun copies gpurun_out/ back only under 64 MiB: drop the per-dispatch kernel traces
+# (the --stats summaries stay) whatever way the session ends
+trap 'find gpurun_out -name "*kernel_trace.csv" -delete 2>/dev/null' EXIT
 
 run_pytest() {  # name, limit, args...
   local name=$1 lim=$2
@@ -46,7 +49,7 @@ for step in "$@"; do
   echo "== $step $(date +%T)"
   case $step in
     update) run_pytest update 400 tests/test_gpu_ppo_update.py ;;
-    dp) run_pytest dp 500 tests/test_gpu_dp.py tests/test_gpu_peer.py ;;
+    dp) run_pytest dp 500 tests/test_gpu_dp.py tests/test_gpu_peer.py tests/test_gpu_rccl_capture.py ;;
     gpu) run_pytest gpu 1000 tests -m gpu ;;
     smoke) run smoke 180 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 300 python bench.py --steps 20 --warmup 5 ;;
@@ -76,6 +79,20 @@ for step in "$@"; do
           --cpu-baseline-seconds 0 --no-graph > $R/gpurun_out/${T}_pmc_$c.log 2>&1) || exit $?
       done ;;
     probe) run probe 120 ./tools/probe/tile_probe 200 ;;
+    gemm)
+      # the GEMM tests, small-M timings, and PMC passes on the M = 64 / 336 dense dX
+      run_pytest gemm 300 tests/test_gpu_layers.py
+      run smallm 120 python tools/bench_smallm.py 4 16 64 128 336
+      for B in 64 336; do
+        (cd /tmp && timeout -s KILL 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY \
+          SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT \
+          SQ_VALU_MFMA_BUSY_CYCLES -d $R/gpurun_out/${T}_gpmc/p1_$B -o run --output-format csv \
+          -- python $R/tools/gemm_one.py 'dense dX' 10 $B > $R/gpurun_out/${T}_gpmc_p1_$B.log 2>&1) || exit 3
+        (cd /tmp && timeout -s KILL 90 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM \
+          SQ_INSTS_SALU SQ_INSTS_MFMA SQ_LDS_IDX_ACTIVE SQ_INSTS_SMEM SQ_WAVES \
+          -d $R/gpurun_out/${T}_gpmc/p2_$B -o run --output-format csv \
+          -- python $R/tools/gemm_one.py 'dense dX' 10 $B > $R/gpurun_out/${T}_gpmc_p2_$B.log 2>&1) || exit 4
+      done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

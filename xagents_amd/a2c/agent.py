@@ -314,10 +314,12 @@ class A2C(ExecutorActorCritic, OnPolicy):
         """Capture the rollout, the update, and the two back to back as hipGraphs (a
         train step replays the combined graph; the per-phase graphs serve the event-timed
         pass, so the update can be timed on its own). Data-parallel steps are
-        captured only when every exchange goes through the peer kernel: a torch
-        collective inside a capture (gloo, or RCCL where capture is unsupported)
-        invalidates the capture and the stream, so those steps run eagerly."""
-        if self.distributed and getattr(self, 'peer', None) is None:
+        captured when every exchange goes through the peer kernel or through RCCL (the
+        nccl backend's all-reduce is graph-capturable: tests/test_gpu_rccl_capture.py);
+        a gloo collective cannot be captured, so gloo steps without the peer path run
+        eagerly (as does any step whose capture raises)."""
+        if self.distributed and getattr(self, 'peer', None) is None and \
+                dist.get_backend() != 'nccl':
             self.use_graph = False
             self._graph = None
             return
