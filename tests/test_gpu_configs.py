@@ -115,27 +115,42 @@ def test_c4_ppo_cnn_128_env_shard(device):
     model = create_model(envs, 'ppo', 'model', seed=55, device=device)
     agent = PPO(envs, model, n_steps=T, seed=55, quiet=True)
     assert agent.executor_path and agent.mb == 4096 and agent.n_mb == 4
-    th0 = _np(model.theta)
     agent._executor_rollout()
-    # one minibatch of the update at full size vs float64
-    np.random.seed(9)
-    perm = np.random.permutation(n * T)[:agent.mb]
-    k = agent._upload_slots(perm)
-    agent._gather_minibatch(k)
-    agent._minibatch_step(k)
-    torch.cuda.synchronize()
     obs = agent.obs_buf[:T].cpu().numpy()
-    idx = perm
-    x = obs[idx % T, idx // T]  # flat env-major index i = env * T + t
-    act = agent.b_act.cpu().numpy().reshape(-1)[idx]
-    oldlp, oldv, ret = (_np(t).reshape(-1)[idx] for t in (agent.b_logp, agent.b_val, agent.b_ret))
-    x64, outs = O.forward(model.layers, th0, x, model.input_shape)
-    logits, v = outs[model.outputs[0]], outs[model.outputs[1]][:, 0]
-    dz, dv = _heads_grad_f64(logits, v, act, oldlp, oldv, ret, 'ppo')
-    g = O.backward(model.layers, th0, x64, outs, {model.outputs[0]: dz, model.outputs[1]: dv[:, None]})
-    assert _rel(_np(agent.grad), g) < 1e-4
+    opt = model.optimizer
+    # three chained minibatch steps of the update at full size, each teacher-forced at the
+    # device's own parameters: the gradient at theta_k vs float64 (1e-4), then the applied
+    # clip + Keras Adam step vs its float64 restatement from the device's own gradient and
+    # moments (the f32 optimizer arithmetic alone: moments 1e-5; the step theta_k+1 - theta_k
+    # 5e-5, since storing theta_k+1 in f32 rounds it by half an ulp of |theta|)
+    np.random.seed(9)
+    it0 = int(opt.iterations.item())
+    for step in range(3):
+        th, m, v_ = _np(model.theta), _np(opt.m), _np(opt.v)
+        idx = np.random.permutation(n * T)[:agent.mb]
+        k = agent._upload_slots(idx)
+        agent._gather_minibatch(k)
+        agent._minibatch_step(k)
+        torch.cuda.synchronize()
+        x = obs[idx % T, idx // T]  # flat env-major index i = env * T + t
+        act = agent.b_act.cpu().numpy().reshape(-1)[idx]
+        oldlp, oldv, ret = (_np(t).reshape(-1)[idx] for t in (agent.b_logp, agent.b_val, agent.b_ret))
+        x64, outs = O.forward(model.layers, th, x, model.input_shape)
+        logits, v = outs[model.outputs[0]], outs[model.outputs[1]][:, 0]
+        dz, dv = _heads_grad_f64(logits, v, act, oldlp, oldv, ret, 'ppo')
+        g = O.backward(model.layers, th, x64, outs, {model.outputs[0]: dz, model.outputs[1]: dv[:, None]})
+        gd = _np(agent.grad)
+        assert _rel(gd, g) < 1e-4, f'step {step}: gradient {_rel(gd, g):.2e}'
+        gc = OR.clip_by_global_norm_f64(gd, agent.grad_norm)[0]
+        th1, m1, v1 = OR.keras_adam_f64(th, m, v_, gc, it0 + step + 1, opt.learning_rate,
+                                        opt.beta_1, opt.beta_2, opt.epsilon)
+        assert int(opt.iterations.item()) == it0 + step + 1
+        em, ev = _rel(_np(opt.m), m1), _rel(_np(opt.v), v1)
+        assert em < 1e-5 and ev < 1e-5, f'step {step}: moments m {em:.2e} v {ev:.2e}'
+        es = _rel(_np(model.theta) - th, th1 - th)
+        assert es < 5e-5, f'step {step}: Adam step {es:.2e}'
     # full train steps
-    it0 = int(model.optimizer.iterations.item())
+    it0 = int(opt.iterations.item())
     for _ in range(2):
         agent.fused_train_step()
     agent._drain_episode_stats()
@@ -165,27 +180,32 @@ def test_c5_td3_64_envs_rb2(device):
     agent = TD3(envs, actor, critic, bufs, gradient_steps=1, seed=55, quiet=True)
     assert agent.batch_size == 64
     agent.fill_buffers()
-    c1 = _np(agent.critic.theta)
-    tt = [_np(m.theta) for m in (agent.target_actor, agent.target_critic, agent.target_critic2)]
-    agent.update_weights(1)
-    torch.cuda.synchronize()
-    s, a, r, d, s2 = (_np(x) for x in (agent.s, agent.a, agent.r, agent.d, agent.s2))
     fw = lambda m, th, x: O.forward(m.layers, th, x, m.input_shape)  # noqa: E731
-    ta = fw(agent.target_actor, tt[0], s2)[1][agent.target_actor.outputs[0]]
-    ta = np.clip(ta + _np(agent.noise), -1, 1)
-    s2a2 = np.concatenate([s2, ta], 1)
-    tv = np.minimum(*[fw(c, th, s2a2)[1][c.outputs[0]]
-                      for c, th in zip((agent.target_critic, agent.target_critic2), tt[1:])])
-    y = r[:, None] + (1 - d[:, None]) * np.float64(np.float32(0.99)) * tv
-    x64, o = fw(agent.critic, c1, np.concatenate([s, a], 1))
-    dv, _ = _critic_head_f64(o[agent.critic.outputs[0]], y, None)
-    g = O.backward(agent.critic.layers, c1, x64, o, {agent.critic.outputs[0]: dv})
-    assert _rel(_np(agent.g_critic), g) < 1e-4
+    # three chained gradient steps, each teacher-forced at the device's own critic and
+    # target parameters (the twin critics, the delayed actor and the Polyak targets move
+    # in between): the critic gradient vs float64 at 1e-4 every step
+    for step in range(3):
+        c1 = _np(agent.critic.theta)
+        tt = [_np(m.theta) for m in (agent.target_actor, agent.target_critic, agent.target_critic2)]
+        agent.update_weights(1)
+        torch.cuda.synchronize()
+        s, a, r, d, s2 = (_np(x) for x in (agent.s, agent.a, agent.r, agent.d, agent.s2))
+        ta = fw(agent.target_actor, tt[0], s2)[1][agent.target_actor.outputs[0]]
+        ta = np.clip(ta + _np(agent.noise), -1, 1)
+        s2a2 = np.concatenate([s2, ta], 1)
+        tv = np.minimum(*[fw(c, th, s2a2)[1][c.outputs[0]]
+                          for c, th in zip((agent.target_critic, agent.target_critic2), tt[1:])])
+        y = r[:, None] + (1 - d[:, None]) * np.float64(np.float32(0.99)) * tv
+        x64, o = fw(agent.critic, c1, np.concatenate([s, a], 1))
+        dv, _ = _critic_head_f64(o[agent.critic.outputs[0]], y, None)
+        g = O.backward(agent.critic.layers, c1, x64, o, {agent.critic.outputs[0]: dv})
+        e = _rel(_np(agent.g_critic), g)
+        assert e < 1e-4, f'step {step}: critic gradient {e:.2e}'
     for _ in range(100):
         agent.train_step()
     agent._drain_episode_stats()
     torch.cuda.synchronize()
     it = int(agent.critic.optimizer.iterations.item())
-    assert it == 1 + agent.games and agent.games > 0
+    assert it == 3 + agent.games and agent.games > 0
     assert agent.steps == 100 * n
     assert np.isfinite(_np(agent.actor.theta)).all()

@@ -12,7 +12,9 @@
 #   ab       bench lines without the CPU baseline: XCD-local vs spread persistent update
 #   prof     rocprofv3 --kernel-trace --stats of the default bench (no CPU baseline)
 #   pmc      FETCH_SIZE / WRITE_SIZE passes per shape (tools/gpurun_pmc_shapes.sh)
-#   c3 c4 c5 secondary bench lines
+#   c3 c4 c5 acer trpo   secondary bench lines
+#   gemm     GEMM tests, small-M timings, PMC passes on the dense dX GEMM
+#   icache   instruction-cache counters of the 16-env update
 #   stamps   per-phase stamp shares of the persistent update (tools/diag_ppo_update.py)
 #   trace    per-block phase timeline of the persistent update (tools/trace_ppo_update.py)
 #   probe    tools/probe/tile_probe (the per-step block work in isolation, old vs new tile)
@@ -25,7 +27,7 @@ R=$PWD
 PYT="python -u -m pytest -v --timeout 180 --timeout-method thread"
 # gpurun copies gpurun_out/ back only under 64 MiB: drop the per-dispatch kernel traces
 # (the --stats summaries stay) whatever way the session ends
-trap 'find gpurun_out -name "*kernel_trace.csv" -delete 2>/dev/null' EXIT
+trap 'find gpurun_out \( -name "*kernel_trace.csv" -o -name "*counter_collection.csv" \) -delete 2>/dev/null' EXIT
 
 run_pytest() {  # name, limit, args...
   local name=$1 lim=$2
@@ -62,10 +64,18 @@ for step in "$@"; do
       (cd /tmp && timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/${T}_prof \
         -o run --output-format csv -- python $R/bench.py --steps 20 --warmup 5 \
         --cpu-baseline-seconds 0 > $R/gpurun_out/${T}_prof_bench.json 2>&1) || exit $? ;;
-    pmc) TAG=${T} timeout -k 10 600 bash tools/gpurun_pmc_shapes.sh > gpurun_out/${T}_pmc.log 2>&1 || exit $? ;;
+    pmc)
+      TAG=${T} timeout -k 10 600 bash tools/gpurun_pmc_shapes.sh > gpurun_out/${T}_pmc.log 2>&1 || exit $?
+      # the per-dispatch counter CSVs are too big to travel back: keep the per-launch summary
+      cp profiles/traffic.json gpurun_out/${T}_traffic.json
+      XA_TRAFFIC_OUT=gpurun_out/${T}_traffic.json python tools/pmc_traffic.py gpurun_out ${T}_n16 ${T}_n256 \
+        > gpurun_out/${T}_traffic.log 2>&1
+      find gpurun_out -name "*counter_collection.csv" -delete ;;
     c3) run c3 300 python bench.py --config c3 --steps 30 --warmup 5 ;;
     c4) run c4 400 python bench.py --config c4 --steps 4 --warmup 1 ;;
     c5) run c5 300 python bench.py --config c5 --steps 30 --warmup 5 ;;
+    acer) run acer 300 python bench.py --config acer --steps 10 --warmup 2 ;;
+    trpo) run trpo 300 python bench.py --config trpo --steps 10 --warmup 2 ;;
     stamps) run stamps 200 python tools/diag_ppo_update.py --no-build ;;
     trace)
       run trace 200 python tools/trace_ppo_update.py --no-build 16 256
@@ -92,6 +102,8 @@ for step in "$@"; do
           SQ_INSTS_SALU SQ_INSTS_MFMA SQ_LDS_IDX_ACTIVE SQ_INSTS_SMEM SQ_WAVES \
           -d $R/gpurun_out/${T}_gpmc/p2_$B -o run --output-format csv \
           -- python $R/tools/gemm_one.py 'dense dX' 10 $B > $R/gpurun_out/${T}_gpmc_p2_$B.log 2>&1) || exit 4
+        python tools/pmc_summary.py 'gemm_' $(find gpurun_out/${T}_gpmc/p1_$B gpurun_out/${T}_gpmc/p2_$B \
+          -name "*counter_collection.csv") > gpurun_out/${T}_gemm_pmc_M$B.txt
       done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac

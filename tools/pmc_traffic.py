@@ -1,10 +1,11 @@
-"""Turn the rocprofv3 PMC passes (tools/gpurun_pmc.sh, tools/gpurun_r02n.sh) into
+"""Turn the rocprofv3 PMC passes (tools/gpurun_pmc_shapes.sh, run by `tools/gpu_steps.sh pmc`) into
 profiles/traffic.json: HBM bytes per launch of the hot kernels, keyed per workload shape
 (`<kernel>_<tag>`, e.g. ppo_update_n16) when the passes ran per shape. FETCH_SIZE / WRITE_SIZE are in KB; on gfx950
 FETCH_SIZE counts half the bytes of wide coalesced reads (MI355X_MICROARCH.md, HBM), so
 it is doubled; WRITE_SIZE is exact for 16-B-per-lane stores."""
 import csv
 import json
+import os
 import sys
 from collections import defaultdict
 from pathlib import Path
@@ -50,7 +51,7 @@ def main(out_dir='gpurun_out', *tags):
     """No tags: gpurun_out/pmc_{FETCH_SIZE,WRITE_SIZE} -> unsuffixed keys (round 1 layout).
     Tags (e.g. r02n_n16): gpurun_out/pmc_<tag>_{FETCH_SIZE,WRITE_SIZE} -> keys suffixed
     with the tag's last '_' field (ppo_update_n16). Merges into the existing file."""
-    f_out = ROOT / 'profiles' / 'traffic.json'
+    f_out = Path(os.environ.get('XA_TRAFFIC_OUT', ROOT / 'profiles' / 'traffic.json'))
     res = json.loads(f_out.read_text()) if f_out.exists() else {}
     if not tags:
         new, fetch = entries(Path(out_dir) / 'pmc_FETCH_SIZE', Path(out_dir) / 'pmc_WRITE_SIZE')
@@ -67,7 +68,7 @@ def main(out_dir='gpurun_out', *tags):
         new, _ = entries(Path(out_dir) / f'pmc_{tag}_FETCH_SIZE',
                          Path(out_dir) / f'pmc_{tag}_WRITE_SIZE', suffix)
         for v in new.values():
-            v['source'] = f'rocprofv3 --pmc passes {tag} (tools/gpurun_r02n.sh, tools/gpurun_pmc_shapes.sh)'
+            v['source'] = f'rocprofv3 --pmc passes {tag} (tools/gpurun_pmc_shapes.sh)'
         res.update(new)
     f_out.parent.mkdir(exist_ok=True)
     f_out.write_text(json.dumps(res, indent=1) + '\n')

@@ -11,12 +11,14 @@
 //   h1_j = tanh(sum_k x_k W1[k][j] + b1_j)              (fma chain over k)
 //   h1 -> LDS (wave-private row), 16 x ds_read_b128 broadcast back
 //   h2_j = tanh(sum of 8 interleaved 8-long fma chains + b2_j)
-//   logit_a = butterfly_sum_j(h2_j * W3[j][a]) + b3_a ;  value likewise
+//   h2 -> the wave's LDS row of this step (a [64 steps][64 units] chunk buffer)
+//   cartpole only: logit_a = butterfly_sum_j(h2_j * W3[j][a]) + b3_a (the sample needs them)
 //   env step (replay: records of 64 steps fetched a chunk ahead, one lane per step,
 //   read back with readlane; cartpole: inverse-CDF sample, then f64 dynamics)
-//   logits / value parked in lane (t & 63)
-// and once per 64-step chunk, lane j on step t0 + j: softmax, log-prob, entropy and
-// (replay env, whose record stream ignores the action) the sample.
+// and once per 64-step chunk, lane j on step t0 + j: the heads the step loop did not need
+// (the value; the logits too for the replay env, whose record stream ignores the action)
+// from the step's h2 row, summed in the pairwise order of the wave butterfly (bitwise the
+// same sums as in-step); softmax, log-prob, entropy and (replay env) the sample.
 // Envs are independent, so no inter-wave synchronisation exists anywhere.
 // The arithmetic order above is restated exactly by oracle/xa_oracle.c.
 #include "../../include/xagents_hip.h"
@@ -27,6 +29,8 @@ namespace {
 constexpr int H = XA_MLP_HIDDEN;
 constexpr int kWaves = 4;
 constexpr int kFusedMaxT = 1024;
+constexpr int kChunk = 64;     // steps per chunk (one per lane in the chunk pass)
+constexpr int kHS = H + 4;     // h2 chunk-buffer row stride (floats): conflict-free row reads
 
 XA_DEV void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -123,6 +127,61 @@ struct LaneMlp {
     heads(layer2(hv), logits, value);
   }
 };
+
+// Heads HF .. A of the chunk pass (HF = 0: logits and value; HF = A: the value only) for
+// the step whose h2 row this lane reads: head a = sum_j h2_j W34[j][a] with the products
+// rounded and summed as pairs, quads, octets, 16-unit rows, then (S2 + S3) + (S0 + S1) --
+// the tree xa_wave_sum's butterfly builds in lane 63, so every head equals its in-step
+// value bit for bit. wt: the wave's [H][AHP] table of (W3[j][0 .. A), w4[j], pad).
+template <int A, int HF>
+XA_DEV void chunk_heads(const float* __restrict__ hrow, const float* __restrict__ wt,
+                        float (&z)[A + 1]) {
+  constexpr int AH = A + 1, AHP = (AH + 3) & ~3;
+  float s_prev[AH], p01[AH];
+  // one 16-unit row per iteration, not unrolled: the row's 16 h2 values and table rows are
+  // all that is live on top of the step loop's state
+#pragma unroll 1
+  for (int r = 0; r < 4; ++r) {
+    float O[AH][2];
+#pragma unroll
+    for (int o = 0; o < 2; ++o) {
+      float Q[AH][2];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int j0 = 16 * r + 8 * o + 4 * q;
+        const float4 h4 = *reinterpret_cast<const float4*>(hrow + j0);
+        const float hj[4] = {h4.x, h4.y, h4.z, h4.w};
+        float v[AH][4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          float wr[AHP];
+#pragma unroll
+          for (int a4 = 0; a4 < AHP; a4 += 4) {
+            const float4 t = *reinterpret_cast<const float4*>(wt + (j0 + u) * AHP + a4);
+            wr[a4] = t.x; wr[a4 + 1] = t.y; wr[a4 + 2] = t.z; wr[a4 + 3] = t.w;
+          }
+#pragma unroll
+          for (int a = HF; a < AH; ++a) v[a][u] = hj[u] * wr[a];
+        }
+#pragma unroll
+        for (int a = HF; a < AH; ++a) Q[a][q] = (v[a][0] + v[a][1]) + (v[a][2] + v[a][3]);
+      }
+#pragma unroll
+      for (int a = HF; a < AH; ++a) O[a][o] = Q[a][0] + Q[a][1];
+    }
+#pragma unroll
+    for (int a = HF; a < AH; ++a) {
+      const float S = O[a][0] + O[a][1];  // row r's sum
+      if (r & 1) {
+        const float pr = s_prev[a] + S;
+        if (r == 1) p01[a] = pr;
+        else z[a] = pr + p01[a];  // (S2 + S3) + (S0 + S1)
+      } else {
+        s_prev[a] = S;
+      }
+    }
+  }
+}
 
 // Categorical over logits (TFP Categorical(logits=...), a2c/agent.py:59-94):
 // log_prob(a) = (l_a - m) - log(sum_k e^{l_k - m}); entropy = -sum p_k log p_k.
@@ -251,6 +310,10 @@ XA_DEV float xa_readlane(float v, int l) {
 template <int OBS, int A, bool REPLAY>
 __global__ __launch_bounds__(256) void mlp_rollout_kernel(XaRolloutArgs p) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int AH = A + 1, AHP = (AH + 3) & ~3;
+  constexpr int HF = REPLAY ? 0 : A;  // first head of the chunk pass
+  __shared__ __attribute__((aligned(16))) float hbuf[kWaves][kChunk * kHS];
+  __shared__ __attribute__((aligned(16))) float wtab[kWaves][H * AHP];
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   const int env = blockIdx.x * kWaves + wid;
@@ -259,10 +322,16 @@ __global__ __launch_bounds__(256) void mlp_rollout_kernel(XaRolloutArgs p) {
   float* sh = smem + wid * H;
   const bool fused = p.ret_out != nullptr && p.return_kind != XA_RETURNS_NONE;
   float* hist = smem + kWaves * H + wid * 3 * T;  // [rew | val | done] per wave when fused
+  float* const hb = hbuf[wid];  // h2 of the chunk's steps, row j = step t0 + j
 
   XA_STAMP_DECL
   LaneMlp<OBS, A> net;
   net.load(p.theta, lane);
+  {  // the chunk pass's head weights, lane j writes row j
+    float* wr = wtab[wid] + lane * AHP;
+#pragma unroll
+    for (int a = 0; a < AHP; ++a) wr[a] = a < A ? net.w3[a] : a == A ? net.w4 : 0.0f;
+  }
 
   const uint64_t ctr = p.rng_counter ? *p.rng_counter : 0ull;
 
@@ -298,14 +367,18 @@ __global__ __launch_bounds__(256) void mlp_rollout_kernel(XaRolloutArgs p) {
     for (int k = 0; k < OBS; ++k) x0[k] = x[k];
     for (int j = 0; j < n; ++j) {
       XA_STAMP(0);
-      float logits[A], value;
+      float logits[A];
       {
         float4 hv[H / 4];
         net.layer1(x, sh, lane, hv);
         XA_STAMP(1);
         const float h2 = net.layer2(hv);
         XA_STAMP(2);
-        net.heads(h2, logits, value);
+        hb[j * kHS + lane] = h2;  // the chunk pass's heads
+        if constexpr (!REPLAY) {
+#pragma unroll
+          for (int a = 0; a < A; ++a) logits[a] = xa_wave_sum(h2 * net.w3[a]) + net.b3[a];
+        }
       }
       XA_STAMP(3);
       const bool mine = lane == j;
@@ -345,10 +418,11 @@ __global__ __launch_bounds__(256) void mlp_rollout_kernel(XaRolloutArgs p) {
           cur = 0;
         }
       }
-      if (mine) {
+      if constexpr (!REPLAY) {
+        if (mine) {
 #pragma unroll
-        for (int a = 0; a < A; ++a) b_l[a] = logits[a];
-        b_val = value;
+          for (int a = 0; a < A; ++a) b_l[a] = logits[a];
+        }
       }
       ep_ret = ep_ret + r;
       if (mine) b_epret = ep_ret;
@@ -357,6 +431,17 @@ __global__ __launch_bounds__(256) void mlp_rollout_kernel(XaRolloutArgs p) {
       XA_STAMP(6);
     }
     // chunk pass: lane j finishes step t0 + j
+    wave_sync();  // the chunk's h2 rows are in LDS
+    {
+      float z[AH];
+      chunk_heads<A, HF>(hb + lane * kHS, wtab[wid], z);
+      if constexpr (REPLAY) {
+#pragma unroll
+        for (int a = 0; a < A; ++a) b_l[a] = z[a] + net.b3[a];
+      }
+      b_val = z[A] + net.b4;
+    }
+    wave_sync();  // the next chunk rewrites the rows
     const float u = p.uniforms ? c.u_given : c.u_philox;
     const CatOut<A> cat = categorical<A>(b_l, u, REPLAY ? -1 : b_act);
     float o_obs[OBS];

@@ -346,8 +346,9 @@ class WalkerVecEnv(TransitionReplayVecEnv):
         return a
 
     def reset(self):
-        """BipedalWalker.reset of every env into the state (the episode counters keep
-        counting, so every reset draws a fresh initial push)."""
+        """BipedalWalker.reset of every env into the state. The initial push is drawn from
+        the env's episode counter, which only a finished episode advances (xa_walker_step),
+        so repeated reset() calls without steps in between replay the same initial state."""
         super().reset()
         if not self._ready:
             return self.state
