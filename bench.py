@@ -60,6 +60,9 @@ def parse():
     p.add_argument('--preprocess', action='store_true',
                    help='c3 / c4: AtariWrapper on device (xa_atari_step: frame skip 4, '
                         'gray + resize of synthetic raw 210x160 RGB frames) in every env step')
+    p.add_argument('--lib', default=None,
+                   help='diagnostic A/B only: load this variant library (tools/build_variant.py) '
+                        'instead of xagents_amd/libxagents_hip.so')
     p.add_argument('--config', default='c2', choices=['c2', 'c3', 'c4', 'c5', 'trpo', 'acer'],
                    help='c2 (default, the BASELINE metric line); c3 DQN Pong-shaped, c4 PPO '
                         'CNN Breakout-shaped (global 1024 envs, strong scaling), c5 TD3')
@@ -592,6 +595,9 @@ def bench_ppo(args, world, rank, device, n_envs):
 
 def main():
     args = parse()
+    if args.lib:
+        from xagents_amd import _lib
+        _lib._lib = _lib.load(args.lib)
     if args.config != 'c2':
         return bench_offpolicy_and_cnn(args)
     import torch.distributed as dist

@@ -142,8 +142,11 @@ def test_c4_ppo_cnn_128_env_shard(device):
         gd = _np(agent.grad)
         assert _rel(gd, g) < 1e-4, f'step {step}: gradient {_rel(gd, g):.2e}'
         gc = OR.clip_by_global_norm_f64(gd, agent.grad_norm)[0]
-        th1, m1, v1 = OR.keras_adam_f64(th, m, v_, gc, it0 + step + 1, opt.learning_rate,
-                                        opt.beta_1, opt.beta_2, opt.epsilon)
+        # the hyper-parameters as the f32 values TF's ApplyAdam computes with (1 - beta_2 of
+        # the f32 0.999 is 0.99998713e-3, 1.3e-5 off the decimal 1e-3)
+        f32 = lambda x: float(np.float32(x))  # noqa: E731
+        th1, m1, v1 = OR.keras_adam_f64(th, m, v_, gc, it0 + step + 1, f32(opt.learning_rate),
+                                        f32(opt.beta_1), f32(opt.beta_2), f32(opt.epsilon))
         assert int(opt.iterations.item()) == it0 + step + 1
         em, ev = _rel(_np(opt.m), m1), _rel(_np(opt.v), v1)
         assert em < 1e-5 and ev < 1e-5, f'step {step}: moments m {em:.2e} v {ev:.2e}'

@@ -7,6 +7,8 @@
 #   update   tests/test_gpu_ppo_update.py
 #   dp       tests/test_gpu_dp.py + tests/test_gpu_peer.py
 #   gpu      the whole -m gpu suite
+#   configs  tests/test_gpu_configs.py (C3 / C4 / C5 at full size)
+#   variants bench A/B of tools/diag_lib/libxa_*.so (tools/build_variant.py) vs the product build
 #   smoke    __graft_entry__.smoke()
 #   bench    the default bench line (with the CPU baseline)
 #   ab       bench lines without the CPU baseline: XCD-local vs spread persistent update
@@ -53,6 +55,7 @@ for step in "$@"; do
     update) run_pytest update 400 tests/test_gpu_ppo_update.py ;;
     dp) run_pytest dp 500 tests/test_gpu_dp.py tests/test_gpu_peer.py tests/test_gpu_rccl_capture.py ;;
     gpu) run_pytest gpu 1000 tests -m gpu ;;
+    configs) run_pytest configs 400 tests/test_gpu_configs.py ;;
     smoke) run smoke 180 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 300 python bench.py --steps 20 --warmup 5 ;;
     ab)
@@ -71,6 +74,18 @@ for step in "$@"; do
       XA_TRAFFIC_OUT=gpurun_out/${T}_traffic.json python tools/pmc_traffic.py gpurun_out ${T}_n16 ${T}_n256 \
         > gpurun_out/${T}_traffic.log 2>&1
       find gpurun_out -name "*counter_collection.csv" -delete ;;
+    variants)
+      # A/B of the diagnostic variant libraries (tools/build_variant.py) against the product
+      # build, interleaved: base, each variant, base again (bench lines without CPU baseline)
+      B="python bench.py --steps 40 --warmup 5 --cpu-baseline-seconds 0 --no-secondary"
+      run var_base1 200 $B
+      for L in tools/diag_lib/libxa_*.so; do
+        n=$(basename $L .so); n=${n#libxa_}
+        [ "$n" = trace ] && continue
+        run var_$n 200 $B --lib $L
+      done
+      run var_base2 200 $B
+      python tools/bench_brief.py gpurun_out/${T}_var_*.out ;;
     c3) run c3 300 python bench.py --config c3 --steps 30 --warmup 5 ;;
     c4) run c4 400 python bench.py --config c4 --steps 4 --warmup 1 ;;
     c5) run c5 300 python bench.py --config c5 --steps 30 --warmup 5 ;;

@@ -470,12 +470,23 @@ __global__ __launch_bounds__(256) void gemm_tile_kernel(XaGemmK kargs) {
 // tile p (gate values fetched when the round started, ahead of the prefetches).
 // ---------------------------------------------------------------------------
 constexpr int RS_KP = 4, RS_UPR = 2;
+// Resident-A row layout, conflict-free for the lane groups of ds_read_b128 (MI355X_MICROARCH.md
+// LDS table: 4 groups of 16 lanes, bank (a/4) mod 64): element k = 16 b + 4 q + j of a row
+// sits at q SR + 4 b + j -- the k quads q = 0..3 of every 16-k step in 4 sub-rows whose
+// stride SR is a multiple of 256 B -- and rows are PA = 4 SR + 4 floats apart, so lane
+// (lq, li) reads its quad at 16-B slot li + b (mod 16) of the bank row: 16 distinct slots in
+// every lane group (the plain k-major row with a +4 pad put two lanes of every group on
+// one slot).
+template <int K>
+constexpr int rs_sr() { return K / 4 > 64 ? K / 4 : 64; }
+template <int K>
+constexpr int rs_pa() { return 4 * rs_sr<K>() + 4; }
 
 template <int MT, int CH, bool GATE>
 __global__ __launch_bounds__(512) void gemm_smallm_res_kernel(XaGemmArgs g, int rounds) {
-  constexpr int K = 128 * CH, KQ = K / RS_KP, PA = K + 4;
+  constexpr int K = 128 * CH, KQ = K / RS_KP, SR = rs_sr<K>(), PA = rs_pa<K>();
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* As = sm;                       // [MT 16][PA]
+  float* As = sm;                       // [MT 16][PA], sub-row layout above
   float* red = sm + MT * 16 * PA;       // [RS_UPR][MT][RS_KP - 1][256] (a tile's own part stays in registers)
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int kp = w % RS_KP, us = w / RS_KP;
@@ -484,10 +495,14 @@ __global__ __launch_bounds__(512) void gemm_smallm_res_kernel(XaGemmArgs g, int 
   const int units = (N + 15) / 16;
   const float* af = static_cast<const float*>(g.a);
   for (int sl = tid; sl < MT * 16 * (K / 4); sl += 512) {
-    const int m = sl / (K / 4), q = sl - m * (K / 4);
+    // 32 consecutive threads: 8 blocks b x the 4 quads q, b fastest -- 512 contiguous bytes
+    // of the global row, and every 8-lane group of the ds_write_b128 one 128-B run of a
+    // sub-row
+    const int m = sl / (K / 4), rem = sl - m * (K / 4);
+    const int q = (rem >> 3) & 3, b = ((rem >> 5) << 3) + (rem & 7);
     const f32x4 z = {0.0f, 0.0f, 0.0f, 0.0f};
-    *reinterpret_cast<f32x4*>(As + m * PA + 4 * q) =
-        m < M ? *reinterpret_cast<const f32x4*>(af + (int64_t)m * g.a_rm + 4 * q) : z;
+    *reinterpret_cast<f32x4*>(As + m * PA + q * SR + 4 * b) =
+        m < M ? *reinterpret_cast<const f32x4*>(af + (int64_t)m * g.a_rm + 16 * b + 4 * q) : z;
   }
   auto unit_of = [&](int r) { return (r * (int)gridDim.x + (int)blockIdx.x) * RS_UPR + us; };
   auto brow = [&](int r) {
@@ -506,7 +521,7 @@ __global__ __launch_bounds__(512) void gemm_smallm_res_kernel(XaGemmArgs g, int 
 #pragma unroll
   for (int gi = 0; gi < RS_R - 1; ++gi) load_b(gi, rb[gi]);
   __syncthreads();
-  const float* as = As + li * PA + kp * KQ + 4 * lq;
+  const float* as = As + li * PA + lq * SR + kp * (KQ / 4);  // k = kp KQ + 16 b' + 4 lq + j
   const int mt_fin = min(kp, MT - 1);  // the m tile this wave finishes (kp < MT)
   for (int r0 = 0; r0 < rounds; r0 += 2) {
 #pragma unroll
@@ -540,7 +555,7 @@ __global__ __launch_bounds__(512) void gemm_smallm_res_kernel(XaGemmArgs g, int 
             f32x4 aq[MT];
 #pragma unroll
             for (int mt = 0; mt < MT; ++mt)
-              aq[mt] = *reinterpret_cast<const f32x4*>(as + mt * 16 * PA + 32 * c + 16 * h);
+              aq[mt] = *reinterpret_cast<const f32x4*>(as + mt * 16 * PA + 8 * c + 4 * h);
 #pragma unroll
             for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -1018,7 +1033,7 @@ void tile_dims(int shape, int& bm, int& bn) {
 template <int MT, int CH, bool GATE>
 void launch_res1(const XaGemmArgs& g, int G, int rounds, hipStream_t s) {
   const size_t lds =
-      sizeof(float) * ((size_t)MT * 16 * (128 * CH + 4) + (size_t)RS_UPR * MT * (RS_KP - 1) * 256);
+      sizeof(float) * ((size_t)MT * 16 * rs_pa<128 * CH>() + (size_t)RS_UPR * MT * (RS_KP - 1) * 256);
   hipLaunchKernelGGL((gemm_smallm_res_kernel<MT, CH, GATE>), dim3(G), dim3(512), lds, s, g, rounds);
 }
 

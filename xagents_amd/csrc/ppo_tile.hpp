@@ -151,23 +151,6 @@ struct PtAcc {
   }
 };
 
-// Keras ApplyAdam (xa_adam.hpp adam_elem) on two parameters at once: the moment updates
-// as packed f32 (v_pk_fma_f32 / v_pk_mul_f32), sqrt and the reciprocal on the hardware
-// units (the update is checked against float64 with a tolerance)
-XA_DEV void adam_pk(xa_f2 g, float& th0, float& th1, float& m0, float& m1, float& v0, float& v1,
-                    float alpha, float omb1, float omb2, float eps) {
-  const xa_f2 m = {m0, m1}, v = {v0, v1};
-  const xa_f2 mn = xa_fma2(g - m, xa_f2{omb1, omb1}, m);
-  const xa_f2 vn = xa_fma2(g * g - v, xa_f2{omb2, omb2}, v);
-  const xa_f2 step = mn * xa_f2{alpha, alpha};
-  th0 = th0 - step.x * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(vn.x) + eps);
-  th1 = th1 - step.y * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(vn.y) + eps);
-  m0 = mn.x;
-  m1 = mn.y;
-  v0 = vn.x;
-  v1 = vn.y;
-}
-
 // ftanh (ac_tile.hpp) on two values at once: packed f32 polynomial and Newton step
 XA_DEV xa_f2 ftanh2(xa_f2 x) {
   const float c = 7.90531110763549805f;

@@ -65,6 +65,7 @@ constexpr int kXcds = 8;            // MI355X: 8 XCDs, each with its own L2
 enum { kCntStats = 0, kAbort = 1, kWin = 2 /* [2] */, kElect = 4 /* [2][kXcds] */ };
 constexpr int kTwoLevelMinG = 64;   // >= 8 blocks per XCD: reduce inside each XCD's L2 first
 
+
 // ---- write-through hand-off primitives (global address space, agent scope) ----
 XA_DEV void st_wt(float* p, float v) {
   __hip_atomic_store((gu32*)p, __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -126,30 +127,44 @@ XA_DEV double gran_f64(const f32x4v& v) {
 
 // Poll n (<= N) granule pairs (write-through loads) until every tag equals `tag`. Bounded
 // by the wall clock and the abort word; false on timeout / abort (the caller leaves).
+// One poll round is ONE L2 round trip: the abort word and the wall clock are read only
+// every 16th round (the abort word then travels in the same batch of loads as the
+// granules, not behind them; read every round from every wave it would pile the whole
+// grid's polls onto one L2 channel), so a granule that lands just after a round was
+// issued is seen one round trip later.
 template <int N>
 XA_DEV bool poll_gran(__amdgpu_buffer_rsrc_t r, const uint32_t (&off)[N], int n, unsigned tag,
                       f32x4v (&v)[N], unsigned* ctl, unsigned epoch, int* status) {
   uint64_t t0 = 0;
-  for (;;) {
+  for (unsigned it = 0;; ++it) {
+    const bool slow = (it & 15u) == 15u;
 #pragma unroll
     for (int u = 0; u < N; ++u)
       if (u < n) v[u] = __builtin_amdgcn_raw_buffer_load_b128(r, off[u], 0, kAuxSc1);
+    const unsigned ab = slow ? __hip_atomic_load((gu32*)(ctl + kAbort), __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT)
+                             : 0u;
     bool ok = true;
 #pragma unroll
     for (int u = 0; u < N; ++u)
       if (u < n) ok = ok && gran_ok(v[u], tag);
     if (ok) return true;
-    const uint64_t now = wall_clock64();
-    if (t0 == 0) t0 = now;
-    else if (now - t0 > kSpinTicks) {
-      __hip_atomic_store((gu32*)(ctl + kAbort), epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (status) __hip_atomic_store((gu32*)status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return false;
+    if (!slow) {
+#ifndef XA_POLL_NOSLEEP
+      __builtin_amdgcn_s_sleep(1);
+#endif
+      continue;
     }
-    if (__hip_atomic_load((gu32*)(ctl + kAbort), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-        epoch)
-      return false;
-    __builtin_amdgcn_s_sleep(1);
+    if (ab == epoch) return false;
+    {
+      const uint64_t now = wall_clock64();
+      if (t0 == 0) t0 = now;
+      else if (now - t0 > kSpinTicks) {
+        __hip_atomic_store((gu32*)(ctl + kAbort), epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (status) __hip_atomic_store((gu32*)status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return false;
+      }
+    }
   }
 }
 
@@ -246,7 +261,7 @@ __host__ __device__ inline Ws carve(void* base, int G, int P, int K) {
   w.ctl = (unsigned*)take(kCtlBytes);
   w.persist = (unsigned*)take(256);
   w.rows_g = take((size_t)G * PP * 8);
-  w.g_g = take(PP * 8 + (size_t)G * 16);
+  w.g_g = take(PP * 8 + (size_t)G * 64);
   w.adv = (double*)take((size_t)K * G * 2 * sizeof(double));
   w.cen_g = take((size_t)G * 16);
   w.xpart_g = take((size_t)kXcds * PP * 16);
@@ -290,7 +305,8 @@ template <int N>
 XA_DEV bool dp_poll(const void* base, const size_t (&off)[N], int n, unsigned tag,
                     uint32_t (&w)[N], unsigned* ctl, unsigned epoch, int* status) {
   uint64_t t0 = 0;
-  for (;;) {
+  for (unsigned it = 0;; ++it) {  // abort word and clock every 16th round, as poll_gran
+    const bool slow = (it & 15u) == 15u;
     bool ok = true;
 #pragma unroll
     for (int u = 0; u < N; ++u)
@@ -299,17 +315,20 @@ XA_DEV bool dp_poll(const void* base, const size_t (&off)[N], int n, unsigned ta
         w[u] = (uint32_t)v;
         ok = ok && (unsigned)(v >> 32) == tag;
       }
+    const unsigned ab = slow ? __hip_atomic_load((gu32*)(ctl + kAbort), __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT)
+                             : 0u;
     if (ok) return true;
-    const uint64_t now = wall_clock64();
-    if (t0 == 0) t0 = now;
-    else if (now - t0 > kSpinTicks) {
-      __hip_atomic_store((gu32*)(ctl + kAbort), epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (status) __hip_atomic_store((gu32*)status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return false;
+    if (slow) {
+      if (ab == epoch) return false;
+      const uint64_t now = wall_clock64();
+      if (t0 == 0) t0 = now;
+      else if (now - t0 > kSpinTicks) {
+        __hip_atomic_store((gu32*)(ctl + kAbort), epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (status) __hip_atomic_store((gu32*)status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return false;
+      }
     }
-    if (__hip_atomic_load((gu32*)(ctl + kAbort), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-        epoch)
-      return false;
     __builtin_amdgcn_s_sleep(1);
   }
 }
@@ -762,8 +781,12 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
   const int CB = (NP2 + G - 1) / G;
   const int c0 = min(NP2, b * CB), nc = min(NP2, c0 + CB) - c0;
   const __amdgpu_buffer_rsrc_t rows_r = rsrc(ws.rows_g, (uint32_t)((size_t)G * PP * 8));
-  const __amdgpu_buffer_rsrc_t g_r = rsrc(ws.g_g, (uint32_t)(PP * 8 + G * 16));
+  const __amdgpu_buffer_rsrc_t g_r = rsrc(ws.g_g, (uint32_t)(PP * 8 + G * 64));
   const uint32_t sq0 = (uint32_t)(PP * 8);  // the sums of squares follow g
+  // norm partials: one per wave (4 G, no block barrier behind the phase-B sums) on grids of
+  // <= 64 blocks, one per block (G) above (phase C polls <= 4 per lane)
+  const bool wave_sq = G <= 64;
+  const int NSQ = wave_sq ? 4 * G : G;
   const __amdgpu_buffer_rsrc_t xp_r = rsrc(ws.xpart_g, (uint32_t)(kXcds * PP * 16));
   float* srow = U.row;
   for (int i = P + tid; i < PP; i += 256) srow[i] = 0.0f;  // the pad stays zero
@@ -869,6 +892,9 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
       XA_STAMP(36);
     }
     if (b >= n_tiles) w2_out(acc);  // no tile of this minibatch: a zero row
+    // the rest of the row, staged in LDS and stored coalesced behind a barrier (measured:
+    // storing it straight from the lanes' registers as scattered pairs made the step slower,
+    // DESIGN.md section 5)
 #ifndef XA_ABL_ROW
     pt_write_row_rest<OBS, A>(acc, [&](int x, float v) { srow[x] = v; });
 #endif
@@ -1176,11 +1202,15 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
       if (__syncthreads_or(bad)) return;
     }
     sq = xa_wave_sum_f64(sq);
-    if (lane == 0) U.wsum[w] = sq;
-    __syncthreads();
-    if (tid == 0)
-      st_gran_f64(g_r, sq0 + (uint32_t)(16 * b), (U.wsum[0] + U.wsum[1]) + (U.wsum[2] + U.wsum[3]),
-                  tag, kWt);
+    if (wave_sq) {
+      if (lane == 0) st_gran_f64(g_r, sq0 + (uint32_t)(16 * (4 * b + w)), sq, tag, kWt);
+    } else {
+      if (lane == 0) U.wsum[w] = sq;
+      __syncthreads();
+      if (tid == 0)
+        st_gran_f64(g_r, sq0 + (uint32_t)(16 * b),
+                    (U.wsum[0] + U.wsum[1]) + (U.wsum[2] + U.wsum[3]), tag, kWt);
+    }
     XA_STAMP(40);
     XA_TRACE_PT(b, k, 3);
 
@@ -1190,6 +1220,18 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
     float gw[16], gr[RPT];
     double tot = 0.0;
     bool bad = false;
+    // the gradient-free half of the Adam moment updates, before the poll (its loads and
+    // multiplies leave the critical path): b1 m and b2 v of the thread's slots
+    float bm[4 * NQ4], bv[4 * NQ4];
+#pragma unroll
+    for (int q4 = 0; q4 < NQ4; ++q4) {
+      const float4 a = U.mv4[0][q4][tid], c = U.mv4[1][q4][tid];
+      const xa_f2 b1 = {p.adam.beta1, p.adam.beta1}, b2 = {p.adam.beta2, p.adam.beta2};
+      const xa_f2 m01 = xa_f2{a.x, a.y} * b1, m23 = xa_f2{a.z, a.w} * b1;
+      const xa_f2 v01 = xa_f2{c.x, c.y} * b2, v23 = xa_f2{c.z, c.w} * b2;
+      bm[4 * q4] = m01.x; bm[4 * q4 + 1] = m01.y; bm[4 * q4 + 2] = m23.x; bm[4 * q4 + 3] = m23.y;
+      bv[4 * q4] = v01.x; bv[4 * q4 + 1] = v01.y; bv[4 * q4 + 2] = v23.x; bv[4 * q4 + 3] = v23.y;
+    }
     {
       constexpr int NG = 8 + RPT, NQ = 4;  // g slice pairs; norm partials per lane (G <= 256)
       uint32_t off[NG + NQ];
@@ -1199,12 +1241,12 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
       for (int h = 0; h < 8; ++h) off[h] = (uint32_t)((256 * h + tid) * 16);
 #pragma unroll
       for (int q = 0; q < RPT; ++q) off[8 + q] = (uint32_t)((ps.rx[q] >= 0 ? ps.rx[q] / 2 : 0) * 16);
-      int n = NG;  // lanes past G poll fewer norm partials (valid ones first)
+      int n = NG;  // lanes past NSQ poll fewer norm partials (valid ones first)
 #pragma unroll
       for (int u = 0; u < NQ; ++u) {
         const int gi = u * 64 + lane;
-        off[NG + u] = gi < G ? sq0 + (uint32_t)(16 * gi) : 0u;
-        n += gi < G;
+        off[NG + u] = gi < NSQ ? sq0 + (uint32_t)(16 * gi) : 0u;
+        n += gi < NSQ;
       }
       if (G <= 32) {
         // few blocks: one round trip for both
@@ -1254,31 +1296,38 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
     const float alpha = U.alpha[k];
 #ifndef XA_ABL_ADAM
     {
-      const xa_f2 sc2 = {sc, sc};
-      float mm[4 * NQ4], vv[4 * NQ4], gg[4 * NQ4], th[4 * NQ4];
+      // m' = b1 m + (1 - b1) sc g, v' = b2 v + (1 - b2) sc^2 g^2 (Keras ApplyAdam on the
+      // clipped gradient sc g, regrouped: the update is checked against float64 with a
+      // tolerance), theta -= alpha m' / (sqrt(v') + eps)
+      const xa_f2 k1 = {sc * omb1, sc * omb1}, k2 = {(sc * sc) * omb2, (sc * sc) * omb2};
+      const xa_f2 al = {alpha, alpha}, ep = {p.adam.eps, p.adam.eps};
+      float th[4 * NQ4];
 #pragma unroll
-      for (int q4 = 0; q4 < NQ4; ++q4) {
-        const float4 a = U.mv4[0][q4][tid], c = U.mv4[1][q4][tid];
-        mm[4 * q4] = a.x; mm[4 * q4 + 1] = a.y; mm[4 * q4 + 2] = a.z; mm[4 * q4 + 3] = a.w;
-        vv[4 * q4] = c.x; vv[4 * q4 + 1] = c.y; vv[4 * q4 + 2] = c.z; vv[4 * q4 + 3] = c.w;
+      for (int q = 0; q < 4 * NQ4; ++q) th[q] = q < 16 ? wv[q] : q < NS ? rv[q - 16] : 0.0f;
+#pragma unroll
+      for (int q = 0; q < NS; q += 2) {
+        const xa_f2 g = {q < 16 ? gw[q] : gr[q - 16], q + 1 < 16 ? gw[q + 1] : q + 1 < NS ? gr[q + 1 - 16] : 0.0f};
+        const xa_f2 mn = xa_fma2(g, k1, xa_f2{bm[q], bm[q + 1]});
+        const xa_f2 vn = xa_fma2(g * g, k2, xa_f2{bv[q], bv[q + 1]});
+        const xa_f2 step = mn * al;
+        const xa_f2 den = xa_f2{__builtin_amdgcn_sqrtf(vn.x), __builtin_amdgcn_sqrtf(vn.y)} + ep;
+        const xa_f2 r = {__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
+        const xa_f2 tn = xa_fma2(-step, r, xa_f2{th[q], th[q + 1]});
+        th[q] = tn.x;
+        th[q + 1] = tn.y;
+        bm[q] = mn.x;
+        bm[q + 1] = mn.y;
+        bv[q] = vn.x;
+        bv[q + 1] = vn.y;
       }
-#pragma unroll
-      for (int q = 0; q < 4 * NQ4; ++q) {
-        gg[q] = q < 16 ? gw[q] : q < NS ? gr[q - 16] : 0.0f;
-        th[q] = q < 16 ? wv[q] : q < NS ? rv[q - 16] : 0.0f;
-      }
-#pragma unroll
-      for (int q = 0; q < NS; q += 2)  // pairs (the pad slot past NS rides along, unused)
-        adam_pk(xa_f2{gg[q], gg[q + 1]} * sc2, th[q], th[q + 1], mm[q], mm[q + 1], vv[q],
-                vv[q + 1], alpha, omb1, omb2, p.adam.eps);
 #pragma unroll
       for (int q = 0; q < 16; ++q) wv[q] = th[q];
 #pragma unroll
       for (int q = 0; q < RPT; ++q) rv[q] = th[16 + q];
 #pragma unroll
       for (int q4 = 0; q4 < NQ4; ++q4) {
-        U.mv4[0][q4][tid] = make_float4(mm[4 * q4], mm[4 * q4 + 1], mm[4 * q4 + 2], mm[4 * q4 + 3]);
-        U.mv4[1][q4][tid] = make_float4(vv[4 * q4], vv[4 * q4 + 1], vv[4 * q4 + 2], vv[4 * q4 + 3]);
+        U.mv4[0][q4][tid] = make_float4(bm[4 * q4], bm[4 * q4 + 1], bm[4 * q4 + 2], bm[4 * q4 + 3]);
+        U.mv4[1][q4][tid] = make_float4(bv[4 * q4], bv[4 * q4 + 1], bv[4 * q4 + 2], bv[4 * q4 + 3]);
       }
     }
 #endif
