@@ -15,6 +15,7 @@
 #   prof     rocprofv3 --kernel-trace --stats of the default bench (no CPU baseline)
 #   pmc      FETCH_SIZE / WRITE_SIZE passes per shape (tools/gpurun_pmc_shapes.sh)
 #   c3 c4 c5 acer trpo   secondary bench lines
+#   profc3   rocprofv3 kernel trace of the C3 bench + per-(kernel, grid) summary
 #   gemm     GEMM tests, small-M timings, PMC passes on the dense dX GEMM
 #   icache   instruction-cache counters of the 16-env update
 #   stamps   per-phase stamp shares of the persistent update (tools/diag_ppo_update.py)
@@ -86,6 +87,12 @@ for step in "$@"; do
       done
       run var_base2 200 $B
       python tools/bench_brief.py gpurun_out/${T}_var_*.out ;;
+    profc3)
+      (cd /tmp && timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/${T}_profc3 \
+        -o run --output-format csv -- python $R/bench.py --config c3 --steps 30 --warmup 5 \
+        --cpu-baseline-seconds 0 > $R/gpurun_out/${T}_profc3_bench.json 2>&1) || exit $?
+      python tools/kernel_shapes.py gpurun_out/${T}_profc3/run_kernel_trace.csv 25 \
+        > gpurun_out/${T}_profc3_shapes.txt 2>&1 ;;
     c3) run c3 300 python bench.py --config c3 --steps 30 --warmup 5 ;;
     c4) run c4 400 python bench.py --config c4 --steps 4 --warmup 1 ;;
     c5) run c5 300 python bench.py --config c5 --steps 30 --warmup 5 ;;

@@ -163,7 +163,7 @@ __global__ __launch_bounds__(256) void probe2(const float* theta, const float* r
       row[canon_of_exchange<OBS, A>(2 * pr)] = v0;
       row[canon_of_exchange<OBS, A>(2 * pr + 1)] = v1;
     };
-    pt_tile<OBS, A, TS>(L, acc, cfg, pre, wv, w2r, st, true,
+    pt_tile<OBS, A, TS>(L, acc, cfg, pre, wv, w2r, rv[0], rv[1], st, true,
                         [&](const PtAcc<OBS, A>& a) { pt_write_row_w2<OBS, A>(a, put_pair); });
     if (STAMPS) st(56);  // tile end
     pt_write_row_rest<OBS, A>(acc, [&](int x, float v) { row[canon_of_exchange<OBS, A>(x)] = v; });

@@ -71,6 +71,20 @@ XA_DEV int exchange_of_rest(int c) {
   return H * H + (c < o.w2 ? c : c - H * H);
 }
 
+// H1 from registers (OBS = 4): the lanes of hidden unit i own its layer-1 weights, lane row
+// lq the weight W1[lq][i] (rest slot 0) and row 0 also b1[i] (slot 1), so the next step's H1
+// needs no LDS refresh of W1 / b1 and no barrier in front of it (pt_tile gathers the four
+// rows' weights with permlane swaps); every other non-W2 parameter sits on the lanes of rows
+// 1..3. The rest slots per thread stay at Dims::RPT.
+#ifdef XA_NO_REGH1  // diagnostic A/B build: layer-1 weights through LDS behind a barrier
+constexpr bool kRegH1On = false;
+#else
+constexpr bool kRegH1On = true;
+#endif
+template <int OBS, int A>
+constexpr bool kRegH1 = kRegH1On && OBS == 4 &&
+                        1 + (offs(OBS, A).P - offs(OBS, A).b2 + 191) / 192 <= Dims<OBS, A>::RPT;
+
 template <int OBS, int A, int TS>
 struct PSlice {
   static constexpr int RPT = Dims<OBS, A>::RPT, NREST = Dims<OBS, A>::NREST;
@@ -78,6 +92,20 @@ struct PSlice {
   int ri[RPT];    // canonical flat index of rest value q, -1 past the end
   int rx[RPT];    // its exchange index, -1 past the end
   int rdst[RPT];  // its float offset inside PtLds, -1 past the end
+  // canonical index of rest slot q of thread tid (-1: none)
+  XA_DEV static int rest_of(int tid, int q) {
+    const Offs o = offs(OBS, A);
+    if constexpr (kRegH1<OBS, A>) {
+      const int w = tid >> 6, lane = tid & 63, lq = lane >> 4, li = lane & 15, i = 16 * w + li;
+      if (q == 0) return o.w1 + lq * H + i;
+      if (lq == 0) return q == 1 ? o.b1 + i : -1;
+      const int id2 = (lq - 1) * 64 + 16 * w + li, r2 = id2 + 192 * (q - 1);
+      return o.b2 + r2 < o.P ? o.b2 + r2 : -1;
+    } else {
+      const int r = tid + 256 * q;
+      return r < NREST ? (r < o.w2 ? r : r + H * H) : -1;
+    }
+  }
   XA_DEV void init(int tid) {
     typedef PtLds<OBS, A, TS> T;
     constexpr int AH = A + 1;
@@ -87,10 +115,9 @@ struct PSlice {
     row0 = 16 * (lane >> 4);
 #pragma unroll
     for (int q = 0; q < RPT; ++q) {
-      const int r = tid + 256 * q;
-      const int e = r < NREST ? (r < o.w2 ? r : r + H * H) : -1;
+      const int e = rest_of(tid, q);
       ri[q] = e;
-      rx[q] = r < NREST ? H * H + r : -1;
+      rx[q] = e >= 0 ? exchange_of_rest<OBS, A>(e) : -1;
       int d = -1;
       if (e < 0) d = -1;
       else if (e < o.b1) d = (int)(offsetof(T, sW1) / 4) + e;
@@ -191,15 +218,29 @@ XA_DEV void load_w2_rows(const PtLds<OBS, A, TS>& L, float (&w2r)[16]) {
   }
 }
 
+// permlane swaps between the four 16-lane rows of a wave (v_permlane16_swap /
+// v_permlane32_swap on the same value): .x of swap16 holds rows (0, 0, 2, 2), .y rows
+// (1, 1, 3, 3); .x of swap32 rows (0, 1, 0, 1), .y rows (2, 3, 2, 3)
+XA_DEV float2 xa_swap16(float v) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return make_float2(__uint_as_float(a[0]), __uint_as_float(a[1]));
+}
+XA_DEV float2 xa_swap32(float v) {
+  const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return make_float2(__uint_as_float(a[0]), __uint_as_float(a[1]));
+}
+
 // One tile: rec = TS packed LDS records {obs[OBS], action (< 0: padding), return, old
-// value, old log-prob}; w2c = the thread's W2 column slice, w2r = load_w2_rows; on the
-// block's last tile of the step (last) w2_out(acc) runs right after the dW2 MFMAs. Ends
-// after the dW1 accumulation (no trailing barrier; the next tile's first LDS writes come
-// after the other waves passed this tile's last barrier).
+// value, old log-prob}; w2c = the thread's W2 column slice, w2r = load_w2_rows (with
+// kRegH1 loaded here, after the first barrier); w1v / b1v = the lane's own layer-1 weight
+// W1[lq][i] and (row 0) b1[i] (kRegH1; unused otherwise); on the block's last tile of the
+// step (last) w2_out(acc) runs right after the dW2 MFMAs. Ends after the dW1 accumulation
+// (no trailing barrier; the next tile's first LDS writes come after the other waves passed
+// this tile's last barrier).
 template <int OBS, int A, int TS, class Stamp, class W2Out>
 XA_DEV void pt_tile(PtLds<OBS, A, TS>& L, PtAcc<OBS, A>& acc, const LossCfg& cfg,
-                    const float* rec, const float (&w2c)[16], const float (&w2r)[16],
-                    Stamp stamp, bool last, W2Out w2_out) {
+                    const float* rec, const float (&w2c)[16], float (&w2r)[16], float w1v,
+                    float b1v, Stamp stamp, bool last, W2Out w2_out) {
   static_assert(TS == 16 || TS == 32, "tile sizes: 16 or 32 samples");
   constexpr int NT = TS / 16, AH = A + 1, R = OBS + 4, LDT = PtLds<OBS, A, TS>::LDT;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
@@ -208,10 +249,30 @@ XA_DEV void pt_tile(PtLds<OBS, A, TS>& L, PtAcc<OBS, A>& acc, const LossCfg& cfg
   // ---- 1: H1 ----
   float h1[NT][4];
   {
+    // w1[j] = W1[kx[j]][i]: the lane's own row first (kRegH1: the weights of rows lq ^ j
+    // from the neighbouring lane rows, no LDS), k order per lane (f32 order only)
     float w1[OBS];
+    int kx[OBS];
+    float b1;
+    if constexpr (kRegH1<OBS, A>) {
+      const float2 s16 = xa_swap16(w1v), s32 = xa_swap32(w1v);
+      const float p1 = (lq & 1) ? s16.x : s16.y;  // row lq ^ 1
+      const float2 s48 = xa_swap32(p1);
+      w1[0] = w1v;
+      w1[1] = p1;
+      w1[2] = (lq & 2) ? s32.x : s32.y;  // row lq ^ 2
+      w1[3] = (lq & 2) ? s48.x : s48.y;  // row lq ^ 3
 #pragma unroll
-    for (int k = 0; k < OBS; ++k) w1[k] = L.sW1[k * H + i];
-    const float b1 = L.sb1[i];
+      for (int j = 0; j < OBS; ++j) kx[j] = lq ^ j;
+      b1 = xa_swap32(xa_swap16(b1v).x).x;  // row 0's b1[i] on every row
+    } else {
+#pragma unroll
+      for (int k = 0; k < OBS; ++k) {
+        w1[k] = L.sW1[k * H + i];
+        kx[k] = k;
+      }
+      b1 = L.sb1[i];
+    }
     stamp(47);  // (diagnostic) the weights are in registers
 #pragma unroll
     for (int mt = 0; mt < NT; ++mt) {
@@ -221,8 +282,8 @@ XA_DEV void pt_tile(PtLds<OBS, A, TS>& L, PtAcc<OBS, A>& acc, const LossCfg& cfg
         const int s = 16 * mt + 4 * lq + r;
         xa_f2 z = {0.0f, 0.0f};
 #pragma unroll
-        for (int k = 0; k < OBS; ++k)
-          z = xa_fma2(xa_f2{rec[s * R + k], rec[(s + 1) * R + k]}, xa_f2{w1[k], w1[k]}, z);
+        for (int j = 0; j < OBS; ++j)
+          z = xa_fma2(xa_f2{rec[s * R + kx[j]], rec[(s + 1) * R + kx[j]]}, xa_f2{w1[j], w1[j]}, z);
         const xa_f2 h = ftanh2(z + xa_f2{b1, b1});
         h1[mt][r] = h.x;
         h1[mt][r + 1] = h.y;
@@ -236,6 +297,7 @@ XA_DEV void pt_tile(PtLds<OBS, A, TS>& L, PtAcc<OBS, A>& acc, const LossCfg& cfg
   }
   stamp(49);  // this wave's H1 is done (before waiting for the others)
   __syncthreads();
+  if constexpr (kRegH1<OBS, A>) load_w2_rows(L, w2r);  // refreshed by every thread by now
   stamp(50);
   // ---- 2: Z2 = H1 W2 on MFMA (two accumulator chains), H2, head partials ----
   float h2[NT][4];
@@ -462,7 +524,7 @@ XA_DEV void pt_write_row_w2(const PtAcc<OBS, A>& acc, PutPair put_pair) {
 
 // the rest of the row (pt_write_row without its W2 part, which pt_tile stored early)
 template <int OBS, int A, class Put>
-XA_DEV void pt_write_row_rest(PtAcc<OBS, A>& acc, Put put) {
+XA_DEV void pt_write_row_rest(PtAcc<OBS, A>& acc, Put put, bool loss_sums = true) {
   constexpr int AH = A + 1;
   const Offs o = offs(OBS, A);
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
@@ -485,10 +547,12 @@ XA_DEV void pt_write_row_rest(PtAcc<OBS, A>& acc, Put put) {
   if (w == 0) {  // the tally lanes: wave 0, lq == 0, one sample each
 #pragma unroll
     for (int a = 0; a < AH; ++a) acc.gb34[a] = xa_sum16(acc.gb34[a]);
-    acc.l_pg = xa_sum16(acc.l_pg);
-    acc.l_v = xa_sum16(acc.l_v);
-    acc.l_ent = xa_sum16(acc.l_ent);
-    acc.l_cnt = xa_sum16(acc.l_cnt);
+    if (loss_sums) {  // (wave 0 is the last to reach the row barrier: skipped when unused)
+      acc.l_pg = xa_sum16(acc.l_pg);
+      acc.l_v = xa_sum16(acc.l_v);
+      acc.l_ent = xa_sum16(acc.l_ent);
+      acc.l_cnt = xa_sum16(acc.l_cnt);
+    }
   }
   if (lq == 0) {
 #pragma unroll

@@ -837,13 +837,15 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
     const int cnt = min(MB, B - m * MB);
     const int n_tiles = (cnt + TS - 1) / TS;
     const unsigned tag = tag_of(k);
-    __syncthreads();  // U.stat, the LDS weights of the previous step
+    // the LDS weights of the previous step's Adam: with the layer-1 weights in registers
+    // (kRegH1) the tile's first barrier orders them (H1 needs none of them), otherwise here
+    if constexpr (!kRegH1<OBS, A>) __syncthreads();
     cfg.adv_mean = U.stat[k][0];
     cfg.adv_std = U.stat[k][1];
     cfg.adv_rstd = U.stat[k][2];
     cfg.loss_scale = U.stat[k][3];
     acc.zero();
-    load_w2_rows(L, w2r);
+    if constexpr (!kRegH1<OBS, A>) load_w2_rows(L, w2r);
     if (p.theta_trace && b == 0) ps.store(p.theta_trace + (size_t)k * P, wv, rv);  // diagnostic
     XA_STAMP(34);
     XA_TRACE_PT(b, k, 0);
@@ -867,7 +869,7 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
         XA_STAMP(35);
         const float* in = &U.pre[((size_t)k * TPB * TS + ((tile - b) / G) * TS) * (OBS + 4)];
 #ifndef XA_ABL_TILE  // diagnostic ablation builds (tools/ablate_update.py) only
-        pt_tile<OBS, A, TS>(L, acc, cfg, in, wv, w2r, stampf, last, w2_out);
+        pt_tile<OBS, A, TS>(L, acc, cfg, in, wv, w2r, rv[0], rv[1], stampf, last, w2_out);
 #else
         if (last) w2_out(acc);
 #endif
@@ -888,7 +890,7 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
       if (tile + G < n_tiles) fetch_tile(k, tile + G);
       __syncthreads();
       XA_STAMP(35);
-      pt_tile<OBS, A, TS>(L, acc, cfg, U.stage, wv, w2r, stampf, last, w2_out);
+      pt_tile<OBS, A, TS>(L, acc, cfg, U.stage, wv, w2r, rv[0], rv[1], stampf, last, w2_out);
       XA_STAMP(36);
     }
     if (b >= n_tiles) w2_out(acc);  // no tile of this minibatch: a zero row
@@ -896,7 +898,7 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
     // storing it straight from the lanes' registers as scattered pairs made the step slower,
     // DESIGN.md section 5)
 #ifndef XA_ABL_ROW
-    pt_write_row_rest<OBS, A>(acc, [&](int x, float v) { srow[x] = v; });
+    pt_write_row_rest<OBS, A>(acc, [&](int x, float v) { srow[x] = v; }, p.loss_out != nullptr);
 #endif
     XA_STAMP(44);
     XA_TRACE_PT(b, k, 1);
