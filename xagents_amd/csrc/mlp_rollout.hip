@@ -27,7 +27,14 @@
 namespace {
 
 constexpr int H = XA_MLP_HIDDEN;
-constexpr int kWaves = 4;
+constexpr int kWaves = 4;       // xa_mlp_forward: waves (samples in flight) per workgroup
+// xa_mlp_rollout: env waves per workgroup. The waves never synchronise; one per workgroup
+// puts every env's wave on a CU of its own, measured fastest (16-env rollout 57.8 us at 4
+// waves, 54.9 at 2, 52.3 at 1: profiles/r03y_variants.txt)
+#ifndef XA_ROLLOUT_WAVES
+#define XA_ROLLOUT_WAVES 1
+#endif
+constexpr int kRollWaves = XA_ROLLOUT_WAVES;
 constexpr int kFusedMaxT = 1024;
 constexpr int kChunk = 64;     // steps per chunk (one per lane in the chunk pass)
 constexpr int kHS = H + 4;     // h2 chunk-buffer row stride (floats): conflict-free row reads
@@ -308,20 +315,20 @@ XA_DEV float xa_readlane(float v, int l) {
 }
 
 template <int OBS, int A, bool REPLAY>
-__global__ __launch_bounds__(256) void mlp_rollout_kernel(XaRolloutArgs p) {
+__global__ __launch_bounds__(64 * kRollWaves) void mlp_rollout_kernel(XaRolloutArgs p) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int AH = A + 1, AHP = (AH + 3) & ~3;
   constexpr int HF = REPLAY ? 0 : A;  // first head of the chunk pass
-  __shared__ __attribute__((aligned(16))) float hbuf[kWaves][kChunk * kHS];
-  __shared__ __attribute__((aligned(16))) float wtab[kWaves][H * AHP];
+  __shared__ __attribute__((aligned(16))) float hbuf[kRollWaves][kChunk * kHS];
+  __shared__ __attribute__((aligned(16))) float wtab[kRollWaves][H * AHP];
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
-  const int env = blockIdx.x * kWaves + wid;
+  const int env = blockIdx.x * kRollWaves + wid;
   if (env >= p.n_envs) return;  // wave-uniform; no block barriers below
   const int T = p.n_steps;
   float* sh = smem + wid * H;
   const bool fused = p.ret_out != nullptr && p.return_kind != XA_RETURNS_NONE;
-  float* hist = smem + kWaves * H + wid * 3 * T;  // [rew | val | done] per wave when fused
+  float* hist = smem + kRollWaves * H + wid * 3 * T;  // [rew | val | done] per wave when fused
   float* const hb = hbuf[wid];  // h2 of the chunk's steps, row j = step t0 + j
 
   XA_STAMP_DECL
@@ -574,13 +581,13 @@ __global__ __launch_bounds__(256) void mlp_forward_kernel(const float* __restric
 template <int OBS, int A>
 int launch_rollout(const XaRolloutArgs* p, hipStream_t s) {
   const bool fused = p->ret_out != nullptr && p->return_kind != XA_RETURNS_NONE;
-  const size_t lds = (size_t)kWaves * H * sizeof(float) +
-                     (fused ? (size_t)kWaves * 3 * p->n_steps * sizeof(float) : 0);
-  dim3 grid((p->n_envs + kWaves - 1) / kWaves);
+  const size_t lds = (size_t)kRollWaves * H * sizeof(float) +
+                     (fused ? (size_t)kRollWaves * 3 * p->n_steps * sizeof(float) : 0);
+  dim3 grid((p->n_envs + kRollWaves - 1) / kRollWaves);
   if (p->env_kind == XA_ENV_REPLAY) {
-    hipLaunchKernelGGL((mlp_rollout_kernel<OBS, A, true>), grid, dim3(256), lds, s, *p);
+    hipLaunchKernelGGL((mlp_rollout_kernel<OBS, A, true>), grid, dim3(64 * kRollWaves), lds, s, *p);
   } else if constexpr (OBS == 4 && A == 2) {
-    hipLaunchKernelGGL((mlp_rollout_kernel<OBS, A, false>), grid, dim3(256), lds, s, *p);
+    hipLaunchKernelGGL((mlp_rollout_kernel<OBS, A, false>), grid, dim3(64 * kRollWaves), lds, s, *p);
   }
   XA_CHECK_LAUNCH("xa_mlp_rollout");
   return 0;

@@ -249,28 +249,29 @@ XA_DEV void pt_tile(PtLds<OBS, A, TS>& L, PtAcc<OBS, A>& acc, const LossCfg& cfg
   // ---- 1: H1 ----
   float h1[NT][4];
   {
-    // w1[j] = W1[kx[j]][i]: the lane's own row first (kRegH1: the weights of rows lq ^ j
-    // from the neighbouring lane rows, no LDS), k order per lane (f32 order only)
+    // w1[k] = W1[k][i] (kRegH1: the weights of rows lq ^ j from the neighbouring lane rows
+    // by permlane swaps, put in k order by selects -- no LDS)
     float w1[OBS];
-    int kx[OBS];
     float b1;
     if constexpr (kRegH1<OBS, A>) {
       const float2 s16 = xa_swap16(w1v), s32 = xa_swap32(w1v);
-      const float p1 = (lq & 1) ? s16.x : s16.y;  // row lq ^ 1
-      const float2 s48 = xa_swap32(p1);
-      w1[0] = w1v;
-      w1[1] = p1;
-      w1[2] = (lq & 2) ? s32.x : s32.y;  // row lq ^ 2
-      w1[3] = (lq & 2) ? s48.x : s48.y;  // row lq ^ 3
+      float vj[4];                        // vj[j] = W1[lq ^ j][i]
+      vj[0] = w1v;
+      vj[1] = (lq & 1) ? s16.x : s16.y;  // row lq ^ 1
+      const float2 s48 = xa_swap32(vj[1]);
+      vj[2] = (lq & 2) ? s32.x : s32.y;  // row lq ^ 2
+      vj[3] = (lq & 2) ? s48.x : s48.y;  // row lq ^ 3
+      const bool o1 = lq & 1, o2 = lq & 2;
 #pragma unroll
-      for (int j = 0; j < OBS; ++j) kx[j] = lq ^ j;
+      for (int k = 0; k < OBS; ++k) {  // j = k ^ lq
+        const float e0 = ((k & 1) != 0) != o1 ? vj[1] : vj[0];
+        const float e1 = ((k & 1) != 0) != o1 ? vj[3] : vj[2];
+        w1[k] = ((k & 2) != 0) != o2 ? e1 : e0;
+      }
       b1 = xa_swap32(xa_swap16(b1v).x).x;  // row 0's b1[i] on every row
     } else {
 #pragma unroll
-      for (int k = 0; k < OBS; ++k) {
-        w1[k] = L.sW1[k * H + i];
-        kx[k] = k;
-      }
+      for (int k = 0; k < OBS; ++k) w1[k] = L.sW1[k * H + i];
       b1 = L.sb1[i];
     }
     stamp(47);  // (diagnostic) the weights are in registers
@@ -282,8 +283,8 @@ XA_DEV void pt_tile(PtLds<OBS, A, TS>& L, PtAcc<OBS, A>& acc, const LossCfg& cfg
         const int s = 16 * mt + 4 * lq + r;
         xa_f2 z = {0.0f, 0.0f};
 #pragma unroll
-        for (int j = 0; j < OBS; ++j)
-          z = xa_fma2(xa_f2{rec[s * R + kx[j]], rec[(s + 1) * R + kx[j]]}, xa_f2{w1[j], w1[j]}, z);
+        for (int k = 0; k < OBS; ++k)
+          z = xa_fma2(xa_f2{rec[s * R + k], rec[(s + 1) * R + k]}, xa_f2{w1[k], w1[k]}, z);
         const xa_f2 h = ftanh2(z + xa_f2{b1, b1});
         h1[mt][r] = h.x;
         h1[mt][r + 1] = h.y;
