@@ -63,7 +63,10 @@ constexpr int kXcds = 8;            // MI355X: 8 XCDs, each with its own L2
 // the XCD-local mode (below) in two parity slots -- launch gen uses slot gen & 1, which
 // launch gen - 1 (of either mode) zeroed at its end
 enum { kCntStats = 0, kAbort = 1, kWin = 2 /* [2] */, kElect = 4 /* [2][kXcds] */ };
-constexpr int kTwoLevelMinG = 64;   // >= 8 blocks per XCD: reduce inside each XCD's L2 first
+#ifndef XA_TWO_LEVEL_MIN_G  // (diagnostic A/B builds override it)
+#define XA_TWO_LEVEL_MIN_G 64
+#endif
+constexpr int kTwoLevelMinG = XA_TWO_LEVEL_MIN_G;  // >= 8 blocks per XCD: reduce inside each XCD's L2 first
 
 
 // ---- write-through hand-off primitives (global address space, agent scope) ----
@@ -1250,7 +1253,10 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
         off[NG + u] = gi < NSQ ? sq0 + (uint32_t)(16 * gi) : 0u;
         n += gi < NSQ;
       }
-      if (G <= 32) {
+#ifndef XA_C_POLL_SPLIT_G
+#define XA_C_POLL_SPLIT_G 32
+#endif
+      if (G <= XA_C_POLL_SPLIT_G) {
         // few blocks: one round trip for both
         bad = !poll_gran<NG + NQ>(g_r, off, n, tag, x, ws.ctl, epoch, p.status);
       } else {
