@@ -39,6 +39,16 @@ def test_ppo_data_parallel_equals_union(device, mode, world):
     _run('ppo_dp_worker.py', world, 'PPO DP OK', extra_env={'XA_PPO_UPDATE': mode})
 
 
+def test_ppo_data_parallel_xcd_local_equals_union(device):
+    """The placement a rank that owns its GPU uses (XA_PPO_PLACE_LOCAL: the update's G
+    workgroups elected on one XCD, hand-offs in that L2, cross-rank slices over the IPC
+    exchange blocks), here with 2 ranks on the one test GPU: the worker's minibatches make
+    G = 2, so both ranks' 8 x G launched workgroups are co-resident and neither election
+    can strand the other's. Must equal the union step like the spread placement."""
+    _run('ppo_dp_worker.py', 2, 'PPO DP OK',
+         extra_env={'XA_PPO_UPDATE': 'persistent', 'XA_PPO_PLACE': 'local'})
+
+
 def test_ppo_persistent_update_waits_for_late_ranks(device):
     """Launch skew between ranks (one process per GPU launches with its own host-side
     delay): rank 1 sleeps 0.5 s on the host before each of 3 train steps, so rank 0's
