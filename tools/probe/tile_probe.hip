@@ -14,6 +14,22 @@
 #include "../../xagents_amd/csrc/ppo_tile.hpp"
 
 using namespace xa_ac;
+
+// the per-pair Keras Adam of the probe's optimizer-step stand-in (the product update folds
+// b1 m / b2 v in ahead of its gradient poll; the arithmetic cost here is the same)
+__device__ inline void adam_pk(xa_f2 g, float& th0, float& th1, float& m0, float& m1, float& v0,
+                               float& v1, float alpha, float omb1, float omb2, float eps) {
+  const xa_f2 m = {m0, m1}, v = {v0, v1};
+  const xa_f2 mn = xa_fma2(g - m, xa_f2{omb1, omb1}, m);
+  const xa_f2 vn = xa_fma2(g * g - v, xa_f2{omb2, omb2}, v);
+  const xa_f2 step = mn * xa_f2{alpha, alpha};
+  th0 = th0 - step.x * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(vn.x) + eps);
+  th1 = th1 - step.y * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(vn.y) + eps);
+  m0 = mn.x;
+  m1 = mn.y;
+  v0 = vn.x;
+  v1 = vn.y;
+}
 constexpr int OBS = 4, A = 2;
 
 XA_DEV unsigned long long rnow() {
