@@ -488,7 +488,10 @@ XA_DEV int elect_local(unsigned* ctl, int G, unsigned par, int xcc, unsigned epo
 // TS = samples per tile (32; 16 when the minibatch has at most 16 tiles of 32: twice the
 // blocks, half the element-wise work per block and step); PRE = every tile input of the
 // launch fits the block's LDS records (gathered once in phase 0); loc = XCD-local mode
-template <int OBS, int A, int TS, bool DP, bool PRE>
+// CB1: every block's phase-B slice takes the column form (the host checked col_b_everywhere);
+// the other forms are then compiled out, which lowers the register allocation of the whole
+// kernel body (16-env update 167 -> 161 us, profiles/r03ah_variants.txt)
+template <int OBS, int A, int TS, bool DP, bool PRE, bool CB1 = false>
 __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws ws, int K,
                                                           int n_mb, int loc) {
   constexpr int RPT = Dims<OBS, A>::RPT;
@@ -1059,7 +1062,8 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
         emit(c, g0, g1);
       }
     }
-    const bool flat_b = !col_b && !two_level && G * nc <= 256 * kBF;
+    constexpr bool other_b = !CB1;  // (CB1: the host guarantees col_b wherever nc > 0)
+    const bool flat_b = other_b && !col_b && !two_level && G * nc <= 256 * kBF;
     if (nc > 0 && flat_b) {
       const bool bad = gather_rows(rows_r, G, nc, [&](int r) {
         return (uint32_t)(((size_t)r * NP2 + c0) * 16);
@@ -1107,7 +1111,7 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
         emit(c, g0, g1);
       }
     }
-    if (nc > 0 && !flat_b && !col_b) {
+    if (other_b && nc > 0 && !flat_b && !col_b) {
       const int SRC = two_level ? kXcds : G;  // sources summed per column
       const int ncol = min(nc, 256), RG = min(SRC, 256 / ncol);
       const int rg = tid / ncol, cq = tid - rg * ncol;
@@ -1394,8 +1398,12 @@ int occupancy_min() {
       (void*)ppo_update_kernel<OBS, A, S, false, false>, (void*)ppo_update_kernel<OBS, A, 16, false, false>,
       (void*)ppo_update_kernel<OBS, A, S, true, false>, (void*)ppo_update_kernel<OBS, A, 16, true, false>,
       (void*)ppo_update_kernel<OBS, A, S, false, true>, (void*)ppo_update_kernel<OBS, A, 16, false, true>,
-      (void*)ppo_update_kernel<OBS, A, S, true, true>, (void*)ppo_update_kernel<OBS, A, 16, true, true>};
-  // (template flags: DP, PRE)
+      (void*)ppo_update_kernel<OBS, A, S, true, true>, (void*)ppo_update_kernel<OBS, A, 16, true, true>,
+      (void*)ppo_update_kernel<OBS, A, 16, false, false, true>,
+      (void*)ppo_update_kernel<OBS, A, 16, true, false, true>,
+      (void*)ppo_update_kernel<OBS, A, 16, false, true, true>,
+      (void*)ppo_update_kernel<OBS, A, 16, true, true, true>};
+  // (template flags: DP, PRE, CB1)
   int occ = 1 << 30;
   for (void* k : kernels) {
     int o = 0;
@@ -1444,6 +1452,19 @@ bool use_local(const XaPpoUpdateArgs* a, int G, int cap) {
   return G < kTwoLevelMinG && (long)G * kXcds <= (long)cap;
 }
 
+// every block's phase-B slice (pair columns [b CB, (b + 1) CB) of NP2) takes the kernel's
+// column form -- the kernel's own col_b test, per block (single-level reduce only)
+bool col_b_everywhere(int G, int P) {
+  const int NP2 = padded(P) / 2, CB = (NP2 + G - 1) / G;
+  for (int b = 0; b < G; ++b) {
+    const int c0 = min(NP2, b * CB), nc = min(NP2, c0 + CB) - c0;
+    if (nc <= 0) continue;
+    const int parts = nc <= 128 ? min(4, 256 / nc) : 1;
+    if (!(parts > 1 && (G + parts - 1) / parts <= kBF)) return false;
+  }
+  return true;
+}
+
 template <int OBS, int A, int TS>
 void launch_ts(const XaPpoUpdateArgs* a, int G, bool dp, bool loc, const Ws& ws, int K, int n_mb,
                hipStream_t s) {
@@ -1453,6 +1474,19 @@ void launch_ts(const XaPpoUpdateArgs* a, int G, bool dp, bool loc, const Ws& ws,
   const int TPB = (n_tiles_max + G - 1) / G;
   const bool pre = K * TPB * TS <= pre_max<OBS>();
   const int l = loc ? 1 : 0;
+  if constexpr (TS == 16) {  // 16-sample tiles: small grids, one-level reduce
+    if (col_b_everywhere(G, offs(OBS, A).P)) {
+      if (dp && pre)
+        hipLaunchKernelGGL((ppo_update_kernel<OBS, A, TS, true, true, true>), grid, dim3(256), 0, s, *a, ws, K, n_mb, l);
+      else if (dp)
+        hipLaunchKernelGGL((ppo_update_kernel<OBS, A, TS, true, false, true>), grid, dim3(256), 0, s, *a, ws, K, n_mb, l);
+      else if (pre)
+        hipLaunchKernelGGL((ppo_update_kernel<OBS, A, TS, false, true, true>), grid, dim3(256), 0, s, *a, ws, K, n_mb, l);
+      else
+        hipLaunchKernelGGL((ppo_update_kernel<OBS, A, TS, false, false, true>), grid, dim3(256), 0, s, *a, ws, K, n_mb, l);
+      return;
+    }
+  }
   if (dp && pre)
     hipLaunchKernelGGL((ppo_update_kernel<OBS, A, TS, true, true>), grid, dim3(256), 0, s, *a, ws, K, n_mb, l);
   else if (dp)
