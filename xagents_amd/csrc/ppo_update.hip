@@ -488,10 +488,12 @@ XA_DEV int elect_local(unsigned* ctl, int G, unsigned par, int xcc, unsigned epo
 // TS = samples per tile (32; 16 when the minibatch has at most 16 tiles of 32: twice the
 // blocks, half the element-wise work per block and step); PRE = every tile input of the
 // launch fits the block's LDS records (gathered once in phase 0); loc = XCD-local mode
-// CB1: every block's phase-B slice takes the column form (the host checked col_b_everywhere);
-// the other forms are then compiled out, which lowers the register allocation of the whole
-// kernel body (16-env update 167 -> 161 us, profiles/r03ah_variants.txt)
-template <int OBS, int A, int TS, bool DP, bool PRE, bool CB1 = false>
+// BF = the phase-B reduce forms compiled in: 0 every form (chosen per block at run time);
+// 1 the column form only (the host checked col_b_everywhere); 2 the two-level reduce only
+// (spread grids of >= kTwoLevelMinG blocks with 32-sample tiles). Compiling the unused forms
+// out lowers the register allocation of the whole kernel body (16-env update 167 -> 161 us,
+// profiles/r03ah_variants.txt)
+template <int OBS, int A, int TS, bool DP, bool PRE, int BF = 0>
 __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws ws, int K,
                                                           int n_mb, int loc) {
   constexpr int RPT = Dims<OBS, A>::RPT;
@@ -523,7 +525,7 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
 
   // ---- census: which XCD this block runs on (a granule, read after the phase-0 hop) ----
   // 16-sample tiles run only on small grids (<= 32 blocks): one level, known at compile time
-  const bool two_level = !loc && TS == S && G >= kTwoLevelMinG;
+  const bool two_level = BF == 2 || (BF == 0 && !loc && TS == S && G >= kTwoLevelMinG);
   const __amdgpu_buffer_rsrc_t cen_r = rsrc(ws.cen_g, (uint32_t)(G * 16));
   if (two_level && tid == 0) st_gran2(cen_r, (uint32_t)(16 * b), __uint_as_float((unsigned)xcc),
                                       __uint_as_float((unsigned)xcc), epoch, true);
@@ -1062,8 +1064,9 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
         emit(c, g0, g1);
       }
     }
-    constexpr bool other_b = !CB1;  // (CB1: the host guarantees col_b wherever nc > 0)
-    const bool flat_b = other_b && !col_b && !two_level && G * nc <= 256 * kBF;
+    // (BF = 1: the host guarantees col_b wherever nc > 0; BF = 2: two_level everywhere)
+    constexpr bool flat_ok = BF == 0, gen_ok = BF != 1;
+    const bool flat_b = flat_ok && !col_b && !two_level && G * nc <= 256 * kBF;
     if (nc > 0 && flat_b) {
       const bool bad = gather_rows(rows_r, G, nc, [&](int r) {
         return (uint32_t)(((size_t)r * NP2 + c0) * 16);
@@ -1111,7 +1114,7 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
         emit(c, g0, g1);
       }
     }
-    if (other_b && nc > 0 && !flat_b && !col_b) {
+    if (gen_ok && nc > 0 && !flat_b && !col_b) {
       const int SRC = two_level ? kXcds : G;  // sources summed per column
       const int ncol = min(nc, 256), RG = min(SRC, 256 / ncol);
       const int rg = tid / ncol, cq = tid - rg * ncol;
@@ -1399,11 +1402,15 @@ int occupancy_min() {
       (void*)ppo_update_kernel<OBS, A, S, true, false>, (void*)ppo_update_kernel<OBS, A, 16, true, false>,
       (void*)ppo_update_kernel<OBS, A, S, false, true>, (void*)ppo_update_kernel<OBS, A, 16, false, true>,
       (void*)ppo_update_kernel<OBS, A, S, true, true>, (void*)ppo_update_kernel<OBS, A, 16, true, true>,
-      (void*)ppo_update_kernel<OBS, A, 16, false, false, true>,
-      (void*)ppo_update_kernel<OBS, A, 16, true, false, true>,
-      (void*)ppo_update_kernel<OBS, A, 16, false, true, true>,
-      (void*)ppo_update_kernel<OBS, A, 16, true, true, true>};
-  // (template flags: DP, PRE, CB1)
+      (void*)ppo_update_kernel<OBS, A, 16, false, false, 1>,
+      (void*)ppo_update_kernel<OBS, A, 16, true, false, 1>,
+      (void*)ppo_update_kernel<OBS, A, 16, false, true, 1>,
+      (void*)ppo_update_kernel<OBS, A, 16, true, true, 1>,
+      (void*)ppo_update_kernel<OBS, A, S, false, false, 2>,
+      (void*)ppo_update_kernel<OBS, A, S, true, false, 2>,
+      (void*)ppo_update_kernel<OBS, A, S, false, true, 2>,
+      (void*)ppo_update_kernel<OBS, A, S, true, true, 2>};
+  // (template flags: DP, PRE, BF)
   int occ = 1 << 30;
   for (void* k : kernels) {
     int o = 0;
@@ -1477,13 +1484,25 @@ void launch_ts(const XaPpoUpdateArgs* a, int G, bool dp, bool loc, const Ws& ws,
   if constexpr (TS == 16) {  // 16-sample tiles: small grids, one-level reduce
     if (col_b_everywhere(G, offs(OBS, A).P)) {
       if (dp && pre)
-        hipLaunchKernelGGL((ppo_update_kernel<OBS, A, TS, true, true, true>), grid, dim3(256), 0, s, *a, ws, K, n_mb, l);
+        hipLaunchKernelGGL((ppo_update_kernel<OBS, A, TS, true, true, 1>), grid, dim3(256), 0, s, *a, ws, K, n_mb, l);
       else if (dp)
-        hipLaunchKernelGGL((ppo_update_kernel<OBS, A, TS, true, false, true>), grid, dim3(256), 0, s, *a, ws, K, n_mb, l);
+        hipLaunchKernelGGL((ppo_update_kernel<OBS, A, TS, true, false, 1>), grid, dim3(256), 0, s, *a, ws, K, n_mb, l);
       else if (pre)
-        hipLaunchKernelGGL((ppo_update_kernel<OBS, A, TS, false, true, true>), grid, dim3(256), 0, s, *a, ws, K, n_mb, l);
+        hipLaunchKernelGGL((ppo_update_kernel<OBS, A, TS, false, true, 1>), grid, dim3(256), 0, s, *a, ws, K, n_mb, l);
       else
-        hipLaunchKernelGGL((ppo_update_kernel<OBS, A, TS, false, false, true>), grid, dim3(256), 0, s, *a, ws, K, n_mb, l);
+        hipLaunchKernelGGL((ppo_update_kernel<OBS, A, TS, false, false, 1>), grid, dim3(256), 0, s, *a, ws, K, n_mb, l);
+      return;
+    }
+  } else {  // 32-sample tiles on a spread grid of >= kTwoLevelMinG blocks: two-level only
+    if (!loc && G >= kTwoLevelMinG) {
+      if (dp && pre)
+        hipLaunchKernelGGL((ppo_update_kernel<OBS, A, TS, true, true, 2>), grid, dim3(256), 0, s, *a, ws, K, n_mb, l);
+      else if (dp)
+        hipLaunchKernelGGL((ppo_update_kernel<OBS, A, TS, true, false, 2>), grid, dim3(256), 0, s, *a, ws, K, n_mb, l);
+      else if (pre)
+        hipLaunchKernelGGL((ppo_update_kernel<OBS, A, TS, false, true, 2>), grid, dim3(256), 0, s, *a, ws, K, n_mb, l);
+      else
+        hipLaunchKernelGGL((ppo_update_kernel<OBS, A, TS, false, false, 2>), grid, dim3(256), 0, s, *a, ws, K, n_mb, l);
       return;
     }
   }
