@@ -30,6 +30,9 @@ F32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: f32-input MFMA dense peak (
 # rollout kernel algorithmic bytes per env-step (replay env): reads obs 16 + state 16 +
 # reward 4 + done 4; writes obs 16 + action/logp/value/entropy/reward/done/epret/return 32
 ROLLOUT_BYTES_PER_ENV_STEP = 40 + 48
+# persistent update: the rollout buffers one epoch reads per sample (obs 16 B + action,
+# old log-prob, old value, return 4 B each)
+UPDATE_BYTES_PER_SAMPLE_EPOCH = 16 + 16
 
 
 def mlp_fwd_flops(obs_dim=4, n_actions=2, hidden=64):
@@ -570,16 +573,32 @@ def bench_ppo(args, world, rank, device, n_envs):
         upd_ms = float(np.mean(ktimes['ppo_update']))
         flops = flops_sample * B * agent.ppo_epochs  # every sample once per epoch
         tf = flops / (upd_ms * 1e-3) / 1e12
+        # SURVEY 8(d) HBM basis (north_star: "fraction of HBM roofline"): the rollout
+        # buffers read once per epoch (obs 16 + action / log-prob / value / return 16 B per
+        # sample) + the optimizer's 7 words per parameter per step (theta, m, v read and
+        # written, the gradient read)
+        P = agent.model.n_params
+        alg_bytes = UPDATE_BYTES_PER_SAMPLE_EPOCH * B * agent.ppo_epochs + 7 * 4 * P * K
+        gbs = alg_bytes / (upd_ms * 1e-3) / 1e9
+        traffic = load_traffic(f'ppo_update_n{n_envs}')
         out['update_roofline'] = {
-            'kernel': 'xa_ppo_update (ppo_update_kernel<4,2>, persistent)', 'bound': 'mfma',
-            'achieved': round(tf, 3), 'peak': F32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
-            'frac': round(tf / F32_MFMA_PEAK_TFLOPS, 5),
-            'traffic': load_traffic(f'ppo_update_n{n_envs}'), 'launch_ms': round(upd_ms, 5),
-            'note': f'3F = {flops_sample} FLOP/sample (fwd + bwd) x {B} samples x '
-                    f'{agent.ppo_epochs} epochs = {K} optimizer steps of {mb} in ONE launch '
-                    f'on {agent.update_blocks} workgroups; latency-bound (2 in-launch '
-                    f'exchanges per optimizer step); launch_ms = HIP event pair on the launch '
-                    f'stream around each launch of 3 eager train steps'}
+            'kernel': 'xa_ppo_update (ppo_update_kernel<4,2>, persistent)', 'bound': 'hbm',
+            'achieved': round(gbs, 3), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+            'frac': round(gbs / HBM_PEAK_GBS, 6), 'traffic': traffic,
+            'algorithmic_bytes': alg_bytes,
+            'traffic_ratio': round(traffic / alg_bytes, 3) if traffic else None,
+            'launch_ms': round(upd_ms, 5),
+            'mfma': {'achieved': round(tf, 3), 'peak': F32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
+                     'frac': round(tf / F32_MFMA_PEAK_TFLOPS, 5),
+                     'flops': flops},
+            'note': f'HBM basis: {UPDATE_BYTES_PER_SAMPLE_EPOCH} B/sample x {B} samples x '
+                    f'{agent.ppo_epochs} epochs + 7 x 4 B x P = {P} x {K} optimizer steps; '
+                    f'mfma: 3F = {flops_sample} FLOP/sample (fwd + bwd) per epoch; {K} '
+                    f'optimizer steps of {mb} in ONE launch on {agent.update_blocks} '
+                    f'workgroups; latency-bound (2 in-launch exchanges per optimizer step); '
+                    f'launch_ms = HIP event pair on the launch stream around each launch of '
+                    f'3 eager train steps; traffic = PMC FETCH_SIZE x 2 + WRITE_SIZE bytes per '
+                    f'launch (profiles/traffic.json)'}
     else:
         grad_ms = float(np.mean(ktimes['ac_grad']))
         tf = flops_sample * mb / (grad_ms * 1e-3) / 1e12

@@ -708,6 +708,17 @@ typedef struct XaHeadGradArgs {
 
 int xa_ac_head_grad(const XaHeadGradArgs* args, void* stream);
 
+/* Advantage statistics of every minibatch of a PPO train step in one launch (the
+ * per-minibatch normalisation of run_ppo_epochs, ppo/agent.py:157-191, with the
+ * minibatches of get_mini_batches 139-155): idx [epochs * batch] holds each epoch's
+ * shuffled flat sample indices (epoch e at e * batch, minibatch m at m * mb_size, the last
+ * one ragged); out[(e * n_mb + m) * 3 + {0, 1, 2}] = f64 [sum, sum^2, count] of
+ * adv = returns[i] - values[i], n_mb = ceil(batch / mb_size). The sums are linear:
+ * all-reduce out across data-parallel ranks once per train step, then xa_ac_head_grad
+ * stats_mode 2 reads each minibatch's triple. */
+int xa_minibatch_adv_sums(const float* returns, const float* values, const int64_t* idx,
+                          int batch, int mb_size, int epochs, double* out, void* stream);
+
 /* MultivariateNormalDiag(loc = mu) with unit scale, the reference's distribution for Box
  * action spaces (A2C.get_distribution, a2c/agent.py:54-63): per row i of mu [n, d],
  * actions_out[i] = mu[i] + N(0, I) (noise [n, d] if given, else Philox4x32-10 Box-Muller

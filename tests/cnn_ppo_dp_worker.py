@@ -1,0 +1,106 @@
+"""Worker for tests/test_gpu_dp.py::test_cnn_ppo_data_parallel_equals_union: the C4
+data-parallel path (PPO with the CNN actor-critic on the layer executor,
+xagents_amd/onpolicy_executor.py) with W processes on ONE HIP device over a gloo group.
+
+Rank r runs PPO on its own Breakout-shaped shard of N envs (synthetic uint8 frames,
+record seed 55 + r): rollout, the advantage statistics of every minibatch all-reduced
+once per train step, and per minibatch the 77 MB gradient all-reduced in buckets (the
+dense layers' slice issued while the conv backward still runs). Rank 0 also runs a
+single-process agent on the union of the shards (data_parallel=False) fed the same
+rollout uniforms and the rank-major union of the ranks' minibatch permutations. The
+data-parallel train step must equal the union step (xagents/ppo/agent.py:157-191):
+actions bit for bit, log-probs / values / returns to f32 rounding (the union's GEMMs run
+at twice the batch, which may pick another split-K count and so another summation
+order), parameters within 1e-4 of the update's norm, identical on every rank, and 16
+optimizer steps taken. Prints 'CNN DP OK <rank>'."""
+import os
+import sys
+from pathlib import Path
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+N, T, E, M, T_REC = 8, 16, 4, 4, 64
+
+
+def make(record, n, data_parallel=None):
+    from xagents_amd import PPO
+    from xagents_amd.envs import Discrete, TransitionReplayVecEnv
+    from xagents_amd.utils.common import create_model
+    envs = TransitionReplayVecEnv('BreakoutNoFrameskip-v4', n, (84, 84, 1), Discrete(4),
+                                  np.uint8, device='cuda', record=record)
+    model = create_model(envs, 'ppo', 'model', seed=21, device='cuda')
+    return PPO(envs, model, n_steps=T, seed=21, quiet=True, ppo_epochs=E, mini_batches=M,
+               data_parallel=data_parallel)
+
+
+def main():
+    dist.init_process_group('gloo')
+    rank, world = dist.get_rank(), dist.get_world_size()
+    torch.cuda.set_device(0)
+    from xagents_amd.envs import record_transitions
+    records = [record_transitions(N, T_REC, (84, 84, 1), np.uint8, seed=55 + r)
+               for r in range(world)]
+    uniforms = [np.random.default_rng(100 + r).random((N, T)).astype(np.float32)
+                for r in range(world)]
+    B, mb = N * T, N * T // M
+    perms = [np.stack([np.random.default_rng(200 + 10 * r + e).permutation(B)
+                       for e in range(E)]).astype(np.int32) for r in range(world)]
+    dp = make(records[rank], N)
+    assert dp.executor_path and dp.distributed and dp.world_size == world
+    if os.environ.get('XA_TEST_BUCKET_MB'):
+        dp.bucket_floats = int(float(os.environ['XA_TEST_BUCKET_MB']) * (1 << 20)) // 4
+    theta0 = dp.model.theta.cpu().numpy().astype(np.float64)
+    dp.set_rollout_uniforms(torch.from_numpy(uniforms[rank]).cuda())
+    dp.set_minibatch_permutation(torch.from_numpy(perms[rank]).cuda())
+    it0 = int(dp.model.optimizer.iterations.item())
+    dp.train_step()
+    torch.cuda.synchronize()
+    got = {k: getattr(dp, k).cpu() for k in ('b_act', 'b_logp', 'b_val', 'b_ret')}
+    got['theta'] = dp.model.theta.cpu()
+    gathered = {}
+    for k, t in got.items():
+        parts = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(parts, t)
+        gathered[k] = parts
+    for p in gathered['theta'][1:]:
+        assert torch.equal(p, gathered['theta'][0]), 'ranks disagree on theta'
+    assert int(dp.model.optimizer.iterations.item()) - it0 == E * M
+    if rank == 0:
+        union_rec = tuple(np.concatenate([r[i] for r in records]) for i in range(5))
+        un = make(union_rec, world * N, data_parallel=False)
+        assert un.executor_path and not un.distributed
+        np.testing.assert_array_equal(un.model.theta.cpu().numpy(), theta0)
+        un.set_rollout_uniforms(torch.from_numpy(np.concatenate(uniforms)).cuda())
+        # union minibatch m = the ranks' minibatch m slices, rank-major, global indices
+        up = np.stack([np.concatenate([np.concatenate(
+            [r * B + perms[r][e][m * mb:(m + 1) * mb] for r in range(world)])
+            for m in range(M)]) for e in range(E)]).astype(np.int32)
+        un.set_minibatch_permutation(torch.from_numpy(up).cuda())
+        un.train_step()
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(un.b_act.cpu().numpy(), torch.cat(gathered['b_act']).numpy(),
+                                      err_msg='actions')
+        exact = []
+        for k in ('b_logp', 'b_val', 'b_ret'):
+            u, d = getattr(un, k).cpu().numpy(), torch.cat(gathered[k]).numpy()
+            exact.append(bool(np.array_equal(u, d)))
+            np.testing.assert_allclose(d, u, rtol=1e-5, atol=1e-6, err_msg=k)
+        tu = un.model.theta.cpu().numpy().astype(np.float64)
+        td = gathered['theta'][0].numpy().astype(np.float64)
+        rel = np.linalg.norm(td - tu) / np.linalg.norm(tu - theta0)
+        print(f'CNN DP W={world}: rollout buffers bit-equal {exact}, theta rel {rel:.2e}',
+              flush=True)
+        assert rel < 1e-4, f'data-parallel update deviates from the union update: {rel:.2e}'
+        assert int(un.model.optimizer.iterations.item()) == E * M
+    dist.barrier()
+    print(f'CNN DP OK {rank}', flush=True)
+    dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

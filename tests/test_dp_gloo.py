@@ -105,3 +105,53 @@ def test_dp_world2_gradient_equals_union_gradient():
                    for ls, ac in args)
     # parameters were broadcast from rank 0
     np.testing.assert_array_equal(res[0][5], res[1][5])
+
+
+def _plateau_worker(rank, world, port, q):
+    """Two plateau reductions inside one DP sync window, then _dp_sync: every rank ends
+    with lr0 * factor^2 (the reference compounds reductions, xagents/base.py:277-284) and
+    rank 0's stop decision."""
+    import time
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from xagents_amd import PPO
+        from xagents_amd.envs import ReplayVecEnv
+        from xagents_amd.utils.common import create_model
+        envs = ReplayVecEnv('CartPole-v1', 4, t_rec=64, seed=55 + rank, device='cpu')
+        model = create_model(envs, 'ppo', 'model', seed=55, device='cpu',
+                             optimizer_kwargs=dict(learning_rate=1e-3))
+        agent = PPO(envs, model, n_steps=8, seed=55, quiet=True, use_graph=False,
+                    plateau_reduce_factor=0.5, plateau_reduce_patience=1,
+                    divergence_monitoring_steps=1)
+        agent.steps, agent.last_reset_time = 100, time.perf_counter()
+        agent.total_rewards.extend([1.0, 2.0])
+        agent.best_reward = 10.0
+        agent.mean_reward = 1.5
+        for _ in range(2):  # two plateaus before the sync
+            agent.update_metrics()
+            agent.mean_reward = 1.5
+        lr_before = model.optimizer.learning_rate
+        stop = agent._dp_sync(stop_local=rank == 0)
+        q.put((rank, lr_before, model.optimizer.learning_rate, stop, agent.early_stop_count))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_dp_plateau_reductions_compound_within_a_sync_window():
+    world, port = 2, _free_port()
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_plateau_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, lr_before, lr_after, stop, early in res:
+        assert lr_before == pytest.approx(1e-3)  # applied only at the sync
+        assert lr_after == pytest.approx(1e-3 * 0.25), lr_after
+        assert stop is True  # rank 0's decision, on every rank
+        assert early == 2

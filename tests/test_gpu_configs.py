@@ -103,8 +103,17 @@ def test_c3_dqn_32_envs_rb1_1m_batch_64(device):
 
 def test_c4_ppo_cnn_128_env_shard(device):
     """C4, one rank's shard: PPO with the CNN actor-critic on 128 Breakout-shaped envs x 128
-    steps (batch 16,384), 4 epochs x 4 minibatches of 4,096."""
-    import nets_f64 as O
+    steps (batch 16,384), 4 epochs x 4 minibatches of 4,096. ALL 16 optimizer steps of one
+    train_step (xagents/ppo/agent.py:157-191) are teacher-forced: each step's gradient,
+    taken at the device's own parameters theta_k on the minibatch the step drew, against
+    the float64 restatement (oracle/nets_torch64.py on the test GPU, pinned to
+    oracle/nets_f64.py by tests/test_oracle.py) at 1e-4 relative; then the applied clip +
+    Keras Adam step against its float64 restatement from the device's own gradient and
+    moments (moments 1e-5; the step theta_k+1 - theta_k 5e-5, since storing theta_k+1 in
+    f32 rounds it by half an ulp of |theta|). The 1e-4 gradient bound (above the 1e-5 of
+    the MLP path) covers ReLU gates that flip between the f32 and f64 forwards at
+    pre-activations ~0 and the cancelling f32 sums of the conv weight gradients."""
+    import nets_torch64 as OT
     import oracle as OR
     from test_gpu_cnn_onpolicy import _heads_grad_f64
     from xagents_amd import PPO
@@ -115,50 +124,68 @@ def test_c4_ppo_cnn_128_env_shard(device):
     model = create_model(envs, 'ppo', 'model', seed=55, device=device)
     agent = PPO(envs, model, n_steps=T, seed=55, quiet=True)
     assert agent.executor_path and agent.mb == 4096 and agent.n_mb == 4
-    agent._executor_rollout()
-    obs = agent.obs_buf[:T].cpu().numpy()
+    B, mb, E = n * T, agent.mb, agent.ppo_epochs
     opt = model.optimizer
-    # three chained minibatch steps of the update at full size, each teacher-forced at the
-    # device's own parameters: the gradient at theta_k vs float64 (1e-4), then the applied
-    # clip + Keras Adam step vs its float64 restatement from the device's own gradient and
-    # moments (the f32 optimizer arithmetic alone: moments 1e-5; the step theta_k+1 - theta_k
-    # 5e-5, since storing theta_k+1 in f32 rounds it by half an ulp of |theta|)
+    trace = []
+    step_fn = agent._minibatch_step
+
+    def traced(nn, k=None):
+        before = (model.theta.clone(), opt.m.clone(), opt.v.clone())
+        step_fn(nn, k)
+        trace.append((k, nn) + before + (agent.grad.clone(),))
+
+    agent._minibatch_step = traced
     np.random.seed(9)
     it0 = int(opt.iterations.item())
-    for step in range(3):
-        th, m, v_ = _np(model.theta), _np(opt.m), _np(opt.v)
-        idx = np.random.permutation(n * T)[:agent.mb]
-        k = agent._upload_slots(idx)
-        agent._gather_minibatch(k)
-        agent._minibatch_step(k)
-        torch.cuda.synchronize()
-        x = obs[idx % T, idx // T]  # flat env-major index i = env * T + t
-        act = agent.b_act.cpu().numpy().reshape(-1)[idx]
-        oldlp, oldv, ret = (_np(t).reshape(-1)[idx] for t in (agent.b_logp, agent.b_val, agent.b_ret))
-        x64, outs = O.forward(model.layers, th, x, model.input_shape)
-        logits, v = outs[model.outputs[0]], outs[model.outputs[1]][:, 0]
-        dz, dv = _heads_grad_f64(logits, v, act, oldlp, oldv, ret, 'ppo')
-        g = O.backward(model.layers, th, x64, outs, {model.outputs[0]: dz, model.outputs[1]: dv[:, None]})
-        gd = _np(agent.grad)
-        assert _rel(gd, g) < 1e-4, f'step {step}: gradient {_rel(gd, g):.2e}'
-        gc = OR.clip_by_global_norm_f64(gd, agent.grad_norm)[0]
-        # the hyper-parameters as the f32 values TF's ApplyAdam computes with (1 - beta_2 of
-        # the f32 0.999 is 0.99998713e-3, 1.3e-5 off the decimal 1e-3)
-        f32 = lambda x: float(np.float32(x))  # noqa: E731
-        th1, m1, v1 = OR.keras_adam_f64(th, m, v_, gc, it0 + step + 1, f32(opt.learning_rate),
-                                        f32(opt.beta_1), f32(opt.beta_2), f32(opt.epsilon))
-        assert int(opt.iterations.item()) == it0 + step + 1
-        em, ev = _rel(_np(opt.m), m1), _rel(_np(opt.v), v1)
-        assert em < 1e-5 and ev < 1e-5, f'step {step}: moments m {em:.2e} v {ev:.2e}'
-        es = _rel(_np(model.theta) - th, th1 - th)
-        assert es < 5e-5, f'step {step}: Adam step {es:.2e}'
-    # full train steps
-    it0 = int(opt.iterations.item())
-    for _ in range(2):
-        agent.fused_train_step()
+    agent.fused_train_step()
     agent._drain_episode_stats()
     torch.cuda.synchronize()
-    assert int(model.optimizer.iterations.item()) - it0 == 2 * 16
+    del agent._minibatch_step
+    assert [t[0] for t in trace] == list(range(E * 4)) and all(t[1] == mb for t in trace)
+    assert int(opt.iterations.item()) - it0 == E * 4
+    assert agent.steps == n * T
+    slots = agent._slots_flat[:E * B].clone()
+    act_all = agent.b_act.reshape(-1)
+    logp_all, val_all, ret_all = (x.reshape(-1).double() for x in
+                                  (agent.b_logp, agent.b_val, agent.b_ret))
+    final = (model.theta.clone(), opt.m.clone(), opt.v.clone())
+    f32 = lambda x: float(np.float32(x))  # noqa: E731
+    o_logits, o_value = model.outputs
+    for k, nn, th, m, v_, gd in trace:
+        e, mi = divmod(k, 4)
+        idx = slots[e * B + mi * mb:e * B + mi * mb + nn]
+        x = agent.obs_buf[idx % T, idx // T]  # flat env-major index i = env * T + t
+        thg = th.double().requires_grad_(True)
+        _, outs = OT.forward(model.layers, thg, x, model.input_shape)
+        logits, val = outs[o_logits], outs[o_value][:, 0]
+        dz, dv = _heads_grad_f64(logits.detach().cpu().numpy(), val.detach().cpu().numpy(),
+                                 act_all[idx].cpu().numpy(), logp_all[idx].cpu().numpy(),
+                                 val_all[idx].cpu().numpy(), ret_all[idx].cpu().numpy(), 'ppo')
+        g, = torch.autograd.grad([logits, outs[o_value]], [thg], grad_outputs=[
+            torch.from_numpy(dz).to(device), torch.from_numpy(dv[:, None]).to(device)])
+        del outs, logits, val, thg
+        g = g.cpu().numpy()
+        gn = _np(gd)
+        assert _rel(gn, g) < 1e-4, f'step {k}: gradient {_rel(gn, g):.2e}'
+        nxt = trace[k + 1][2:5] if k + 1 < len(trace) else final
+        gc = OR.clip_by_global_norm_f64(gn, agent.grad_norm)[0]
+        # the hyper-parameters as the f32 values TF's ApplyAdam computes with (1 - beta_2 of
+        # the f32 0.999 is 0.99998713e-3, 1.3e-5 off the decimal 1e-3)
+        th0n = _np(th)
+        th1, m1, v1 = OR.keras_adam_f64(th0n, _np(m), _np(v_), gc, it0 + k + 1,
+                                        f32(opt.learning_rate), f32(opt.beta_1),
+                                        f32(opt.beta_2), f32(opt.epsilon))
+        em, ev = _rel(_np(nxt[1]), m1), _rel(_np(nxt[2]), v1)
+        assert em < 1e-5 and ev < 1e-5, f'step {k}: moments m {em:.2e} v {ev:.2e}'
+        es = _rel(_np(nxt[0]) - th0n, th1 - th0n)
+        assert es < 5e-5, f'step {k}: Adam step {es:.2e}'
+    del trace
+    # more full train steps
+    it0 = int(opt.iterations.item())
+    agent.fused_train_step()
+    agent._drain_episode_stats()
+    torch.cuda.synchronize()
+    assert int(model.optimizer.iterations.item()) - it0 == 16
     assert agent.steps == 2 * n * T
     assert np.isfinite(_np(model.theta)).all()
 

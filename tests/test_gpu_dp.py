@@ -39,6 +39,18 @@ def test_ppo_data_parallel_equals_union(device, mode, world):
     _run('ppo_dp_worker.py', world, 'PPO DP OK', extra_env={'XA_PPO_UPDATE': mode})
 
 
+@pytest.mark.parametrize('world,bucket_mb', [(2, None), (4, None), (2, '0')])
+def test_cnn_ppo_data_parallel_equals_union(device, world, bucket_mb):
+    """BASELINE configs[3]'s path: PPO with the CNN actor-critic on the layer executor,
+    data parallel over W ranks (advantage statistics all-reduced once per train step, the
+    77 MB gradient all-reduced per minibatch in buckets overlapping the conv backward),
+    equal to one process on the union of the shards (tests/cnn_ppo_dp_worker.py;
+    xagents/ppo/agent.py:157-191). bucket_mb '0': one bucket per layer (every layer's
+    slice goes out as soon as it is final)."""
+    _run('cnn_ppo_dp_worker.py', world, 'CNN DP OK',
+         extra_env={'XA_TEST_BUCKET_MB': bucket_mb} if bucket_mb else None, timeout=200)
+
+
 def test_ppo_data_parallel_xcd_local_equals_union(device):
     """The placement a rank that owns its GPU uses (XA_PPO_PLACE_LOCAL: the update's G
     workgroups elected on one XCD, hand-offs in that L2, cross-rank slices over the IPC

@@ -93,6 +93,16 @@ for step in "$@"; do
         --cpu-baseline-seconds 0 > $R/gpurun_out/${T}_profc3_bench.json 2>&1) || exit $?
       python tools/kernel_shapes.py gpurun_out/${T}_profc3/run_kernel_trace.csv 25 \
         > gpurun_out/${T}_profc3_shapes.txt 2>&1 ;;
+    profc5)
+      # C5 (TD3): the whole bench line, then one gradient step's launches on their own
+      (cd /tmp && timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/${T}_profc5 \
+        -o run --output-format csv -- python $R/bench.py --config c5 --steps 30 --warmup 5 \
+        --cpu-baseline-seconds 0 > $R/gpurun_out/${T}_profc5_bench.json 2>&1) || exit $?
+      (cd /tmp && timeout -k 10 180 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/${T}_profc5g \
+        -o run --output-format csv -- python $R/tools/td3_grad_steps.py 50 \
+        > $R/gpurun_out/${T}_profc5g.log 2>&1) || exit $?
+      python tools/kernel_shapes.py gpurun_out/${T}_profc5g/run_kernel_trace.csv 40 \
+        > gpurun_out/${T}_profc5g_shapes.txt 2>&1 ;;
     c3) run c3 300 python bench.py --config c3 --steps 30 --warmup 5 ;;
     c4) run c4 400 python bench.py --config c4 --steps 4 --warmup 1 ;;
     c5) run c5 300 python bench.py --config c5 --steps 30 --warmup 5 ;;

@@ -37,13 +37,29 @@ def _inputs():
         PKG_DIR.parent / 'include' / 'xagents_hip.h']
 
 
+def _flags_key():
+    return (' '.join([HIPCC, *CFLAGS]) + '\0').encode()
+
+
 def source_hash():
-    """16 hex digits of SHA-256 over every library input (name + bytes): baked into the
-    library as xa_build_hash(), compared by needs_build() and _lib.load()."""
+    """16 hex digits of SHA-256 over every library input (name + bytes) and the compiler
+    command (HIPCC + CFLAGS): baked into the library as xa_build_hash(), compared by
+    needs_build() and _lib.load()."""
     h = hashlib.sha256()
     for f in _inputs():
         h.update(f.name.encode() + b'\0' + f.read_bytes() + b'\0')
+    h.update(_flags_key())
     return h.hexdigest()[:16]
+
+
+def _object_key(src):
+    """What one object depends on: its source, every csrc header and the C ABI header
+    (the .hip files include no other .hip), the compiler command."""
+    h = hashlib.sha256()
+    for f in [src] + sorted(CSRC.glob('*.hpp')) + [PKG_DIR.parent / 'include' / 'xagents_hip.h']:
+        h.update(f.name.encode() + b'\0' + f.read_bytes() + b'\0')
+    h.update(_flags_key())
+    return h.hexdigest()
 
 
 def library_hash(path=LIB_PATH):
@@ -67,13 +83,23 @@ def build_library(force=False, verbose=False):
     digest = source_hash()
 
     def compile_one(src):
+        # only xa_runtime.hip carries the library hash; every other object is rebuilt
+        # when its own inputs change (key file next to the object)
         obj = BUILD_DIR / (src.stem + '.o')
-        cmd = [HIPCC, *CFLAGS, f'-DXA_BUILD_HASH="{digest}"', '-c', str(src), '-o', str(obj)]
+        stamp = obj.with_suffix('.key')
+        runtime = src.name == 'xa_runtime.hip'
+        key = _object_key(src)
+        if not force and not runtime and obj.exists() and stamp.exists() and \
+                stamp.read_text() == key:
+            return obj
+        extra = [f'-DXA_BUILD_HASH="{digest}"'] if runtime else []
+        cmd = [HIPCC, *CFLAGS, *extra, '-c', str(src), '-o', str(obj)]
         if verbose:
             print(' '.join(cmd))
         res = subprocess.run(cmd, capture_output=True, text=True)
         if res.returncode != 0:
             raise RuntimeError(f'hipcc failed for {src.name}:\n{res.stderr}')
+        stamp.write_text(key)
         return obj
 
     with ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as pool:

@@ -398,6 +398,8 @@ _SIGNATURES = {
          c_void_p, c_void_p, c_void_p, c_int64, c_void_p],
     ),
     'xa_ac_head_grad': (c_int, [POINTER(XaHeadGradArgs), c_void_p]),
+    'xa_minibatch_adv_sums': (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
+                                      c_void_p, c_void_p]),
     'xa_diag_gaussian': (
         c_int,
         [c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_uint64, c_int, c_void_p, c_int64,

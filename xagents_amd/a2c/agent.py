@@ -150,13 +150,17 @@ class A2C(ExecutorActorCritic, OnPolicy):
     def set_rollout_uniforms(self, uniforms):
         """Parity mode: the fused rollout samples every action by inverse CDF from these
         [n_envs, n_steps] f32 device uniforms (held, not copied) instead of the Philox
-        stream; None restores Philox."""
-        if self.executor_path:
-            raise NotImplementedError('rollout uniforms are injected on the fused MLP path')
+        stream; None restores Philox. On the layer-executor path (Categorical actors) the
+        uniforms are copied time-major once, so each step's xa_categorical reads a row."""
         if uniforms is not None:
             assert uniforms.dtype == torch.float32 and uniforms.is_contiguous() and \
                 tuple(uniforms.shape) == (self.n_envs, self.n_steps), \
                 f'Expected f32 [{self.n_envs}, {self.n_steps}] uniforms'
+        if self.executor_path:
+            if self.gaussian:
+                raise NotImplementedError('rollout uniforms drive Categorical sampling only')
+            self._exec_uniforms = None if uniforms is None else uniforms.t().contiguous()
+            return
         self._rollout_uniforms = uniforms
         self._rargs.uniforms = None if uniforms is None else uniforms.data_ptr()
         self._graph = None
@@ -317,12 +321,19 @@ class A2C(ExecutorActorCritic, OnPolicy):
         captured when every exchange goes through the peer kernel or through RCCL (the
         nccl backend's all-reduce is graph-capturable: tests/test_gpu_rccl_capture.py);
         a gloo collective cannot be captured, so gloo steps without the peer path run
-        eagerly (as does any step whose capture raises)."""
-        if self.distributed and getattr(self, 'peer', None) is None and \
-                dist.get_backend() != 'nccl':
+        eagerly (as does any step whose capture raises). A multi-rank RCCL collective
+        replayed from a hipGraph has only been tested at world size 1, so RCCL steps of
+        W > 1 ranks stay eager unless XA_CAPTURE_RCCL=1; and in data-parallel runs the
+        capture-or-eager outcome is agreed collectively (every rank captures, then a MIN
+        all-reduce of the success flags), so no rank replays a graph while another runs
+        the step eagerly."""
+        rccl_only = self.distributed and getattr(self, 'peer', None) is None
+        if rccl_only and (dist.get_backend() != 'nccl' or (
+                self.world_size > 1 and os.environ.get('XA_CAPTURE_RCCL', '0') != '1')):
             self.use_graph = False
             self._graph = None
             return
+        ok = True
         try:
             graphs = []
             # rollout, update, and both back to back: the timed loop replays the third (one
@@ -337,6 +348,16 @@ class A2C(ExecutorActorCritic, OnPolicy):
             self._graph = graphs
         except Exception as exc:  # collectives that refuse capture -> eager launches
             warnings.warn(f'hipGraph capture failed ({exc}); running the train step eagerly')
+            ok = False
+        if self.distributed:
+            flag = torch.tensor([1 if ok else 0], dtype=torch.int32)
+            if dist.get_backend() == 'nccl':
+                flag = flag.to(self.device)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+            ok = bool(int(flag.item()))
+            if not ok and self._graph is not None:
+                warnings.warn('hipGraph capture failed on another rank; running eagerly')
+        if not ok:
             self.use_graph = False
             self._graph = None
 

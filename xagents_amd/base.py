@@ -190,8 +190,13 @@ class BaseAgent(ABC):
             self.plateau_count += 1
         if self.plateau_count >= self.plateau_reduce_patience:
             current_lr, new_lr = None, None
+            pending = getattr(self, '_pending_lr', None)
             for model in self.output_models:
                 current_lr = model.optimizer.learning_rate
+                if pending is not None and model is self.output_models[-1]:
+                    # data parallel: a reduction not applied yet (it waits for the next
+                    # _dp_sync) compounds with this one, as the reference's would
+                    current_lr = pending
                 new_lr = current_lr * self.plateau_reduce_factor
             self.display_message(f'Learning rate reduced {current_lr} -> {new_lr}')
             if getattr(self, 'distributed', False):

@@ -318,6 +318,62 @@ extern "C" int xa_diag_gaussian(const float* mu, int64_t ld_mu, int n, int d, co
   return 0;
 }
 
+// One workgroup per (epoch, minibatch): f64 [sum adv, sum adv^2, count] of adv = returns -
+// values over the minibatch's flat sample indices (run_ppo_epochs' per-minibatch
+// normalisation, ppo/agent.py:180-183), summed in a fixed order (lane-strided partials,
+// wave butterfly, waves in index order) so every call gives the same bits.
+namespace {
+
+__global__ __launch_bounds__(256) void minibatch_adv_sums_kernel(
+    const float* __restrict__ returns, const float* __restrict__ values,
+    const int64_t* __restrict__ idx, int batch, int mb_size, int n_mb,
+    double* __restrict__ out) {
+  __shared__ double red[2][4];
+  const int set = blockIdx.x, e = set / n_mb, m = set - e * n_mb;
+  const int64_t base = (int64_t)e * batch + (int64_t)m * mb_size;
+  const int cnt = min(mb_size, batch - m * mb_size);
+  double s1 = 0.0, s2 = 0.0;
+  for (int q = threadIdx.x; q < cnt; q += blockDim.x) {
+    const int64_t i = idx[base + q];
+    const double adv = (double)(returns[i] - values[i]);
+    s1 += adv;
+    s2 += adv * adv;
+  }
+  s1 = xa_wave_sum_f64(s1);
+  s2 = xa_wave_sum_f64(s2);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) {
+    red[0][w] = s1;
+    red[1][w] = s2;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t1 = 0.0, t2 = 0.0;
+    for (int k = 0; k < 4; ++k) {
+      t1 += red[0][k];
+      t2 += red[1][k];
+    }
+    out[set * 3 + 0] = t1;
+    out[set * 3 + 1] = t2;
+    out[set * 3 + 2] = (double)cnt;
+  }
+}
+
+}  // namespace
+
+extern "C" int xa_minibatch_adv_sums(const float* returns, const float* values,
+                                     const int64_t* idx, int batch, int mb_size, int epochs,
+                                     double* out, void* stream) {
+  XA_CHECK_ARG(returns && values && idx && out && batch > 0 && mb_size > 0 &&
+                   mb_size <= batch && epochs > 0,
+               "xa_minibatch_adv_sums: bad arguments");
+  const int n_mb = (batch + mb_size - 1) / mb_size;
+  hipLaunchKernelGGL(minibatch_adv_sums_kernel, dim3(epochs * n_mb), dim3(256), 0,
+                     (hipStream_t)stream, returns, values, idx, batch, mb_size, n_mb, out);
+  XA_CHECK_LAUNCH("xa_minibatch_adv_sums");
+  return 0;
+}
+
 extern "C" int xa_ac_head_grad(const XaHeadGradArgs* p, void* stream) {
   XA_CHECK_ARG(p && (p->dist_kind != XA_DIST_DIAG_GAUSSIAN || (p->actions_f && p->ld_actions >= p->n_actions)),
                "xa_ac_head_grad: a Gaussian head needs actions_f [n, >= n_actions]");

@@ -249,14 +249,18 @@ class LayerExecutor:
         return [self.touts[i] for i in self.model.outputs]
 
     # ---- backward ----------------------------------------------------------------
-    def backward(self, d_outputs, grad, batch=None, dinput=None, accumulate=False):
+    def backward(self, d_outputs, grad, batch=None, dinput=None, accumulate=False,
+                 on_grad=None):
         """d_outputs: gradients w.r.t. the output layers (model.outputs order, [b, n]).
         Writes the flat parameter gradient into `grad` (Keras variable order; None skips
         the parameter gradients) and, if given, d(loss)/d(input) into `dinput` [b, in]
         (dense input layers). `batch` (<= B) back-propagates only the first rows of the
         last forward (samples are independent rows, so a prefix of every buffer is a
         smaller batch). `accumulate` adds the parameter gradient to `grad` (chunked
-        minibatches)."""
+        minibatches). `on_grad(w0)` is called once the launches writing a layer's weight
+        and bias gradient (flat offsets w0 ..) are queued, before its input gradient's:
+        layers finish in reverse order, so grad[w0:] is then final (the hook of the
+        data-parallel path's bucketed all-reduce)."""
         Bb = batch or self.B
         assert Bb <= self.B
         tp = self.model.theta.data_ptr()
@@ -306,6 +310,8 @@ class LayerExecutor:
                     gemm(1, n_out, Bb, None, d.data_ptr(), gp + 4 * b0, a_m=(1, 0, 0),
                          a_k=(1, 0, 0), b_ks=n_out, b_ns=1, ldc=n_out, beta=accumulate,
                          workspace=self.workspace)
+                    if on_grad is not None:
+                        on_grad(w0)
                 if j == -1 and dinput is not None:
                     gemm(Bb, n_in, n_out, d.data_ptr(), tp + 4 * w0, dinput.data_ptr(),
                          a_m=(1, n_out, 0), b_ks=1, b_ns=n_out, ldc=n_in,
@@ -334,6 +340,8 @@ class LayerExecutor:
                     gemm(1, F, rows * P, None, d.data_ptr(), gp + 4 * b0, a_m=(1, 0, 0),
                          a_k=(1, 0, 0), b_ks=F, b_ns=1, ldc=F, beta=accumulate,
                          workspace=self.workspace)
+                if gp is not None and on_grad is not None:
+                    on_grad(w0)
                 if j != -1:
                     assert not written[j], 'a conv input with two consumers is not supported'
                     if self._dgrad_ok(i):

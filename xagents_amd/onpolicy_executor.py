@@ -11,8 +11,11 @@ Rollout (A2C.get_batch, xagents/a2c/agent.py:96-139), per step t:
     terminal-obs feed-through of a2c/agent.py:132-136)                 xa_replay_env_step
 then V(get_states()) and GAE / n-step returns (xa_gae / xa_nstep_returns).
 Update (PPO.run_ppo_epochs ppo/agent.py:157-191, A2C.train_step a2c/agent.py:190-218):
-per minibatch gather (xa_ring_gather) -> forward -> xa_ac_head_grad -> backward ->
-[RCCL all-reduce of the gradient and of the advantage sums] -> tf.clip_by_global_norm +
+every epoch's shuffle drawn and uploaded at once, the advantage statistics of every
+minibatch in one launch (xa_minibatch_adv_sums) [+ ONE all-reduce of them per train step],
+then per minibatch gather (xa_ring_gather) -> forward -> xa_ac_head_grad -> backward
+[-> bucketed RCCL all-reduce of the gradient: the dense layers' slice is issued as soon as
+its weight gradient is final, overlapping the conv backward] -> tf.clip_by_global_norm +
 Keras Adam (xa_clip_adam).
 Layouts: frames time-major [T+1, N, ...] (each step's batch is contiguous for the
 GEMMs); per-step scalars env-major [N, T] (concat_step_batches order, base.py:549-564).
@@ -89,11 +92,19 @@ class ExecutorActorCritic:
         self.dlogits = torch.zeros(mb, self.n_actions, **f32)
         self.dvalue = torch.zeros(mb, 1, **f32)
         self.head_loss = torch.zeros(3, **f32)
-        self.adv_sums = torch.zeros(3, dtype=torch.float64, device=dev)
+        E = getattr(self, 'ppo_epochs', 1)
+        # [sum adv, sum adv^2, count] of every (epoch, minibatch) of a train step
+        self.adv_sums = torch.zeros(E * self.n_mb, 3, dtype=torch.float64, device=dev)
         self.grad = torch.zeros(self.model.n_params, **f32)
         self.adam_ws = torch.zeros(1024, dtype=torch.float64, device=dev)
-        self._slots_obs = torch.zeros(mb, dtype=torch.int64, device=dev)
-        self._slots_flat = torch.zeros(mb, dtype=torch.int64, device=dev)
+        # every epoch's shuffled sample slots of a train step, uploaded in one copy
+        self._slots_obs = torch.zeros(E * B, dtype=torch.int64, device=dev)
+        self._slots_flat = torch.zeros(E * B, dtype=torch.int64, device=dev)
+        self._exec_uniforms = None
+        # data parallel: all-reduce buckets of at least this many bytes, issued while the
+        # backward of the earlier layers runs (XA_BUCKET_MB, default 4)
+        import os
+        self.bucket_floats = int(float(os.environ.get('XA_BUCKET_MB', '4')) * (1 << 20)) // 4
         if self.distributed:
             torch.distributed.broadcast(self.model.theta, 0)
 
@@ -115,7 +126,9 @@ class ExecutorActorCritic:
                      self.b_act.data_ptr() + 4 * t * A, self.b_logp.data_ptr() + 4 * t,
                      self.b_ent.data_ptr() + 4 * t, T, stream())
             else:
-                call('xa_categorical', logits.data_ptr(), A, N, A, None,
+                u = self._exec_uniforms
+                call('xa_categorical', logits.data_ptr(), A, N, A,
+                     None if u is None else u.data_ptr() + 4 * t * N,
                      self.rng_counter.data_ptr(), self.rng_seed, t, None,
                      self.b_act.data_ptr() + 4 * t, self.b_logp.data_ptr() + 4 * t,
                      self.b_ent.data_ptr() + 4 * t, T, stream())
@@ -157,8 +170,10 @@ class ExecutorActorCritic:
         self._slots_flat[:idx.size].copy_(torch.from_numpy(idx))
         return idx.size
 
-    def _gather_minibatch(self, n):
-        so, sf = self._slots_obs.data_ptr(), self._slots_flat.data_ptr()
+    def _gather_minibatch(self, n, off=0):
+        """Gather the n samples whose slots start at slot row `off`."""
+        so = self._slots_obs.data_ptr() + 8 * off
+        sf = self._slots_flat.data_ptr() + 8 * off
         call('xa_ring_gather', self.obs_buf.data_ptr(), self.mb_obs.data_ptr(), so, n,
              self.envs.obs_bytes, stream())
         act_bytes = 4 * self.n_actions if self.gaussian else 4
@@ -166,7 +181,11 @@ class ExecutorActorCritic:
                              (self.b_val, self.mb_val, 4), (self.b_ret, self.mb_ret, 4)):
             call('xa_ring_gather', src.data_ptr(), dst.data_ptr(), sf, n, nb, stream())
 
-    def _minibatch_step(self, n):
+    def _minibatch_step(self, n, k=None):
+        """One optimizer step on the gathered minibatch of n samples. k: its row of
+        adv_sums (the train step's precomputed, all-reduced advantage statistics); None
+        computes them from the minibatch itself (all-reduced in place when data
+        parallel)."""
         A = self.n_actions
         for j, ex in enumerate(self.ex_chunks):
             c0 = j * self.chunk
@@ -195,23 +214,33 @@ class ExecutorActorCritic:
         h.adv_eps = float(getattr(self, 'advantage_epsilon', 0.0))
         h.dlogits, h.dvalues, h.loss = (self.dlogits.data_ptr(), self.dvalue.data_ptr(),
                                         self.head_loss.data_ptr())
-        h.adv_stats = self.adv_sums.data_ptr()
         h.stats_mode = 0
-        if self.distributed and self.loss_kind == XA_LOSS_PPO:
+        if self.loss_kind == XA_LOSS_PPO and k is not None:
+            h.stats_mode, h.adv_stats = 2, self.adv_sums[k].data_ptr()
+        elif self.distributed and self.loss_kind == XA_LOSS_PPO:
+            sums = self.adv_sums[0]
+            h.adv_stats = sums.data_ptr()
             h.stats_mode = 1
             call('xa_ac_head_grad', ctypes.byref(h), stream())
-            torch.distributed.all_reduce(self.adv_sums)
+            torch.distributed.all_reduce(sums)
             h.stats_mode = 2
         call('xa_ac_head_grad', ctypes.byref(h), stream())
-        for j, ex in enumerate(self.ex_chunks):
+        works = []
+        n_chunks = sum(1 for j in range(len(self.ex_chunks)) if j * self.chunk < n)
+        hook = self._bucket_hook(works) if self.distributed else None
+        for j, ex in enumerate(self.ex_chunks[:n_chunks]):
             c0 = j * self.chunk
-            if c0 >= n:
-                break
             rows = min(ex.B, n - c0)
             ex.backward([self.dlogits[c0:c0 + rows], self.dvalue[c0:c0 + rows]], self.grad,
-                        batch=rows, accumulate=j > 0)
+                        batch=rows, accumulate=j > 0,
+                        on_grad=hook if j == n_chunks - 1 else None)
         if self.distributed:
-            torch.distributed.all_reduce(self.grad)
+            # the slice no bucket has taken yet (the first layers), then wait for the
+            # buckets in flight: the optimizer reads the whole all-reduced gradient
+            if self._bucket_hi > 0:
+                torch.distributed.all_reduce(self.grad[:self._bucket_hi])
+            for w in works:
+                w.wait()
         opt = self.model.optimizer
         call('xa_adam_step_bump', opt.iterations.data_ptr(), stream())
         kernels.clip_adam(self.model.theta, opt.m, opt.v, self.grad, opt.iterations,
@@ -219,17 +248,59 @@ class ExecutorActorCritic:
                           clip_norm=self.grad_norm, grad_scale=1.0 / self.world_size,
                           workspace=self.adam_ws)
 
+    def _bucket_hook(self, works):
+        """Backward hook of the last chunk (LayerExecutor.backward on_grad): layers finish
+        in reverse parameter order, so once layer l's weight gradient is queued the slice
+        grad[w0_l:] is final; every slice of at least bucket_floats goes into an async
+        all-reduce right away (on RCCL's stream, behind the launches that wrote it) while
+        the compute stream goes on with the earlier layers' backward. For the CNN
+        actor-critic the first bucket is the dense layers' 77 MB, in flight during the dense
+        input gradient and the conv backward."""
+        self._bucket_hi = self.model.n_params
+
+        def hook(w0):
+            if self._bucket_hi - w0 >= self.bucket_floats:
+                works.append(torch.distributed.all_reduce(self.grad[w0:self._bucket_hi],
+                                                          async_op=True))
+                self._bucket_hi = w0
+        return hook
+
+    def _shuffles(self):
+        """Every epoch's permutation of the env-major batch (get_mini_batches,
+        ppo/agent.py:139-155): numpy's global RNG, one np.random.permutation per epoch in
+        epoch order; or the parity-mode permutations of set_minibatch_permutation."""
+        B = self.n_envs * self.n_steps
+        host = getattr(self, '_host_perm', None)
+        if host is not None:
+            return host.cpu().numpy().astype(np.int64).reshape(-1)
+        return np.concatenate([np.random.permutation(B) for _ in range(self.ppo_epochs)])
+
     def _executor_update(self):
         B = self.n_envs * self.n_steps
         if self.loss_kind == XA_LOSS_PPO:
-            # every epoch reshuffles the batch, then contiguous minibatch slices
-            # (ppo/agent.py:139-155); the permutation uses numpy's global RNG
-            for _ in range(self.ppo_epochs):
-                perm = np.random.permutation(B)
+            # all epochs' shuffles at once, then contiguous minibatch slices of each; the
+            # advantage statistics of all E x M minibatches in one launch and (data
+            # parallel) one all-reduce, instead of one blocking collective per minibatch
+            E = self.ppo_epochs
+            if self._slots_obs.numel() < E * B or self.adv_sums.shape[0] < E * self.n_mb:
+                # ppo_epochs raised after construction
+                dev = self.device
+                self._slots_obs = torch.zeros(E * B, dtype=torch.int64, device=dev)
+                self._slots_flat = torch.zeros(E * B, dtype=torch.int64, device=dev)
+                self.adv_sums = torch.zeros(E * self.n_mb, 3, dtype=torch.float64, device=dev)
+            self._upload_slots(self._shuffles())
+            call('xa_minibatch_adv_sums', self.b_ret.data_ptr(), self.b_val.data_ptr(),
+                 self._slots_flat.data_ptr(), B, self.mb, self.ppo_epochs,
+                 self.adv_sums.data_ptr(), stream())
+            if self.distributed:
+                torch.distributed.all_reduce(self.adv_sums)
+            k = 0
+            for e in range(self.ppo_epochs):
                 for m in range(self.n_mb):
-                    n = self._upload_slots(perm[m * self.mb:(m + 1) * self.mb])
-                    self._gather_minibatch(n)
-                    self._minibatch_step(n)
+                    n = min(self.mb, B - m * self.mb)
+                    self._gather_minibatch(n, e * B + m * self.mb)
+                    self._minibatch_step(n, k)
+                    k += 1
         else:
             n = self._upload_slots(np.arange(B))
             self._gather_minibatch(n)

@@ -205,7 +205,14 @@ class PPO(A2C):
         # XCD-local placement of small grids (xa_ppo_update): automatic in one process; data
         # parallel only when every rank owns its GPU (ranks sharing one could strand each
         # other's XCD elections). XA_PPO_PLACE=spread|local overrides.
+        # The election needs G free CU slots on ONE XCD (at G = 32 with one block per CU:
+        # all 8 x 32 CUs idle), so it assumes the update owns the GPU while it runs: a
+        # kernel overlapping it on another stream could hold a CU on every XCD and stall
+        # every spinning block until the abort. The opt-in side-stream statistics copy
+        # (XA_STATS_SIDE_STREAM=1) can overlap the update, so it forces the spread grid.
         place = os.environ.get('XA_PPO_PLACE', 'auto')
+        if getattr(self, 'stats_side_stream', False) and place != 'local':
+            place = 'spread'
         if place == 'spread':
             u.placement = _lib.XA_PPO_PLACE_SPREAD
         elif place == 'local' or (self.distributed and getattr(self, '_ranks_share', 1) == 1):
