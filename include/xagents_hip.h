@@ -665,6 +665,67 @@ int xa_critic_td_grad(const float* v1, const float* v2, const float* tv1, const 
                       const float* rewards, const float* dones, int batch, float gamma,
                       float huber_delta, float* dv1, float* dv2, float* loss, void* stream);
 
+/* One network of the fused TD3 / DDPG gradient step: the flat Keras-order parameters of a
+ * 3-layer .cfg MLP (W1 [in][h1], b1, W2 [h1][h2], b2, W3 [h2][out], b3) and, for the
+ * networks that learn, their Keras Adam state (t = *step + 1 this step; the launch adds 1). */
+typedef struct XaTdNet {
+  float* theta;
+  float* m;
+  float* v;
+  int* step;
+  float lr, beta1, beta2, eps;
+} XaTdNet;
+
+/* A whole DDPG / TD3 gradient step (DDPG.update_weights' body, ddpg/agent.py:129-147:
+ * update_critic_weights 104-127, update_actor_weights 87-102, sync_target_models 73-85;
+ * TD3's twin critics + target smoothing, td3/agent.py:66-110) in ONE persistent launch of
+ * n_blocks resident workgroups (0: the default) with grid barriers between its phases.
+ * Batch rows are the ring rows `slots` [batch] (concat_buffer_samples order) of the f32
+ * replay rings (states / new_states [.][obs_dim], actions [.][act_dim], rewards, dones).
+ * twin: TD3 (critic 2 + target critic 2); smooth: TD3 target smoothing (Philox normals at
+ * (row, column, *rng_counter), key seed, times noise_sigma, clipped to +-noise_clip, the
+ * counter advanced by 1 -- the draw of xa_noisy_actions); actor_update: this step updates the
+ * actor through the updated critic 1 and Polyak-averages every target (tau). Critic loss
+ * Sum_b (v - y)^2 per critic (huber_delta > 0: opt-in Huber-TD), actor loss -mean Q.
+ * Outputs: the sampled batch (out_s, out_a, out_r, out_d, out_s2), noise_out [batch][act]
+ * (optional), dv1 / dv2 [batch] and the raw gradients g_* (before Adam), loss_out [batch]
+ * (optional); parameters, moments and step counters in place. workspace: zeroed once by
+ * the caller (xa_td3_update_workspace_bytes), reused by every launch without a reset; a
+ * barrier that times out (10 s) sets *status = 1 and the workspace must be re-zeroed. */
+typedef struct XaTd3UpdateArgs {
+  int batch, obs_dim, act_dim, h1, h2;
+  int twin, smooth, actor_update;
+  float gamma, tau, noise_sigma, noise_clip, huber_delta;
+  const float* ring_states;
+  const float* ring_new_states;
+  const float* ring_actions;
+  const float* ring_rewards;
+  const float* ring_dones;
+  const int64_t* slots;
+  uint64_t* rng_counter;
+  uint64_t seed;
+  XaTdNet actor, critic1, critic2, target_actor, target_critic1, target_critic2;
+  float* out_s;
+  float* out_a;
+  float* out_r;
+  float* out_d;
+  float* out_s2;
+  float* noise_out;
+  float* dv1;
+  float* dv2;
+  float* loss_out;
+  float* g_actor;
+  float* g_critic1;
+  float* g_critic2;
+  void* workspace;
+  size_t workspace_bytes;
+  int n_blocks;
+  int* status;
+} XaTd3UpdateArgs;
+
+size_t xa_td3_update_workspace_bytes(int batch, int obs_dim, int act_dim, int h1, int h2);
+int xa_td3_update(const XaTd3UpdateArgs* args, void* stream);
+
 /* TFP Categorical(logits) over n logit rows (A2C.get_model_outputs, a2c/agent.py:65-94):
  * log-prob and entropy of the given actions (actions_in) or of an inverse-CDF sample
  * with uniforms[i] or Philox(i, step, *rng_counter, seed). Same arithmetic as the fused

@@ -57,6 +57,8 @@ for step in "$@"; do
     dp) run_pytest dp 500 tests/test_gpu_dp.py tests/test_gpu_peer.py tests/test_gpu_rccl_capture.py ;;
     gpu) run_pytest gpu 1000 tests -m gpu ;;
     configs) run_pytest configs 400 tests/test_gpu_configs.py ;;
+    td3) run_pytest td3 400 tests/test_gpu_td3.py tests/test_gpu_scale.py tests/test_gpu_configs.py::test_c5_td3_64_envs_rb2 ;;
+    c4dp) run_pytest c4dp 600 tests/test_gpu_dp.py -k cnn tests/test_gpu_configs.py::test_c4_ppo_cnn_128_env_shard ;;
     smoke) run smoke 180 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 300 python bench.py --steps 20 --warmup 5 ;;
     ab)

@@ -304,6 +304,31 @@ class XaPeerAllReduceArgs(Structure):
     ]
 
 
+class XaTdNet(Structure):
+    _fields_ = [('theta', c_void_p), ('m', c_void_p), ('v', c_void_p), ('step', c_void_p),
+                ('lr', c_float), ('beta1', c_float), ('beta2', c_float), ('eps', c_float)]
+
+
+class XaTd3UpdateArgs(Structure):
+    _fields_ = [
+        ('batch', c_int), ('obs_dim', c_int), ('act_dim', c_int), ('h1', c_int), ('h2', c_int),
+        ('twin', c_int), ('smooth', c_int), ('actor_update', c_int),
+        ('gamma', c_float), ('tau', c_float), ('noise_sigma', c_float), ('noise_clip', c_float),
+        ('huber_delta', c_float),
+        ('ring_states', c_void_p), ('ring_new_states', c_void_p), ('ring_actions', c_void_p),
+        ('ring_rewards', c_void_p), ('ring_dones', c_void_p), ('slots', c_void_p),
+        ('rng_counter', c_void_p), ('seed', c_uint64),
+        ('actor', XaTdNet), ('critic1', XaTdNet), ('critic2', XaTdNet),
+        ('target_actor', XaTdNet), ('target_critic1', XaTdNet), ('target_critic2', XaTdNet),
+        ('out_s', c_void_p), ('out_a', c_void_p), ('out_r', c_void_p), ('out_d', c_void_p),
+        ('out_s2', c_void_p), ('noise_out', c_void_p), ('dv1', c_void_p), ('dv2', c_void_p),
+        ('loss_out', c_void_p), ('g_actor', c_void_p), ('g_critic1', c_void_p),
+        ('g_critic2', c_void_p),
+        ('workspace', c_void_p), ('workspace_bytes', ctypes.c_size_t),
+        ('n_blocks', c_int), ('status', c_void_p),
+    ]
+
+
 XA_RING_DEQUE = 0
 XA_RING_RB2 = 1
 XA_ACT_NONE = 0
@@ -398,6 +423,8 @@ _SIGNATURES = {
          c_void_p, c_void_p, c_void_p, c_int64, c_void_p],
     ),
     'xa_ac_head_grad': (c_int, [POINTER(XaHeadGradArgs), c_void_p]),
+    'xa_td3_update_workspace_bytes': (ctypes.c_size_t, [c_int, c_int, c_int, c_int, c_int]),
+    'xa_td3_update': (c_int, [POINTER(XaTd3UpdateArgs), c_void_p]),
     'xa_minibatch_adv_sums': (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                                       c_void_p, c_void_p]),
     'xa_diag_gaussian': (

@@ -1,0 +1,987 @@
+// TD3 / DDPG gradient step in ONE persistent launch (xa_td3_update): the sample gather,
+// both critics' forward / TD head / backward / Keras Adam and, on policy-delay steps, the
+// actor's forward / -mean Q backward through the UPDATED critic 1 / Keras Adam and the
+// Polyak sync of every target network. Replaces DDPG.update_critic_weights +
+// update_actor_weights + sync_target_models (xagents/ddpg/agent.py:73-147) and TD3's twin
+// critic / target-smoothing update (xagents/td3/agent.py:66-110) -- at batch 64 those are
+// ~90 small launches of 4-12 us each (profiles/r04a_c5_grad_step_kernel_shapes.txt).
+//
+// Networks: the 3-layer MLPs of the .cfg models (in -> H1 relu -> H2 relu -> out; the
+// actor's output tanh, the critics' linear), parameters in Keras order (W1 [in][H1], b1,
+// W2 [H1][H2], b2, W3 [H2][out], b3), batch rows r = the sampled transitions.
+//
+// G resident workgroups of 256 threads run the phases below; a phase's jobs are dealt
+// round-robin (job j -> workgroup j mod G) and a grid barrier separates the phases. A job
+// is one 64-row x 16-column output tile: both operands staged in LDS (zero padded to a
+// multiple of 16 along K), wave w computes rows 16 w .. 16 w + 15 on v_mfma_f32_16x16x4f32,
+// K in chunks of 16 (lane (i, q) reads k0 + 4q .. 4q + 3 of its row / column as one float4,
+// component s feeding MFMA step s: one consistent k order for A and B).
+//   P1  L1 forward: target actor (s'), critic 1 / 2 ([s, a]), actor (s, policy steps)
+//   P2  L2 forward of the same networks
+//   P3  L3: target actor tanh (+ TD3 smoothing noise, clip) -> a'; critics -> v1, v2;
+//       actor tanh -> pi(s)
+//   P4  target critics L1 on [s', a'];  P5  L2
+//   P6  target critics L3 -> tv1, tv2; TD head y = r + (1 - d) gamma min(tv1, tv2),
+//       dv = 2 (v - y) (MSE) or clip(v - y, +-delta) (opt-in Huber), per-sample loss
+//   P7  critics backward: dW2 / db2 (dZ2 = dv W3^T gate(h2) formed while staging), dH1,
+//       dW3 / db3
+//   P8  critics: dW1 / db1 with the Keras Adam step applied in the same job, Adam of every
+//       other critic parameter (+ Polyak of the critic targets on policy steps)
+//   policy steps only:
+//   P9  critic 1 L1 on [s, pi(s)] (updated critic 1);  P10 L2
+//   P11 dH1 of -mean Q (dZ2 = -W3^T gate(h2) / B)
+//   P12 d pi = dH1 W1[s.. s + A]^T, times tanh' -> dZ3 of the actor
+//   P13 actor backward: dW2 / db2, dH1, dW3 / db3
+//   P14 actor dW1 / db1 + Adam + Polyak, Adam + Polyak of the other actor parameters
+// Hand-offs follow MI355X_MICROARCH.md's visibility table row 1: every in-launch produced
+// word (activations, gradients, updated parameters) is stored write-through (sc1) and
+// loaded with sc1 loads; a barrier drains (vmcnt 0), joins the workgroup and ONE lane adds
+// to an agent-scope counter that ONE lane polls. The counter is never reset: the workspace
+// keeps the value the previous launch left (`base`), so graph replays need no memset.
+#include <math.h>
+
+#include "../../include/xagents_hip.h"
+#include "xa_adam.hpp"
+#include "xa_common.hpp"
+
+namespace {
+
+typedef __attribute__((address_space(1))) unsigned gu32;
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+
+constexpr int kRsrcWord3 = 0x00020000;  // raw buffer, gfx9-family resource word 3
+constexpr int kAuxSc1 = 16;             // buffer instruction aux bits: write-through (sc1)
+constexpr uint64_t kSpinTicks = 1000000000;  // 10 s of the 100 MHz wall clock per barrier
+constexpr int kRows = 64, kCols = 16;   // output tile of one job
+constexpr int kMaxK = 416;              // largest GEMM depth (H1, H2, batch, in)
+constexpr int kLd = kMaxK + 4;          // LDS row stride of the staged operands
+constexpr int kAux = 2048 + 1024;       // LDS floats: W3 slice + dZ3 rows of the dZ2 former
+constexpr int kU = 8;                   // loads in flight per thread while staging
+
+XA_DEV f32x4v mfma4(float a, float b, f32x4v c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// ---- write-through hand-off accesses ----
+XA_DEV float ldc(const float* p) {
+  return __uint_as_float(__hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+XA_DEV void stc(float* p, float v) {
+  __hip_atomic_store((gu32*)p, __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// (the base is made wave-uniform explicitly: a buffer resource lives in scalar registers)
+XA_DEV __amdgpu_buffer_rsrc_t rsrc(const void* base) {
+  const uint64_t u = (uint64_t)(uintptr_t)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
+  void* ub = (void*)(uintptr_t)(((uint64_t)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(ub, 0, 0x7FFFFFF0, kRsrcWord3);
+}
+XA_DEV float4 ld4c(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
+  const f32x4v v = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, kAuxSc1);
+  return make_float4(v[0], v[1], v[2], v[3]);
+}
+
+XA_DEV float philox_normal(uint32_t i, uint32_t j, uint64_t ctr, uint64_t seed) {
+  // the same draw as xa_noisy_actions (offpolicy.hip)
+  const xa_u4 r = xa_philox(i, j, (uint32_t)ctr, (uint32_t)(ctr >> 32), (uint32_t)seed,
+                            (uint32_t)(seed >> 32));
+  const float u1 = ((float)(r.x >> 8) + 1.0f) * 5.9604644775390625e-08f;
+  const float u2 = (float)(r.y >> 8) * 5.9604644775390625e-08f;
+  return sqrtf(-2.0f * logf(u1)) * cosf(6.283185307179586f * u2);
+}
+
+// ---- network views ----
+struct Net {
+  float* th;
+  float* m;
+  float* v;
+  int in, out;
+  int w1, b1, w2, b2, w3, b3, P;
+  float alpha;  // Adam step size of this launch's step (online networks)
+};
+
+XA_DEV Net make_net(const XaTdNet& d, int in, int H1, int H2, int out, bool adam) {
+  Net n;
+  n.th = d.theta;
+  n.m = d.m;
+  n.v = d.v;
+  n.in = in;
+  n.out = out;
+  n.w1 = 0;
+  n.b1 = in * H1;
+  n.w2 = n.b1 + H1;
+  n.b2 = n.w2 + H1 * H2;
+  n.w3 = n.b2 + H2;
+  n.b3 = n.w3 + H2 * out;
+  n.P = n.b3 + out;
+  n.alpha = adam ? adam_alpha(d.lr, d.beta1, d.beta2, *d.step + 1) : 0.0f;
+  return n;
+}
+
+// A row source: row r of X = [src0 row | src1 row] (src1 optional), each source either a
+// dense [rows][ld] buffer or a replay ring addressed through the sample slots
+struct XSrc {
+  const float* p0;
+  int w0, ld0;
+  bool slot0, coh0;
+  const float* p1;
+  int w1, ld1;
+  bool slot1, coh1;
+};
+XA_DEV XSrc xsrc(const float* p, int w, int ld, bool slot, bool coh) {
+  XSrc x;
+  x.p0 = p;
+  x.w0 = w;
+  x.ld0 = ld;
+  x.slot0 = slot;
+  x.coh0 = coh;
+  x.p1 = nullptr;
+  x.w1 = 0;
+  x.ld1 = 0;
+  x.slot1 = false;
+  x.coh1 = false;
+  return x;
+}
+XA_DEV XSrc xcat(XSrc a, const float* p, int w, int ld, bool slot, bool coh) {
+  a.p1 = p;
+  a.w1 = w;
+  a.ld1 = ld;
+  a.slot1 = slot;
+  a.coh1 = coh;
+  return a;
+}
+XA_DEV float xload(const XSrc& x, const int64_t* slots, int r, int k) {
+  if (k < x.w0) {
+    const int64_t row = x.slot0 ? slots[r] : r;
+    const float* p = x.p0 + row * x.ld0 + k;
+    return x.coh0 ? ldc(p) : *p;
+  }
+  const int64_t row = x.slot1 ? slots[r] : r;
+  const float* p = x.p1 + row * x.ld1 + (k - x.w0);
+  return x.coh1 ? ldc(p) : *p;
+}
+
+// A gradient source dZ [rows][cols]: a dense buffer (ld), or the layer-2 output gradient
+// formed on the fly: dZ[r][k] = (sum_a d3[r][a] W3[k][a]) (h2[r][k] > 0), with d3 [rows][n3]
+// (or the constant c3 when d3 is null: the actor loss -mean Q gives -1 / B)
+struct DZ {
+  const float* buf;
+  int ld;
+  const float* h2;
+  int H2;
+  const float* w3;
+  int n3;
+  const float* d3;
+  float c3;
+};
+XA_DEV DZ dz_buf(const float* p, int ld) {
+  DZ d;
+  d.buf = p;
+  d.ld = ld;
+  d.h2 = nullptr;
+  d.H2 = 0;
+  d.w3 = nullptr;
+  d.n3 = 0;
+  d.d3 = nullptr;
+  d.c3 = 0.0f;
+  return d;
+}
+XA_DEV DZ dz_h2(const float* h2, int H2, const float* w3, int n3, const float* d3, float c3) {
+  DZ d;
+  d.buf = nullptr;
+  d.ld = H2;
+  d.h2 = h2;
+  d.H2 = H2;
+  d.w3 = w3;
+  d.n3 = n3;
+  d.d3 = d3;
+  d.c3 = c3;
+  return d;
+}
+
+struct Lds {
+  float* A;    // [64][kLd]
+  float* B;    // [16][kLd]
+  float* aux;  // [kAux]
+};
+
+XA_DEV int pad16(int k) { return (k + 15) & ~15; }
+
+// ---- the tile product: wave w, rows 16 w .. 16 w + 15, 16 columns; K padded to 16 ----
+XA_DEV f32x4v tile_mma(const Lds& s, int Kp) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int i = lane & 15, q = lane >> 4;
+  const float* pa = s.A + (16 * w + i) * kLd + 4 * q;
+  const float* pb = s.B + i * kLd + 4 * q;
+  f32x4v c0 = {0.0f, 0.0f, 0.0f, 0.0f}, c1 = {0.0f, 0.0f, 0.0f, 0.0f};
+  for (int k0 = 0; k0 < Kp; k0 += 16) {
+    const float4 a = *reinterpret_cast<const float4*>(pa + k0);
+    const float4 b = *reinterpret_cast<const float4*>(pb + k0);
+    c0 = mfma4(a.x, b.x, c0);
+    c1 = mfma4(a.y, b.y, c1);
+    c0 = mfma4(a.z, b.z, c0);
+    c1 = mfma4(a.w, b.w, c1);
+  }
+  return c0 + c1;
+}
+
+// ---- staging ----
+// A[row][k] = X[r0 + row][k] (rows < nrows, k < K, zero elsewhere up to Kp)
+XA_DEV void stage_a_rows(const Lds& s, const XSrc& x, const int64_t* slots, int r0, int nrows,
+                         int K) {
+  const int Kp = pad16(K);
+  const bool vec = x.p1 == nullptr && !x.slot0 && x.coh0 && (K & 3) == 0 && (x.ld0 & 3) == 0;
+  if (vec) {
+    const __amdgpu_buffer_rsrc_t r = rsrc(x.p0);
+    const int K4 = Kp >> 2, total = kRows * K4;
+    for (int e0 = threadIdx.x; e0 < total; e0 += 256 * kU) {
+      float4 v[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int e = e0 + 256 * u, row = e / K4, k = 4 * (e - row * K4);
+        v[u] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (e < total && row < nrows && k < K)
+          v[u] = ld4c(r, (uint32_t)(((r0 + row) * x.ld0 + k) * 4));
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int e = e0 + 256 * u, row = e / K4, k = 4 * (e - row * K4);
+        if (e < total) *reinterpret_cast<float4*>(&s.A[row * kLd + k]) = v[u];
+      }
+    }
+    return;
+  }
+  const int total = kRows * Kp;
+  for (int e0 = threadIdx.x; e0 < total; e0 += 256 * kU) {
+    float v[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int e = e0 + 256 * u, row = e / Kp, k = e - row * Kp;
+      v[u] = (e < total && row < nrows && k < K) ? xload(x, slots, r0 + row, k) : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int e = e0 + 256 * u, row = e / Kp, k = e - row * Kp;
+      if (e < total) s.A[row * kLd + k] = v[u];
+    }
+  }
+}
+
+// A[i][k] = X[k][i0 + i] (the transposed input of a weight gradient: i < ni in-features,
+// k < nk samples)
+XA_DEV void stage_a_trans(const Lds& s, const XSrc& x, const int64_t* slots, int i0, int ni,
+                          int nk) {
+  const int Kp = pad16(nk), total = kRows * Kp;
+  for (int e0 = threadIdx.x; e0 < total; e0 += 256 * kU) {
+    float v[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int e = e0 + 256 * u, k = e >> 6, i = e & 63;
+      v[u] = (e < total && i < ni && k < nk) ? xload(x, slots, k, i0 + i) : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int e = e0 + 256 * u, k = e >> 6, i = e & 63;
+      if (e < total) s.A[i * kLd + k] = v[u];
+    }
+  }
+}
+
+// the dZ2 former's LDS inputs: W3 rows [k0, k0 + nk) (n3 each) and d3 rows [r0, r0 + nr)
+XA_DEV void stage_dz_aux(const Lds& s, const DZ& d, int k0, int nk, int r0, int nr) {
+  if (!d.h2) return;
+  for (int e = threadIdx.x; e < nk * d.n3; e += 256) s.aux[e] = ldc(d.w3 + k0 * d.n3 + e);
+  float* sd = s.aux + 2048;
+  if (d.d3)
+    for (int e = threadIdx.x; e < nr * d.n3; e += 256) sd[e] = ldc(d.d3 + r0 * d.n3 + e);
+  __syncthreads();
+}
+// dZ2[r][k] from the staged aux (k relative to the aux's k0, r relative to its r0)
+XA_DEV float dz_form(const Lds& s, const DZ& d, float h, int rr, int kk) {
+  float g;
+  if (d.d3) {
+    const float* sd = s.aux + 2048 + rr * d.n3;
+    const float* w = s.aux + kk * d.n3;
+    g = sd[0] * w[0];
+    for (int a = 1; a < d.n3; ++a) g = fmaf(sd[a], w[a], g);
+  } else {
+    g = d.c3 * s.aux[kk * d.n3];
+  }
+  return h > 0.0f ? g : 0.0f;
+}
+
+// A[row][k] = dZ[r0 + row][k] (k < K = the layer's output width)
+XA_DEV void stage_a_dz(const Lds& s, const DZ& d, int r0, int nrows, int K) {
+  const int Kp = pad16(K), total = kRows * Kp;
+  if (d.h2) stage_dz_aux(s, d, 0, K, r0, min(nrows, kRows));
+  const float* src = d.h2 ? d.h2 : d.buf;
+  for (int e0 = threadIdx.x; e0 < total; e0 += 256 * kU) {
+    float v[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int e = e0 + 256 * u, row = e / Kp, k = e - row * Kp;
+      v[u] = (e < total && row < nrows && k < K) ? ldc(src + (int64_t)(r0 + row) * d.ld + k) : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int e = e0 + 256 * u, row = e / Kp, k = e - row * Kp;
+      if (e < total) s.A[row * kLd + k] = (d.h2 && row < nrows && k < K) ? dz_form(s, d, v[u], row, k) : v[u];
+    }
+  }
+}
+
+// B^T[j][k] = W[k][c0 + j] (forward: W row-major [K][N]; j < nc valid columns)
+XA_DEV void stage_b_fwd(const Lds& s, const float* W, int N, int c0, int nc, int K) {
+  const int Kp = pad16(K), total = kCols * Kp;
+  for (int e0 = threadIdx.x; e0 < total; e0 += 256 * kU) {
+    float v[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int e = e0 + 256 * u, k = e >> 4, j = e & 15;
+      v[u] = (e < total && j < nc && k < K) ? ldc(W + (int64_t)k * N + c0 + j) : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int e = e0 + 256 * u, k = e >> 4, j = e & 15;
+      if (e < total) s.B[j * kLd + k] = v[u];
+    }
+  }
+}
+
+// B^T[j][k] = W[c0 + j][k] (input gradient dZ W^T: W row-major [in][K])
+XA_DEV void stage_b_rows(const Lds& s, const float* W, int K, int c0, int nc) {
+  const int Kp = pad16(K), total = kCols * Kp;
+  for (int e0 = threadIdx.x; e0 < total; e0 += 256 * kU) {
+    float v[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int e = e0 + 256 * u, j = e / Kp, k = e - j * Kp;
+      v[u] = (e < total && j < nc && k < K) ? ldc(W + (int64_t)(c0 + j) * K + k) : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int e = e0 + 256 * u, j = e / Kp, k = e - j * Kp;
+      if (e < total) s.B[j * kLd + k] = v[u];
+    }
+  }
+}
+
+// B^T[j][k] = dZ[k][j0 + j] (weight gradient: k < nk samples, j < nc columns)
+XA_DEV void stage_b_dz(const Lds& s, const DZ& d, int j0, int nc, int nk) {
+  const int Kp = pad16(nk), total = kCols * Kp;
+  if (d.h2) stage_dz_aux(s, d, j0, nc, 0, nk);
+  const float* src = d.h2 ? d.h2 : d.buf;
+  for (int e0 = threadIdx.x; e0 < total; e0 += 256 * kU) {
+    float v[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int e = e0 + 256 * u, k = e >> 4, j = e & 15;
+      v[u] = (e < total && j < nc && k < nk) ? ldc(src + (int64_t)k * d.ld + j0 + j) : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int e = e0 + 256 * u, k = e >> 4, j = e & 15;
+      if (e < total) s.B[j * kLd + k] = (d.h2 && j < nc && k < nk) ? dz_form(s, d, v[u], k, j) : v[u];
+    }
+  }
+}
+
+// ---- epilogue helpers: lane l holds D[4 (l >> 4) + r][l & 15] of the wave's 16 rows ----
+XA_DEV int out_row(int r) { return 16 * (threadIdx.x >> 6) + 4 * ((threadIdx.x & 63) >> 4) + r; }
+XA_DEV int out_col() { return threadIdx.x & 15; }
+
+enum { ACT_NONE = 0, ACT_RELU = 1, ACT_TANH = 2 };
+
+XA_DEV float act_f(float v, int act) {
+  if (act == ACT_RELU) return fmaxf(v, 0.0f);
+  if (act == ACT_TANH) return xa_tanhf(v);
+  return v;
+}
+
+// forward job: out[r][c] = act(X W + b) on rows [r0, r0 + 64) x cols [c0, c0 + 16)
+XA_DEV f32x4v fwd_tile(const Lds& s, const XSrc& x, const int64_t* slots, int r0, int B,
+                       const float* W, const float* bias, int K, int N, int c0) {
+  stage_a_rows(s, x, slots, r0, min(kRows, B - r0), K);
+  stage_b_fwd(s, W, N, c0, min(kCols, N - c0), K);
+  __syncthreads();
+  f32x4v acc = tile_mma(s, pad16(K));
+  const int c = c0 + out_col();
+  if (c < N) {
+    const float b = ldc(bias + c);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc[r] = acc[r] + b;
+  }
+  return acc;
+}
+
+XA_DEV void fwd_job(const Lds& s, const XSrc& x, const int64_t* slots, int r0, int B,
+                    const float* W, const float* bias, int K, int N, int c0, int act, float* out) {
+  const f32x4v acc = fwd_tile(s, x, slots, r0, B, W, bias, K, N, c0);
+  const int c = c0 + out_col();
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = r0 + out_row(r);
+    if (row < B && c < N) stc(out + (int64_t)row * N + c, act_f(acc[r], act));
+  }
+}
+
+// input-gradient job: out[r][c] = (dZ W^T)[r][c] * gate (gate: the source layer's relu
+// output > 0), rows [r0, r0 + 64) x cols [c0, c0 + 16) of the layer input (width nin)
+XA_DEV f32x4v dx_tile(const Lds& s, const DZ& d, int r0, int B, const float* W, int K, int c0,
+                      int nc) {
+  stage_a_dz(s, d, r0, min(kRows, B - r0), K);
+  stage_b_rows(s, W, K, c0, nc);
+  __syncthreads();
+  return tile_mma(s, pad16(K));
+}
+
+// weight-gradient tile: D[i][j] = sum_k X[k][i0 + i] dZ[k][j0 + j] (i < ni, j < nc, k < B);
+// the bias gradient sum_k dZ[k][j0 + j] (fixed k order) lands in bsum[j] when bsum != 0
+XA_DEV f32x4v dw_tile(const Lds& s, const XSrc& x, const int64_t* slots, const DZ& d, int i0,
+                      int ni, int j0, int nc, int B, float* bsum) {
+  stage_a_trans(s, x, slots, i0, ni, B);
+  stage_b_dz(s, d, j0, nc, B);
+  __syncthreads();
+  if (bsum && threadIdx.x < nc) {
+    float t = 0.0f;
+    for (int k = 0; k < B; ++k) t += s.B[threadIdx.x * kLd + k];
+    bsum[threadIdx.x] = t;
+  }
+  return tile_mma(s, pad16(B));
+}
+
+// Keras Adam (+ Polyak into the target) of one parameter from its raw gradient
+XA_DEV void adam_one(const Net& n, float g, int i, float omb1, float omb2, float eps,
+                     float* target, float tau) {
+  float th = ldc(n.th + i), m = n.m[i], v = n.v[i];
+  adam_elem(g, th, m, v, n.alpha, omb1, omb2, eps);
+  stc(n.th + i, th);
+  n.m[i] = m;
+  n.v[i] = v;
+  if (target) {
+    const float y = target[i];
+    target[i] = tau == 1.0f ? th : (1.0f - tau) * y + tau * th;
+  }
+}
+
+// weight-gradient job: raw gradient into grad (W [nin][N] at offset w, bias at b when the
+// tile is the first of its column), optionally the Adam step (+ Polyak) of those elements
+XA_DEV void dw_job(const Lds& s, const XSrc& x, const int64_t* slots, const DZ& d, int nin,
+                   int N, int i0, int j0, int B, float* grad, int w, int b, const Net* adam,
+                   const XaTdNet* opt, float* target, float tau, float* bsum_lds) {
+  const int ni = min(kRows, nin - i0), nc = min(kCols, N - j0);
+  const bool first = i0 == 0;
+  const f32x4v acc = dw_tile(s, x, slots, d, i0, ni, j0, nc, B, first ? bsum_lds : nullptr);
+  const float omb1 = opt ? 1.0f - opt->beta1 : 0.0f, omb2 = opt ? 1.0f - opt->beta2 : 0.0f;
+  const float eps = opt ? opt->eps : 0.0f;
+  const int j = out_col();
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = out_row(r);
+    if (i < ni && j < nc) {
+      const int e = w + (i0 + i) * N + j0 + j;
+      stc(grad + e, acc[r]);
+      if (adam) adam_one(*adam, acc[r], e, omb1, omb2, eps, target, tau);
+    }
+  }
+  if (first) {
+    __syncthreads();
+    if (threadIdx.x < nc) {
+      const int e = b + j0 + threadIdx.x;
+      const float g = bsum_lds[threadIdx.x];
+      stc(grad + e, g);
+      if (adam) adam_one(*adam, g, e, omb1, omb2, eps, target, tau);
+    }
+  }
+}
+
+// ---- the grid barrier ----
+struct Sync {
+  unsigned* cnt;
+  unsigned* abort_w;
+  unsigned base, G, n, epoch;
+  int* status;
+};
+
+XA_DEV bool grid_sync(Sync& y, int& lds_flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  y.n += 1;
+  if (threadIdx.x == 0) {
+    __hip_atomic_fetch_add((gu32*)y.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned target = y.base + y.n * y.G;
+    int ok = 1;
+    const uint64_t t0 = wall_clock64();
+    for (unsigned it = 0;; ++it) {
+      const unsigned c = __hip_atomic_load((gu32*)y.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((int)(c - target) >= 0) break;  // wrap-safe: the counter only grows
+      if ((it & 15u) == 15u) {
+        if (__hip_atomic_load((gu32*)y.abort_w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+            y.epoch) {
+          ok = 0;
+          break;
+        }
+        if (wall_clock64() - t0 > kSpinTicks) {
+          __hip_atomic_store((gu32*)y.abort_w, y.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (y.status)
+            __hip_atomic_store((gu32*)y.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ok = 0;
+          break;
+        }
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    lds_flag = ok;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  __syncthreads();
+  return lds_flag != 0;
+}
+
+// workspace: control words, then the activations / gradients of the step (floats)
+struct Ws {
+  unsigned* cnt;      // barrier counter (monotonic)
+  unsigned* base;     // the counter value at the start of the next launch
+  unsigned* abort_w;  // the epoch of a launch that timed out
+  unsigned* epoch;    // launches so far
+  float* h1[6];       // per network slot: target actor, critic 1, critic 2, actor, target
+  float* h2[6];       // critic 1, target critic 2 (slot 6 = critic 1 on [s, pi(s)])
+  float* q1;          // critic 1 on [s, pi(s)]: h1
+  float* q2;          //                         h2
+  float* ta;          // a' [B][A] (smoothed target action)
+  float* pa;          // pi(s) [B][A]
+  float* v1;          // critic values [B]
+  float* v2;
+  float* dh1[2];      // critics' dH1 [B][H1]
+  float* dq1;         // dH1 of -mean Q [B][H1]
+  float* dz3;         // actor output gradient [B][A]
+  float* dh1a;        // actor dH1 [B][H1]
+  size_t total;
+};
+
+__host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+__host__ __device__ inline Ws carve(void* base_p, int B, int H1, int H2, int A) {
+  Ws w;
+  char* c = (char*)base_p;
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    char* q = c + off;
+    off = align_up(off + bytes, 256);
+    return q;
+  };
+  unsigned* ctl = (unsigned*)take(1024);
+  w.cnt = ctl;
+  w.base = ctl + 64;
+  w.abort_w = ctl + 128;
+  w.epoch = ctl + 192;
+  for (int i = 0; i < 6; ++i) {
+    w.h1[i] = (float*)take((size_t)B * H1 * 4);
+    w.h2[i] = (float*)take((size_t)B * H2 * 4);
+  }
+  w.q1 = (float*)take((size_t)B * H1 * 4);
+  w.q2 = (float*)take((size_t)B * H2 * 4);
+  w.ta = (float*)take((size_t)B * A * 4);
+  w.pa = (float*)take((size_t)B * A * 4);
+  w.v1 = (float*)take((size_t)B * 4);
+  w.v2 = (float*)take((size_t)B * 4);
+  w.dh1[0] = (float*)take((size_t)B * H1 * 4);
+  w.dh1[1] = (float*)take((size_t)B * H1 * 4);
+  w.dq1 = (float*)take((size_t)B * H1 * 4);
+  w.dz3 = (float*)take((size_t)B * A * 4);
+  w.dh1a = (float*)take((size_t)B * H1 * 4);
+  w.total = off;
+  return w;
+}
+
+enum { N_TA = 0, N_C1 = 1, N_C2 = 2, N_AC = 3, N_TC1 = 4, N_TC2 = 5 };
+
+__global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ int s_flag;
+  __shared__ float s_bsum[kCols];
+  const Lds s{smem, smem + kRows * kLd, smem + (kRows + kCols) * kLd};
+  const int G = gridDim.x, b = blockIdx.x, tid = threadIdx.x;
+  const int B = p.batch, S = p.obs_dim, A = p.act_dim, H1 = p.h1, H2 = p.h2;
+  const int C = S + A;
+  const bool twin = p.twin != 0, pol = p.actor_update != 0;
+  const Ws ws = carve(p.workspace, B, H1, H2, A);
+  Sync y;
+  y.cnt = ws.cnt;
+  y.abort_w = ws.abort_w;
+  y.base = *ws.base;
+  y.epoch = *ws.epoch + 1u;
+  y.G = (unsigned)G;
+  y.n = 0;
+  y.status = p.status;
+  // networks (the Adam step sizes from the step counters as the launch finds them)
+  const Net ta = make_net(p.target_actor, S, H1, H2, A, false);
+  const Net c1 = make_net(p.critic1, C, H1, H2, 1, true);
+  const Net c2 = make_net(twin ? p.critic2 : p.critic1, C, H1, H2, 1, twin);
+  const Net ac = make_net(p.actor, S, H1, H2, A, pol);
+  const Net tc1 = make_net(p.target_critic1, C, H1, H2, 1, false);
+  const Net tc2 = make_net(twin ? p.target_critic2 : p.target_critic1, C, H1, H2, 1, false);
+  const int64_t* slots = p.slots;
+  const int RT = (B + kRows - 1) / kRows;
+  const int CT1 = (H1 + kCols - 1) / kCols, CT2 = (H2 + kCols - 1) / kCols;
+  const float* rs = p.ring_states;
+  const float* rn = p.ring_new_states;
+  const float* ra = p.ring_actions;
+
+  // the sampled batch for the caller (concat_buffer_samples' arrays), from the last block
+  if (b == G - 1) {
+    for (int e = tid; e < B * S; e += 256) {
+      const int r = e / S, k = e - r * S;
+      p.out_s[e] = rs[slots[r] * S + k];
+      p.out_s2[e] = rn[slots[r] * S + k];
+    }
+    for (int e = tid; e < B * A; e += 256) {
+      const int r = e / A, k = e - r * A;
+      p.out_a[e] = ra[slots[r] * A + k];
+    }
+    for (int r = tid; r < B; r += 256) {
+      p.out_r[r] = p.ring_rewards[slots[r]];
+      p.out_d[r] = p.ring_dones[slots[r]];
+    }
+  }
+
+  // ---- P1 / P2: L1 and L2 forward of the target actor, the critics (and the actor) ----
+  // the networks of P1 - P3: target actor, critic 1, [critic 2], [actor]
+  const int nn = 2 + (twin ? 1 : 0) + (pol ? 1 : 0);
+  auto net_id = [&](int t) { return t < 2 ? t : (t == 2 && twin) ? N_C2 : N_AC; };
+  auto net_of = [&](int id) -> const Net& {
+    return id == N_TA ? ta : id == N_C1 ? c1 : id == N_C2 ? c2 : id == N_AC ? ac
+                                             : id == N_TC1 ? tc1 : tc2;
+  };
+  auto in_of = [&](int id) -> XSrc {
+    if (id == N_TA) return xsrc(rn, S, S, true, false);            // s'
+    if (id == N_AC) return xsrc(rs, S, S, true, false);            // s
+    return xcat(xsrc(rs, S, S, true, false), ra, A, A, true, false);  // [s, a]
+  };
+  for (int layer = 1; layer <= 2; ++layer) {
+    const int CT = layer == 1 ? CT1 : CT2, per = RT * CT;
+    for (int j = b; j < nn * per; j += G) {
+      const int id = net_id(j / per), rem = j % per, rt = rem / CT, ct = rem % CT;
+      const Net& n = net_of(id);
+      if (layer == 1)
+        fwd_job(s, in_of(id), slots, rt * kRows, B, n.th + n.w1, n.th + n.b1, n.in, H1, ct * kCols,
+                ACT_RELU, ws.h1[id]);
+      else
+        fwd_job(s, xsrc(ws.h1[id], H1, H1, false, true), slots, rt * kRows, B, n.th + n.w2,
+                n.th + n.b2, H1, H2, ct * kCols, ACT_RELU, ws.h2[id]);
+      __syncthreads();
+    }
+    if (!grid_sync(y, s_flag)) return;
+  }
+
+  // ---- P3: L3 (target actor + smoothing, critic values, actor pi(s)) ----
+  {
+    const uint64_t ctr = p.rng_counter ? *p.rng_counter : 0ull;
+    for (int j = b; j < nn * RT; j += G) {
+      const int id = net_id(j / RT), rt = j % RT, r0 = rt * kRows;
+      const Net& n = net_of(id);
+      const int N = n.out;
+      const f32x4v acc = fwd_tile(s, xsrc(ws.h2[id], H2, H2, false, true), slots, r0, B,
+                                  n.th + n.w3, n.th + n.b3, H2, N, 0);
+      const int c = out_col();
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = r0 + out_row(r);
+        if (row >= B || c >= N) continue;
+        if (id == N_TA) {
+          float a = xa_tanhf(acc[r]);
+          if (p.smooth) {
+            float nz = 0.0f;
+            if (p.noise_sigma != 0.0f) {
+              nz = philox_normal((uint32_t)row, (uint32_t)c, ctr, p.seed) * p.noise_sigma;
+              nz = fminf(fmaxf(nz, -p.noise_clip), p.noise_clip);
+            }
+            if (p.noise_out) p.noise_out[row * A + c] = nz;
+            a = fminf(fmaxf(a + nz, -1.0f), 1.0f);
+          }
+          stc(ws.ta + row * A + c, a);
+        } else if (id == N_AC) {
+          stc(ws.pa + row * A + c, xa_tanhf(acc[r]));
+        } else {
+          stc((id == N_C1 ? ws.v1 : ws.v2) + row, acc[r]);
+        }
+      }
+      __syncthreads();
+    }
+    if (!grid_sync(y, s_flag)) return;
+  }
+
+  // ---- P4 / P5: target critics L1 on [s', a'], L2 ----
+  const int nt = twin ? 2 : 1;
+  for (int layer = 1; layer <= 2; ++layer) {
+    const int CT = layer == 1 ? CT1 : CT2, per = RT * CT;
+    for (int j = b; j < nt * per; j += G) {
+      const int id = N_TC1 + j / per, rem = j % per, rt = rem / CT, ct = rem % CT;
+      const Net& n = net_of(id);
+      if (layer == 1)
+        fwd_job(s, xcat(xsrc(rn, S, S, true, false), ws.ta, A, A, false, true), slots,
+                rt * kRows, B, n.th + n.w1, n.th + n.b1, C, H1, ct * kCols, ACT_RELU, ws.h1[id]);
+      else
+        fwd_job(s, xsrc(ws.h1[id], H1, H1, false, true), slots, rt * kRows, B, n.th + n.w2,
+                n.th + n.b2, H1, H2, ct * kCols, ACT_RELU, ws.h2[id]);
+      __syncthreads();
+    }
+    if (!grid_sync(y, s_flag)) return;
+  }
+
+  // ---- P6: target values and the TD head ----
+  for (int j = b; j < RT; j += G) {
+    const int r0 = j * kRows;
+    const f32x4v t1 = fwd_tile(s, xsrc(ws.h2[N_TC1], H2, H2, false, true), slots, r0, B,
+                               tc1.th + tc1.w3, tc1.th + tc1.b3, H2, 1, 0);
+    __syncthreads();
+    f32x4v t2 = t1;
+    if (twin) {
+      t2 = fwd_tile(s, xsrc(ws.h2[N_TC2], H2, H2, false, true), slots, r0, B, tc2.th + tc2.w3,
+                    tc2.th + tc2.b3, H2, 1, 0);
+    }
+    if (out_col() == 0) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = r0 + out_row(r);
+        if (row >= B) continue;
+        const float tv = twin ? fminf(t1[r], t2[r]) : t1[r];
+        const int64_t sl = slots[row];
+        const float yv = p.ring_rewards[sl] + ((1.0f - p.ring_dones[sl]) * p.gamma) * tv;
+        const float hd = p.huber_delta;
+        auto term = [hd](float e, float& d) {
+          if (hd > 0.0f) {
+            d = fminf(fmaxf(e, -hd), hd);
+            const float ae = fabsf(e);
+            return ae <= hd ? 0.5f * (e * e) : hd * (ae - 0.5f * hd);
+          }
+          d = 2.0f * e;
+          return e * e;
+        };
+        float d1;
+        float l = term(ldc(ws.v1 + row) - yv, d1);
+        stc(p.dv1 + row, d1);
+        if (twin) {
+          float d2;
+          l = l + term(ldc(ws.v2 + row) - yv, d2);
+          stc(p.dv2 + row, d2);
+        }
+        if (p.loss_out) p.loss_out[row] = l;
+      }
+    }
+    __syncthreads();
+  }
+  if (!grid_sync(y, s_flag)) return;
+
+  // ---- P7: critics backward (dW2 / db2, dH1, dW3 / db3) ----
+  {
+    const int IT1 = (H1 + kRows - 1) / kRows, IT2 = (H2 + kRows - 1) / kRows;
+    const int n_dx = RT * CT1, n_dw2 = IT1 * CT2, n_dw3 = IT2;
+    const int per = n_dx + n_dw2 + n_dw3;  // the heavy input-gradient jobs first
+    for (int j = b; j < nt * per; j += G) {
+      const int ci = j / per, q = j % per;
+      const Net& n = ci ? c2 : c1;
+      const int id = ci ? N_C2 : N_C1;
+      float* dv = ci ? p.dv2 : p.dv1;
+      float* grad = ci ? p.g_critic2 : p.g_critic1;
+      const DZ d2 = dz_h2(ws.h2[id], H2, n.th + n.w3, 1, dv, 0.0f);
+      if (q < n_dx) {
+        const int rt = q / CT1, ct = q % CT1, r0 = rt * kRows, c0 = ct * kCols;
+        const f32x4v acc = dx_tile(s, d2, r0, B, n.th + n.w2, H2, c0, min(kCols, H1 - c0));
+        const int c = c0 + out_col();
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = r0 + out_row(r);
+          if (row < B && c < H1) {
+            const float g = ldc(ws.h1[id] + row * H1 + c) > 0.0f ? acc[r] : 0.0f;
+            stc(ws.dh1[ci] + row * H1 + c, g);
+          }
+        }
+      } else if (q < n_dx + n_dw2) {
+        const int t = q - n_dx, it = t / CT2, ct = t % CT2;
+        dw_job(s, xsrc(ws.h1[id], H1, H1, false, true), slots, d2, H1, H2, it * kRows,
+               ct * kCols, B, grad, n.w2, n.b2, nullptr, nullptr, nullptr, 0.0f, s_bsum);
+      } else {
+        const int it = q - n_dx - n_dw2;
+        dw_job(s, xsrc(ws.h2[id], H2, H2, false, true), slots, dz_buf(dv, 1), H2, 1, it * kRows,
+               0, B, grad, n.w3, n.b3, nullptr, nullptr, nullptr, 0.0f, s_bsum);
+      }
+      __syncthreads();
+    }
+    if (!grid_sync(y, s_flag)) return;
+  }
+
+  // ---- P8: critics dW1 / db1 + Adam, Adam of the rest (+ Polyak on policy steps) ----
+  {
+    const int n_w1 = CT1;                       // one in-feature tile (C <= 64)
+    const int rest = c1.P - c1.w2, chunk = 4096, n_ad = (rest + chunk - 1) / chunk;
+    const int per = n_w1 + n_ad;
+    for (int j = b; j < nt * per; j += G) {
+      const int ci = j / per, q = j % per;
+      const Net& n = ci ? c2 : c1;
+      const XaTdNet& opt = ci ? p.critic2 : p.critic1;
+      float* grad = ci ? p.g_critic2 : p.g_critic1;
+      float* tgt = pol ? (ci ? p.target_critic2.theta : p.target_critic1.theta) : nullptr;
+      if (q < n_w1) {
+        dw_job(s, in_of(ci ? N_C2 : N_C1), slots, dz_buf(ws.dh1[ci], H1), C, H1, 0, q * kCols,
+               B, grad, n.w1, n.b1, &n, &opt, tgt, p.tau, s_bsum);
+      } else {
+        const int lo = n.w2 + (q - n_w1) * chunk, hi = min(n.P, lo + chunk);
+        const float omb1 = 1.0f - opt.beta1, omb2 = 1.0f - opt.beta2;
+        for (int i = lo + tid; i < hi; i += 256)
+          adam_one(n, ldc(grad + i), i, omb1, omb2, opt.eps, tgt, p.tau);
+      }
+      __syncthreads();
+    }
+  }
+
+  if (pol) {
+    if (!grid_sync(y, s_flag)) return;
+    // ---- P9 / P10: critic 1 (updated) on [s, pi(s)] ----
+    const XSrc spa = xcat(xsrc(rs, S, S, true, false), ws.pa, A, A, false, true);
+    for (int layer = 1; layer <= 2; ++layer) {
+      const int CT = layer == 1 ? CT1 : CT2;
+      for (int j = b; j < RT * CT; j += G) {
+        const int rt = j / CT, ct = j % CT;
+        if (layer == 1)
+          fwd_job(s, spa, slots, rt * kRows, B, c1.th + c1.w1, c1.th + c1.b1, C, H1, ct * kCols,
+                  ACT_RELU, ws.q1);
+        else
+          fwd_job(s, xsrc(ws.q1, H1, H1, false, true), slots, rt * kRows, B, c1.th + c1.w2,
+                  c1.th + c1.b2, H1, H2, ct * kCols, ACT_RELU, ws.q2);
+        __syncthreads();
+      }
+      if (!grid_sync(y, s_flag)) return;
+    }
+    // ---- P11: dH1 of -mean Q (dQ / dv = -1 / B per row) ----
+    const DZ dq2 = dz_h2(ws.q2, H2, c1.th + c1.w3, 1, nullptr, -1.0f / (float)B);
+    for (int j = b; j < RT * CT1; j += G) {
+      const int rt = j / CT1, ct = j % CT1, r0 = rt * kRows, c0 = ct * kCols;
+      const f32x4v acc = dx_tile(s, dq2, r0, B, c1.th + c1.w2, H2, c0, min(kCols, H1 - c0));
+      const int c = c0 + out_col();
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = r0 + out_row(r);
+        if (row < B && c < H1)
+          stc(ws.dq1 + row * H1 + c, ldc(ws.q1 + row * H1 + c) > 0.0f ? acc[r] : 0.0f);
+      }
+      __syncthreads();
+    }
+    if (!grid_sync(y, s_flag)) return;
+    // ---- P12: d pi(s) = dH1 W1[S + a][:]^T, times tanh' -> the actor's output gradient ----
+    for (int j = b; j < RT; j += G) {
+      const int r0 = j * kRows;
+      const f32x4v acc = dx_tile(s, dz_buf(ws.dq1, H1), r0, B, c1.th + c1.w1, H1, S, A);
+      const int c = out_col();
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = r0 + out_row(r);
+        if (row < B && c < A) {
+          const float pv = ldc(ws.pa + row * A + c);
+          stc(ws.dz3 + row * A + c, acc[r] * (1.0f - pv * pv));
+        }
+      }
+      __syncthreads();
+    }
+    if (!grid_sync(y, s_flag)) return;
+    // ---- P13: actor backward (dW2 / db2, dH1, dW3 / db3) ----
+    {
+      const int IT1 = (H1 + kRows - 1) / kRows, IT2 = (H2 + kRows - 1) / kRows;
+      const int n_dx = RT * CT1, n_dw2 = IT1 * CT2, n_dw3 = IT2;
+      const DZ d2 = dz_h2(ws.h2[N_AC], H2, ac.th + ac.w3, A, ws.dz3, 0.0f);
+      for (int j = b; j < n_dx + n_dw2 + n_dw3; j += G) {
+        if (j < n_dx) {
+          const int rt = j / CT1, ct = j % CT1, r0 = rt * kRows, c0 = ct * kCols;
+          const f32x4v acc = dx_tile(s, d2, r0, B, ac.th + ac.w2, H2, c0, min(kCols, H1 - c0));
+          const int c = c0 + out_col();
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = r0 + out_row(r);
+            if (row < B && c < H1)
+              stc(ws.dh1a + row * H1 + c,
+                  ldc(ws.h1[N_AC] + row * H1 + c) > 0.0f ? acc[r] : 0.0f);
+          }
+        } else if (j < n_dx + n_dw2) {
+          const int t = j - n_dx, it = t / CT2, ct = t % CT2;
+          dw_job(s, xsrc(ws.h1[N_AC], H1, H1, false, true), slots, d2, H1, H2, it * kRows,
+                 ct * kCols, B, p.g_actor, ac.w2, ac.b2, nullptr, nullptr, nullptr, 0.0f, s_bsum);
+        } else {
+          const int it = j - n_dx - n_dw2;
+          dw_job(s, xsrc(ws.h2[N_AC], H2, H2, false, true), slots, dz_buf(ws.dz3, A), H2, A,
+                 it * kRows, 0, B, p.g_actor, ac.w3, ac.b3, nullptr, nullptr, nullptr, 0.0f,
+                 s_bsum);
+        }
+        __syncthreads();
+      }
+      if (!grid_sync(y, s_flag)) return;
+    }
+    // ---- P14: actor dW1 / db1 + Adam + Polyak, Adam + Polyak of the rest ----
+    {
+      const int rest = ac.P - ac.w2, chunk = 4096, n_ad = (rest + chunk - 1) / chunk;
+      for (int j = b; j < CT1 + n_ad; j += G) {
+        if (j < CT1) {
+          dw_job(s, xsrc(rs, S, S, true, false), slots, dz_buf(ws.dh1a, H1), S, H1, 0,
+                 j * kCols, B, p.g_actor, ac.w1, ac.b1, &ac, &p.actor, p.target_actor.theta,
+                 p.tau, s_bsum);
+        } else {
+          const int lo = ac.w2 + (j - CT1) * chunk, hi = min(ac.P, lo + chunk);
+          const float omb1 = 1.0f - p.actor.beta1, omb2 = 1.0f - p.actor.beta2;
+          for (int i = lo + tid; i < hi; i += 256)
+            adam_one(ac, ldc(p.g_actor + i), i, omb1, omb2, p.actor.eps, p.target_actor.theta,
+                     p.tau);
+        }
+        __syncthreads();
+      }
+    }
+  }
+
+  // the step counters, the noise counter and the next launch's barrier base: every block
+  // read them before its first barrier, which block 0 has passed
+  if (b == 0 && tid == 0) {
+    *p.critic1.step += 1;
+    if (twin) *p.critic2.step += 1;
+    if (pol) *p.actor.step += 1;
+    if (p.smooth && p.rng_counter) *p.rng_counter += 1ull;
+    *ws.base = y.base + y.n * y.G;
+    *ws.epoch = y.epoch;
+  }
+}
+
+}  // namespace
+
+extern "C" size_t xa_td3_update_workspace_bytes(int batch, int obs_dim, int act_dim, int h1,
+                                                int h2) {
+  (void)obs_dim;
+  return carve(nullptr, batch, h1, h2, act_dim).total;
+}
+
+extern "C" int xa_td3_update(const XaTd3UpdateArgs* p, void* stream) {
+  XA_CHECK_ARG(p != nullptr, "xa_td3_update: null args");
+  const XaTd3UpdateArgs& a = *p;
+  XA_CHECK_ARG(a.batch > 0 && a.obs_dim > 0 && a.act_dim > 0 && a.act_dim <= 16 && a.h1 > 0 &&
+                   a.h2 > 0,
+               "xa_td3_update: bad sizes");
+  XA_CHECK_ARG(a.batch <= kMaxK && a.h1 <= kMaxK && a.h2 <= kMaxK &&
+                   a.obs_dim + a.act_dim <= 64 && a.h2 * a.act_dim <= 2048 &&
+                   a.batch * a.act_dim <= 1024,
+               "xa_td3_update: sizes beyond the kernel's tiles (batch, h1, h2 <= %d; obs + act "
+               "<= 64; h2 act, batch act <= 2048, 1024)",
+               kMaxK);
+  XA_CHECK_ARG(a.ring_states && a.ring_new_states && a.ring_actions && a.ring_rewards &&
+                   a.ring_dones && a.slots && a.workspace && a.dv1 && a.g_critic1 &&
+                   (!a.twin || (a.dv2 && a.g_critic2 && a.critic2.theta && a.target_critic2.theta)) &&
+                   (!a.actor_update || a.g_actor) && a.out_s && a.out_a && a.out_r && a.out_d &&
+                   a.out_s2,
+               "xa_td3_update: missing buffers");
+  XA_CHECK_ARG(a.workspace_bytes >= carve(nullptr, a.batch, a.h1, a.h2, a.act_dim).total,
+               "xa_td3_update: workspace too small");
+  int cus = 256, dev = 0;
+  if (hipGetDevice(&dev) == hipSuccess)
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const int G = a.n_blocks > 0 ? min(a.n_blocks, cus) : min(128, cus);
+  const size_t lds = sizeof(float) * ((size_t)(kRows + kCols) * kLd + kAux);
+  hipLaunchKernelGGL(td3_update_kernel, dim3(G), dim3(256), lds, (hipStream_t)stream, a);
+  XA_CHECK_LAUNCH("xa_td3_update");
+  return 0;
+}

@@ -168,14 +168,119 @@ class DDPG(OffPolicy):
 
     def update_weights(self, gradient_steps):
         """ddpg/agent.py:129-147. The sample indices come from the host RNG exactly as
-        before; the device work of a gradient step (gather, critic update; actor update and
-        Polyak sync) is captured once per phase and replayed as hipGraphs, since at batch
-        sizes like 64 its ~40 small launches are launch-bound when issued from Python."""
+        before. The device work of a gradient step (gather, critic update; actor update and
+        Polyak sync) is ONE persistent launch (xa_td3_update, csrc/td3_update.hip) when the
+        models are the 3-layer .cfg MLPs and the run is one process; otherwise the layer
+        executor's ~40-90 launches, captured once per phase and replayed as hipGraphs."""
+        fused = self._fused_args()
         for gradient_step in range(int(gradient_steps)):
             self.replay.upload_slots(self.replay.sample_slots())
+            policy = gradient_step % self.policy_delay == 0
+            if fused is not None:
+                self._run_phase('fused_actor' if policy else 'fused',
+                                lambda p=policy: self._fused_step(p))
+                continue
             self._run_phase('critic', self._critic_phase)
-            if gradient_step % self.policy_delay == 0:
+            if policy:
                 self._run_phase('actor', self._actor_phase)
+
+    # ---- the fused gradient step (xa_td3_update) -------------------------------------
+    def _fused_ok(self):
+        import os
+        if os.environ.get('XA_TD3_FUSED', '1') == '0' or self.distributed:
+            return False
+        if self.replay.obs_t != torch.float32 or self.replay.act_t != torch.float32:
+            return False
+        if len(self.envs.obs_shape) != 1:
+            return False
+        models = [self.actor, self.critic] + ([self.critic2] if hasattr(self, 'critic2') else [])
+        want = {id(self.actor): ['relu', 'relu', 'tanh']}
+        h = None
+        for m in models:
+            ls = m.layers
+            if len(ls) != 3 or any(l.kind != 'dense' for l in ls) or list(m.outputs) != [2]:
+                return False
+            acts = [l.activation or 'linear' for l in ls]
+            if acts != want.get(id(m), ['relu', 'relu', 'linear']):
+                return False
+            if any(l.input_index != i - 1 for i, l in enumerate(ls)):
+                return False
+            dims = (ls[0].units, ls[1].units)
+            if h is not None and dims != h:
+                return False
+            h = dims
+        S, A = self.S, self.A
+        if self.actor.layers[2].units != A or self.critic.layers[2].units != 1:
+            return False
+        if self.actor.layers[0].in_features != S or self.critic.layers[0].in_features != S + A:
+            return False
+        B = self.batch_size
+        return max(B, h[0], h[1]) <= 416 and S + A <= 64 and h[1] * A <= 2048 and B * A <= 1024
+
+    def _fused_args(self):
+        """The launch arguments of xa_td3_update (built once), or None when the fused step
+        does not apply (data parallel: the gradients are all-reduced between the backward
+        and Adam; other model shapes)."""
+        if '_fused' in self.__dict__:
+            return self.__dict__['_fused']
+        from xagents_amd import _lib
+        from xagents_amd._lib import XaTd3UpdateArgs
+        fused = None
+        if self._fused_ok():
+            a = XaTd3UpdateArgs()
+            B, S, A = self.batch_size, self.S, self.A
+            H1, H2 = self.actor.layers[0].units, self.actor.layers[1].units
+            a.batch, a.obs_dim, a.act_dim, a.h1, a.h2 = B, S, A, H1, H2
+            twin = hasattr(self, 'critic2')
+            a.twin = a.smooth = int(twin)
+            a.gamma = kernels._f32(self.gamma)
+            a.tau = kernels._f32(self.tau)
+            a.noise_sigma = kernels._f32(getattr(self, 'policy_noise_coef', 0.0))
+            a.noise_clip = kernels._f32(getattr(self, 'noise_clip', 0.0))
+            a.huber_delta = kernels._f32(self.huber_delta or 0.0)
+            r = self.replay
+            a.ring_states, a.ring_new_states = r.states.data_ptr(), r.new_states.data_ptr()
+            a.ring_actions = r.actions.data_ptr()
+            a.ring_rewards, a.ring_dones = r.rewards.data_ptr(), r.dones.data_ptr()
+            a.slots = r.slots.data_ptr()
+            a.rng_counter, a.seed = self.rng_counter.data_ptr(), self.rng_seed
+
+            def net(model, target=False):
+                n = type(a.actor)()
+                n.theta = model.theta.data_ptr()
+                if not target:
+                    opt = model.optimizer
+                    n.m, n.v, n.step = opt.m.data_ptr(), opt.v.data_ptr(), opt.iterations.data_ptr()
+                    n.lr, n.beta1 = opt.learning_rate, opt.beta_1
+                    n.beta2, n.eps = opt.beta_2, opt.epsilon
+                return n
+            a.actor, a.critic1 = net(self.actor), net(self.critic)
+            a.target_actor, a.target_critic1 = net(self.target_actor, True), net(self.target_critic, True)
+            if twin:
+                a.critic2, a.target_critic2 = net(self.critic2), net(self.target_critic2, True)
+            a.out_s, a.out_a, a.out_r = self.s.data_ptr(), self.a.data_ptr(), self.r.data_ptr()
+            a.out_d, a.out_s2 = self.d.data_ptr(), self.s2.data_ptr()
+            a.noise_out = self.noise.data_ptr()
+            a.dv1, a.dv2 = self.dv1.data_ptr(), self.dv2.data_ptr()
+            a.loss_out = self.critic_loss.data_ptr()
+            a.g_actor, a.g_critic1 = self.g_actor.data_ptr(), self.g_critic.data_ptr()
+            if twin:
+                a.g_critic2 = self.g_critic2.data_ptr()
+            nbytes = _lib.load().xa_td3_update_workspace_bytes(B, S, A, H1, H2)
+            self._fused_ws = torch.zeros(nbytes, dtype=torch.uint8, device=self.device)
+            self._fused_status = torch.zeros(1, dtype=torch.int32, device=self.device)
+            a.workspace, a.workspace_bytes = self._fused_ws.data_ptr(), nbytes
+            import os
+            a.n_blocks = int(os.environ.get('XA_TD3_BLOCKS', '0'))
+            a.status = self._fused_status.data_ptr()
+            fused = a
+        self.__dict__['_fused'] = fused
+        return fused
+
+    def _fused_step(self, policy):
+        a = self._fused
+        a.actor_update = int(policy)
+        call('xa_td3_update', ctypes.byref(a), stream())
 
     def _critic_phase(self):
         self.replay.gather(self.replay.slots, self.s, self.a, self.r, self.d, self.s2)
@@ -207,6 +312,7 @@ class DDPG(OffPolicy):
     def _on_lr_change(self):
         self.__dict__['_graphs'] = {}  # the learning rates are baked into the launches
         self.__dict__['_warm'] = set()
+        self.__dict__.pop('_fused', None)  # (and into the fused step's arguments)
 
     def _step_phase(self):
         """get_step_actions + one xa_replay_env_step (ring append) writing the step's
