@@ -307,6 +307,34 @@ def dominant_gemm_roofline(executors, step):
                     f'step is launch-bound at batch 64)'}
 
 
+def fused_td3_roofline(agent, launches=10):
+    """Roofline of the fused TD3 gradient step (xa_td3_update, one persistent launch per
+    gradient step): HIP event pairs on the launch stream around `launches` eager launches
+    (gradient_steps 1: every step updates the actor)."""
+    import numpy as np
+    import torch
+    agent.fused_timing = []
+    try:
+        for _ in range(launches):
+            agent.update_weights(1)
+        torch.cuda.synchronize()
+        rows = list(agent.fused_timing)
+    finally:
+        agent.fused_timing = None
+    ms = float(np.mean([e0.elapsed_time(e1) for _, e0, e1 in rows]))
+    pol = sum(p for p, _, _ in rows) / len(rows)
+    flops = pol * agent.fused_step_flops(True) + (1 - pol) * agent.fused_step_flops(False)
+    tf = flops / (ms * 1e-3) / 1e12
+    return {'kernel': 'xa_td3_update (one persistent launch per gradient step: twin critics, '
+                      'TD head, backward, Adam, actor update, Polyak)', 'bound': 'mfma',
+            'achieved': round(tf, 4), 'peak': F32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
+            'frac': round(tf / F32_MFMA_PEAK_TFLOPS, 5), 'traffic': None,
+            'launch_ms': round(ms, 5), 'flops_per_launch': int(flops),
+            'note': f'2 M N K FLOP of every GEMM of the step at batch {agent.batch_size}, '
+                    f'mean of {len(rows)} event-timed launches; latency-bound (grid barriers '
+                    f'between 8 / 14 phases)'}
+
+
 def bench_offpolicy_and_cnn(args):
     """Secondary configs (TRPO, ACER); one JSON line each."""
     world, rank, device = _dist_setup()
@@ -442,10 +470,13 @@ def run_secondary(args, config, world, rank, device, steps, warmup, cpu_seconds,
         # one eager gradient step for the event pairs (the timed steps replay hipGraphs,
         # which carry no events)
         agent.use_graph = False
-        rl = dominant_gemm_roofline(
-            [agent.ex_actor, agent.ex_target_actor, agent.ex_critic, agent.ex_critic2,
-             agent.ex_target_critic, agent.ex_target_critic2, agent.ex_critic_pi],
-            lambda: agent.update_weights(1))
+        if agent._fused_args() is not None:
+            rl = fused_td3_roofline(agent)
+        else:
+            rl = dominant_gemm_roofline(
+                [agent.ex_actor, agent.ex_target_actor, agent.ex_critic, agent.ex_critic2,
+                 agent.ex_target_critic, agent.ex_target_critic2, agent.ex_critic_pi],
+                lambda: agent.update_weights(1))
         agent.use_graph = True
         if rl:
             line['roofline'] = rl

@@ -16,7 +16,10 @@ def main():
     from xagents_amd.layers import gemm
     lib = _lib.load()
     dev = torch.device('cuda')
-    N, K = 37632, 512
+    import os
+    # XA_SMALLM_K: the depth (128 / 256 / 512 reach the small-M kernel; no shipped cfg has a
+    # 128-unit dense layer, ADVICE r03: measure the K = 128 sub-row padding)
+    N, K = 37632, int(os.environ.get('XA_SMALLM_K', '512'))
     for M in [int(a) for a in sys.argv[1:]] or [64, 128, 336]:
         a = torch.randn(M, K, device=dev)
         w = torch.randn(N, K, device=dev) * 0.01

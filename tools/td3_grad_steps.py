@@ -35,6 +35,26 @@ def main():
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / n_steps
     print(f'TD3 gradient step: {dt * 1e3:.4f} ms ({n_steps} steps, graph replay)', flush=True)
+    if agent._fused_args() is not None:
+        # per-phase barrier times of the fused launch (block 0's 100 MHz wall clock, the
+        # workspace control area's trace words: [0] start, [i] barrier i done, [15] end)
+        import numpy as np
+        rows = []
+        agent.use_graph = False
+        for _ in range(20):
+            agent.update_weights(1)
+            torch.cuda.synchronize()
+            tr = agent._fused_ws[896:1024].cpu().numpy().view(np.uint64).astype(np.int64)
+            rows.append(tr)
+        diffs = []
+        for tr in rows:
+            n = int(np.count_nonzero(tr[1:15] > tr[0]))
+            marks = np.asarray(list(tr[:n + 1]) + [tr[15]], np.float64)
+            diffs.append(np.diff(marks) / 100.0)  # 100 MHz ticks -> us
+        d = np.median(np.stack(diffs), 0)
+        print('fused phases (us, block 0, median of 20 eager launches): ' +
+              ' '.join(f'P{i + 1} {v:.1f}' for i, v in enumerate(d)) + f' | total {d.sum():.1f}',
+              flush=True)
 
 
 if __name__ == '__main__':

@@ -81,6 +81,12 @@ XA_DEV float4 ld4c(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
   const f32x4v v = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, kAuxSc1);
   return make_float4(v[0], v[1], v[2], v[3]);
 }
+// 16 bytes through the cache hierarchy (parameters no phase of this launch has written yet)
+XA_DEV float4 ld4p(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
+  const f32x4v v = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0);
+  return make_float4(v[0], v[1], v[2], v[3]);
+}
+XA_DEV float ldw(const float* p, bool coh) { return coh ? ldc(p) : *p; }
 
 XA_DEV float philox_normal(uint32_t i, uint32_t j, uint64_t ctr, uint64_t seed) {
   // the same draw as xa_noisy_actions (offpolicy.hip)
@@ -205,6 +211,10 @@ struct Lds {
   float* B;    // [16][kLd]
   float* aux;  // [kAux]
 };
+// the dynamic LDS of the launch (named at file scope so the out-of-line job functions
+// address it directly as LDS)
+extern __shared__ __attribute__((aligned(16))) float td3_smem[];
+XA_DEV Lds lds() { return Lds{td3_smem, td3_smem + kRows * kLd, td3_smem + (kRows + kCols) * kLd}; }
 
 XA_DEV int pad16(int k) { return (k + 15) & ~15; }
 
@@ -331,15 +341,45 @@ XA_DEV void stage_a_dz(const Lds& s, const DZ& d, int r0, int nrows, int K) {
   }
 }
 
-// B^T[j][k] = W[k][c0 + j] (forward: W row-major [K][N]; j < nc valid columns)
-XA_DEV void stage_b_fwd(const Lds& s, const float* W, int N, int c0, int nc, int K) {
-  const int Kp = pad16(K), total = kCols * Kp;
+// B^T[j][k] = W[k][c0 + j] (forward: W row-major [K][N]; j < nc valid columns); coh: W was
+// written earlier in this launch (sc1 loads), else plain loads
+XA_DEV void stage_b_fwd(const Lds& s, const float* W, int N, int c0, int nc, int K, bool coh) {
+  const int Kp = pad16(K);
+  if ((N & 3) == 0 && (c0 & 3) == 0) {
+    // four float4 per row k (lanes t = e & 3), each wholly inside or outside [c0, c0 + nc)
+    const __amdgpu_buffer_rsrc_t r = rsrc(W);
+    const int total = 4 * Kp;
+    for (int e0 = threadIdx.x; e0 < total; e0 += 256 * kU) {
+      float4 v[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int e = e0 + 256 * u, k = e >> 2, t = e & 3;
+        v[u] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (e < total && 4 * t < nc && k < K) {
+          const uint32_t off = (uint32_t)(((int64_t)k * N + c0 + 4 * t) * 4);
+          v[u] = coh ? ld4c(r, off) : ld4p(r, off);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int e = e0 + 256 * u, k = e >> 2, t = e & 3;
+        if (e < total) {
+          s.B[(4 * t) * kLd + k] = v[u].x;
+          s.B[(4 * t + 1) * kLd + k] = v[u].y;
+          s.B[(4 * t + 2) * kLd + k] = v[u].z;
+          s.B[(4 * t + 3) * kLd + k] = v[u].w;
+        }
+      }
+    }
+    return;
+  }
+  const int total = kCols * Kp;
   for (int e0 = threadIdx.x; e0 < total; e0 += 256 * kU) {
     float v[kU];
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
       const int e = e0 + 256 * u, k = e >> 4, j = e & 15;
-      v[u] = (e < total && j < nc && k < K) ? ldc(W + (int64_t)k * N + c0 + j) : 0.0f;
+      v[u] = (e < total && j < nc && k < K) ? ldw(W + (int64_t)k * N + c0 + j, coh) : 0.0f;
     }
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
@@ -350,14 +390,37 @@ XA_DEV void stage_b_fwd(const Lds& s, const float* W, int N, int c0, int nc, int
 }
 
 // B^T[j][k] = W[c0 + j][k] (input gradient dZ W^T: W row-major [in][K])
-XA_DEV void stage_b_rows(const Lds& s, const float* W, int K, int c0, int nc) {
-  const int Kp = pad16(K), total = kCols * Kp;
+XA_DEV void stage_b_rows(const Lds& s, const float* W, int K, int c0, int nc, bool coh) {
+  const int Kp = pad16(K);
+  if ((K & 3) == 0) {
+    const __amdgpu_buffer_rsrc_t r = rsrc(W);
+    const int K4 = Kp >> 2, total = kCols * K4;
+    for (int e0 = threadIdx.x; e0 < total; e0 += 256 * kU) {
+      float4 v[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int e = e0 + 256 * u, j = e / K4, k = 4 * (e - j * K4);
+        v[u] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (e < total && j < nc && k < K) {
+          const uint32_t off = (uint32_t)(((int64_t)(c0 + j) * K + k) * 4);
+          v[u] = coh ? ld4c(r, off) : ld4p(r, off);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int e = e0 + 256 * u, j = e / K4, k = 4 * (e - j * K4);
+        if (e < total) *reinterpret_cast<float4*>(&s.B[j * kLd + k]) = v[u];
+      }
+    }
+    return;
+  }
+  const int total = kCols * Kp;
   for (int e0 = threadIdx.x; e0 < total; e0 += 256 * kU) {
     float v[kU];
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
       const int e = e0 + 256 * u, j = e / Kp, k = e - j * Kp;
-      v[u] = (e < total && j < nc && k < K) ? ldc(W + (int64_t)(c0 + j) * K + k) : 0.0f;
+      v[u] = (e < total && j < nc && k < K) ? ldw(W + (int64_t)(c0 + j) * K + k, coh) : 0.0f;
     }
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
@@ -400,24 +463,28 @@ XA_DEV float act_f(float v, int act) {
 }
 
 // forward job: out[r][c] = act(X W + b) on rows [r0, r0 + 64) x cols [c0, c0 + 16)
-XA_DEV f32x4v fwd_tile(const Lds& s, const XSrc& x, const int64_t* slots, int r0, int B,
-                       const float* W, const float* bias, int K, int N, int c0) {
+// (the tile functions are out of line: one copy each instead of one per call site)
+__device__ __noinline__ f32x4v fwd_tile(XSrc x, const int64_t* slots, int r0, int B,
+                                        const float* W, const float* bias, int K, int N, int c0,
+                                        bool coh) {
+  const Lds s = lds();
   stage_a_rows(s, x, slots, r0, min(kRows, B - r0), K);
-  stage_b_fwd(s, W, N, c0, min(kCols, N - c0), K);
+  stage_b_fwd(s, W, N, c0, min(kCols, N - c0), K, coh);
   __syncthreads();
   f32x4v acc = tile_mma(s, pad16(K));
   const int c = c0 + out_col();
   if (c < N) {
-    const float b = ldc(bias + c);
+    const float b = ldw(bias + c, coh);
 #pragma unroll
     for (int r = 0; r < 4; ++r) acc[r] = acc[r] + b;
   }
   return acc;
 }
 
-XA_DEV void fwd_job(const Lds& s, const XSrc& x, const int64_t* slots, int r0, int B,
-                    const float* W, const float* bias, int K, int N, int c0, int act, float* out) {
-  const f32x4v acc = fwd_tile(s, x, slots, r0, B, W, bias, K, N, c0);
+XA_DEV void fwd_job(const XSrc& x, const int64_t* slots, int r0, int B, const float* W,
+                    const float* bias, int K, int N, int c0, int act, float* out,
+                    bool coh = false) {
+  const f32x4v acc = fwd_tile(x, slots, r0, B, W, bias, K, N, c0, coh);
   const int c = c0 + out_col();
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
@@ -428,18 +495,20 @@ XA_DEV void fwd_job(const Lds& s, const XSrc& x, const int64_t* slots, int r0, i
 
 // input-gradient job: out[r][c] = (dZ W^T)[r][c] * gate (gate: the source layer's relu
 // output > 0), rows [r0, r0 + 64) x cols [c0, c0 + 16) of the layer input (width nin)
-XA_DEV f32x4v dx_tile(const Lds& s, const DZ& d, int r0, int B, const float* W, int K, int c0,
-                      int nc) {
+__device__ __noinline__ f32x4v dx_tile(DZ d, int r0, int B, const float* W, int K, int c0,
+                                       int nc, bool coh) {
+  const Lds s = lds();
   stage_a_dz(s, d, r0, min(kRows, B - r0), K);
-  stage_b_rows(s, W, K, c0, nc);
+  stage_b_rows(s, W, K, c0, nc, coh);
   __syncthreads();
   return tile_mma(s, pad16(K));
 }
 
 // weight-gradient tile: D[i][j] = sum_k X[k][i0 + i] dZ[k][j0 + j] (i < ni, j < nc, k < B);
 // the bias gradient sum_k dZ[k][j0 + j] (fixed k order) lands in bsum[j] when bsum != 0
-XA_DEV f32x4v dw_tile(const Lds& s, const XSrc& x, const int64_t* slots, const DZ& d, int i0,
-                      int ni, int j0, int nc, int B, float* bsum) {
+__device__ __noinline__ f32x4v dw_tile(XSrc x, const int64_t* slots, DZ d, int i0, int ni,
+                                       int j0, int nc, int B, float* bsum) {
+  const Lds s = lds();
   stage_a_trans(s, x, slots, i0, ni, B);
   stage_b_dz(s, d, j0, nc, B);
   __syncthreads();
@@ -467,12 +536,12 @@ XA_DEV void adam_one(const Net& n, float g, int i, float omb1, float omb2, float
 
 // weight-gradient job: raw gradient into grad (W [nin][N] at offset w, bias at b when the
 // tile is the first of its column), optionally the Adam step (+ Polyak) of those elements
-XA_DEV void dw_job(const Lds& s, const XSrc& x, const int64_t* slots, const DZ& d, int nin,
+XA_DEV void dw_job(const XSrc& x, const int64_t* slots, const DZ& d, int nin,
                    int N, int i0, int j0, int B, float* grad, int w, int b, const Net* adam,
                    const XaTdNet* opt, float* target, float tau, float* bsum_lds) {
   const int ni = min(kRows, nin - i0), nc = min(kCols, N - j0);
   const bool first = i0 == 0;
-  const f32x4v acc = dw_tile(s, x, slots, d, i0, ni, j0, nc, B, first ? bsum_lds : nullptr);
+  const f32x4v acc = dw_tile(x, slots, d, i0, ni, j0, nc, B, first ? bsum_lds : nullptr);
   const float omb1 = opt ? 1.0f - opt->beta1 : 0.0f, omb2 = opt ? 1.0f - opt->beta2 : 0.0f;
   const float eps = opt ? opt->eps : 0.0f;
   const int j = out_col();
@@ -502,6 +571,7 @@ struct Sync {
   unsigned* abort_w;
   unsigned base, G, n, epoch;
   int* status;
+  unsigned long long* trace;  // block 0 only: the wall clock as each barrier completes
 };
 
 XA_DEV bool grid_sync(Sync& y, int& lds_flag) {
@@ -533,6 +603,7 @@ XA_DEV bool grid_sync(Sync& y, int& lds_flag) {
       __builtin_amdgcn_s_sleep(1);
     }
     lds_flag = ok;
+    if (y.trace && y.n < 15) y.trace[y.n] = wall_clock64();
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   __syncthreads();
@@ -545,15 +616,21 @@ struct Ws {
   unsigned* base;     // the counter value at the start of the next launch
   unsigned* abort_w;  // the epoch of a launch that timed out
   unsigned* epoch;    // launches so far
-  float* h1[6];       // per network slot: target actor, critic 1, critic 2, actor, target
-  float* h2[6];       // critic 1, target critic 2 (slot 6 = critic 1 on [s, pi(s)])
+  unsigned long long* trace;  // [16] wall clock at launch start and after every barrier
+                              // (block 0; tools/td3_grad_steps.py reads it)
+  float* h1all;       // [6][B][H1] per network slot: target actor, critic 1, critic 2,
+  float* h2all;       // [6][B][H2]   actor, target critic 1, target critic 2
+  __host__ __device__ float* h1(int id) const { return h1all + (size_t)id * h1s; }
+  __host__ __device__ float* h2(int id) const { return h2all + (size_t)id * h2s; }
+  size_t h1s, h2s;
   float* q1;          // critic 1 on [s, pi(s)]: h1
   float* q2;          //                         h2
   float* ta;          // a' [B][A] (smoothed target action)
   float* pa;          // pi(s) [B][A]
   float* v1;          // critic values [B]
   float* v2;
-  float* dh1[2];      // critics' dH1 [B][H1]
+  float* dh1all;      // critics' dH1 [2][B][H1]
+  __host__ __device__ float* dh1(int c) const { return dh1all + (size_t)c * h1s; }
   float* dq1;         // dH1 of -mean Q [B][H1]
   float* dz3;         // actor output gradient [B][A]
   float* dh1a;        // actor dH1 [B][H1]
@@ -576,18 +653,18 @@ __host__ __device__ inline Ws carve(void* base_p, int B, int H1, int H2, int A) 
   w.base = ctl + 64;
   w.abort_w = ctl + 128;
   w.epoch = ctl + 192;
-  for (int i = 0; i < 6; ++i) {
-    w.h1[i] = (float*)take((size_t)B * H1 * 4);
-    w.h2[i] = (float*)take((size_t)B * H2 * 4);
-  }
+  w.trace = (unsigned long long*)(ctl + 224);
+  w.h1s = align_up((size_t)B * H1, 64);
+  w.h2s = align_up((size_t)B * H2, 64);
+  w.h1all = (float*)take(6 * w.h1s * 4);
+  w.h2all = (float*)take(6 * w.h2s * 4);
   w.q1 = (float*)take((size_t)B * H1 * 4);
   w.q2 = (float*)take((size_t)B * H2 * 4);
   w.ta = (float*)take((size_t)B * A * 4);
   w.pa = (float*)take((size_t)B * A * 4);
   w.v1 = (float*)take((size_t)B * 4);
   w.v2 = (float*)take((size_t)B * 4);
-  w.dh1[0] = (float*)take((size_t)B * H1 * 4);
-  w.dh1[1] = (float*)take((size_t)B * H1 * 4);
+  w.dh1all = (float*)take(2 * w.h1s * 4);
   w.dq1 = (float*)take((size_t)B * H1 * 4);
   w.dz3 = (float*)take((size_t)B * A * 4);
   w.dh1a = (float*)take((size_t)B * H1 * 4);
@@ -598,10 +675,8 @@ __host__ __device__ inline Ws carve(void* base_p, int B, int H1, int H2, int A) 
 enum { N_TA = 0, N_C1 = 1, N_C2 = 2, N_AC = 3, N_TC1 = 4, N_TC2 = 5 };
 
 __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
   __shared__ int s_flag;
   __shared__ float s_bsum[kCols];
-  const Lds s{smem, smem + kRows * kLd, smem + (kRows + kCols) * kLd};
   const int G = gridDim.x, b = blockIdx.x, tid = threadIdx.x;
   const int B = p.batch, S = p.obs_dim, A = p.act_dim, H1 = p.h1, H2 = p.h2;
   const int C = S + A;
@@ -615,8 +690,9 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
   y.G = (unsigned)G;
   y.n = 0;
   y.status = p.status;
+  y.trace = b == 0 ? ws.trace : nullptr;
+  if (b == 0 && tid == 0) ws.trace[0] = wall_clock64();
   // networks (the Adam step sizes from the step counters as the launch finds them)
-  const Net ta = make_net(p.target_actor, S, H1, H2, A, false);
   const Net c1 = make_net(p.critic1, C, H1, H2, 1, true);
   const Net c2 = make_net(twin ? p.critic2 : p.critic1, C, H1, H2, 1, twin);
   const Net ac = make_net(p.actor, S, H1, H2, A, pol);
@@ -650,9 +726,13 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
   // the networks of P1 - P3: target actor, critic 1, [critic 2], [actor]
   const int nn = 2 + (twin ? 1 : 0) + (pol ? 1 : 0);
   auto net_id = [&](int t) { return t < 2 ? t : (t == 2 && twin) ? N_C2 : N_AC; };
-  auto net_of = [&](int id) -> const Net& {
-    return id == N_TA ? ta : id == N_C1 ? c1 : id == N_C2 ? c2 : id == N_AC ? ac
-                                             : id == N_TC1 ? tc1 : tc2;
+  // a network's view by slot id (by value from the kernel arguments: no stack arrays)
+  auto net_of = [&](int id) -> Net {
+    const bool actor_like = id == N_TA || id == N_AC;
+    const XaTdNet& d = id == N_TA ? p.target_actor : id == N_C1 ? p.critic1
+                     : id == N_C2 ? p.critic2 : id == N_AC ? p.actor
+                     : id == N_TC1 ? p.target_critic1 : p.target_critic2;
+    return make_net(d, actor_like ? S : C, H1, H2, actor_like ? A : 1, false);
   };
   auto in_of = [&](int id) -> XSrc {
     if (id == N_TA) return xsrc(rn, S, S, true, false);            // s'
@@ -663,13 +743,13 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
     const int CT = layer == 1 ? CT1 : CT2, per = RT * CT;
     for (int j = b; j < nn * per; j += G) {
       const int id = net_id(j / per), rem = j % per, rt = rem / CT, ct = rem % CT;
-      const Net& n = net_of(id);
+      const Net n = net_of(id);
       if (layer == 1)
-        fwd_job(s, in_of(id), slots, rt * kRows, B, n.th + n.w1, n.th + n.b1, n.in, H1, ct * kCols,
-                ACT_RELU, ws.h1[id]);
+        fwd_job(in_of(id), slots, rt * kRows, B, n.th + n.w1, n.th + n.b1, n.in, H1, ct * kCols,
+                ACT_RELU, ws.h1(id));
       else
-        fwd_job(s, xsrc(ws.h1[id], H1, H1, false, true), slots, rt * kRows, B, n.th + n.w2,
-                n.th + n.b2, H1, H2, ct * kCols, ACT_RELU, ws.h2[id]);
+        fwd_job(xsrc(ws.h1(id), H1, H1, false, true), slots, rt * kRows, B, n.th + n.w2,
+                n.th + n.b2, H1, H2, ct * kCols, ACT_RELU, ws.h2(id));
       __syncthreads();
     }
     if (!grid_sync(y, s_flag)) return;
@@ -680,10 +760,10 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
     const uint64_t ctr = p.rng_counter ? *p.rng_counter : 0ull;
     for (int j = b; j < nn * RT; j += G) {
       const int id = net_id(j / RT), rt = j % RT, r0 = rt * kRows;
-      const Net& n = net_of(id);
+      const Net n = net_of(id);
       const int N = n.out;
-      const f32x4v acc = fwd_tile(s, xsrc(ws.h2[id], H2, H2, false, true), slots, r0, B,
-                                  n.th + n.w3, n.th + n.b3, H2, N, 0);
+      const f32x4v acc = fwd_tile(xsrc(ws.h2(id), H2, H2, false, true), slots, r0, B,
+                                  n.th + n.w3, n.th + n.b3, H2, N, 0, false);
       const int c = out_col();
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -718,13 +798,13 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
     const int CT = layer == 1 ? CT1 : CT2, per = RT * CT;
     for (int j = b; j < nt * per; j += G) {
       const int id = N_TC1 + j / per, rem = j % per, rt = rem / CT, ct = rem % CT;
-      const Net& n = net_of(id);
+      const Net n = net_of(id);
       if (layer == 1)
-        fwd_job(s, xcat(xsrc(rn, S, S, true, false), ws.ta, A, A, false, true), slots,
-                rt * kRows, B, n.th + n.w1, n.th + n.b1, C, H1, ct * kCols, ACT_RELU, ws.h1[id]);
+        fwd_job(xcat(xsrc(rn, S, S, true, false), ws.ta, A, A, false, true), slots,
+                rt * kRows, B, n.th + n.w1, n.th + n.b1, C, H1, ct * kCols, ACT_RELU, ws.h1(id));
       else
-        fwd_job(s, xsrc(ws.h1[id], H1, H1, false, true), slots, rt * kRows, B, n.th + n.w2,
-                n.th + n.b2, H1, H2, ct * kCols, ACT_RELU, ws.h2[id]);
+        fwd_job(xsrc(ws.h1(id), H1, H1, false, true), slots, rt * kRows, B, n.th + n.w2,
+                n.th + n.b2, H1, H2, ct * kCols, ACT_RELU, ws.h2(id));
       __syncthreads();
     }
     if (!grid_sync(y, s_flag)) return;
@@ -733,13 +813,13 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
   // ---- P6: target values and the TD head ----
   for (int j = b; j < RT; j += G) {
     const int r0 = j * kRows;
-    const f32x4v t1 = fwd_tile(s, xsrc(ws.h2[N_TC1], H2, H2, false, true), slots, r0, B,
-                               tc1.th + tc1.w3, tc1.th + tc1.b3, H2, 1, 0);
+    const f32x4v t1 = fwd_tile(xsrc(ws.h2(N_TC1), H2, H2, false, true), slots, r0, B,
+                               tc1.th + tc1.w3, tc1.th + tc1.b3, H2, 1, 0, false);
     __syncthreads();
     f32x4v t2 = t1;
     if (twin) {
-      t2 = fwd_tile(s, xsrc(ws.h2[N_TC2], H2, H2, false, true), slots, r0, B, tc2.th + tc2.w3,
-                    tc2.th + tc2.b3, H2, 1, 0);
+      t2 = fwd_tile(xsrc(ws.h2(N_TC2), H2, H2, false, true), slots, r0, B, tc2.th + tc2.w3,
+                    tc2.th + tc2.b3, H2, 1, 0, false);
     }
     if (out_col() == 0) {
 #pragma unroll
@@ -781,30 +861,30 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
     const int per = n_dx + n_dw2 + n_dw3;  // the heavy input-gradient jobs first
     for (int j = b; j < nt * per; j += G) {
       const int ci = j / per, q = j % per;
-      const Net& n = ci ? c2 : c1;
+      const Net n = ci ? c2 : c1;
       const int id = ci ? N_C2 : N_C1;
       float* dv = ci ? p.dv2 : p.dv1;
       float* grad = ci ? p.g_critic2 : p.g_critic1;
-      const DZ d2 = dz_h2(ws.h2[id], H2, n.th + n.w3, 1, dv, 0.0f);
+      const DZ d2 = dz_h2(ws.h2(id), H2, n.th + n.w3, 1, dv, 0.0f);
       if (q < n_dx) {
         const int rt = q / CT1, ct = q % CT1, r0 = rt * kRows, c0 = ct * kCols;
-        const f32x4v acc = dx_tile(s, d2, r0, B, n.th + n.w2, H2, c0, min(kCols, H1 - c0));
+        const f32x4v acc = dx_tile(d2, r0, B, n.th + n.w2, H2, c0, min(kCols, H1 - c0), false);
         const int c = c0 + out_col();
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int row = r0 + out_row(r);
           if (row < B && c < H1) {
-            const float g = ldc(ws.h1[id] + row * H1 + c) > 0.0f ? acc[r] : 0.0f;
-            stc(ws.dh1[ci] + row * H1 + c, g);
+            const float g = ldc(ws.h1(id) + row * H1 + c) > 0.0f ? acc[r] : 0.0f;
+            stc(ws.dh1(ci) + row * H1 + c, g);
           }
         }
       } else if (q < n_dx + n_dw2) {
         const int t = q - n_dx, it = t / CT2, ct = t % CT2;
-        dw_job(s, xsrc(ws.h1[id], H1, H1, false, true), slots, d2, H1, H2, it * kRows,
+        dw_job(xsrc(ws.h1(id), H1, H1, false, true), slots, d2, H1, H2, it * kRows,
                ct * kCols, B, grad, n.w2, n.b2, nullptr, nullptr, nullptr, 0.0f, s_bsum);
       } else {
         const int it = q - n_dx - n_dw2;
-        dw_job(s, xsrc(ws.h2[id], H2, H2, false, true), slots, dz_buf(dv, 1), H2, 1, it * kRows,
+        dw_job(xsrc(ws.h2(id), H2, H2, false, true), slots, dz_buf(dv, 1), H2, 1, it * kRows,
                0, B, grad, n.w3, n.b3, nullptr, nullptr, nullptr, 0.0f, s_bsum);
       }
       __syncthreads();
@@ -819,12 +899,12 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
     const int per = n_w1 + n_ad;
     for (int j = b; j < nt * per; j += G) {
       const int ci = j / per, q = j % per;
-      const Net& n = ci ? c2 : c1;
+      const Net n = ci ? c2 : c1;
       const XaTdNet& opt = ci ? p.critic2 : p.critic1;
       float* grad = ci ? p.g_critic2 : p.g_critic1;
       float* tgt = pol ? (ci ? p.target_critic2.theta : p.target_critic1.theta) : nullptr;
       if (q < n_w1) {
-        dw_job(s, in_of(ci ? N_C2 : N_C1), slots, dz_buf(ws.dh1[ci], H1), C, H1, 0, q * kCols,
+        dw_job(in_of(ci ? N_C2 : N_C1), slots, dz_buf(ws.dh1(ci), H1), C, H1, 0, q * kCols,
                B, grad, n.w1, n.b1, &n, &opt, tgt, p.tau, s_bsum);
       } else {
         const int lo = n.w2 + (q - n_w1) * chunk, hi = min(n.P, lo + chunk);
@@ -845,11 +925,11 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
       for (int j = b; j < RT * CT; j += G) {
         const int rt = j / CT, ct = j % CT;
         if (layer == 1)
-          fwd_job(s, spa, slots, rt * kRows, B, c1.th + c1.w1, c1.th + c1.b1, C, H1, ct * kCols,
-                  ACT_RELU, ws.q1);
+          fwd_job(spa, slots, rt * kRows, B, c1.th + c1.w1, c1.th + c1.b1, C, H1, ct * kCols,
+                  ACT_RELU, ws.q1, true);
         else
-          fwd_job(s, xsrc(ws.q1, H1, H1, false, true), slots, rt * kRows, B, c1.th + c1.w2,
-                  c1.th + c1.b2, H1, H2, ct * kCols, ACT_RELU, ws.q2);
+          fwd_job(xsrc(ws.q1, H1, H1, false, true), slots, rt * kRows, B, c1.th + c1.w2,
+                  c1.th + c1.b2, H1, H2, ct * kCols, ACT_RELU, ws.q2, true);
         __syncthreads();
       }
       if (!grid_sync(y, s_flag)) return;
@@ -858,7 +938,7 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
     const DZ dq2 = dz_h2(ws.q2, H2, c1.th + c1.w3, 1, nullptr, -1.0f / (float)B);
     for (int j = b; j < RT * CT1; j += G) {
       const int rt = j / CT1, ct = j % CT1, r0 = rt * kRows, c0 = ct * kCols;
-      const f32x4v acc = dx_tile(s, dq2, r0, B, c1.th + c1.w2, H2, c0, min(kCols, H1 - c0));
+      const f32x4v acc = dx_tile(dq2, r0, B, c1.th + c1.w2, H2, c0, min(kCols, H1 - c0), true);
       const int c = c0 + out_col();
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -872,7 +952,7 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
     // ---- P12: d pi(s) = dH1 W1[S + a][:]^T, times tanh' -> the actor's output gradient ----
     for (int j = b; j < RT; j += G) {
       const int r0 = j * kRows;
-      const f32x4v acc = dx_tile(s, dz_buf(ws.dq1, H1), r0, B, c1.th + c1.w1, H1, S, A);
+      const f32x4v acc = dx_tile(dz_buf(ws.dq1, H1), r0, B, c1.th + c1.w1, H1, S, A, true);
       const int c = out_col();
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -889,26 +969,26 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
     {
       const int IT1 = (H1 + kRows - 1) / kRows, IT2 = (H2 + kRows - 1) / kRows;
       const int n_dx = RT * CT1, n_dw2 = IT1 * CT2, n_dw3 = IT2;
-      const DZ d2 = dz_h2(ws.h2[N_AC], H2, ac.th + ac.w3, A, ws.dz3, 0.0f);
+      const DZ d2 = dz_h2(ws.h2(N_AC), H2, ac.th + ac.w3, A, ws.dz3, 0.0f);
       for (int j = b; j < n_dx + n_dw2 + n_dw3; j += G) {
         if (j < n_dx) {
           const int rt = j / CT1, ct = j % CT1, r0 = rt * kRows, c0 = ct * kCols;
-          const f32x4v acc = dx_tile(s, d2, r0, B, ac.th + ac.w2, H2, c0, min(kCols, H1 - c0));
+          const f32x4v acc = dx_tile(d2, r0, B, ac.th + ac.w2, H2, c0, min(kCols, H1 - c0), false);
           const int c = c0 + out_col();
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int row = r0 + out_row(r);
             if (row < B && c < H1)
               stc(ws.dh1a + row * H1 + c,
-                  ldc(ws.h1[N_AC] + row * H1 + c) > 0.0f ? acc[r] : 0.0f);
+                  ldc(ws.h1(N_AC) + row * H1 + c) > 0.0f ? acc[r] : 0.0f);
           }
         } else if (j < n_dx + n_dw2) {
           const int t = j - n_dx, it = t / CT2, ct = t % CT2;
-          dw_job(s, xsrc(ws.h1[N_AC], H1, H1, false, true), slots, d2, H1, H2, it * kRows,
+          dw_job(xsrc(ws.h1(N_AC), H1, H1, false, true), slots, d2, H1, H2, it * kRows,
                  ct * kCols, B, p.g_actor, ac.w2, ac.b2, nullptr, nullptr, nullptr, 0.0f, s_bsum);
         } else {
           const int it = j - n_dx - n_dw2;
-          dw_job(s, xsrc(ws.h2[N_AC], H2, H2, false, true), slots, dz_buf(ws.dz3, A), H2, A,
+          dw_job(xsrc(ws.h2(N_AC), H2, H2, false, true), slots, dz_buf(ws.dz3, A), H2, A,
                  it * kRows, 0, B, p.g_actor, ac.w3, ac.b3, nullptr, nullptr, nullptr, 0.0f,
                  s_bsum);
         }
@@ -921,7 +1001,7 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
       const int rest = ac.P - ac.w2, chunk = 4096, n_ad = (rest + chunk - 1) / chunk;
       for (int j = b; j < CT1 + n_ad; j += G) {
         if (j < CT1) {
-          dw_job(s, xsrc(rs, S, S, true, false), slots, dz_buf(ws.dh1a, H1), S, H1, 0,
+          dw_job(xsrc(rs, S, S, true, false), slots, dz_buf(ws.dh1a, H1), S, H1, 0,
                  j * kCols, B, p.g_actor, ac.w1, ac.b1, &ac, &p.actor, p.target_actor.theta,
                  p.tau, s_bsum);
         } else {
@@ -945,6 +1025,7 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
     if (p.smooth && p.rng_counter) *p.rng_counter += 1ull;
     *ws.base = y.base + y.n * y.G;
     *ws.epoch = y.epoch;
+    ws.trace[15] = wall_clock64();  // block 0's end (the last phase's tail may run on)
   }
 }
 

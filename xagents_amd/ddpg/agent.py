@@ -277,10 +277,39 @@ class DDPG(OffPolicy):
         self.__dict__['_fused'] = fused
         return fused
 
+    # (bench) a list to collect (policy step, start event, end event) of eager fused launches
+    fused_timing = None
+
     def _fused_step(self, policy):
         a = self._fused
         a.actor_update = int(policy)
+        ev = None
+        if self.fused_timing is not None:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
         call('xa_td3_update', ctypes.byref(a), stream())
+        if ev is not None:
+            ev[1].record()
+            self.fused_timing.append((bool(policy),) + ev)
+
+    def fused_step_flops(self, policy=True):
+        """Algorithmic FLOPs of one fused gradient step (2 M N K per GEMM): the forwards of
+        the target actor, the critics and the target critics, the critics' weight and input
+        gradients; on policy steps the actor forward, critic 1 forward on [s, pi(s)] and its
+        input gradient, the actor's weight and input gradients."""
+        B, S, A = self.batch_size, self.S, self.A
+        H1, H2 = self.actor.layers[0].units, self.actor.layers[1].units
+        C = S + A
+        mm = lambda i, o: 2 * B * i * o  # noqa: E731
+        mlp = lambda i, o: mm(i, H1) + mm(H1, H2) + mm(H2, o)  # noqa: E731
+        nc = 2 if hasattr(self, 'critic2') else 1
+        f = mlp(S, A) + 2 * nc * mlp(C, 1)                    # target actor, critics, targets
+        f += nc * (mlp(C, 1) + mm(H1, H2) + mm(H2, 1))         # critics: dW + dX
+        if policy:
+            f += mlp(S, A) + mm(C, H1) + mm(H1, H2)              # actor, critic 1 on [s, pi]
+            f += mm(H2, 1) + mm(H1, H2) + mm(H1, A)              # d(-mean Q) / d pi
+            f += mlp(S, A) + mm(H1, H2) + mm(H2, A)              # actor: dW + dX
+        return f
 
     def _critic_phase(self):
         self.replay.gather(self.replay.slots, self.s, self.a, self.r, self.d, self.s2)
