@@ -58,6 +58,16 @@ for step in "$@"; do
     gpu) run_pytest gpu 1000 tests -m gpu ;;
     configs) run_pytest configs 400 tests/test_gpu_configs.py ;;
     td3) run_pytest td3 400 tests/test_gpu_td3.py tests/test_gpu_scale.py tests/test_gpu_configs.py::test_c5_td3_64_envs_rb2 ;;
+    td3time)
+      for G in ${TD3_GS:-64 128 256}; do
+        XA_TD3_BLOCKS=$G run td3time_$G 120 python tools/td3_grad_steps.py 50
+      done ;;
+    c4w2)
+      # W = 2 rehearsal of the C4 data-parallel bench with both ranks on the one GPU (gloo;
+      # the speed means nothing, the line checks the N > 1 code path end to end)
+      XA_BENCH_SHARED_DEVICE=1 HSA_ENABLE_IPC_MODE_LEGACY=0 run c4w2 400 python -m torch.distributed.run \
+        --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py \
+        --config c4 --gpus 2 --steps 2 --warmup 1 --cpu-baseline-seconds 0 ;;
     c4dp) run_pytest c4dp 600 tests/test_gpu_dp.py -k cnn tests/test_gpu_configs.py::test_c4_ppo_cnn_128_env_shard ;;
     smoke) run smoke 180 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 300 python bench.py --steps 20 --warmup 5 ;;

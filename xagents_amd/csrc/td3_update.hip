@@ -54,7 +54,6 @@ constexpr int kAuxSc1 = 16;             // buffer instruction aux bits: write-th
 constexpr uint64_t kSpinTicks = 1000000000;  // 10 s of the 100 MHz wall clock per barrier
 constexpr int kRows = 64, kCols = 16;   // output tile of one job
 constexpr int kMaxK = 416;              // largest GEMM depth (H1, H2, batch, in)
-constexpr int kLd = kMaxK + 4;          // LDS row stride of the staged operands
 constexpr int kAux = 2048 + 1024;       // LDS floats: W3 slice + dZ3 rows of the dZ2 former
 constexpr int kU = 8;                   // loads in flight per thread while staging
 
@@ -207,105 +206,122 @@ XA_DEV DZ dz_h2(const float* h2, int H2, const float* w3, int n3, const float* d
 }
 
 struct Lds {
-  float* A;    // [64][kLd]
-  float* B;    // [16][kLd]
+  float* A;    // 64 x Kp floats: chunked rows (CR) or k-major rows of 64 (KM)
+  float* B;    // 16 x Kp floats: CR (16 rows) or k-major rows of 16 (KM)
   float* aux;  // [kAux]
 };
 // the dynamic LDS of the launch (named at file scope so the out-of-line job functions
 // address it directly as LDS)
 extern __shared__ __attribute__((aligned(16))) float td3_smem[];
-XA_DEV Lds lds() { return Lds{td3_smem, td3_smem + kRows * kLd, td3_smem + (kRows + kCols) * kLd}; }
+XA_DEV Lds lds() {
+  return Lds{td3_smem, td3_smem + kRows * kMaxK, td3_smem + (kRows + kCols) * kMaxK};
+}
 
 XA_DEV int pad16(int k) { return (k + 15) & ~15; }
 
-// ---- the tile product: wave w, rows 16 w .. 16 w + 15, 16 columns; K padded to 16 ----
-XA_DEV f32x4v tile_mma(const Lds& s, int Kp) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int i = lane & 15, q = lane >> 4;
-  const float* pa = s.A + (16 * w + i) * kLd + 4 * q;
-  const float* pb = s.B + i * kLd + 4 * q;
-  f32x4v c0 = {0.0f, 0.0f, 0.0f, 0.0f}, c1 = {0.0f, 0.0f, 0.0f, 0.0f};
-  for (int k0 = 0; k0 < Kp; k0 += 16) {
-    const float4 a = *reinterpret_cast<const float4*>(pa + k0);
-    const float4 b = *reinterpret_cast<const float4*>(pb + k0);
-    c0 = mfma4(a.x, b.x, c0);
-    c1 = mfma4(a.y, b.y, c1);
-    c0 = mfma4(a.z, b.z, c0);
-    c1 = mfma4(a.w, b.w, c1);
-  }
-  return c0 + c1;
+// Operand layouts in LDS (both written by LDS-DMA, 1 KB per wave instruction):
+//   CR  chunked rows: element (row r, k) at (k / 16 * nrow + r) * 16 + k % 16 -- a 16-row x
+//       16-k chunk is one DMA instruction; MFMA lane (i, q) reads k0 + 4q .. + 3 of its row as
+//       one float4 (the 64 lanes read 1 KB of consecutive 16-B slots)
+//   KM  k-major: element (k, c) at k * width + c (width 64 or 16) -- rows of the global
+//       matrix as they lie; MFMA lane (i, q) reads element (k0 + 4q + s, i) for step s
+XA_DEV int cr_idx(int r, int k, int nrow) { return ((k >> 4) * nrow + r) * 16 + (k & 15); }
+
+typedef __attribute__((address_space(3))) void lds_void;
+constexpr uint32_t kOob = 0xFFFFFFF0u;  // a buffer offset past every range: the DMA lands zeros
+
+XA_DEV __amdgpu_buffer_rsrc_t rsrc_dma(const void* base) {
+  const uint64_t u = (uint64_t)(uintptr_t)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
+  void* ub = (void*)(uintptr_t)(((uint64_t)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(ub, 0, 0x7FFFFFF0, kRsrcWord3);
+}
+// one wave instruction: 64 lanes x 16 B into LDS at dst (wave-uniform) + 16 lane
+XA_DEV void dma16(__amdgpu_buffer_rsrc_t r, float* dst, uint32_t voff, bool coh) {
+  lds_void* d = (lds_void*)dst;
+  if (coh) __builtin_amdgcn_raw_ptr_buffer_load_lds(r, d, 16, voff, 0, 0, kAuxSc1);
+  else __builtin_amdgcn_raw_ptr_buffer_load_lds(r, d, 16, voff, 0, 0, 0);
+}
+XA_DEV void dma_wait() {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
 }
 
-// ---- staging ----
-// A[row][k] = X[r0 + row][k] (rows < nrows, k < K, zero elsewhere up to Kp)
-XA_DEV void stage_a_rows(const Lds& s, const XSrc& x, const int64_t* slots, int r0, int nrows,
-                         int K) {
-  const int Kp = pad16(K);
-  const bool vec = x.p1 == nullptr && !x.slot0 && x.coh0 && (K & 3) == 0 && (x.ld0 & 3) == 0;
-  if (vec) {
-    const __amdgpu_buffer_rsrc_t r = rsrc(x.p0);
-    const int K4 = Kp >> 2, total = kRows * K4;
-    for (int e0 = threadIdx.x; e0 < total; e0 += 256 * kU) {
-      float4 v[kU];
-#pragma unroll
-      for (int u = 0; u < kU; ++u) {
-        const int e = e0 + 256 * u, row = e / K4, k = 4 * (e - row * K4);
-        v[u] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        if (e < total && row < nrows && k < K)
-          v[u] = ld4c(r, (uint32_t)(((r0 + row) * x.ld0 + k) * 4));
-      }
-#pragma unroll
-      for (int u = 0; u < kU; ++u) {
-        const int e = e0 + 256 * u, row = e / K4, k = 4 * (e - row * K4);
-        if (e < total) *reinterpret_cast<float4*>(&s.A[row * kLd + k]) = v[u];
-      }
+// CR tile of nrow (64 / 16) rows: tile row r = source row (rowmap ? rowmap[r] : r0 + r) of a
+// row-major matrix (ld floats, K % 4 == 0 and ld % 4 == 0), k < K; rows >= vrows and k >= K
+// are zeros up to Kp
+XA_DEV void dma_cr(float* dst, int nrow, const float* base, int64_t ld, int r0,
+                   const int64_t* rowmap, int vrows, int K, int Kp, bool coh) {
+  const __amdgpu_buffer_rsrc_t rs = rsrc_dma(base);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int nrb = nrow >> 4, ninst = nrb * (Kp >> 4);
+  const int rr = lane >> 2, kk = 4 * (lane & 3);
+  for (int t = w; t < ninst; t += 4) {
+    const int kc = t / nrb, rb = t - kc * nrb, row = 16 * rb + rr, k = 16 * kc + kk;
+    uint32_t voff = kOob;
+    if (row < vrows && k < K) {
+      const int64_t gr = rowmap ? rowmap[row] : (int64_t)(r0 + row);
+      voff = (uint32_t)((gr * ld + k) * 4);
     }
-    return;
-  }
-  const int total = kRows * Kp;
-  for (int e0 = threadIdx.x; e0 < total; e0 += 256 * kU) {
-    float v[kU];
-#pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const int e = e0 + 256 * u, row = e / Kp, k = e - row * Kp;
-      v[u] = (e < total && row < nrows && k < K) ? xload(x, slots, r0 + row, k) : 0.0f;
-    }
-#pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const int e = e0 + 256 * u, row = e / Kp, k = e - row * Kp;
-      if (e < total) s.A[row * kLd + k] = v[u];
-    }
+    dma16(rs, dst + (kc * nrow + 16 * rb) * 16, voff, coh);
   }
 }
 
-// A[i][k] = X[k][i0 + i] (the transposed input of a weight gradient: i < ni in-features,
-// k < nk samples)
-XA_DEV void stage_a_trans(const Lds& s, const XSrc& x, const int64_t* slots, int i0, int ni,
-                          int nk) {
-  const int Kp = pad16(nk), total = kRows * Kp;
-  for (int e0 = threadIdx.x; e0 < total; e0 += 256 * kU) {
-    float v[kU];
+// KM tile of width wd (64 / 16) floats: row k = source row (rowmap ? rowmap[k] : k) columns
+// c0 .. c0 + wd (ld % 4 == 0, c0 % 4 == 0), k < vK, column < vc (vc % 4 == 0); zeros elsewhere
+// up to Kp rows
+XA_DEV void dma_km(float* dst, int wd, const float* base, int64_t ld, int c0,
+                   const int64_t* rowmap, int vK, int vc, int Kp, bool coh) {
+  const __amdgpu_buffer_rsrc_t rs = rsrc_dma(base);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int per = wd >> 2, rows_per = 64 / per, ninst = Kp / rows_per;
+  const int kr = lane / per, c = 4 * (lane - kr * per);
+  for (int t = w; t < ninst; t += 4) {
+    const int k = t * rows_per + kr;
+    uint32_t voff = kOob;
+    if (k < vK && c < vc) {
+      const int64_t gr = rowmap ? rowmap[k] : (int64_t)k;
+      voff = (uint32_t)((gr * ld + c0 + c) * 4);
+    }
+    dma16(rs, dst + t * 256, voff, coh);
+  }
+}
+
+// scalar loads into registers (concatenated or gathered rows the DMA cannot take), all issued
+// before the first LDS write: element (a, b) of an na x nb grid, value x(a, b) when a < va and
+// b < vb (else 0), dst(a, b, v)
+template <class Ld, class Dst>
+XA_DEV void sload(int na, int nb, int va, int vb, Ld ld, Dst dst) {
+  constexpr int kS = 16;
+  const int total = na * nb;
+  for (int e0 = threadIdx.x; e0 < total; e0 += 256 * kS) {
+    float v[kS];
 #pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const int e = e0 + 256 * u, k = e >> 6, i = e & 63;
-      v[u] = (e < total && i < ni && k < nk) ? xload(x, slots, k, i0 + i) : 0.0f;
+    for (int u = 0; u < kS; ++u) {
+      const int e = e0 + 256 * u, a = e / nb, b = e - a * nb;
+      v[u] = (e < total && a < va && b < vb) ? ld(a, b) : 0.0f;
     }
 #pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const int e = e0 + 256 * u, k = e >> 6, i = e & 63;
-      if (e < total) s.A[i * kLd + k] = v[u];
+    for (int u = 0; u < kS; ++u) {
+      const int e = e0 + 256 * u, a = e / nb, b = e - a * nb;
+      if (e < total) dst(a, b, v[u]);
     }
   }
+}
+
+XA_DEV bool dma_src(const XSrc& x) {
+  return x.p1 == nullptr && (x.w0 & 3) == 0 && (x.ld0 & 3) == 0;
 }
 
 // the dZ2 former's LDS inputs: W3 rows [k0, k0 + nk) (n3 each) and d3 rows [r0, r0 + nr)
+// (scalar loads; the caller's dma_wait orders them)
 XA_DEV void stage_dz_aux(const Lds& s, const DZ& d, int k0, int nk, int r0, int nr) {
   if (!d.h2) return;
   for (int e = threadIdx.x; e < nk * d.n3; e += 256) s.aux[e] = ldc(d.w3 + k0 * d.n3 + e);
   float* sd = s.aux + 2048;
   if (d.d3)
     for (int e = threadIdx.x; e < nr * d.n3; e += 256) sd[e] = ldc(d.d3 + r0 * d.n3 + e);
-  __syncthreads();
 }
 // dZ2[r][k] from the staged aux (k relative to the aux's k0, r relative to its r0)
 XA_DEV float dz_form(const Lds& s, const DZ& d, float h, int rr, int kk) {
@@ -321,133 +337,32 @@ XA_DEV float dz_form(const Lds& s, const DZ& d, float h, int rr, int kk) {
   return h > 0.0f ? g : 0.0f;
 }
 
-// A[row][k] = dZ[r0 + row][k] (k < K = the layer's output width)
-XA_DEV void stage_a_dz(const Lds& s, const DZ& d, int r0, int nrows, int K) {
-  const int Kp = pad16(K), total = kRows * Kp;
-  if (d.h2) stage_dz_aux(s, d, 0, K, r0, min(nrows, kRows));
-  const float* src = d.h2 ? d.h2 : d.buf;
-  for (int e0 = threadIdx.x; e0 < total; e0 += 256 * kU) {
-    float v[kU];
-#pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const int e = e0 + 256 * u, row = e / Kp, k = e - row * Kp;
-      v[u] = (e < total && row < nrows && k < K) ? ldc(src + (int64_t)(r0 + row) * d.ld + k) : 0.0f;
+// ---- the tile product: wave w, rows 16 w .. 16 w + 15, 16 columns; K padded to 16 ----
+template <bool A_CR, bool B_CR>
+XA_DEV f32x4v tile_mma(const Lds& s, int Kp) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int i = lane & 15, q = lane >> 4;
+  f32x4v c0 = {0.0f, 0.0f, 0.0f, 0.0f}, c1 = {0.0f, 0.0f, 0.0f, 0.0f};
+  for (int k0 = 0; k0 < Kp; k0 += 16) {
+    float4 a, b;
+    if constexpr (A_CR) {
+      a = *reinterpret_cast<const float4*>(s.A + ((k0 >> 4) * kRows + 16 * w + i) * 16 + 4 * q);
+    } else {
+      const float* pa = s.A + (k0 + 4 * q) * kRows + 16 * w + i;
+      a = make_float4(pa[0], pa[kRows], pa[2 * kRows], pa[3 * kRows]);
     }
-#pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const int e = e0 + 256 * u, row = e / Kp, k = e - row * Kp;
-      if (e < total) s.A[row * kLd + k] = (d.h2 && row < nrows && k < K) ? dz_form(s, d, v[u], row, k) : v[u];
+    if constexpr (B_CR) {
+      b = *reinterpret_cast<const float4*>(s.B + ((k0 >> 4) * kCols + i) * 16 + 4 * q);
+    } else {
+      const float* pb = s.B + (k0 + 4 * q) * kCols + i;
+      b = make_float4(pb[0], pb[kCols], pb[2 * kCols], pb[3 * kCols]);
     }
+    c0 = mfma4(a.x, b.x, c0);
+    c1 = mfma4(a.y, b.y, c1);
+    c0 = mfma4(a.z, b.z, c0);
+    c1 = mfma4(a.w, b.w, c1);
   }
-}
-
-// B^T[j][k] = W[k][c0 + j] (forward: W row-major [K][N]; j < nc valid columns); coh: W was
-// written earlier in this launch (sc1 loads), else plain loads
-XA_DEV void stage_b_fwd(const Lds& s, const float* W, int N, int c0, int nc, int K, bool coh) {
-  const int Kp = pad16(K);
-  if ((N & 3) == 0 && (c0 & 3) == 0) {
-    // four float4 per row k (lanes t = e & 3), each wholly inside or outside [c0, c0 + nc)
-    const __amdgpu_buffer_rsrc_t r = rsrc(W);
-    const int total = 4 * Kp;
-    for (int e0 = threadIdx.x; e0 < total; e0 += 256 * kU) {
-      float4 v[kU];
-#pragma unroll
-      for (int u = 0; u < kU; ++u) {
-        const int e = e0 + 256 * u, k = e >> 2, t = e & 3;
-        v[u] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        if (e < total && 4 * t < nc && k < K) {
-          const uint32_t off = (uint32_t)(((int64_t)k * N + c0 + 4 * t) * 4);
-          v[u] = coh ? ld4c(r, off) : ld4p(r, off);
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < kU; ++u) {
-        const int e = e0 + 256 * u, k = e >> 2, t = e & 3;
-        if (e < total) {
-          s.B[(4 * t) * kLd + k] = v[u].x;
-          s.B[(4 * t + 1) * kLd + k] = v[u].y;
-          s.B[(4 * t + 2) * kLd + k] = v[u].z;
-          s.B[(4 * t + 3) * kLd + k] = v[u].w;
-        }
-      }
-    }
-    return;
-  }
-  const int total = kCols * Kp;
-  for (int e0 = threadIdx.x; e0 < total; e0 += 256 * kU) {
-    float v[kU];
-#pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const int e = e0 + 256 * u, k = e >> 4, j = e & 15;
-      v[u] = (e < total && j < nc && k < K) ? ldw(W + (int64_t)k * N + c0 + j, coh) : 0.0f;
-    }
-#pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const int e = e0 + 256 * u, k = e >> 4, j = e & 15;
-      if (e < total) s.B[j * kLd + k] = v[u];
-    }
-  }
-}
-
-// B^T[j][k] = W[c0 + j][k] (input gradient dZ W^T: W row-major [in][K])
-XA_DEV void stage_b_rows(const Lds& s, const float* W, int K, int c0, int nc, bool coh) {
-  const int Kp = pad16(K);
-  if ((K & 3) == 0) {
-    const __amdgpu_buffer_rsrc_t r = rsrc(W);
-    const int K4 = Kp >> 2, total = kCols * K4;
-    for (int e0 = threadIdx.x; e0 < total; e0 += 256 * kU) {
-      float4 v[kU];
-#pragma unroll
-      for (int u = 0; u < kU; ++u) {
-        const int e = e0 + 256 * u, j = e / K4, k = 4 * (e - j * K4);
-        v[u] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        if (e < total && j < nc && k < K) {
-          const uint32_t off = (uint32_t)(((int64_t)(c0 + j) * K + k) * 4);
-          v[u] = coh ? ld4c(r, off) : ld4p(r, off);
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < kU; ++u) {
-        const int e = e0 + 256 * u, j = e / K4, k = 4 * (e - j * K4);
-        if (e < total) *reinterpret_cast<float4*>(&s.B[j * kLd + k]) = v[u];
-      }
-    }
-    return;
-  }
-  const int total = kCols * Kp;
-  for (int e0 = threadIdx.x; e0 < total; e0 += 256 * kU) {
-    float v[kU];
-#pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const int e = e0 + 256 * u, j = e / Kp, k = e - j * Kp;
-      v[u] = (e < total && j < nc && k < K) ? ldw(W + (int64_t)(c0 + j) * K + k, coh) : 0.0f;
-    }
-#pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const int e = e0 + 256 * u, j = e / Kp, k = e - j * Kp;
-      if (e < total) s.B[j * kLd + k] = v[u];
-    }
-  }
-}
-
-// B^T[j][k] = dZ[k][j0 + j] (weight gradient: k < nk samples, j < nc columns)
-XA_DEV void stage_b_dz(const Lds& s, const DZ& d, int j0, int nc, int nk) {
-  const int Kp = pad16(nk), total = kCols * Kp;
-  if (d.h2) stage_dz_aux(s, d, j0, nc, 0, nk);
-  const float* src = d.h2 ? d.h2 : d.buf;
-  for (int e0 = threadIdx.x; e0 < total; e0 += 256 * kU) {
-    float v[kU];
-#pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const int e = e0 + 256 * u, k = e >> 4, j = e & 15;
-      v[u] = (e < total && j < nc && k < nk) ? ldc(src + (int64_t)k * d.ld + j0 + j) : 0.0f;
-    }
-#pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const int e = e0 + 256 * u, k = e >> 4, j = e & 15;
-      if (e < total) s.B[j * kLd + k] = (d.h2 && j < nc && k < nk) ? dz_form(s, d, v[u], k, j) : v[u];
-    }
-  }
+  return c0 + c1;
 }
 
 // ---- epilogue helpers: lane l holds D[4 (l >> 4) + r][l & 15] of the wave's 16 rows ----
@@ -464,14 +379,24 @@ XA_DEV float act_f(float v, int act) {
 
 // forward job: out[r][c] = act(X W + b) on rows [r0, r0 + 64) x cols [c0, c0 + 16)
 // (the tile functions are out of line: one copy each instead of one per call site)
+// forward tile: A = X rows (CR), B = W[k][c0 ..] (KM)
 __device__ __noinline__ f32x4v fwd_tile(XSrc x, const int64_t* slots, int r0, int B,
                                         const float* W, const float* bias, int K, int N, int c0,
                                         bool coh) {
   const Lds s = lds();
-  stage_a_rows(s, x, slots, r0, min(kRows, B - r0), K);
-  stage_b_fwd(s, W, N, c0, min(kCols, N - c0), K, coh);
-  __syncthreads();
-  f32x4v acc = tile_mma(s, pad16(K));
+  const int Kp = pad16(K), nrows = min(kRows, B - r0), nc = min(kCols, N - c0);
+  if (dma_src(x) && (K & 3) == 0)
+    dma_cr(s.A, kRows, x.p0, x.ld0, r0, x.slot0 ? slots + r0 : nullptr, nrows, K, Kp, x.coh0);
+  else
+    sload(kRows, Kp, nrows, K, [&](int r, int k) { return xload(x, slots, r0 + r, k); },
+          [&](int r, int k, float v) { s.A[cr_idx(r, k, kRows)] = v; });
+  if ((N & 3) == 0 && (c0 & 3) == 0 && (nc & 3) == 0)
+    dma_km(s.B, kCols, W, N, c0, nullptr, K, nc, Kp, coh);
+  else
+    sload(Kp, kCols, K, nc, [&](int k, int j) { return ldw(W + (int64_t)k * N + c0 + j, coh); },
+          [&](int k, int j, float v) { s.B[k * kCols + j] = v; });
+  dma_wait();
+  f32x4v acc = tile_mma<true, false>(s, Kp);
   const int c = c0 + out_col();
   if (c < N) {
     const float b = ldw(bias + c, coh);
@@ -493,31 +418,69 @@ XA_DEV void fwd_job(const XSrc& x, const int64_t* slots, int r0, int B, const fl
   }
 }
 
-// input-gradient job: out[r][c] = (dZ W^T)[r][c] * gate (gate: the source layer's relu
-// output > 0), rows [r0, r0 + 64) x cols [c0, c0 + 16) of the layer input (width nin)
+// input-gradient tile: (dZ W^T)[r][c] on rows [r0, r0 + 64) x cols [c0, c0 + 16) of the layer
+// input (W row-major [in][K]): A = dZ rows (CR, the dZ2 former applied in LDS), B = W rows
+// c0 .. (CR)
 __device__ __noinline__ f32x4v dx_tile(DZ d, int r0, int B, const float* W, int K, int c0,
                                        int nc, bool coh) {
   const Lds s = lds();
-  stage_a_dz(s, d, r0, min(kRows, B - r0), K);
-  stage_b_rows(s, W, K, c0, nc, coh);
-  __syncthreads();
-  return tile_mma(s, pad16(K));
+  const int Kp = pad16(K), nrows = min(kRows, B - r0);
+  const float* src = d.h2 ? d.h2 : d.buf;
+  if ((K & 3) == 0 && (d.ld & 3) == 0)
+    dma_cr(s.A, kRows, src, d.ld, r0, nullptr, nrows, K, Kp, true);
+  else
+    sload(kRows, Kp, nrows, K, [&](int r, int k) { return ldc(src + (int64_t)(r0 + r) * d.ld + k); },
+          [&](int r, int k, float v) { s.A[cr_idx(r, k, kRows)] = v; });
+  if ((K & 3) == 0)
+    dma_cr(s.B, kCols, W, K, c0, nullptr, nc, K, Kp, coh);
+  else
+    sload(kCols, Kp, nc, K, [&](int j, int k) { return ldw(W + (int64_t)(c0 + j) * K + k, coh); },
+          [&](int j, int k, float v) { s.B[cr_idx(j, k, kCols)] = v; });
+  stage_dz_aux(s, d, 0, K, r0, nrows);
+  dma_wait();
+  if (d.h2) {
+    for (int e = threadIdx.x; e < kRows * Kp; e += 256) {
+      const int kc = e >> 10, r = (e >> 4) & 63, k = 16 * kc + (e & 15);
+      if (r < nrows && k < K) s.A[e] = dz_form(s, d, s.A[e], r, k);
+    }
+    __syncthreads();
+  }
+  return tile_mma<true, true>(s, Kp);
 }
 
-// weight-gradient tile: D[i][j] = sum_k X[k][i0 + i] dZ[k][j0 + j] (i < ni, j < nc, k < B);
-// the bias gradient sum_k dZ[k][j0 + j] (fixed k order) lands in bsum[j] when bsum != 0
+// weight-gradient tile: D[i][j] = sum_k X[k][i0 + i] dZ[k][j0 + j] (i < ni, j < nc, k < B):
+// A = X rows (KM, width 64), B = dZ rows (KM, width 16); the bias gradient
+// sum_k dZ[k][j0 + j] (fixed k order) lands in bsum[j] when bsum != 0
 __device__ __noinline__ f32x4v dw_tile(XSrc x, const int64_t* slots, DZ d, int i0, int ni,
                                        int j0, int nc, int B, float* bsum) {
   const Lds s = lds();
-  stage_a_trans(s, x, slots, i0, ni, B);
-  stage_b_dz(s, d, j0, nc, B);
-  __syncthreads();
+  const int Kp = pad16(B);
+  if (dma_src(x) && (ni & 3) == 0 && (i0 & 3) == 0)
+    dma_km(s.A, kRows, x.p0, x.ld0, i0, x.slot0 ? slots : nullptr, B, ni, Kp, x.coh0);
+  else
+    sload(Kp, kRows, B, ni, [&](int k, int i) { return xload(x, slots, k, i0 + i); },
+          [&](int k, int i, float v) { s.A[k * kRows + i] = v; });
+  const float* src = d.h2 ? d.h2 : d.buf;
+  if ((d.ld & 3) == 0 && (j0 & 3) == 0 && (nc & 3) == 0)
+    dma_km(s.B, kCols, src, d.ld, j0, nullptr, B, nc, Kp, true);
+  else
+    sload(Kp, kCols, B, nc, [&](int k, int j) { return ldc(src + (int64_t)k * d.ld + j0 + j); },
+          [&](int k, int j, float v) { s.B[k * kCols + j] = v; });
+  stage_dz_aux(s, d, j0, nc, 0, B);
+  dma_wait();
+  if (d.h2) {
+    for (int e = threadIdx.x; e < Kp * kCols; e += 256) {
+      const int k = e >> 4, j = e & 15;
+      if (k < B && j < nc) s.B[e] = dz_form(s, d, s.B[e], k, j);
+    }
+    __syncthreads();
+  }
   if (bsum && threadIdx.x < nc) {
     float t = 0.0f;
-    for (int k = 0; k < B; ++k) t += s.B[threadIdx.x * kLd + k];
+    for (int k = 0; k < B; ++k) t += s.B[k * kCols + threadIdx.x];
     bsum[threadIdx.x] = t;
   }
-  return tile_mma(s, pad16(B));
+  return tile_mma<false, false>(s, Kp);
 }
 
 // Keras Adam (+ Polyak into the target) of one parameter from its raw gradient
@@ -1061,7 +1024,7 @@ extern "C" int xa_td3_update(const XaTd3UpdateArgs* p, void* stream) {
   if (hipGetDevice(&dev) == hipSuccess)
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   const int G = a.n_blocks > 0 ? min(a.n_blocks, cus) : min(128, cus);
-  const size_t lds = sizeof(float) * ((size_t)(kRows + kCols) * kLd + kAux);
+  const size_t lds = sizeof(float) * ((size_t)(kRows + kCols) * kMaxK + kAux);
   hipLaunchKernelGGL(td3_update_kernel, dim3(G), dim3(256), lds, (hipStream_t)stream, a);
   XA_CHECK_LAUNCH("xa_td3_update");
   return 0;
