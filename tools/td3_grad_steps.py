@@ -55,6 +55,17 @@ def main():
         print('fused phases (us, block 0, median of 20 eager launches): ' +
               ' '.join(f'P{i + 1} {v:.1f}' for i, v in enumerate(d)) + f' | total {d.sum():.1f}',
               flush=True)
+        # inside block 0's first job of each phase: entry, loads issued, operands in LDS,
+        # MFMA done (us after the phase's barrier), from the last launch
+        tr = rows[-1]
+        dt = agent._fused_ws[1024:1024 + 8192].cpu().numpy().view(np.uint64).astype(np.int64)
+        for p in range(len(d) - 1):
+            pts = dt[8 * p:8 * p + 4]
+            if (pts <= 0).any() or pts[0] < tr[0]:
+                continue
+            rel = (pts - tr[p]) / 100.0
+            print(f'  P{p + 1} job: entry {rel[0]:.2f} issued {rel[1]:.2f} ready {rel[2]:.2f} '
+                  f'mma {rel[3]:.2f} us', flush=True)
 
 
 if __name__ == '__main__':

@@ -219,6 +219,14 @@ XA_DEV Lds lds() {
 
 XA_DEV int pad16(int k) { return (k + 15) & ~15; }
 
+// (diagnostic) block 0 stamps the wall clock at points of the first job of every phase into
+// the workspace's detail trace (tools/td3_grad_steps.py): slot 8 p + point
+__shared__ int td3_dslot;
+__shared__ unsigned long long* td3_dbuf;
+XA_DEV void dstamp(int point) {
+  if (threadIdx.x == 0 && td3_dslot >= 0) td3_dbuf[td3_dslot + point] = wall_clock64();
+}
+
 // Operand layouts in LDS (both written by LDS-DMA, 1 KB per wave instruction):
 //   CR  chunked rows: element (row r, k) at (k / 16 * nrow + r) * 16 + k % 16 -- a 16-row x
 //       16-k chunk is one DMA instruction; MFMA lane (i, q) reads k0 + 4q .. + 3 of its row as
@@ -384,6 +392,7 @@ __device__ __noinline__ f32x4v fwd_tile(XSrc x, const int64_t* slots, int r0, in
                                         const float* W, const float* bias, int K, int N, int c0,
                                         bool coh) {
   const Lds s = lds();
+  dstamp(0);
   const int Kp = pad16(K), nrows = min(kRows, B - r0), nc = min(kCols, N - c0);
   if (dma_src(x) && (K & 3) == 0)
     dma_cr(s.A, kRows, x.p0, x.ld0, r0, x.slot0 ? slots + r0 : nullptr, nrows, K, Kp, x.coh0);
@@ -395,8 +404,11 @@ __device__ __noinline__ f32x4v fwd_tile(XSrc x, const int64_t* slots, int r0, in
   else
     sload(Kp, kCols, K, nc, [&](int k, int j) { return ldw(W + (int64_t)k * N + c0 + j, coh); },
           [&](int k, int j, float v) { s.B[k * kCols + j] = v; });
+  dstamp(1);
   dma_wait();
+  dstamp(2);
   f32x4v acc = tile_mma<true, false>(s, Kp);
+  dstamp(3);
   const int c = c0 + out_col();
   if (c < N) {
     const float b = ldw(bias + c, coh);
@@ -424,6 +436,7 @@ XA_DEV void fwd_job(const XSrc& x, const int64_t* slots, int r0, int B, const fl
 __device__ __noinline__ f32x4v dx_tile(DZ d, int r0, int B, const float* W, int K, int c0,
                                        int nc, bool coh) {
   const Lds s = lds();
+  dstamp(0);
   const int Kp = pad16(K), nrows = min(kRows, B - r0);
   const float* src = d.h2 ? d.h2 : d.buf;
   if ((K & 3) == 0 && (d.ld & 3) == 0)
@@ -437,6 +450,7 @@ __device__ __noinline__ f32x4v dx_tile(DZ d, int r0, int B, const float* W, int 
     sload(kCols, Kp, nc, K, [&](int j, int k) { return ldw(W + (int64_t)(c0 + j) * K + k, coh); },
           [&](int j, int k, float v) { s.B[cr_idx(j, k, kCols)] = v; });
   stage_dz_aux(s, d, 0, K, r0, nrows);
+  dstamp(1);
   dma_wait();
   if (d.h2) {
     for (int e = threadIdx.x; e < kRows * Kp; e += 256) {
@@ -445,7 +459,10 @@ __device__ __noinline__ f32x4v dx_tile(DZ d, int r0, int B, const float* W, int 
     }
     __syncthreads();
   }
-  return tile_mma<true, true>(s, Kp);
+  dstamp(2);
+  const f32x4v acc = tile_mma<true, true>(s, Kp);
+  dstamp(3);
+  return acc;
 }
 
 // weight-gradient tile: D[i][j] = sum_k X[k][i0 + i] dZ[k][j0 + j] (i < ni, j < nc, k < B):
@@ -454,6 +471,7 @@ __device__ __noinline__ f32x4v dx_tile(DZ d, int r0, int B, const float* W, int 
 __device__ __noinline__ f32x4v dw_tile(XSrc x, const int64_t* slots, DZ d, int i0, int ni,
                                        int j0, int nc, int B, float* bsum) {
   const Lds s = lds();
+  dstamp(0);
   const int Kp = pad16(B);
   if (dma_src(x) && (ni & 3) == 0 && (i0 & 3) == 0)
     dma_km(s.A, kRows, x.p0, x.ld0, i0, x.slot0 ? slots : nullptr, B, ni, Kp, x.coh0);
@@ -467,6 +485,7 @@ __device__ __noinline__ f32x4v dw_tile(XSrc x, const int64_t* slots, DZ d, int i
     sload(Kp, kCols, B, nc, [&](int k, int j) { return ldc(src + (int64_t)k * d.ld + j0 + j); },
           [&](int k, int j, float v) { s.B[k * kCols + j] = v; });
   stage_dz_aux(s, d, j0, nc, 0, B);
+  dstamp(1);
   dma_wait();
   if (d.h2) {
     for (int e = threadIdx.x; e < Kp * kCols; e += 256) {
@@ -480,7 +499,10 @@ __device__ __noinline__ f32x4v dw_tile(XSrc x, const int64_t* slots, DZ d, int i
     for (int k = 0; k < B; ++k) t += s.B[k * kCols + threadIdx.x];
     bsum[threadIdx.x] = t;
   }
-  return tile_mma<false, false>(s, Kp);
+  dstamp(2);
+  const f32x4v acc = tile_mma<false, false>(s, Kp);
+  dstamp(3);
+  return acc;
 }
 
 // Keras Adam (+ Polyak into the target) of one parameter from its raw gradient
@@ -579,6 +601,7 @@ struct Ws {
   unsigned* base;     // the counter value at the start of the next launch
   unsigned* abort_w;  // the epoch of a launch that timed out
   unsigned* epoch;    // launches so far
+  unsigned long long* dtrace;  // [16][8] points inside block 0's first job of each phase
   unsigned long long* trace;  // [16] wall clock at launch start and after every barrier
                               // (block 0; tools/td3_grad_steps.py reads it)
   float* h1all;       // [6][B][H1] per network slot: target actor, critic 1, critic 2,
@@ -617,6 +640,7 @@ __host__ __device__ inline Ws carve(void* base_p, int B, int H1, int H2, int A) 
   w.abort_w = ctl + 128;
   w.epoch = ctl + 192;
   w.trace = (unsigned long long*)(ctl + 224);
+  w.dtrace = (unsigned long long*)take(8192);
   w.h1s = align_up((size_t)B * H1, 64);
   w.h2s = align_up((size_t)B * H2, 64);
   w.h1all = (float*)take(6 * w.h1s * 4);
@@ -655,6 +679,11 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
   y.status = p.status;
   y.trace = b == 0 ? ws.trace : nullptr;
   if (b == 0 && tid == 0) ws.trace[0] = wall_clock64();
+  if (tid == 0) {
+    td3_dslot = -1;
+    td3_dbuf = ws.dtrace;
+  }
+  __syncthreads();
   // networks (the Adam step sizes from the step counters as the launch finds them)
   const Net c1 = make_net(p.critic1, C, H1, H2, 1, true);
   const Net c2 = make_net(twin ? p.critic2 : p.critic1, C, H1, H2, 1, twin);
@@ -705,6 +734,7 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
   for (int layer = 1; layer <= 2; ++layer) {
     const int CT = layer == 1 ? CT1 : CT2, per = RT * CT;
     for (int j = b; j < nn * per; j += G) {
+      if (tid == 0) td3_dslot = (b == 0 && j == b) ? 8 * (int)y.n : -1;
       const int id = net_id(j / per), rem = j % per, rt = rem / CT, ct = rem % CT;
       const Net n = net_of(id);
       if (layer == 1)
@@ -722,6 +752,7 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
   {
     const uint64_t ctr = p.rng_counter ? *p.rng_counter : 0ull;
     for (int j = b; j < nn * RT; j += G) {
+      if (tid == 0) td3_dslot = (b == 0 && j == b) ? 8 * (int)y.n : -1;
       const int id = net_id(j / RT), rt = j % RT, r0 = rt * kRows;
       const Net n = net_of(id);
       const int N = n.out;
@@ -760,6 +791,7 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
   for (int layer = 1; layer <= 2; ++layer) {
     const int CT = layer == 1 ? CT1 : CT2, per = RT * CT;
     for (int j = b; j < nt * per; j += G) {
+      if (tid == 0) td3_dslot = (b == 0 && j == b) ? 8 * (int)y.n : -1;
       const int id = N_TC1 + j / per, rem = j % per, rt = rem / CT, ct = rem % CT;
       const Net n = net_of(id);
       if (layer == 1)
@@ -775,6 +807,7 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
 
   // ---- P6: target values and the TD head ----
   for (int j = b; j < RT; j += G) {
+    if (tid == 0) td3_dslot = (b == 0 && j == b) ? 8 * (int)y.n : -1;
     const int r0 = j * kRows;
     const f32x4v t1 = fwd_tile(xsrc(ws.h2(N_TC1), H2, H2, false, true), slots, r0, B,
                                tc1.th + tc1.w3, tc1.th + tc1.b3, H2, 1, 0, false);
@@ -823,6 +856,7 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
     const int n_dx = RT * CT1, n_dw2 = IT1 * CT2, n_dw3 = IT2;
     const int per = n_dx + n_dw2 + n_dw3;  // the heavy input-gradient jobs first
     for (int j = b; j < nt * per; j += G) {
+      if (tid == 0) td3_dslot = (b == 0 && j == b) ? 8 * (int)y.n : -1;
       const int ci = j / per, q = j % per;
       const Net n = ci ? c2 : c1;
       const int id = ci ? N_C2 : N_C1;
@@ -861,6 +895,7 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
     const int rest = c1.P - c1.w2, chunk = 4096, n_ad = (rest + chunk - 1) / chunk;
     const int per = n_w1 + n_ad;
     for (int j = b; j < nt * per; j += G) {
+      if (tid == 0) td3_dslot = (b == 0 && j == b) ? 8 * (int)y.n : -1;
       const int ci = j / per, q = j % per;
       const Net n = ci ? c2 : c1;
       const XaTdNet& opt = ci ? p.critic2 : p.critic1;
@@ -886,6 +921,7 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
     for (int layer = 1; layer <= 2; ++layer) {
       const int CT = layer == 1 ? CT1 : CT2;
       for (int j = b; j < RT * CT; j += G) {
+        if (tid == 0) td3_dslot = (b == 0 && j == b) ? 8 * (int)y.n : -1;
         const int rt = j / CT, ct = j % CT;
         if (layer == 1)
           fwd_job(spa, slots, rt * kRows, B, c1.th + c1.w1, c1.th + c1.b1, C, H1, ct * kCols,
@@ -900,6 +936,7 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
     // ---- P11: dH1 of -mean Q (dQ / dv = -1 / B per row) ----
     const DZ dq2 = dz_h2(ws.q2, H2, c1.th + c1.w3, 1, nullptr, -1.0f / (float)B);
     for (int j = b; j < RT * CT1; j += G) {
+      if (tid == 0) td3_dslot = (b == 0 && j == b) ? 8 * (int)y.n : -1;
       const int rt = j / CT1, ct = j % CT1, r0 = rt * kRows, c0 = ct * kCols;
       const f32x4v acc = dx_tile(dq2, r0, B, c1.th + c1.w2, H2, c0, min(kCols, H1 - c0), true);
       const int c = c0 + out_col();
@@ -914,6 +951,7 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
     if (!grid_sync(y, s_flag)) return;
     // ---- P12: d pi(s) = dH1 W1[S + a][:]^T, times tanh' -> the actor's output gradient ----
     for (int j = b; j < RT; j += G) {
+      if (tid == 0) td3_dslot = (b == 0 && j == b) ? 8 * (int)y.n : -1;
       const int r0 = j * kRows;
       const f32x4v acc = dx_tile(dz_buf(ws.dq1, H1), r0, B, c1.th + c1.w1, H1, S, A, true);
       const int c = out_col();
@@ -934,6 +972,7 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
       const int n_dx = RT * CT1, n_dw2 = IT1 * CT2, n_dw3 = IT2;
       const DZ d2 = dz_h2(ws.h2(N_AC), H2, ac.th + ac.w3, A, ws.dz3, 0.0f);
       for (int j = b; j < n_dx + n_dw2 + n_dw3; j += G) {
+        if (tid == 0) td3_dslot = (b == 0 && j == b) ? 8 * (int)y.n : -1;
         if (j < n_dx) {
           const int rt = j / CT1, ct = j % CT1, r0 = rt * kRows, c0 = ct * kCols;
           const f32x4v acc = dx_tile(d2, r0, B, ac.th + ac.w2, H2, c0, min(kCols, H1 - c0), false);
@@ -963,6 +1002,7 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
     {
       const int rest = ac.P - ac.w2, chunk = 4096, n_ad = (rest + chunk - 1) / chunk;
       for (int j = b; j < CT1 + n_ad; j += G) {
+        if (tid == 0) td3_dslot = (b == 0 && j == b) ? 8 * (int)y.n : -1;
         if (j < CT1) {
           dw_job(xsrc(rs, S, S, true, false), slots, dz_buf(ws.dh1a, H1), S, H1, 0,
                  j * kCols, B, p.g_actor, ac.w1, ac.b1, &ac, &p.actor, p.target_actor.theta,
