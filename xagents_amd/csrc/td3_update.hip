@@ -256,6 +256,10 @@ XA_DEV void dma_wait() {
   __syncthreads();
 }
 
+// (the row map is read BEFORE the first DMA is issued: loads, stores and LDS-DMA retire in
+// issue order, so a row-map load between two DMAs would make the second wait for the first)
+typedef __attribute__((address_space(1))) const int64_t gi64;
+
 // CR tile of nrow (64 / 16) rows: tile row r = source row (rowmap ? rowmap[r] : r0 + r) of a
 // row-major matrix (ld floats, K % 4 == 0 and ld % 4 == 0), k < K; rows >= vrows and k >= K
 // are zeros up to Kp
@@ -265,16 +269,21 @@ XA_DEV void dma_cr(float* dst, int nrow, const float* base, int64_t ld, int r0,
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int nrb = nrow >> 4, ninst = nrb * (Kp >> 4);
   const int rr = lane >> 2, kk = 4 * (lane & 3);
+  int64_t gr[4];
+#pragma unroll
+  for (int rb = 0; rb < 4; ++rb) {
+    const int row = 16 * rb + rr;
+    gr[rb] = (rb < nrb && row < vrows) ? (rowmap ? ((gi64*)rowmap)[row] : (int64_t)(r0 + row)) : -1;
+  }
   for (int t = w; t < ninst; t += 4) {
-    const int kc = t / nrb, rb = t - kc * nrb, row = 16 * rb + rr, k = 16 * kc + kk;
-    uint32_t voff = kOob;
-    if (row < vrows && k < K) {
-      const int64_t gr = rowmap ? rowmap[row] : (int64_t)(r0 + row);
-      voff = (uint32_t)((gr * ld + k) * 4);
-    }
+    const int kc = t / nrb, rb = t - kc * nrb, k = 16 * kc + kk;
+    const int64_t g = rb == 0 ? gr[0] : rb == 1 ? gr[1] : rb == 2 ? gr[2] : gr[3];
+    const uint32_t voff = (g >= 0 && k < K) ? (uint32_t)((g * ld + k) * 4) : kOob;
     dma16(rs, dst + (kc * nrow + 16 * rb) * 16, voff, coh);
   }
 }
+
+constexpr int kKmMax = 16;  // k-major DMA instructions per wave with a row map (batch <= 256)
 
 // KM tile of width wd (64 / 16) floats: row k = source row (rowmap ? rowmap[k] : k) columns
 // c0 .. c0 + wd (ld % 4 == 0, c0 % 4 == 0), k < vK, column < vc (vc % 4 == 0); zeros elsewhere
@@ -285,13 +294,26 @@ XA_DEV void dma_km(float* dst, int wd, const float* base, int64_t ld, int c0,
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int per = wd >> 2, rows_per = 64 / per, ninst = Kp / rows_per;
   const int kr = lane / per, c = 4 * (lane - kr * per);
+  if (rowmap) {
+    int64_t gr[kKmMax];
+#pragma unroll
+    for (int m = 0; m < kKmMax; ++m) {
+      const int k = (w + 4 * m) * rows_per + kr;
+      gr[m] = (w + 4 * m < ninst && k < vK) ? ((gi64*)rowmap)[k] : -1;
+    }
+#pragma unroll
+    for (int m = 0; m < kKmMax; ++m) {
+      const int t = w + 4 * m;
+      if (t < ninst) {
+        const uint32_t voff = (gr[m] >= 0 && c < vc) ? (uint32_t)((gr[m] * ld + c0 + c) * 4) : kOob;
+        dma16(rs, dst + t * 256, voff, coh);
+      }
+    }
+    return;
+  }
   for (int t = w; t < ninst; t += 4) {
     const int k = t * rows_per + kr;
-    uint32_t voff = kOob;
-    if (k < vK && c < vc) {
-      const int64_t gr = rowmap ? rowmap[k] : (int64_t)k;
-      voff = (uint32_t)((gr * ld + c0 + c) * 4);
-    }
+    const uint32_t voff = (k < vK && c < vc) ? (uint32_t)(((int64_t)k * ld + c0 + c) * 4) : kOob;
     dma16(rs, dst + t * 256, voff, coh);
   }
 }
@@ -322,16 +344,70 @@ XA_DEV bool dma_src(const XSrc& x) {
   return x.p1 == nullptr && (x.w0 & 3) == 0 && (x.ld0 & 3) == 0;
 }
 
-// the dZ2 former's LDS inputs: W3 rows [k0, k0 + nk) (n3 each) and d3 rows [r0, r0 + nr)
-// (scalar loads; the caller's dma_wait orders them)
-XA_DEV void stage_dz_aux(const Lds& s, const DZ& d, int k0, int nk, int r0, int nr) {
-  if (!d.h2) return;
-  for (int e = threadIdx.x; e < nk * d.n3; e += 256) s.aux[e] = ldc(d.w3 + k0 * d.n3 + e);
-  float* sd = s.aux + 2048;
-  if (d.d3)
-    for (int e = threadIdx.x; e < nr * d.n3; e += 256) sd[e] = ldc(d.d3 + r0 * d.n3 + e);
+// the dZ2 former's LDS inputs: W3 rows [k0, k0 + nk) (n3 each, nk n3 <= 2048) and d3 rows
+// [r0, r0 + nr) (nr n3 <= 1024), loaded into registers by aux_load BEFORE the tile's DMA is
+// issued and written to LDS by aux_store after it (only the aux loads are waited for there)
+struct AuxRegs {
+  float w[8], d[4];
+};
+XA_DEV AuxRegs aux_load(const DZ& d, int k0, int nk, int r0, int nr) {
+  AuxRegs a;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int e = threadIdx.x + 256 * u;
+    a.w[u] = (d.h2 && e < nk * d.n3) ? ldc(d.w3 + k0 * d.n3 + e) : 0.0f;
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int e = threadIdx.x + 256 * u;
+    a.d[u] = (d.h2 && d.d3 && e < nr * d.n3) ? ldc(d.d3 + r0 * d.n3 + e) : 0.0f;
+  }
+  return a;
 }
-// dZ2[r][k] from the staged aux (k relative to the aux's k0, r relative to its r0)
+XA_DEV void aux_store(const Lds& s, const DZ& d, const AuxRegs& a, int nk, int nr) {
+  if (!d.h2) return;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int e = threadIdx.x + 256 * u;
+    if (e < nk * d.n3) s.aux[e] = a.w[u];
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int e = threadIdx.x + 256 * u;
+    if (d.d3 && e < nr * d.n3) s.aux[2048 + e] = a.d[u];
+  }
+}
+// dZ2 = g(r, k) (h > 0) for 4 consecutive values of one row / one sample (the aux tables
+// indexed relative to the tile: kk = first of the 4 columns, rr = the row)
+template <int N3>  // N3 = 0: the width d.n3 at run time
+XA_DEV float4 dz_form4(const Lds& s, const DZ& d, float4 h, int rr, int kk) {
+  const int n3 = N3 > 0 ? N3 : d.n3;
+  float g[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const float* w = s.aux + (kk + u) * n3;
+    if (d.d3) {
+      const float* dr = s.aux + 2048 + rr * n3;
+      float t = dr[0] * w[0];
+      if constexpr (N3 > 0) {
+#pragma unroll
+        for (int a = 1; a < N3; ++a) t = fmaf(dr[a], w[a], t);
+      } else {
+        for (int a = 1; a < n3; ++a) t = fmaf(dr[a], w[a], t);
+      }
+      g[u] = t;
+    } else {
+      g[u] = d.c3 * w[0];
+    }
+  }
+  return make_float4(h.x > 0.0f ? g[0] : 0.0f, h.y > 0.0f ? g[1] : 0.0f,
+                     h.z > 0.0f ? g[2] : 0.0f, h.w > 0.0f ? g[3] : 0.0f);
+}
+XA_DEV float4 dz_form4(const Lds& s, const DZ& d, float4 h, int rr, int kk) {
+  return d.n3 == 1 ? dz_form4<1>(s, d, h, rr, kk)
+         : d.n3 == 4 ? dz_form4<4>(s, d, h, rr, kk) : dz_form4<0>(s, d, h, rr, kk);
+}
+// scalar form (the non-vector staging paths)
 XA_DEV float dz_form(const Lds& s, const DZ& d, float h, int rr, int kk) {
   float g;
   if (d.d3) {
@@ -439,6 +515,7 @@ __device__ __noinline__ f32x4v dx_tile(DZ d, int r0, int B, const float* W, int 
   dstamp(0);
   const int Kp = pad16(K), nrows = min(kRows, B - r0);
   const float* src = d.h2 ? d.h2 : d.buf;
+  const AuxRegs ax = aux_load(d, 0, K, r0, nrows);
   if ((K & 3) == 0 && (d.ld & 3) == 0)
     dma_cr(s.A, kRows, src, d.ld, r0, nullptr, nrows, K, Kp, true);
   else
@@ -449,13 +526,17 @@ __device__ __noinline__ f32x4v dx_tile(DZ d, int r0, int B, const float* W, int 
   else
     sload(kCols, Kp, nc, K, [&](int j, int k) { return ldw(W + (int64_t)(c0 + j) * K + k, coh); },
           [&](int j, int k, float v) { s.B[cr_idx(j, k, kCols)] = v; });
-  stage_dz_aux(s, d, 0, K, r0, nrows);
+  aux_store(s, d, ax, K, nrows);
   dstamp(1);
   dma_wait();
   if (d.h2) {
-    for (int e = threadIdx.x; e < kRows * Kp; e += 256) {
-      const int kc = e >> 10, r = (e >> 4) & 63, k = 16 * kc + (e & 15);
-      if (r < nrows && k < K) s.A[e] = dz_form(s, d, s.A[e], r, k);
+    // 4 consecutive k of one row per float4 (K % 4 == 0 on this path)
+    for (int e4 = threadIdx.x; e4 < kRows * Kp / 4; e4 += 256) {
+      const int e = 4 * e4, kc = e >> 10, r = (e >> 4) & 63, k = 16 * kc + (e & 15);
+      if (r < nrows && k < K) {
+        float4* p = reinterpret_cast<float4*>(s.A + e);
+        *p = dz_form4(s, d, *p, r, k);
+      }
     }
     __syncthreads();
   }
@@ -473,6 +554,7 @@ __device__ __noinline__ f32x4v dw_tile(XSrc x, const int64_t* slots, DZ d, int i
   const Lds s = lds();
   dstamp(0);
   const int Kp = pad16(B);
+  const AuxRegs ax = aux_load(d, j0, nc, 0, B);
   if (dma_src(x) && (ni & 3) == 0 && (i0 & 3) == 0)
     dma_km(s.A, kRows, x.p0, x.ld0, i0, x.slot0 ? slots : nullptr, B, ni, Kp, x.coh0);
   else
@@ -484,13 +566,17 @@ __device__ __noinline__ f32x4v dw_tile(XSrc x, const int64_t* slots, DZ d, int i
   else
     sload(Kp, kCols, B, nc, [&](int k, int j) { return ldc(src + (int64_t)k * d.ld + j0 + j); },
           [&](int k, int j, float v) { s.B[k * kCols + j] = v; });
-  stage_dz_aux(s, d, j0, nc, 0, B);
+  aux_store(s, d, ax, nc, B);
   dstamp(1);
   dma_wait();
   if (d.h2) {
-    for (int e = threadIdx.x; e < Kp * kCols; e += 256) {
-      const int k = e >> 4, j = e & 15;
-      if (k < B && j < nc) s.B[e] = dz_form(s, d, s.B[e], k, j);
+    // 4 consecutive columns of one sample per float4 (nc % 4 == 0 on this path)
+    for (int e4 = threadIdx.x; e4 < Kp * kCols / 4; e4 += 256) {
+      const int k = e4 >> 2, j = 4 * (e4 & 3);
+      if (k < B && j < nc) {
+        float4* p = reinterpret_cast<float4*>(s.B + 4 * e4);
+        *p = dz_form4(s, d, *p, k, j);
+      }
     }
     __syncthreads();
   }
@@ -1046,11 +1132,12 @@ extern "C" int xa_td3_update(const XaTd3UpdateArgs* p, void* stream) {
   XA_CHECK_ARG(a.batch > 0 && a.obs_dim > 0 && a.act_dim > 0 && a.act_dim <= 16 && a.h1 > 0 &&
                    a.h2 > 0,
                "xa_td3_update: bad sizes");
-  XA_CHECK_ARG(a.batch <= kMaxK && a.h1 <= kMaxK && a.h2 <= kMaxK &&
+  XA_CHECK_ARG(a.batch <= 256 && a.h1 <= kMaxK && a.h2 <= kMaxK && a.h1 % 4 == 0 &&
+                   a.h2 % 4 == 0 &&
                    a.obs_dim + a.act_dim <= 64 && a.h2 * a.act_dim <= 2048 &&
                    a.batch * a.act_dim <= 1024,
-               "xa_td3_update: sizes beyond the kernel's tiles (batch, h1, h2 <= %d; obs + act "
-               "<= 64; h2 act, batch act <= 2048, 1024)",
+               "xa_td3_update: sizes beyond the kernel's tiles (batch <= 256; h1, h2 <= %d and "
+               "multiples of 4; obs + act <= 64; h2 act, batch act <= 2048, 1024)",
                kMaxK);
   XA_CHECK_ARG(a.ring_states && a.ring_new_states && a.ring_actions && a.ring_rewards &&
                    a.ring_dones && a.slots && a.workspace && a.dv1 && a.g_critic1 &&

@@ -215,7 +215,8 @@ class DDPG(OffPolicy):
         if self.actor.layers[0].in_features != S or self.critic.layers[0].in_features != S + A:
             return False
         B = self.batch_size
-        return max(B, h[0], h[1]) <= 416 and S + A <= 64 and h[1] * A <= 2048 and B * A <= 1024
+        return (B <= 256 and max(h) <= 416 and h[0] % 4 == 0 and h[1] % 4 == 0 and S + A <= 64
+                and h[1] * A <= 2048 and B * A <= 1024)
 
     def _fused_args(self):
         """The launch arguments of xa_td3_update (built once), or None when the fused step
