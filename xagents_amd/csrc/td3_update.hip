@@ -156,13 +156,17 @@ XA_DEV XSrc xcat(XSrc a, const float* p, int w, int ld, bool slot, bool coh) {
   a.coh1 = coh;
   return a;
 }
+// the batch's ring rows, copied to LDS at launch start (read per element by xload)
+__shared__ int64_t td3_slots[256];
+
 XA_DEV float xload(const XSrc& x, const int64_t* slots, int r, int k) {
+  (void)slots;
   if (k < x.w0) {
-    const int64_t row = x.slot0 ? slots[r] : r;
+    const int64_t row = x.slot0 ? td3_slots[r] : r;
     const float* p = x.p0 + row * x.ld0 + k;
     return x.coh0 ? ldc(p) : *p;
   }
-  const int64_t row = x.slot1 ? slots[r] : r;
+  const int64_t row = x.slot1 ? td3_slots[r] : r;
   const float* p = x.p1 + row * x.ld1 + (k - x.w0);
   return x.coh1 ? ldc(p) : *p;
 }
@@ -423,28 +427,39 @@ XA_DEV float dz_form(const Lds& s, const DZ& d, float h, int rr, int kk) {
 
 // ---- the tile product: wave w, rows 16 w .. 16 w + 15, 16 columns; K padded to 16 ----
 template <bool A_CR, bool B_CR>
+XA_DEV float4 mma_a(const Lds& s, int k0, int w, int i, int q) {
+  if constexpr (A_CR) {
+    return *reinterpret_cast<const float4*>(s.A + ((k0 >> 4) * kRows + 16 * w + i) * 16 + 4 * q);
+  } else {
+    const float* pa = s.A + (k0 + 4 * q) * kRows + 16 * w + i;
+    return make_float4(pa[0], pa[kRows], pa[2 * kRows], pa[3 * kRows]);
+  }
+}
+template <bool A_CR, bool B_CR>
+XA_DEV float4 mma_b(const Lds& s, int k0, int i, int q) {
+  if constexpr (B_CR) {
+    return *reinterpret_cast<const float4*>(s.B + ((k0 >> 4) * kCols + i) * 16 + 4 * q);
+  } else {
+    const float* pb = s.B + (k0 + 4 * q) * kCols + i;
+    return make_float4(pb[0], pb[kCols], pb[2 * kCols], pb[3 * kCols]);
+  }
+}
+// the next 16-deep chunk's operands are read from LDS while the current chunk's 4 MFMAs run
+template <bool A_CR, bool B_CR>
 XA_DEV f32x4v tile_mma(const Lds& s, int Kp) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int i = lane & 15, q = lane >> 4;
   f32x4v c0 = {0.0f, 0.0f, 0.0f, 0.0f}, c1 = {0.0f, 0.0f, 0.0f, 0.0f};
+  float4 a = mma_a<A_CR, B_CR>(s, 0, w, i, q), b = mma_b<A_CR, B_CR>(s, 0, i, q);
   for (int k0 = 0; k0 < Kp; k0 += 16) {
-    float4 a, b;
-    if constexpr (A_CR) {
-      a = *reinterpret_cast<const float4*>(s.A + ((k0 >> 4) * kRows + 16 * w + i) * 16 + 4 * q);
-    } else {
-      const float* pa = s.A + (k0 + 4 * q) * kRows + 16 * w + i;
-      a = make_float4(pa[0], pa[kRows], pa[2 * kRows], pa[3 * kRows]);
-    }
-    if constexpr (B_CR) {
-      b = *reinterpret_cast<const float4*>(s.B + ((k0 >> 4) * kCols + i) * 16 + 4 * q);
-    } else {
-      const float* pb = s.B + (k0 + 4 * q) * kCols + i;
-      b = make_float4(pb[0], pb[kCols], pb[2 * kCols], pb[3 * kCols]);
-    }
+    const int kn = k0 + 16 < Kp ? k0 + 16 : k0;
+    const float4 an = mma_a<A_CR, B_CR>(s, kn, w, i, q), bn = mma_b<A_CR, B_CR>(s, kn, i, q);
     c0 = mfma4(a.x, b.x, c0);
     c1 = mfma4(a.y, b.y, c1);
     c0 = mfma4(a.z, b.z, c0);
     c1 = mfma4(a.w, b.w, c1);
+    a = an;
+    b = bn;
   }
   return c0 + c1;
 }
@@ -480,17 +495,15 @@ __device__ __noinline__ f32x4v fwd_tile(XSrc x, const int64_t* slots, int r0, in
   else
     sload(Kp, kCols, K, nc, [&](int k, int j) { return ldw(W + (int64_t)k * N + c0 + j, coh); },
           [&](int k, int j, float v) { s.B[k * kCols + j] = v; });
+  const int c = c0 + out_col();
+  const float bv = c < N ? ldw(bias + c, coh) : 0.0f;  // (in flight with the operands)
   dstamp(1);
   dma_wait();
   dstamp(2);
   f32x4v acc = tile_mma<true, false>(s, Kp);
   dstamp(3);
-  const int c = c0 + out_col();
-  if (c < N) {
-    const float b = ldw(bias + c, coh);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) acc[r] = acc[r] + b;
-  }
+  for (int r = 0; r < 4; ++r) acc[r] = acc[r] + bv;
   return acc;
 }
 
@@ -605,6 +618,89 @@ XA_DEV void adam_one(const Net& n, float g, int i, float omb1, float omb2, float
   }
 }
 
+// Adam (+ Polyak) of parameters [lo, hi) from their raw gradients: every load of a thread's
+// elements issued before the first update (one memory round trip, not one per element)
+__device__ __noinline__ void adam_range(Net n, const float* grad, int lo, int hi, float omb1,
+                                        float omb2, float eps, float* target, float tau) {
+  constexpr int kA = 16;
+  for (int i0 = lo + (int)threadIdx.x; i0 < hi; i0 += 256 * kA) {
+    float g[kA], th[kA], m[kA], v[kA], tg[kA];
+#pragma unroll
+    for (int u = 0; u < kA; ++u) {
+      const int i = min(i0 + 256 * u, hi - 1);
+      g[u] = ldc(grad + i);
+      th[u] = ldc(n.th + i);
+      m[u] = n.m[i];
+      v[u] = n.v[i];
+      tg[u] = target ? target[i] : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < kA; ++u) {
+      const int i = i0 + 256 * u;
+      if (i >= hi) break;
+      adam_elem(g[u], th[u], m[u], v[u], n.alpha, omb1, omb2, eps);
+      stc(n.th + i, th[u]);
+      n.m[i] = m[u];
+      n.v[i] = v[u];
+      if (target) target[i] = tau == 1.0f ? th[u] : (1.0f - tau) * tg[u] + tau * th[u];
+    }
+  }
+}
+
+// ---- narrow outputs (N <= 4: the L3 heads, d pi): a row-dot form instead of a 16-column
+// MFMA tile that would be 1 / 16 - 1 / 4 useful. The 4 lanes of a quad share one row
+// r = r0 + 16 w + lane / 4 and split k (lane p: k = 16 t + 4 p .. + 3); every load of the
+// row is issued before the first product; quad sums end with the totals in all 4 lanes ----
+// Wt[n][k] (n < N, k < K, zeros up to Kp) into aux + off: fwd W [K][N] (rows = k) or
+// rows c0 .. c0 + N of W [in][K] (rows = the outputs)
+XA_DEV void stage_wt(const Lds& s, int off, const float* W, int K, int N, bool rows_are_k,
+                     int c0, bool coh) {
+  const int Kp = pad16(K);
+  for (int e = threadIdx.x; e < N * Kp; e += 256) {
+    const int n = e / Kp, k = e - n * Kp;
+    float v = 0.0f;
+    if (k < K) v = ldw(rows_are_k ? W + (int64_t)k * N + n : W + (int64_t)(c0 + n) * K + k, coh);
+    s.aux[off + e] = v;
+  }
+}
+constexpr int kNT = 26;  // 16-deep k chunks a lane may hold (K <= 416)
+__device__ __noinline__ f32x4v narrow_rows(const float* X, int ld, int r0, int nrows, int K,
+                                           int N, int off) {
+  const Lds s = lds();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int rl = 16 * w + (lane >> 2), pq = lane & 3, Kp = pad16(K), nt = Kp >> 4;
+  const __amdgpu_buffer_rsrc_t rs = rsrc(X);
+  const bool ok = rl < nrows;
+  float4 x[kNT];
+#pragma unroll
+  for (int t = 0; t < kNT; ++t) {
+    const int k = 16 * t + 4 * pq;
+    x[t] = (ok && t < nt && k < K) ? ld4c(rs, (uint32_t)(((int64_t)(r0 + rl) * ld + k) * 4))
+                                   : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  }
+  f32x4v acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+  for (int n = 0; n < 4; ++n) {
+    if (n >= N) continue;
+    const float* wt = s.aux + off + n * Kp + 4 * pq;
+    float a = 0.0f;
+#pragma unroll
+    for (int t = 0; t < kNT; ++t) {
+      if (t < nt) {
+        const float4 wv = *reinterpret_cast<const float4*>(wt + 16 * t);
+        a = fmaf(x[t].x, wv.x, a);
+        a = fmaf(x[t].y, wv.y, a);
+        a = fmaf(x[t].z, wv.z, a);
+        a = fmaf(x[t].w, wv.w, a);
+      }
+    }
+    a = a + __shfl_xor(a, 1);
+    a = a + __shfl_xor(a, 2);
+    acc[n] = a;
+  }
+  return acc;
+}
+
 // weight-gradient job: raw gradient into grad (W [nin][N] at offset w, bias at b when the
 // tile is the first of its column), optionally the Adam step (+ Polyak) of those elements
 XA_DEV void dw_job(const XSrc& x, const int64_t* slots, const DZ& d, int nin,
@@ -616,13 +712,37 @@ XA_DEV void dw_job(const XSrc& x, const int64_t* slots, const DZ& d, int nin,
   const float omb1 = opt ? 1.0f - opt->beta1 : 0.0f, omb2 = opt ? 1.0f - opt->beta2 : 0.0f;
   const float eps = opt ? opt->eps : 0.0f;
   const int j = out_col();
+  if (adam) {
+    // the 4 elements' parameter / moment / target loads together, then the updates
+    float th[4], m[4], v[4], tg[4];
+    int ee[4];
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int i = out_row(r);
-    if (i < ni && j < nc) {
-      const int e = w + (i0 + i) * N + j0 + j;
+    for (int r = 0; r < 4; ++r) {
+      const int i = out_row(r);
+      const bool ok = i < ni && j < nc;
+      ee[r] = ok ? w + (i0 + i) * N + j0 + j : -1;
+      const int e = ok ? ee[r] : w;
+      th[r] = ldc(adam->th + e);
+      m[r] = adam->m[e];
+      v[r] = adam->v[e];
+      tg[r] = target ? target[e] : 0.0f;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (ee[r] < 0) continue;
+      const int e = ee[r];
       stc(grad + e, acc[r]);
-      if (adam) adam_one(*adam, acc[r], e, omb1, omb2, eps, target, tau);
+      adam_elem(acc[r], th[r], m[r], v[r], adam->alpha, omb1, omb2, eps);
+      stc(adam->th + e, th[r]);
+      adam->m[e] = m[r];
+      adam->v[e] = v[r];
+      if (target) target[e] = tau == 1.0f ? th[r] : (1.0f - tau) * tg[r] + tau * th[r];
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = out_row(r);
+      if (i < ni && j < nc) stc(grad + w + (i0 + i) * N + j0 + j, acc[r]);
     }
   }
   if (first) {
@@ -769,6 +889,7 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
     td3_dslot = -1;
     td3_dbuf = ws.dtrace;
   }
+  for (int r = tid; r < p.batch; r += 256) td3_slots[r] = p.slots[r];
   __syncthreads();
   // networks (the Adam step sizes from the step counters as the launch finds them)
   const Net c1 = make_net(p.critic1, C, H1, H2, 1, true);
@@ -842,15 +963,15 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
       const int id = net_id(j / RT), rt = j % RT, r0 = rt * kRows;
       const Net n = net_of(id);
       const int N = n.out;
-      const f32x4v acc = fwd_tile(xsrc(ws.h2(id), H2, H2, false, true), slots, r0, B,
-                                  n.th + n.w3, n.th + n.b3, H2, N, 0, false);
-      const int c = out_col();
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = r0 + out_row(r);
-        if (row >= B || c >= N) continue;
+      stage_wt(lds(), 0, n.th + n.w3, H2, N, true, 0, false);
+      __syncthreads();
+      const f32x4v acc = narrow_rows(ws.h2(id), H2, r0, min(kRows, B - r0), H2, N, 0);
+      const int row = r0 + 16 * (tid >> 6) + ((tid & 63) >> 2), c = tid & 3;
+      if (row < B && c < N) {
+        const float z = (c == 0 ? acc[0] : c == 1 ? acc[1] : c == 2 ? acc[2] : acc[3]) +
+                        n.th[n.b3 + c];
         if (id == N_TA) {
-          float a = xa_tanhf(acc[r]);
+          float a = xa_tanhf(z);
           if (p.smooth) {
             float nz = 0.0f;
             if (p.noise_sigma != 0.0f) {
@@ -862,9 +983,9 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
           }
           stc(ws.ta + row * A + c, a);
         } else if (id == N_AC) {
-          stc(ws.pa + row * A + c, xa_tanhf(acc[r]));
+          stc(ws.pa + row * A + c, xa_tanhf(z));
         } else {
-          stc((id == N_C1 ? ws.v1 : ws.v2) + row, acc[r]);
+          stc((id == N_C1 ? ws.v1 : ws.v2) + row, z);
         }
       }
       __syncthreads();
@@ -894,22 +1015,19 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
   // ---- P6: target values and the TD head ----
   for (int j = b; j < RT; j += G) {
     if (tid == 0) td3_dslot = (b == 0 && j == b) ? 8 * (int)y.n : -1;
-    const int r0 = j * kRows;
-    const f32x4v t1 = fwd_tile(xsrc(ws.h2(N_TC1), H2, H2, false, true), slots, r0, B,
-                               tc1.th + tc1.w3, tc1.th + tc1.b3, H2, 1, 0, false);
+    const int r0 = j * kRows, nr = min(kRows, B - r0);
+    stage_wt(lds(), 0, tc1.th + tc1.w3, H2, 1, true, 0, false);
+    if (twin) stage_wt(lds(), kMaxK, tc2.th + tc2.w3, H2, 1, true, 0, false);
     __syncthreads();
-    f32x4v t2 = t1;
-    if (twin) {
-      t2 = fwd_tile(xsrc(ws.h2(N_TC2), H2, H2, false, true), slots, r0, B, tc2.th + tc2.w3,
-                    tc2.th + tc2.b3, H2, 1, 0, false);
-    }
-    if (out_col() == 0) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = r0 + out_row(r);
-        if (row >= B) continue;
-        const float tv = twin ? fminf(t1[r], t2[r]) : t1[r];
-        const int64_t sl = slots[row];
+    const f32x4v t1 = narrow_rows(ws.h2(N_TC1), H2, r0, nr, H2, 1, 0);
+    const f32x4v t2 = twin ? narrow_rows(ws.h2(N_TC2), H2, r0, nr, H2, 1, kMaxK) : t1;
+    if ((tid & 3) == 0) {
+      {
+        const int row = r0 + 16 * (tid >> 6) + ((tid & 63) >> 2);
+        if (row >= B) goto head_done;
+        const float tv = twin ? fminf(t1[0] + tc1.th[tc1.b3], t2[0] + tc2.th[tc2.b3])
+                              : t1[0] + tc1.th[tc1.b3];
+        const int64_t sl = td3_slots[row];
         const float yv = p.ring_rewards[sl] + ((1.0f - p.ring_dones[sl]) * p.gamma) * tv;
         const float hd = p.huber_delta;
         auto term = [hd](float e, float& d) {
@@ -931,6 +1049,7 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
         }
         if (p.loss_out) p.loss_out[row] = l;
       }
+    head_done:;
     }
     __syncthreads();
   }
@@ -993,8 +1112,7 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
       } else {
         const int lo = n.w2 + (q - n_w1) * chunk, hi = min(n.P, lo + chunk);
         const float omb1 = 1.0f - opt.beta1, omb2 = 1.0f - opt.beta2;
-        for (int i = lo + tid; i < hi; i += 256)
-          adam_one(n, ldc(grad + i), i, omb1, omb2, opt.eps, tgt, p.tau);
+        adam_range(n, grad, lo, hi, omb1, omb2, opt.eps, tgt, p.tau);
       }
       __syncthreads();
     }
@@ -1039,15 +1157,14 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
     for (int j = b; j < RT; j += G) {
       if (tid == 0) td3_dslot = (b == 0 && j == b) ? 8 * (int)y.n : -1;
       const int r0 = j * kRows;
-      const f32x4v acc = dx_tile(dz_buf(ws.dq1, H1), r0, B, c1.th + c1.w1, H1, S, A, true);
-      const int c = out_col();
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = r0 + out_row(r);
-        if (row < B && c < A) {
-          const float pv = ldc(ws.pa + row * A + c);
-          stc(ws.dz3 + row * A + c, acc[r] * (1.0f - pv * pv));
-        }
+      stage_wt(lds(), 0, c1.th + c1.w1, H1, A, false, S, true);
+      __syncthreads();
+      const f32x4v acc = narrow_rows(ws.dq1, H1, r0, min(kRows, B - r0), H1, A, 0);
+      const int row = r0 + 16 * (tid >> 6) + ((tid & 63) >> 2), c = tid & 3;
+      if (row < B && c < A) {
+        const float dp = c == 0 ? acc[0] : c == 1 ? acc[1] : c == 2 ? acc[2] : acc[3];
+        const float pv = ldc(ws.pa + row * A + c);
+        stc(ws.dz3 + row * A + c, dp * (1.0f - pv * pv));
       }
       __syncthreads();
     }
@@ -1096,9 +1213,7 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
         } else {
           const int lo = ac.w2 + (j - CT1) * chunk, hi = min(ac.P, lo + chunk);
           const float omb1 = 1.0f - p.actor.beta1, omb2 = 1.0f - p.actor.beta2;
-          for (int i = lo + tid; i < hi; i += 256)
-            adam_one(ac, ldc(p.g_actor + i), i, omb1, omb2, p.actor.eps, p.target_actor.theta,
-                     p.tau);
+          adam_range(ac, p.g_actor, lo, hi, omb1, omb2, p.actor.eps, p.target_actor.theta, p.tau);
         }
         __syncthreads();
       }
@@ -1150,7 +1265,7 @@ extern "C" int xa_td3_update(const XaTd3UpdateArgs* p, void* stream) {
   int cus = 256, dev = 0;
   if (hipGetDevice(&dev) == hipSuccess)
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  const int G = a.n_blocks > 0 ? min(a.n_blocks, cus) : min(128, cus);
+  const int G = a.n_blocks > 0 ? min(a.n_blocks, cus) : min(256, cus);
   const size_t lds = sizeof(float) * ((size_t)(kRows + kCols) * kMaxK + kAux);
   hipLaunchKernelGGL(td3_update_kernel, dim3(G), dim3(256), lds, (hipStream_t)stream, a);
   XA_CHECK_LAUNCH("xa_td3_update");
