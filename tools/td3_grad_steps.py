@@ -44,7 +44,7 @@ def main():
         for _ in range(20):
             agent.update_weights(1)
             torch.cuda.synchronize()
-            tr = agent._fused_ws[896:1024].cpu().numpy().view(np.uint64).astype(np.int64)
+            tr = agent._fused_ws[1536:1664].cpu().numpy().view(np.uint64).astype(np.int64)
             rows.append(tr)
         diffs = []
         for tr in rows:
@@ -58,7 +58,7 @@ def main():
         # inside block 0's first job of each phase: entry, loads issued, operands in LDS,
         # MFMA done (us after the phase's barrier), from the last launch
         tr = rows[-1]
-        dt = agent._fused_ws[1024:1024 + 8192].cpu().numpy().view(np.uint64).astype(np.int64)
+        dt = agent._fused_ws[2048:2048 + 8192].cpu().numpy().view(np.uint64).astype(np.int64)
         for p in range(len(d) - 1):
             pts = dt[8 * p:8 * p + 4]
             if (pts <= 0).any() or pts[0] < tr[0]:

@@ -52,7 +52,8 @@ typedef float f32x4v __attribute__((ext_vector_type(4)));
 constexpr int kRsrcWord3 = 0x00020000;  // raw buffer, gfx9-family resource word 3
 constexpr int kAuxSc1 = 16;             // buffer instruction aux bits: write-through (sc1)
 constexpr uint64_t kSpinTicks = 1000000000;  // 10 s of the 100 MHz wall clock per barrier
-constexpr int kRows = 64, kCols = 16;   // output tile of one job
+constexpr int kRows = 64, kCols = 16;   // weight-gradient / narrow job rows, tile columns
+constexpr int kTR = 32;                 // rows of a forward / input-gradient job
 constexpr int kMaxK = 416;              // largest GEMM depth (H1, H2, batch, in)
 constexpr int kAux = 2048 + 1024;       // LDS floats: W3 slice + dZ3 rows of the dZ2 former
 constexpr int kU = 8;                   // loads in flight per thread while staging
@@ -86,6 +87,10 @@ XA_DEV float4 ld4p(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
   return make_float4(v[0], v[1], v[2], v[3]);
 }
 XA_DEV float ldw(const float* p, bool coh) { return coh ? ldc(p) : *p; }
+// one 16-B write-through store (a vector store)
+XA_DEV void st4c(__amdgpu_buffer_rsrc_t r, uint32_t byte_off, f32x4v v) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, byte_off, 0, kAuxSc1);
+}
 
 XA_DEV float philox_normal(uint32_t i, uint32_t j, uint64_t ctr, uint64_t seed) {
   // the same draw as xa_noisy_actions (offpolicy.hip)
@@ -222,6 +227,8 @@ XA_DEV Lds lds() {
 }
 
 XA_DEV int pad16(int k) { return (k + 15) & ~15; }
+// the two k halves of a forward / input-gradient tile, row-major [kTR][16] each
+__shared__ __attribute__((aligned(16))) float td3_part[2 * 32 * 16];
 
 // (diagnostic) block 0 stamps the wall clock at points of the first job of every phase into
 // the workspace's detail trace (tools/td3_grad_steps.py): slot 8 p + point
@@ -476,64 +483,109 @@ XA_DEV float act_f(float v, int act) {
   return v;
 }
 
-// forward job: out[r][c] = act(X W + b) on rows [r0, r0 + 64) x cols [c0, c0 + 16)
-// (the tile functions are out of line: one copy each instead of one per call site)
-// forward tile: A = X rows (CR), B = W[k][c0 ..] (KM)
-__device__ __noinline__ f32x4v fwd_tile(XSrc x, const int64_t* slots, int r0, int B,
-                                        const float* W, const float* bias, int K, int N, int c0,
-                                        bool coh) {
+// ---- forward / input-gradient jobs: a kTR-row x 16-column output tile; wave w computes
+// rows 16 (w & 1) .. + 15 over the k chunks of half w >> 1 (the halves meet in LDS, summed
+// in a fixed order), then 128 threads finish one float4 of a row each: bias + activation or
+// the relu gate, one 16-B write-through store. Operands and the epilogue's inputs are all in
+// flight before the first wait ----
+XA_DEV float4 mma_a_tr(const Lds& s, int k0, int rb, int i, int q) {
+  return *reinterpret_cast<const float4*>(s.A + ((k0 >> 4) * kTR + 16 * rb + i) * 16 + 4 * q);
+}
+template <bool B_CR>
+XA_DEV void tile_mma_split(const Lds& s, int Kp) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int i = lane & 15, q = lane >> 4, rb = w & 1, kh = w >> 1;
+  const int nch = Kp >> 4, h0 = (nch + 1) >> 1;
+  const int lo = kh ? h0 : 0, hi = kh ? nch : h0;
+  f32x4v c0 = {0.0f, 0.0f, 0.0f, 0.0f}, c1 = {0.0f, 0.0f, 0.0f, 0.0f};
+  if (lo < hi) {
+    float4 a = mma_a_tr(s, 16 * lo, rb, i, q), b = mma_b<false, B_CR>(s, 16 * lo, i, q);
+    for (int c = lo; c < hi; ++c) {
+      const int kn = 16 * (c + 1 < hi ? c + 1 : c);
+      const float4 an = mma_a_tr(s, kn, rb, i, q), bn = mma_b<false, B_CR>(s, kn, i, q);
+      c0 = mfma4(a.x, b.x, c0);
+      c1 = mfma4(a.y, b.y, c1);
+      c0 = mfma4(a.z, b.z, c0);
+      c1 = mfma4(a.w, b.w, c1);
+      a = an;
+      b = bn;
+    }
+  }
+  const f32x4v acc = c0 + c1;
+  float* part = td3_part + kh * (kTR * kCols);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) part[(16 * rb + 4 * q + r) * kCols + i] = acc[r];
+  __syncthreads();
+}
+// the tile's float4 of thread t < 128: row t / 4, columns 4 (t % 4) .. + 3 (both halves)
+XA_DEV float4 tile_out4() {
+  const int t = threadIdx.x;
+  const float4 u = *reinterpret_cast<const float4*>(td3_part + 4 * t);
+  const float4 v = *reinterpret_cast<const float4*>(td3_part + kTR * kCols + 4 * t);
+  return make_float4(u.x + v.x, u.y + v.y, u.z + v.z, u.w + v.w);
+}
+
+// forward job: out[r][c] = act(X W + b) on rows [r0, r0 + kTR) x cols [c0, c0 + 16)
+// (A = X rows (CR), B = W[k][c0 ..] (KM); N % 4 == 0; the job functions are out of line:
+// one copy each instead of one per call site)
+__device__ __noinline__ void fwd_tile(XSrc x, const int64_t* slots, int r0, int B,
+                                      const float* W, const float* bias, int K, int N, int c0,
+                                      bool coh, int act, float* out) {
   const Lds s = lds();
   dstamp(0);
-  const int Kp = pad16(K), nrows = min(kRows, B - r0), nc = min(kCols, N - c0);
+  const int Kp = pad16(K), nrows = min(kTR, B - r0), nc = min(kCols, N - c0);
+  const int t = threadIdx.x, row = r0 + (t >> 2), c = c0 + 4 * (t & 3);
+  const bool st = t < 4 * kTR && row < B && c < N;
+  float4 bv = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  if (st) bv = coh ? ld4c(rsrc(bias), (uint32_t)(c * 4)) : *reinterpret_cast<const float4*>(bias + c);
   if (dma_src(x) && (K & 3) == 0)
-    dma_cr(s.A, kRows, x.p0, x.ld0, r0, x.slot0 ? slots + r0 : nullptr, nrows, K, Kp, x.coh0);
+    dma_cr(s.A, kTR, x.p0, x.ld0, r0, x.slot0 ? slots + r0 : nullptr, nrows, K, Kp, x.coh0);
   else
-    sload(kRows, Kp, nrows, K, [&](int r, int k) { return xload(x, slots, r0 + r, k); },
-          [&](int r, int k, float v) { s.A[cr_idx(r, k, kRows)] = v; });
+    sload(kTR, Kp, nrows, K, [&](int r, int k) { return xload(x, slots, r0 + r, k); },
+          [&](int r, int k, float v) { s.A[cr_idx(r, k, kTR)] = v; });
   if ((N & 3) == 0 && (c0 & 3) == 0 && (nc & 3) == 0)
     dma_km(s.B, kCols, W, N, c0, nullptr, K, nc, Kp, coh);
   else
     sload(Kp, kCols, K, nc, [&](int k, int j) { return ldw(W + (int64_t)k * N + c0 + j, coh); },
           [&](int k, int j, float v) { s.B[k * kCols + j] = v; });
-  const int c = c0 + out_col();
-  const float bv = c < N ? ldw(bias + c, coh) : 0.0f;  // (in flight with the operands)
   dstamp(1);
   dma_wait();
   dstamp(2);
-  f32x4v acc = tile_mma<true, false>(s, Kp);
+  tile_mma_split<false>(s, Kp);
   dstamp(3);
-#pragma unroll
-  for (int r = 0; r < 4; ++r) acc[r] = acc[r] + bv;
-  return acc;
+  if (st) {
+    const float4 z = tile_out4();
+    const f32x4v o = {act_f(z.x + bv.x, act), act_f(z.y + bv.y, act), act_f(z.z + bv.z, act),
+                      act_f(z.w + bv.w, act)};
+    st4c(rsrc(out), (uint32_t)(((int64_t)row * N + c) * 4), o);
+  }
 }
 
 XA_DEV void fwd_job(const XSrc& x, const int64_t* slots, int r0, int B, const float* W,
                     const float* bias, int K, int N, int c0, int act, float* out,
                     bool coh = false) {
-  const f32x4v acc = fwd_tile(x, slots, r0, B, W, bias, K, N, c0, coh);
-  const int c = c0 + out_col();
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int row = r0 + out_row(r);
-    if (row < B && c < N) stc(out + (int64_t)row * N + c, act_f(acc[r], act));
-  }
+  fwd_tile(x, slots, r0, B, W, bias, K, N, c0, coh, act, out);
 }
 
-// input-gradient tile: (dZ W^T)[r][c] on rows [r0, r0 + 64) x cols [c0, c0 + 16) of the layer
-// input (W row-major [in][K]): A = dZ rows (CR, the dZ2 former applied in LDS), B = W rows
-// c0 .. (CR)
-__device__ __noinline__ f32x4v dx_tile(DZ d, int r0, int B, const float* W, int K, int c0,
-                                       int nc, bool coh) {
+// input-gradient job: out[r][c] = (dZ W^T)[r][c] (gate[r][c] > 0) on rows [r0, r0 + kTR) x
+// cols [c0, c0 + 16) of the layer input (W row-major [in][K], out / gate [B][ld]):
+// A = dZ rows (CR, the dZ2 former applied in LDS), B = W rows c0 .. (CR)
+__device__ __noinline__ void dx_tile(DZ d, int r0, int B, const float* W, int K, int c0,
+                                     int nc, bool coh, const float* gate, float* out, int ld) {
   const Lds s = lds();
   dstamp(0);
-  const int Kp = pad16(K), nrows = min(kRows, B - r0);
+  const int Kp = pad16(K), nrows = min(kTR, B - r0);
+  const int t = threadIdx.x, row = r0 + (t >> 2), c = c0 + 4 * (t & 3);
+  const bool st = t < 4 * kTR && row < B && c < c0 + nc;
+  float4 gv = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  if (st) gv = ld4c(rsrc(gate), (uint32_t)(((int64_t)row * ld + c) * 4));
   const float* src = d.h2 ? d.h2 : d.buf;
   const AuxRegs ax = aux_load(d, 0, K, r0, nrows);
   if ((K & 3) == 0 && (d.ld & 3) == 0)
-    dma_cr(s.A, kRows, src, d.ld, r0, nullptr, nrows, K, Kp, true);
+    dma_cr(s.A, kTR, src, d.ld, r0, nullptr, nrows, K, Kp, true);
   else
-    sload(kRows, Kp, nrows, K, [&](int r, int k) { return ldc(src + (int64_t)(r0 + r) * d.ld + k); },
-          [&](int r, int k, float v) { s.A[cr_idx(r, k, kRows)] = v; });
+    sload(kTR, Kp, nrows, K, [&](int r, int k) { return ldc(src + (int64_t)(r0 + r) * d.ld + k); },
+          [&](int r, int k, float v) { s.A[cr_idx(r, k, kTR)] = v; });
   if ((K & 3) == 0)
     dma_cr(s.B, kCols, W, K, c0, nullptr, nc, K, Kp, coh);
   else
@@ -544,8 +596,8 @@ __device__ __noinline__ f32x4v dx_tile(DZ d, int r0, int B, const float* W, int 
   dma_wait();
   if (d.h2) {
     // 4 consecutive k of one row per float4 (K % 4 == 0 on this path)
-    for (int e4 = threadIdx.x; e4 < kRows * Kp / 4; e4 += 256) {
-      const int e = 4 * e4, kc = e >> 10, r = (e >> 4) & 63, k = 16 * kc + (e & 15);
+    for (int e4 = threadIdx.x; e4 < kTR * Kp / 4; e4 += 256) {
+      const int e = 4 * e4, kc = e / (kTR * 16), r = (e >> 4) & (kTR - 1), k = 16 * kc + (e & 15);
       if (r < nrows && k < K) {
         float4* p = reinterpret_cast<float4*>(s.A + e);
         *p = dz_form4(s, d, *p, r, k);
@@ -554,16 +606,26 @@ __device__ __noinline__ f32x4v dx_tile(DZ d, int r0, int B, const float* W, int 
     __syncthreads();
   }
   dstamp(2);
-  const f32x4v acc = tile_mma<true, true>(s, Kp);
+  tile_mma_split<true>(s, Kp);
   dstamp(3);
-  return acc;
+  if (st) {
+    const float4 z = tile_out4();
+    const f32x4v o = {gv.x > 0.0f ? z.x : 0.0f, gv.y > 0.0f ? z.y : 0.0f,
+                      gv.z > 0.0f ? z.z : 0.0f, gv.w > 0.0f ? z.w : 0.0f};
+    st4c(rsrc(out), (uint32_t)(((int64_t)row * ld + c) * 4), o);
+  }
 }
 
-// weight-gradient tile: D[i][j] = sum_k X[k][i0 + i] dZ[k][j0 + j] (i < ni, j < nc, k < B):
-// A = X rows (KM, width 64), B = dZ rows (KM, width 16); the bias gradient
-// sum_k dZ[k][j0 + j] (fixed k order) lands in bsum[j] when bsum != 0
-__device__ __noinline__ f32x4v dw_tile(XSrc x, const int64_t* slots, DZ d, int i0, int ni,
-                                       int j0, int nc, int B, float* bsum) {
+// weight-gradient tiles: D_t[i][j] = sum_k X[k][i0 + i] dZ[k][j0 + 16 t + j] for nt <= 4
+// column tiles t sharing the staged A (i < ni, columns < nc of the nt x 16, k < B):
+// A = X rows (KM, width 64), B = dZ rows (nt KM tiles of width 16); the bias gradients
+// sum_k dZ[k][j0 + j] (fixed k order) land in bsum[j] when bsum != 0
+struct Acc4 {
+  f32x4v t[4];
+};
+constexpr int kMaxDwTiles = 4;
+__device__ __noinline__ Acc4 dw_tile(XSrc x, const int64_t* slots, DZ d, int i0, int ni, int j0,
+                                     int nc, int nt, int B, float* bsum) {
   const Lds s = lds();
   dstamp(0);
   const int Kp = pad16(B);
@@ -574,18 +636,24 @@ __device__ __noinline__ f32x4v dw_tile(XSrc x, const int64_t* slots, DZ d, int i
     sload(Kp, kRows, B, ni, [&](int k, int i) { return xload(x, slots, k, i0 + i); },
           [&](int k, int i, float v) { s.A[k * kRows + i] = v; });
   const float* src = d.h2 ? d.h2 : d.buf;
-  if ((d.ld & 3) == 0 && (j0 & 3) == 0 && (nc & 3) == 0)
-    dma_km(s.B, kCols, src, d.ld, j0, nullptr, B, nc, Kp, true);
-  else
-    sload(Kp, kCols, B, nc, [&](int k, int j) { return ldc(src + (int64_t)k * d.ld + j0 + j); },
-          [&](int k, int j, float v) { s.B[k * kCols + j] = v; });
+  const bool vec = (d.ld & 3) == 0 && (j0 & 3) == 0 && (nc & 3) == 0;
+  for (int t = 0; t < nt; ++t) {
+    float* bt = s.B + t * Kp * kCols;
+    const int jt = j0 + kCols * t, nct = min(kCols, nc - kCols * t);
+    if (vec)
+      dma_km(bt, kCols, src, d.ld, jt, nullptr, B, nct, Kp, true);
+    else
+      sload(Kp, kCols, B, nct, [&](int k, int j) { return ldc(src + (int64_t)k * d.ld + jt + j); },
+            [&](int k, int j, float v) { bt[k * kCols + j] = v; });
+  }
   aux_store(s, d, ax, nc, B);
   dstamp(1);
   dma_wait();
   if (d.h2) {
     // 4 consecutive columns of one sample per float4 (nc % 4 == 0 on this path)
-    for (int e4 = threadIdx.x; e4 < Kp * kCols / 4; e4 += 256) {
-      const int k = e4 >> 2, j = 4 * (e4 & 3);
+    for (int e4 = threadIdx.x; e4 < nt * Kp * kCols / 4; e4 += 256) {
+      const int t = e4 / (Kp * kCols / 4), r4 = e4 - t * (Kp * kCols / 4);
+      const int k = r4 >> 2, j = kCols * t + 4 * (r4 & 3);
       if (k < B && j < nc) {
         float4* p = reinterpret_cast<float4*>(s.B + 4 * e4);
         *p = dz_form4(s, d, *p, k, j);
@@ -594,14 +662,25 @@ __device__ __noinline__ f32x4v dw_tile(XSrc x, const int64_t* slots, DZ d, int i
     __syncthreads();
   }
   if (bsum && threadIdx.x < nc) {
-    float t = 0.0f;
-    for (int k = 0; k < B; ++k) t += s.B[k * kCols + threadIdx.x];
-    bsum[threadIdx.x] = t;
+    const int t = threadIdx.x >> 4, j = threadIdx.x & 15;
+    const float* bt = s.B + t * Kp * kCols;
+    float acc = 0.0f;
+    for (int k = 0; k < B; ++k) acc += bt[k * kCols + j];
+    bsum[threadIdx.x] = acc;
   }
   dstamp(2);
-  const f32x4v acc = tile_mma<false, false>(s, Kp);
+  Acc4 r;
+#pragma unroll
+  for (int t = 0; t < kMaxDwTiles; ++t) {
+    r.t[t] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+    if (t < nt) {
+      Lds st = s;
+      st.B = s.B + t * Kp * kCols;
+      r.t[t] = tile_mma<false, false>(st, Kp);
+    }
+  }
   dstamp(3);
-  return acc;
+  return r;
 }
 
 // Keras Adam (+ Polyak into the target) of one parameter from its raw gradient
@@ -618,32 +697,54 @@ XA_DEV void adam_one(const Net& n, float g, int i, float omb1, float omb2, float
   }
 }
 
-// Adam (+ Polyak) of parameters [lo, hi) from their raw gradients: every load of a thread's
-// elements issued before the first update (one memory round trip, not one per element)
+// Adam (+ Polyak) of parameters [lo, hi) from their raw gradients (lo % 4 == 0 and every
+// array 16-B aligned): float4 groups, every load of a thread's groups issued before the
+// first update (one memory round trip, not one per element); the < 4 trailing elements
+// of the network scalar
+constexpr int kAdamG = 4;  // float4 groups per thread per round
+XA_DEV int adam_chunk(int rest, int jobs) {
+  const int per = 4 * 256;  // one group per thread
+  const int c = (rest + jobs - 1) / jobs;
+  return max(per, (c + per - 1) / per * per);
+}
 __device__ __noinline__ void adam_range(Net n, const float* grad, int lo, int hi, float omb1,
                                         float omb2, float eps, float* target, float tau) {
-  constexpr int kA = 16;
-  for (int i0 = lo + (int)threadIdx.x; i0 < hi; i0 += 256 * kA) {
-    float g[kA], th[kA], m[kA], v[kA], tg[kA];
+  const int hi4 = lo + ((hi - lo) & ~3);
+  const __amdgpu_buffer_rsrc_t rg = rsrc(grad), rt = rsrc(n.th);
+  for (int g0 = lo / 4 + (int)threadIdx.x; 4 * g0 < hi4; g0 += 256 * kAdamG) {
+    float4 g[kAdamG], th[kAdamG], m[kAdamG], v[kAdamG], tg[kAdamG];
 #pragma unroll
-    for (int u = 0; u < kA; ++u) {
-      const int i = min(i0 + 256 * u, hi - 1);
-      g[u] = ldc(grad + i);
-      th[u] = ldc(n.th + i);
-      m[u] = n.m[i];
-      v[u] = n.v[i];
-      tg[u] = target ? target[i] : 0.0f;
+    for (int u = 0; u < kAdamG; ++u) {
+      const int i = 4 * min(g0 + 256 * u, hi4 / 4 - 1);
+      g[u] = ld4c(rg, (uint32_t)i * 4u);
+      th[u] = ld4c(rt, (uint32_t)i * 4u);
+      m[u] = *reinterpret_cast<const float4*>(n.m + i);
+      v[u] = *reinterpret_cast<const float4*>(n.v + i);
+      tg[u] = target ? *reinterpret_cast<const float4*>(target + i) : make_float4(0, 0, 0, 0);
     }
 #pragma unroll
-    for (int u = 0; u < kA; ++u) {
-      const int i = i0 + 256 * u;
-      if (i >= hi) break;
-      adam_elem(g[u], th[u], m[u], v[u], n.alpha, omb1, omb2, eps);
-      stc(n.th + i, th[u]);
-      n.m[i] = m[u];
-      n.v[i] = v[u];
-      if (target) target[i] = tau == 1.0f ? th[u] : (1.0f - tau) * tg[u] + tau * th[u];
+    for (int u = 0; u < kAdamG; ++u) {
+      const int i = 4 * (g0 + 256 * u);
+      if (i >= hi4) break;
+      float* gp = &g[u].x;
+      float* tp = &th[u].x;
+      float* mp = &m[u].x;
+      float* vp = &v[u].x;
+      float* yp = &tg[u].x;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        adam_elem(gp[c], tp[c], mp[c], vp[c], n.alpha, omb1, omb2, eps);
+        yp[c] = tau == 1.0f ? tp[c] : (1.0f - tau) * yp[c] + tau * tp[c];
+      }
+      st4c(rt, (uint32_t)i * 4u, f32x4v{th[u].x, th[u].y, th[u].z, th[u].w});
+      *reinterpret_cast<float4*>(n.m + i) = m[u];
+      *reinterpret_cast<float4*>(n.v + i) = v[u];
+      if (target) *reinterpret_cast<float4*>(target + i) = tg[u];
     }
+  }
+  if ((int)threadIdx.x < hi - hi4) {
+    const int i = hi4 + threadIdx.x;
+    adam_one(n, ldc(grad + i), i, omb1, omb2, eps, target, tau);
   }
 }
 
@@ -701,48 +802,65 @@ __device__ __noinline__ f32x4v narrow_rows(const float* X, int ld, int r0, int n
   return acc;
 }
 
-// weight-gradient job: raw gradient into grad (W [nin][N] at offset w, bias at b when the
-// tile is the first of its column), optionally the Adam step (+ Polyak) of those elements
-XA_DEV void dw_job(const XSrc& x, const int64_t* slots, const DZ& d, int nin,
-                   int N, int i0, int j0, int B, float* grad, int w, int b, const Net* adam,
-                   const XaTdNet* opt, float* target, float tau, float* bsum_lds) {
-  const int ni = min(kRows, nin - i0), nc = min(kCols, N - j0);
+// weight-gradient job over columns [j0, j0 + 16 nt) of W [nin][N] (offset w; the bias at b
+// when the job holds the first in-feature tile): the raw gradient into grad, optionally the
+// Adam step (+ Polyak) of those elements
+// (the Adam options by value: no pointer into the kernel's private frame)
+struct AdamOpt {
+  float omb1, omb2, eps, tau;
+  float* target;
+  bool on;
+};
+XA_DEV AdamOpt adam_opt(const XaTdNet& o, float* target, float tau) {
+  return AdamOpt{1.0f - o.beta1, 1.0f - o.beta2, o.eps, tau, target, true};
+}
+XA_DEV AdamOpt no_adam() { return AdamOpt{0.0f, 0.0f, 0.0f, 0.0f, nullptr, false}; }
+XA_DEV void dw_job(const XSrc& x, const int64_t* slots, const DZ& d, int nin, int N, int i0,
+                   int j0, int nt, int B, float* grad, int w, int b, const Net& an,
+                   const AdamOpt& ao, float* bsum_lds) {
+  const int ni = min(kRows, nin - i0), nc = min(kCols * nt, N - j0);
+  nt = (nc + kCols - 1) / kCols;
   const bool first = i0 == 0;
-  const f32x4v acc = dw_tile(x, slots, d, i0, ni, j0, nc, B, first ? bsum_lds : nullptr);
-  const float omb1 = opt ? 1.0f - opt->beta1 : 0.0f, omb2 = opt ? 1.0f - opt->beta2 : 0.0f;
-  const float eps = opt ? opt->eps : 0.0f;
-  const int j = out_col();
-  if (adam) {
-    // the 4 elements' parameter / moment / target loads together, then the updates
-    float th[4], m[4], v[4], tg[4];
-    int ee[4];
+  const Acc4 acc = dw_tile(x, slots, d, i0, ni, j0, nc, nt, B, first ? bsum_lds : nullptr);
+  const float omb1 = ao.omb1, omb2 = ao.omb2, eps = ao.eps, tau = ao.tau;
+  float* const target = ao.target;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int i = out_row(r);
-      const bool ok = i < ni && j < nc;
-      ee[r] = ok ? w + (i0 + i) * N + j0 + j : -1;
-      const int e = ok ? ee[r] : w;
-      th[r] = ldc(adam->th + e);
-      m[r] = adam->m[e];
-      v[r] = adam->v[e];
-      tg[r] = target ? target[e] : 0.0f;
-    }
+  for (int t = 0; t < kMaxDwTiles; ++t) {
+    if (t >= nt) continue;
+    const int j = kCols * t + out_col();
+    if (ao.on) {
+      // the 4 elements' parameter / moment / target loads together, then the updates
+      float th[4], m[4], v[4], tg[4];
+      int ee[4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      if (ee[r] < 0) continue;
-      const int e = ee[r];
-      stc(grad + e, acc[r]);
-      adam_elem(acc[r], th[r], m[r], v[r], adam->alpha, omb1, omb2, eps);
-      stc(adam->th + e, th[r]);
-      adam->m[e] = m[r];
-      adam->v[e] = v[r];
-      if (target) target[e] = tau == 1.0f ? th[r] : (1.0f - tau) * tg[r] + tau * th[r];
-    }
-  } else {
+      for (int r = 0; r < 4; ++r) {
+        const int i = out_row(r);
+        const bool ok = i < ni && j < nc;
+        ee[r] = ok ? w + (i0 + i) * N + j0 + j : -1;
+        const int e = ok ? ee[r] : w;
+        th[r] = ldc(an.th + e);
+        m[r] = an.m[e];
+        v[r] = an.v[e];
+        tg[r] = target ? target[e] : 0.0f;
+      }
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int i = out_row(r);
-      if (i < ni && j < nc) stc(grad + w + (i0 + i) * N + j0 + j, acc[r]);
+      for (int r = 0; r < 4; ++r) {
+        if (ee[r] < 0) continue;
+        const int e = ee[r];
+        const float g = acc.t[t][r];
+        stc(grad + e, g);
+        adam_elem(g, th[r], m[r], v[r], an.alpha, omb1, omb2, eps);
+        stc(an.th + e, th[r]);
+        an.m[e] = m[r];
+        an.v[e] = v[r];
+        if (target) target[e] = tau == 1.0f ? th[r] : (1.0f - tau) * tg[r] + tau * th[r];
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = out_row(r);
+        if (i < ni && j < nc) stc(grad + w + (i0 + i) * N + j0 + j, acc.t[t][r]);
+      }
     }
   }
   if (first) {
@@ -751,32 +869,50 @@ XA_DEV void dw_job(const XSrc& x, const int64_t* slots, const DZ& d, int nin,
       const int e = b + j0 + threadIdx.x;
       const float g = bsum_lds[threadIdx.x];
       stc(grad + e, g);
-      if (adam) adam_one(*adam, g, e, omb1, omb2, eps, target, tau);
+      if (ao.on) adam_one(an, g, e, omb1, omb2, eps, target, tau);
     }
   }
 }
 
-// ---- the grid barrier ----
+// ---- the grid barrier: a counter sharded over 8 lines (block b adds to shard b % 8: 32
+// arrivals per line instead of 256 on one), polled by one lane per block as the sum of the
+// shards; only the blocks that held a job in the phase arrive (the rest only wait), so the
+// target grows by min(G, jobs) per barrier ----
+constexpr int kShards = 8, kShardStride = 32;  // u32 words between shards (128 B)
 struct Sync {
   unsigned* cnt;
   unsigned* abort_w;
-  unsigned base, G, n, epoch;
+  unsigned target, G, n, epoch;
   int* status;
   unsigned long long* trace;  // block 0 only: the wall clock as each barrier completes
 };
 
-XA_DEV bool grid_sync(Sync& y, int& lds_flag) {
+XA_DEV unsigned shard_sum(const unsigned* cnt) {
+  unsigned v[kShards];
+#pragma unroll
+  for (int s = 0; s < kShards; ++s)
+    v[s] = __hip_atomic_load((gu32*)(cnt + kShardStride * s), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+  unsigned t = 0;
+#pragma unroll
+  for (int s = 0; s < kShards; ++s) t += v[s];
+  return t;
+}
+
+XA_DEV bool grid_sync(Sync& y, int& lds_flag, int jobs) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   y.n += 1;
+  const unsigned m = (unsigned)min((int)y.G, max(jobs, 0));
+  y.target += m;
   if (threadIdx.x == 0) {
-    __hip_atomic_fetch_add((gu32*)y.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned target = y.base + y.n * y.G;
+    if (blockIdx.x < m)
+      __hip_atomic_fetch_add((gu32*)(y.cnt + kShardStride * (blockIdx.x % kShards)), 1u,
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     int ok = 1;
     const uint64_t t0 = wall_clock64();
     for (unsigned it = 0;; ++it) {
-      const unsigned c = __hip_atomic_load((gu32*)y.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if ((int)(c - target) >= 0) break;  // wrap-safe: the counter only grows
+      if ((int)(shard_sum(y.cnt) - y.target) >= 0) break;  // wrap-safe: the shards only grow
       if ((it & 15u) == 15u) {
         if (__hip_atomic_load((gu32*)y.abort_w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
             y.epoch) {
@@ -803,8 +939,8 @@ XA_DEV bool grid_sync(Sync& y, int& lds_flag) {
 
 // workspace: control words, then the activations / gradients of the step (floats)
 struct Ws {
-  unsigned* cnt;      // barrier counter (monotonic)
-  unsigned* base;     // the counter value at the start of the next launch
+  unsigned* cnt;      // barrier counter shards (monotonic)
+  unsigned* base;     // the shards' sum at the start of the next launch
   unsigned* abort_w;  // the epoch of a launch that timed out
   unsigned* epoch;    // launches so far
   unsigned long long* dtrace;  // [16][8] points inside block 0's first job of each phase
@@ -840,12 +976,12 @@ __host__ __device__ inline Ws carve(void* base_p, int B, int H1, int H2, int A) 
     off = align_up(off + bytes, 256);
     return q;
   };
-  unsigned* ctl = (unsigned*)take(1024);
-  w.cnt = ctl;
-  w.base = ctl + 64;
-  w.abort_w = ctl + 128;
-  w.epoch = ctl + 192;
-  w.trace = (unsigned long long*)(ctl + 224);
+  unsigned* ctl = (unsigned*)take(2048);  // bytes: [0, 1024) counter shards, 1024 base,
+  w.cnt = ctl;                              // 1152 abort, 1280 epoch, [1536, 1664) trace
+  w.base = ctl + 256;
+  w.abort_w = ctl + 288;
+  w.epoch = ctl + 320;
+  w.trace = (unsigned long long*)(ctl + 384);
   w.dtrace = (unsigned long long*)take(8192);
   w.h1s = align_up((size_t)B * H1, 64);
   w.h2s = align_up((size_t)B * H2, 64);
@@ -869,7 +1005,7 @@ enum { N_TA = 0, N_C1 = 1, N_C2 = 2, N_AC = 3, N_TC1 = 4, N_TC2 = 5 };
 
 __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
   __shared__ int s_flag;
-  __shared__ float s_bsum[kCols];
+  __shared__ float s_bsum[kCols * kMaxDwTiles];
   const int G = gridDim.x, b = blockIdx.x, tid = threadIdx.x;
   const int B = p.batch, S = p.obs_dim, A = p.act_dim, H1 = p.h1, H2 = p.h2;
   const int C = S + A;
@@ -878,7 +1014,7 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
   Sync y;
   y.cnt = ws.cnt;
   y.abort_w = ws.abort_w;
-  y.base = *ws.base;
+  y.target = *ws.base;
   y.epoch = *ws.epoch + 1u;
   y.G = (unsigned)G;
   y.n = 0;
@@ -889,35 +1025,59 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
     td3_dslot = -1;
     td3_dbuf = ws.dtrace;
   }
-  for (int r = tid; r < p.batch; r += 256) td3_slots[r] = p.slots[r];
-  __syncthreads();
-  // networks (the Adam step sizes from the step counters as the launch finds them)
+  // networks (the Adam step sizes from the step counters as the launch finds them; their
+  // loads in flight with the slot loads)
   const Net c1 = make_net(p.critic1, C, H1, H2, 1, true);
   const Net c2 = make_net(twin ? p.critic2 : p.critic1, C, H1, H2, 1, twin);
   const Net ac = make_net(p.actor, S, H1, H2, A, pol);
+  if (tid < p.batch) td3_slots[tid] = p.slots[tid];  // (batch <= 256)
+  __syncthreads();
   const Net tc1 = make_net(p.target_critic1, C, H1, H2, 1, false);
   const Net tc2 = make_net(twin ? p.target_critic2 : p.target_critic1, C, H1, H2, 1, false);
   const int64_t* slots = p.slots;
-  const int RT = (B + kRows - 1) / kRows;
+  const int RT = (B + kRows - 1) / kRows, RTT = (B + kTR - 1) / kTR;
   const int CT1 = (H1 + kCols - 1) / kCols, CT2 = (H2 + kCols - 1) / kCols;
+  // column tiles per weight-gradient job (they share the staged A; the B region holds
+  // kCols x kMaxK floats, one k-major [pad16(B)][16] tile per column tile)
+  const int NTW = max(1, min(kMaxDwTiles, (kCols * kMaxK) / (pad16(B) * kCols)));
+  const int CTW2 = (CT2 + NTW - 1) / NTW, CTW1 = (CT1 + NTW - 1) / NTW;
   const float* rs = p.ring_states;
   const float* rn = p.ring_new_states;
   const float* ra = p.ring_actions;
 
-  // the sampled batch for the caller (concat_buffer_samples' arrays), from the last block
+  // the sampled batch for the caller (concat_buffer_samples' arrays), from the last block:
+  // element e of [s | s' | a | r | d], every load of a thread in flight before its stores
   if (b == G - 1) {
-    for (int e = tid; e < B * S; e += 256) {
-      const int r = e / S, k = e - r * S;
-      p.out_s[e] = rs[slots[r] * S + k];
-      p.out_s2[e] = rn[slots[r] * S + k];
-    }
-    for (int e = tid; e < B * A; e += 256) {
-      const int r = e / A, k = e - r * A;
-      p.out_a[e] = ra[slots[r] * A + k];
-    }
-    for (int r = tid; r < B; r += 256) {
-      p.out_r[r] = p.ring_rewards[slots[r]];
-      p.out_d[r] = p.ring_dones[slots[r]];
+    const int nS = B * S, nA = B * A, tot = 2 * nS + nA + 2 * B;
+    constexpr int kGu = 16;
+    for (int e0 = tid; e0 < tot; e0 += 256 * kGu) {
+      float v[kGu];
+#pragma unroll
+      for (int u = 0; u < kGu; ++u) {
+        int e = e0 + 256 * u;
+        float x = 0.0f;
+        if (e < nS) {
+          x = rs[td3_slots[e / S] * S + e % S];
+        } else if ((e -= nS) < nS) {
+          x = rn[td3_slots[e / S] * S + e % S];
+        } else if ((e -= nS) < nA) {
+          x = ra[td3_slots[e / A] * A + e % A];
+        } else if ((e -= nA) < B) {
+          x = p.ring_rewards[td3_slots[e]];
+        } else if ((e -= B) < B) {
+          x = p.ring_dones[td3_slots[e]];
+        }
+        v[u] = x;
+      }
+#pragma unroll
+      for (int u = 0; u < kGu; ++u) {
+        int e = e0 + 256 * u;
+        if (e < nS) p.out_s[e] = v[u];
+        else if ((e -= nS) < nS) p.out_s2[e] = v[u];
+        else if ((e -= nS) < nA) p.out_a[e] = v[u];
+        else if ((e -= nA) < B) p.out_r[e] = v[u];
+        else if ((e -= B) < B) p.out_d[e] = v[u];
+      }
     }
   }
 
@@ -939,20 +1099,20 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
     return xcat(xsrc(rs, S, S, true, false), ra, A, A, true, false);  // [s, a]
   };
   for (int layer = 1; layer <= 2; ++layer) {
-    const int CT = layer == 1 ? CT1 : CT2, per = RT * CT;
+    const int CT = layer == 1 ? CT1 : CT2, per = RTT * CT;
     for (int j = b; j < nn * per; j += G) {
       if (tid == 0) td3_dslot = (b == 0 && j == b) ? 8 * (int)y.n : -1;
       const int id = net_id(j / per), rem = j % per, rt = rem / CT, ct = rem % CT;
       const Net n = net_of(id);
       if (layer == 1)
-        fwd_job(in_of(id), slots, rt * kRows, B, n.th + n.w1, n.th + n.b1, n.in, H1, ct * kCols,
+        fwd_job(in_of(id), slots, rt * kTR, B, n.th + n.w1, n.th + n.b1, n.in, H1, ct * kCols,
                 ACT_RELU, ws.h1(id));
       else
-        fwd_job(xsrc(ws.h1(id), H1, H1, false, true), slots, rt * kRows, B, n.th + n.w2,
+        fwd_job(xsrc(ws.h1(id), H1, H1, false, true), slots, rt * kTR, B, n.th + n.w2,
                 n.th + n.b2, H1, H2, ct * kCols, ACT_RELU, ws.h2(id));
       __syncthreads();
     }
-    if (!grid_sync(y, s_flag)) return;
+    if (!grid_sync(y, s_flag, nn * per)) return;
   }
 
   // ---- P3: L3 (target actor + smoothing, critic values, actor pi(s)) ----
@@ -990,26 +1150,26 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
       }
       __syncthreads();
     }
-    if (!grid_sync(y, s_flag)) return;
+    if (!grid_sync(y, s_flag, nn * RT)) return;
   }
 
   // ---- P4 / P5: target critics L1 on [s', a'], L2 ----
   const int nt = twin ? 2 : 1;
   for (int layer = 1; layer <= 2; ++layer) {
-    const int CT = layer == 1 ? CT1 : CT2, per = RT * CT;
+    const int CT = layer == 1 ? CT1 : CT2, per = RTT * CT;
     for (int j = b; j < nt * per; j += G) {
       if (tid == 0) td3_dslot = (b == 0 && j == b) ? 8 * (int)y.n : -1;
       const int id = N_TC1 + j / per, rem = j % per, rt = rem / CT, ct = rem % CT;
       const Net n = net_of(id);
       if (layer == 1)
         fwd_job(xcat(xsrc(rn, S, S, true, false), ws.ta, A, A, false, true), slots,
-                rt * kRows, B, n.th + n.w1, n.th + n.b1, C, H1, ct * kCols, ACT_RELU, ws.h1(id));
+                rt * kTR, B, n.th + n.w1, n.th + n.b1, C, H1, ct * kCols, ACT_RELU, ws.h1(id));
       else
-        fwd_job(xsrc(ws.h1(id), H1, H1, false, true), slots, rt * kRows, B, n.th + n.w2,
+        fwd_job(xsrc(ws.h1(id), H1, H1, false, true), slots, rt * kTR, B, n.th + n.w2,
                 n.th + n.b2, H1, H2, ct * kCols, ACT_RELU, ws.h2(id));
       __syncthreads();
     }
-    if (!grid_sync(y, s_flag)) return;
+    if (!grid_sync(y, s_flag, nt * per)) return;
   }
 
   // ---- P6: target values and the TD head ----
@@ -1053,12 +1213,12 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
     }
     __syncthreads();
   }
-  if (!grid_sync(y, s_flag)) return;
+  if (!grid_sync(y, s_flag, RT)) return;
 
   // ---- P7: critics backward (dW2 / db2, dH1, dW3 / db3) ----
   {
     const int IT1 = (H1 + kRows - 1) / kRows, IT2 = (H2 + kRows - 1) / kRows;
-    const int n_dx = RT * CT1, n_dw2 = IT1 * CT2, n_dw3 = IT2;
+    const int n_dx = RTT * CT1, n_dw2 = IT1 * CTW2, n_dw3 = IT2;
     const int per = n_dx + n_dw2 + n_dw3;  // the heavy input-gradient jobs first
     for (int j = b; j < nt * per; j += G) {
       if (tid == 0) td3_dslot = (b == 0 && j == b) ? 8 * (int)y.n : -1;
@@ -1069,36 +1229,32 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
       float* grad = ci ? p.g_critic2 : p.g_critic1;
       const DZ d2 = dz_h2(ws.h2(id), H2, n.th + n.w3, 1, dv, 0.0f);
       if (q < n_dx) {
-        const int rt = q / CT1, ct = q % CT1, r0 = rt * kRows, c0 = ct * kCols;
-        const f32x4v acc = dx_tile(d2, r0, B, n.th + n.w2, H2, c0, min(kCols, H1 - c0), false);
-        const int c = c0 + out_col();
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = r0 + out_row(r);
-          if (row < B && c < H1) {
-            const float g = ldc(ws.h1(id) + row * H1 + c) > 0.0f ? acc[r] : 0.0f;
-            stc(ws.dh1(ci) + row * H1 + c, g);
-          }
-        }
+        const int rt = q / CT1, ct = q % CT1, c0 = ct * kCols;
+        dx_tile(d2, rt * kTR, B, n.th + n.w2, H2, c0, min(kCols, H1 - c0), false, ws.h1(id),
+                ws.dh1(ci), H1);
       } else if (q < n_dx + n_dw2) {
-        const int t = q - n_dx, it = t / CT2, ct = t % CT2;
+        const int t = q - n_dx, it = t / CTW2, ct = t % CTW2;
         dw_job(xsrc(ws.h1(id), H1, H1, false, true), slots, d2, H1, H2, it * kRows,
-               ct * kCols, B, grad, n.w2, n.b2, nullptr, nullptr, nullptr, 0.0f, s_bsum);
+               ct * NTW * kCols, NTW, B, grad, n.w2, n.b2, n, no_adam(), s_bsum);
       } else {
         const int it = q - n_dx - n_dw2;
         dw_job(xsrc(ws.h2(id), H2, H2, false, true), slots, dz_buf(dv, 1), H2, 1, it * kRows,
-               0, B, grad, n.w3, n.b3, nullptr, nullptr, nullptr, 0.0f, s_bsum);
+               0, 1, B, grad, n.w3, n.b3, n, no_adam(), s_bsum);
       }
       __syncthreads();
     }
-    if (!grid_sync(y, s_flag)) return;
+    if (!grid_sync(y, s_flag, nt * per)) return;
   }
 
-  // ---- P8: critics dW1 / db1 + Adam, Adam of the rest (+ Polyak on policy steps) ----
+  // ---- P8: critics dW1 / db1 + Adam, Adam of the rest (+ Polyak on policy steps); the
+  // rest in chunks sized so the phase's jobs fill the grid ----
+  int p8_jobs;
   {
-    const int n_w1 = CT1;                       // one in-feature tile (C <= 64)
-    const int rest = c1.P - c1.w2, chunk = 4096, n_ad = (rest + chunk - 1) / chunk;
+    const int n_w1 = CTW1;                      // one in-feature tile (C <= 64)
+    const int rest = c1.P - c1.w2, chunk = adam_chunk(rest, max(1, (G - nt * n_w1) / nt));
+    const int n_ad = (rest + chunk - 1) / chunk;
     const int per = n_w1 + n_ad;
+    p8_jobs = nt * per;
     for (int j = b; j < nt * per; j += G) {
       if (tid == 0) td3_dslot = (b == 0 && j == b) ? 8 * (int)y.n : -1;
       const int ci = j / per, q = j % per;
@@ -1107,8 +1263,8 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
       float* grad = ci ? p.g_critic2 : p.g_critic1;
       float* tgt = pol ? (ci ? p.target_critic2.theta : p.target_critic1.theta) : nullptr;
       if (q < n_w1) {
-        dw_job(in_of(ci ? N_C2 : N_C1), slots, dz_buf(ws.dh1(ci), H1), C, H1, 0, q * kCols,
-               B, grad, n.w1, n.b1, &n, &opt, tgt, p.tau, s_bsum);
+        dw_job(in_of(ci ? N_C2 : N_C1), slots, dz_buf(ws.dh1(ci), H1), C, H1, 0,
+               q * NTW * kCols, NTW, B, grad, n.w1, n.b1, n, adam_opt(opt, tgt, p.tau), s_bsum);
       } else {
         const int lo = n.w2 + (q - n_w1) * chunk, hi = min(n.P, lo + chunk);
         const float omb1 = 1.0f - opt.beta1, omb2 = 1.0f - opt.beta2;
@@ -1119,40 +1275,34 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
   }
 
   if (pol) {
-    if (!grid_sync(y, s_flag)) return;
+    if (!grid_sync(y, s_flag, p8_jobs)) return;
     // ---- P9 / P10: critic 1 (updated) on [s, pi(s)] ----
     const XSrc spa = xcat(xsrc(rs, S, S, true, false), ws.pa, A, A, false, true);
     for (int layer = 1; layer <= 2; ++layer) {
       const int CT = layer == 1 ? CT1 : CT2;
-      for (int j = b; j < RT * CT; j += G) {
+      for (int j = b; j < RTT * CT; j += G) {
         if (tid == 0) td3_dslot = (b == 0 && j == b) ? 8 * (int)y.n : -1;
         const int rt = j / CT, ct = j % CT;
         if (layer == 1)
-          fwd_job(spa, slots, rt * kRows, B, c1.th + c1.w1, c1.th + c1.b1, C, H1, ct * kCols,
+          fwd_job(spa, slots, rt * kTR, B, c1.th + c1.w1, c1.th + c1.b1, C, H1, ct * kCols,
                   ACT_RELU, ws.q1, true);
         else
-          fwd_job(xsrc(ws.q1, H1, H1, false, true), slots, rt * kRows, B, c1.th + c1.w2,
+          fwd_job(xsrc(ws.q1, H1, H1, false, true), slots, rt * kTR, B, c1.th + c1.w2,
                   c1.th + c1.b2, H1, H2, ct * kCols, ACT_RELU, ws.q2, true);
         __syncthreads();
       }
-      if (!grid_sync(y, s_flag)) return;
+      if (!grid_sync(y, s_flag, RTT * CT)) return;
     }
     // ---- P11: dH1 of -mean Q (dQ / dv = -1 / B per row) ----
     const DZ dq2 = dz_h2(ws.q2, H2, c1.th + c1.w3, 1, nullptr, -1.0f / (float)B);
-    for (int j = b; j < RT * CT1; j += G) {
+    for (int j = b; j < RTT * CT1; j += G) {
       if (tid == 0) td3_dslot = (b == 0 && j == b) ? 8 * (int)y.n : -1;
-      const int rt = j / CT1, ct = j % CT1, r0 = rt * kRows, c0 = ct * kCols;
-      const f32x4v acc = dx_tile(dq2, r0, B, c1.th + c1.w2, H2, c0, min(kCols, H1 - c0), true);
-      const int c = c0 + out_col();
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = r0 + out_row(r);
-        if (row < B && c < H1)
-          stc(ws.dq1 + row * H1 + c, ldc(ws.q1 + row * H1 + c) > 0.0f ? acc[r] : 0.0f);
-      }
+      const int rt = j / CT1, ct = j % CT1, c0 = ct * kCols;
+      dx_tile(dq2, rt * kTR, B, c1.th + c1.w2, H2, c0, min(kCols, H1 - c0), true, ws.q1, ws.dq1,
+              H1);
       __syncthreads();
     }
-    if (!grid_sync(y, s_flag)) return;
+    if (!grid_sync(y, s_flag, RTT * CT1)) return;
     // ---- P12: d pi(s) = dH1 W1[S + a][:]^T, times tanh' -> the actor's output gradient ----
     for (int j = b; j < RT; j += G) {
       if (tid == 0) td3_dslot = (b == 0 && j == b) ? 8 * (int)y.n : -1;
@@ -1168,50 +1318,43 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
       }
       __syncthreads();
     }
-    if (!grid_sync(y, s_flag)) return;
+    if (!grid_sync(y, s_flag, RT)) return;
     // ---- P13: actor backward (dW2 / db2, dH1, dW3 / db3) ----
     {
       const int IT1 = (H1 + kRows - 1) / kRows, IT2 = (H2 + kRows - 1) / kRows;
-      const int n_dx = RT * CT1, n_dw2 = IT1 * CT2, n_dw3 = IT2;
+      const int n_dx = RTT * CT1, n_dw2 = IT1 * CTW2, n_dw3 = IT2;
       const DZ d2 = dz_h2(ws.h2(N_AC), H2, ac.th + ac.w3, A, ws.dz3, 0.0f);
       for (int j = b; j < n_dx + n_dw2 + n_dw3; j += G) {
         if (tid == 0) td3_dslot = (b == 0 && j == b) ? 8 * (int)y.n : -1;
         if (j < n_dx) {
-          const int rt = j / CT1, ct = j % CT1, r0 = rt * kRows, c0 = ct * kCols;
-          const f32x4v acc = dx_tile(d2, r0, B, ac.th + ac.w2, H2, c0, min(kCols, H1 - c0), false);
-          const int c = c0 + out_col();
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int row = r0 + out_row(r);
-            if (row < B && c < H1)
-              stc(ws.dh1a + row * H1 + c,
-                  ldc(ws.h1(N_AC) + row * H1 + c) > 0.0f ? acc[r] : 0.0f);
-          }
+          const int rt = j / CT1, ct = j % CT1, c0 = ct * kCols;
+          dx_tile(d2, rt * kTR, B, ac.th + ac.w2, H2, c0, min(kCols, H1 - c0), false,
+                  ws.h1(N_AC), ws.dh1a, H1);
         } else if (j < n_dx + n_dw2) {
-          const int t = j - n_dx, it = t / CT2, ct = t % CT2;
+          const int t = j - n_dx, it = t / CTW2, ct = t % CTW2;
           dw_job(xsrc(ws.h1(N_AC), H1, H1, false, true), slots, d2, H1, H2, it * kRows,
-                 ct * kCols, B, p.g_actor, ac.w2, ac.b2, nullptr, nullptr, nullptr, 0.0f, s_bsum);
+                 ct * NTW * kCols, NTW, B, p.g_actor, ac.w2, ac.b2, ac, no_adam(), s_bsum);
         } else {
           const int it = j - n_dx - n_dw2;
           dw_job(xsrc(ws.h2(N_AC), H2, H2, false, true), slots, dz_buf(ws.dz3, A), H2, A,
-                 it * kRows, 0, B, p.g_actor, ac.w3, ac.b3, nullptr, nullptr, nullptr, 0.0f,
-                 s_bsum);
+                 it * kRows, 0, 1, B, p.g_actor, ac.w3, ac.b3, ac, no_adam(), s_bsum);
         }
         __syncthreads();
       }
-      if (!grid_sync(y, s_flag)) return;
+      if (!grid_sync(y, s_flag, n_dx + n_dw2 + n_dw3)) return;
     }
     // ---- P14: actor dW1 / db1 + Adam + Polyak, Adam + Polyak of the rest ----
     {
-      const int rest = ac.P - ac.w2, chunk = 4096, n_ad = (rest + chunk - 1) / chunk;
-      for (int j = b; j < CT1 + n_ad; j += G) {
+      const int rest = ac.P - ac.w2, chunk = adam_chunk(rest, max(1, G - CTW1));
+      const int n_ad = (rest + chunk - 1) / chunk;
+      for (int j = b; j < CTW1 + n_ad; j += G) {
         if (tid == 0) td3_dslot = (b == 0 && j == b) ? 8 * (int)y.n : -1;
-        if (j < CT1) {
+        if (j < CTW1) {
           dw_job(xsrc(rs, S, S, true, false), slots, dz_buf(ws.dh1a, H1), S, H1, 0,
-                 j * kCols, B, p.g_actor, ac.w1, ac.b1, &ac, &p.actor, p.target_actor.theta,
-                 p.tau, s_bsum);
+                 j * NTW * kCols, NTW, B, p.g_actor, ac.w1, ac.b1, ac,
+                 adam_opt(p.actor, p.target_actor.theta, p.tau), s_bsum);
         } else {
-          const int lo = ac.w2 + (j - CT1) * chunk, hi = min(ac.P, lo + chunk);
+          const int lo = ac.w2 + (j - CTW1) * chunk, hi = min(ac.P, lo + chunk);
           const float omb1 = 1.0f - p.actor.beta1, omb2 = 1.0f - p.actor.beta2;
           adam_range(ac, p.g_actor, lo, hi, omb1, omb2, p.actor.eps, p.target_actor.theta, p.tau);
         }
@@ -1227,7 +1370,7 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
     if (twin) *p.critic2.step += 1;
     if (pol) *p.actor.step += 1;
     if (p.smooth && p.rng_counter) *p.rng_counter += 1ull;
-    *ws.base = y.base + y.n * y.G;
+    *ws.base = y.target;
     *ws.epoch = y.epoch;
     ws.trace[15] = wall_clock64();  // block 0's end (the last phase's tail may run on)
   }
