@@ -15,6 +15,7 @@
 #   prof     rocprofv3 --kernel-trace --stats of the default bench (no CPU baseline)
 #   pmc      FETCH_SIZE / WRITE_SIZE passes per shape (tools/gpurun_pmc_shapes.sh)
 #   c3 c4 c5 acer trpo   secondary bench lines
+#   c2g      C2 bench lines at update grids $C2_GS (XA_PPO_MAX_BLOCKS)
 #   profc3   rocprofv3 kernel trace of the C3 bench + per-(kernel, grid) summary
 #   gemm     GEMM tests, small-M timings, PMC passes on the dense dX GEMM
 #   icache   instruction-cache counters of the 16-env update
@@ -115,6 +116,27 @@ for step in "$@"; do
         > $R/gpurun_out/${T}_profc5g.log 2>&1) || exit $?
       python tools/kernel_shapes.py gpurun_out/${T}_profc5g/run_kernel_trace.csv 40 \
         > gpurun_out/${T}_profc5g_shapes.txt 2>&1 ;;
+    c2g)
+      # C2 update grid A/B: fewer workgroups with more tiles each (XA_PPO_MAX_BLOCKS)
+      for G in ${C2_GS:-256 128}; do
+        XA_PPO_MAX_BLOCKS=$G run c2g_$G 200 python bench.py --steps 30 --warmup 5 \
+          --cpu-baseline-seconds 0 --no-secondary
+      done
+      python tools/bench_brief.py gpurun_out/${T}_c2g_*.out ;;
+    td3pmc)
+      # instruction-fetch and wait counters of the fused TD3 launch (one pass each)
+      (cd /tmp && rocprofv3 -L > $R/gpurun_out/${T}_counters.txt 2>&1) || true
+      (cd /tmp && timeout -s KILL 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY \
+        SQ_WAIT_ANY SQ_IFETCH SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM -d $R/gpurun_out/${T}_td3pmc1 \
+        -o run --output-format csv -- python $R/tools/td3_grad_steps.py 10 \
+        > $R/gpurun_out/${T}_td3pmc1.log 2>&1) || exit 3
+      python tools/pmc_summary.py td3_update $(find gpurun_out/${T}_td3pmc1 -name "*counter_collection.csv") \
+        > gpurun_out/${T}_td3pmc.txt
+      (cd /tmp && timeout -s KILL 90 rocprofv3 --pmc SQC_ICACHE_MISSES SQC_ICACHE_HITS \
+        -d $R/gpurun_out/${T}_td3pmc2 -o run --output-format csv -- python $R/tools/td3_grad_steps.py 10 \
+        > $R/gpurun_out/${T}_td3pmc2.log 2>&1) || exit 4
+      python tools/pmc_summary.py td3_update $(find gpurun_out/${T}_td3pmc2 -name "*counter_collection.csv") \
+        >> gpurun_out/${T}_td3pmc.txt ;;
     c3) run c3 300 python bench.py --config c3 --steps 30 --warmup 5 ;;
     c4) run c4 400 python bench.py --config c4 --steps 4 --warmup 1 ;;
     c5) run c5 300 python bench.py --config c5 --steps 30 --warmup 5 ;;

@@ -41,7 +41,7 @@ def main():
         import numpy as np
         rows = []
         agent.use_graph = False
-        for _ in range(20):
+        for _ in range(40):
             agent.update_weights(1)
             torch.cuda.synchronize()
             tr = agent._fused_ws[1536:1664].cpu().numpy().view(np.uint64).astype(np.int64)
@@ -51,10 +51,15 @@ def main():
             n = int(np.count_nonzero(tr[1:15] > tr[0]))
             marks = np.asarray(list(tr[:n + 1]) + [tr[15]], np.float64)
             diffs.append(np.diff(marks) / 100.0)  # 100 MHz ticks -> us
+        # the launch's phases in barrier order (xa_td3_update's P-numbers: P3 / P6 / P12 run
+        # as the row tiles' last jobs of P2 / P5 / P11)
+        names = ['P1', 'P2', 'P4', 'P5', 'P7', 'P8', 'P9', 'P10', 'P11', 'P13', 'P14']
+        n_max = max(len(x) for x in diffs)
+        diffs = [x for x in diffs if len(x) == n_max]
         d = np.median(np.stack(diffs), 0)
-        print('fused phases (us, block 0, median of 20 eager launches): ' +
-              ' '.join(f'P{i + 1} {v:.1f}' for i, v in enumerate(d)) + f' | total {d.sum():.1f}',
-              flush=True)
+        print(f'fused phases (us, block 0, median of {len(diffs)} eager policy launches): ' +
+              ' '.join(f'{names[i] if i < len(names) else i} {v:.1f}' for i, v in enumerate(d)) +
+              f' | total {d.sum():.1f}', flush=True)
         # inside block 0's first job of each phase: entry, loads issued, operands in LDS,
         # MFMA done (us after the phase's barrier), from the last launch
         tr = rows[-1]
@@ -64,7 +69,7 @@ def main():
             if (pts <= 0).any() or pts[0] < tr[0]:
                 continue
             rel = (pts - tr[p]) / 100.0
-            print(f'  P{p + 1} job: entry {rel[0]:.2f} issued {rel[1]:.2f} ready {rel[2]:.2f} '
+            print(f'  {names[p] if p < len(names) else p} job: entry {rel[0]:.2f} issued {rel[1]:.2f} ready {rel[2]:.2f} '
                   f'mma {rel[3]:.2f} us', flush=True)
 
 

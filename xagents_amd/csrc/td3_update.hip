@@ -11,28 +11,32 @@
 // W2 [H1][H2], b2, W3 [H2][out], b3), batch rows r = the sampled transitions.
 //
 // G resident workgroups of 256 threads run the phases below; a phase's jobs are dealt
-// round-robin (job j -> workgroup j mod G) and a grid barrier separates the phases. A job
-// is one 64-row x 16-column output tile: both operands staged in LDS (zero padded to a
-// multiple of 16 along K), wave w computes rows 16 w .. 16 w + 15 on v_mfma_f32_16x16x4f32,
-// K in chunks of 16 (lane (i, q) reads k0 + 4q .. 4q + 3 of its row / column as one float4,
-// component s feeding MFMA step s: one consistent k order for A and B).
+// round-robin (job j -> workgroup j mod G) and a grid barrier separates the phases. A
+// forward / input-gradient job is one 32-row x 16-column output tile: both operands staged
+// in LDS by LDS-DMA (zero padded to a multiple of 16 along K), wave w computes rows
+// 16 (w & 1) .. + 15 over half w >> 1 of the k chunks on v_mfma_f32_16x16x4f32 (lane (i, q)
+// reads k0 + 4q .. 4q + 3 of its row / column as one float4, component s feeding MFMA step
+// s: one consistent k order for A and B), the halves summed in LDS. A weight-gradient job
+// is 64 in-features x up to 4 column tiles of 16 sharing the staged A.
 //   P1  L1 forward: target actor (s'), critic 1 / 2 ([s, a]), actor (s, policy steps)
-//   P2  L2 forward of the same networks
-//   P3  L3: target actor tanh (+ TD3 smoothing noise, clip) -> a'; critics -> v1, v2;
-//       actor tanh -> pi(s)
-//   P4  target critics L1 on [s', a'];  P5  L2
-//   P6  target critics L3 -> tv1, tv2; TD head y = r + (1 - d) gamma min(tv1, tv2),
-//       dv = 2 (v - y) (MSE) or clip(v - y, +-delta) (opt-in Huber), per-sample loss
+//   P2  L2 forward of the same networks, + each tile's partial of the narrow L3 product;
+//       the last job of a row tile finishes L3: target actor tanh (+ TD3 smoothing noise,
+//       clip) -> a'; critics -> v1, v2; actor tanh -> pi(s)
+//   P4  target critics L1 on [s', a'];  P5  L2 (+ the L3 partials; the row tile's last job
+//       runs the TD head y = r + (1 - d) gamma min(tv1, tv2), dv = 2 (v - y) (MSE) or
+//       clip(v - y, +-delta) (opt-in Huber), per-sample loss)
 //   P7  critics backward: dW2 / db2 (dZ2 = dv W3^T gate(h2) formed while staging), dH1,
 //       dW3 / db3
 //   P8  critics: dW1 / db1 with the Keras Adam step applied in the same job, Adam of every
 //       other critic parameter (+ Polyak of the critic targets on policy steps)
 //   policy steps only:
 //   P9  critic 1 L1 on [s, pi(s)] (updated critic 1);  P10 L2
-//   P11 dH1 of -mean Q (dZ2 = -W3^T gate(h2) / B)
-//   P12 d pi = dH1 W1[s.. s + A]^T, times tanh' -> dZ3 of the actor
+//   P11 dH1 of -mean Q (dZ2 = -W3^T gate(h2) / B), + the partials of d pi = dH1 W1[s..s+A]^T;
+//       the row tile's last job forms the actor's output gradient d pi (1 - pi^2)
 //   P13 actor backward: dW2 / db2, dH1, dW3 / db3
 //   P14 actor dW1 / db1 + Adam + Polyak, Adam + Polyak of the other actor parameters
+// (the phases once numbered P3, P6 and P12 -- the narrow L3 / TD-head / d pi products --
+// run as the row tiles' last jobs of P2, P5 and P11: a ticket per row tile, no barrier)
 // Hand-offs follow MI355X_MICROARCH.md's visibility table row 1: every in-launch produced
 // word (activations, gradients, updated parameters) is stored write-through (sc1) and
 // loaded with sc1 loads; a barrier drains (vmcnt 0), joins the workgroup and ONE lane adds
@@ -483,6 +487,77 @@ XA_DEV float act_f(float v, int act) {
   return v;
 }
 
+// ---- narrow follow-on products (the L3 heads, d pi) as column-tile partials: a forward /
+// input-gradient job also sums its 16 columns' share of out[r][n] = sum_c y[r][c] Wh(c, n)
+// (Wh(c, n) = w[c sc + n sn], n < nh <= 4) into hp[(ct B + r) nh + n]; the job that
+// completes a row tile's set (its add to the tile's ticket returned per - 1) finishes the
+// product from the partials (fixed column-tile order) before it reaches the grid barrier,
+// so the phase that used to compute these products is gone ----
+struct Head {
+  const float* w;  // null: no head
+  float* hp;
+  unsigned* ticket;
+  int sc, sn, nh, ct, per;
+  bool coh;
+};
+XA_DEV Head no_head() { return Head{nullptr, nullptr, nullptr, 0, 0, 0, 0, 1, false}; }
+__shared__ int td3_last;
+// thread t < 4 kTR holds y[row][c .. c + 3] (zeros outside the tile): its quad's sum
+// (lanes t ^ 1, t ^ 2) is the 16-column partial of every n; lane n of the quad stores n
+XA_DEV bool head_partial(const Head& h, const float (&wv)[4][4], float4 y, int row, int B) {
+  if (!h.w) return false;
+  const int t = threadIdx.x;
+  float pn[4];
+#pragma unroll
+  for (int n = 0; n < 4; ++n) {
+    float a = y.x * wv[n][0];
+    a = fmaf(y.y, wv[n][1], a);
+    a = fmaf(y.z, wv[n][2], a);
+    a = fmaf(y.w, wv[n][3], a);
+    a = a + __shfl_xor(a, 1);
+    a = a + __shfl_xor(a, 2);
+    pn[n] = a;
+  }
+  const int q = t & 3;
+  if (t < 4 * kTR && row < B && q < h.nh)
+    stc(h.hp + ((int64_t)h.ct * B + row) * h.nh + q,
+        q == 0 ? pn[0] : q == 1 ? pn[1] : q == 2 ? pn[2] : pn[3]);
+  // the ticket: every storing wave drained, then one add for the workgroup
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0) {
+    const unsigned old = __hip_atomic_fetch_add((gu32*)h.ticket, 1u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+    const bool last = old + 1u == (unsigned)h.per;
+    // the set is complete: the next launch's adds start from zero
+    if (last) __hip_atomic_store((gu32*)h.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    td3_last = last;
+  }
+  __syncthreads();
+  return td3_last != 0;
+}
+XA_DEV void head_weights(const Head& h, int c, bool on, float (&wv)[4][4]) {
+#pragma unroll
+  for (int n = 0; n < 4; ++n)
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      wv[n][u] = (h.w && on && n < h.nh) ? ldw(h.w + (int64_t)(c + u) * h.sc + (int64_t)n * h.sn, h.coh)
+                                          : 0.0f;
+}
+constexpr int kMaxCT = (kMaxK + 15) / 16;
+// the finished product of (row, n): the column-tile partials summed in tile order
+__device__ __noinline__ float head_total(const float* hp, int CT, int B, int nh, int row, int n) {
+  float v[kMaxCT];
+#pragma unroll
+  for (int u = 0; u < kMaxCT; ++u)
+    v[u] = u < CT ? ldc(hp + ((int64_t)u * B + row) * nh + n) : 0.0f;
+  float a = v[0];
+#pragma unroll
+  for (int u = 1; u < kMaxCT; ++u)
+    if (u < CT) a = a + v[u];
+  return a;
+}
+
 // ---- forward / input-gradient jobs: a kTR-row x 16-column output tile; wave w computes
 // rows 16 (w & 1) .. + 15 over the k chunks of half w >> 1 (the halves meet in LDS, summed
 // in a fixed order), then 128 threads finish one float4 of a row each: bias + activation or
@@ -528,9 +603,9 @@ XA_DEV float4 tile_out4() {
 // forward job: out[r][c] = act(X W + b) on rows [r0, r0 + kTR) x cols [c0, c0 + 16)
 // (A = X rows (CR), B = W[k][c0 ..] (KM); N % 4 == 0; the job functions are out of line:
 // one copy each instead of one per call site)
-__device__ __noinline__ void fwd_tile(XSrc x, const int64_t* slots, int r0, int B,
+__device__ __noinline__ bool fwd_tile(XSrc x, const int64_t* slots, int r0, int B,
                                       const float* W, const float* bias, int K, int N, int c0,
-                                      bool coh, int act, float* out) {
+                                      bool coh, int act, float* out, Head h) {
   const Lds s = lds();
   dstamp(0);
   const int Kp = pad16(K), nrows = min(kTR, B - r0), nc = min(kCols, N - c0);
@@ -538,6 +613,8 @@ __device__ __noinline__ void fwd_tile(XSrc x, const int64_t* slots, int r0, int 
   const bool st = t < 4 * kTR && row < B && c < N;
   float4 bv = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   if (st) bv = coh ? ld4c(rsrc(bias), (uint32_t)(c * 4)) : *reinterpret_cast<const float4*>(bias + c);
+  float wv[4][4];
+  head_weights(h, c, st, wv);
   if (dma_src(x) && (K & 3) == 0)
     dma_cr(s.A, kTR, x.p0, x.ld0, r0, x.slot0 ? slots + r0 : nullptr, nrows, K, Kp, x.coh0);
   else
@@ -553,25 +630,28 @@ __device__ __noinline__ void fwd_tile(XSrc x, const int64_t* slots, int r0, int 
   dstamp(2);
   tile_mma_split<false>(s, Kp);
   dstamp(3);
+  float4 y = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   if (st) {
     const float4 z = tile_out4();
-    const f32x4v o = {act_f(z.x + bv.x, act), act_f(z.y + bv.y, act), act_f(z.z + bv.z, act),
-                      act_f(z.w + bv.w, act)};
-    st4c(rsrc(out), (uint32_t)(((int64_t)row * N + c) * 4), o);
+    y = make_float4(act_f(z.x + bv.x, act), act_f(z.y + bv.y, act), act_f(z.z + bv.z, act),
+                    act_f(z.w + bv.w, act));
+    st4c(rsrc(out), (uint32_t)(((int64_t)row * N + c) * 4), f32x4v{y.x, y.y, y.z, y.w});
   }
+  return head_partial(h, wv, y, row, B);
 }
 
-XA_DEV void fwd_job(const XSrc& x, const int64_t* slots, int r0, int B, const float* W,
+XA_DEV bool fwd_job(const XSrc& x, const int64_t* slots, int r0, int B, const float* W,
                     const float* bias, int K, int N, int c0, int act, float* out,
-                    bool coh = false) {
-  fwd_tile(x, slots, r0, B, W, bias, K, N, c0, coh, act, out);
+                    bool coh = false, const Head& h = no_head()) {
+  return fwd_tile(x, slots, r0, B, W, bias, K, N, c0, coh, act, out, h);
 }
 
 // input-gradient job: out[r][c] = (dZ W^T)[r][c] (gate[r][c] > 0) on rows [r0, r0 + kTR) x
 // cols [c0, c0 + 16) of the layer input (W row-major [in][K], out / gate [B][ld]):
 // A = dZ rows (CR, the dZ2 former applied in LDS), B = W rows c0 .. (CR)
-__device__ __noinline__ void dx_tile(DZ d, int r0, int B, const float* W, int K, int c0,
-                                     int nc, bool coh, const float* gate, float* out, int ld) {
+__device__ __noinline__ bool dx_tile(DZ d, int r0, int B, const float* W, int K, int c0,
+                                     int nc, bool coh, const float* gate, float* out, int ld,
+                                     Head h) {
   const Lds s = lds();
   dstamp(0);
   const int Kp = pad16(K), nrows = min(kTR, B - r0);
@@ -579,6 +659,8 @@ __device__ __noinline__ void dx_tile(DZ d, int r0, int B, const float* W, int K,
   const bool st = t < 4 * kTR && row < B && c < c0 + nc;
   float4 gv = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   if (st) gv = ld4c(rsrc(gate), (uint32_t)(((int64_t)row * ld + c) * 4));
+  float wv[4][4];
+  head_weights(h, c, st, wv);
   const float* src = d.h2 ? d.h2 : d.buf;
   const AuxRegs ax = aux_load(d, 0, K, r0, nrows);
   if ((K & 3) == 0 && (d.ld & 3) == 0)
@@ -608,12 +690,14 @@ __device__ __noinline__ void dx_tile(DZ d, int r0, int B, const float* W, int K,
   dstamp(2);
   tile_mma_split<true>(s, Kp);
   dstamp(3);
+  float4 y = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   if (st) {
     const float4 z = tile_out4();
-    const f32x4v o = {gv.x > 0.0f ? z.x : 0.0f, gv.y > 0.0f ? z.y : 0.0f,
-                      gv.z > 0.0f ? z.z : 0.0f, gv.w > 0.0f ? z.w : 0.0f};
-    st4c(rsrc(out), (uint32_t)(((int64_t)row * ld + c) * 4), o);
+    y = make_float4(gv.x > 0.0f ? z.x : 0.0f, gv.y > 0.0f ? z.y : 0.0f,
+                    gv.z > 0.0f ? z.z : 0.0f, gv.w > 0.0f ? z.w : 0.0f);
+    st4c(rsrc(out), (uint32_t)(((int64_t)row * ld + c) * 4), f32x4v{y.x, y.y, y.z, y.w});
   }
+  return head_partial(h, wv, y, row, B);
 }
 
 // weight-gradient tiles: D_t[i][j] = sum_k X[k][i0 + i] dZ[k][j0 + 16 t + j] for nt <= 4
@@ -746,60 +830,6 @@ __device__ __noinline__ void adam_range(Net n, const float* grad, int lo, int hi
     const int i = hi4 + threadIdx.x;
     adam_one(n, ldc(grad + i), i, omb1, omb2, eps, target, tau);
   }
-}
-
-// ---- narrow outputs (N <= 4: the L3 heads, d pi): a row-dot form instead of a 16-column
-// MFMA tile that would be 1 / 16 - 1 / 4 useful. The 4 lanes of a quad share one row
-// r = r0 + 16 w + lane / 4 and split k (lane p: k = 16 t + 4 p .. + 3); every load of the
-// row is issued before the first product; quad sums end with the totals in all 4 lanes ----
-// Wt[n][k] (n < N, k < K, zeros up to Kp) into aux + off: fwd W [K][N] (rows = k) or
-// rows c0 .. c0 + N of W [in][K] (rows = the outputs)
-XA_DEV void stage_wt(const Lds& s, int off, const float* W, int K, int N, bool rows_are_k,
-                     int c0, bool coh) {
-  const int Kp = pad16(K);
-  for (int e = threadIdx.x; e < N * Kp; e += 256) {
-    const int n = e / Kp, k = e - n * Kp;
-    float v = 0.0f;
-    if (k < K) v = ldw(rows_are_k ? W + (int64_t)k * N + n : W + (int64_t)(c0 + n) * K + k, coh);
-    s.aux[off + e] = v;
-  }
-}
-constexpr int kNT = 26;  // 16-deep k chunks a lane may hold (K <= 416)
-__device__ __noinline__ f32x4v narrow_rows(const float* X, int ld, int r0, int nrows, int K,
-                                           int N, int off) {
-  const Lds s = lds();
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int rl = 16 * w + (lane >> 2), pq = lane & 3, Kp = pad16(K), nt = Kp >> 4;
-  const __amdgpu_buffer_rsrc_t rs = rsrc(X);
-  const bool ok = rl < nrows;
-  float4 x[kNT];
-#pragma unroll
-  for (int t = 0; t < kNT; ++t) {
-    const int k = 16 * t + 4 * pq;
-    x[t] = (ok && t < nt && k < K) ? ld4c(rs, (uint32_t)(((int64_t)(r0 + rl) * ld + k) * 4))
-                                   : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-  }
-  f32x4v acc = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-  for (int n = 0; n < 4; ++n) {
-    if (n >= N) continue;
-    const float* wt = s.aux + off + n * Kp + 4 * pq;
-    float a = 0.0f;
-#pragma unroll
-    for (int t = 0; t < kNT; ++t) {
-      if (t < nt) {
-        const float4 wv = *reinterpret_cast<const float4*>(wt + 16 * t);
-        a = fmaf(x[t].x, wv.x, a);
-        a = fmaf(x[t].y, wv.y, a);
-        a = fmaf(x[t].z, wv.z, a);
-        a = fmaf(x[t].w, wv.w, a);
-      }
-    }
-    a = a + __shfl_xor(a, 1);
-    a = a + __shfl_xor(a, 2);
-    acc[n] = a;
-  }
-  return acc;
 }
 
 // weight-gradient job over columns [j0, j0 + 16 nt) of W [nin][N] (offset w; the bias at b
@@ -962,6 +992,12 @@ struct Ws {
   float* dq1;         // dH1 of -mean Q [B][H1]
   float* dz3;         // actor output gradient [B][A]
   float* dh1a;        // actor dH1 [B][H1]
+  float* hp3all;      // head partials [6][CT2][B][4] per network slot (L3 of each network)
+  __host__ __device__ float* hp3(int id) const { return hp3all + (size_t)id * hp3s; }
+  size_t hp3s;
+  float* hpp;         // d pi partials [CT1][B][A]
+  unsigned* tickets;  // [7 slots][8 row tiles], 128 B apart: the head tickets
+  __device__ unsigned* ticket(int slot, int rt) const { return tickets + 32 * (8 * slot + rt); }
   size_t total;
 };
 
@@ -997,6 +1033,11 @@ __host__ __device__ inline Ws carve(void* base_p, int B, int H1, int H2, int A) 
   w.dq1 = (float*)take((size_t)B * H1 * 4);
   w.dz3 = (float*)take((size_t)B * A * 4);
   w.dh1a = (float*)take((size_t)B * H1 * 4);
+  const int CT1 = (H1 + 15) / 16, CT2 = (H2 + 15) / 16;
+  w.hp3s = align_up((size_t)CT2 * B * 4, 64);
+  w.hp3all = (float*)take(6 * w.hp3s * 4);
+  w.hpp = (float*)take((size_t)CT1 * B * A * 4);
+  w.tickets = (unsigned*)take(7 * 8 * 128);
   w.total = off;
   return w;
 }
@@ -1098,62 +1139,56 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
     if (id == N_AC) return xsrc(rs, S, S, true, false);            // s
     return xcat(xsrc(rs, S, S, true, false), ra, A, A, true, false);  // [s, a]
   };
+  const uint64_t ctr = p.rng_counter ? *p.rng_counter : 0ull;
   for (int layer = 1; layer <= 2; ++layer) {
     const int CT = layer == 1 ? CT1 : CT2, per = RTT * CT;
     for (int j = b; j < nn * per; j += G) {
       if (tid == 0) td3_dslot = (b == 0 && j == b) ? 8 * (int)y.n : -1;
       const int id = net_id(j / per), rem = j % per, rt = rem / CT, ct = rem % CT;
       const Net n = net_of(id);
-      if (layer == 1)
+      if (layer == 1) {
         fwd_job(in_of(id), slots, rt * kTR, B, n.th + n.w1, n.th + n.b1, n.in, H1, ct * kCols,
                 ACT_RELU, ws.h1(id));
-      else
-        fwd_job(xsrc(ws.h1(id), H1, H1, false, true), slots, rt * kTR, B, n.th + n.w2,
-                n.th + n.b2, H1, H2, ct * kCols, ACT_RELU, ws.h2(id));
+      } else {
+        // + the L3 partials of the tile's 16 units; the row tile's last job finishes L3:
+        // target actor tanh (+ TD3 smoothing noise, clip) -> a', critics -> v1, v2,
+        // actor tanh -> pi(s)
+        const Head hd{n.th + n.w3, ws.hp3(id), ws.ticket(id, rt), n.out, 1, n.out, ct, CT2,
+                      false};
+        if (fwd_job(xsrc(ws.h1(id), H1, H1, false, true), slots, rt * kTR, B, n.th + n.w2,
+                    n.th + n.b2, H1, H2, ct * kCols, ACT_RELU, ws.h2(id), false, hd)) {
+          const int N = n.out, r0 = rt * kTR, nr = min(kTR, B - r0);
+          for (int e = tid; e < nr * N; e += 256) {
+            const int row = r0 + e / N, c = e % N;
+            const float z = head_total(ws.hp3(id), CT2, B, N, row, c) + n.th[n.b3 + c];
+            if (id == N_TA) {
+              float a = xa_tanhf(z);
+              if (p.smooth) {
+                float nz = 0.0f;
+                if (p.noise_sigma != 0.0f) {
+                  nz = philox_normal((uint32_t)row, (uint32_t)c, ctr, p.seed) * p.noise_sigma;
+                  nz = fminf(fmaxf(nz, -p.noise_clip), p.noise_clip);
+                }
+                if (p.noise_out) p.noise_out[row * A + c] = nz;
+                a = fminf(fmaxf(a + nz, -1.0f), 1.0f);
+              }
+              stc(ws.ta + row * A + c, a);
+            } else if (id == N_AC) {
+              stc(ws.pa + row * A + c, xa_tanhf(z));
+            } else {
+              stc((id == N_C1 ? ws.v1 : ws.v2) + row, z);
+            }
+          }
+        }
+      }
       __syncthreads();
     }
     if (!grid_sync(y, s_flag, nn * per)) return;
   }
 
-  // ---- P3: L3 (target actor + smoothing, critic values, actor pi(s)) ----
-  {
-    const uint64_t ctr = p.rng_counter ? *p.rng_counter : 0ull;
-    for (int j = b; j < nn * RT; j += G) {
-      if (tid == 0) td3_dslot = (b == 0 && j == b) ? 8 * (int)y.n : -1;
-      const int id = net_id(j / RT), rt = j % RT, r0 = rt * kRows;
-      const Net n = net_of(id);
-      const int N = n.out;
-      stage_wt(lds(), 0, n.th + n.w3, H2, N, true, 0, false);
-      __syncthreads();
-      const f32x4v acc = narrow_rows(ws.h2(id), H2, r0, min(kRows, B - r0), H2, N, 0);
-      const int row = r0 + 16 * (tid >> 6) + ((tid & 63) >> 2), c = tid & 3;
-      if (row < B && c < N) {
-        const float z = (c == 0 ? acc[0] : c == 1 ? acc[1] : c == 2 ? acc[2] : acc[3]) +
-                        n.th[n.b3 + c];
-        if (id == N_TA) {
-          float a = xa_tanhf(z);
-          if (p.smooth) {
-            float nz = 0.0f;
-            if (p.noise_sigma != 0.0f) {
-              nz = philox_normal((uint32_t)row, (uint32_t)c, ctr, p.seed) * p.noise_sigma;
-              nz = fminf(fmaxf(nz, -p.noise_clip), p.noise_clip);
-            }
-            if (p.noise_out) p.noise_out[row * A + c] = nz;
-            a = fminf(fmaxf(a + nz, -1.0f), 1.0f);
-          }
-          stc(ws.ta + row * A + c, a);
-        } else if (id == N_AC) {
-          stc(ws.pa + row * A + c, xa_tanhf(z));
-        } else {
-          stc((id == N_C1 ? ws.v1 : ws.v2) + row, z);
-        }
-      }
-      __syncthreads();
-    }
-    if (!grid_sync(y, s_flag, nn * RT)) return;
-  }
-
-  // ---- P4 / P5: target critics L1 on [s', a'], L2 ----
+  // ---- P4 / P5: target critics L1 on [s', a'], L2 (+ the target values' partials; the
+  // row tile's last job runs the TD head: y = r + (1 - d) gamma min(tv1, tv2),
+  // dv = 2 (v - y) (MSE) or clip(v - y, +-delta) (opt-in Huber), per-sample loss) ----
   const int nt = twin ? 2 : 1;
   for (int layer = 1; layer <= 2; ++layer) {
     const int CT = layer == 1 ? CT1 : CT2, per = RTT * CT;
@@ -1161,59 +1196,49 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
       if (tid == 0) td3_dslot = (b == 0 && j == b) ? 8 * (int)y.n : -1;
       const int id = N_TC1 + j / per, rem = j % per, rt = rem / CT, ct = rem % CT;
       const Net n = net_of(id);
-      if (layer == 1)
+      if (layer == 1) {
         fwd_job(xcat(xsrc(rn, S, S, true, false), ws.ta, A, A, false, true), slots,
                 rt * kTR, B, n.th + n.w1, n.th + n.b1, C, H1, ct * kCols, ACT_RELU, ws.h1(id));
-      else
-        fwd_job(xsrc(ws.h1(id), H1, H1, false, true), slots, rt * kTR, B, n.th + n.w2,
-                n.th + n.b2, H1, H2, ct * kCols, ACT_RELU, ws.h2(id));
+      } else {
+        const Head hd{n.th + n.w3, ws.hp3(id), ws.ticket(N_TC1, rt), 1, 1, 1, ct, nt * CT2,
+                      false};
+        if (fwd_job(xsrc(ws.h1(id), H1, H1, false, true), slots, rt * kTR, B, n.th + n.w2,
+                    n.th + n.b2, H1, H2, ct * kCols, ACT_RELU, ws.h2(id), false, hd)) {
+          const int r0 = rt * kTR, nr = min(kTR, B - r0);
+          if (tid < nr) {
+            const int row = r0 + tid;
+            const float t1 = head_total(ws.hp3(N_TC1), CT2, B, 1, row, 0) + tc1.th[tc1.b3];
+            const float tv = twin
+                ? fminf(t1, head_total(ws.hp3(N_TC2), CT2, B, 1, row, 0) + tc2.th[tc2.b3])
+                : t1;
+            const int64_t sl = td3_slots[row];
+            const float yv = p.ring_rewards[sl] + ((1.0f - p.ring_dones[sl]) * p.gamma) * tv;
+            const float hdl = p.huber_delta;
+            auto term = [hdl](float e, float& d) {
+              if (hdl > 0.0f) {
+                d = fminf(fmaxf(e, -hdl), hdl);
+                const float ae = fabsf(e);
+                return ae <= hdl ? 0.5f * (e * e) : hdl * (ae - 0.5f * hdl);
+              }
+              d = 2.0f * e;
+              return e * e;
+            };
+            float d1;
+            float l = term(ldc(ws.v1 + row) - yv, d1);
+            stc(p.dv1 + row, d1);
+            if (twin) {
+              float d2;
+              l = l + term(ldc(ws.v2 + row) - yv, d2);
+              stc(p.dv2 + row, d2);
+            }
+            if (p.loss_out) p.loss_out[row] = l;
+          }
+        }
+      }
       __syncthreads();
     }
     if (!grid_sync(y, s_flag, nt * per)) return;
   }
-
-  // ---- P6: target values and the TD head ----
-  for (int j = b; j < RT; j += G) {
-    if (tid == 0) td3_dslot = (b == 0 && j == b) ? 8 * (int)y.n : -1;
-    const int r0 = j * kRows, nr = min(kRows, B - r0);
-    stage_wt(lds(), 0, tc1.th + tc1.w3, H2, 1, true, 0, false);
-    if (twin) stage_wt(lds(), kMaxK, tc2.th + tc2.w3, H2, 1, true, 0, false);
-    __syncthreads();
-    const f32x4v t1 = narrow_rows(ws.h2(N_TC1), H2, r0, nr, H2, 1, 0);
-    const f32x4v t2 = twin ? narrow_rows(ws.h2(N_TC2), H2, r0, nr, H2, 1, kMaxK) : t1;
-    if ((tid & 3) == 0) {
-      {
-        const int row = r0 + 16 * (tid >> 6) + ((tid & 63) >> 2);
-        if (row >= B) goto head_done;
-        const float tv = twin ? fminf(t1[0] + tc1.th[tc1.b3], t2[0] + tc2.th[tc2.b3])
-                              : t1[0] + tc1.th[tc1.b3];
-        const int64_t sl = td3_slots[row];
-        const float yv = p.ring_rewards[sl] + ((1.0f - p.ring_dones[sl]) * p.gamma) * tv;
-        const float hd = p.huber_delta;
-        auto term = [hd](float e, float& d) {
-          if (hd > 0.0f) {
-            d = fminf(fmaxf(e, -hd), hd);
-            const float ae = fabsf(e);
-            return ae <= hd ? 0.5f * (e * e) : hd * (ae - 0.5f * hd);
-          }
-          d = 2.0f * e;
-          return e * e;
-        };
-        float d1;
-        float l = term(ldc(ws.v1 + row) - yv, d1);
-        stc(p.dv1 + row, d1);
-        if (twin) {
-          float d2;
-          l = l + term(ldc(ws.v2 + row) - yv, d2);
-          stc(p.dv2 + row, d2);
-        }
-        if (p.loss_out) p.loss_out[row] = l;
-      }
-    head_done:;
-    }
-    __syncthreads();
-  }
-  if (!grid_sync(y, s_flag, RT)) return;
 
   // ---- P7: critics backward (dW2 / db2, dH1, dW3 / db3) ----
   {
@@ -1231,7 +1256,7 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
       if (q < n_dx) {
         const int rt = q / CT1, ct = q % CT1, c0 = ct * kCols;
         dx_tile(d2, rt * kTR, B, n.th + n.w2, H2, c0, min(kCols, H1 - c0), false, ws.h1(id),
-                ws.dh1(ci), H1);
+                ws.dh1(ci), H1, no_head());
       } else if (q < n_dx + n_dw2) {
         const int t = q - n_dx, it = t / CTW2, ct = t % CTW2;
         dw_job(xsrc(ws.h1(id), H1, H1, false, true), slots, d2, H1, H2, it * kRows,
@@ -1293,32 +1318,28 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
       }
       if (!grid_sync(y, s_flag, RTT * CT)) return;
     }
-    // ---- P11: dH1 of -mean Q (dQ / dv = -1 / B per row) ----
+    // ---- P11: dH1 of -mean Q (dQ / dv = -1 / B per row), + the partials of
+    // d pi(s) = dH1 W1[S + a][:]^T; the row tile's last job forms the actor's output
+    // gradient d pi (1 - pi^2) ----
     const DZ dq2 = dz_h2(ws.q2, H2, c1.th + c1.w3, 1, nullptr, -1.0f / (float)B);
     for (int j = b; j < RTT * CT1; j += G) {
       if (tid == 0) td3_dslot = (b == 0 && j == b) ? 8 * (int)y.n : -1;
       const int rt = j / CT1, ct = j % CT1, c0 = ct * kCols;
-      dx_tile(dq2, rt * kTR, B, c1.th + c1.w2, H2, c0, min(kCols, H1 - c0), true, ws.q1, ws.dq1,
-              H1);
-      __syncthreads();
-    }
-    if (!grid_sync(y, s_flag, RTT * CT1)) return;
-    // ---- P12: d pi(s) = dH1 W1[S + a][:]^T, times tanh' -> the actor's output gradient ----
-    for (int j = b; j < RT; j += G) {
-      if (tid == 0) td3_dslot = (b == 0 && j == b) ? 8 * (int)y.n : -1;
-      const int r0 = j * kRows;
-      stage_wt(lds(), 0, c1.th + c1.w1, H1, A, false, S, true);
-      __syncthreads();
-      const f32x4v acc = narrow_rows(ws.dq1, H1, r0, min(kRows, B - r0), H1, A, 0);
-      const int row = r0 + 16 * (tid >> 6) + ((tid & 63) >> 2), c = tid & 3;
-      if (row < B && c < A) {
-        const float dp = c == 0 ? acc[0] : c == 1 ? acc[1] : c == 2 ? acc[2] : acc[3];
-        const float pv = ldc(ws.pa + row * A + c);
-        stc(ws.dz3 + row * A + c, dp * (1.0f - pv * pv));
+      const Head hd{c1.th + c1.w1 + (size_t)S * H1, ws.hpp, ws.ticket(6, rt), 1, H1, A, ct, CT1,
+                    true};
+      if (dx_tile(dq2, rt * kTR, B, c1.th + c1.w2, H2, c0, min(kCols, H1 - c0), true, ws.q1,
+                  ws.dq1, H1, hd)) {
+        const int r0 = rt * kTR, nr = min(kTR, B - r0);
+        for (int e = tid; e < nr * A; e += 256) {
+          const int row = r0 + e / A, c = e % A;
+          const float dp = head_total(ws.hpp, CT1, B, A, row, c);
+          const float pv = ldc(ws.pa + row * A + c);
+          stc(ws.dz3 + row * A + c, dp * (1.0f - pv * pv));
+        }
       }
       __syncthreads();
     }
-    if (!grid_sync(y, s_flag, RT)) return;
+    if (!grid_sync(y, s_flag, RTT * CT1)) return;
     // ---- P13: actor backward (dW2 / db2, dH1, dW3 / db3) ----
     {
       const int IT1 = (H1 + kRows - 1) / kRows, IT2 = (H2 + kRows - 1) / kRows;
@@ -1329,7 +1350,7 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
         if (j < n_dx) {
           const int rt = j / CT1, ct = j % CT1, c0 = ct * kCols;
           dx_tile(d2, rt * kTR, B, ac.th + ac.w2, H2, c0, min(kCols, H1 - c0), false,
-                  ws.h1(N_AC), ws.dh1a, H1);
+                  ws.h1(N_AC), ws.dh1a, H1, no_head());
         } else if (j < n_dx + n_dw2) {
           const int t = j - n_dx, it = t / CTW2, ct = t % CTW2;
           dw_job(xsrc(ws.h1(N_AC), H1, H1, false, true), slots, d2, H1, H2, it * kRows,
@@ -1387,7 +1408,7 @@ extern "C" size_t xa_td3_update_workspace_bytes(int batch, int obs_dim, int act_
 extern "C" int xa_td3_update(const XaTd3UpdateArgs* p, void* stream) {
   XA_CHECK_ARG(p != nullptr, "xa_td3_update: null args");
   const XaTd3UpdateArgs& a = *p;
-  XA_CHECK_ARG(a.batch > 0 && a.obs_dim > 0 && a.act_dim > 0 && a.act_dim <= 16 && a.h1 > 0 &&
+  XA_CHECK_ARG(a.batch > 0 && a.obs_dim > 0 && a.act_dim > 0 && a.act_dim <= 4 && a.h1 > 0 &&
                    a.h2 > 0,
                "xa_td3_update: bad sizes");
   XA_CHECK_ARG(a.batch <= 256 && a.h1 <= kMaxK && a.h2 <= kMaxK && a.h1 % 4 == 0 &&
@@ -1395,7 +1416,7 @@ extern "C" int xa_td3_update(const XaTd3UpdateArgs* p, void* stream) {
                    a.obs_dim + a.act_dim <= 64 && a.h2 * a.act_dim <= 2048 &&
                    a.batch * a.act_dim <= 1024,
                "xa_td3_update: sizes beyond the kernel's tiles (batch <= 256; h1, h2 <= %d and "
-               "multiples of 4; obs + act <= 64; h2 act, batch act <= 2048, 1024)",
+               "multiples of 4; act <= 4; obs + act <= 64; h2 act, batch act <= 2048, 1024)",
                kMaxK);
   XA_CHECK_ARG(a.ring_states && a.ring_new_states && a.ring_actions && a.ring_rewards &&
                    a.ring_dones && a.slots && a.workspace && a.dv1 && a.g_critic1 &&

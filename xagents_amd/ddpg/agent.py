@@ -216,7 +216,7 @@ class DDPG(OffPolicy):
             return False
         B = self.batch_size
         return (B <= 256 and max(h) <= 416 and h[0] % 4 == 0 and h[1] % 4 == 0 and S + A <= 64
-                and h[1] * A <= 2048 and B * A <= 1024)
+                and A <= 4 and h[1] * A <= 2048 and B * A <= 1024)
 
     def _fused_args(self):
         """The launch arguments of xa_td3_update (built once), or None when the fused step

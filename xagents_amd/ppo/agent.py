@@ -89,6 +89,11 @@ class PPO(A2C):
                 E * self.n_mb <= 128:
             obs_dim, A = self.model.obs_dim, self.n_actions
             G = kernels.ppo_update_blocks(obs_dim, A, MB)
+            # (measurement knob: fewer workgroups, more tiles each -- fewer gradient rows to
+            # exchange per optimizer step)
+            g_cap = int(os.environ.get('XA_PPO_MAX_BLOCKS', '0'))
+            if G > 0 and g_cap > 0:
+                G = min(G, g_cap)
             if G > 0 and self.distributed:
                 # every rank's workgroups must be resident together: ranks sharing a GPU
                 # split its capacity
