@@ -355,6 +355,50 @@ XA_DEV void sload(int na, int nb, int va, int vb, Ld ld, Dst dst) {
   }
 }
 
+// [src0 | src1] rows as float4 quads (every width and ld a multiple of 4): quad q of an
+// nr x (Kp / 4) grid, tile row r (source row r0 + r, through the slots for ring sources)
+// and features k0 + k .. + 3 (k < K; zeros for r >= vr, k >= K), all of a thread's loads
+// issued before its first LDS write. Ring rows are plain 16-B loads (64-bit addresses);
+// in-launch hand-off sources are 16-B sc1 buffer loads
+XA_DEV bool quad_src(const XSrc& x, int k0) {
+  return (x.w0 & 3) == 0 && (x.ld0 & 3) == 0 && (k0 & 3) == 0 &&
+         (x.p1 == nullptr || ((x.w1 & 3) == 0 && (x.ld1 & 3) == 0));
+}
+template <class Dst>
+XA_DEV void xgather4(const XSrc& x, int r0, int nr, int vr, int k0, int K, int Kp, Dst dst) {
+  constexpr int kQ = 4;
+  const __amdgpu_buffer_rsrc_t rs0 = rsrc(x.p0), rs1 = rsrc(x.p1 ? x.p1 : x.p0);
+  const int nq = Kp >> 2, total = nr * nq;
+  for (int e0 = threadIdx.x; e0 < total; e0 += 256 * kQ) {
+    f32x4v v[kQ];
+#pragma unroll
+    for (int u = 0; u < kQ; ++u) {
+      const int e = e0 + 256 * u, r = e / nq, k = 4 * (e - r * nq);
+      v[u] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+      if (e < total && r < vr && k < K) {
+        const int f = k0 + k;
+        const bool first = f < x.w0;
+        const float* pb = first ? x.p0 : x.p1;
+        const bool slot = first ? x.slot0 : x.slot1, coh = first ? x.coh0 : x.coh1;
+        const int ld = first ? x.ld0 : x.ld1, c = first ? f : f - x.w0;
+        const int64_t row = slot ? td3_slots[r0 + r] : (int64_t)(r0 + r);
+        if (coh) {
+          const uint32_t off = (uint32_t)((row * ld + c) * 4);
+          v[u] = first ? __builtin_amdgcn_raw_buffer_load_b128(rs0, off, 0, kAuxSc1)
+                       : __builtin_amdgcn_raw_buffer_load_b128(rs1, off, 0, kAuxSc1);
+        } else {
+          v[u] = *reinterpret_cast<const f32x4v*>(pb + row * ld + c);
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kQ; ++u) {
+      const int e = e0 + 256 * u, r = e / nq, k = 4 * (e - r * nq);
+      if (e < total) dst(r, k, v[u]);
+    }
+  }
+}
+
 XA_DEV bool dma_src(const XSrc& x) {
   return x.p1 == nullptr && (x.w0 & 3) == 0 && (x.ld0 & 3) == 0;
 }
@@ -617,6 +661,10 @@ __device__ __noinline__ bool fwd_tile(XSrc x, const int64_t* slots, int r0, int 
   head_weights(h, c, st, wv);
   if (dma_src(x) && (K & 3) == 0)
     dma_cr(s.A, kTR, x.p0, x.ld0, r0, x.slot0 ? slots + r0 : nullptr, nrows, K, Kp, x.coh0);
+  else if (quad_src(x, 0) && (K & 3) == 0)
+    xgather4(x, r0, kTR, nrows, 0, K, Kp, [&](int r, int k, f32x4v v) {
+      *reinterpret_cast<f32x4v*>(s.A + cr_idx(r, k, kTR)) = v;
+    });
   else
     sload(kTR, Kp, nrows, K, [&](int r, int k) { return xload(x, slots, r0 + r, k); },
           [&](int r, int k, float v) { s.A[cr_idx(r, k, kTR)] = v; });
@@ -716,6 +764,10 @@ __device__ __noinline__ Acc4 dw_tile(XSrc x, const int64_t* slots, DZ d, int i0,
   const AuxRegs ax = aux_load(d, j0, nc, 0, B);
   if (dma_src(x) && (ni & 3) == 0 && (i0 & 3) == 0)
     dma_km(s.A, kRows, x.p0, x.ld0, i0, x.slot0 ? slots : nullptr, B, ni, Kp, x.coh0);
+  else if (quad_src(x, i0) && (ni & 3) == 0)
+    xgather4(x, 0, Kp, B, i0, ni, kRows, [&](int k, int i, f32x4v v) {
+      *reinterpret_cast<f32x4v*>(s.A + k * kRows + i) = v;
+    });
   else
     sload(Kp, kRows, B, ni, [&](int k, int i) { return xload(x, slots, k, i0 + i); },
           [&](int k, int i, float v) { s.A[k * kRows + i] = v; });
