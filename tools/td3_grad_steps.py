@@ -64,6 +64,11 @@ def main():
         # MFMA done (us after the phase's barrier), from the last launch
         tr = rows[-1]
         dt = agent._fused_ws[2048:2048 + 8192].cpu().numpy().view(np.uint64).astype(np.int64)
+        pro = dt[8 * 15:8 * 15 + 4]
+        if (pro > 0).all() and pro[0] >= tr[0]:
+            rel = (pro - tr[0]) / 100.0
+            print(f'  prologue: start {rel[0]:.2f} slots issued {rel[1]:.2f} slots in LDS '
+                  f'{rel[2]:.2f} P1 loop {rel[3]:.2f} us', flush=True)
         for p in range(len(d) - 1):
             pts = dt[8 * p:8 * p + 4]
             if (pts <= 0).any() or pts[0] < tr[0]:

@@ -906,53 +906,62 @@ XA_DEV void dw_job(const XSrc& x, const int64_t* slots, const DZ& d, int nin, in
   const Acc4 acc = dw_tile(x, slots, d, i0, ni, j0, nc, nt, B, first ? bsum_lds : nullptr);
   const float omb1 = ao.omb1, omb2 = ao.omb2, eps = ao.eps, tau = ao.tau;
   float* const target = ao.target;
+  // (the bias gradient of column threadIdx.x < nc was summed by this same thread)
+  const bool has_b = first && (int)threadIdx.x < nc;
+  if (ao.on) {
+    // every parameter / moment / target load of the thread's nt x 4 elements and of its
+    // bias element in flight before the first update: one memory round trip
+    float th[kMaxDwTiles][4], m[kMaxDwTiles][4], v[kMaxDwTiles][4], tg[kMaxDwTiles][4];
+    int ee[kMaxDwTiles][4];
 #pragma unroll
-  for (int t = 0; t < kMaxDwTiles; ++t) {
-    if (t >= nt) continue;
-    const int j = kCols * t + out_col();
-    if (ao.on) {
-      // the 4 elements' parameter / moment / target loads together, then the updates
-      float th[4], m[4], v[4], tg[4];
-      int ee[4];
+    for (int t = 0; t < kMaxDwTiles; ++t) {
+      const int j = kCols * t + out_col();
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int i = out_row(r);
-        const bool ok = i < ni && j < nc;
-        ee[r] = ok ? w + (i0 + i) * N + j0 + j : -1;
-        const int e = ok ? ee[r] : w;
-        th[r] = ldc(an.th + e);
-        m[r] = an.m[e];
-        v[r] = an.v[e];
-        tg[r] = target ? target[e] : 0.0f;
+        const bool ok = t < nt && i < ni && j < nc;
+        ee[t][r] = ok ? w + (i0 + i) * N + j0 + j : -1;
+        const int e = ok ? ee[t][r] : w;
+        th[t][r] = t < nt ? ldc(an.th + e) : 0.0f;
+        m[t][r] = t < nt ? an.m[e] : 0.0f;
+        v[t][r] = t < nt ? an.v[e] : 0.0f;
+        tg[t][r] = (t < nt && target) ? target[e] : 0.0f;
       }
+    }
+    const int eb = b + j0 + (has_b ? (int)threadIdx.x : 0);
+    float bth = 0.0f, bm = 0.0f, bv = 0.0f, btg = 0.0f;
+    if (has_b) {
+      bth = ldc(an.th + eb);
+      bm = an.m[eb];
+      bv = an.v[eb];
+      btg = target ? target[eb] : 0.0f;
+    }
+    auto upd = [&](int e, float g, float th_, float m_, float v_, float tg_) {
+      stc(grad + e, g);
+      adam_elem(g, th_, m_, v_, an.alpha, omb1, omb2, eps);
+      stc(an.th + e, th_);
+      an.m[e] = m_;
+      an.v[e] = v_;
+      if (target) target[e] = tau == 1.0f ? th_ : (1.0f - tau) * tg_ + tau * th_;
+    };
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        if (ee[r] < 0) continue;
-        const int e = ee[r];
-        const float g = acc.t[t][r];
-        stc(grad + e, g);
-        adam_elem(g, th[r], m[r], v[r], an.alpha, omb1, omb2, eps);
-        stc(an.th + e, th[r]);
-        an.m[e] = m[r];
-        an.v[e] = v[r];
-        if (target) target[e] = tau == 1.0f ? th[r] : (1.0f - tau) * tg[r] + tau * th[r];
-      }
-    } else {
+    for (int t = 0; t < kMaxDwTiles; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (ee[t][r] >= 0) upd(ee[t][r], acc.t[t][r], th[t][r], m[t][r], v[t][r], tg[t][r]);
+    if (has_b) upd(eb, bsum_lds[threadIdx.x], bth, bm, bv, btg);
+  } else {
+#pragma unroll
+    for (int t = 0; t < kMaxDwTiles; ++t) {
+      if (t >= nt) continue;
+      const int j = kCols * t + out_col();
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int i = out_row(r);
         if (i < ni && j < nc) stc(grad + w + (i0 + i) * N + j0 + j, acc.t[t][r]);
       }
     }
-  }
-  if (first) {
-    __syncthreads();
-    if (threadIdx.x < nc) {
-      const int e = b + j0 + threadIdx.x;
-      const float g = bsum_lds[threadIdx.x];
-      stc(grad + e, g);
-      if (ao.on) adam_one(an, g, e, omb1, omb2, eps, target, tau);
-    }
+    if (has_b) stc(grad + b + j0 + threadIdx.x, bsum_lds[threadIdx.x]);
   }
 }
 
@@ -1115,16 +1124,19 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
   y.trace = b == 0 ? ws.trace : nullptr;
   if (b == 0 && tid == 0) ws.trace[0] = wall_clock64();
   if (tid == 0) {
-    td3_dslot = -1;
+    td3_dslot = b == 0 ? 8 * 15 : -1;  // (diagnostic) the prologue's points in slot 15
     td3_dbuf = ws.dtrace;
   }
+  dstamp(0);
   // networks (the Adam step sizes from the step counters as the launch finds them; their
   // loads in flight with the slot loads)
   const Net c1 = make_net(p.critic1, C, H1, H2, 1, true);
   const Net c2 = make_net(twin ? p.critic2 : p.critic1, C, H1, H2, 1, twin);
   const Net ac = make_net(p.actor, S, H1, H2, A, pol);
   if (tid < p.batch) td3_slots[tid] = p.slots[tid];  // (batch <= 256)
+  dstamp(1);
   __syncthreads();
+  dstamp(2);
   const Net tc1 = make_net(p.target_critic1, C, H1, H2, 1, false);
   const Net tc2 = make_net(twin ? p.target_critic2 : p.target_critic1, C, H1, H2, 1, false);
   const int64_t* slots = p.slots;
@@ -1173,6 +1185,8 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
       }
     }
   }
+
+  dstamp(3);
 
   // ---- P1 / P2: L1 and L2 forward of the target actor, the critics (and the actor) ----
   // the networks of P1 - P3: target actor, critic 1, [critic 2], [actor]
