@@ -90,7 +90,18 @@ XA_DEV float4 ld4p(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
   const f32x4v v = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0);
   return make_float4(v[0], v[1], v[2], v[3]);
 }
-XA_DEV float ldw(const float* p, bool coh) { return coh ? ldc(p) : *p; }
+// plain loads / stores through the GLOBAL address space: a generic (flat) access in an
+// out-of-line function would also count on lgkmcnt, so every later LDS wait would wait for it
+typedef __attribute__((address_space(1))) float gf32;
+typedef __attribute__((address_space(1))) f32x4v gv4;
+XA_DEV float ldg(const float* p) { return *(const gf32*)p; }
+XA_DEV void stg(float* p, float v) { *(gf32*)p = v; }
+XA_DEV float4 ldg4(const float* p) {
+  const f32x4v v = *(const gv4*)p;
+  return make_float4(v[0], v[1], v[2], v[3]);
+}
+XA_DEV void stg4(float* p, float4 v) { *(gv4*)p = f32x4v{v.x, v.y, v.z, v.w}; }
+XA_DEV float ldw(const float* p, bool coh) { return coh ? ldc(p) : ldg(p); }
 // one 16-B write-through store (a vector store)
 XA_DEV void st4c(__amdgpu_buffer_rsrc_t r, uint32_t byte_off, f32x4v v) {
   __builtin_amdgcn_raw_buffer_store_b128(v, r, byte_off, 0, kAuxSc1);
@@ -173,11 +184,11 @@ XA_DEV float xload(const XSrc& x, const int64_t* slots, int r, int k) {
   if (k < x.w0) {
     const int64_t row = x.slot0 ? td3_slots[r] : r;
     const float* p = x.p0 + row * x.ld0 + k;
-    return x.coh0 ? ldc(p) : *p;
+    return x.coh0 ? ldc(p) : ldg(p);
   }
   const int64_t row = x.slot1 ? td3_slots[r] : r;
   const float* p = x.p1 + row * x.ld1 + (k - x.w0);
-  return x.coh1 ? ldc(p) : *p;
+  return x.coh1 ? ldc(p) : ldg(p);
 }
 
 // A gradient source dZ [rows][cols]: a dense buffer (ld), or the layer-2 output gradient
@@ -239,7 +250,9 @@ __shared__ __attribute__((aligned(16))) float td3_part[2 * 32 * 16];
 __shared__ int td3_dslot;
 __shared__ unsigned long long* td3_dbuf;
 XA_DEV void dstamp(int point) {
-  if (threadIdx.x == 0 && td3_dslot >= 0) td3_dbuf[td3_dslot + point] = wall_clock64();
+  if (threadIdx.x == 0 && td3_dslot >= 0)
+    *((__attribute__((address_space(1))) unsigned long long*)td3_dbuf + td3_dslot + point) =
+        wall_clock64();
 }
 
 // Operand layouts in LDS (both written by LDS-DMA, 1 KB per wave instruction):
@@ -387,7 +400,7 @@ XA_DEV void xgather4(const XSrc& x, int r0, int nr, int vr, int k0, int K, int K
           v[u] = first ? __builtin_amdgcn_raw_buffer_load_b128(rs0, off, 0, kAuxSc1)
                        : __builtin_amdgcn_raw_buffer_load_b128(rs1, off, 0, kAuxSc1);
         } else {
-          v[u] = *reinterpret_cast<const f32x4v*>(pb + row * ld + c);
+          v[u] = *(const gv4*)(pb + row * ld + c);
         }
       }
     }
@@ -647,16 +660,34 @@ XA_DEV float4 tile_out4() {
 // forward job: out[r][c] = act(X W + b) on rows [r0, r0 + kTR) x cols [c0, c0 + 16)
 // (A = X rows (CR), B = W[k][c0 ..] (KM); N % 4 == 0; the job functions are out of line:
 // one copy each instead of one per call site)
-__device__ __noinline__ bool fwd_tile(XSrc x, const int64_t* slots, int r0, int B,
-                                      const float* W, const float* bias, int K, int N, int c0,
-                                      bool coh, int act, float* out, Head h) {
+// (the job functions take their arguments through LDS, written by every wave of the
+// calling workgroup just before the call: a by-value struct argument would travel through
+// scratch memory, one store / load round trip on every call)
+struct FwdArgs {
+  XSrc x;
+  const float* W;
+  const float* bias;
+  float* out;
+  Head h;
+  int r0, B, K, N, c0, act;
+  bool coh;
+};
+__shared__ FwdArgs td3_fa;
+__device__ __noinline__ bool fwd_tile(const int64_t* slots) {
+  const FwdArgs fa = td3_fa;
+  const XSrc x = fa.x;
+  const Head h = fa.h;
+  const float *W = fa.W, *bias = fa.bias;
+  float* out = fa.out;
+  const int r0 = fa.r0, B = fa.B, K = fa.K, N = fa.N, c0 = fa.c0, act = fa.act;
+  const bool coh = fa.coh;
   const Lds s = lds();
   dstamp(0);
   const int Kp = pad16(K), nrows = min(kTR, B - r0), nc = min(kCols, N - c0);
   const int t = threadIdx.x, row = r0 + (t >> 2), c = c0 + 4 * (t & 3);
   const bool st = t < 4 * kTR && row < B && c < N;
   float4 bv = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-  if (st) bv = coh ? ld4c(rsrc(bias), (uint32_t)(c * 4)) : *reinterpret_cast<const float4*>(bias + c);
+  if (st) bv = coh ? ld4c(rsrc(bias), (uint32_t)(c * 4)) : ldg4(bias + c);
   float wv[4][4];
   head_weights(h, c, st, wv);
   if (dma_src(x) && (K & 3) == 0)
@@ -691,15 +722,31 @@ __device__ __noinline__ bool fwd_tile(XSrc x, const int64_t* slots, int r0, int 
 XA_DEV bool fwd_job(const XSrc& x, const int64_t* slots, int r0, int B, const float* W,
                     const float* bias, int K, int N, int c0, int act, float* out,
                     bool coh = false, const Head& h = no_head()) {
-  return fwd_tile(x, slots, r0, B, W, bias, K, N, c0, coh, act, out, h);
+  td3_fa = FwdArgs{x, W, bias, out, h, r0, B, K, N, c0, act, coh};
+  return fwd_tile(slots);
 }
 
 // input-gradient job: out[r][c] = (dZ W^T)[r][c] (gate[r][c] > 0) on rows [r0, r0 + kTR) x
 // cols [c0, c0 + 16) of the layer input (W row-major [in][K], out / gate [B][ld]):
 // A = dZ rows (CR, the dZ2 former applied in LDS), B = W rows c0 .. (CR)
-__device__ __noinline__ bool dx_tile(DZ d, int r0, int B, const float* W, int K, int c0,
-                                     int nc, bool coh, const float* gate, float* out, int ld,
-                                     Head h) {
+struct DxArgs {
+  DZ d;
+  const float* W;
+  const float* gate;
+  float* out;
+  Head h;
+  int r0, B, K, c0, nc, ld;
+  bool coh;
+};
+__shared__ DxArgs td3_xa;
+__device__ __noinline__ bool dx_tile_lds() {
+  const DxArgs xa = td3_xa;
+  const DZ d = xa.d;
+  const Head h = xa.h;
+  const float *W = xa.W, *gate = xa.gate;
+  float* out = xa.out;
+  const int r0 = xa.r0, B = xa.B, K = xa.K, c0 = xa.c0, nc = xa.nc, ld = xa.ld;
+  const bool coh = xa.coh;
   const Lds s = lds();
   dstamp(0);
   const int Kp = pad16(K), nrows = min(kTR, B - r0);
@@ -751,13 +798,31 @@ __device__ __noinline__ bool dx_tile(DZ d, int r0, int B, const float* W, int K,
 // weight-gradient tiles: D_t[i][j] = sum_k X[k][i0 + i] dZ[k][j0 + 16 t + j] for nt <= 4
 // column tiles t sharing the staged A (i < ni, columns < nc of the nt x 16, k < B):
 // A = X rows (KM, width 64), B = dZ rows (nt KM tiles of width 16); the bias gradients
-// sum_k dZ[k][j0 + j] (fixed k order) land in bsum[j] when bsum != 0
+// sum_k dZ[k][j0 + j] (fixed k order) land in td3_bsum[j] when want_b (each by thread j)
+XA_DEV bool dx_tile(const DZ& d, int r0, int B, const float* W, int K, int c0, int nc, bool coh,
+                    const float* gate, float* out, int ld, const Head& h) {
+  td3_xa = DxArgs{d, W, gate, out, h, r0, B, K, c0, nc, ld, coh};
+  return dx_tile_lds();
+}
+
+__shared__ float td3_bsum[kCols * 4];  // the bias gradients of a weight-gradient job
 struct Acc4 {
   f32x4v t[4];
 };
 constexpr int kMaxDwTiles = 4;
-__device__ __noinline__ Acc4 dw_tile(XSrc x, const int64_t* slots, DZ d, int i0, int ni, int j0,
-                                     int nc, int nt, int B, float* bsum) {
+struct DwArgs {
+  XSrc x;
+  DZ d;
+  int i0, ni, j0, nc, nt, B;
+  bool want_b;
+};
+__shared__ DwArgs td3_wa;
+__device__ __noinline__ Acc4 dw_tile_lds(const int64_t* slots) {
+  const DwArgs wa = td3_wa;
+  const XSrc x = wa.x;
+  const DZ d = wa.d;
+  const int i0 = wa.i0, ni = wa.ni, j0 = wa.j0, nc = wa.nc, nt = wa.nt, B = wa.B;
+  const bool want_b = wa.want_b;
   const Lds s = lds();
   dstamp(0);
   const int Kp = pad16(B);
@@ -797,12 +862,12 @@ __device__ __noinline__ Acc4 dw_tile(XSrc x, const int64_t* slots, DZ d, int i0,
     }
     __syncthreads();
   }
-  if (bsum && threadIdx.x < nc) {
+  if (want_b && (int)threadIdx.x < nc) {
     const int t = threadIdx.x >> 4, j = threadIdx.x & 15;
     const float* bt = s.B + t * Kp * kCols;
     float acc = 0.0f;
     for (int k = 0; k < B; ++k) acc += bt[k * kCols + j];
-    bsum[threadIdx.x] = acc;
+    td3_bsum[threadIdx.x] = acc;
   }
   dstamp(2);
   Acc4 r;
@@ -822,14 +887,14 @@ __device__ __noinline__ Acc4 dw_tile(XSrc x, const int64_t* slots, DZ d, int i0,
 // Keras Adam (+ Polyak into the target) of one parameter from its raw gradient
 XA_DEV void adam_one(const Net& n, float g, int i, float omb1, float omb2, float eps,
                      float* target, float tau) {
-  float th = ldc(n.th + i), m = n.m[i], v = n.v[i];
+  float th = ldc(n.th + i), m = ldg(n.m + i), v = ldg(n.v + i);
   adam_elem(g, th, m, v, n.alpha, omb1, omb2, eps);
   stc(n.th + i, th);
-  n.m[i] = m;
-  n.v[i] = v;
+  stg(n.m + i, m);
+  stg(n.v + i, v);
   if (target) {
-    const float y = target[i];
-    target[i] = tau == 1.0f ? th : (1.0f - tau) * y + tau * th;
+    const float y = ldg(target + i);
+    stg(target + i, tau == 1.0f ? th : (1.0f - tau) * y + tau * th);
   }
 }
 
@@ -854,9 +919,9 @@ __device__ __noinline__ void adam_range(Net n, const float* grad, int lo, int hi
       const int i = 4 * min(g0 + 256 * u, hi4 / 4 - 1);
       g[u] = ld4c(rg, (uint32_t)i * 4u);
       th[u] = ld4c(rt, (uint32_t)i * 4u);
-      m[u] = *reinterpret_cast<const float4*>(n.m + i);
-      v[u] = *reinterpret_cast<const float4*>(n.v + i);
-      tg[u] = target ? *reinterpret_cast<const float4*>(target + i) : make_float4(0, 0, 0, 0);
+      m[u] = ldg4(n.m + i);
+      v[u] = ldg4(n.v + i);
+      tg[u] = target ? ldg4(target + i) : make_float4(0, 0, 0, 0);
     }
 #pragma unroll
     for (int u = 0; u < kAdamG; ++u) {
@@ -873,9 +938,9 @@ __device__ __noinline__ void adam_range(Net n, const float* grad, int lo, int hi
         yp[c] = tau == 1.0f ? tp[c] : (1.0f - tau) * yp[c] + tau * tp[c];
       }
       st4c(rt, (uint32_t)i * 4u, f32x4v{th[u].x, th[u].y, th[u].z, th[u].w});
-      *reinterpret_cast<float4*>(n.m + i) = m[u];
-      *reinterpret_cast<float4*>(n.v + i) = v[u];
-      if (target) *reinterpret_cast<float4*>(target + i) = tg[u];
+      stg4(n.m + i, m[u]);
+      stg4(n.v + i, v[u]);
+      if (target) stg4(target + i, tg[u]);
     }
   }
   if ((int)threadIdx.x < hi - hi4) {
@@ -899,11 +964,12 @@ XA_DEV AdamOpt adam_opt(const XaTdNet& o, float* target, float tau) {
 XA_DEV AdamOpt no_adam() { return AdamOpt{0.0f, 0.0f, 0.0f, 0.0f, nullptr, false}; }
 XA_DEV void dw_job(const XSrc& x, const int64_t* slots, const DZ& d, int nin, int N, int i0,
                    int j0, int nt, int B, float* grad, int w, int b, const Net& an,
-                   const AdamOpt& ao, float* bsum_lds) {
+                   const AdamOpt& ao) {
   const int ni = min(kRows, nin - i0), nc = min(kCols * nt, N - j0);
   nt = (nc + kCols - 1) / kCols;
   const bool first = i0 == 0;
-  const Acc4 acc = dw_tile(x, slots, d, i0, ni, j0, nc, nt, B, first ? bsum_lds : nullptr);
+  td3_wa = DwArgs{x, d, i0, ni, j0, nc, nt, B, first};
+  const Acc4 acc = dw_tile_lds(slots);
   const float omb1 = ao.omb1, omb2 = ao.omb2, eps = ao.eps, tau = ao.tau;
   float* const target = ao.target;
   // (the bias gradient of column threadIdx.x < nc was summed by this same thread)
@@ -949,7 +1015,7 @@ XA_DEV void dw_job(const XSrc& x, const int64_t* slots, const DZ& d, int nin, in
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         if (ee[t][r] >= 0) upd(ee[t][r], acc.t[t][r], th[t][r], m[t][r], v[t][r], tg[t][r]);
-    if (has_b) upd(eb, bsum_lds[threadIdx.x], bth, bm, bv, btg);
+    if (has_b) upd(eb, td3_bsum[threadIdx.x], bth, bm, bv, btg);
   } else {
 #pragma unroll
     for (int t = 0; t < kMaxDwTiles; ++t) {
@@ -961,7 +1027,7 @@ XA_DEV void dw_job(const XSrc& x, const int64_t* slots, const DZ& d, int nin, in
         if (i < ni && j < nc) stc(grad + w + (i0 + i) * N + j0 + j, acc.t[t][r]);
       }
     }
-    if (has_b) stc(grad + b + j0 + threadIdx.x, bsum_lds[threadIdx.x]);
+    if (has_b) stc(grad + b + j0 + threadIdx.x, td3_bsum[threadIdx.x]);
   }
 }
 
@@ -1107,7 +1173,6 @@ enum { N_TA = 0, N_C1 = 1, N_C2 = 2, N_AC = 3, N_TC1 = 4, N_TC2 = 5 };
 
 __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
   __shared__ int s_flag;
-  __shared__ float s_bsum[kCols * kMaxDwTiles];
   const int G = gridDim.x, b = blockIdx.x, tid = threadIdx.x;
   const int B = p.batch, S = p.obs_dim, A = p.act_dim, H1 = p.h1, H2 = p.h2;
   const int C = S + A;
@@ -1326,11 +1391,11 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
       } else if (q < n_dx + n_dw2) {
         const int t = q - n_dx, it = t / CTW2, ct = t % CTW2;
         dw_job(xsrc(ws.h1(id), H1, H1, false, true), slots, d2, H1, H2, it * kRows,
-               ct * NTW * kCols, NTW, B, grad, n.w2, n.b2, n, no_adam(), s_bsum);
+               ct * NTW * kCols, NTW, B, grad, n.w2, n.b2, n, no_adam());
       } else {
         const int it = q - n_dx - n_dw2;
         dw_job(xsrc(ws.h2(id), H2, H2, false, true), slots, dz_buf(dv, 1), H2, 1, it * kRows,
-               0, 1, B, grad, n.w3, n.b3, n, no_adam(), s_bsum);
+               0, 1, B, grad, n.w3, n.b3, n, no_adam());
       }
       __syncthreads();
     }
@@ -1355,7 +1420,7 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
       float* tgt = pol ? (ci ? p.target_critic2.theta : p.target_critic1.theta) : nullptr;
       if (q < n_w1) {
         dw_job(in_of(ci ? N_C2 : N_C1), slots, dz_buf(ws.dh1(ci), H1), C, H1, 0,
-               q * NTW * kCols, NTW, B, grad, n.w1, n.b1, n, adam_opt(opt, tgt, p.tau), s_bsum);
+               q * NTW * kCols, NTW, B, grad, n.w1, n.b1, n, adam_opt(opt, tgt, p.tau));
       } else {
         const int lo = n.w2 + (q - n_w1) * chunk, hi = min(n.P, lo + chunk);
         const float omb1 = 1.0f - opt.beta1, omb2 = 1.0f - opt.beta2;
@@ -1420,11 +1485,11 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
         } else if (j < n_dx + n_dw2) {
           const int t = j - n_dx, it = t / CTW2, ct = t % CTW2;
           dw_job(xsrc(ws.h1(N_AC), H1, H1, false, true), slots, d2, H1, H2, it * kRows,
-                 ct * NTW * kCols, NTW, B, p.g_actor, ac.w2, ac.b2, ac, no_adam(), s_bsum);
+                 ct * NTW * kCols, NTW, B, p.g_actor, ac.w2, ac.b2, ac, no_adam());
         } else {
           const int it = j - n_dx - n_dw2;
           dw_job(xsrc(ws.h2(N_AC), H2, H2, false, true), slots, dz_buf(ws.dz3, A), H2, A,
-                 it * kRows, 0, 1, B, p.g_actor, ac.w3, ac.b3, ac, no_adam(), s_bsum);
+                 it * kRows, 0, 1, B, p.g_actor, ac.w3, ac.b3, ac, no_adam());
         }
         __syncthreads();
       }
@@ -1439,7 +1504,7 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
         if (j < CTW1) {
           dw_job(xsrc(rs, S, S, true, false), slots, dz_buf(ws.dh1a, H1), S, H1, 0,
                  j * NTW * kCols, NTW, B, p.g_actor, ac.w1, ac.b1, ac,
-                 adam_opt(p.actor, p.target_actor.theta, p.tau), s_bsum);
+                 adam_opt(p.actor, p.target_actor.theta, p.tau));
         } else {
           const int lo = ac.w2 + (j - CTW1) * chunk, hi = min(ac.P, lo + chunk);
           const float omb1 = 1.0f - p.actor.beta1, omb2 = 1.0f - p.actor.beta2;
