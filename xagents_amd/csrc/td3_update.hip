@@ -1193,11 +1193,13 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
     td3_dbuf = ws.dtrace;
   }
   dstamp(0);
-  // networks (the Adam step sizes from the step counters as the launch finds them; their
-  // loads in flight with the slot loads)
-  const Net c1 = make_net(p.critic1, C, H1, H2, 1, true);
-  const Net c2 = make_net(twin ? p.critic2 : p.critic1, C, H1, H2, 1, twin);
-  const Net ac = make_net(p.actor, S, H1, H2, A, pol);
+  // networks; the step counters as the launch finds them are read here (in flight with the
+  // slot loads) and the Adam step sizes formed only where the optimizer steps run
+  Net c1 = make_net(p.critic1, C, H1, H2, 1, false);
+  Net c2 = make_net(twin ? p.critic2 : p.critic1, C, H1, H2, 1, false);
+  Net ac = make_net(p.actor, S, H1, H2, A, false);
+  const int step_c1 = *p.critic1.step, step_c2 = twin ? *p.critic2.step : 0;
+  const int step_ac = pol ? *p.actor.step : 0;
   if (tid < p.batch) td3_slots[tid] = p.slots[tid];  // (batch <= 256)
   dstamp(1);
   __syncthreads();
@@ -1404,6 +1406,8 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
 
   // ---- P8: critics dW1 / db1 + Adam, Adam of the rest (+ Polyak on policy steps); the
   // rest in chunks sized so the phase's jobs fill the grid ----
+  c1.alpha = adam_alpha(p.critic1.lr, p.critic1.beta1, p.critic1.beta2, step_c1 + 1);
+  if (twin) c2.alpha = adam_alpha(p.critic2.lr, p.critic2.beta1, p.critic2.beta2, step_c2 + 1);
   int p8_jobs;
   {
     const int n_w1 = CTW1;                      // one in-feature tile (C <= 64)
@@ -1496,6 +1500,7 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
       if (!grid_sync(y, s_flag, n_dx + n_dw2 + n_dw3)) return;
     }
     // ---- P14: actor dW1 / db1 + Adam + Polyak, Adam + Polyak of the rest ----
+    ac.alpha = adam_alpha(p.actor.lr, p.actor.beta1, p.actor.beta2, step_ac + 1);
     {
       const int rest = ac.P - ac.w2, chunk = adam_chunk(rest, max(1, G - CTW1));
       const int n_ad = (rest + chunk - 1) / chunk;
