@@ -974,7 +974,76 @@ XA_DEV void dw_job(const XSrc& x, const int64_t* slots, const DZ& d, int nin, in
   float* const target = ao.target;
   // (the bias gradient of column threadIdx.x < nc was summed by this same thread)
   const bool has_b = first && (int)threadIdx.x < nc;
-  if (ao.on) {
+  if ((N & 3) == 0 && (j0 & 3) == 0 && (w & 3) == 0) {
+    // the tile through LDS, row-major [64 in-features][64 (+ 4 pad)]: every thread then owns
+    // whole float4 groups -- 16-B loads and write-through stores instead of scattered words
+    constexpr int kTS = kRows + 4;
+    float* T = lds().A;
+    __syncthreads();  // every wave's MFMA reads of the staged operands are done
+#pragma unroll
+    for (int t = 0; t < kMaxDwTiles; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (t < nt) T[out_row(r) * kTS + kCols * t + out_col()] = acc.t[t][r];
+    __syncthreads();
+    const __amdgpu_buffer_rsrc_t rg = rsrc(grad), rt = rsrc(an.th);
+    float4 gq[4], thq[4], mq[4], vq[4], tq[4];
+    int eq[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int f = (int)threadIdx.x + 256 * u, i = f >> 4, c = 4 * (f & 15);
+      const bool ok = i < ni && c < nc;
+      eq[u] = ok ? w + (i0 + i) * N + j0 + c : -1;
+      const float4 z = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      gq[u] = ok ? *reinterpret_cast<const float4*>(T + i * kTS + c) : z;
+      thq[u] = mq[u] = vq[u] = tq[u] = z;
+      if (ao.on && ok) {
+        thq[u] = ld4c(rt, (uint32_t)eq[u] * 4u);
+        mq[u] = ldg4(an.m + eq[u]);
+        vq[u] = ldg4(an.v + eq[u]);
+        if (target) tq[u] = ldg4(target + eq[u]);
+      }
+    }
+    const int eb = b + j0 + (has_b ? (int)threadIdx.x : 0);
+    float bth = 0.0f, bm = 0.0f, bv = 0.0f, btg = 0.0f;
+    if (ao.on && has_b) {
+      bth = ldc(an.th + eb);
+      bm = ldg(an.m + eb);
+      bv = ldg(an.v + eb);
+      btg = target ? ldg(target + eb) : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (eq[u] < 0) continue;
+      st4c(rg, (uint32_t)eq[u] * 4u, f32x4v{gq[u].x, gq[u].y, gq[u].z, gq[u].w});
+      if (!ao.on) continue;
+      float* gp = &gq[u].x;
+      float* tp = &thq[u].x;
+      float* mp = &mq[u].x;
+      float* vp = &vq[u].x;
+      float* yp = &tq[u].x;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        adam_elem(gp[c], tp[c], mp[c], vp[c], an.alpha, omb1, omb2, eps);
+        yp[c] = tau == 1.0f ? tp[c] : (1.0f - tau) * yp[c] + tau * tp[c];
+      }
+      st4c(rt, (uint32_t)eq[u] * 4u, f32x4v{thq[u].x, thq[u].y, thq[u].z, thq[u].w});
+      stg4(an.m + eq[u], mq[u]);
+      stg4(an.v + eq[u], vq[u]);
+      if (target) stg4(target + eq[u], tq[u]);
+    }
+    if (has_b) {
+      const float g = td3_bsum[threadIdx.x];
+      stc(grad + eb, g);
+      if (ao.on) {
+        adam_elem(g, bth, bm, bv, an.alpha, omb1, omb2, eps);
+        stc(an.th + eb, bth);
+        stg(an.m + eb, bm);
+        stg(an.v + eb, bv);
+        if (target) stg(target + eb, tau == 1.0f ? bth : (1.0f - tau) * btg + tau * bth);
+      }
+    }
+  } else if (ao.on) {
     // every parameter / moment / target load of the thread's nt x 4 elements and of its
     // bias element in flight before the first update: one memory round trip
     float th[kMaxDwTiles][4], m[kMaxDwTiles][4], v[kMaxDwTiles][4], tg[kMaxDwTiles][4];
