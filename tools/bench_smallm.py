@@ -2,6 +2,7 @@
 (M x 37632 x 512, B read k-major, ReLU gate) at the batches that reach the small-M kernel
 (C3 64, ACER 336) plus 128, against the generic tile kernels (force_small = 2); prints us
 per launch and TFLOP/s (HIP events, 50 launches)."""
+import os
 import sys
 from pathlib import Path
 
@@ -14,9 +15,10 @@ sys.path.insert(0, str(ROOT))
 def main():
     from xagents_amd import _lib
     from xagents_amd.layers import gemm
-    lib = _lib.load()
+    # XA_LIB: a diagnostic variant library (tools/build_variant.py) instead of the product
+    lib = _lib.load(os.environ['XA_LIB']) if os.environ.get('XA_LIB') else _lib.load()
+    _lib._lib = lib
     dev = torch.device('cuda')
-    import os
     # XA_SMALLM_K: the depth (128 / 256 / 512 reach the small-M kernel; no shipped cfg has a
     # 128-unit dense layer, ADVICE r03: measure the K = 128 sub-row padding)
     N, K = 37632, int(os.environ.get('XA_SMALLM_K', '512'))

@@ -15,6 +15,7 @@
 #   prof     rocprofv3 --kernel-trace --stats of the default bench (no CPU baseline)
 #   pmc      FETCH_SIZE / WRITE_SIZE passes per shape (tools/gpurun_pmc_shapes.sh)
 #   c3 c4 c5 acer trpo   secondary bench lines
+#   ringab   small-M dX ring-depth variants vs product, K = 128 / 256 small-M timings
 #   c2g      C2 bench lines at update grids $C2_GS (XA_PPO_MAX_BLOCKS)
 #   profc3   rocprofv3 kernel trace of the C3 bench + per-(kernel, grid) summary
 #   gemm     GEMM tests, small-M timings, PMC passes on the dense dX GEMM
@@ -137,6 +138,17 @@ for step in "$@"; do
         > $R/gpurun_out/${T}_td3pmc2.log 2>&1) || exit 4
       python tools/pmc_summary.py td3_update $(find gpurun_out/${T}_td3pmc2 -name "*counter_collection.csv") \
         >> gpurun_out/${T}_td3pmc.txt ;;
+    ringab)
+      # small-M dense dX: B-ring depth variants (tools/diag_lib/libxa_ring*.so, built with
+      # tools/build_variant.py ringN -DXA_SMALLM_RING=N --src gemm) vs the product, and the
+      # K = 128 shapes
+      run ring_base 120 python tools/bench_smallm.py 64 336
+      for L in tools/diag_lib/libxa_ring*.so; do
+        n=$(basename $L .so); n=${n#libxa_}
+        XA_LIB=$L run ring_$n 120 python tools/bench_smallm.py 64 336
+      done
+      XA_SMALLM_K=128 run smallk128 120 python tools/bench_smallm.py 16 64 128
+      XA_SMALLM_K=256 run smallk256 120 python tools/bench_smallm.py 16 64 128 ;;
     c3) run c3 300 python bench.py --config c3 --steps 30 --warmup 5 ;;
     c4) run c4 400 python bench.py --config c4 --steps 4 --warmup 1 ;;
     c5) run c5 300 python bench.py --config c5 --steps 30 --warmup 5 ;;

@@ -470,6 +470,12 @@ __global__ __launch_bounds__(256) void gemm_tile_kernel(XaGemmK kargs) {
 // tile p (gate values fetched when the round started, ahead of the prefetches).
 // ---------------------------------------------------------------------------
 constexpr int RS_KP = 4, RS_UPR = 2;
+// rounds the B ring spans (the round loop is unrolled by this): 2 keeps 2 CH - 1 chunks of B
+// in flight per wave
+#ifndef XA_SMALLM_RING
+#define XA_SMALLM_RING 2
+#endif
+constexpr int RS_NR = XA_SMALLM_RING;
 // Resident-A row layout, conflict-free for the lane groups of ds_read_b128 (MI355X_MICROARCH.md
 // LDS table: 4 groups of 16 lanes, bank (a/4) mod 64): element k = 16 b + 4 q + j of a row
 // sits at q SR + 4 b + j -- the k quads q = 0..3 of every 16-k step in 4 sub-rows whose
@@ -510,8 +516,8 @@ __global__ __launch_bounds__(512) void gemm_smallm_res_kernel(XaGemmArgs g, int 
     return g.b + (int64_t)n * g.b_ns + kp * KQ + 4 * lq;
   };
   // B ring over the flattened chunk sequence gi = r CH + c of this wave's rounds: RS_R slots
-  // (two rounds), chunk gi + RS_R - 1 fetched while chunk gi is computed
-  constexpr int RS_R = 2 * CH;
+  // (RS_NR rounds), chunk gi + RS_R - 1 fetched while chunk gi is computed
+  constexpr int RS_R = RS_NR * CH;
   f32x4 rb[RS_R][2];
   auto load_b = [&](int gi, f32x4 (&dst)[2]) {
     const float* p = brow(gi / CH) + 32 * (gi % CH);
@@ -523,9 +529,9 @@ __global__ __launch_bounds__(512) void gemm_smallm_res_kernel(XaGemmArgs g, int 
   __syncthreads();
   const float* as = As + li * PA + lq * SR + kp * (KQ / 4);  // k = kp KQ + 16 b' + 4 lq + j
   const int mt_fin = min(kp, MT - 1);  // the m tile this wave finishes (kp < MT)
-  for (int r0 = 0; r0 < rounds; r0 += 2) {
+  for (int r0 = 0; r0 < rounds; r0 += RS_NR) {
 #pragma unroll
-    for (int par = 0; par < 2; ++par) {
+    for (int par = 0; par < RS_NR; ++par) {
       const int r = r0 + par;
       const int unit = unit_of(r);
       const bool live = unit < units;
@@ -1116,7 +1122,7 @@ extern "C" int xa_gemm(const XaGemmArgs* p, void* stream) {
       cus = 256;
     const int G = std::min(cus, (units + RS_UPR - 1) / RS_UPR);
     int rounds = (units + RS_UPR * G - 1) / (RS_UPR * G);
-    rounds += rounds & 1;  // the round loop is unrolled by 2
+    rounds = (rounds + RS_NR - 1) / RS_NR * RS_NR;  // the round loop is unrolled by RS_NR
     const int mt = (g.M + 15) / 16, ch = g.K / 128;
     const bool gate = g.gate != nullptr;
     if (mt <= 1) launch_res<1>(g, ch, gate, G, rounds, s);
