@@ -870,14 +870,49 @@ __device__ __noinline__ Acc4 dw_tile_lds(const int64_t* slots) {
     td3_bsum[threadIdx.x] = acc;
   }
   dstamp(2);
+  // one pass over k for every column tile: A's 4 k-major words per chunk read once, each
+  // tile's B words and 4 MFMAs per chunk, the next chunk's words read during this chunk's
+  // MFMAs
   Acc4 r;
+  {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int i = lane & 15, q = lane >> 4;
+    const int tstride = Kp * kCols;
 #pragma unroll
-  for (int t = 0; t < kMaxDwTiles; ++t) {
-    r.t[t] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
-    if (t < nt) {
-      Lds st = s;
-      st.B = s.B + t * Kp * kCols;
-      r.t[t] = tile_mma<false, false>(st, Kp);
+    for (int t = 0; t < kMaxDwTiles; ++t) r.t[t] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+    float4 a = mma_a<false, false>(s, 0, w, i, q);
+    float4 bb[kMaxDwTiles];
+#pragma unroll
+    for (int t = 0; t < kMaxDwTiles; ++t) {
+      const float* pb = s.B + t * tstride + 4 * q * kCols + i;
+      bb[t] = t < nt ? make_float4(pb[0], pb[kCols], pb[2 * kCols], pb[3 * kCols])
+                     : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    }
+    for (int k0 = 0; k0 < Kp; k0 += 16) {
+      const int kn = k0 + 16 < Kp ? k0 + 16 : k0;
+      const float4 an = mma_a<false, false>(s, kn, w, i, q);
+      float4 bn[kMaxDwTiles];
+#pragma unroll
+      for (int t = 0; t < kMaxDwTiles; ++t) {
+        const float* pb = s.B + t * tstride + (kn + 4 * q) * kCols + i;
+        bn[t] = t < nt ? make_float4(pb[0], pb[kCols], pb[2 * kCols], pb[3 * kCols]) : bb[t];
+      }
+      // (k step outer, tile inner: consecutive MFMAs on independent accumulators)
+#pragma unroll
+      for (int t = 0; t < kMaxDwTiles; ++t)
+        if (t < nt) r.t[t] = mfma4(a.x, bb[t].x, r.t[t]);
+#pragma unroll
+      for (int t = 0; t < kMaxDwTiles; ++t)
+        if (t < nt) r.t[t] = mfma4(a.y, bb[t].y, r.t[t]);
+#pragma unroll
+      for (int t = 0; t < kMaxDwTiles; ++t)
+        if (t < nt) r.t[t] = mfma4(a.z, bb[t].z, r.t[t]);
+#pragma unroll
+      for (int t = 0; t < kMaxDwTiles; ++t)
+        if (t < nt) r.t[t] = mfma4(a.w, bb[t].w, r.t[t]);
+      a = an;
+#pragma unroll
+      for (int t = 0; t < kMaxDwTiles; ++t) bb[t] = bn[t];
     }
   }
   dstamp(3);
