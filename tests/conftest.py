@@ -22,6 +22,11 @@ def device():
     from xagents_amd import _lib
 
     _lib.load()  # raises loudly if the extension is missing
+    import os
+    if os.environ.get('XA_LIB'):
+        # (diagnostic A/B only) run the GPU tests against a variant build of the library
+        # (tools/build_variant.py); the driver's runs never set it
+        _lib._lib = _lib.load(os.environ['XA_LIB'])
     return torch.device('cuda')
 
 

@@ -15,6 +15,7 @@
 #   prof     rocprofv3 --kernel-trace --stats of the default bench (no CPU baseline)
 #   pmc      FETCH_SIZE / WRITE_SIZE passes per shape (tools/gpurun_pmc_shapes.sh)
 #   c3 c4 c5 acer trpo   secondary bench lines
+#   rsplit   two-wave rollout step variant: bit-exact tests on it + bench A/B
 #   ringab   small-M dX ring-depth variants vs product, K = 128 / 256 small-M timings
 #   c2g      C2 bench lines at update grids $C2_GS (XA_PPO_MAX_BLOCKS)
 #   profc3   rocprofv3 kernel trace of the C3 bench + per-(kernel, grid) summary
@@ -149,6 +150,15 @@ for step in "$@"; do
       done
       XA_SMALLM_K=128 run smallk128 120 python tools/bench_smallm.py 16 64 128
       XA_SMALLM_K=256 run smallk256 120 python tools/bench_smallm.py 16 64 128 ;;
+    rsplit)
+      # the two-wave rollout step (XA_ROLL_SPLIT=1 variant, tools/diag_lib/libxa_rsplit.so):
+      # bit-exact vs the oracle (the rollout tests on the variant), then bench A/B
+      XA_LIB=tools/diag_lib/libxa_rsplit.so run_pytest rsplit_test 200 tests/test_gpu_kernels.py -k rollout
+      B="python bench.py --steps 40 --warmup 5 --cpu-baseline-seconds 0 --no-secondary"
+      run rs_base1 200 $B
+      run rs_split 200 $B --lib tools/diag_lib/libxa_rsplit.so
+      run rs_base2 200 $B
+      python tools/bench_brief.py gpurun_out/${T}_rs_*.out ;;
     c3) run c3 300 python bench.py --config c3 --steps 30 --warmup 5 ;;
     c4) run c4 400 python bench.py --config c4 --steps 4 --warmup 1 ;;
     c5) run c5 300 python bench.py --config c5 --steps 30 --warmup 5 ;;
