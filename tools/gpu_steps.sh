@@ -62,8 +62,13 @@ for step in "$@"; do
     configs) run_pytest configs 400 tests/test_gpu_configs.py ;;
     td3) run_pytest td3 400 tests/test_gpu_td3.py tests/test_gpu_scale.py tests/test_gpu_configs.py::test_c5_td3_64_envs_rb2 ;;
     td3time)
+      # wall time per gradient step on the product build, per-phase barrier times on the
+      # trace build (tools/diag_lib/libxa_td3trace.so: tools/build_variant.py td3trace
+      # -DXA_TD3_TRACE=1 --src td3_update)
       for G in ${TD3_GS:-64 128 256}; do
         XA_TD3_BLOCKS=$G run td3time_$G 120 python tools/td3_grad_steps.py 50
+        XA_TD3_BLOCKS=$G XA_LIB=tools/diag_lib/libxa_td3trace.so run td3trace_$G 120 \
+          python tools/td3_grad_steps.py 50
       done ;;
     c4w2)
       # W = 2 rehearsal of the C4 data-parallel bench with both ranks on the one GPU (gloo;

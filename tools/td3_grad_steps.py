@@ -1,7 +1,7 @@
 """C5 (TD3, 64 BipedalWalker-shaped envs, ReplayBuffer2) gradient steps alone, for a
 rocprofv3 kernel trace of one gradient step's launches (tools/gpu_steps.sh profc5).
 
-usage: python tools/td3_grad_steps.py [n_steps]"""
+usage: python tools/td3_grad_steps.py [n_steps]   (XA_LIB=<trace build>: + per-phase times)"""
 import sys
 import time
 from pathlib import Path
@@ -11,9 +11,15 @@ sys.path.insert(0, str(ROOT))
 
 
 def main():
+    import os
+
     import numpy as np
     import torch
-    from xagents_amd import TD3
+    from xagents_amd import TD3, _lib
+    if os.environ.get('XA_LIB'):
+        # the per-phase trace needs a diagnostic build (tools/build_variant.py td3trace
+        # -DXA_TD3_TRACE=1 --src td3_update): the product writes no trace
+        _lib._lib = _lib.load(os.environ['XA_LIB'])
     from xagents_amd.envs import create_envs
     from xagents_amd.utils.common import create_buffers, create_model
     n_steps = int(sys.argv[1]) if len(sys.argv) > 1 else 50
@@ -35,7 +41,7 @@ def main():
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / n_steps
     print(f'TD3 gradient step: {dt * 1e3:.4f} ms ({n_steps} steps, graph replay)', flush=True)
-    if agent._fused_args() is not None:
+    if agent._fused_args() is not None and os.environ.get('XA_LIB'):
         # per-phase barrier times of the fused launch (block 0's 100 MHz wall clock, the
         # workspace control area's trace words: [0] start, [i] barrier i done, [15] end)
         import numpy as np

@@ -249,7 +249,13 @@ __shared__ __attribute__((aligned(16))) float td3_part[2 * 32 * 16];
 // the workspace's detail trace (tools/td3_grad_steps.py): slot 8 p + point
 __shared__ int td3_dslot;
 __shared__ unsigned long long* td3_dbuf;
+// (diagnostic builds only: -DXA_TD3_TRACE=1, tools/build_variant.py; a trace store in the
+// product would hold block 0 one store round trip at every barrier)
+#ifndef XA_TD3_TRACE
+#define XA_TD3_TRACE 0
+#endif
 XA_DEV void dstamp(int point) {
+  if (!XA_TD3_TRACE) return;
   if (threadIdx.x == 0 && td3_dslot >= 0)
     *((__attribute__((address_space(1))) unsigned long long*)td3_dbuf + td3_dslot + point) =
         wall_clock64();
@@ -1191,7 +1197,7 @@ XA_DEV bool grid_sync(Sync& y, int& lds_flag, int jobs) {
       __builtin_amdgcn_s_sleep(1);
     }
     lds_flag = ok;
-    if (y.trace && y.n < 15) y.trace[y.n] = wall_clock64();
+    if (XA_TD3_TRACE && y.trace && y.n < 15) y.trace[y.n] = wall_clock64();
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   __syncthreads();
@@ -1291,7 +1297,7 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
   y.n = 0;
   y.status = p.status;
   y.trace = b == 0 ? ws.trace : nullptr;
-  if (b == 0 && tid == 0) ws.trace[0] = wall_clock64();
+  if (XA_TD3_TRACE && b == 0 && tid == 0) ws.trace[0] = wall_clock64();
   if (tid == 0) {
     td3_dslot = b == 0 ? 8 * 15 : -1;  // (diagnostic) the prologue's points in slot 15
     td3_dbuf = ws.dtrace;
@@ -1633,7 +1639,8 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
     if (p.smooth && p.rng_counter) *p.rng_counter += 1ull;
     *ws.base = y.target;
     *ws.epoch = y.epoch;
-    ws.trace[15] = wall_clock64();  // block 0's end (the last phase's tail may run on)
+    // block 0's end (the last phase's tail may run on)
+    if (XA_TD3_TRACE) ws.trace[15] = wall_clock64();
   }
 }
 
