@@ -331,8 +331,8 @@ def fused_td3_roofline(agent, launches=10):
             'frac': round(tf / F32_MFMA_PEAK_TFLOPS, 5), 'traffic': None,
             'launch_ms': round(ms, 5), 'flops_per_launch': int(flops),
             'note': f'2 M N K FLOP of every GEMM of the step at batch {agent.batch_size}, '
-                    f'mean of {len(rows)} event-timed launches; latency-bound (grid barriers '
-                    f'between 8 / 14 phases)'}
+                    f'mean of {len(rows)} event-timed launches; latency-bound (5 / 10 grid '
+                    f'barriers between the 6 / 11 phases of a critic / policy step)'}
 
 
 def bench_offpolicy_and_cnn(args):
