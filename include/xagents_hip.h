@@ -726,6 +726,34 @@ typedef struct XaTd3UpdateArgs {
 size_t xa_td3_update_workspace_bytes(int batch, int obs_dim, int act_dim, int h1, int h2);
 int xa_td3_update(const XaTd3UpdateArgs* args, void* stream);
 
+/* The exploration step's actions of DDPG / TD3 in ONE launch (DDPG.get_step_actions,
+ * ddpg/agent.py:60-71, with the actor of actor_model.cfg: in -> h1 relu -> h2 relu -> act
+ * tanh): out[i][a] = clip(tanh(actor(states[i]))[a] + noise, lo, hi), noise = clip(sigma
+ * N(0, 1), +-noise_clip) drawn by Philox4x32-10 at (i, a, *rng_counter, seed) exactly as
+ * xa_noisy_actions draws it (noise_out optional); *rng_counter += 1 at the end when bump.
+ * theta: the actor's flat Keras-order parameters. Workspace (xa_td3_act_workspace_bytes)
+ * zeroed once by the caller and reused by every launch; n <= 256, h1, h2 <= 416 and
+ * multiples of 4, act_dim <= 4. */
+typedef struct XaTd3ActArgs {
+  int n, obs_dim, act_dim, h1, h2;
+  const float* states;
+  const float* theta;
+  float sigma, noise_clip, lo, hi;
+  uint64_t* rng_counter;
+  uint64_t seed;
+  int bump;
+  float* out;
+  int ld_out;
+  float* noise_out;
+  void* workspace;
+  size_t workspace_bytes;
+  int n_blocks;
+  int* status;
+} XaTd3ActArgs;
+
+size_t xa_td3_act_workspace_bytes(int n, int obs_dim, int act_dim, int h1, int h2);
+int xa_td3_act(const XaTd3ActArgs* args, void* stream);
+
 /* TFP Categorical(logits) over n logit rows (A2C.get_model_outputs, a2c/agent.py:65-94):
  * log-prob and entropy of the given actions (actions_in) or of an inverse-CDF sample
  * with uniforms[i] or Philox(i, step, *rng_counter, seed). Same arithmetic as the fused

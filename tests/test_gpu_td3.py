@@ -154,3 +154,45 @@ def test_captured_env_phase_matches_eager(device, kind):
         np.testing.assert_array_equal(a, b)
     assert out[0][1] == out[1][1]
     assert out[1][1][0] > 0  # some episodes finished (gradient steps ran)
+
+
+@pytest.mark.parametrize('kind', ['td3', 'ddpg'])
+def test_fused_step_actions_vs_f64(device, kind):
+    """get_step_actions in one launch (xa_td3_act): clip(tanh(actor(s)) + noise, -1, 1)
+    against the float64 actor forward with the noise the launch drew; the draw is bit-equal
+    to xa_noisy_actions' at the same counter, and the counter advances by one per call.
+    40 envs: a full and a ragged 32-row tile."""
+    sys.path.insert(0, str(ROOT / 'oracle'))
+    import nets_f64 as O
+    from xagents_amd._lib import call, stream
+    agent = _agent(device, kind, n=40)
+    fa = agent._fused_act_args()
+    assert fa is not None
+    torch.manual_seed(0)
+    agent.envs.state.copy_(torch.randn_like(agent.envs.state))
+    c0 = int(agent.rng_counter.item())
+    noise = torch.zeros_like(agent.step_actions)
+    fa.noise_out = noise.data_ptr()
+    try:
+        out = agent.get_step_actions().clone()
+    finally:
+        fa.noise_out = None
+    torch.cuda.synchronize()
+    assert int(agent.rng_counter.item()) == c0 + 1
+    nz = _np(noise)
+    assert nz.std() > 0.01
+    act = agent.actor
+    _, o = O.forward(act.layers, _np(act.theta), _np(agent.envs.state), act.input_shape)
+    ref = np.clip(o[act.outputs[0]] + nz, -1, 1)
+    np.testing.assert_allclose(_np(out), ref, rtol=0, atol=1e-5)
+    # xa_noisy_actions' draw at the same counter (zero input, unbounded clip)
+    ctr = agent.rng_counter.clone().fill_(c0)
+    zero = torch.zeros_like(agent.step_actions)
+    n2 = torch.zeros_like(zero)
+    o2 = torch.zeros_like(zero)
+    rows, cols = zero.shape
+    call('xa_noisy_actions', zero.data_ptr(), cols, rows, cols,
+         float(np.float32(agent.step_noise_coef)), float('inf'), float('-inf'), float('inf'),
+         ctr.data_ptr(), agent.rng_seed, o2.data_ptr(), cols, n2.data_ptr(), stream())
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(_np(n2), nz)

@@ -329,6 +329,18 @@ class XaTd3UpdateArgs(Structure):
     ]
 
 
+class XaTd3ActArgs(Structure):
+    _fields_ = [
+        ('n', c_int), ('obs_dim', c_int), ('act_dim', c_int), ('h1', c_int), ('h2', c_int),
+        ('states', c_void_p), ('theta', c_void_p),
+        ('sigma', c_float), ('noise_clip', c_float), ('lo', c_float), ('hi', c_float),
+        ('rng_counter', c_void_p), ('seed', c_uint64), ('bump', c_int),
+        ('out', c_void_p), ('ld_out', c_int), ('noise_out', c_void_p),
+        ('workspace', c_void_p), ('workspace_bytes', ctypes.c_size_t),
+        ('n_blocks', c_int), ('status', c_void_p),
+    ]
+
+
 XA_RING_DEQUE = 0
 XA_RING_RB2 = 1
 XA_ACT_NONE = 0
@@ -425,6 +437,8 @@ _SIGNATURES = {
     'xa_ac_head_grad': (c_int, [POINTER(XaHeadGradArgs), c_void_p]),
     'xa_td3_update_workspace_bytes': (ctypes.c_size_t, [c_int, c_int, c_int, c_int, c_int]),
     'xa_td3_update': (c_int, [POINTER(XaTd3UpdateArgs), c_void_p]),
+    'xa_td3_act_workspace_bytes': (ctypes.c_size_t, [c_int, c_int, c_int, c_int, c_int]),
+    'xa_td3_act': (c_int, [POINTER(XaTd3ActArgs), c_void_p]),
     'xa_minibatch_adv_sums': (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                                       c_void_p, c_void_p]),
     'xa_diag_gaussian': (

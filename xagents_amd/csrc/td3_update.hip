@@ -1644,6 +1644,71 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
   }
 }
 
+// ---- the exploration step's actions (DDPG.get_step_actions, ddpg/agent.py:60-71):
+// clip(tanh(actor(s)) + N(0, sigma) clipped, lo, hi) for the env states in ONE launch -- P1
+// actor L1 on the states, P2 actor L2 with the L3 partials; each row tile's last job
+// finishes tanh + noise (the same Philox draw as xa_noisy_actions) + clip. One grid
+// barrier; block 0 bumps the noise counter at the end (every block read it at launch
+// start) ----
+__global__ __launch_bounds__(256) void td3_act_kernel(XaTd3ActArgs p) {
+  __shared__ int s_flag;
+  const int G = gridDim.x, b = blockIdx.x, tid = threadIdx.x;
+  const int n = p.n, S = p.obs_dim, A = p.act_dim, H1 = p.h1, H2 = p.h2;
+  const Ws ws = carve(p.workspace, n, H1, H2, A);
+  Sync y;
+  y.cnt = ws.cnt;
+  y.abort_w = ws.abort_w;
+  y.target = *ws.base;
+  y.epoch = *ws.epoch + 1u;
+  y.G = (unsigned)G;
+  y.n = 0;
+  y.status = p.status;
+  y.trace = nullptr;
+  if (tid == 0) {
+    td3_dslot = -1;
+    td3_dbuf = ws.dtrace;
+  }
+  const uint64_t ctr = p.rng_counter ? *p.rng_counter : 0ull;
+  XaTdNet d{};
+  d.theta = const_cast<float*>(p.theta);
+  const Net ac = make_net(d, S, H1, H2, A, false);
+  const int RTT = (n + kTR - 1) / kTR;
+  const int CT1 = (H1 + kCols - 1) / kCols, CT2 = (H2 + kCols - 1) / kCols;
+  __syncthreads();
+  for (int j = b; j < RTT * CT1; j += G) {
+    const int rt = j / CT1, ct = j % CT1;
+    fwd_job(xsrc(p.states, S, S, false, false), nullptr, rt * kTR, n, ac.th + ac.w1,
+            ac.th + ac.b1, S, H1, ct * kCols, ACT_RELU, ws.h1(N_AC));
+    __syncthreads();
+  }
+  if (!grid_sync(y, s_flag, RTT * CT1)) return;
+  for (int j = b; j < RTT * CT2; j += G) {
+    const int rt = j / CT2, ct = j % CT2;
+    const Head hd{ac.th + ac.w3, ws.hp3(N_AC), ws.ticket(N_AC, rt), A, 1, A, ct, CT2, false};
+    if (fwd_job(xsrc(ws.h1(N_AC), H1, H1, false, true), nullptr, rt * kTR, n, ac.th + ac.w2,
+                ac.th + ac.b2, H1, H2, ct * kCols, ACT_RELU, ws.h2(N_AC), false, hd)) {
+      const int r0 = rt * kTR, nr = min(kTR, n - r0);
+      for (int e = tid; e < nr * A; e += 256) {
+        const int row = r0 + e / A, c = e % A;
+        const float z = head_total(ws.hp3(N_AC), CT2, n, A, row, c) + ac.th[ac.b3 + c];
+        float nz = 0.0f;
+        if (p.sigma != 0.0f) {
+          nz = philox_normal((uint32_t)row, (uint32_t)c, ctr, p.seed) * p.sigma;
+          nz = fminf(fmaxf(nz, -p.noise_clip), p.noise_clip);
+        }
+        if (p.noise_out) p.noise_out[row * A + c] = nz;
+        p.out[(int64_t)row * p.ld_out + c] = fminf(fmaxf(xa_tanhf(z) + nz, p.lo), p.hi);
+      }
+    }
+    __syncthreads();
+  }
+  if (b == 0 && tid == 0) {
+    if (p.bump && p.rng_counter) *p.rng_counter += 1ull;
+    *ws.base = y.target;
+    *ws.epoch = y.epoch;
+  }
+}
+
 }  // namespace
 
 extern "C" size_t xa_td3_update_workspace_bytes(int batch, int obs_dim, int act_dim, int h1,
@@ -1680,5 +1745,34 @@ extern "C" int xa_td3_update(const XaTd3UpdateArgs* p, void* stream) {
   const size_t lds = sizeof(float) * ((size_t)(kRows + kCols) * kMaxK + kAux);
   hipLaunchKernelGGL(td3_update_kernel, dim3(G), dim3(256), lds, (hipStream_t)stream, a);
   XA_CHECK_LAUNCH("xa_td3_update");
+  return 0;
+}
+
+extern "C" size_t xa_td3_act_workspace_bytes(int n, int obs_dim, int act_dim, int h1, int h2) {
+  (void)obs_dim;
+  return carve(nullptr, n, h1, h2, act_dim).total;
+}
+
+extern "C" int xa_td3_act(const XaTd3ActArgs* p, void* stream) {
+  XA_CHECK_ARG(p != nullptr, "xa_td3_act: null args");
+  const XaTd3ActArgs& a = *p;
+  XA_CHECK_ARG(a.n > 0 && a.n <= 256 && a.obs_dim > 0 && a.act_dim > 0 && a.act_dim <= 4 &&
+                   a.h1 > 0 && a.h2 > 0 && a.h1 <= kMaxK && a.h2 <= kMaxK && a.h1 % 4 == 0 &&
+                   a.h2 % 4 == 0 && a.obs_dim <= 64 && a.ld_out >= a.act_dim,
+               "xa_td3_act: sizes beyond the kernel's tiles (n <= 256; h1, h2 <= %d and "
+               "multiples of 4; act <= 4; obs <= 64)",
+               kMaxK);
+  XA_CHECK_ARG(a.states && a.theta && a.out && a.workspace &&
+                   a.workspace_bytes >= carve(nullptr, a.n, a.h1, a.h2, a.act_dim).total,
+               "xa_td3_act: missing buffers or workspace too small");
+  int cus = 256, dev = 0;
+  if (hipGetDevice(&dev) == hipSuccess)
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  // jobs per phase: (n / 32) x (h / 16); no more workgroups than the wider phase holds
+  const int jobs = ((a.n + kTR - 1) / kTR) * ((max(a.h1, a.h2) + kCols - 1) / kCols);
+  const int G = a.n_blocks > 0 ? min(a.n_blocks, cus) : min(min(jobs, 256), cus);
+  const size_t lds = sizeof(float) * ((size_t)(kRows + kCols) * kMaxK + kAux);
+  hipLaunchKernelGGL(td3_act_kernel, dim3(G), dim3(256), lds, (hipStream_t)stream, a);
+  XA_CHECK_LAUNCH("xa_td3_act");
   return 0;
 }

@@ -116,10 +116,49 @@ class DDPG(OffPolicy):
 
     # ---- reference surface ---------------------------------------------------------
     def get_step_actions(self):
-        """clip(actor(s) + N(0, step_noise_coef), -1, 1) (ddpg/agent.py:60-71)."""
+        """clip(actor(s) + N(0, step_noise_coef), -1, 1) (ddpg/agent.py:60-71): one launch
+        (xa_td3_act: actor forward, tanh, the noise and the clip, the counter bump) when the
+        actor is the 3-layer .cfg MLP; otherwise the layer executor + xa_noisy_actions."""
+        fa = self._fused_act_args()
+        if fa is not None:
+            fa.states = self.envs.state.data_ptr()
+            call('xa_td3_act', ctypes.byref(fa), stream())
+            return self.step_actions
         a = self.ex_step.forward(self.envs.state)[0]
         self._noisy(a, self.step_noise_coef, float('inf'), self.step_actions)
         return self.step_actions
+
+    def _fused_act_args(self):
+        """xa_td3_act's launch arguments (built once), or None (other actor shapes, an env
+        batch over 256 or a non-contiguous f32 state)."""
+        if '_fused_act' in self.__dict__:
+            return self.__dict__['_fused_act']
+        import os
+        from xagents_amd import _lib
+        from xagents_amd._lib import XaTd3ActArgs
+        fa = None
+        st = getattr(self.envs, 'state', None)
+        if (os.environ.get('XA_TD3_FUSED', '1') != '0' and self._fused_ok() and
+                isinstance(st, torch.Tensor) and st.dtype == torch.float32 and st.dim() == 2 and
+                st.is_contiguous() and st.shape[1] == self.S and st.shape[0] <= 256):
+            fa = XaTd3ActArgs()
+            n, S, A = st.shape[0], self.S, self.A
+            H1, H2 = self.actor.layers[0].units, self.actor.layers[1].units
+            fa.n, fa.obs_dim, fa.act_dim, fa.h1, fa.h2 = n, S, A, H1, H2
+            fa.states, fa.theta = st.data_ptr(), self.actor.theta.data_ptr()
+            fa.sigma = kernels._f32(self.step_noise_coef)
+            fa.noise_clip = float('inf')
+            fa.lo, fa.hi = kernels._f32(-1.0), kernels._f32(1.0)
+            fa.rng_counter, fa.seed, fa.bump = self.rng_counter.data_ptr(), self.rng_seed, 1
+            fa.out, fa.ld_out = self.step_actions.data_ptr(), self.step_actions.shape[1]
+            fa.noise_out = None
+            nbytes = _lib.load().xa_td3_act_workspace_bytes(n, S, A, H1, H2)
+            self._fused_act_ws = torch.zeros(nbytes, dtype=torch.uint8, device=self.device)
+            fa.workspace, fa.workspace_bytes = self._fused_act_ws.data_ptr(), nbytes
+            fa.n_blocks = int(os.environ.get('XA_TD3_ACT_BLOCKS', '0'))
+            fa.status = None
+        self.__dict__['_fused_act'] = fa
+        return fa
 
     def _play_actions(self):
         """play(): the actor's output without exploration noise (self.actor(states),
