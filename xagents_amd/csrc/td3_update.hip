@@ -565,6 +565,18 @@ struct Head {
 };
 XA_DEV Head no_head() { return Head{nullptr, nullptr, nullptr, 0, 0, 0, 0, 1, false}; }
 __shared__ int td3_last;
+// B operand of the block's first job in the next phase, staged by LDS-DMA while the grid
+// barrier waits (the weights of that job were last written before the barrier the block is
+// in); td3_bpre tells the job to skip its own B staging
+__shared__ int td3_bpre;
+struct PreB {
+  const float* W;
+  int kind;  // 0 none; 1 forward (KM rows k < K, columns c0 .. of W [K][N]); 2 input
+             // gradient (CR rows c0 .. c0 + nc of W [in][K])
+  int N, K, c0, nc;
+  bool coh;
+};
+XA_DEV PreB no_preb() { return PreB{nullptr, 0, 0, 0, 0, 0, false}; }
 // thread t < 4 kTR holds y[row][c .. c + 3] (zeros outside the tile): its quad's sum
 // (lanes t ^ 1, t ^ 2) is the 16-column partial of every n; lane n of the quad stores n
 XA_DEV bool head_partial(const Head& h, const float (&wv)[4][4], float4 y, int row, int B) {
@@ -705,13 +717,16 @@ __device__ __noinline__ bool fwd_tile(const int64_t* slots) {
   else
     sload(kTR, Kp, nrows, K, [&](int r, int k) { return xload(x, slots, r0 + r, k); },
           [&](int r, int k, float v) { s.A[cr_idx(r, k, kTR)] = v; });
-  if ((N & 3) == 0 && (c0 & 3) == 0 && (nc & 3) == 0)
+  const bool bpre = td3_bpre != 0;  // (staged during the barrier: the same DMA)
+  if (bpre) {
+  } else if ((N & 3) == 0 && (c0 & 3) == 0 && (nc & 3) == 0)
     dma_km(s.B, kCols, W, N, c0, nullptr, K, nc, Kp, coh);
   else
     sload(Kp, kCols, K, nc, [&](int k, int j) { return ldw(W + (int64_t)k * N + c0 + j, coh); },
           [&](int k, int j, float v) { s.B[k * kCols + j] = v; });
   dstamp(1);
   dma_wait();
+  if (bpre && threadIdx.x == 0) td3_bpre = 0;
   dstamp(2);
   tile_mma_split<false>(s, Kp);
   dstamp(3);
@@ -769,7 +784,9 @@ __device__ __noinline__ bool dx_tile_lds() {
   else
     sload(kTR, Kp, nrows, K, [&](int r, int k) { return ldc(src + (int64_t)(r0 + r) * d.ld + k); },
           [&](int r, int k, float v) { s.A[cr_idx(r, k, kTR)] = v; });
-  if ((K & 3) == 0)
+  const bool bpre = td3_bpre != 0;  // (staged during the barrier: the same DMA)
+  if (bpre) {
+  } else if ((K & 3) == 0)
     dma_cr(s.B, kCols, W, K, c0, nullptr, nc, K, Kp, coh);
   else
     sload(kCols, Kp, nc, K, [&](int j, int k) { return ldw(W + (int64_t)(c0 + j) * K + k, coh); },
@@ -777,6 +794,7 @@ __device__ __noinline__ bool dx_tile_lds() {
   aux_store(s, d, ax, K, nrows);
   dstamp(1);
   dma_wait();
+  if (bpre && threadIdx.x == 0) td3_bpre = 0;
   if (d.h2) {
     // 4 consecutive k of one row per float4 (K % 4 == 0 on this path)
     for (int e4 = threadIdx.x; e4 < kTR * Kp / 4; e4 += 256) {
@@ -1166,16 +1184,27 @@ XA_DEV unsigned shard_sum(const unsigned* cnt) {
   return t;
 }
 
-XA_DEV bool grid_sync(Sync& y, int& lds_flag, int jobs) {
+XA_DEV bool grid_sync(Sync& y, int& lds_flag, int jobs, const PreB& pb = no_preb()) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   y.n += 1;
   const unsigned m = (unsigned)min((int)y.G, max(jobs, 0));
   y.target += m;
+  if (threadIdx.x == 0 && blockIdx.x < m)
+    __hip_atomic_fetch_add((gu32*)(y.cnt + kShardStride * (blockIdx.x % kShards)), 1u,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // the next job's weights into LDS while the barrier waits (every wave issues its share)
+  if (pb.kind == 1 && (pb.N & 3) == 0 && (pb.c0 & 3) == 0) {
+    const int nc = min(kCols, pb.N - pb.c0);
+    if ((nc & 3) == 0) {
+      dma_km(lds().B, kCols, pb.W, pb.N, pb.c0, nullptr, pb.K, nc, pad16(pb.K), pb.coh);
+      if (threadIdx.x == 0) td3_bpre = 1;
+    }
+  } else if (pb.kind == 2 && (pb.K & 3) == 0) {
+    dma_cr(lds().B, kCols, pb.W, pb.K, pb.c0, nullptr, pb.nc, pb.K, pad16(pb.K), pb.coh);
+    if (threadIdx.x == 0) td3_bpre = 1;
+  }
   if (threadIdx.x == 0) {
-    if (blockIdx.x < m)
-      __hip_atomic_fetch_add((gu32*)(y.cnt + kShardStride * (blockIdx.x % kShards)), 1u,
-                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     int ok = 1;
     const uint64_t t0 = wall_clock64();
     for (unsigned it = 0;; ++it) {
@@ -1301,6 +1330,7 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
   if (tid == 0) {
     td3_dslot = b == 0 ? 8 * 15 : -1;  // (diagnostic) the prologue's points in slot 15
     td3_dbuf = ws.dtrace;
+    td3_bpre = 0;
   }
   dstamp(0);
   // networks; the step counters as the launch finds them are read here (in flight with the
@@ -1383,6 +1413,46 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
     return xcat(xsrc(rs, S, S, true, false), ra, A, A, true, false);  // [s, a]
   };
   const uint64_t ctr = p.rng_counter ? *p.rng_counter : 0ull;
+  // the B operand of this block's first job in the next phase (prefetched at the barrier;
+  // the same job enumeration as the phase loops below)
+  auto pre_fwd = [&](const float* W, int N, int K, int ct, bool coh) {
+    return PreB{W, 1, N, K, ct * kCols, min(kCols, N - ct * kCols), coh};
+  };
+  auto pre_dx = [&](const float* W, int K, int ct, bool coh) {
+    return PreB{W, 2, 0, K, ct * kCols, min(kCols, H1 - ct * kCols), coh};
+  };
+  auto pre_p2 = [&]() {
+    const int per = RTT * CT2;
+    if (b >= nn * per) return no_preb();
+    const Net n = net_of(net_id(b / per));
+    return pre_fwd(n.th + n.w2, H2, H1, (b % per) % CT2, false);
+  };
+  auto pre_p5 = [&]() {
+    const int per = RTT * CT2, ntc = twin ? 2 : 1;
+    if (b >= ntc * per) return no_preb();
+    const Net n = net_of(N_TC1 + b / per);
+    return pre_fwd(n.th + n.w2, H2, H1, (b % per) % CT2, false);
+  };
+  auto pre_p7 = [&]() {
+    const int IT1 = (H1 + kRows - 1) / kRows, IT2 = (H2 + kRows - 1) / kRows;
+    const int n_dx = RTT * CT1, per = n_dx + IT1 * CTW2 + IT2, ntc = twin ? 2 : 1;
+    const int ci = b / per, q = b % per;
+    if (b >= ntc * per || q >= n_dx) return no_preb();
+    const Net n = ci ? c2 : c1;
+    return pre_dx(n.th + n.w2, H2, q % CT1, false);
+  };
+  auto pre_p10 = [&]() {
+    if (b >= RTT * CT2) return no_preb();
+    return pre_fwd(c1.th + c1.w2, H2, H1, b % CT2, true);
+  };
+  auto pre_p11 = [&]() {
+    if (b >= RTT * CT1) return no_preb();
+    return pre_dx(c1.th + c1.w2, H2, b % CT1, true);
+  };
+  auto pre_p13 = [&]() {
+    if (b >= RTT * CT1) return no_preb();  // (the input-gradient jobs come first)
+    return pre_dx(ac.th + ac.w2, H2, b % CT1, false);
+  };
   for (int layer = 1; layer <= 2; ++layer) {
     const int CT = layer == 1 ? CT1 : CT2, per = RTT * CT;
     for (int j = b; j < nn * per; j += G) {
@@ -1426,7 +1496,7 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
       }
       __syncthreads();
     }
-    if (!grid_sync(y, s_flag, nn * per)) return;
+    if (!grid_sync(y, s_flag, nn * per, layer == 1 ? pre_p2() : no_preb())) return;
   }
 
   // ---- P4 / P5: target critics L1 on [s', a'], L2 (+ the target values' partials; the
@@ -1480,7 +1550,7 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
       }
       __syncthreads();
     }
-    if (!grid_sync(y, s_flag, nt * per)) return;
+    if (!grid_sync(y, s_flag, nt * per, layer == 1 ? pre_p5() : pre_p7())) return;
   }
 
   // ---- P7: critics backward (dW2 / db2, dH1, dW3 / db3) ----
@@ -1561,7 +1631,7 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
                   c1.th + c1.b2, H1, H2, ct * kCols, ACT_RELU, ws.q2, true);
         __syncthreads();
       }
-      if (!grid_sync(y, s_flag, RTT * CT)) return;
+      if (!grid_sync(y, s_flag, RTT * CT, layer == 1 ? pre_p10() : pre_p11())) return;
     }
     // ---- P11: dH1 of -mean Q (dQ / dv = -1 / B per row), + the partials of
     // d pi(s) = dH1 W1[S + a][:]^T; the row tile's last job forms the actor's output
@@ -1584,7 +1654,7 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
       }
       __syncthreads();
     }
-    if (!grid_sync(y, s_flag, RTT * CT1)) return;
+    if (!grid_sync(y, s_flag, RTT * CT1, pre_p13())) return;
     // ---- P13: actor backward (dW2 / db2, dH1, dW3 / db3) ----
     {
       const int IT1 = (H1 + kRows - 1) / kRows, IT2 = (H2 + kRows - 1) / kRows;
@@ -1667,6 +1737,7 @@ __global__ __launch_bounds__(256) void td3_act_kernel(XaTd3ActArgs p) {
   if (tid == 0) {
     td3_dslot = -1;
     td3_dbuf = ws.dtrace;
+    td3_bpre = 0;
   }
   const uint64_t ctr = p.rng_counter ? *p.rng_counter : 0ull;
   XaTdNet d{};
@@ -1681,7 +1752,12 @@ __global__ __launch_bounds__(256) void td3_act_kernel(XaTd3ActArgs p) {
             ac.th + ac.b1, S, H1, ct * kCols, ACT_RELU, ws.h1(N_AC));
     __syncthreads();
   }
-  if (!grid_sync(y, s_flag, RTT * CT1)) return;
+  auto pre_act2 = [&]() {
+    if (b >= RTT * CT2) return no_preb();
+    const int ct = b % CT2;
+    return PreB{ac.th + ac.w2, 1, H2, H1, ct * kCols, min(kCols, H2 - ct * kCols), false};
+  };
+  if (!grid_sync(y, s_flag, RTT * CT1, pre_act2())) return;
   for (int j = b; j < RTT * CT2; j += G) {
     const int rt = j / CT2, ct = j % CT2;
     const Head hd{ac.th + ac.w3, ws.hp3(N_AC), ws.ticket(N_AC, rt), A, 1, A, ct, CT2, false};
