@@ -128,6 +128,10 @@ class DDPG(OffPolicy):
         self._noisy(a, self.step_noise_coef, float('inf'), self.step_actions)
         return self.step_actions
 
+    def _step_noise(self):
+        """(sigma, counter bump) of the exploration step: DDPG draws N(0, step_noise_coef)."""
+        return self.step_noise_coef, 1
+
     def _fused_act_args(self):
         """xa_td3_act's launch arguments (built once), or None (other actor shapes, an env
         batch over 256 or a non-contiguous f32 state)."""
@@ -146,10 +150,11 @@ class DDPG(OffPolicy):
             H1, H2 = self.actor.layers[0].units, self.actor.layers[1].units
             fa.n, fa.obs_dim, fa.act_dim, fa.h1, fa.h2 = n, S, A, H1, H2
             fa.states, fa.theta = st.data_ptr(), self.actor.theta.data_ptr()
-            fa.sigma = kernels._f32(self.step_noise_coef)
+            sigma, bump = self._step_noise()
+            fa.sigma = kernels._f32(sigma)
             fa.noise_clip = float('inf')
             fa.lo, fa.hi = kernels._f32(-1.0), kernels._f32(1.0)
-            fa.rng_counter, fa.seed, fa.bump = self.rng_counter.data_ptr(), self.rng_seed, 1
+            fa.rng_counter, fa.seed, fa.bump = self.rng_counter.data_ptr(), self.rng_seed, bump
             fa.out, fa.ld_out = self.step_actions.data_ptr(), self.step_actions.shape[1]
             fa.noise_out = None
             nbytes = _lib.load().xa_td3_act_workspace_bytes(n, S, A, H1, H2)

@@ -8,6 +8,8 @@ architecture (its own initialisation -- identical to critic1's when the model se
 set, as seeded Keras initializers give the same draw) with its own Adam at critic1's
 learning rate; target_critic2 copies critic2.
 """
+import ctypes
+
 import numpy as np
 import torch
 
@@ -58,11 +60,20 @@ class TD3(DDPG):
         self._sync_params(self.critic2, self.target_critic2)
 
     def get_step_actions(self):
-        """actor(s), no exploration noise (td3/agent.py:57-64)."""
+        """actor(s), no exploration noise (td3/agent.py:57-64): one launch (xa_td3_act with
+        sigma 0, no counter bump) when the actor is the 3-layer .cfg MLP."""
+        fa = self._fused_act_args()
+        if fa is not None:
+            fa.states = self.envs.state.data_ptr()
+            call('xa_td3_act', ctypes.byref(fa), stream())
+            return self.step_actions
         a = self.ex_step.forward(self.envs.state)[0]
         call('xa_copy_block', a.data_ptr(), self.A, self.step_actions.data_ptr(), self.A,
              self.n_envs, self.A, stream())
         return self.step_actions
+
+    def _step_noise(self):
+        return 0.0, 0
 
     def _target_inputs(self):
         """clip(target_actor(s') + clip(0.2 N, -0.5, 0.5), -1, 1) (td3/agent.py:83-91)."""
