@@ -39,6 +39,11 @@ def make(kind, rank, data_parallel=True, gradient_steps=2):
     agent = cls(envs, actor, critic, bufs, gradient_steps=gradient_steps, seed=3, quiet=True)
     if not data_parallel:
         agent.distributed, agent.world_size = False, 1
+        # the local reference runs the same layer-executor step as the data-parallel ranks
+        # (a one-process agent would otherwise take the fused xa_td3_update / xa_td3_act,
+        # whose sums run in another order)
+        agent.__dict__['_fused'] = None
+        agent.__dict__['_fused_act'] = None
     return agent
 
 

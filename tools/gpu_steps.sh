@@ -15,6 +15,7 @@
 #   prof     rocprofv3 --kernel-trace --stats of the default bench (no CPU baseline)
 #   pmc      FETCH_SIZE / WRITE_SIZE passes per shape (tools/gpurun_pmc_shapes.sh)
 #   c3 c4 c5 acer trpo   secondary bench lines
+#   pollab   persistent-update poll sleep variants: bench + C2 FETCH_SIZE
 #   rsplit   two-wave rollout step variant: bit-exact tests on it + bench A/B
 #   ringab   small-M dX ring-depth variants vs product, K = 128 / 256 small-M timings
 #   c2g      C2 bench lines at update grids $C2_GS (XA_PPO_MAX_BLOCKS)
@@ -164,6 +165,29 @@ for step in "$@"; do
       run rs_split 200 $B --lib tools/diag_lib/libxa_rsplit.so
       run rs_base2 200 $B
       python tools/bench_brief.py gpurun_out/${T}_rs_*.out ;;
+    pollab)
+      # poll-round sleep of the persistent update (XA_POLL_SLEEP variants,
+      # tools/diag_lib/libxa_poll*.so) vs the product: bench lines (16-env + C2) and the
+      # C2 update's FETCH_SIZE per launch
+      B="python bench.py --steps 30 --warmup 5 --cpu-baseline-seconds 0 --no-secondary"
+      run poll_base 200 $B
+      for L in tools/diag_lib/libxa_poll*.so; do
+        n=$(basename $L .so); n=${n#libxa_}
+        run poll_$n 200 $B --lib $L
+      done
+      python tools/bench_brief.py gpurun_out/${T}_poll_*.out
+      for L in product tools/diag_lib/libxa_poll*.so; do
+        n=$(basename $L .so); n=${n#libxa_}
+        LIBARG=""; [ "$L" != product ] && LIBARG="--lib $R/$L"
+        (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $R/gpurun_out/${T}_pollpmc_$n \
+          -o run --output-format csv -- python $R/bench.py --n-envs 256 --no-c2 --steps 2 --warmup 1 \
+          --cpu-baseline-seconds 0 --no-graph --no-secondary $LIBARG \
+          > $R/gpurun_out/${T}_pollpmc_$n.log 2>&1) || exit 7
+        echo "== $n" >> gpurun_out/${T}_pollpmc.txt
+        python tools/pmc_summary.py ppo_update $(find gpurun_out/${T}_pollpmc_$n -name "*counter_collection.csv") \
+          >> gpurun_out/${T}_pollpmc.txt
+        find gpurun_out/${T}_pollpmc_$n -name "*counter_collection.csv" -delete
+      done ;;
     c3) run c3 300 python bench.py --config c3 --steps 30 --warmup 5 ;;
     c4) run c4 400 python bench.py --config c4 --steps 4 --warmup 1 ;;
     c5) run c5 300 python bench.py --config c5 --steps 30 --warmup 5 ;;

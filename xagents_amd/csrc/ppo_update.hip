@@ -135,6 +135,10 @@ XA_DEV double gran_f64(const f32x4v& v) {
 // granules, not behind them; read every round from every wave it would pile the whole
 // grid's polls onto one L2 channel), so a granule that lands just after a round was
 // issued is seen one round trip later.
+// (measurement knob) s_sleep units (64 cycles) between poll rounds
+#ifndef XA_POLL_SLEEP
+#define XA_POLL_SLEEP 1
+#endif
 template <int N>
 XA_DEV bool poll_gran(__amdgpu_buffer_rsrc_t r, const uint32_t (&off)[N], int n, unsigned tag,
                       f32x4v (&v)[N], unsigned* ctl, unsigned epoch, int* status) {
@@ -154,7 +158,7 @@ XA_DEV bool poll_gran(__amdgpu_buffer_rsrc_t r, const uint32_t (&off)[N], int n,
     if (ok) return true;
     if (!slow) {
 #ifndef XA_POLL_NOSLEEP
-      __builtin_amdgcn_s_sleep(1);
+      __builtin_amdgcn_s_sleep(XA_POLL_SLEEP);
 #endif
       continue;
     }
@@ -332,7 +336,7 @@ XA_DEV bool dp_poll(const void* base, const size_t (&off)[N], int n, unsigned ta
         return false;
       }
     }
-    __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_s_sleep(XA_POLL_SLEEP);
   }
 }
 
@@ -434,7 +438,7 @@ XA_DEV bool hop_wait(unsigned* ctl, int which, unsigned target, unsigned epoch, 
         ok = 0;
         break;
       }
-      __builtin_amdgcn_s_sleep(1);
+      __builtin_amdgcn_s_sleep(XA_POLL_SLEEP);
     }
     lds_flag = ok;
   }
@@ -475,7 +479,7 @@ XA_DEV int elect_local(unsigned* ctl, int G, unsigned par, int xcc, unsigned epo
             __hip_atomic_store((gu32*)status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           break;
         }
-        __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_s_sleep(XA_POLL_SLEEP);
       }
       if (win == (unsigned)xcc + 1u) id = (int)r;
     }
