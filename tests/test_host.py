@@ -344,3 +344,30 @@ def test_ctypes_structs_match_the_c_abi(tmp_path):
         assert got[(s.__name__, 'size')] == ctypes.sizeof(s), s.__name__
         for f in s._fields_:
             assert got[(s.__name__, f[0])] == getattr(s, f[0]).offset, (s.__name__, f[0])
+
+
+def test_fused_td3_entry_points_validate_sizes():
+    """xa_td3_update / xa_td3_act refuse shapes beyond their tiles with a message (checked
+    before any device call, so this runs without a GPU), and size their workspaces on the
+    host (control words, activations, head partials, tickets grow with the batch)."""
+    import ctypes
+    from xagents_amd import _lib
+    lib = _lib.load()
+    a = _lib.XaTd3ActArgs()
+    a.n, a.obs_dim, a.act_dim, a.h1, a.h2, a.ld_out = 64, 24, 5, 400, 300, 5
+    assert lib.xa_td3_act(ctypes.byref(a), None) != 0
+    assert b'act <= 4' in lib.xa_last_error()
+    a.act_dim, a.ld_out, a.h1 = 4, 4, 402
+    assert lib.xa_td3_act(ctypes.byref(a), None) != 0
+    assert b'multiples of 4' in lib.xa_last_error()
+    a.h1 = 400
+    assert lib.xa_td3_act(ctypes.byref(a), None) != 0  # no buffers
+    assert b'missing buffers' in lib.xa_last_error()
+    u = _lib.XaTd3UpdateArgs()
+    u.batch, u.obs_dim, u.act_dim, u.h1, u.h2 = 300, 24, 4, 400, 300
+    assert lib.xa_td3_update(ctypes.byref(u), None) != 0
+    assert b'batch <= 256' in lib.xa_last_error()
+    w64 = lib.xa_td3_update_workspace_bytes(64, 24, 4, 400, 300)
+    w128 = lib.xa_td3_update_workspace_bytes(128, 24, 4, 400, 300)
+    assert 0 < w64 < w128
+    assert lib.xa_td3_act_workspace_bytes(64, 24, 4, 400, 300) == w64
