@@ -254,6 +254,51 @@ __global__ void replay_step_scalars_kernel(XaReplayStepArgs a) {
   a.cursor[i] = c + 1 < a.t_rec ? c + 1 : 0;
 }
 
+// small observations (vector envs): both phases in ONE launch, one workgroup per env -- the
+// frame bytes of env i by its workgroup, then its scalars by thread 0 (the cursor is read
+// by every thread before thread 0 advances it behind the barrier)
+__global__ __launch_bounds__(256) void replay_step_small_kernel(XaReplayStepArgs a) {
+  const int i = blockIdx.x;
+  const int64_t ob = a.obs_bytes;
+  const int c = a.cursor[i];
+  const uint8_t* s_new = (const uint8_t*)a.rep_obs + ((int64_t)i * a.t_rec + c) * ob;
+  const uint8_t* s_post = (const uint8_t*)a.rep_state + ((int64_t)i * a.t_rec + c) * ob;
+  uint8_t* st = (uint8_t*)a.state + (int64_t)i * ob;
+  const int64_t slot = a.ring_states ? (int64_t)i * a.capacity + ring_slot(a, i) : 0;
+  for (int64_t e = threadIdx.x; e < ob; e += blockDim.x) {
+    const uint8_t old = st[e], nw = s_new[e], post = s_post[e];
+    if (a.ring_states) {
+      ((uint8_t*)a.ring_states)[slot * ob + e] = old;
+      ((uint8_t*)a.ring_new_states)[slot * ob + e] = nw;
+    }
+    if (a.out_states) ((uint8_t*)a.out_states)[(int64_t)i * ob + e] = old;
+    if (a.out_new_states) ((uint8_t*)a.out_new_states)[(int64_t)i * ob + e] = nw;
+    st[e] = post;
+  }
+  __syncthreads();  // (ring_slot and the cursor above were read before the scalars advance them)
+  if (threadIdx.x != 0) return;
+  const float r = a.rep_rew[(int64_t)i * a.t_rec + c];
+  const float d = a.rep_done[(int64_t)i * a.t_rec + c];
+  if (a.ring_states) {
+    const uint8_t* src = (const uint8_t*)a.actions + (int64_t)i * a.act_bytes;
+    uint8_t* dst = (uint8_t*)a.ring_actions + slot * a.act_bytes;
+    for (int64_t e = 0; e < a.act_bytes; ++e) dst[e] = src[e];
+    a.ring_rewards[slot] = r;
+    a.ring_dones[slot] = d;
+    const int64_t cnt = a.ring_count[i];
+    a.ring_count[i] = a.ring_kind == XA_RING_RB2 ? (cnt < a.capacity ? cnt + 1 : cnt) : cnt + 1;
+  }
+  const int64_t o = (int64_t)i * (a.out_ld > 0 ? a.out_ld : 1);
+  if (a.out_rewards) a.out_rewards[o] = r;
+  if (a.out_dones) a.out_dones[o] = d;
+  float ep = a.ep_return[i] + r;
+  if (a.done_epret) a.done_epret[o] = d != 0.0f ? ep : 0.0f;
+  if (d != 0.0f) ep = 0.0f;
+  a.ep_return[i] = ep;
+  a.done[i] = d;
+  a.cursor[i] = c + 1 < a.t_rec ? c + 1 : 0;
+}
+
 // dst[r][c] = src[r][c] for a rows x cols block (concat / column slices of [B, n] rows)
 __global__ __launch_bounds__(256) void copy_block_kernel(const float* __restrict__ src,
                                                          int64_t ld_src, float* __restrict__ dst,
@@ -438,6 +483,11 @@ extern "C" int xa_replay_env_step(const XaReplayStepArgs* p, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const int64_t chunk = 4096;
   dim3 grid((unsigned)((a.obs_bytes + chunk - 1) / chunk), a.n_envs);
+  if (a.obs_bytes <= 4096) {  // vector observations: one launch
+    hipLaunchKernelGGL(replay_step_small_kernel, dim3(a.n_envs), dim3(256), 0, s, a);
+    XA_CHECK_LAUNCH("xa_replay_env_step (small)");
+    return 0;
+  }
   hipLaunchKernelGGL(replay_step_frames_kernel, grid, dim3(256), 0, s, a, chunk);
   XA_CHECK_LAUNCH("xa_replay_env_step (frames)");
   hipLaunchKernelGGL(replay_step_scalars_kernel, dim3((a.n_envs + 63) / 64), dim3(64), 0, s, a);
