@@ -628,8 +628,10 @@ class OffPolicy(BaseAgent, ABC):
         self._step_args = XaReplayStepArgs()
         env.fill_step_args(self._step_args)
         n, K = self.n_envs, self._STATS_ROWS
-        self._st_done = torch.zeros(K, n, dtype=torch.float32, device=self.device)
-        self._st_epret = torch.zeros(K, n, dtype=torch.float32, device=self.device)
+        # per step: [done row | episode-return row] (one copy per step fills both)
+        self._st = torch.zeros(K, 2, n, dtype=torch.float32, device=self.device)
+        self._st_done = self._st[:, 0]
+        self._st_epret = self._st[:, 1]
         self._st_row = 0
         self._st_host = []
 
@@ -693,13 +695,11 @@ class OffPolicy(BaseAgent, ABC):
         rows = self._st_row
         if rows == 0:
             return
-        hd = torch.empty(rows, self.n_envs).pin_memory()
-        he = torch.empty(rows, self.n_envs).pin_memory()
-        hd.copy_(self._st_done[:rows], non_blocking=True)
-        he.copy_(self._st_epret[:rows], non_blocking=True)
+        h = torch.empty(rows, 2, self.n_envs).pin_memory()
+        h.copy_(self._st[:rows], non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
-        self._st_host.append((hd, he, ev))
+        self._st_host.append((h[:, 0], h[:, 1], ev))
         self._st_row = 0
         while len(self._st_host) > 1:
             self._fold_offpolicy_stats(*self._st_host.pop(0))

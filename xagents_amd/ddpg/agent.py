@@ -410,14 +410,14 @@ class DDPG(OffPolicy):
             self.steps += self.n_envs
             dones = self._host_row_dones(row)
         else:
-            if not hasattr(self, '_stage_done'):
-                f32 = dict(dtype=torch.float32, device=self.device)
-                self._stage_done = torch.zeros(self.n_envs, **f32)
-                self._stage_epret = torch.zeros(self.n_envs, **f32)
+            if not hasattr(self, '_stage'):
+                # [done row | episode-return row] written by the captured env step
+                self._stage = torch.zeros(2, self.n_envs, dtype=torch.float32,
+                                          device=self.device)
+                self._stage_done, self._stage_epret = self._stage[0], self._stage[1]
             self._run_phase('step', self._step_phase)
             r = self._st_row
-            self._st_done[r].copy_(self._stage_done)
-            self._st_epret[r].copy_(self._stage_epret)
+            self._st[r].copy_(self._stage)  # both rows in one copy
             self.replay.appended()
             self._st_row += 1
             if self._st_row == self._STATS_ROWS:
