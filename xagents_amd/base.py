@@ -691,7 +691,12 @@ class OffPolicy(BaseAgent, ABC):
         out = self._play_out[:2, 0].cpu().numpy()
         return out[:1], out[1:]
 
+    def _device_checks(self):
+        """Raise on an error a persistent launch reported through its device status word
+        (subclasses; called with every statistics flush, so no extra sync per step)."""
+
     def _flush_offpolicy_stats(self):
+        self._device_checks()
         rows = self._st_row
         if rows == 0:
             return

@@ -128,6 +128,15 @@ class DDPG(OffPolicy):
         self._noisy(a, self.step_noise_coef, float('inf'), self.step_actions)
         return self.step_actions
 
+    def _device_checks(self):
+        """A fused launch whose grid barrier timed out (its workgroups were not all resident
+        within 10 s) set the status word and left the step unfinished: fail loudly."""
+        st = self.__dict__.get('_fused_status')
+        if st is not None and int(st.item()) != 0:
+            raise RuntimeError('xa_td3_update / xa_td3_act: a grid barrier timed out (the '
+                               'persistent launch needs every workgroup resident); the '
+                               'gradient step state is invalid')
+
     def _step_noise(self):
         """(sigma, counter bump) of the exploration step: DDPG draws N(0, step_noise_coef)."""
         return self.step_noise_coef, 1
@@ -161,7 +170,9 @@ class DDPG(OffPolicy):
             self._fused_act_ws = torch.zeros(nbytes, dtype=torch.uint8, device=self.device)
             fa.workspace, fa.workspace_bytes = self._fused_act_ws.data_ptr(), nbytes
             fa.n_blocks = int(os.environ.get('XA_TD3_ACT_BLOCKS', '0'))
-            fa.status = None
+            if '_fused_status' not in self.__dict__:
+                self._fused_status = torch.zeros(1, dtype=torch.int32, device=self.device)
+            fa.status = self._fused_status.data_ptr()
         self.__dict__['_fused_act'] = fa
         return fa
 
@@ -313,7 +324,8 @@ class DDPG(OffPolicy):
                 a.g_critic2 = self.g_critic2.data_ptr()
             nbytes = _lib.load().xa_td3_update_workspace_bytes(B, S, A, H1, H2)
             self._fused_ws = torch.zeros(nbytes, dtype=torch.uint8, device=self.device)
-            self._fused_status = torch.zeros(1, dtype=torch.int32, device=self.device)
+            if '_fused_status' not in self.__dict__:
+                self._fused_status = torch.zeros(1, dtype=torch.int32, device=self.device)
             a.workspace, a.workspace_bytes = self._fused_ws.data_ptr(), nbytes
             import os
             a.n_blocks = int(os.environ.get('XA_TD3_BLOCKS', '0'))
