@@ -43,11 +43,15 @@ def _step_close(got, th0, ref, lr=1e-3, tol=2e-2):
     assert err < tol, f'update mismatch {err:.3g} (units of lr)'
 
 
-@pytest.mark.parametrize('kind', ['td3', 'ddpg'])
-def test_one_gradient_step_vs_f64(device, kind):
+@pytest.mark.parametrize('kind,n', [('td3', 4), ('ddpg', 4), ('td3', 50)])
+def test_one_gradient_step_vs_f64(device, kind, n):
+    """n = 4: batch 8 (one ragged row tile); n = 50: batch 100 -- four 32-row tiles (the last
+    ragged), two 64-row weight-gradient k blocks, three column tiles per weight-gradient job."""
     sys.path.insert(0, str(ROOT / 'oracle'))
     import nets_f64 as O
-    agent = _agent(device, kind)
+    agent = _agent(device, kind, n=n)
+    if n > 4:
+        assert agent._fused_args() is not None and agent.batch_size == 2 * n
     agent.fill_buffers()
     twin = kind == 'td3'
     nets = [agent.actor, agent.critic] + ([agent.critic2] if twin else [])
