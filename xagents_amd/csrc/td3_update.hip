@@ -1184,7 +1184,13 @@ XA_DEV unsigned shard_sum(const unsigned* cnt) {
   return t;
 }
 
-XA_DEV bool grid_sync(Sync& y, int& lds_flag, int jobs, const PreB& pb = no_preb()) {
+struct NoMid {
+  XA_DEV void operator()() const {}
+};
+// mid: work every thread does after the arrival, while thread 0 waits (the Adam step sizes)
+template <class Mid = NoMid>
+XA_DEV bool grid_sync(Sync& y, int& lds_flag, int jobs, const PreB& pb = no_preb(),
+                      const Mid& mid = Mid()) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   y.n += 1;
@@ -1204,6 +1210,7 @@ XA_DEV bool grid_sync(Sync& y, int& lds_flag, int jobs, const PreB& pb = no_preb
     dma_cr(lds().B, kCols, pb.W, pb.K, pb.c0, nullptr, pb.nc, pb.K, pad16(pb.K), pb.coh);
     if (threadIdx.x == 0) td3_bpre = 1;
   }
+  mid();
   if (threadIdx.x == 0) {
     int ok = 1;
     const uint64_t t0 = wall_clock64();
@@ -1581,13 +1588,16 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
       }
       __syncthreads();
     }
-    if (!grid_sync(y, s_flag, nt * per)) return;
+    // (the critics' Adam step sizes formed while the barrier waits)
+    auto alphas = [&]() {
+      c1.alpha = adam_alpha(p.critic1.lr, p.critic1.beta1, p.critic1.beta2, step_c1 + 1);
+      if (twin) c2.alpha = adam_alpha(p.critic2.lr, p.critic2.beta1, p.critic2.beta2, step_c2 + 1);
+    };
+    if (!grid_sync(y, s_flag, nt * per, no_preb(), alphas)) return;
   }
 
   // ---- P8: critics dW1 / db1 + Adam, Adam of the rest (+ Polyak on policy steps); the
   // rest in chunks sized so the phase's jobs fill the grid ----
-  c1.alpha = adam_alpha(p.critic1.lr, p.critic1.beta1, p.critic1.beta2, step_c1 + 1);
-  if (twin) c2.alpha = adam_alpha(p.critic2.lr, p.critic2.beta1, p.critic2.beta2, step_c2 + 1);
   int p8_jobs;
   {
     const int n_w1 = CTW1;                      // one in-feature tile (C <= 64)
@@ -1677,10 +1687,12 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
         }
         __syncthreads();
       }
-      if (!grid_sync(y, s_flag, n_dx + n_dw2 + n_dw3)) return;
+      auto alpha_ac = [&]() {
+        ac.alpha = adam_alpha(p.actor.lr, p.actor.beta1, p.actor.beta2, step_ac + 1);
+      };
+      if (!grid_sync(y, s_flag, n_dx + n_dw2 + n_dw3, no_preb(), alpha_ac)) return;
     }
     // ---- P14: actor dW1 / db1 + Adam + Polyak, Adam + Polyak of the rest ----
-    ac.alpha = adam_alpha(p.actor.lr, p.actor.beta1, p.actor.beta2, step_ac + 1);
     {
       const int rest = ac.P - ac.w2, chunk = adam_chunk(rest, max(1, G - CTW1));
       const int n_ad = (rest + chunk - 1) / chunk;
