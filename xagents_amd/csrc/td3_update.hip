@@ -1391,9 +1391,10 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
 #pragma unroll
       for (int u = 0; u < kGu; ++u) {
         int e = e0 + 256 * u;
-        if (e < nS) p.out_s[e] = v[u];
-        else if ((e -= nS) < nS) p.out_s2[e] = v[u];
-        else if ((e -= nS) < nA) p.out_a[e] = v[u];
+        // (s, s', a write-through: later phases read them back as dense rows)
+        if (e < nS) stc(p.out_s + e, v[u]);
+        else if ((e -= nS) < nS) stc(p.out_s2 + e, v[u]);
+        else if ((e -= nS) < nA) stc(p.out_a + e, v[u]);
         else if ((e -= nA) < B) p.out_r[e] = v[u];
         else if ((e -= B) < B) p.out_d[e] = v[u];
       }
@@ -1414,6 +1415,9 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
                      : id == N_TC1 ? p.target_critic1 : p.target_critic2;
     return make_net(d, actor_like ? S : C, H1, H2, actor_like ? A : 1, false);
   };
+  // the sampled batch as dense rows (the caller's copies, written through by the last block
+  // before its first barrier): what every phase after P1 stages instead of ring rows
+  const XSrc sa_dense = xcat(xsrc(p.out_s, S, S, false, true), p.out_a, A, A, false, true);
   auto in_of = [&](int id) -> XSrc {
     if (id == N_TA) return xsrc(rn, S, S, true, false);            // s'
     if (id == N_AC) return xsrc(rs, S, S, true, false);            // s
@@ -1517,7 +1521,7 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
       const int id = N_TC1 + j / per, rem = j % per, rt = rem / CT, ct = rem % CT;
       const Net n = net_of(id);
       if (layer == 1) {
-        fwd_job(xcat(xsrc(rn, S, S, true, false), ws.ta, A, A, false, true), slots,
+        fwd_job(xcat(xsrc(p.out_s2, S, S, false, true), ws.ta, A, A, false, true), slots,
                 rt * kTR, B, n.th + n.w1, n.th + n.b1, C, H1, ct * kCols, ACT_RELU, ws.h1(id));
       } else {
         const Head hd{n.th + n.w3, ws.hp3(id), ws.ticket(N_TC1, rt), 1, 1, 1, ct, nt * CT2,
@@ -1613,7 +1617,7 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
       float* grad = ci ? p.g_critic2 : p.g_critic1;
       float* tgt = pol ? (ci ? p.target_critic2.theta : p.target_critic1.theta) : nullptr;
       if (q < n_w1) {
-        dw_job(in_of(ci ? N_C2 : N_C1), slots, dz_buf(ws.dh1(ci), H1), C, H1, 0,
+        dw_job(sa_dense, slots, dz_buf(ws.dh1(ci), H1), C, H1, 0,
                q * NTW * kCols, NTW, B, grad, n.w1, n.b1, n, adam_opt(opt, tgt, p.tau));
       } else {
         const int lo = n.w2 + (q - n_w1) * chunk, hi = min(n.P, lo + chunk);
@@ -1627,7 +1631,7 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
   if (pol) {
     if (!grid_sync(y, s_flag, p8_jobs)) return;
     // ---- P9 / P10: critic 1 (updated) on [s, pi(s)] ----
-    const XSrc spa = xcat(xsrc(rs, S, S, true, false), ws.pa, A, A, false, true);
+    const XSrc spa = xcat(xsrc(p.out_s, S, S, false, true), ws.pa, A, A, false, true);
     for (int layer = 1; layer <= 2; ++layer) {
       const int CT = layer == 1 ? CT1 : CT2;
       for (int j = b; j < RTT * CT; j += G) {
@@ -1699,7 +1703,7 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
       for (int j = b; j < CTW1 + n_ad; j += G) {
         if (tid == 0) td3_dslot = (b == 0 && j == b) ? 8 * (int)y.n : -1;
         if (j < CTW1) {
-          dw_job(xsrc(rs, S, S, true, false), slots, dz_buf(ws.dh1a, H1), S, H1, 0,
+          dw_job(xsrc(p.out_s, S, S, false, true), slots, dz_buf(ws.dh1a, H1), S, H1, 0,
                  j * NTW * kCols, NTW, B, p.g_actor, ac.w1, ac.b1, ac,
                  adam_opt(p.actor, p.target_actor.theta, p.tau));
         } else {
