@@ -21,11 +21,13 @@ def _close(got, ref, rtol=1e-4):
 
 
 # shapes reaching each kernel: small 64x64, square 128x128, tall 256x64, wide 64x256, and
-# few-row many-split shapes (the batch-16/32 dense forward; ragged M / N / K splits)
+# few-row many-split shapes (the batch-16/32/64 dense forward -- the split-K forward kernel
+# for M <= 64, N % 64 == 0, K >= 8192; ragged M / N / K splits)
 _SHAPES = [(37, 50, 29, 1), (64, 512, 3000, 8), (130, 70, 1000, 4), (300, 257, 400, 1),
            (1000, 40, 333, 2), (50, 700, 290, 3), (40, 50, 20000, 16), (200, 64, 17001, 1),
            (16, 512, 37632, 256), (5, 1000, 3001, 16), (32, 36, 8000, 64), (1, 512, 9000, 64),
-           (17, 260, 5000, 32)]
+           (17, 260, 5000, 32), (64, 512, 37632, 256), (32, 512, 37632, 256),
+           (33, 448, 12345, 100)]
 
 
 @pytest.mark.parametrize('small', [False, True])

@@ -18,6 +18,7 @@
 #   pollab   persistent-update poll sleep variants: bench + C2 FETCH_SIZE
 #   rsplit   two-wave rollout step variant: bit-exact tests on it + bench A/B
 #   ringab   small-M dX ring-depth variants vs product, K = 128 / 256 small-M timings
+#   fwd      split-K dense forward: GEMM tests + timing vs the generic kernels
 #   c2g      C2 bench lines at update grids $C2_GS (XA_PPO_MAX_BLOCKS)
 #   profc3   rocprofv3 kernel trace of the C3 bench + per-(kernel, grid) summary
 #   gemm     GEMM tests, small-M timings, PMC passes on the dense dX GEMM
@@ -188,6 +189,10 @@ for step in "$@"; do
           >> gpurun_out/${T}_pollpmc.txt
         find gpurun_out/${T}_pollpmc_$n -name "*counter_collection.csv" -delete
       done ;;
+    fwd)
+      # the split-K dense forward vs the generic tile kernels; its GEMM tests
+      run_pytest fwdtest 300 tests/test_gpu_layers.py -k "plain_bias_relu or layer_executor"
+      run fwd 120 python tools/bench_fwd.py 16 32 64 ;;
     c3) run c3 300 python bench.py --config c3 --steps 30 --warmup 5 ;;
     c4) run c4 400 python bench.py --config c4 --steps 4 --warmup 1 ;;
     c5) run c5 300 python bench.py --config c5 --steps 30 --warmup 5 ;;

@@ -608,6 +608,105 @@ __global__ __launch_bounds__(512) void gemm_smallm_res_kernel(XaGemmArgs g, int 
 }
 
 // ---------------------------------------------------------------------------
+// Few-row dense forward over a huge K (the NatureCNN dense layer's forward at the acting /
+// learner batches: M <= 64, N = 512, K = 37632): split z of the S workgroups owns the k range
+// [z per, (z + 1) per) for EVERY output -- its A slice [M][per] in LDS (read once), its W
+// rows streamed from HBM straight into MFMA operand registers (lane (q, i) loads
+// W[k + q][16 ct + i] for the wave's 8 column tiles, a 4-deep register ring of k steps), the
+// whole M x N partial in the wave's accumulators; the partial goes to the split workspace and
+// the split reduce sums the S partials in split order (+ bias / activation / beta). Each W
+// byte is read once and A once per split, against the tile kernels' N / 64 re-reads of A and
+// K / 256-row splits (traffic-bound there).
+// 256 threads = 4 waves; wave w owns column tiles [w NT / 4, (w + 1) NT / 4) of every row tile.
+// ---------------------------------------------------------------------------
+constexpr int FS_RING = 4;   // k steps of W in flight per wave
+constexpr int FS_CTW = 8;    // column tiles per wave (N <= 512)
+template <int MT>
+__global__ __launch_bounds__(256) void gemm_fwd_splitk_kernel(XaGemmArgs g, int per, int stride) {
+  extern __shared__ __attribute__((aligned(16))) float As[];  // [16 MT][stride]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int i = lane & 15, q = lane >> 4;
+  const int M = g.M, N = g.N, K = g.K;
+  const int z = blockIdx.x, k0 = z * per, kn = max(0, min(K, k0 + per) - k0);
+  const int NT = N >> 4, ctw = NT >> 2, ct0 = w * ctw;  // (N % 64 == 0: whole tiles per wave)
+  const float* af = static_cast<const float*>(g.a);
+  // A slice into LDS (zeros past M and past the split's k range), float4 per thread
+  for (int e = tid; e < 16 * MT * (per >> 2); e += 256) {
+    const int r = e / (per >> 2), kk = 4 * (e - r * (per >> 2));
+    f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
+    if (r < M && kk < kn) {
+      const float* src = af + (int64_t)r * g.a_rm + k0 + kk;
+      if (kk + 4 <= kn) {
+        v = *reinterpret_cast<const f32x4*>(src);
+      } else {
+        for (int u = 0; u < 4; ++u) v[u] = kk + u < kn ? src[u] : 0.0f;
+      }
+    }
+    *reinterpret_cast<f32x4*>(As + r * stride + kk) = v;
+  }
+  // W ring: step s = rows k0 + 4 s .. + 3, this lane's row k0 + 4 s + q, its 8 columns
+  const int steps = (kn + 3) >> 2;
+  const float* bq = g.b + (int64_t)(k0 + q) * g.b_ks + 16 * ct0 + i;
+  auto load_w = [&](int st, float (&dst)[FS_CTW]) {
+    const bool ok = st < steps && 4 * st + q < kn;
+    const float* p = bq + (int64_t)(4 * st) * g.b_ks;
+#pragma unroll
+    for (int c = 0; c < FS_CTW; ++c) dst[c] = (ok && c < ctw) ? p[16 * c] : 0.0f;
+  };
+  float rb[FS_RING][FS_CTW];
+#pragma unroll
+  for (int u = 0; u < FS_RING - 1; ++u) load_w(u, rb[u]);
+  __syncthreads();
+  f32x4 acc[MT][FS_CTW];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int c = 0; c < FS_CTW; ++c) acc[mt][c] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  const float* ar = As + i * stride + q;
+  for (int s0 = 0; s0 < steps; s0 += FS_RING) {
+#pragma unroll
+    for (int u = 0; u < FS_RING; ++u) {
+      // (the slot the previous step freed takes step s + FS_RING - 1)
+      load_w(s0 + u + FS_RING - 1, rb[(u + FS_RING - 1) % FS_RING]);
+      __builtin_amdgcn_sched_barrier(0);
+      if (s0 + u < steps) {
+        float av[MT];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) av[mt] = ar[mt * 16 * stride + 4 * (s0 + u)];
+#pragma unroll
+        for (int c = 0; c < FS_CTW; ++c)
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt)
+            if (c < ctw) acc[mt][c] = mfma4(av[mt], rb[u][c], acc[mt][c]);
+      }
+    }
+  }
+  // the partial: lane holds D[4 (lane >> 4) + r][lane & 15] of each tile
+  float* part = g.partials + (int64_t)z * M * N;
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int c = 0; c < FS_CTW; ++c) {
+      if (c >= ctw) continue;
+      const int n = 16 * (ct0 + c) + i;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = 16 * mt + 4 * q + r;
+        if (m < M) part[(int64_t)m * N + n] = acc[mt][c][r];
+      }
+    }
+}
+
+// the split-K forward path's contract (and its per-split k range, a multiple of 4)
+bool fwd_splitk_ok(const XaGemmArgs& g) {
+  return !g.force_small && g.a != nullptr && !g.a_u8 && g.a_pm == 1 && g.a_pk == 1 &&
+         g.a_rk == 1 && g.a_rm % 4 == 0 && ((uintptr_t)g.a & 15) == 0 && g.b_ns == 1 &&
+         g.M <= 64 && g.N % 64 == 0 && g.N <= 64 * FS_CTW && g.K >= 8192 && !g.gate &&
+         g.splits > 1 && g.partials != nullptr;
+}
+int fwd_splitk_per(const XaGemmArgs& g) { return ((g.K + g.splits - 1) / g.splits + 3) & ~3; }
+
+// ---------------------------------------------------------------------------
 // Skinny path (weight gradients of the convs: M, N <= 256 / 64, K = rows x positions in
 // the millions): one wave per workgroup owns a 32 x 32 output tile and a K range; the
 // operands come straight from global memory (A rows / B rows are contiguous along m / n
@@ -1129,6 +1228,29 @@ extern "C" int xa_gemm(const XaGemmArgs* p, void* stream) {
     else if (mt <= 2) launch_res<2>(g, ch, gate, G, rounds, s);
     else launch_res<4>(g, ch, gate, G, rounds, s);
     XA_CHECK_LAUNCH("xa_gemm (small M, resident A)");
+    return 0;
+  }
+  if (fwd_splitk_ok(g) && fwd_splitk_per(g) <= 512) {
+    const int per = fwd_splitk_per(g), stride = per % 8 == 0 ? per + 4 : per;
+    const int mt = (g.M + 15) / 16;
+    const size_t lds = sizeof(float) * (size_t)16 * (mt <= 1 ? 1 : mt <= 2 ? 2 : 4) * stride;
+    if (mt <= 1)
+      hipLaunchKernelGGL(gemm_fwd_splitk_kernel<1>, dim3(g.splits), dim3(256), lds, s, g, per, stride);
+    else if (mt <= 2)
+      hipLaunchKernelGGL(gemm_fwd_splitk_kernel<2>, dim3(g.splits), dim3(256), lds, s, g, per, stride);
+    else
+      hipLaunchKernelGGL(gemm_fwd_splitk_kernel<4>, dim3(g.splits), dim3(256), lds, s, g, per, stride);
+    XA_CHECK_LAUNCH("xa_gemm (split-K forward)");
+    const int64_t total = (int64_t)g.M * g.N;
+    if (total <= 65536 && g.splits >= 64) {
+      hipLaunchKernelGGL(gemm_split_reduce_wide_kernel, dim3((int)((total + 63) / 64)),
+                         dim3(1024), 0, s, g, g.splits);
+    } else {
+      const int64_t want = (total + 255) / 256;
+      const int blocks = (int)(want < 4096 ? want : 4096);
+      hipLaunchKernelGGL(gemm_split_reduce_kernel, dim3(blocks), dim3(256), 0, s, g, g.splits);
+    }
+    XA_CHECK_LAUNCH("xa_gemm (split reduce)");
     return 0;
   }
   dim3 grid((g.M + BM - 1) / BM, (g.N + BN - 1) / BN, g.splits);
