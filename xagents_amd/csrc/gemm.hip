@@ -612,14 +612,18 @@ __global__ __launch_bounds__(512) void gemm_smallm_res_kernel(XaGemmArgs g, int 
 // learner batches: M <= 64, N = 512, K = 37632): split z of the S workgroups owns the k range
 // [z per, (z + 1) per) for EVERY output -- its A slice [M][per] in LDS (read once), its W
 // rows streamed from HBM straight into MFMA operand registers (lane (q, i) loads
-// W[k + q][16 ct + i] for the wave's 8 column tiles, a 4-deep register ring of k steps), the
+// W[k + q][16 ct + i] for the wave's 8 column tiles, an 8-deep register ring of k steps), the
 // whole M x N partial in the wave's accumulators; the partial goes to the split workspace and
 // the split reduce sums the S partials in split order (+ bias / activation / beta). Each W
 // byte is read once and A once per split, against the tile kernels' N / 64 re-reads of A and
 // K / 256-row splits (traffic-bound there).
 // 256 threads = 4 waves; wave w owns column tiles [w NT / 4, (w + 1) NT / 4) of every row tile.
 // ---------------------------------------------------------------------------
-constexpr int FS_RING = 4;   // k steps of W in flight per wave
+#ifndef XA_FS_RING
+#define XA_FS_RING 8
+#endif
+constexpr int FS_RING = XA_FS_RING;  // k steps of W in the register ring per wave (7 in flight:
+                                     // ~56 KB per CU, the W stream's latency x rate)
 constexpr int FS_CTW = 8;    // column tiles per wave (N <= 512)
 template <int MT>
 __global__ __launch_bounds__(256) void gemm_fwd_splitk_kernel(XaGemmArgs g, int per, int stride) {
