@@ -16,7 +16,10 @@ def main():
     from xagents_amd import _lib
     from xagents_amd._lib import XA_ACT_RELU
     from xagents_amd.layers import gemm
-    lib = _lib.load()
+    import os
+    # XA_LIB: a variant build (tools/build_variant.py) instead of the product
+    lib = _lib.load(os.environ['XA_LIB']) if os.environ.get('XA_LIB') else _lib.load()
+    _lib._lib = lib
     dev = torch.device('cuda')
     N, K = 512, 37632
     for M in [int(a) for a in sys.argv[1:]] or [16, 32, 64]:

@@ -192,7 +192,11 @@ for step in "$@"; do
     fwd)
       # the split-K dense forward vs the generic tile kernels; its GEMM tests
       run_pytest fwdtest 300 tests/test_gpu_layers.py -k "plain_bias_relu or layer_executor"
-      run fwd 120 python tools/bench_fwd.py 16 32 64 ;;
+      run fwd 120 python tools/bench_fwd.py 16 32 64
+      for L in tools/diag_lib/libxa_fsring*.so; do
+        n=$(basename $L .so); n=${n#libxa_}
+        XA_LIB=$L run fwd_$n 120 python tools/bench_fwd.py 32 64
+      done ;;
     c3) run c3 300 python bench.py --config c3 --steps 30 --warmup 5 ;;
     c4) run c4 400 python bench.py --config c4 --steps 4 --warmup 1 ;;
     c5) run c5 300 python bench.py --config c5 --steps 30 --warmup 5 ;;
