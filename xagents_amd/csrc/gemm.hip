@@ -608,8 +608,8 @@ __global__ __launch_bounds__(512) void gemm_smallm_res_kernel(XaGemmArgs g, int 
 }
 
 // ---------------------------------------------------------------------------
-// Few-row dense forward over a huge K (the NatureCNN dense layer's forward at the acting /
-// learner batches: M <= 64, N = 512, K = 37632): split z of the S workgroups owns the k range
+// Few-row dense forward over a huge K (the NatureCNN dense layer's forward at the acting
+// batch: 17 <= M <= 32, N = 512, K = 37632; see fwd_splitk_ok): split z of the S workgroups owns the k range
 // [z per, (z + 1) per) for EVERY output -- its A slice [M][per] in LDS (read once), its W
 // rows streamed from HBM straight into MFMA operand registers (lane (q, i) loads
 // W[k + q][16 ct + i] for the wave's 8 column tiles, an 8-deep register ring of k steps), the
@@ -701,11 +701,17 @@ __global__ __launch_bounds__(256) void gemm_fwd_splitk_kernel(XaGemmArgs g, int 
     }
 }
 
-// the split-K forward path's contract (and its per-split k range, a multiple of 4)
+// the split-K forward path's contract (and its per-split k range, a multiple of 4). Measured
+// (profiles/r04v_fwd_splitk_ab.txt, 256 splits, N 512, K 37632): M = 32 34.0 us vs 37.7 us on
+// the tile kernels; M = 64 48.7 vs 40.5 us -- the 256 whole-width partials (M N 4 B each,
+// written and read back by the split reduce) cost more than the A re-reads they save -- and
+// M = 16 98.6 vs 35.1 us (the one-row-tile form); ring depth 4 / 8 / 12 within noise. So
+// 17 <= M <= 32 only.
 bool fwd_splitk_ok(const XaGemmArgs& g) {
   return !g.force_small && g.a != nullptr && !g.a_u8 && g.a_pm == 1 && g.a_pk == 1 &&
          g.a_rk == 1 && g.a_rm % 4 == 0 && ((uintptr_t)g.a & 15) == 0 && g.b_ns == 1 &&
-         g.M <= 64 && g.N % 64 == 0 && g.N <= 64 * FS_CTW && g.K >= 8192 && !g.gate &&
+         g.M > 16 && g.M <= 32 && g.N % 64 == 0 && g.N <= 64 * FS_CTW && g.K >= 8192 &&
+         !g.gate &&
          g.splits > 1 && g.partials != nullptr;
 }
 int fwd_splitk_per(const XaGemmArgs& g) { return ((g.K + g.splits - 1) / g.splits + 3) & ~3; }
