@@ -194,6 +194,7 @@ for step in "$@"; do
       run_pytest fwdtest 300 tests/test_gpu_layers.py -k "plain_bias_relu or layer_executor"
       run fwd 120 python tools/bench_fwd.py 16 32 64
       for L in tools/diag_lib/libxa_fsring*.so; do
+        [ -e "$L" ] || continue
         n=$(basename $L .so); n=${n#libxa_}
         XA_LIB=$L run fwd_$n 120 python tools/bench_fwd.py 32 64
       done ;;
