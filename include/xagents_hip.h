@@ -511,6 +511,23 @@ int xa_ring_scatter(const void* src, void* ring, const int64_t* slots, int n_ite
 int xa_ring_gather(const void* ring, void* dst, const int64_t* slots, int n_items,
                    int64_t item_bytes, void* stream);
 
+/* Every field of one sampled batch in one launch: dst_f[i] = ring_f[slots[i]] for the
+ * n_fields (<= XA_GATHER_MAX_FIELDS) rings of concat_buffer_samples' [states, actions,
+ * rewards, dones, new_states] (xagents/base.py:344-368), one slot list for all of them. */
+#define XA_GATHER_MAX_FIELDS 8
+typedef struct XaGatherField {
+  const void* ring;
+  void* dst;
+  int64_t item_bytes;
+} XaGatherField;
+typedef struct XaGatherArgs {
+  XaGatherField field[XA_GATHER_MAX_FIELDS];
+  int n_fields;
+  int n_items;
+  const int64_t* slots;
+} XaGatherArgs;
+int xa_ring_gather_fields(const XaGatherArgs* args, void* stream);
+
 /* dst = (1 - tau) dst + tau src (DDPG.sync_target_models, xagents/ddpg/agent.py:73-85);
  * tau = 1 copies (DQN.sync_target_model, dqn/agent.py:97-105). */
 int xa_polyak(const float* src, float* dst, int64_t n, float tau, void* stream);

@@ -9,6 +9,7 @@ import numpy as np
 import oracle
 import pytest
 
+from xagents_amd._lib import XA_RING_DEQUE
 from xagents_amd.utils.buffers import BaseBuffer, ReplayBuffer1, ReplayBuffer2
 from xagents_amd.utils.common import create_buffers
 
@@ -264,6 +265,38 @@ def test_rb2_batched_randint_matches_per_buffer_calls():
         np.random.seed(11)
         got = np.random.randint(0, size, n * k)
         np.testing.assert_array_equal(ref, got)
+
+
+def test_rb1_fast_sampler_matches_random_sample():
+    """DeviceReplay's RB1 draw (replay._sample_ranges through getrandbits) returns exactly the
+    reference's per-buffer random.sample(range(length), k) results (buffers.py:96-104) and
+    leaves the module RNG in the same state, across the pool (n <= 21) and set branches."""
+    from xagents_amd.replay import DeviceReplay, _fast_sampler
+    fast = _fast_sampler()
+    assert fast is not None
+    cases = [[0], [2, 3, 21, 22], [5, 30, 100], [31250] * 32, [1, 2, 3, 4, 1000],
+             list(range(6, 60, 7))]
+    for lengths in cases:
+        for k in (0, 1, 2, 3, 6, 10):
+            if k > min(lengths):
+                continue
+            random.seed(sum(lengths) + k)
+            ref = [q for n in lengths for q in random.sample(range(n), k)]
+            after_ref = random.random()
+            random.seed(sum(lengths) + k)
+            got = fast(lengths, k)
+            assert got == ref and random.random() == after_ref, (lengths, k)
+    # the ring slots of a full and a wrapped deque (start + pos) % size, env-major
+    rep = DeviceReplay.__new__(DeviceReplay)
+    rep.kind, rep.n, rep.cap, rep.k = XA_RING_DEQUE, 3, 50, 2
+    rep.host_count = np.array([7, 50, 133], np.int64)
+    random.seed(5)
+    want = []
+    for i, cnt in enumerate(rep.host_count.tolist()):
+        length = min(cnt, 50)
+        want += [i * 50 + (cnt - length + p) % 50 for p in random.sample(range(length), 2)]
+    random.seed(5)
+    np.testing.assert_array_equal(rep.sample_slots(), want)
 
 
 # ---- LazyFrames and the per-env states view (xagents/utils/common.py:23-64) --------------

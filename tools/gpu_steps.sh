@@ -114,7 +114,9 @@ for step in "$@"; do
         -o run --output-format csv -- python $R/bench.py --config c3 --steps 30 --warmup 5 \
         --cpu-baseline-seconds 0 > $R/gpurun_out/${T}_profc3_bench.json 2>&1) || exit $?
       python tools/kernel_shapes.py gpurun_out/${T}_profc3/run_kernel_trace.csv 25 \
-        > gpurun_out/${T}_profc3_shapes.txt 2>&1 ;;
+        > gpurun_out/${T}_profc3_shapes.txt 2>&1
+      python tools/step_timeline.py gpurun_out/${T}_profc3/run_kernel_trace.csv \
+        > gpurun_out/${T}_profc3_timeline.txt 2>&1 ;;
     profc5)
       # C5 (TD3): the whole bench line, then one gradient step's launches on their own
       (cd /tmp && timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/${T}_profc5 \
@@ -157,6 +159,17 @@ for step in "$@"; do
       done
       XA_SMALLM_K=128 run smallk128 120 python tools/bench_smallm.py 16 64 128
       XA_SMALLM_K=256 run smallk256 120 python tools/bench_smallm.py 16 64 128 ;;
+    sdiag)
+      # small-M dense dX: no-MFMA / no-HBM-stream diagnostic variants (XA_SMALLM_DIAG 1 / 2)
+      run sdiag_base 120 python tools/bench_smallm.py 4 16 64
+      for v in 1 2; do
+        XA_LIB=tools/diag_lib/libxa_sdiag$v.so run sdiag_$v 120 python tools/bench_smallm.py 4 16 64
+      done ;;
+    smallm)
+      run_pytest smallmtest 300 tests/test_gpu_layers.py -k "small_m or dense_input or layer_executor"
+      run smallm 120 python tools/bench_smallm.py 16 64 128 336 ;;
+    c3host) run c3host 300 python tools/c3_host_profile.py ;;
+    sstamps) XA_LIB=tools/diag_lib/libxa_sdiag3.so run sstamps 120 python tools/smallm_stamps.py 64 16 ;;
     rsplit)
       # the two-wave rollout step (XA_ROLL_SPLIT=1 variant, tools/diag_lib/libxa_rsplit.so):
       # bit-exact vs the oracle (the rollout tests on the variant), then bench A/B

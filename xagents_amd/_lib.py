@@ -236,6 +236,18 @@ class XaTrpoHeadArgs(Structure):
     ]
 
 
+XA_GATHER_MAX_FIELDS = 8
+
+
+class XaGatherField(Structure):
+    _fields_ = [('ring', c_void_p), ('dst', c_void_p), ('item_bytes', c_int64)]
+
+
+class XaGatherArgs(Structure):
+    _fields_ = [('field', XaGatherField * XA_GATHER_MAX_FIELDS), ('n_fields', c_int),
+                ('n_items', c_int), ('slots', c_void_p)]
+
+
 class XaReplayStepArgs(Structure):
     _fields_ = [
         ('n_envs', c_int), ('t_rec', c_int),
@@ -419,6 +431,7 @@ _SIGNATURES = {
     ),
     'xa_ring_scatter': (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int64, c_void_p]),
     'xa_ring_gather': (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int64, c_void_p]),
+    'xa_ring_gather_fields': (c_int, [c_void_p, c_void_p]),
     'xa_polyak': (c_int, [c_void_p, c_void_p, c_int64, c_float, c_void_p]),
     'xa_adam_step_bump': (c_int, [c_void_p, c_void_p]),
     'xa_replay_env_step': (c_int, [POINTER(XaReplayStepArgs), c_void_p]),

@@ -472,6 +472,12 @@ __global__ __launch_bounds__(256) void gemm_tile_kernel(XaGemmK kargs) {
 constexpr int RS_KP = 4, RS_UPR = 2;
 // rounds the B ring spans (the round loop is unrolled by this): 2 keeps 2 CH - 1 chunks of B
 // in flight per wave
+// XA_SMALLM_DIAG (diagnostic builds only): 1 = VALU FMAs instead of the MFMAs, 2 = every
+// round streams round 0's B rows again (cache hits, no HBM stream), 3 = shader-clock stamps
+// per wave and round into the split workspace (tools/smallm_stamps.py)
+#ifndef XA_SMALLM_DIAG
+#define XA_SMALLM_DIAG 0
+#endif
 #ifndef XA_SMALLM_RING
 #define XA_SMALLM_RING 2
 #endif
@@ -500,15 +506,37 @@ __global__ __launch_bounds__(512) void gemm_smallm_res_kernel(XaGemmArgs g, int 
   const int M = g.M, N = g.N;
   const int units = (N + 15) / 16;
   const float* af = static_cast<const float*>(g.a);
-  for (int sl = tid; sl < MT * 16 * (K / 4); sl += 512) {
+#if XA_SMALLM_DIAG == 3
+  // diagnostic: lane 0 of every wave stamps the shader clock into the split workspace (u64
+  // slot (block 8 + wave) 16 + i: 0 start, 1 after the A prologue, 2 + 2 r / 3 + 2 r round r's
+  // chunk loop done / round done)
+  auto stamp = [&](int i) {
+    if (lane == 0 && g.partials)
+      ((__attribute__((address_space(1))) unsigned long long*)g.partials)[(blockIdx.x * 8 + w) * 16 + i] =
+          __builtin_amdgcn_s_memtime();
+  };
+#else
+  auto stamp = [](int) {};
+#endif
+  stamp(0);
+  // A into LDS: every thread's PER float4 loads issued before the B ring's first loads and
+  // before any LDS write (a load -> wait -> write loop serialised PER round trips: 17.5k
+  // cycles of prologue at M = 64, profiles/r04y_smallm_stamps.txt)
+  constexpr int PER = MT * 16 * (K / 4) / 512;
+  static_assert(PER * 512 == MT * 16 * (K / 4), "A slots per thread");
+  f32x4 va[PER];
+  int va_at[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
     // 32 consecutive threads: 8 blocks b x the 4 quads q, b fastest -- 512 contiguous bytes
     // of the global row, and every 8-lane group of the ds_write_b128 one 128-B run of a
     // sub-row
+    const int sl = tid + 512 * i;
     const int m = sl / (K / 4), rem = sl - m * (K / 4);
     const int q = (rem >> 3) & 3, b = ((rem >> 5) << 3) + (rem & 7);
-    const f32x4 z = {0.0f, 0.0f, 0.0f, 0.0f};
-    *reinterpret_cast<f32x4*>(As + m * PA + q * SR + 4 * b) =
-        m < M ? *reinterpret_cast<const f32x4*>(af + (int64_t)m * g.a_rm + 16 * b + 4 * q) : z;
+    va_at[i] = m * PA + q * SR + 4 * b;
+    va[i] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    if (m < M) va[i] = *reinterpret_cast<const f32x4*>(af + (int64_t)m * g.a_rm + 16 * b + 4 * q);
   }
   auto unit_of = [&](int r) { return (r * (int)gridDim.x + (int)blockIdx.x) * RS_UPR + us; };
   auto brow = [&](int r) {
@@ -520,13 +548,20 @@ __global__ __launch_bounds__(512) void gemm_smallm_res_kernel(XaGemmArgs g, int 
   constexpr int RS_R = RS_NR * CH;
   f32x4 rb[RS_R][2];
   auto load_b = [&](int gi, f32x4 (&dst)[2]) {
+#if XA_SMALLM_DIAG == 2
+    const float* p = brow(0) + 32 * (gi % CH);  // diagnostic: every round re-reads round 0 (L2 hits)
+#else
     const float* p = brow(gi / CH) + 32 * (gi % CH);
+#endif
     dst[0] = *reinterpret_cast<const f32x4*>(p);
     dst[1] = *reinterpret_cast<const f32x4*>(p + 16);
   };
 #pragma unroll
   for (int gi = 0; gi < RS_R - 1; ++gi) load_b(gi, rb[gi]);
+#pragma unroll
+  for (int i = 0; i < PER; ++i) *reinterpret_cast<f32x4*>(As + va_at[i]) = va[i];
   __syncthreads();
+  stamp(1);
   const float* as = As + li * PA + lq * SR + kp * (KQ / 4);  // k = kp KQ + 16 b' + 4 lq + j
   const int mt_fin = min(kp, MT - 1);  // the m tile this wave finishes (kp < MT)
   for (int r0 = 0; r0 < rounds; r0 += RS_NR) {
@@ -566,18 +601,22 @@ __global__ __launch_bounds__(512) void gemm_smallm_res_kernel(XaGemmArgs g, int 
             for (int j = 0; j < 4; ++j)
 #pragma unroll
               for (int mt = 0; mt < MT; ++mt)
+#if XA_SMALLM_DIAG == 1
+                acc[mt][j] = fmaf(aq[mt][j], rb[u][h][j], acc[mt][j]);  // diagnostic: no MFMA
+#else
                 acc[mt] = mfma4(aq[mt][j], rb[u][h][j], acc[mt]);
+#endif
           }
         }
       }
+      if (r < 7) stamp(2 + 2 * r);
       // slot of part p in m tile mt's scratch: p, or p - 1 past the finishing wave mt
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
         if (mt == kp) continue;
         const int slot = kp < mt ? kp : kp - 1;
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          red[((us * MT + mt) * (RS_KP - 1) + slot) * 256 + q * 64 + lane] = acc[mt][q];
+        *reinterpret_cast<f32x4*>(red + ((us * MT + mt) * (RS_KP - 1) + slot) * 256 + 4 * lane) =
+            acc[mt];
       }
       __syncthreads();
       if (kp < MT && live && n < N) {
@@ -585,14 +624,15 @@ __global__ __launch_bounds__(512) void gemm_smallm_res_kernel(XaGemmArgs g, int 
 #pragma unroll
         for (int mt = 1; mt < MT; ++mt)
           if (mt == kp) own = acc[mt];
+        f32x4 part[RS_KP - 1];
+#pragma unroll
+        for (int p = 0; p < RS_KP - 1; ++p)
+          part[p] = *reinterpret_cast<const f32x4*>(red + ((us * MT + kp) * (RS_KP - 1) + p) * 256 + 4 * lane);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           float v = 0.0f;
 #pragma unroll
-          for (int p = 0; p < RS_KP; ++p)
-            v += p == kp ? own[q]
-                         : red[((us * MT + kp) * (RS_KP - 1) + (p < kp ? p : p - 1)) * 256 +
-                               q * 64 + lane];
+          for (int p = 0; p < RS_KP; ++p) v += p == kp ? own[q] : part[p < kp ? p : p - 1][q];
           const int m = 16 * kp + 4 * lq + q;
           if (m < M) {
             v = epilogue(v, n, g);
@@ -603,6 +643,7 @@ __global__ __launch_bounds__(512) void gemm_smallm_res_kernel(XaGemmArgs g, int 
         }
       }
       __syncthreads();
+      if (r < 7) stamp(3 + 2 * r);
     }
   }
 }

@@ -146,6 +146,24 @@ __global__ __launch_bounds__(256) void ring_gather_kernel(const uint8_t* __restr
   }
 }
 
+// every field of a sampled batch in one launch: blockIdx.z = field (wave-uniform), the
+// field's bytes spread over blockIdx.x as ring_gather_kernel does
+__global__ __launch_bounds__(256) void ring_gather_fields_kernel(XaGatherArgs a) {
+  const int i = blockIdx.y, f = blockIdx.z;
+  if (i >= a.n_items || f >= a.n_fields) return;
+  const int64_t nb = a.field[f].item_bytes;
+  const uint8_t* s = static_cast<const uint8_t*>(a.field[f].ring) + a.slots[i] * nb;
+  uint8_t* d = static_cast<uint8_t*>(a.field[f].dst) + (int64_t)i * nb;
+  if ((nb & 15) == 0 && ((uintptr_t)s & 15) == 0 && ((uintptr_t)d & 15) == 0) {
+    const int64_t n16 = nb >> 4;
+    for (int64_t e = blockIdx.x * 256ll + threadIdx.x; e < n16; e += (int64_t)gridDim.x * 256)
+      reinterpret_cast<uint4*>(d)[e] = reinterpret_cast<const uint4*>(s)[e];
+  } else {
+    for (int64_t e = blockIdx.x * 256ll + threadIdx.x; e < nb; e += (int64_t)gridDim.x * 256)
+      d[e] = s[e];
+  }
+}
+
 // y = (1 - tau) y + tau x (DDPG.sync_target_models, ddpg/agent.py:73-85); tau = 1: copy
 __global__ __launch_bounds__(256) void polyak_kernel(const float* __restrict__ x,
                                                      float* __restrict__ y, int64_t n,
@@ -443,6 +461,25 @@ extern "C" int xa_ring_gather(const void* ring, void* dst, const int64_t* slots,
   hipLaunchKernelGGL(ring_gather_kernel, dim3(gx, n_items), dim3(256), 0, (hipStream_t)stream,
                      (const uint8_t*)ring, (uint8_t*)dst, slots, n_items, item_bytes);
   XA_CHECK_LAUNCH("xa_ring_gather");
+  return 0;
+}
+
+extern "C" int xa_ring_gather_fields(const XaGatherArgs* p, void* stream) {
+  XA_CHECK_ARG(p != nullptr, "xa_ring_gather_fields: null args");
+  const XaGatherArgs& a = *p;
+  XA_CHECK_ARG(a.n_fields > 0 && a.n_fields <= XA_GATHER_MAX_FIELDS && a.n_items > 0 && a.slots,
+               "xa_ring_gather_fields: need 1..%d fields, n_items > 0 and slots",
+               XA_GATHER_MAX_FIELDS);
+  int gx = 1;
+  for (int f = 0; f < a.n_fields; ++f) {
+    XA_CHECK_ARG(a.field[f].ring && a.field[f].dst && a.field[f].item_bytes > 0,
+                 "xa_ring_gather_fields: field %d: null ring / dst or item_bytes <= 0", f);
+    const int g = ring_grid_x(a.field[f].item_bytes);
+    gx = g > gx ? g : gx;
+  }
+  hipLaunchKernelGGL(ring_gather_fields_kernel, dim3(gx, a.n_items, a.n_fields), dim3(256), 0,
+                     (hipStream_t)stream, a);
+  XA_CHECK_LAUNCH("xa_ring_gather_fields");
   return 0;
 }
 

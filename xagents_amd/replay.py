@@ -16,13 +16,85 @@ same RNG streams in the same order:
   `np.random.randint(0, min(current_size, size), k)`.
 The per-env buffer objects passed in keep their `current_size` attribute in step.
 """
+import ctypes
+import math
 import random
 
 import numpy as np
 import torch
 
-from xagents_amd._lib import XA_RING_DEQUE, XA_RING_RB2, call, stream
+from xagents_amd._lib import XA_RING_DEQUE, XA_RING_RB2, XaGatherArgs, call, stream
 from xagents_amd.utils.buffers import ReplayBuffer1, ReplayBuffer2
+
+
+def _sample_range(n, k, getrandbits):
+    """random.sample(range(n), k) on the module RNG, drawn through getrandbits directly: the
+    same algorithm, the same draws and the same results as CPython's Random.sample with
+    _randbelow_with_getrandbits (Lib/random.py, 3.8-3.12: a pool of n items when n is at
+    most the small-set size, else rejection against the selected set), minus the per-call
+    overhead (C3's 32 per-env samples took ~100 us of host time per train step through
+    random.sample; tests/test_host.py checks the identity and the RNG state after)."""
+    if not 0 <= k <= n:
+        raise ValueError('Sample larger than population or is negative')
+    setsize = 21
+    if k > 5:
+        setsize += 4 ** math.ceil(math.log(k * 3, 4))
+    out = []
+    if n <= setsize:
+        pool = list(range(n))
+        for i in range(k):
+            m = n - i
+            b = m.bit_length()
+            r = getrandbits(b)
+            while r >= m:
+                r = getrandbits(b)
+            out.append(pool[r])
+            pool[r] = pool[m - 1]
+    else:
+        b = n.bit_length()
+        sel = set()
+        for _ in range(k):
+            r = getrandbits(b)
+            while r >= n or r in sel:
+                r = getrandbits(b)
+            sel.add(r)
+            out.append(r)
+    return out
+
+
+def _sample_ranges(lengths, k, getrandbits):
+    """[random.sample(range(n), k) for n in lengths], flattened, as _sample_range draws them;
+    the k = 2 set case (C3's per-env batch of 2) inline."""
+    out = []
+    if k == 2:
+        for n in lengths:
+            if n <= 21:
+                out.extend(_sample_range(n, 2, getrandbits))
+                continue
+            b = n.bit_length()
+            r0 = getrandbits(b)
+            while r0 >= n:
+                r0 = getrandbits(b)
+            r1 = getrandbits(b)
+            while r1 >= n or r1 == r0:
+                r1 = getrandbits(b)
+            out.append(r0)
+            out.append(r1)
+        return out
+    for n in lengths:
+        out.extend(_sample_range(n, k, getrandbits))
+    return out
+
+
+def _fast_sampler():
+    """_sample_ranges bound to the module RNG when that RNG draws through getrandbits (the
+    stock random.Random); None otherwise (callers then use random.sample)."""
+    inst = random._inst
+    rb = getattr(type(inst), '_randbelow', None)
+    if rb is not getattr(random.Random, '_randbelow_with_getrandbits', object()):
+        return None
+    gb = inst.getrandbits
+    return lambda lengths, k: _sample_ranges(lengths, k, gb)
 
 
 class DeviceReplay:
@@ -92,14 +164,20 @@ class DeviceReplay:
             size = min(int(self.host_count[0]), self.cap)
             idx = np.random.randint(0, size, self.n * self.k).astype(np.int64)
             return np.repeat(np.arange(self.n, dtype=np.int64) * self.cap, self.k) + idx
+        if self.kind != XA_RING_RB2:
+            cnt = self.host_count
+            length = np.minimum(cnt, self.cap)
+            fast = _fast_sampler()
+            if fast:
+                pos = np.asarray(fast(length.tolist(), self.k), np.int64)
+            else:
+                pos = np.asarray([q for n in length.tolist()
+                                  for q in random.sample(range(n), self.k)], np.int64)
+            idx = (np.repeat(cnt - length, self.k) + pos) % self.cap
+            return np.repeat(np.arange(self.n, dtype=np.int64) * self.cap, self.k) + idx
         for i in range(self.n):
             cnt = int(self.host_count[i])
-            if self.kind == XA_RING_RB2:
-                idx = np.random.randint(0, min(cnt, self.cap), self.k)
-            else:
-                length = min(cnt, self.cap)
-                pos = np.asarray(random.sample(range(length), self.k), np.int64)
-                idx = ((cnt - length) + pos) % self.cap
+            idx = np.random.randint(0, min(cnt, self.cap), self.k)
             out[i * self.k:(i + 1) * self.k] = i * self.cap + idx
         return out
 
@@ -116,10 +194,19 @@ class DeviceReplay:
         return self.slots
 
     def gather(self, slots, states, actions, rewards, dones, new_states):
-        m = slots.numel()
-        sp = slots.data_ptr()
-        for ring, dst, nb in ((self.states, states, self.obs_bytes),
-                              (self.new_states, new_states, self.obs_bytes),
-                              (self.actions, actions, self.act_bytes),
-                              (self.rewards, rewards, 4), (self.dones, dones, 4)):
-            call('xa_ring_gather', ring.data_ptr(), dst.data_ptr(), sp, m, nb, stream())
+        """The five fields of one sampled batch in one xa_ring_gather_fields launch (the
+        argument block is built once per destination set and reused)."""
+        key = (slots.data_ptr(), slots.numel(), states.data_ptr(), actions.data_ptr(),
+               rewards.data_ptr(), dones.data_ptr(), new_states.data_ptr())
+        if getattr(self, '_gkey', None) != key:
+            a = XaGatherArgs()
+            fields = ((self.states, states, self.obs_bytes),
+                      (self.new_states, new_states, self.obs_bytes),
+                      (self.actions, actions, self.act_bytes),
+                      (self.rewards, rewards, 4), (self.dones, dones, 4))
+            for f, (ring, dst, nb) in enumerate(fields):
+                a.field[f].ring, a.field[f].dst, a.field[f].item_bytes = \
+                    ring.data_ptr(), dst.data_ptr(), nb
+            a.n_fields, a.n_items, a.slots = len(fields), slots.numel(), slots.data_ptr()
+            self._gargs, self._gkey = a, key
+        call('xa_ring_gather_fields', ctypes.byref(self._gargs), stream())
