@@ -27,7 +27,9 @@ _SHAPES = [(37, 50, 29, 1), (64, 512, 3000, 8), (130, 70, 1000, 4), (300, 257, 4
            (1000, 40, 333, 2), (50, 700, 290, 3), (40, 50, 20000, 16), (200, 64, 17001, 1),
            (16, 512, 37632, 256), (5, 1000, 3001, 16), (32, 36, 8000, 64), (1, 512, 9000, 64),
            (17, 260, 5000, 32), (64, 512, 37632, 256), (32, 512, 37632, 256),
-           (33, 448, 12345, 100)]
+           (33, 448, 12345, 100),
+           # few-column heads (row-dot path: N <= 8, K <= 4096)
+           (64, 6, 512, 2), (128, 1, 512, 1), (3, 8, 4096, 4), (1000, 5, 77, 1)]
 
 
 @pytest.mark.parametrize('small', [False, True])

@@ -649,6 +649,49 @@ __global__ __launch_bounds__(512) void gemm_smallm_res_kernel(XaGemmArgs g, int 
 }
 
 // ---------------------------------------------------------------------------
+// Few-column dense layer (the network heads: N <= 8 Q values / logits / values over K <= 4096
+// hidden units): one wave per output row m, lane l accumulates k = l, l + 64, ... for every
+// column in registers, then a fixed-order xor butterfly over the wave (deterministic), and
+// lane n applies bias / activation / gate / beta to column n. One launch without a K split:
+// the tile path's split + reduce took ~10 + ~5 us for these shapes (profiles/r04aa C3
+// timeline), latency, not work.
+// ---------------------------------------------------------------------------
+constexpr int RD_MAXN = 8;
+
+__global__ __launch_bounds__(256) void gemm_rowdot_kernel(XaGemmArgs g) {
+  const int lane = threadIdx.x & 63;
+  const int m = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (m >= g.M) return;
+  const float* a = static_cast<const float*>(g.a) + (int64_t)m * g.a_rm;
+  float acc[RD_MAXN];
+#pragma unroll
+  for (int n = 0; n < RD_MAXN; ++n) acc[n] = 0.0f;
+  for (int k = lane; k < g.K; k += 64) {
+    const float av = a[k];
+    const float* w = g.b + (int64_t)k * g.b_ks;
+#pragma unroll
+    for (int n = 0; n < RD_MAXN; ++n)
+      if (n < g.N) acc[n] = fmaf(av, w[(int64_t)n * g.b_ns], acc[n]);
+  }
+  float v = 0.0f;
+#pragma unroll
+  for (int n = 0; n < RD_MAXN; ++n) {
+    float t = acc[n];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off);
+    if (lane == n) v = t;
+  }
+  if (lane < g.N) store_c(epilogue(v, lane, g), m, lane, g);
+}
+
+// the row-dot path's contract: f32 A with plain rows (A(m, k) = a[m lda + k]), N <= 8,
+// K <= 4096, no split requested by the caller beyond the default
+bool rowdot_ok(const XaGemmArgs& g) {
+  return !g.force_small && g.a != nullptr && !g.a_u8 && g.a_pm == 1 && g.a_pk == 1 &&
+         g.a_rk == 1 && g.N <= RD_MAXN && g.K <= 4096 && g.M <= (1 << 20);
+}
+
+// ---------------------------------------------------------------------------
 // Few-row dense forward over a huge K (the NatureCNN dense layer's forward at the acting
 // batch: 17 <= M <= 32, N = 512, K = 37632; see fwd_splitk_ok): split z of the S workgroups owns the k range
 // [z per, (z + 1) per) for EVERY output -- its A slice [M][per] in LDS (read once), its W
@@ -1279,6 +1322,11 @@ extern "C" int xa_gemm(const XaGemmArgs* p, void* stream) {
     else if (mt <= 2) launch_res<2>(g, ch, gate, G, rounds, s);
     else launch_res<4>(g, ch, gate, G, rounds, s);
     XA_CHECK_LAUNCH("xa_gemm (small M, resident A)");
+    return 0;
+  }
+  if (rowdot_ok(g)) {
+    hipLaunchKernelGGL(gemm_rowdot_kernel, dim3((g.M + 3) / 4), dim3(256), 0, s, g);
+    XA_CHECK_LAUNCH("xa_gemm (row dot)");
     return 0;
   }
   if (fwd_splitk_ok(g) && fwd_splitk_per(g) <= 512) {
