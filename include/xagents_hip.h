@@ -403,7 +403,9 @@ typedef struct XaGemmArgs {
   int64_t ld_gate;
   int beta;
   int force_small; /* 1: always the 64 x 64 small-tile kernel; 2: the generic tile kernels,
-                     never the small-M ones (tests / A-B timing) */
+                     never the small-M ones; 3: every path but the few-column row-dot one;
+                     4: the default paths plus the split-K few-row forward (tests / A-B
+                     timing) */
 } XaGemmArgs;
 
 int xa_gemm(const XaGemmArgs* args, void* stream);

@@ -33,7 +33,9 @@ _SHAPES = [(37, 50, 29, 1), (64, 512, 3000, 8), (130, 70, 1000, 4), (300, 257, 4
 
 
 @pytest.mark.parametrize('small', [False, True])
-@pytest.mark.parametrize('M,N,K,splits', _SHAPES)
+@pytest.mark.parametrize('M,N,K,splits', _SHAPES + [
+    # the opt-in split-K few-row forward (force_small 4 below; default paths elsewhere)
+    (32, 512, 37632, 256), (17, 448, 12345, 100)])
 def test_gemm_plain_bias_relu_split(device, M, N, K, splits, small):
     from xagents_amd.layers import gemm
     from xagents_amd._lib import XA_ACT_RELU
@@ -46,7 +48,7 @@ def test_gemm_plain_bias_relu_split(device, M, N, K, splits, small):
     ws = torch.empty(splits * M * N + 1, device=device)
     gemm(M, N, K, ta.data_ptr(), tb.data_ptr(), C.data_ptr(), a_m=(1, K, 0), b_ks=N, b_ns=1,
          ldc=N, bias=tbias.data_ptr(), act=XA_ACT_RELU, workspace=ws, splits=splits,
-         force_small=small)
+         force_small=4 if (small and M in (17, 32) and K > 10000) else small)
     ref = np.maximum(A.astype(np.float64) @ B + b, 0)
     _close(C.cpu().numpy(), ref)
 

@@ -29,7 +29,7 @@ def main():
         c = torch.empty(M, N, device=dev)
         s = lib.xa_gemm_splits(M, N, K)
         ws = torch.empty(max(s, 1) * M * N + 1, device=dev)
-        for label, force in (('split-K fwd', 0), ('generic', 1)):
+        for label, force in (('split-K fwd', 4), ('default', 0)):
             def run():
                 gemm(M, N, K, a.data_ptr(), w.data_ptr(), c.data_ptr(), a_m=(1, K, 0), b_ks=N,
                      b_ns=1, ldc=N, bias=bias.data_ptr(), act=XA_ACT_RELU, workspace=ws,

@@ -790,9 +790,13 @@ __global__ __launch_bounds__(256) void gemm_fwd_splitk_kernel(XaGemmArgs g, int 
 // the tile kernels; M = 64 48.7 vs 40.5 us -- the 256 whole-width partials (M N 4 B each,
 // written and read back by the split reduce) cost more than the A re-reads they save -- and
 // M = 16 98.6 vs 35.1 us (the one-row-tile form); ring depth 4 / 8 / 12 within noise. So
-// 17 <= M <= 32 only.
+// 17 <= M <= 32 only, and only on request (force_small = 4): its summation order differs
+// from the tile kernels' that every other batch size takes, and the data-parallel test
+// compares a rank's 32-row minibatch forward with the union's 64-row one -- theta deviated
+// 1.2e-4 from the union step with this path vs 1.3e-6 without (profiles/r04ad_dprel.txt),
+// for a 3.7-us gain at C3's acting batch.
 bool fwd_splitk_ok(const XaGemmArgs& g) {
-  return !g.force_small && g.a != nullptr && !g.a_u8 && g.a_pm == 1 && g.a_pk == 1 &&
+  return g.force_small == 4 && g.a != nullptr && !g.a_u8 && g.a_pm == 1 && g.a_pk == 1 &&
          g.a_rk == 1 && g.a_rm % 4 == 0 && ((uintptr_t)g.a & 15) == 0 && g.b_ns == 1 &&
          g.M > 16 && g.M <= 32 && g.N % 64 == 0 && g.N <= 64 * FS_CTW && g.K >= 8192 &&
          !g.gate &&
@@ -1247,7 +1251,8 @@ void launch_res(const XaGemmArgs& g, int ch, bool gate, int G, int rounds, hipSt
 // 16-B aligned with lda, ldb multiples of 4, M <= 64, K in {128, 256, 512} (all of A in
 // LDS), and enough 16-column units (N >= 2048) to cover the chip
 bool smallm_res_ok(const XaGemmArgs& g) {
-  return !g.force_small && g.a != nullptr && !g.a_u8 && g.a_pm == 1 && g.a_pk == 1 &&
+  return (!g.force_small || g.force_small >= 3) && g.a != nullptr && !g.a_u8 && g.a_pm == 1 &&
+         g.a_pk == 1 &&
          g.a_rk == 1 && g.a_rm % 4 == 0 && ((uintptr_t)g.a & 15) == 0 && g.b_ks == 1 &&
          g.b_ns % 4 == 0 && ((uintptr_t)g.b & 15) == 0 && g.M <= 64 &&
          (g.K == 128 || g.K == 256 || g.K == 512) && g.N >= 2048;

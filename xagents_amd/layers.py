@@ -14,11 +14,14 @@ the GEMM loader (xagents/base.py:505-506).
 Buffers are allocated per batch size and reused; all launches go to torch's current
 stream (graph-capturable).
 """
+import os
+
 import torch
 
 from xagents_amd import _lib
 from xagents_amd._lib import XA_ACT_NONE, XA_ACT_RELU, XA_ACT_TANH, XaGemmArgs, call, stream
 
+_FORCE = int(os.environ.get('XA_GEMM_FORCE', '0'))
 _ACTS = {None: XA_ACT_NONE, 'linear': XA_ACT_NONE, 'relu': XA_ACT_RELU, 'tanh': XA_ACT_TANH}
 
 
@@ -55,7 +58,8 @@ def gemm(M, N, K, a, b, c, *, a_u8=False, a_m=(1, 0, 0), a_k=(1, 1, 0), b_ks, b_
     g.act = act
     g.gate, g.ld_gate = gate, ld_gate
     g.beta = int(beta)
-    g.force_small = int(force_small)
+    # XA_GEMM_FORCE (diagnostic A/B): a force_small code for every call that passes none
+    g.force_small = int(force_small) or _FORCE
     call('xa_gemm', ctypes_ref(g), stream())
 
 
