@@ -11,8 +11,8 @@ rollout uniforms and the rank-major union of the ranks' minibatch permutations. 
 data-parallel train step must equal the union step (xagents/ppo/agent.py:157-191):
 actions bit for bit, log-probs / values / returns to f32 rounding (the union's GEMMs run
 at twice the batch, which may pick another split-K count and so another summation
-order), parameters within 1e-4 of the update's norm, identical on every rank, and 16
-optimizer steps taken. Prints 'CNN DP OK <rank>'."""
+order), parameters within 5e-4 of the update's norm, identical on every rank, and 16
+optimizer steps taken (the parameter bound: comment at the assert). Prints 'CNN DP OK <rank>'."""
 import os
 import sys
 from pathlib import Path
@@ -39,11 +39,15 @@ def make(record, n, data_parallel=None):
 
 
 def main():
+    if os.environ.get('XA_LIB'):  # a diagnostic variant library (tools/cnn_dp_rel.sh)
+        from xagents_amd import _lib
+        _lib._lib = _lib.load(os.environ['XA_LIB'])
     dist.init_process_group('gloo')
     rank, world = dist.get_rank(), dist.get_world_size()
     torch.cuda.set_device(0)
     from xagents_amd.envs import record_transitions
-    records = [record_transitions(N, T_REC, (84, 84, 1), np.uint8, seed=55 + r)
+    base = int(os.environ.get('XA_DP_SEED', '55'))  # tools/cnn_dp_rel.sh sweeps it
+    records = [record_transitions(N, T_REC, (84, 84, 1), np.uint8, seed=base + r)
                for r in range(world)]
     uniforms = [np.random.default_rng(100 + r).random((N, T)).astype(np.float32)
                 for r in range(world)]
@@ -95,7 +99,14 @@ def main():
         rel = np.linalg.norm(td - tu) / np.linalg.norm(tu - theta0)
         print(f'CNN DP W={world}: rollout buffers bit-equal {exact}, theta rel {rel:.2e}',
               flush=True)
-        assert rel < 1e-4, f'data-parallel update deviates from the union update: {rel:.2e}'
+        # the union sums each minibatch's weight gradient over 2x the rows in one pass, the
+        # ranks in halves + an all-reduce: f32 regrouping, and a sample whose PPO ratio sits
+        # on the clip boundary (or a ReLU input at 0) can take the other branch. Measured
+        # over record seeds 55 / 155 / 255 and four GEMM builds (profiles/r04ag_dprel.txt):
+        # 3.5e-7 .. 1.0e-5, and 1.20e-4 in the two builds whose head / dense arithmetic puts
+        # one sample of seed 55 across such a boundary -- one flipped sample; a wrong
+        # exchange (a missing rank, a stale bucket) deviates by O(1)
+        assert rel < 5e-4, f'data-parallel update deviates from the union update: {rel:.2e}'
         assert int(un.model.optimizer.iterations.item()) == E * M
     dist.barrier()
     print(f'CNN DP OK {rank}', flush=True)
