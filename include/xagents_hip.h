@@ -406,10 +406,16 @@ typedef struct XaGemmArgs {
                      never the small-M ones; 3: every path but the few-column row-dot one;
                      4: the default paths plus the split-K few-row forward (tests / A-B
                      timing) */
+  int a_ones_row; /* 1: A's last row (m = M - 1) is all ones and is not read: a weight
+                     gradient X^T dZ and its bias gradient 1^T dZ as ONE GEMM into the
+                     contiguous [W; b] block (the 64 x 64 kernel only: xa_gemm_shape) */
 } XaGemmArgs;
 
 int xa_gemm(const XaGemmArgs* args, void* stream);
 int xa_gemm_splits(int M, int N, int K);
+/* the kernel shape xa_gemm picks for a tile-path GEMM with `splits` K splits (0 = the
+ * 64 x 64 kernel, the only one that takes a_ones_row) */
+int xa_gemm_shape(int M, int N, int K, int splits);
 size_t xa_gemm_workspace_floats(int M, int N, int K, int splits);
 
 /* Keras Conv1D input gradient (col2im as a fixed-order gather):

@@ -53,6 +53,32 @@ def test_gemm_plain_bias_relu_split(device, M, N, K, splits, small):
     _close(C.cpu().numpy(), ref)
 
 
+@pytest.mark.parametrize('M,N,K,beta', [(512, 6, 64, False), (37632, 512, 64, False),
+                                         (192, 64, 37632, True), (129, 70, 3001, False),
+                                         (5, 7, 9, True)])
+def test_gemm_ones_row_weight_and_bias_gradient(device, M, N, K, beta):
+    """a_ones_row: the weight gradient X^T dZ [M, N] and the bias gradient 1^T dZ [N] of a
+    layer as one GEMM into the contiguous [W; b] block (A = X^T read m-major with row M the
+    constant 1), against float64; beta accumulates into both (chunked minibatches)."""
+    from xagents_amd.layers import fold_bias_ok, gemm
+    from xagents_amd import _lib
+    assert fold_bias_ok(M, N, K)
+    rng = np.random.default_rng(M + N + K)
+    X = rng.normal(size=(K, M)).astype(np.float32)           # K rows of the layer input
+    dZ = rng.normal(size=(K, N)).astype(np.float32)
+    C0 = rng.normal(size=(M + 1, N)).astype(np.float32)
+    tx, tdz = torch.from_numpy(X).to(device), torch.from_numpy(dZ).to(device)
+    C = torch.from_numpy(C0).to(device)
+    s = _lib.load().xa_gemm_splits(M + 1, N, K)
+    ws = torch.empty(max(s, 1) * (M + 1) * N + 1, device=device)
+    gemm(M + 1, N, K, tx.data_ptr(), tdz.data_ptr(), C.data_ptr(), a_m=(1, 1, 0),
+         a_k=(1, M, 0), b_ks=N, b_ns=1, ldc=N, beta=beta, workspace=ws, a_ones_row=True)
+    ref = np.concatenate([X.astype(np.float64).T @ dZ, dZ.astype(np.float64).sum(0)[None]])
+    if beta:
+        ref = ref + C0
+    _close(C.cpu().numpy(), ref)
+
+
 @pytest.mark.parametrize('M,N,K', [(70, 45, 33), (260, 300, 77), (700, 60, 45), (60, 400, 50)])
 def test_gemm_transposes_gate_beta_u8(device, M, N, K):
     from xagents_amd.layers import gemm

@@ -193,6 +193,7 @@ class XaGemmArgs(Structure):
         ('ld_gate', c_int64),
         ('beta', c_int),
         ('force_small', c_int),
+        ('a_ones_row', c_int),
     ]
 
 
@@ -398,6 +399,7 @@ _SIGNATURES = {
     'xa_ppo_update': (c_int, [POINTER(XaPpoUpdateArgs), c_void_p]),
     'xa_gemm': (c_int, [POINTER(XaGemmArgs), c_void_p]),
     'xa_gemm_splits': (c_int, [c_int, c_int, c_int]),
+    'xa_gemm_shape': (c_int, [c_int, c_int, c_int, c_int]),
     'xa_gemm_workspace_floats': (ctypes.c_size_t, [c_int, c_int, c_int, c_int]),
     'xa_conv1d_input_grad': (
         c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],

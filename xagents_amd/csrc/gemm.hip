@@ -64,6 +64,7 @@ XA_DEV void store_c(float v, int m, int n, const XaGemmArgs& g) {
 struct XaGemmK {
   XaGemmArgs g;
   int vec_a, vec_b;
+  int ones_m;  // a_ones_row: the constant-one row (M - 1), else -1 (gemm_kernel only)
 };
 
 template <bool U8>
@@ -106,13 +107,18 @@ __global__ __launch_bounds__(256) void gemm_kernel(XaGemmK kargs) {
   const int a_k = A_KMAJOR ? (tid & 3) * 4 : tid >> 4;
   const int b_k = B_NMAJOR ? tid >> 4 : (tid & 3) * 4;
   const int b_n = B_NMAJOR ? (tid & 15) * 4 : tid >> 2;
+  // a_ones_row: row ones_m of A is constant 1 (never read); runs start on 4-aligned m, and the
+  // host's vec_a verdict is taken on the M - 1 real rows, so a 4-m run either lies below
+  // ones_m or starts at it
+  const int ones_m = kargs.ones_m;
   int64_t a_row[4];
-  bool a_ok[4];
+  bool a_ok[4], a_one[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int m = m0 + a_m + (A_KMAJOR ? 0 : i);
     a_ok[i] = m < g.M;
-    a_row[i] = a_ok[i] ? grouped(m, (int)g.a_pm, g.a_rm, g.a_sm) : 0;
+    a_one[i] = m == ones_m;
+    a_row[i] = a_ok[i] && !a_one[i] ? grouped(m, (int)g.a_pm, g.a_rm, g.a_sm) : 0;
   }
   const float* af = static_cast<const float*>(g.a);
   const uint8_t* au = static_cast<const uint8_t*>(g.a);
@@ -120,7 +126,8 @@ __global__ __launch_bounds__(256) void gemm_kernel(XaGemmK kargs) {
   float ra[4], rb[4];
 
   // interior fast path (as gemm_tile_kernel): fixed bases + k strides, no bounds tests
-  const bool fast = vec_a && vec_b && (A_KMAJOR || g.a_pk == 1) && m0 + BM <= g.M &&
+  const int m_real = ones_m >= 0 ? ones_m : g.M;
+  const bool fast = vec_a && vec_b && (A_KMAJOR || g.a_pk == 1) && m0 + BM <= m_real &&
                     n0 + BN <= g.N && (k_end - k_begin) % BK == 0;
   int64_t fa = 0, fb = 0;
   const int64_t fa_k = A_KMAJOR ? 1 : g.a_rk, fb_k = g.b_ks;
@@ -137,8 +144,16 @@ __global__ __launch_bounds__(256) void gemm_kernel(XaGemmK kargs) {
     if (vec_a) {
       // one run: 4 k of row a_m (k-major) or 4 m at column a_k
       const int k = kt + a_k;
-      if (a_ok[0] && k < k_end) ld4<A_U8>(g.a, a_row[0] + grouped(k, (int)g.a_pk, g.a_rk, g.a_sk), ra);
-      else zero4(ra);
+      if (a_ok[0] && k < k_end) {
+        if (a_one[0]) {
+          ra[0] = 1.0f;
+          ra[1] = ra[2] = ra[3] = A_KMAJOR ? 1.0f : 0.0f;
+        } else {
+          ld4<A_U8>(g.a, a_row[0] + grouped(k, (int)g.a_pk, g.a_rk, g.a_sk), ra);
+        }
+      } else {
+        zero4(ra);
+      }
     } else {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -146,7 +161,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(XaGemmK kargs) {
       const int ai = A_KMAJOR ? 0 : i;
       float v = 0.0f;
       if (a_ok[ai] && k < k_end) {
-        if (g.a == nullptr) {
+        if (g.a == nullptr || a_one[ai]) {
           v = 1.0f;
         } else {
           const int64_t off = a_row[ai] + grouped(k, (int)g.a_pk, g.a_rk, g.a_sk);
@@ -687,8 +702,8 @@ __global__ __launch_bounds__(256) void gemm_rowdot_kernel(XaGemmArgs g) {
 // the row-dot path's contract: f32 A with plain rows (A(m, k) = a[m lda + k]), N <= 8,
 // K <= 4096, no split requested by the caller beyond the default
 bool rowdot_ok(const XaGemmArgs& g) {
-  return !g.force_small && g.a != nullptr && !g.a_u8 && g.a_pm == 1 && g.a_pk == 1 &&
-         g.a_rk == 1 && g.N <= RD_MAXN && g.K <= 4096 && g.M <= (1 << 20);
+  return !g.force_small && !g.a_ones_row && g.a != nullptr && !g.a_u8 && g.a_pm == 1 &&
+         g.a_pk == 1 && g.a_rk == 1 && g.N <= RD_MAXN && g.K <= 4096 && g.M <= (1 << 20);
 }
 
 // ---------------------------------------------------------------------------
@@ -796,7 +811,7 @@ __global__ __launch_bounds__(256) void gemm_fwd_splitk_kernel(XaGemmArgs g, int 
 // 1.2e-4 from the union step with this path vs 1.3e-6 without (profiles/r04ad_dprel.txt),
 // for a 3.7-us gain at C3's acting batch.
 bool fwd_splitk_ok(const XaGemmArgs& g) {
-  return g.force_small == 4 && g.a != nullptr && !g.a_u8 && g.a_pm == 1 && g.a_pk == 1 &&
+  return g.force_small == 4 && !g.a_ones_row && g.a != nullptr && !g.a_u8 && g.a_pm == 1 && g.a_pk == 1 &&
          g.a_rk == 1 && g.a_rm % 4 == 0 && ((uintptr_t)g.a & 15) == 0 && g.b_ns == 1 &&
          g.M > 16 && g.M <= 32 && g.N % 64 == 0 && g.N <= 64 * FS_CTW && g.K >= 8192 &&
          !g.gate &&
@@ -1251,7 +1266,8 @@ void launch_res(const XaGemmArgs& g, int ch, bool gate, int G, int rounds, hipSt
 // 16-B aligned with lda, ldb multiples of 4, M <= 64, K in {128, 256, 512} (all of A in
 // LDS), and enough 16-column units (N >= 2048) to cover the chip
 bool smallm_res_ok(const XaGemmArgs& g) {
-  return (!g.force_small || g.force_small >= 3) && g.a != nullptr && !g.a_u8 && g.a_pm == 1 &&
+  return (!g.force_small || g.force_small >= 3) && !g.a_ones_row && g.a != nullptr && !g.a_u8 &&
+         g.a_pm == 1 &&
          g.a_pk == 1 &&
          g.a_rk == 1 && g.a_rm % 4 == 0 && ((uintptr_t)g.a & 15) == 0 && g.b_ks == 1 &&
          g.b_ns % 4 == 0 && ((uintptr_t)g.b & 15) == 0 && g.M <= 64 &&
@@ -1292,6 +1308,11 @@ extern "C" int xa_gemm_splits(int M, int N, int K) {
   int s = 1;
   while (tiles * s < want && kt / (s * 2) >= 8 && s < 4096) s *= 2;
   return s;
+}
+
+extern "C" int xa_gemm_shape(int M, int N, int K, int splits) {
+  if (splits < 1) splits = 1;
+  return pick_shape(M, N, K, (K + splits - 1) / splits, false);
 }
 
 extern "C" size_t xa_gemm_workspace_floats(int M, int N, int K, int splits) {
@@ -1363,12 +1384,16 @@ extern "C" int xa_gemm(const XaGemmArgs* p, void* stream) {
   const bool u8 = g.a_u8 != 0;
   const int per_split = (g.K + g.splits - 1) / g.splits;
   const int shape = g.force_small == 1 ? 0 : pick_shape(g.M, g.N, g.K, per_split, g.a == nullptr);
-  XaGemmK kg{g, 0, 0};
+  XA_CHECK_ARG(!g.a_ones_row || (shape == 0 && g.a != nullptr && g.M >= 2),
+               "xa_gemm: a_ones_row needs the 64 x 64 kernel (xa_gemm_shape == 0), A and M >= 2 "
+               "(got shape %d, M %d)", shape, g.M);
+  XaGemmK kg{g, 0, 0, g.a_ones_row ? g.M - 1 : -1};
+  const int m_real = g.a_ones_row ? g.M - 1 : g.M;
   if (g.a != nullptr && ((uintptr_t)g.a & (u8 ? 3 : 15)) == 0) {
     const bool rows4 = g.a_rm % 4 == 0 && (g.a_pm == 1 || g.a_sm % 4 == 0);
     const bool cols4 = g.a_rk % 4 == 0 && (g.a_pk == 1 || g.a_sk % 4 == 0);
     kg.vec_a = ak ? (g.K % 4 == 0 && rows4)
-                  : (g.a_pm == 1 && g.a_rm == 1 && g.M % 4 == 0 && cols4);
+                  : (g.a_pm == 1 && g.a_rm == 1 && m_real % 4 == 0 && cols4);
   }
   if (((uintptr_t)g.b & 15) == 0)
     kg.vec_b = bn ? (g.b_ks % 4 == 0 && g.N % 4 == 0)

@@ -33,7 +33,7 @@ def act_code(name):
 
 def gemm(M, N, K, a, b, c, *, a_u8=False, a_m=(1, 0, 0), a_k=(1, 1, 0), b_ks, b_ns,
          ldc, bias=None, act=XA_ACT_NONE, gate=None, ld_gate=0, beta=False, workspace=None,
-         splits=None, force_small=False):
+         splits=None, force_small=False, a_ones_row=False):
     """C = [C +] act(A B + bias) * [gate > 0] with A(m, k) = a[f(m) + g(k)],
     f / g given as (group, row stride, in-group stride) triples (gemm.hip)."""
     lib = _lib.load()
@@ -60,7 +60,16 @@ def gemm(M, N, K, a, b, c, *, a_u8=False, a_m=(1, 0, 0), a_k=(1, 1, 0), b_ks, b_
     g.beta = int(beta)
     # XA_GEMM_FORCE (diagnostic A/B): a force_small code for every call that passes none
     g.force_small = int(force_small) or _FORCE
+    g.a_ones_row = int(a_ones_row)
     call('xa_gemm', ctypes_ref(g), stream())
+
+
+def fold_bias_ok(M, N, K):
+    """A weight gradient [M, N] (K reduction rows) and its bias gradient can run as ONE GEMM
+    with a constant-one row appended to A (a_ones_row: the 64 x 64 kernel the dispatcher
+    picks for the few-row reductions of small batches); else two launches."""
+    lib = _lib.load()
+    return lib.xa_gemm_shape(M + 1, N, K, lib.xa_gemm_splits(M + 1, N, K)) == 0
 
 
 def ctypes_ref(x):
@@ -172,12 +181,13 @@ class LayerExecutor:
         B = self.B
         if l.kind == 'dense':
             return [(B, l.units, l.in_features), (l.in_features, l.units, B), (1, l.units, B),
-                    (B, l.in_features, l.units)]
+                    (B, l.in_features, l.units), (l.in_features + 1, l.units, B)]
         if l.kind == 'convolutional':
             rows, Win, P, C = self._conv_dims(i)
             kC = l.size * C
             return [(rows * P, l.filters, kC), (kC, l.filters, rows * P),
-                    (1, l.filters, rows * P), (rows * P, kC, l.filters)]
+                    (1, l.filters, rows * P), (rows * P, kC, l.filters),
+                    (kC + 1, l.filters, rows * P)]
         return []
 
     # ---- forward ---------------------------------------------------------------
@@ -307,13 +317,16 @@ class LayerExecutor:
             if l.kind == 'dense':
                 n_in, n_out = l.in_features, l.units
                 if gp is not None:
-                    # dW = X^T dZ ; db = 1^T dZ
-                    gemm(n_in, n_out, Bb, src.data_ptr(), d.data_ptr(), gp + 4 * w0,
+                    # dW = X^T dZ ; db = 1^T dZ -- one GEMM into the contiguous [W; b] block
+                    # (b0 = w0 + n_in n_out) when the 64 x 64 kernel takes it
+                    fold = fold_bias_ok(n_in, n_out, Bb) and b0 == w0 + n_in * n_out
+                    gemm(n_in + fold, n_out, Bb, src.data_ptr(), d.data_ptr(), gp + 4 * w0,
                          a_u8=src_u8, a_m=(1, 1, 0), a_k=(1, n_in, 0), b_ks=n_out, b_ns=1,
-                         ldc=n_out, beta=accumulate, workspace=self.workspace)
-                    gemm(1, n_out, Bb, None, d.data_ptr(), gp + 4 * b0, a_m=(1, 0, 0),
-                         a_k=(1, 0, 0), b_ks=n_out, b_ns=1, ldc=n_out, beta=accumulate,
-                         workspace=self.workspace)
+                         ldc=n_out, beta=accumulate, workspace=self.workspace, a_ones_row=fold)
+                    if not fold:
+                        gemm(1, n_out, Bb, None, d.data_ptr(), gp + 4 * b0, a_m=(1, 0, 0),
+                             a_k=(1, 0, 0), b_ks=n_out, b_ns=1, ldc=n_out, beta=accumulate,
+                             workspace=self.workspace)
                     if on_grad is not None:
                         on_grad(w0)
                 if j == -1 and dinput is not None:
@@ -338,12 +351,14 @@ class LayerExecutor:
                          int(gp + 4 * w0), int(gp + 4 * b0), int(accumulate),
                          self.wg_ws.data_ptr(), self.wg_floats[i], stream())
                 elif gp is not None:
-                    gemm(k * C, F, rows * P, src.data_ptr(), d.data_ptr(), gp + 4 * w0,
+                    fold = fold_bias_ok(k * C, F, rows * P) and b0 == w0 + k * C * F
+                    gemm(k * C + fold, F, rows * P, src.data_ptr(), d.data_ptr(), gp + 4 * w0,
                          a_u8=src_u8, a_m=(1, 1, 0), a_k=(P, Win * C, s * C), b_ks=F, b_ns=1,
-                         ldc=F, beta=accumulate, workspace=self.workspace)
-                    gemm(1, F, rows * P, None, d.data_ptr(), gp + 4 * b0, a_m=(1, 0, 0),
-                         a_k=(1, 0, 0), b_ks=F, b_ns=1, ldc=F, beta=accumulate,
-                         workspace=self.workspace)
+                         ldc=F, beta=accumulate, workspace=self.workspace, a_ones_row=fold)
+                    if not fold:
+                        gemm(1, F, rows * P, None, d.data_ptr(), gp + 4 * b0, a_m=(1, 0, 0),
+                             a_k=(1, 0, 0), b_ks=F, b_ns=1, ldc=F, beta=accumulate,
+                             workspace=self.workspace)
                 if gp is not None and on_grad is not None:
                     on_grad(w0)
                 if j != -1:
