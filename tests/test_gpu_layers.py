@@ -29,7 +29,9 @@ _SHAPES = [(37, 50, 29, 1), (64, 512, 3000, 8), (130, 70, 1000, 4), (300, 257, 4
            (17, 260, 5000, 32), (64, 512, 37632, 256), (32, 512, 37632, 256),
            (33, 448, 12345, 100),
            # few-column heads (row-dot path: N <= 8, K <= 4096)
-           (64, 6, 512, 2), (128, 1, 512, 1), (3, 8, 4096, 4), (1000, 5, 77, 1)]
+           (64, 6, 512, 2), (128, 1, 512, 1), (3, 8, 4096, 4), (1000, 5, 77, 1),
+           # few-k (elementwise path: K <= 8)
+           (64, 512, 6, 1), (300, 64, 4, 1), (7, 9, 1, 1)]
 
 
 @pytest.mark.parametrize('small', [False, True])
@@ -50,6 +52,24 @@ def test_gemm_plain_bias_relu_split(device, M, N, K, splits, small):
          ldc=N, bias=tbias.data_ptr(), act=XA_ACT_RELU, workspace=ws, splits=splits,
          force_small=4 if (small and M in (17, 32) and K > 10000) else small)
     ref = np.maximum(A.astype(np.float64) @ B + b, 0)
+    _close(C.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize('M,N,K', [(64, 512, 6), (128, 37632, 4), (5, 3, 1)])
+def test_gemm_head_input_gradient_few_k(device, M, N, K):
+    """The heads' input gradient dX = dZ W^T with K = the head width (<= 8: the few-k path),
+    the source layer's ReLU gate and beta accumulation (two heads into one dX), vs f64."""
+    from xagents_amd.layers import gemm
+    rng = np.random.default_rng(M + N + K)
+    dZ = rng.normal(size=(M, K)).astype(np.float32)
+    W = rng.normal(size=(N, K)).astype(np.float32)           # the head's [n_in, n_out] block^T
+    gate = rng.normal(size=(M, N)).astype(np.float32)
+    C0 = rng.normal(size=(M, N)).astype(np.float32)
+    tdz, tw, tg = (torch.from_numpy(x).to(device) for x in (dZ, W, gate))
+    C = torch.from_numpy(C0).to(device)
+    gemm(M, N, K, tdz.data_ptr(), tw.data_ptr(), C.data_ptr(), a_m=(1, K, 0), b_ks=1, b_ns=K,
+         ldc=N, gate=tg.data_ptr(), ld_gate=N, beta=True, workspace=torch.empty(1, device=device))
+    ref = C0 + np.where(gate > 0, dZ.astype(np.float64) @ W.T, 0.0)
     _close(C.cpu().numpy(), ref)
 
 

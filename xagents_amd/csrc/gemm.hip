@@ -681,12 +681,25 @@ __global__ __launch_bounds__(256) void gemm_rowdot_kernel(XaGemmArgs g) {
   float acc[RD_MAXN];
 #pragma unroll
   for (int n = 0; n < RD_MAXN; ++n) acc[n] = 0.0f;
-  for (int k = lane; k < g.K; k += 64) {
-    const float av = a[k];
-    const float* w = g.b + (int64_t)k * g.b_ks;
+  // RD_U k steps per pass with every load of the pass issued before the FMAs (one memory
+  // round trip per pass instead of one per k step: K = 512 is one pass)
+  constexpr int RD_U = 8;
+  for (int k0 = lane; k0 < g.K; k0 += 64 * RD_U) {
+    float av[RD_U], wv[RD_U][RD_MAXN];
 #pragma unroll
-    for (int n = 0; n < RD_MAXN; ++n)
-      if (n < g.N) acc[n] = fmaf(av, w[(int64_t)n * g.b_ns], acc[n]);
+    for (int u = 0; u < RD_U; ++u) {
+      const int k = k0 + 64 * u;
+      const bool in = k < g.K;
+      av[u] = in ? a[k] : 0.0f;
+      const float* w = g.b + (int64_t)(in ? k : 0) * g.b_ks;
+#pragma unroll
+      for (int n = 0; n < RD_MAXN; ++n)
+        wv[u][n] = (in && n < g.N) ? w[(int64_t)n * g.b_ns] : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < RD_U; ++u)
+#pragma unroll
+      for (int n = 0; n < RD_MAXN; ++n) acc[n] = fmaf(av[u], wv[u][n], acc[n]);
   }
   float v = 0.0f;
 #pragma unroll
@@ -697,6 +710,28 @@ __global__ __launch_bounds__(256) void gemm_rowdot_kernel(XaGemmArgs g) {
     if (lane == n) v = t;
   }
   if (lane < g.N) store_c(epilogue(v, lane, g), m, lane, g);
+}
+
+// Few-k GEMM (K <= 8: the network heads' input gradient dZ W^T, K = the head width): one
+// thread per output, its K products in k order, the usual epilogue (gate / beta).
+constexpr int SK_MAXK = 8;
+
+__global__ __launch_bounds__(256) void gemm_smallk_kernel(XaGemmArgs g) {
+  const int64_t e = blockIdx.x * 256ll + threadIdx.x;
+  if (e >= (int64_t)g.M * g.N) return;
+  const int m = (int)(e / g.N), n = (int)(e - (int64_t)m * g.N);
+  const float* a = static_cast<const float*>(g.a) + (int64_t)m * g.a_rm;
+  const float* b = g.b + (int64_t)n * g.b_ns;
+  float v = 0.0f;
+#pragma unroll
+  for (int k = 0; k < SK_MAXK; ++k)
+    if (k < g.K) v = fmaf(a[k], b[(int64_t)k * g.b_ks], v);
+  store_c(epilogue(v, n, g), m, n, g);
+}
+
+bool smallk_ok(const XaGemmArgs& g) {
+  return !g.force_small && !g.a_ones_row && g.a != nullptr && !g.a_u8 && g.a_pm == 1 &&
+         g.a_pk == 1 && g.a_rk == 1 && g.K <= SK_MAXK && (int64_t)g.M * g.N < (1ll << 31);
 }
 
 // the row-dot path's contract: f32 A with plain rows (A(m, k) = a[m lda + k]), N <= 8,
@@ -1348,6 +1383,12 @@ extern "C" int xa_gemm(const XaGemmArgs* p, void* stream) {
     else if (mt <= 2) launch_res<2>(g, ch, gate, G, rounds, s);
     else launch_res<4>(g, ch, gate, G, rounds, s);
     XA_CHECK_LAUNCH("xa_gemm (small M, resident A)");
+    return 0;
+  }
+  if (smallk_ok(g)) {
+    const int64_t total = (int64_t)g.M * g.N;
+    hipLaunchKernelGGL(gemm_smallk_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, g);
+    XA_CHECK_LAUNCH("xa_gemm (few k)");
     return 0;
   }
   if (rowdot_ok(g)) {
