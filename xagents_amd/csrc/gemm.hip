@@ -968,10 +968,10 @@ __global__ __launch_bounds__(256) void gemm_split_reduce_kernel(XaGemmArgs g, in
 // M N <= 64 K, splits in the hundreds or thousands): lane = output (one 256-B row segment
 // per split), 16 waves cut the split range into contiguous pieces summed with 8 loads in
 // flight, pieces combined in wave order through LDS
-__global__ __launch_bounds__(1024) void gemm_split_reduce_wide_kernel(XaGemmArgs g, int splits) {
+XA_DEV void split_reduce_wide(const XaGemmArgs& g, int splits, int bx) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int total = g.M * g.N;
-  const int e = blockIdx.x * 64 + lane;
+  const int e = bx * 64 + lane;
   const int per = (splits + 15) / 16;
   const int z0 = w * per, z1 = min(splits, z0 + per);
   __shared__ float part[16][64];
@@ -997,6 +997,19 @@ __global__ __launch_bounds__(1024) void gemm_split_reduce_wide_kernel(XaGemmArgs
     const int m = e / g.N, n = e - m * g.N;
     store_c(epilogue(s, n, g), m, n, g);
   }
+}
+
+__global__ __launch_bounds__(1024) void gemm_split_reduce_wide_kernel(XaGemmArgs g, int splits) {
+  split_reduce_wide(g, splits, blockIdx.x);
+}
+
+// two split reduces in one launch (the conv weight and bias gradients): blocks [0, nb1) reduce
+// g1, the rest g2 -- each output summed exactly as gemm_split_reduce_wide_kernel sums it
+__global__ __launch_bounds__(1024) void gemm_split_reduce_wide2_kernel(XaGemmArgs g1,
+                                                                       XaGemmArgs g2, int nb1,
+                                                                       int splits) {
+  if ((int)blockIdx.x < nb1) split_reduce_wide(g1, splits, blockIdx.x);
+  else split_reduce_wide(g2, splits, blockIdx.x - nb1);
 }
 
 // ---------------------------------------------------------------------------
@@ -1546,12 +1559,12 @@ extern "C" int xa_conv1d_wgrad(const void* x, int x_u8, const float* dy, int row
   r.partials = workspace;
   r.beta = accumulate;
   r.act = XA_ACT_NONE;
-  hipLaunchKernelGGL(gemm_split_reduce_wide_kernel, dim3((kc * filters + 63) / 64), dim3(1024), 0,
-                     s, r, kWgBlocks);
-  r.M = 1;
-  r.c = db;
-  r.partials = workspace + (size_t)kWgBlocks * kc * filters;
-  hipLaunchKernelGGL(gemm_split_reduce_wide_kernel, dim3((filters + 63) / 64), dim3(1024), 0, s, r,
+  XaGemmArgs rb = r;
+  rb.M = 1;
+  rb.c = db;
+  rb.partials = workspace + (size_t)kWgBlocks * kc * filters;
+  const int nbw = (kc * filters + 63) / 64, nbb = (filters + 63) / 64;
+  hipLaunchKernelGGL(gemm_split_reduce_wide2_kernel, dim3(nbw + nbb), dim3(1024), 0, s, r, rb, nbw,
                      kWgBlocks);
   XA_CHECK_LAUNCH("xa_conv1d_wgrad (reduce)");
   return 0;

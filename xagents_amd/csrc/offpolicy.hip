@@ -283,15 +283,37 @@ __global__ __launch_bounds__(256) void replay_step_small_kernel(XaReplayStepArgs
   const uint8_t* s_post = (const uint8_t*)a.rep_state + ((int64_t)i * a.t_rec + c) * ob;
   uint8_t* st = (uint8_t*)a.state + (int64_t)i * ob;
   const int64_t slot = a.ring_states ? (int64_t)i * a.capacity + ring_slot(a, i) : 0;
-  for (int64_t e = threadIdx.x; e < ob; e += blockDim.x) {
-    const uint8_t old = st[e], nw = s_new[e], post = s_post[e];
-    if (a.ring_states) {
-      ((uint8_t*)a.ring_states)[slot * ob + e] = old;
-      ((uint8_t*)a.ring_new_states)[slot * ob + e] = nw;
+  const uintptr_t bases = (uintptr_t)a.state | (uintptr_t)a.rep_obs | (uintptr_t)a.rep_state |
+                          (uintptr_t)a.ring_states | (uintptr_t)a.ring_new_states |
+                          (uintptr_t)a.out_states | (uintptr_t)a.out_new_states;
+  if ((ob & 15) == 0 && (bases & 15) == 0) {
+    // 16-B moves (frames: 7056 B = 441 per env): every address is a 16-B aligned base plus
+    // a multiple of ob
+    const int64_t n16 = ob >> 4;
+    for (int64_t e = threadIdx.x; e < n16; e += blockDim.x) {
+      const uint4 old = reinterpret_cast<const uint4*>(st)[e];
+      const uint4 nw = reinterpret_cast<const uint4*>(s_new)[e];
+      const uint4 post = reinterpret_cast<const uint4*>(s_post)[e];
+      if (a.ring_states) {
+        reinterpret_cast<uint4*>((uint8_t*)a.ring_states + slot * ob)[e] = old;
+        reinterpret_cast<uint4*>((uint8_t*)a.ring_new_states + slot * ob)[e] = nw;
+      }
+      if (a.out_states) reinterpret_cast<uint4*>((uint8_t*)a.out_states + (int64_t)i * ob)[e] = old;
+      if (a.out_new_states)
+        reinterpret_cast<uint4*>((uint8_t*)a.out_new_states + (int64_t)i * ob)[e] = nw;
+      reinterpret_cast<uint4*>(st)[e] = post;
     }
-    if (a.out_states) ((uint8_t*)a.out_states)[(int64_t)i * ob + e] = old;
-    if (a.out_new_states) ((uint8_t*)a.out_new_states)[(int64_t)i * ob + e] = nw;
-    st[e] = post;
+  } else {
+    for (int64_t e = threadIdx.x; e < ob; e += blockDim.x) {
+      const uint8_t old = st[e], nw = s_new[e], post = s_post[e];
+      if (a.ring_states) {
+        ((uint8_t*)a.ring_states)[slot * ob + e] = old;
+        ((uint8_t*)a.ring_new_states)[slot * ob + e] = nw;
+      }
+      if (a.out_states) ((uint8_t*)a.out_states)[(int64_t)i * ob + e] = old;
+      if (a.out_new_states) ((uint8_t*)a.out_new_states)[(int64_t)i * ob + e] = nw;
+      st[e] = post;
+    }
   }
   __syncthreads();  // (ring_slot and the cursor above were read before the scalars advance them)
   if (threadIdx.x != 0) return;
@@ -520,7 +542,9 @@ extern "C" int xa_replay_env_step(const XaReplayStepArgs* p, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const int64_t chunk = 4096;
   dim3 grid((unsigned)((a.obs_bytes + chunk - 1) / chunk), a.n_envs);
-  if (a.obs_bytes <= 4096) {  // vector observations: one launch
+  // vector observations and single frames up to 32 KB (C3's 84 x 84 frames: 7056 B): one
+  // launch, one workgroup per env
+  if (a.obs_bytes <= 4096 || (a.obs_bytes <= 32768 && (a.obs_bytes & 15) == 0)) {
     hipLaunchKernelGGL(replay_step_small_kernel, dim3(a.n_envs), dim3(256), 0, s, a);
     XA_CHECK_LAUNCH("xa_replay_env_step (small)");
     return 0;
