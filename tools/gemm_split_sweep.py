@@ -23,7 +23,7 @@ def main():
         big = torch.randn(max(B * 37632, 37632 * 512), device=dev)
         out = torch.empty(max(B * 37632, 37632 * 512), device=dev)
         for name, M, N, K, am, ak, bks, bns, is_u8 in shapes(B):
-            if not name.startswith('dense'):
+            if not (name.startswith('dense') or name.startswith('conv') and 'dcol' not in name):
                 continue
             cur = lib.xa_gemm_splits(M, N, K)
             ws = torch.empty(min(512 * M * N, 1 << 28), device=dev)

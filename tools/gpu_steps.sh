@@ -169,6 +169,7 @@ for step in "$@"; do
       run_pytest smallmtest 300 tests/test_gpu_layers.py -k "small_m or dense_input or layer_executor"
       run smallm 120 python tools/bench_smallm.py 16 64 128 336 ;;
     dprel) run dprel 700 bash tools/cnn_dp_rel.sh ;;
+    sweep) run sweep 400 python tools/gemm_split_sweep.py 32 64 128 ;;
     c3host) run c3host 300 python tools/c3_host_profile.py ;;
     sstamps) XA_LIB=tools/diag_lib/libxa_sdiag3.so run sstamps 120 python tools/smallm_stamps.py 64 16 ;;
     rsplit)
