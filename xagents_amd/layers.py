@@ -14,6 +14,7 @@ the GEMM loader (xagents/base.py:505-506).
 Buffers are allocated per batch size and reused; all launches go to torch's current
 stream (graph-capturable).
 """
+import functools
 import os
 
 import torch
@@ -64,6 +65,7 @@ def gemm(M, N, K, a, b, c, *, a_u8=False, a_m=(1, 0, 0), a_k=(1, 1, 0), b_ks, b_
     call('xa_gemm', ctypes_ref(g), stream())
 
 
+@functools.lru_cache(maxsize=None)
 def fold_bias_ok(M, N, K):
     """A weight gradient [M, N] (K reduction rows) and its bias gradient can run as ONE GEMM
     with a constant-one row appended to A (a_ones_row: the 64 x 64 kernel the dispatcher
