@@ -324,15 +324,39 @@ def fused_td3_roofline(agent, launches=10):
     ms = float(np.mean([e0.elapsed_time(e1) for _, e0, e1 in rows]))
     pol = sum(p for p, _, _ in rows) / len(rows)
     flops = pol * agent.fused_step_flops(True) + (1 - pol) * agent.fused_step_flops(False)
+    nbytes = pol * fused_td3_bytes(agent, True) + (1 - pol) * fused_td3_bytes(agent, False)
     tf = flops / (ms * 1e-3) / 1e12
+    gbs = nbytes / (ms * 1e-3) / 1e9
     return {'kernel': 'xa_td3_update (one persistent launch per gradient step: twin critics, '
-                      'TD head, backward, Adam, actor update, Polyak)', 'bound': 'mfma',
-            'achieved': round(tf, 4), 'peak': F32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
-            'frac': round(tf / F32_MFMA_PEAK_TFLOPS, 5), 'traffic': None,
-            'launch_ms': round(ms, 5), 'flops_per_launch': int(flops),
-            'note': f'2 M N K FLOP of every GEMM of the step at batch {agent.batch_size}, '
-                    f'mean of {len(rows)} event-timed launches; latency-bound (5 / 10 grid '
-                    f'barriers between the 6 / 11 phases of a critic / policy step)'}
+                      'TD head, backward, Adam, actor update, Polyak)', 'bound': 'hbm',
+            'achieved': round(gbs, 3), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+            'frac': round(gbs / HBM_PEAK_GBS, 5), 'traffic': None,
+            'launch_ms': round(ms, 5), 'bytes_per_launch': int(nbytes),
+            'mfma': {'achieved': round(tf, 4), 'peak': F32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
+                     'frac': round(tf / F32_MFMA_PEAK_TFLOPS, 5),
+                     'flops_per_launch': int(flops)},
+            'note': f'HBM basis (SURVEY 8d C5): algorithmic bytes of one gradient step at batch '
+                    f'{agent.batch_size} (theta / m / v / gradient of every trained network '
+                    f'7 x 4 B x P, every target network read, + written on policy steps, the '
+                    f'sampled batch gathered and written) / the mean of {len(rows)} '
+                    f'event-timed launches; MFMA basis (2 M N K FLOP of every GEMM) under '
+                    f'"mfma"; latency-bound (5 / 10 grid barriers between the 6 / 11 phases '
+                    f'of a critic / policy step)'}
+
+
+def fused_td3_bytes(agent, policy=True):
+    """Algorithmic HBM bytes of one DDPG / TD3 gradient step: the trained
+    networks' theta, m, v read and written and their raw gradient written and read back
+    (7 x 4 B per parameter: the critics every step, the actor on policy steps); the target
+    networks read by the target forwards (target actor, target critics) and, on policy
+    steps, written by the Polyak sync; the sampled batch (s, s', a, r, d) read from the rings
+    and written for the caller."""
+    nc = 2 if hasattr(agent, 'critic2') else 1
+    pa, pc = agent.actor.n_params, agent.critic.n_params
+    trained = nc * pc + (pa if policy else 0)
+    targets = (pa + nc * pc) * (8 if policy else 4)
+    batch = agent.batch_size * (2 * agent.S + agent.A + 2) * 4 * 2
+    return 7 * 4 * trained + targets + batch
 
 
 def bench_offpolicy_and_cnn(args):
@@ -464,7 +488,9 @@ def run_secondary(args, config, world, rank, device, steps, warmup, cpu_seconds,
         agent = TD3(envs, actor, critic, bufs, gradient_steps=1, seed=args.seed, quiet=True)
         agent.fill_buffers()
         # env steps with their done-triggered gradient steps, and one gradient step alone
+        it0 = int(agent.critic.optimizer.iterations.item())
         el = _timed(agent.train_step, steps, warmup, world)
+        grad_steps = int(agent.critic.optimizer.iterations.item()) - it0
         g_el = _timed(lambda: agent.update_weights(1), steps, warmup, world)
         env_steps = n * steps * world
         # one eager gradient step for the event pairs (the timed steps replay hipGraphs,
@@ -485,7 +511,17 @@ def run_secondary(args, config, world, rank, device, steps, warmup, cpu_seconds,
                         'workload': 'TD3 BipedalWalker-v3-shaped, 64 envs, ReplayBuffer2, '
                                     'per-buffer batch 1 (100 // 64), gradient_steps 1 '
                                     '(BASELINE configs[4])',
-                        'n_envs_per_gpu': n, 'parallelism': f'dp{world}'},
+                        'n_envs_per_gpu': n, 'parallelism': f'dp{world}',
+                        # the value depends on how often episodes end: every finished
+                        # episode of the union triggers gradient_steps gradient steps
+                        # (ddpg/agent.py:157-166)
+                        'synthetic_episode_length': 'record dones ~ Bernoulli(1/200) per step '
+                                                    '(Geometric, mean 200) + a forced terminal '
+                                                    'at the record end (t_rec 256)',
+                        'gradient_steps_per_env_step': round(
+                            grad_steps / ((steps + warmup) * n * world), 5),
+                        'gradient_steps_per_train_step': round(
+                            grad_steps / (steps + warmup), 4)},
                     gradient_step_ms=round(g_el / steps * 1e3, 4))
     line['value'] = round(env_steps / el, 1)
     line['ms_per_step'] = round(el / steps * 1e3, 4)
@@ -514,6 +550,10 @@ def compact_secondaries(args, device):
             out[cfg] = {k: r[k] for k in ('value', 'unit', 'ms_per_step', 'scaling', 'steps',
                                           'warmup') if k in r}
             out[cfg]['workload'] = r['config']['workload']
+            for k in ('synthetic_episode_length', 'gradient_steps_per_env_step',
+                      'gradient_steps_per_train_step'):
+                if k in r['config']:
+                    out[cfg][k] = r['config'][k]
             out[cfg]['roofline'] = r.get('roofline')
             out[cfg]['cpu_baseline'] = r.get('cpu_baseline')
             if 'gradient_step_ms' in r:

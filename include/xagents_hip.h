@@ -716,7 +716,16 @@ typedef struct XaTdNet {
  * (optional), dv1 / dv2 [batch] and the raw gradients g_* (before Adam), loss_out [batch]
  * (optional); parameters, moments and step counters in place. workspace: zeroed once by
  * the caller (xa_td3_update_workspace_bytes), reused by every launch without a reset; a
- * barrier that times out (10 s) sets *status = 1 and the workspace must be re-zeroed. */
+ * barrier that times out (10 s) sets *status = 1 and the workspace must be re-zeroed;
+ * while *status != 0 every launch returns without touching anything.
+ * stage 0: the whole step. Data parallel (ranks all-reduce the raw gradients between
+ * launches, ddpg/agent.py:104-127 + the rank sum): stage 1 writes the critics' raw gradients
+ * (and the sampled batch, the noise, the actor forward on policy steps); stage 2 applies the
+ * critics' Adam to g_critic* x critic_grad_scale (+ Polyak of the critic targets on policy
+ * steps) and on policy steps writes the actor's raw gradient through the updated critic 1;
+ * stage 3 (actor_update = 1) applies the actor's Adam to g_actor x actor_grad_scale + the
+ * Polyak of the target actor. Each stage bumps the counters it owns (1: the noise counter,
+ * 2: the critics' steps, 3: the actor's step). */
 typedef struct XaTd3UpdateArgs {
   int batch, obs_dim, act_dim, h1, h2;
   int twin, smooth, actor_update;
@@ -746,6 +755,8 @@ typedef struct XaTd3UpdateArgs {
   size_t workspace_bytes;
   int n_blocks;
   int* status;
+  int stage;
+  float critic_grad_scale, actor_grad_scale;
 } XaTd3UpdateArgs;
 
 size_t xa_td3_update_workspace_bytes(int batch, int obs_dim, int act_dim, int h1, int h2);

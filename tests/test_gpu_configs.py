@@ -190,9 +190,12 @@ def test_c4_ppo_cnn_128_env_shard(device):
     assert np.isfinite(_np(model.theta)).all()
 
 
-def test_c5_td3_64_envs_rb2(device):
+@pytest.mark.parametrize('fused', [True, False], ids=['fused', 'executor'])
+def test_c5_td3_64_envs_rb2(device, fused):
     """C5 on one GPU: TD3, 64 BipedalWalker-shaped envs, ReplayBuffer2 (1M total, per-buffer
-    batch 100 // 64 = 1), gradient_steps 1; one gradient step vs float64."""
+    batch 100 // 64 = 1), gradient_steps 1; three chained gradient steps vs float64 on both
+    the fused xa_td3_update and the layer-executor step: both critics' and (on the policy
+    steps) the actor's raw gradients at 1e-4."""
     from test_gpu_scale import _critic_head_f64
     import nets_f64 as O
     from xagents_amd import TD3
@@ -209,14 +212,22 @@ def test_c5_td3_64_envs_rb2(device):
     assert bufs[0].batch_size == 1 and bufs[0].size == 1_000_000 // n
     agent = TD3(envs, actor, critic, bufs, gradient_steps=1, seed=55, quiet=True)
     assert agent.batch_size == 64
+    if fused:
+        assert agent._fused_args() is not None
+    else:
+        agent.__dict__['_fused'] = agent.__dict__['_fused_act'] = None
     agent.fill_buffers()
     fw = lambda m, th, x: O.forward(m.layers, th, x, m.input_shape)  # noqa: E731
     # three chained gradient steps, each teacher-forced at the device's own critic and
     # target parameters (the twin critics, the delayed actor and the Polyak targets move
-    # in between): the critic gradient vs float64 at 1e-4 every step
+    # in between): the critic gradients vs float64 at 1e-4 every step and the actor's
+    # through the device's updated critic 1 (each update_weights(1) call runs its gradient
+    # step 0, a policy step)
     for step in range(3):
-        c1 = _np(agent.critic.theta)
+        c1, c2 = _np(agent.critic.theta), _np(agent.critic2.theta)
+        ac0 = _np(agent.actor.theta)
         tt = [_np(m.theta) for m in (agent.target_actor, agent.target_critic, agent.target_critic2)]
+        it_a = int(agent.actor.optimizer.iterations.item())
         agent.update_weights(1)
         torch.cuda.synchronize()
         s, a, r, d, s2 = (_np(x) for x in (agent.s, agent.a, agent.r, agent.d, agent.s2))
@@ -226,11 +237,26 @@ def test_c5_td3_64_envs_rb2(device):
         tv = np.minimum(*[fw(c, th, s2a2)[1][c.outputs[0]]
                           for c, th in zip((agent.target_critic, agent.target_critic2), tt[1:])])
         y = r[:, None] + (1 - d[:, None]) * np.float64(np.float32(0.99)) * tv
-        x64, o = fw(agent.critic, c1, np.concatenate([s, a], 1))
-        dv, _ = _critic_head_f64(o[agent.critic.outputs[0]], y, None)
-        g = O.backward(agent.critic.layers, c1, x64, o, {agent.critic.outputs[0]: dv})
-        e = _rel(_np(agent.g_critic), g)
-        assert e < 1e-4, f'step {step}: critic gradient {e:.2e}'
+        for name, c, th, gd in (('critic 1', agent.critic, c1, agent.g_critic),
+                                ('critic 2', agent.critic2, c2, agent.g_critic2)):
+            x64, o = fw(c, th, np.concatenate([s, a], 1))
+            dv, _ = _critic_head_f64(o[c.outputs[0]], y, None)
+            g = O.backward(c.layers, th, x64, o, {c.outputs[0]: dv})
+            e = _rel(_np(gd), g)
+            assert e < 1e-4, f'step {step}: {name} gradient {e:.2e}'
+        # update_weights(1) runs gradient step 0 of its call: a policy step every call
+        assert int(agent.actor.optimizer.iterations.item()) == it_a + 1
+        act = agent.actor
+        xa, oa = fw(act, ac0, s)
+        spa = np.concatenate([s, oa[act.outputs[0]]], 1)
+        c1n = _np(agent.critic.theta)
+        xc, oc = fw(agent.critic, c1n, spa)
+        _, dx = O.backward(agent.critic.layers, c1n, xc, oc,
+                           {agent.critic.outputs[0]: -np.ones((len(s), 1)) / len(s)},
+                           want_input_grad=True)
+        ga = O.backward(act.layers, ac0, xa, oa, {act.outputs[0]: dx[:, s.shape[1]:]})
+        e = _rel(_np(agent.g_actor), ga)
+        assert e < 1e-4, f'step {step}: actor gradient {e:.2e}'
     for _ in range(100):
         agent.train_step()
     agent._drain_episode_stats()

@@ -145,11 +145,12 @@ def test_dqn_huber_opt_in_vs_f64(device):
 # ---------------------------------------------------------------------------------------
 # DDPG / TD3 (ddpg/agent.py:87-127, td3/agent.py:66-110)
 # ---------------------------------------------------------------------------------------
-def _ddpg(device, kind, huber=None):
+def _ddpg(device, kind, huber=None, n=4, fused=True):
+    """n envs with one RB2 each, batch 2 n. fused=False forces the layer-executor step (the
+    path a non-MLP cfg takes) in place of xa_td3_update / xa_td3_act."""
     from xagents_amd import DDPG, TD3
     from xagents_amd.envs import create_envs
     from xagents_amd.utils.common import create_buffers, create_model
-    n = 4
     envs = create_envs('BipedalWalker-v3', n, device=device, seed=4, t_rec=64)
     kw = dict(seed=7, device=device, optimizer_kwargs=dict(learning_rate=LR))
     actor = create_model(envs, kind, 'actor_model', **kw)
@@ -160,6 +161,10 @@ def _ddpg(device, kind, huber=None):
     random.seed(2)
     agent = cls(envs, actor, critic, bufs, gradient_steps=1, tau=0.05, seed=3, quiet=True,
                 gamma=0.99, huber_delta=huber)
+    if fused:
+        assert agent._fused_args() is not None and agent._fused_act_args() is not None
+    else:
+        agent.__dict__['_fused'] = agent.__dict__['_fused_act'] = None
     agent.fill_buffers()
     return agent
 
@@ -173,10 +178,20 @@ def _critic_head_f64(v, y, huber):
     return 2 * e, e * e
 
 
-@pytest.mark.parametrize('kind,huber', [('td3', None), ('ddpg', None), ('td3', 0.5)])
-def test_critic_actor_raw_gradients_and_chained_steps(device, kind, huber):
+@pytest.mark.parametrize('fused', [True, False], ids=['fused', 'executor'])
+@pytest.mark.parametrize('kind,huber,n', [('td3', None, 4), ('ddpg', None, 4), ('td3', 0.5, 4),
+                                          ('td3', None, 32), ('td3', None, 50),
+                                          ('ddpg', None, 50)])
+def test_critic_actor_raw_gradients_and_chained_steps(device, kind, huber, n, fused):
+    """Both gradient-step paths (the fused xa_td3_update and the layer executor, which a
+    non-MLP cfg takes) against float64 over 3 chained steps: dv and the per-sample loss at
+    1e-5, g_critic / g_critic2 / g_actor at 1e-4 (magnitude, not sign: the chained Adam
+    moments are non-zero). Batch 8 is one ragged row tile of the fused kernel; batch 64 (C5's)
+    two full ones; batch 100 four with a ragged last, two 64-row weight-gradient k blocks and
+    three column tiles per weight-gradient job, the cross-tile head tickets included."""
     import nets_f64 as O
-    agent = _ddpg(device, kind, huber)
+    agent = _ddpg(device, kind, huber, n=n, fused=fused)
+    assert agent.batch_size == 2 * n
     twin = kind == 'td3'
     critics = [agent.critic] + ([agent.critic2] if twin else [])
     tcrit = [agent.target_critic] + ([agent.target_critic2] if twin else [])

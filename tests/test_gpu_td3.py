@@ -43,15 +43,27 @@ def _step_close(got, th0, ref, lr=1e-3, tol=2e-2):
     assert err < tol, f'update mismatch {err:.3g} (units of lr)'
 
 
-@pytest.mark.parametrize('kind,n', [('td3', 4), ('ddpg', 4), ('td3', 50)])
-def test_one_gradient_step_vs_f64(device, kind, n):
-    """n = 4: batch 8 (one ragged row tile); n = 50: batch 100 -- four 32-row tiles (the last
-    ragged), two 64-row weight-gradient k blocks, three column tiles per weight-gradient job."""
+def _rel(got, want):
+    return float(np.linalg.norm(got - want) / max(np.linalg.norm(want), 1e-30))
+
+
+@pytest.mark.parametrize('fused', [True, False], ids=['fused', 'executor'])
+@pytest.mark.parametrize('kind,n', [('td3', 4), ('ddpg', 4), ('td3', 32), ('td3', 50)])
+def test_one_gradient_step_vs_f64(device, kind, n, fused):
+    """n = 4: batch 8 (one ragged row tile); n = 32: batch 64 (C5's); n = 50: batch 100 --
+    four 32-row tiles (the last ragged), two 64-row weight-gradient k blocks, three column
+    tiles per weight-gradient job. The raw gradients g_critic / g_critic2 / g_actor at 1e-4
+    relative (magnitude: a first Adam step from zero moments is ~ lr sign(g), so the step
+    check alone would pass a gradient off by a factor), then the applied step and the
+    Polyak targets."""
     sys.path.insert(0, str(ROOT / 'oracle'))
     import nets_f64 as O
     agent = _agent(device, kind, n=n)
-    if n > 4:
-        assert agent._fused_args() is not None and agent.batch_size == 2 * n
+    assert agent.batch_size == 2 * n
+    if fused:
+        assert agent._fused_args() is not None
+    else:
+        agent.__dict__['_fused'] = agent.__dict__['_fused_act'] = None
     agent.fill_buffers()
     twin = kind == 'td3'
     nets = [agent.actor, agent.critic] + ([agent.critic2] if twin else [])
@@ -75,11 +87,14 @@ def test_one_gradient_step_vs_f64(device, kind, n):
     y = r[:, None] + (1 - d[:, None]) * 0.99 * tv
     sa = np.concatenate([s, a], 1)
     new = [None] * len(nets)
+    g_dev = [None, agent.g_critic] + ([agent.g_critic2] if twin else [])
     for ci in range(1, len(nets)):
         c = nets[ci]
         x64, o = fw(c, th0[ci], sa)
         v = o[c.outputs[0]]
         g = O.backward(c.layers, th0[ci], x64, o, {c.outputs[0]: 2 * (v - y)})
+        e = _rel(_np(g_dev[ci]), g)
+        assert e < 1e-4, f'critic {ci}: raw gradient {e:.2e}'
         new[ci] = _adam(th0[ci], 0, 0, g, 1)
     # actor step through the UPDATED critic1 (the reference updates critics first)
     act = agent.actor
@@ -91,6 +106,15 @@ def test_one_gradient_step_vs_f64(device, kind, n):
                        {agent.critic.outputs[0]: -np.ones((B, 1)) / B}, want_input_grad=True)
     ga = O.backward(act.layers, th0[0], xa, oa, {act.outputs[0]: dx[:, s.shape[1]:]})
     new[0] = _adam(th0[0], 0, 0, ga, 1)
+    # the raw actor gradient through the device's own updated critic 1 (an element whose
+    # critic gradient is ~0 takes an Adam step that f32 and f64 may round apart)
+    c1 = _np(agent.critic.theta)
+    xc, oc = fw(agent.critic, c1, spa)
+    _, dx = O.backward(agent.critic.layers, c1, xc, oc,
+                       {agent.critic.outputs[0]: -np.ones((B, 1)) / B}, want_input_grad=True)
+    ga = O.backward(act.layers, th0[0], xa, oa, {act.outputs[0]: dx[:, s.shape[1]:]})
+    e = _rel(_np(agent.g_actor), ga)
+    assert e < 1e-4, f'actor: raw gradient {e:.2e}'
     for m, th_ref, t0 in zip(nets, new, th0):
         _step_close(_np(m.theta), t0, th_ref)
     for tm, t0, th_ref in zip(tnets, tt0, new):
@@ -207,3 +231,32 @@ def test_fused_step_actions_vs_f64(device, kind):
          ctr.data_ptr(), agent.rng_seed, o2.data_ptr(), cols, n2.data_ptr(), stream())
     torch.cuda.synchronize()
     np.testing.assert_array_equal(_np(n2), nz)
+
+
+def test_fused_grid_size_is_bit_neutral_and_status_clean(device):
+    """The fused step's result does not depend on its grid: 40 chained gradient steps at
+    batch 8 on 256 workgroups (most blocks hold no job in most phases, so they would have
+    arrived at no barrier before every block had to arrive at a launch's first one, ADVICE
+    r04) and on 32 give bit-identical weights, moments and step counters, and the status
+    word stays 0 (no barrier timed out)."""
+    import random
+    out = []
+    for G in (256, 32):
+        np.random.seed(0)
+        random.seed(0)
+        agent = _agent(device, 'td3')
+        a = agent._fused_args()
+        assert a is not None
+        a.n_blocks = G
+        agent.fill_buffers()
+        agent.update_weights(40)
+        torch.cuda.synchronize()
+        assert int(agent._fused_status.item()) == 0
+        assert int(agent.critic.optimizer.iterations.item()) == 40
+        assert int(agent.actor.optimizer.iterations.item()) == 20
+        nets = [agent.actor, agent.critic, agent.critic2, agent.target_actor,
+                agent.target_critic, agent.target_critic2]
+        out.append([_np(x) for m in nets for x in (m.theta,) + (
+            (m.optimizer.m, m.optimizer.v) if getattr(m, 'optimizer', None) is not None else ())])
+    for x, y in zip(*out):
+        np.testing.assert_array_equal(x, y)

@@ -62,7 +62,8 @@ for step in "$@"; do
     dp) run_pytest dp 500 tests/test_gpu_dp.py tests/test_gpu_peer.py tests/test_gpu_rccl_capture.py ;;
     gpu) run_pytest gpu 1000 tests -m gpu ;;
     configs) run_pytest configs 400 tests/test_gpu_configs.py ;;
-    td3) run_pytest td3 400 tests/test_gpu_td3.py tests/test_gpu_scale.py tests/test_gpu_configs.py::test_c5_td3_64_envs_rb2 ;;
+    td3) run_pytest td3 600 tests/test_gpu_td3.py tests/test_gpu_scale.py tests/test_gpu_configs.py::test_c5_td3_64_envs_rb2 ;;
+    td3dp) run_pytest td3dp 450 tests/test_gpu_dp.py -k td3 ;;
     td3time)
       # wall time per gradient step on the product build, per-phase barrier times on the
       # trace build (tools/diag_lib/libxa_td3trace.so: tools/build_variant.py td3trace

@@ -339,6 +339,7 @@ class XaTd3UpdateArgs(Structure):
         ('g_critic2', c_void_p),
         ('workspace', c_void_p), ('workspace_bytes', ctypes.c_size_t),
         ('n_blocks', c_int), ('status', c_void_p),
+        ('stage', c_int), ('critic_grad_scale', c_float), ('actor_grad_scale', c_float),
     ]
 
 

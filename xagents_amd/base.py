@@ -161,6 +161,11 @@ class BaseAgent(ABC):
                 f'Best reward updated: {self.best_reward} -> {self.mean_reward}'
             )
             if self.checkpoints:
+                # a persistent launch that failed (device status word) left the weights
+                # invalid: raise before any of them reaches a checkpoint file
+                checks = getattr(self, '_device_checks', None)
+                if checks is not None:
+                    checks()
                 for model, checkpoint in zip(self.output_models, self.checkpoints):
                     model.save_weights(checkpoint)
         self.best_reward = max(self.mean_reward, self.best_reward)

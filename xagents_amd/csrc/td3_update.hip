@@ -968,7 +968,8 @@ XA_DEV int adam_chunk(int rest, int jobs) {
   return max(per, (c + per - 1) / per * per);
 }
 __device__ __noinline__ void adam_range(Net n, const float* grad, int lo, int hi, float omb1,
-                                        float omb2, float eps, float* target, float tau) {
+                                        float omb2, float eps, float* target, float tau,
+                                        float gs = 1.0f) {
   const int hi4 = lo + ((hi - lo) & ~3);
   const __amdgpu_buffer_rsrc_t rg = rsrc(grad), rt = rsrc(n.th);
   for (int g0 = lo / 4 + (int)threadIdx.x; 4 * g0 < hi4; g0 += 256 * kAdamG) {
@@ -993,7 +994,7 @@ __device__ __noinline__ void adam_range(Net n, const float* grad, int lo, int hi
       float* yp = &tg[u].x;
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        adam_elem(gp[c], tp[c], mp[c], vp[c], n.alpha, omb1, omb2, eps);
+        adam_elem(gp[c] * gs, tp[c], mp[c], vp[c], n.alpha, omb1, omb2, eps);
         yp[c] = tau == 1.0f ? tp[c] : (1.0f - tau) * yp[c] + tau * tp[c];
       }
       st4c(rt, (uint32_t)i * 4u, f32x4v{th[u].x, th[u].y, th[u].z, th[u].w});
@@ -1004,7 +1005,7 @@ __device__ __noinline__ void adam_range(Net n, const float* grad, int lo, int hi
   }
   if ((int)threadIdx.x < hi - hi4) {
     const int i = hi4 + threadIdx.x;
-    adam_one(n, ldc(grad + i), i, omb1, omb2, eps, target, tau);
+    adam_one(n, ldc(grad + i) * gs, i, omb1, omb2, eps, target, tau);
   }
 }
 
@@ -1194,7 +1195,12 @@ XA_DEV bool grid_sync(Sync& y, int& lds_flag, int jobs, const PreB& pb = no_preb
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   y.n += 1;
-  const unsigned m = (unsigned)min((int)y.G, max(jobs, 0));
+  // EVERY block arrives at a launch's first barrier: each block reads the launch-start words
+  // (barrier base, epoch, step and noise counters) before it arrives, so once block 0 has
+  // passed this barrier its end-of-launch writes cannot reach a block that has not yet
+  // read them, however late that block was dispatched. Later barriers count
+  // only the blocks that held a job.
+  const unsigned m = y.n == 1 ? y.G : (unsigned)min((int)y.G, max(jobs, 0));
   y.target += m;
   if (threadIdx.x == 0 && blockIdx.x < m)
     __hip_atomic_fetch_add((gu32*)(y.cnt + kShardStride * (blockIdx.x % kShards)), 1u,
@@ -1319,10 +1325,19 @@ enum { N_TA = 0, N_C1 = 1, N_C2 = 2, N_AC = 3, N_TC1 = 4, N_TC2 = 5 };
 
 __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
   __shared__ int s_flag;
+  // a launch whose barrier timed out left the control words inconsistent (a stale barrier
+  // base, partial arrivals in the shards): every later launch is a no-op until the caller
+  // re-zeroes the workspace and the status word (it raises on the status)
+  if (p.status && *(const volatile int*)p.status != 0) return;
   const int G = gridDim.x, b = blockIdx.x, tid = threadIdx.x;
   const int B = p.batch, S = p.obs_dim, A = p.act_dim, H1 = p.h1, H2 = p.h2;
   const int C = S + A;
   const bool twin = p.twin != 0, pol = p.actor_update != 0;
+  // 0: the whole gradient step; data parallel (the gradients all-reduced between launches):
+  // 1 critics' forward / backward -> raw gradients, 2 critics' Adam (+ Polyak) and, on
+  // policy steps, the actor's forward / backward through the updated critic 1 -> raw
+  // gradient, 3 the actor's Adam + Polyak
+  const int stage = p.stage;
   const Ws ws = carve(p.workspace, B, H1, H2, A);
   Sync y;
   y.cnt = ws.cnt;
@@ -1366,7 +1381,7 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
 
   // the sampled batch for the caller (concat_buffer_samples' arrays), from the last block:
   // element e of [s | s' | a | r | d], every load of a thread in flight before its stores
-  if (b == G - 1) {
+  if (stage <= 1 && b == G - 1) {
     const int nS = B * S, nA = B * A, tot = 2 * nS + nA + 2 * B;
     constexpr int kGu = 16;
     for (int e0 = tid; e0 < tot; e0 += 256 * kGu) {
@@ -1464,6 +1479,9 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
     if (b >= RTT * CT1) return no_preb();  // (the input-gradient jobs come first)
     return pre_dx(ac.th + ac.w2, H2, b % CT1, false);
   };
+  const int nt = twin ? 2 : 1;
+  int p8_jobs = 0;
+  if (stage <= 1) {
   for (int layer = 1; layer <= 2; ++layer) {
     const int CT = layer == 1 ? CT1 : CT2, per = RTT * CT;
     for (int j = b; j < nn * per; j += G) {
@@ -1513,7 +1531,6 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
   // ---- P4 / P5: target critics L1 on [s', a'], L2 (+ the target values' partials; the
   // row tile's last job runs the TD head: y = r + (1 - d) gamma min(tv1, tv2),
   // dv = 2 (v - y) (MSE) or clip(v - y, +-delta) (opt-in Huber), per-sample loss) ----
-  const int nt = twin ? 2 : 1;
   for (int layer = 1; layer <= 2; ++layer) {
     const int CT = layer == 1 ? CT1 : CT2, per = RTT * CT;
     for (int j = b; j < nt * per; j += G) {
@@ -1601,12 +1618,11 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
   }
 
   // ---- P8: critics dW1 / db1 + Adam, Adam of the rest (+ Polyak on policy steps); the
-  // rest in chunks sized so the phase's jobs fill the grid ----
-  int p8_jobs;
+  // rest in chunks sized so the phase's jobs fill the grid. Stage 1: dW1 / db1 only ----
   {
     const int n_w1 = CTW1;                      // one in-feature tile (C <= 64)
     const int rest = c1.P - c1.w2, chunk = adam_chunk(rest, max(1, (G - nt * n_w1) / nt));
-    const int n_ad = (rest + chunk - 1) / chunk;
+    const int n_ad = stage == 1 ? 0 : (rest + chunk - 1) / chunk;
     const int per = n_w1 + n_ad;
     p8_jobs = nt * per;
     for (int j = b; j < nt * per; j += G) {
@@ -1617,8 +1633,8 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
       float* grad = ci ? p.g_critic2 : p.g_critic1;
       float* tgt = pol ? (ci ? p.target_critic2.theta : p.target_critic1.theta) : nullptr;
       if (q < n_w1) {
-        dw_job(sa_dense, slots, dz_buf(ws.dh1(ci), H1), C, H1, 0,
-               q * NTW * kCols, NTW, B, grad, n.w1, n.b1, n, adam_opt(opt, tgt, p.tau));
+        dw_job(sa_dense, slots, dz_buf(ws.dh1(ci), H1), C, H1, 0, q * NTW * kCols, NTW, B,
+               grad, n.w1, n.b1, n, stage == 1 ? no_adam() : adam_opt(opt, tgt, p.tau));
       } else {
         const int lo = n.w2 + (q - n_w1) * chunk, hi = min(n.P, lo + chunk);
         const float omb1 = 1.0f - opt.beta1, omb2 = 1.0f - opt.beta2;
@@ -1627,8 +1643,31 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
       __syncthreads();
     }
   }
+  }  // stage <= 1
 
-  if (pol) {
+  // ---- stage 2, P8': the critics' Keras Adam (+ Polyak of their targets on policy steps)
+  // from the all-reduced gradients, every parameter in chunks that fill the grid ----
+  if (stage == 2) {
+    // (a launch with no later barrier opens with one: every block reads the step counters
+    // before block 0 bumps them)
+    if (!pol && !grid_sync(y, s_flag, G)) return;
+    c1.alpha = adam_alpha(p.critic1.lr, p.critic1.beta1, p.critic1.beta2, step_c1 + 1);
+    if (twin) c2.alpha = adam_alpha(p.critic2.lr, p.critic2.beta1, p.critic2.beta2, step_c2 + 1);
+    const int chunk = adam_chunk(c1.P, max(1, G / nt)), per = (c1.P + chunk - 1) / chunk;
+    p8_jobs = nt * per;
+    for (int j = b; j < nt * per; j += G) {
+      const int ci = j / per, q = j % per;
+      const Net n = ci ? c2 : c1;
+      const XaTdNet& opt = ci ? p.critic2 : p.critic1;
+      float* tgt = pol ? (ci ? p.target_critic2.theta : p.target_critic1.theta) : nullptr;
+      const int lo = q * chunk, hi = min(n.P, lo + chunk);
+      adam_range(n, ci ? p.g_critic2 : p.g_critic1, lo, hi, 1.0f - opt.beta1, 1.0f - opt.beta2,
+                 opt.eps, tgt, p.tau, p.critic_grad_scale);
+      __syncthreads();
+    }
+  }
+
+  if (pol && (stage == 0 || stage == 2)) {
     if (!grid_sync(y, s_flag, p8_jobs)) return;
     // ---- P9 / P10: critic 1 (updated) on [s, pi(s)] ----
     const XSrc spa = xcat(xsrc(p.out_s, S, S, false, true), ws.pa, A, A, false, true);
@@ -1696,16 +1735,17 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
       };
       if (!grid_sync(y, s_flag, n_dx + n_dw2 + n_dw3, no_preb(), alpha_ac)) return;
     }
-    // ---- P14: actor dW1 / db1 + Adam + Polyak, Adam + Polyak of the rest ----
+    // ---- P14: actor dW1 / db1 + Adam + Polyak, Adam + Polyak of the rest (stage 2:
+    // dW1 / db1 only) ----
     {
       const int rest = ac.P - ac.w2, chunk = adam_chunk(rest, max(1, G - CTW1));
-      const int n_ad = (rest + chunk - 1) / chunk;
+      const int n_ad = stage == 2 ? 0 : (rest + chunk - 1) / chunk;
       for (int j = b; j < CTW1 + n_ad; j += G) {
         if (tid == 0) td3_dslot = (b == 0 && j == b) ? 8 * (int)y.n : -1;
         if (j < CTW1) {
           dw_job(xsrc(p.out_s, S, S, false, true), slots, dz_buf(ws.dh1a, H1), S, H1, 0,
                  j * NTW * kCols, NTW, B, p.g_actor, ac.w1, ac.b1, ac,
-                 adam_opt(p.actor, p.target_actor.theta, p.tau));
+                 stage == 2 ? no_adam() : adam_opt(p.actor, p.target_actor.theta, p.tau));
         } else {
           const int lo = ac.w2 + (j - CTW1) * chunk, hi = min(ac.P, lo + chunk);
           const float omb1 = 1.0f - p.actor.beta1, omb2 = 1.0f - p.actor.beta2;
@@ -1716,13 +1756,30 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
     }
   }
 
+  // ---- stage 3: the actor's Keras Adam + Polyak of the target actor from the all-reduced
+  // gradient (scaled: the ranks' -mean Q gradients are summed) ----
+  if (stage == 3) {
+    if (!grid_sync(y, s_flag, G)) return;  // (every block has read the actor's step)
+    ac.alpha = adam_alpha(p.actor.lr, p.actor.beta1, p.actor.beta2, step_ac + 1);
+    const int chunk = adam_chunk(ac.P, G), per = (ac.P + chunk - 1) / chunk;
+    for (int j = b; j < per; j += G) {
+      const int lo = j * chunk, hi = min(ac.P, lo + chunk);
+      adam_range(ac, p.g_actor, lo, hi, 1.0f - p.actor.beta1, 1.0f - p.actor.beta2, p.actor.eps,
+                 p.target_actor.theta, p.tau, p.actor_grad_scale);
+      __syncthreads();
+    }
+  }
+
   // the step counters, the noise counter and the next launch's barrier base: every block
-  // read them before its first barrier, which block 0 has passed
+  // read them before its first barrier, which block 0 has passed and which every block
+  // arrives at
   if (b == 0 && tid == 0) {
-    *p.critic1.step += 1;
-    if (twin) *p.critic2.step += 1;
-    if (pol) *p.actor.step += 1;
-    if (p.smooth && p.rng_counter) *p.rng_counter += 1ull;
+    if (stage == 0 || stage == 2) {
+      *p.critic1.step += 1;
+      if (twin) *p.critic2.step += 1;
+    }
+    if (pol && (stage == 0 || stage == 3)) *p.actor.step += 1;
+    if (p.smooth && p.rng_counter && stage <= 1) *p.rng_counter += 1ull;
     *ws.base = y.target;
     *ws.epoch = y.epoch;
     // block 0's end (the last phase's tail may run on)
@@ -1738,6 +1795,7 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
 // start) ----
 __global__ __launch_bounds__(256) void td3_act_kernel(XaTd3ActArgs p) {
   __shared__ int s_flag;
+  if (p.status && *(const volatile int*)p.status != 0) return;  // (as td3_update_kernel)
   const int G = gridDim.x, b = blockIdx.x, tid = threadIdx.x;
   const int n = p.n, S = p.obs_dim, A = p.act_dim, H1 = p.h1, H2 = p.h2;
   const Ws ws = carve(p.workspace, n, H1, H2, A);
@@ -1830,6 +1888,9 @@ extern "C" int xa_td3_update(const XaTd3UpdateArgs* p, void* stream) {
                "xa_td3_update: missing buffers");
   XA_CHECK_ARG(a.workspace_bytes >= carve(nullptr, a.batch, a.h1, a.h2, a.act_dim).total,
                "xa_td3_update: workspace too small");
+  XA_CHECK_ARG(a.stage >= 0 && a.stage <= 3 && (a.stage != 3 || (a.actor_update && a.g_actor)),
+               "xa_td3_update: stage must be 0 (whole step) or 1 / 2 / 3 (data parallel; "
+               "stage 3 needs actor_update)");
   int cus = 256, dev = 0;
   if (hipGetDevice(&dev) == hipSuccess)
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);

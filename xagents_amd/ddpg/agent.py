@@ -231,6 +231,9 @@ class DDPG(OffPolicy):
         for gradient_step in range(int(gradient_steps)):
             self.replay.upload_slots(self.replay.sample_slots())
             policy = gradient_step % self.policy_delay == 0
+            if fused is not None and self.distributed:
+                self._fused_dp_step(policy)
+                continue
             if fused is not None:
                 self._run_phase('fused_actor' if policy else 'fused',
                                 lambda p=policy: self._fused_step(p))
@@ -242,7 +245,7 @@ class DDPG(OffPolicy):
     # ---- the fused gradient step (xa_td3_update) -------------------------------------
     def _fused_ok(self):
         import os
-        if os.environ.get('XA_TD3_FUSED', '1') == '0' or self.distributed:
+        if os.environ.get('XA_TD3_FUSED', '1') == '0':
             return False
         if self.replay.obs_t != torch.float32 or self.replay.act_t != torch.float32:
             return False
@@ -275,8 +278,8 @@ class DDPG(OffPolicy):
 
     def _fused_args(self):
         """The launch arguments of xa_td3_update (built once), or None when the fused step
-        does not apply (data parallel: the gradients are all-reduced between the backward
-        and Adam; other model shapes)."""
+        does not apply (other model shapes). Data parallel runs it in stages with the
+        gradient all-reduces between them (_fused_dp_step)."""
         if '_fused' in self.__dict__:
             return self.__dict__['_fused']
         from xagents_amd import _lib
@@ -330,6 +333,12 @@ class DDPG(OffPolicy):
             import os
             a.n_blocks = int(os.environ.get('XA_TD3_BLOCKS', '0'))
             a.status = self._fused_status.data_ptr()
+            a.stage = 0
+            # data parallel: the critics' losses are batch sums (Keras MSE + minimize), the
+            # actor's a batch mean, so Adam takes the rank sum of the critics' gradients as
+            # it is and the actor's over world (the executor path's _reduce_grad scales)
+            a.critic_grad_scale = 1.0
+            a.actor_grad_scale = kernels._f32(1.0 / self.world_size)
             fused = a
         self.__dict__['_fused'] = fused
         return fused
@@ -348,6 +357,33 @@ class DDPG(OffPolicy):
         if ev is not None:
             ev[1].record()
             self.fused_timing.append((bool(policy),) + ev)
+
+    def _fused_dp_step(self, policy):
+        """One data-parallel gradient step on the fused kernel: stage 1 (critics' raw
+        gradients) -> all-reduce of both critics' gradients (one flat buffer) -> stage 2
+        (critics' Adam [+ Polyak]; on policy steps the actor's raw gradient through the
+        updated critic 1) -> all-reduce of the actor's gradient -> stage 3 (actor Adam +
+        Polyak). Three launches and one or two collectives instead of the executor's ~90
+        launches (ddpg/agent.py:129-147 on the union of the ranks' batches)."""
+        import torch.distributed as dist
+        a = self._fused
+        a.actor_update = int(policy)
+        try:
+            a.stage = 1
+            call('xa_td3_update', ctypes.byref(a), stream())
+            dist.all_reduce(self._g_critics_flat())
+            a.stage = 2
+            call('xa_td3_update', ctypes.byref(a), stream())
+            if policy:
+                dist.all_reduce(self.g_actor)
+                a.stage = 3
+                call('xa_td3_update', ctypes.byref(a), stream())
+        finally:
+            a.stage = 0
+
+    def _g_critics_flat(self):
+        """The buffer holding every critic's raw gradient (one all-reduce per step)."""
+        return self.g_critic
 
     def fused_step_flops(self, policy=True):
         """Algorithmic FLOPs of one fused gradient step (2 M N K per GEMM): the forwards of

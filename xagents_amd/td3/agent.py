@@ -55,9 +55,17 @@ class TD3(DDPG):
         B = self.batch_size
         self.ex_critic2 = LayerExecutor(self.critic2, B)
         self.ex_target_critic2 = LayerExecutor(self.target_critic2, B)
-        self.g_critic2 = torch.zeros(self.critic2.n_params, dtype=torch.float32,
-                                     device=self.device)
+        # both critics' raw gradients in one buffer (critic 2's part 256-B aligned for the
+        # fused kernel's 16-B accesses): one all-reduce per data-parallel gradient step
+        P1, P2 = self.critic.n_params, self.critic2.n_params
+        off = (P1 + 63) // 64 * 64
+        self._g_crit_all = torch.zeros(off + P2, dtype=torch.float32, device=self.device)
+        self.g_critic = self._g_crit_all[:P1]
+        self.g_critic2 = self._g_crit_all[off:]
         self._sync_params(self.critic2, self.target_critic2)
+
+    def _g_critics_flat(self):
+        return self._g_crit_all
 
     def get_step_actions(self):
         """actor(s), no exploration noise (td3/agent.py:57-64): one launch (xa_td3_act with
