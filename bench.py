@@ -321,8 +321,11 @@ def fused_td3_roofline(agent, launches=10):
         rows = list(agent.fused_timing)
     finally:
         agent.fused_timing = None
-    ms = float(np.mean([e0.elapsed_time(e1) for _, e0, e1 in rows]))
-    pol = sum(p for p, _, _ in rows) / len(rows)
+    # one gradient step's launch time: one launch, or the sum of its data-parallel stages
+    # (the collectives between them excluded)
+    ms = float(np.mean([sum(e0.elapsed_time(e1) for e0, e1 in evs) for _, evs in rows]))
+    pol = sum(p for p, _ in rows) / len(rows)
+    stages = len(rows[-1][1])
     flops = pol * agent.fused_step_flops(True) + (1 - pol) * agent.fused_step_flops(False)
     nbytes = pol * fused_td3_bytes(agent, True) + (1 - pol) * fused_td3_bytes(agent, False)
     tf = flops / (ms * 1e-3) / 1e12
@@ -341,7 +344,9 @@ def fused_td3_roofline(agent, launches=10):
                     f'sampled batch gathered and written) / the mean of {len(rows)} '
                     f'event-timed launches; MFMA basis (2 M N K FLOP of every GEMM) under '
                     f'"mfma"; latency-bound (5 / 10 grid barriers between the 6 / 11 phases '
-                    f'of a critic / policy step)'}
+                    f'of a critic / policy step)' + (
+                        f'; data parallel: the {stages} stage launches of a step summed, the '
+                        f'gradient all-reduces between them excluded' if stages > 1 else '')}
 
 
 def fused_td3_bytes(agent, policy=True):
@@ -512,6 +517,11 @@ def run_secondary(args, config, world, rank, device, steps, warmup, cpu_seconds,
                                     'per-buffer batch 1 (100 // 64), gradient_steps 1 '
                                     '(BASELINE configs[4])',
                         'n_envs_per_gpu': n, 'parallelism': f'dp{world}',
+                        'gradient_step': (
+                            'layer executor' if agent._fused_args() is None else
+                            'xa_td3_update, one persistent launch' if world == 1 else
+                            'xa_td3_update in 3 stages: critic gradients, all-reduce, critic '
+                            'Adam + actor gradient, all-reduce, actor Adam'),
                         # the value depends on how often episodes end: every finished
                         # episode of the union triggers gradient_steps gradient steps
                         # (ddpg/agent.py:157-166)

@@ -412,6 +412,27 @@ typedef struct XaGemmArgs {
 } XaGemmArgs;
 
 int xa_gemm(const XaGemmArgs* args, void* stream);
+
+/* Keras Adam (training_ops ApplyAdam, utils/common.py:476) applied in a weight-gradient
+ * GEMM's epilogue: DQN's update minimizes the MSE with no gradient clip
+ * (dqn/agent.py:158-171), so a layer's Adam step needs only its own gradient and the
+ * gradient never has to leave the GEMM. Element (m, n) of C, at offset e = m ldc + n, is
+ * the gradient of the parameter theta[e] with moments m[e], v[e]; t = *step (already
+ * bumped, xa_adam_step_bump), g scaled by grad_scale. */
+typedef struct XaAdamApply {
+  float* theta;
+  float* m;
+  float* v;
+  const int* step;
+  float lr, beta1, beta2, eps, grad_scale;
+} XaAdamApply;
+
+/* C = A B as xa_gemm (the 64 x 64 kernel, one K split: a dense layer's [W; b] weight
+ * gradient X^T dZ with a_ones_row, A m-major, B n-major f32, N and ldc multiples of 4, no
+ * bias / activation / gate / beta), then the Adam step of every element in the epilogue;
+ * args->c (optional, may be NULL) receives the raw gradient. Replaces the dense layer's
+ * share of tape.gradient + Adam.apply_gradients (dqn/agent.py:170-171). */
+int xa_gemm_adam(const XaGemmArgs* args, const XaAdamApply* adam, void* stream);
 int xa_gemm_splits(int M, int N, int K);
 /* the kernel shape xa_gemm picks for a tile-path GEMM with `splits` K splits (0 = the
  * 64 x 64 kernel, the only one that takes a_ones_row) */

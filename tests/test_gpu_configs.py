@@ -42,6 +42,10 @@ def test_c3_dqn_32_envs_rb1_1m_batch_64(device):
     agent = DQN(envs, model, bufs, double=True, seed=55, quiet=True, epsilon_start=0.5,
                 epsilon_end=0.02)
     assert agent.replay.states.shape[:2] == (n, 31250) and agent.batch_size == 64
+    # the 37632 x 512 layer's Keras Adam runs in its weight-gradient GEMM (xa_gemm_adam);
+    # its raw gradient is written too on request, so the whole gradient is checked
+    assert agent._fused_adam_layers()[0], 'the dense layer should take the fused Adam'
+    agent.write_raw_grad = True
     agent.fill_buffers()
     assert [b.current_size for b in bufs] == [64] * n
     th0, tt0 = _np(model.theta), _np(agent.target_model.theta)

@@ -175,3 +175,48 @@ def test_dqn_captured_learner_matches_eager(device, double):
                     agent.model.optimizer.m.cpu().numpy(), agent.b_act.cpu().numpy()])
     for a, b in zip(*out):
         np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize('double', [False, True])
+def test_fused_dense_adam_is_bit_identical(device, double):
+    """The dense 37632 x 512 layer's Keras Adam inside its weight-gradient GEMM
+    (xa_gemm_adam, the gradient never written) against the unfused path (gradient GEMM ->
+    xa_clip_adam over every parameter): the same arithmetic per element, so parameters,
+    moments and step counters are bit-identical after 3 chained train steps, and so are the
+    raw gradients when the fused path is asked to write them."""
+    import random
+    from xagents_amd import DQN
+    from xagents_amd.envs import create_envs
+    from xagents_amd.utils.common import create_buffers, create_model
+    out = []
+    for fused, raw in ((False, False), (True, False), (True, True)):
+        envs = create_envs('PongNoFrameskip-v4', 2, device=device, seed=3)
+        model = create_model(envs, 'dqn', 'model', seed=9, device=device,
+                             optimizer_kwargs=dict(learning_rate=1e-3))
+        bufs = create_buffers('dqn', 40, 4, 2, initial_size=20)
+        np.random.seed(1)
+        random.seed(1)
+        agent = DQN(envs, model, bufs, double=double, seed=2, quiet=True, epsilon_start=0.0,
+                    epsilon_end=0.0, gamma=0.99)
+        if not fused:
+            agent.__dict__['_fused_adam'] = ([], [])
+        else:
+            assert agent._fused_adam_layers()[0]
+        agent.write_raw_grad = raw
+        agent.fill_buffers()
+        grads = []
+        for _ in range(3):
+            agent.at_step_start()
+            agent.train_step()
+            agent.at_step_end()
+            grads.append(agent.grad.clone())
+        torch.cuda.synchronize()
+        opt = model.optimizer
+        out.append(([t.cpu().numpy() for t in (model.theta, opt.m, opt.v, opt.iterations)],
+                    [g.cpu().numpy() for g in grads]))
+    for x, y in zip(out[0][0], out[1][0]):
+        np.testing.assert_array_equal(x, y)
+    for x, y in zip(out[0][0], out[2][0]):
+        np.testing.assert_array_equal(x, y)
+    for x, y in zip(out[0][1], out[2][1]):
+        np.testing.assert_array_equal(x, y)

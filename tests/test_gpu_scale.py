@@ -67,6 +67,9 @@ def _dqn(device, double, huber=None):
     random.seed(1)
     agent = DQN(envs, model, bufs, double=double, seed=2, quiet=True, epsilon_start=0.0,
                 epsilon_end=0.0, gamma=0.99, huber_delta=huber)
+    # the dense layer's Adam runs inside its weight-gradient GEMM: ask it for the raw
+    # gradient too, so the whole gradient is checked
+    agent.write_raw_grad = True
     agent.fill_buffers()
     agent.target_model.theta.mul_(0.97)  # the target differs, so double DQN matters
     return agent

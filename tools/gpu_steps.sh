@@ -64,6 +64,7 @@ for step in "$@"; do
     configs) run_pytest configs 400 tests/test_gpu_configs.py ;;
     td3) run_pytest td3 600 tests/test_gpu_td3.py tests/test_gpu_scale.py tests/test_gpu_configs.py::test_c5_td3_64_envs_rb2 ;;
     td3dp) run_pytest td3dp 450 tests/test_gpu_dp.py -k td3 ;;
+    dqn) run_pytest dqn 400 tests/test_gpu_dqn.py tests/test_gpu_scale.py -k "dqn" tests/test_gpu_configs.py::test_c3_dqn_32_envs_rb1_1m_batch_64 ;;
     td3time)
       # wall time per gradient step on the product build, per-phase barrier times on the
       # trace build (tools/diag_lib/libxa_td3trace.so: tools/build_variant.py td3trace
@@ -79,7 +80,14 @@ for step in "$@"; do
       XA_BENCH_SHARED_DEVICE=1 HSA_ENABLE_IPC_MODE_LEGACY=0 run c4w2 400 python -m torch.distributed.run \
         --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py \
         --config c4 --gpus 2 --steps 2 --warmup 1 --cpu-baseline-seconds 0 ;;
-    c4dp) run_pytest c4dp 600 tests/test_gpu_dp.py -k cnn tests/test_gpu_configs.py::test_c4_ppo_cnn_128_env_shard ;;
+    c4dp) run_pytest c4dp 600 -s tests/test_gpu_dp.py -k cnn tests/test_gpu_configs.py::test_c4_ppo_cnn_128_env_shard ;;
+    c5w2)
+      # W = 2 rehearsal of the C5 data-parallel bench with both ranks on the one GPU (gloo;
+      # the fused TD3 stages on 96 workgroups per rank so both ranks' launches are resident)
+      XA_TD3_BLOCKS=96 XA_BENCH_SHARED_DEVICE=1 HSA_ENABLE_IPC_MODE_LEGACY=0 run c5w2 300 \
+        python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+        --master-port 29518 bench.py --config c5 --gpus 2 --steps 20 --warmup 3 \
+        --cpu-baseline-seconds 0 ;;
     smoke) run smoke 180 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 300 python bench.py --steps 20 --warmup 5 ;;
     ab)

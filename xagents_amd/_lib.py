@@ -197,6 +197,14 @@ class XaGemmArgs(Structure):
     ]
 
 
+class XaAdamApply(Structure):
+    _fields_ = [
+        ('theta', c_void_p), ('m', c_void_p), ('v', c_void_p), ('step', c_void_p),
+        ('lr', c_float), ('beta1', c_float), ('beta2', c_float), ('eps', c_float),
+        ('grad_scale', c_float),
+    ]
+
+
 class XaAtariStepArgs(Structure):
     _fields_ = [
         ('n_envs', c_int), ('t_raw', c_int), ('height', c_int), ('width', c_int),
@@ -399,6 +407,7 @@ _SIGNATURES = {
     'xa_ppo_update_workspace_bytes': (ctypes.c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int]),
     'xa_ppo_update': (c_int, [POINTER(XaPpoUpdateArgs), c_void_p]),
     'xa_gemm': (c_int, [POINTER(XaGemmArgs), c_void_p]),
+    'xa_gemm_adam': (c_int, [POINTER(XaGemmArgs), POINTER(XaAdamApply), c_void_p]),
     'xa_gemm_splits': (c_int, [c_int, c_int, c_int]),
     'xa_gemm_shape': (c_int, [c_int, c_int, c_int, c_int]),
     'xa_gemm_workspace_floats': (ctypes.c_size_t, [c_int, c_int, c_int, c_int]),

@@ -23,6 +23,7 @@
 #include <algorithm>
 
 #include "../../include/xagents_hip.h"
+#include "xa_adam.hpp"
 #include "xa_common.hpp"
 
 namespace {
@@ -65,6 +66,7 @@ struct XaGemmK {
   XaGemmArgs g;
   int vec_a, vec_b;
   int ones_m;  // a_ones_row: the constant-one row (M - 1), else -1 (gemm_kernel only)
+  XaAdamApply ad;  // (gemm_kernel<..., ADAM = true> only) the epilogue's Adam step
 };
 
 template <bool U8>
@@ -88,7 +90,9 @@ XA_DEV void zero4(float* d) { d[0] = d[1] = d[2] = d[3] = 0.0f; }
 
 // A_KMAJOR: g(k) is unit stride (loader reads along k); otherwise along m.
 // B_NMAJOR: b_ns == 1 (loader reads along n); otherwise along k.
-template <bool A_KMAJOR, bool B_NMAJOR, bool A_U8>
+// ADAM: the epilogue applies Keras Adam to the parameters the tile is the gradient of
+// (xa_gemm_adam; one K split, no bias / activation / gate / beta, N % 4 == 0)
+template <bool A_KMAJOR, bool B_NMAJOR, bool A_U8, bool ADAM = false>
 __global__ __launch_bounds__(256) void gemm_kernel(XaGemmK kargs) {
   const XaGemmArgs& g = kargs.g;
   const bool vec_a = kargs.vec_a, vec_b = kargs.vec_b;
@@ -231,6 +235,58 @@ __global__ __launch_bounds__(256) void gemm_kernel(XaGemmK kargs) {
     }
   }
 
+  if (ADAM) {
+    // the tile through LDS (the main loop ended on a barrier), then thread t owns row t / 4,
+    // columns 16 (t % 4) .. + 15 as four float4 groups: every gradient / parameter / moment
+    // access a 16-B load or store, all of a thread's loads in flight before its updates
+    constexpr int LDT = BN + 4;
+    __shared__ __attribute__((aligned(16))) float T[BM * LDT];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          T[(wm * 32 + i * 16 + 4 * (lane >> 4) + r) * LDT + wn * 32 + j * 16 + (lane & 15)] =
+              acc[i][j][r];
+    __syncthreads();
+    const XaAdamApply& ad = kargs.ad;
+    const float alpha = adam_alpha(ad.lr, ad.beta1, ad.beta2, *ad.step);
+    const float omb1 = 1.0f - ad.beta1, omb2 = 1.0f - ad.beta2;
+    const int row = tid >> 2, m = m0 + row, cb = 16 * (tid & 3);
+    if (m < g.M) {
+      f32x4 gq[4], th[4], mq[4], vq[4];
+      int64_t e[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int n = n0 + cb + 4 * q;
+        e[q] = n < g.N ? (int64_t)m * g.ldc + n : -1;
+        gq[q] = *reinterpret_cast<const f32x4*>(&T[row * LDT + cb + 4 * q]);
+        if (e[q] >= 0) {
+          th[q] = *reinterpret_cast<const f32x4*>(ad.theta + e[q]);
+          mq[q] = *reinterpret_cast<const f32x4*>(ad.m + e[q]);
+          vq[q] = *reinterpret_cast<const f32x4*>(ad.v + e[q]);
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (e[q] < 0) continue;
+        if (g.c) *reinterpret_cast<f32x4*>(g.c + e[q]) = gq[q];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          float t = th[q][c], mm = mq[q][c], vv = vq[q][c];
+          adam_elem(gq[q][c] * ad.grad_scale, t, mm, vv, alpha, omb1, omb2, ad.eps);
+          th[q][c] = t;
+          mq[q][c] = mm;
+          vq[q][c] = vv;
+        }
+        *reinterpret_cast<f32x4*>(ad.theta + e[q]) = th[q];
+        *reinterpret_cast<f32x4*>(ad.m + e[q]) = mq[q];
+        *reinterpret_cast<f32x4*>(ad.v + e[q]) = vq[q];
+      }
+    }
+    return;
+  }
   // D(row = 4 (lane >> 4) + r, col = lane & 15) of each 16 x 16 tile
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -1344,11 +1400,18 @@ extern "C" int xa_gemm_splits(int M, int N, int K) {
     // actually launched (it drops to 64x64 below 256 K per split) covers ~1024 workgroups
     // (tools/gemm_split_sweep.py: 336 x 512 x 37632 187 us at 128 splits vs 227 us at 256;
     // 4096 x 512 x 37632 1209 us at 8 vs 1246 us at 16)
+    // ... or, on the 128 x 128 kernel, 512 of its 4x-larger workgroups when the next
+    // doubling would drop to the 64 x 64 kernel (128 x 512 x 37632, the double-DQN online
+    // forward: 62.9 us at 128 splits vs 67.6 us at 256, profiles/r04an_split_sweep.txt)
     int s = 1;
     while (s < 4096 && kt / (s * 2) >= 8) {
       int tm, tn;
-      tile_dims(pick_shape(M, N, K, (K + s - 1) / s, false), tm, tn);
-      if ((int64_t)((M + tm - 1) / tm) * ((N + tn - 1) / tn) * s >= 1024) break;
+      const int sh = pick_shape(M, N, K, (K + s - 1) / s, false);
+      tile_dims(sh, tm, tn);
+      const int64_t wg = (int64_t)((M + tm - 1) / tm) * ((N + tn - 1) / tn) * s;
+      if (wg >= 1024) break;
+      if (sh == 22 && wg >= 512 && pick_shape(M, N, K, (K + 2 * s - 1) / (2 * s), false) == 0)
+        break;
       s *= 2;
     }
     return s;
@@ -1365,6 +1428,48 @@ extern "C" int xa_gemm_shape(int M, int N, int K, int splits) {
 
 extern "C" size_t xa_gemm_workspace_floats(int M, int N, int K, int splits) {
   return splits > 1 ? (size_t)splits * M * N : 0;
+}
+
+// the kernel argument: the public args + the host's vectorisation verdicts (XaGemmK)
+static XaGemmK kernel_args(const XaGemmArgs& g) {
+  const bool ak = g.a_pk == 1 && g.a_rk == 1, bn = g.b_ns == 1, u8 = g.a_u8 != 0;
+  XaGemmK kg{g, 0, 0, g.a_ones_row ? g.M - 1 : -1, XaAdamApply{}};
+  const int m_real = g.a_ones_row ? g.M - 1 : g.M;
+  if (g.a != nullptr && ((uintptr_t)g.a & (u8 ? 3 : 15)) == 0) {
+    const bool rows4 = g.a_rm % 4 == 0 && (g.a_pm == 1 || g.a_sm % 4 == 0);
+    const bool cols4 = g.a_rk % 4 == 0 && (g.a_pk == 1 || g.a_sk % 4 == 0);
+    kg.vec_a = ak ? (g.K % 4 == 0 && rows4)
+                  : (g.a_pm == 1 && g.a_rm == 1 && m_real % 4 == 0 && cols4);
+  }
+  if (((uintptr_t)g.b & 15) == 0)
+    kg.vec_b = bn ? (g.b_ks % 4 == 0 && g.N % 4 == 0)
+                  : (g.b_ks == 1 && g.b_ns % 4 == 0 && g.K % 4 == 0);
+  return kg;
+}
+
+extern "C" int xa_gemm_adam(const XaGemmArgs* p, const XaAdamApply* ad, void* stream) {
+  XA_CHECK_ARG(p != nullptr && ad != nullptr, "xa_gemm_adam: null args");
+  const XaGemmArgs& g = *p;
+  XA_CHECK_ARG(g.M > 0 && g.N > 0 && g.K > 0 && g.a && g.b, "xa_gemm_adam: bad sizes or operands");
+  XA_CHECK_ARG(g.a_pm > 0 && g.a_pk > 0 && (int64_t)g.M * g.N < (1ll << 31),
+               "xa_gemm_adam: bad groups or M * N >= 2^31");
+  const bool ak = g.a_pk == 1 && g.a_rk == 1, bn = g.b_ns == 1;
+  XA_CHECK_ARG(g.splits == 1 && !g.bias && g.act == XA_ACT_NONE && !g.gate && !g.beta &&
+                   !g.a_u8 && !ak && bn && g.N % 4 == 0 && g.ldc % 4 == 0 &&
+                   pick_shape(g.M, g.N, g.K, g.K, false) == 0,
+               "xa_gemm_adam: needs one K split, no bias / activation / gate / beta, f32 m-major "
+               "A, n-major B, N and ldc multiples of 4 and the 64 x 64 kernel");
+  XA_CHECK_ARG(ad->theta && ad->m && ad->v && ad->step &&
+                   (((uintptr_t)ad->theta | (uintptr_t)ad->m | (uintptr_t)ad->v |
+                     (uintptr_t)g.c) & 15) == 0,
+               "xa_gemm_adam: theta / m / v / step missing or not 16-B aligned");
+  XaGemmK kg = kernel_args(g);
+  kg.ad = *ad;
+  dim3 grid((g.M + BM - 1) / BM, (g.N + BN - 1) / BN, 1);
+  hipLaunchKernelGGL((gemm_kernel<false, true, false, true>), grid, dim3(256), 0,
+                     (hipStream_t)stream, kg);
+  XA_CHECK_LAUNCH("xa_gemm_adam");
+  return 0;
 }
 
 extern "C" int xa_gemm(const XaGemmArgs* p, void* stream) {
@@ -1441,17 +1546,7 @@ extern "C" int xa_gemm(const XaGemmArgs* p, void* stream) {
   XA_CHECK_ARG(!g.a_ones_row || (shape == 0 && g.a != nullptr && g.M >= 2),
                "xa_gemm: a_ones_row needs the 64 x 64 kernel (xa_gemm_shape == 0), A and M >= 2 "
                "(got shape %d, M %d)", shape, g.M);
-  XaGemmK kg{g, 0, 0, g.a_ones_row ? g.M - 1 : -1};
-  const int m_real = g.a_ones_row ? g.M - 1 : g.M;
-  if (g.a != nullptr && ((uintptr_t)g.a & (u8 ? 3 : 15)) == 0) {
-    const bool rows4 = g.a_rm % 4 == 0 && (g.a_pm == 1 || g.a_sm % 4 == 0);
-    const bool cols4 = g.a_rk % 4 == 0 && (g.a_pk == 1 || g.a_sk % 4 == 0);
-    kg.vec_a = ak ? (g.K % 4 == 0 && rows4)
-                  : (g.a_pm == 1 && g.a_rm == 1 && m_real % 4 == 0 && cols4);
-  }
-  if (((uintptr_t)g.b & 15) == 0)
-    kg.vec_b = bn ? (g.b_ks % 4 == 0 && g.N % 4 == 0)
-                  : (g.b_ks == 1 && g.b_ns % 4 == 0 && g.K % 4 == 0);
+  const XaGemmK kg = kernel_args(g);
   if (shape == 2) {
     hipLaunchKernelGGL(colsum_kernel, dim3(1, (g.N + 63) / 64, g.splits), dim3(256), 0, s, g);
   } else if (shape == 1) {

@@ -343,12 +343,19 @@ class DDPG(OffPolicy):
         self.__dict__['_fused'] = fused
         return fused
 
-    # (bench) a list to collect (policy step, start event, end event) of eager fused launches
+    # (bench) a list to collect (policy step, [(start, end) events of its launches]) of
+    # eager fused gradient steps
     fused_timing = None
 
     def _fused_step(self, policy):
         a = self._fused
         a.actor_update = int(policy)
+        self._fused_launch(a)
+        self._fused_timing_row(policy)
+
+    def _fused_launch(self, a):
+        """One xa_td3_update launch (event-timed into self._launch_events when the bench
+        collects fused_timing)."""
         ev = None
         if self.fused_timing is not None:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -356,7 +363,12 @@ class DDPG(OffPolicy):
         call('xa_td3_update', ctypes.byref(a), stream())
         if ev is not None:
             ev[1].record()
-            self.fused_timing.append((bool(policy),) + ev)
+            self.__dict__.setdefault('_launch_events', []).append(ev)
+
+    def _fused_timing_row(self, policy):
+        """(bench) file this gradient step's launch events: (policy, [(start, end), ...])."""
+        if self.fused_timing is not None:
+            self.fused_timing.append((bool(policy), self.__dict__.pop('_launch_events', [])))
 
     def _fused_dp_step(self, policy):
         """One data-parallel gradient step on the fused kernel: stage 1 (critics' raw
@@ -370,16 +382,17 @@ class DDPG(OffPolicy):
         a.actor_update = int(policy)
         try:
             a.stage = 1
-            call('xa_td3_update', ctypes.byref(a), stream())
+            self._fused_launch(a)
             dist.all_reduce(self._g_critics_flat())
             a.stage = 2
-            call('xa_td3_update', ctypes.byref(a), stream())
+            self._fused_launch(a)
             if policy:
                 dist.all_reduce(self.g_actor)
                 a.stage = 3
-                call('xa_td3_update', ctypes.byref(a), stream())
+                self._fused_launch(a)
         finally:
             a.stage = 0
+        self._fused_timing_row(policy)
 
     def _g_critics_flat(self):
         """The buffer holding every critic's raw gradient (one all-reduce per step)."""

@@ -10,7 +10,9 @@ train_step (dqn/agent.py:182-197), all on device except the reference's host RNG
     get_targets          Q(s), [Q(s')], Qt(s') (one online pass over [s; s'] when double)
                          -> xa_dqn_td_grad (TD target, MSE gradient of the batch sum)
     update_gradients     CNN backward (xa_gemm / xa_conv1d_input_grad) -> Keras Adam
-                         (no gradient clipping, optimizer.minimize) via xa_clip_adam
+                         (no gradient clipping, optimizer.minimize): the 37632 x 512 dense
+                         layer's step inside its weight-gradient GEMM (xa_gemm_adam, no
+                         gradient round trip), the other layers' via xa_clip_adam
 at_step_end: hard target copy when steps % target_sync_steps == 0 (xa_polyak, tau 1).
 """
 import numpy as np
@@ -20,7 +22,7 @@ from xagents_amd import kernels
 from xagents_amd._lib import call, stream
 from xagents_amd.base import OffPolicy
 from xagents_amd.envs import Discrete
-from xagents_amd.layers import LayerExecutor
+from xagents_amd.layers import LayerExecutor, adam_apply
 
 
 class DQN(OffPolicy):
@@ -142,8 +144,50 @@ class DQN(OffPolicy):
              self.n_actions, kernels._f32(self.gamma), kernels._f32(self.huber_delta or 0.0),
              self.dq.data_ptr(), self.td_loss.data_ptr(), stream())
 
+    # the raw gradient of the dense layers whose Adam step runs inside their weight-gradient
+    # GEMM is written to self.grad only on request (the raw-gradient parity tests)
+    write_raw_grad = False
+
+    def _fused_adam_layers(self):
+        """Dense layers (the 37632 x 512 one of the NatureCNN cfg) whose Keras Adam step runs
+        in the weight-gradient GEMM's epilogue (xa_gemm_adam): the reference's DQN update has
+        no gradient clip (dqn/agent.py:158-171), so a layer's step needs only its own
+        gradient. Not when data parallel (the gradient is all-reduced before Adam)."""
+        if '_fused_adam' not in self.__dict__:
+            import os
+            ex, layers = self.ex_online, self.model.layers
+            fl = [] if self.distributed or os.environ.get('XA_DQN_FUSED_ADAM', '1') == '0' else [
+                i for i, l in enumerate(layers)
+                if l.kind == 'dense' and l.in_features * l.units >= (1 << 20) and
+                ex.adam_fusable(i, self.batch_size)]
+            # the parameter ranges the remaining Adam launches cover
+            rest, lo = [], 0
+            for i in fl:
+                w0, b0 = ex.offsets[i]
+                if w0 > lo:
+                    rest.append((lo, w0))
+                lo = b0 + layers[i].units
+            if lo < self.model.n_params:
+                rest.append((lo, self.model.n_params))
+            self._fused_adam = (fl, rest)
+        return self._fused_adam
+
     def _apply(self):
         opt = self.model.optimizer
+        fl, rest = self._fused_adam_layers()
+        if fl:
+            # t += 1 first: the fused epilogues read it; the dense layers' Adam runs inside
+            # the backward, the rest of the parameters in one launch per range
+            th, m, v = self.model.theta, opt.m, opt.v
+            call('xa_adam_step_bump', opt.iterations.data_ptr(), stream())
+            spec = {i: (adam_apply(th, m, v, opt.iterations, opt, self.ex_online.offsets[i][0]),
+                        self.write_raw_grad) for i in fl}
+            self.ex_online.backward([self.dq], self.grad, batch=self.batch_size, adam=spec)
+            for lo, hi in rest:
+                kernels.clip_adam(th[lo:hi], m[lo:hi], v[lo:hi], self.grad[lo:hi],
+                                  opt.iterations, opt.learning_rate, opt.beta_1, opt.beta_2,
+                                  opt.epsilon, clip_norm=0.0, workspace=self.adam_ws)
+            return
         self.ex_online.backward([self.dq], self.grad, batch=self.batch_size)
         scale = self._reduce_grad(self.grad)
         call('xa_adam_step_bump', opt.iterations.data_ptr(), stream())

@@ -20,7 +20,8 @@ import os
 import torch
 
 from xagents_amd import _lib
-from xagents_amd._lib import XA_ACT_NONE, XA_ACT_RELU, XA_ACT_TANH, XaGemmArgs, call, stream
+from xagents_amd._lib import (XA_ACT_NONE, XA_ACT_RELU, XA_ACT_TANH, XaAdamApply, XaGemmArgs,
+                              call, stream)
 
 _FORCE = int(os.environ.get('XA_GEMM_FORCE', '0'))
 _ACTS = {None: XA_ACT_NONE, 'linear': XA_ACT_NONE, 'relu': XA_ACT_RELU, 'tanh': XA_ACT_TANH}
@@ -32,11 +33,9 @@ def act_code(name):
     return _ACTS[name]
 
 
-def gemm(M, N, K, a, b, c, *, a_u8=False, a_m=(1, 0, 0), a_k=(1, 1, 0), b_ks, b_ns,
-         ldc, bias=None, act=XA_ACT_NONE, gate=None, ld_gate=0, beta=False, workspace=None,
-         splits=None, force_small=False, a_ones_row=False):
-    """C = [C +] act(A B + bias) * [gate > 0] with A(m, k) = a[f(m) + g(k)],
-    f / g given as (group, row stride, in-group stride) triples (gemm.hip)."""
+def _gemm_args(M, N, K, a, b, c, *, a_u8=False, a_m=(1, 0, 0), a_k=(1, 1, 0), b_ks, b_ns,
+               ldc, bias=None, act=XA_ACT_NONE, gate=None, ld_gate=0, beta=False, workspace=None,
+               splits=None, force_small=False, a_ones_row=False):
     lib = _lib.load()
     s = splits if splits is not None else lib.xa_gemm_splits(M, N, K)
     g = XaGemmArgs()
@@ -62,7 +61,33 @@ def gemm(M, N, K, a, b, c, *, a_u8=False, a_m=(1, 0, 0), a_k=(1, 1, 0), b_ks, b_
     # XA_GEMM_FORCE (diagnostic A/B): a force_small code for every call that passes none
     g.force_small = int(force_small) or _FORCE
     g.a_ones_row = int(a_ones_row)
-    call('xa_gemm', ctypes_ref(g), stream())
+    return g
+
+
+def gemm(M, N, K, a, b, c, **kw):
+    """C = [C +] act(A B + bias) * [gate > 0] with A(m, k) = a[f(m) + g(k)],
+    f / g given as (group, row stride, in-group stride) triples (gemm.hip)."""
+    call('xa_gemm', ctypes_ref(_gemm_args(M, N, K, a, b, c, **kw)), stream())
+
+
+def gemm_adam(M, N, K, a, b, c, adam, **kw):
+    """A weight-gradient GEMM with Keras Adam in its epilogue (xa_gemm_adam): `adam` an
+    XaAdamApply over the parameters C is the gradient of; c = None writes no gradient."""
+    call('xa_gemm_adam', ctypes_ref(_gemm_args(M, N, K, a, b, c, splits=1, **kw)),
+         ctypes_ref(adam), stream())
+
+
+def adam_apply(theta, m, v, step, opt, offset, grad_scale=1.0):
+    """XaAdamApply of the parameters theta[offset:] (Keras Adam state m, v, iterations step
+    of optimizer `opt`)."""
+    from xagents_amd.kernels import _f32
+    ad = XaAdamApply()
+    ad.theta, ad.m, ad.v = theta.data_ptr() + 4 * offset, m.data_ptr() + 4 * offset, \
+        v.data_ptr() + 4 * offset
+    ad.step = step.data_ptr()
+    ad.lr, ad.beta1, ad.beta2 = _f32(opt.learning_rate), _f32(opt.beta_1), _f32(opt.beta_2)
+    ad.eps, ad.grad_scale = _f32(opt.epsilon), _f32(grad_scale)
+    return ad
 
 
 @functools.lru_cache(maxsize=None)
@@ -133,6 +158,21 @@ class LayerExecutor:
         if name == 'softmax' and i in self.model.outputs:
             return XA_ACT_NONE
         return act_code(name)
+
+    def adam_fusable(self, i, batch=None):
+        """Dense layer i's [W; b] weight gradient can carry its Adam step (xa_gemm_adam: the
+        64 x 64 kernel with the bias as a constant-one row, one K split, f32 input, 16-B
+        aligned rows)."""
+        l = self.layers[i]
+        if l.kind != 'dense' or self._src_layer(i) == -1:
+            return False
+        Bb = batch or self.B
+        w0, b0 = self.offsets[i]
+        lib = _lib.load()
+        n_in, n_out = l.in_features, l.units
+        return (b0 == w0 + n_in * n_out and w0 % 4 == 0 and n_out % 4 == 0 and
+                lib.xa_gemm_splits(n_in + 1, n_out, Bb) == 1 and
+                lib.xa_gemm_shape(n_in + 1, n_out, Bb, 1) == 0)
 
     def _dgrad_ok(self, i):
         """xa_conv1d_dgrad needs F % 4 == 0 and a 16-byte aligned kernel slice."""
@@ -266,7 +306,7 @@ class LayerExecutor:
 
     # ---- backward ----------------------------------------------------------------
     def backward(self, d_outputs, grad, batch=None, dinput=None, accumulate=False,
-                 on_grad=None):
+                 on_grad=None, adam=None):
         """d_outputs: gradients w.r.t. the output layers (model.outputs order, [b, n]).
         Writes the flat parameter gradient into `grad` (Keras variable order; None skips
         the parameter gradients) and, if given, d(loss)/d(input) into `dinput` [b, in]
@@ -276,8 +316,12 @@ class LayerExecutor:
         minibatches). `on_grad(w0)` is called once the launches writing a layer's weight
         and bias gradient (flat offsets w0 ..) are queued, before its input gradient's:
         layers finish in reverse order, so grad[w0:] is then final (the hook of the
-        data-parallel path's bucketed all-reduce)."""
+        data-parallel path's bucketed all-reduce). `adam` {layer index: (XaAdamApply,
+        keep_grad)}: those dense layers (adam_fusable) take their Keras Adam step inside the
+        weight-gradient GEMM (xa_gemm_adam) after their input gradient has read W; `grad`
+        then receives their raw gradient only when keep_grad."""
         Bb = batch or self.B
+        assert adam is None or not accumulate
         assert Bb <= self.B
         tp = self.model.theta.data_ptr()
         gp = grad.data_ptr() if grad is not None else None
@@ -318,19 +362,34 @@ class LayerExecutor:
                 gate_j = self.outs[j].data_ptr()
             if l.kind == 'dense':
                 n_in, n_out = l.in_features, l.units
-                if gp is not None:
-                    # dW = X^T dZ ; db = 1^T dZ -- one GEMM into the contiguous [W; b] block
-                    # (b0 = w0 + n_in n_out) when the 64 x 64 kernel takes it
-                    fold = fold_bias_ok(n_in, n_out, Bb) and b0 == w0 + n_in * n_out
-                    gemm(n_in + fold, n_out, Bb, src.data_ptr(), d.data_ptr(), gp + 4 * w0,
-                         a_u8=src_u8, a_m=(1, 1, 0), a_k=(1, n_in, 0), b_ks=n_out, b_ns=1,
-                         ldc=n_out, beta=accumulate, workspace=self.workspace, a_ones_row=fold)
-                    if not fold:
-                        gemm(1, n_out, Bb, None, d.data_ptr(), gp + 4 * b0, a_m=(1, 0, 0),
-                             a_k=(1, 0, 0), b_ks=n_out, b_ns=1, ldc=n_out, beta=accumulate,
-                             workspace=self.workspace)
-                    if on_grad is not None:
+                fused = adam is not None and i in adam
+
+                def wgrad():
+                    if fused:
+                        # [W; b] gradient + the layer's Adam step in one launch; reads W's
+                        # old value nowhere (the input gradient below ran first)
+                        ad, keep = adam[i]
+                        gemm_adam(n_in + 1, n_out, Bb, src.data_ptr(), d.data_ptr(),
+                                  gp + 4 * w0 if keep else None, ad, a_m=(1, 1, 0),
+                                  a_k=(1, n_in, 0), b_ks=n_out, b_ns=1, ldc=n_out,
+                                  a_ones_row=True)
+                    elif gp is not None:
+                        # dW = X^T dZ ; db = 1^T dZ -- one GEMM into the contiguous [W; b]
+                        # block (b0 = w0 + n_in n_out) when the 64 x 64 kernel takes it
+                        fold = fold_bias_ok(n_in, n_out, Bb) and b0 == w0 + n_in * n_out
+                        gemm(n_in + fold, n_out, Bb, src.data_ptr(), d.data_ptr(), gp + 4 * w0,
+                             a_u8=src_u8, a_m=(1, 1, 0), a_k=(1, n_in, 0), b_ks=n_out, b_ns=1,
+                             ldc=n_out, beta=accumulate, workspace=self.workspace,
+                             a_ones_row=fold)
+                        if not fold:
+                            gemm(1, n_out, Bb, None, d.data_ptr(), gp + 4 * b0, a_m=(1, 0, 0),
+                                 a_k=(1, 0, 0), b_ks=n_out, b_ns=1, ldc=n_out, beta=accumulate,
+                                 workspace=self.workspace)
+                    if gp is not None and on_grad is not None:
                         on_grad(w0)
+
+                if not fused:
+                    wgrad()
                 if j == -1 and dinput is not None:
                     gemm(Bb, n_in, n_out, d.data_ptr(), tp + 4 * w0, dinput.data_ptr(),
                          a_m=(1, n_out, 0), b_ks=1, b_ns=n_out, ldc=n_in,
@@ -344,6 +403,8 @@ class LayerExecutor:
                          beta=written[j], workspace=self.workspace)
                     self._timing_end(ev, f'dense dX {Bb}x{n_in}x{n_out}', 2.0 * Bb * n_in * n_out)
                     written[j] = True
+                if fused:
+                    wgrad()
             else:
                 rows, Win, P, C = self._conv_dims(i, Bb)
                 k, s, F = l.size, l.stride, l.filters
