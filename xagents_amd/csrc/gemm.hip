@@ -196,6 +196,25 @@ __global__ __launch_bounds__(256) void gemm_kernel(XaGemmK kargs) {
     }
   };
 
+  // ADAM: the parameters / moments of this thread's four float4 groups of the tile (group
+  // f = tid + 256 q: row f / 16, columns 4 (f % 16) .. + 3; a wave's load covers 4 rows x
+  // 256 contiguous bytes) are loaded before the main loop, in flight under the GEMM
+  f32x4 pth[ADAM ? 4 : 1], pm[ADAM ? 4 : 1], pv[ADAM ? 4 : 1];
+  int64_t pe[ADAM ? 4 : 1];
+  if (ADAM) {
+    const XaAdamApply& ad = kargs.ad;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int f = tid + 256 * q, m = m0 + (f >> 4), n = n0 + 4 * (f & 15);
+      pe[q] = (m < g.M && n < g.N) ? (int64_t)m * g.ldc + n : -1;
+      if (pe[q] >= 0) {
+        pth[q] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(ad.theta + pe[q]));
+        pm[q] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(ad.m + pe[q]));
+        pv[q] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(ad.v + pe[q]));
+      }
+    }
+  }
+
   f32x4 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -236,54 +255,43 @@ __global__ __launch_bounds__(256) void gemm_kernel(XaGemmK kargs) {
   }
 
   if (ADAM) {
-    // the tile through LDS (the main loop ended on a barrier), then thread t owns row t / 4,
-    // columns 16 (t % 4) .. + 15 as four float4 groups: every gradient / parameter / moment
-    // access a 16-B load or store, all of a thread's loads in flight before its updates
+    // the tile through LDS (the main loop ended on a barrier; the tile reuses the operand
+    // stash), then every thread updates its four prefetched float4 groups
     constexpr int LDT = BN + 4;
-    __shared__ __attribute__((aligned(16))) float T[BM * LDT];
+    static_assert(2 * BK * LDA >= BM * LDT / 2 && 2 * BK * LDB >= BM * LDT / 2, "tile stash");
+    float* const Ta = &As[0][0];  // rows 0 .. 31 (both stash buffers, contiguous)
+    float* const Tb = &Bs[0][0];  // rows 32 .. 63
+    auto T = [&](int r, int c) -> float& {
+      return r < BM / 2 ? Ta[r * LDT + c] : Tb[(r - BM / 2) * LDT + c];
+    };
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          T[(wm * 32 + i * 16 + 4 * (lane >> 4) + r) * LDT + wn * 32 + j * 16 + (lane & 15)] =
-              acc[i][j][r];
+          T(wm * 32 + i * 16 + 4 * (lane >> 4) + r, wn * 32 + j * 16 + (lane & 15)) = acc[i][j][r];
     __syncthreads();
     const XaAdamApply& ad = kargs.ad;
     const float alpha = adam_alpha(ad.lr, ad.beta1, ad.beta2, *ad.step);
     const float omb1 = 1.0f - ad.beta1, omb2 = 1.0f - ad.beta2;
-    const int row = tid >> 2, m = m0 + row, cb = 16 * (tid & 3);
-    if (m < g.M) {
-      f32x4 gq[4], th[4], mq[4], vq[4];
-      int64_t e[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int n = n0 + cb + 4 * q;
-        e[q] = n < g.N ? (int64_t)m * g.ldc + n : -1;
-        gq[q] = *reinterpret_cast<const f32x4*>(&T[row * LDT + cb + 4 * q]);
-        if (e[q] >= 0) {
-          th[q] = *reinterpret_cast<const f32x4*>(ad.theta + e[q]);
-          mq[q] = *reinterpret_cast<const f32x4*>(ad.m + e[q]);
-          vq[q] = *reinterpret_cast<const f32x4*>(ad.v + e[q]);
-        }
+    for (int q = 0; q < 4; ++q) {
+      if (pe[q] < 0) continue;
+      const int f = tid + 256 * q, r = f >> 4, c = 4 * (f & 15);
+      const f32x4 gq = *reinterpret_cast<const f32x4*>(&T(r, c));
+      if (g.c) __builtin_nontemporal_store(gq, reinterpret_cast<f32x4*>(g.c + pe[q]));
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float t = pth[q][u], mm = pm[q][u], vv = pv[q][u];
+        adam_elem(gq[u] * ad.grad_scale, t, mm, vv, alpha, omb1, omb2, ad.eps);
+        pth[q][u] = t;
+        pm[q][u] = mm;
+        pv[q][u] = vv;
       }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        if (e[q] < 0) continue;
-        if (g.c) *reinterpret_cast<f32x4*>(g.c + e[q]) = gq[q];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          float t = th[q][c], mm = mq[q][c], vv = vq[q][c];
-          adam_elem(gq[q][c] * ad.grad_scale, t, mm, vv, alpha, omb1, omb2, ad.eps);
-          th[q][c] = t;
-          mq[q][c] = mm;
-          vq[q][c] = vv;
-        }
-        *reinterpret_cast<f32x4*>(ad.theta + e[q]) = th[q];
-        *reinterpret_cast<f32x4*>(ad.m + e[q]) = mq[q];
-        *reinterpret_cast<f32x4*>(ad.v + e[q]) = vq[q];
-      }
+      __builtin_nontemporal_store(pth[q], reinterpret_cast<f32x4*>(ad.theta + pe[q]));
+      __builtin_nontemporal_store(pm[q], reinterpret_cast<f32x4*>(ad.m + pe[q]));
+      __builtin_nontemporal_store(pv[q], reinterpret_cast<f32x4*>(ad.v + pe[q]));
     }
     return;
   }

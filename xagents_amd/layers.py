@@ -82,6 +82,7 @@ def adam_apply(theta, m, v, step, opt, offset, grad_scale=1.0):
     of optimizer `opt`)."""
     from xagents_amd.kernels import _f32
     ad = XaAdamApply()
+    offset = int(offset)
     ad.theta, ad.m, ad.v = theta.data_ptr() + 4 * offset, m.data_ptr() + 4 * offset, \
         v.data_ptr() + 4 * offset
     ad.step = step.data_ptr()
