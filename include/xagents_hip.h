@@ -403,9 +403,8 @@ typedef struct XaGemmArgs {
   int64_t ld_gate;
   int beta;
   int force_small; /* 1: always the 64 x 64 small-tile kernel; 2: the generic tile kernels,
-                     never the small-M ones; 3: every path but the few-column row-dot one;
-                     4: the default paths plus the split-K few-row forward (tests / A-B
-                     timing) */
+                     never the small-M ones; 3: every path but the few-column row-dot one
+                     (tests / A-B timing) */
   int a_ones_row; /* 1: A's last row (m = M - 1) is all ones and is not read: a weight
                      gradient X^T dZ and its bias gradient 1^T dZ as ONE GEMM into the
                      contiguous [W; b] block (the 64 x 64 kernel only: xa_gemm_shape) */

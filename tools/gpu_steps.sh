@@ -16,9 +16,6 @@
 #   pmc      FETCH_SIZE / WRITE_SIZE passes per shape (tools/gpurun_pmc_shapes.sh)
 #   c3 c4 c5 acer trpo   secondary bench lines
 #   pollab   persistent-update poll sleep variants: bench + C2 FETCH_SIZE
-#   rsplit   two-wave rollout step variant: bit-exact tests on it + bench A/B
-#   ringab   small-M dX ring-depth variants vs product, K = 128 / 256 small-M timings
-#   fwd      split-K dense forward: GEMM tests + timing vs the generic kernels
 #   c2g      C2 bench lines at update grids $C2_GS (XA_PPO_MAX_BLOCKS)
 #   profc3   rocprofv3 kernel trace of the C3 bench + per-(kernel, grid) summary
 #   gemm     GEMM tests, small-M timings, PMC passes on the dense dX GEMM
@@ -157,39 +154,12 @@ for step in "$@"; do
         > $R/gpurun_out/${T}_td3pmc2.log 2>&1) || exit 4
       python tools/pmc_summary.py td3_update $(find gpurun_out/${T}_td3pmc2 -name "*counter_collection.csv") \
         >> gpurun_out/${T}_td3pmc.txt ;;
-    ringab)
-      # small-M dense dX: B-ring depth variants (tools/diag_lib/libxa_ring*.so, built with
-      # tools/build_variant.py ringN -DXA_SMALLM_RING=N --src gemm) vs the product, and the
-      # K = 128 shapes
-      run ring_base 120 python tools/bench_smallm.py 64 336
-      for L in tools/diag_lib/libxa_ring*.so; do
-        n=$(basename $L .so); n=${n#libxa_}
-        XA_LIB=$L run ring_$n 120 python tools/bench_smallm.py 64 336
-      done
-      XA_SMALLM_K=128 run smallk128 120 python tools/bench_smallm.py 16 64 128
-      XA_SMALLM_K=256 run smallk256 120 python tools/bench_smallm.py 16 64 128 ;;
-    sdiag)
-      # small-M dense dX: no-MFMA / no-HBM-stream diagnostic variants (XA_SMALLM_DIAG 1 / 2)
-      run sdiag_base 120 python tools/bench_smallm.py 4 16 64
-      for v in 1 2; do
-        XA_LIB=tools/diag_lib/libxa_sdiag$v.so run sdiag_$v 120 python tools/bench_smallm.py 4 16 64
-      done ;;
     smallm)
       run_pytest smallmtest 300 tests/test_gpu_layers.py -k "small_m or dense_input or layer_executor"
       run smallm 120 python tools/bench_smallm.py 16 64 128 336 ;;
     dprel) run dprel 700 bash tools/cnn_dp_rel.sh ;;
     sweep) run sweep 400 python tools/gemm_split_sweep.py 32 64 128 ;;
     c3host) run c3host 300 python tools/c3_host_profile.py ;;
-    sstamps) XA_LIB=tools/diag_lib/libxa_sdiag3.so run sstamps 120 python tools/smallm_stamps.py 64 16 ;;
-    rsplit)
-      # the two-wave rollout step (XA_ROLL_SPLIT=1 variant, tools/diag_lib/libxa_rsplit.so):
-      # bit-exact vs the oracle (the rollout tests on the variant), then bench A/B
-      XA_LIB=tools/diag_lib/libxa_rsplit.so run_pytest rsplit_test 200 tests/test_gpu_kernels.py -k rollout
-      B="python bench.py --steps 40 --warmup 5 --cpu-baseline-seconds 0 --no-secondary"
-      run rs_base1 200 $B
-      run rs_split 200 $B --lib tools/diag_lib/libxa_rsplit.so
-      run rs_base2 200 $B
-      python tools/bench_brief.py gpurun_out/${T}_rs_*.out ;;
     pollab)
       # poll-round sleep of the persistent update (XA_POLL_SLEEP variants,
       # tools/diag_lib/libxa_poll*.so) vs the product: bench lines (16-env + C2) and the
@@ -212,15 +182,6 @@ for step in "$@"; do
         python tools/pmc_summary.py ppo_update $(find gpurun_out/${T}_pollpmc_$n -name "*counter_collection.csv") \
           >> gpurun_out/${T}_pollpmc.txt
         find gpurun_out/${T}_pollpmc_$n -name "*counter_collection.csv" -delete
-      done ;;
-    fwd)
-      # the split-K dense forward vs the generic tile kernels; its GEMM tests
-      run_pytest fwdtest 300 tests/test_gpu_layers.py -k "plain_bias_relu or layer_executor"
-      run fwd 120 python tools/bench_fwd.py 16 32 64
-      for L in tools/diag_lib/libxa_fsring*.so; do
-        [ -e "$L" ] || continue
-        n=$(basename $L .so); n=${n#libxa_}
-        XA_LIB=$L run fwd_$n 120 python tools/bench_fwd.py 32 64
       done ;;
     c3) run c3 300 python bench.py --config c3 --steps 30 --warmup 5 ;;
     c4) run c4 400 python bench.py --config c4 --steps 4 --warmup 1 ;;

@@ -550,17 +550,8 @@ __global__ __launch_bounds__(256) void gemm_tile_kernel(XaGemmK kargs) {
 // ---------------------------------------------------------------------------
 constexpr int RS_KP = 4, RS_UPR = 2;
 // rounds the B ring spans (the round loop is unrolled by this): 2 keeps 2 CH - 1 chunks of B
-// in flight per wave
-// XA_SMALLM_DIAG (diagnostic builds only): 1 = VALU FMAs instead of the MFMAs, 2 = every
-// round streams round 0's B rows again (cache hits, no HBM stream), 3 = shader-clock stamps
-// per wave and round into the split workspace (tools/smallm_stamps.py)
-#ifndef XA_SMALLM_DIAG
-#define XA_SMALLM_DIAG 0
-#endif
-#ifndef XA_SMALLM_RING
-#define XA_SMALLM_RING 2
-#endif
-constexpr int RS_NR = XA_SMALLM_RING;
+// in flight per wave (3 / 4 measured slower, profiles/r04m_smallm_ring_and_k_ab.txt)
+constexpr int RS_NR = 2;
 // Resident-A row layout, conflict-free for the lane groups of ds_read_b128 (MI355X_MICROARCH.md
 // LDS table: 4 groups of 16 lanes, bank (a/4) mod 64): element k = 16 b + 4 q + j of a row
 // sits at q SR + 4 b + j -- the k quads q = 0..3 of every 16-k step in 4 sub-rows whose
@@ -585,19 +576,6 @@ __global__ __launch_bounds__(512) void gemm_smallm_res_kernel(XaGemmArgs g, int 
   const int M = g.M, N = g.N;
   const int units = (N + 15) / 16;
   const float* af = static_cast<const float*>(g.a);
-#if XA_SMALLM_DIAG == 3
-  // diagnostic: lane 0 of every wave stamps the shader clock into the split workspace (u64
-  // slot (block 8 + wave) 16 + i: 0 start, 1 after the A prologue, 2 + 2 r / 3 + 2 r round r's
-  // chunk loop done / round done)
-  auto stamp = [&](int i) {
-    if (lane == 0 && g.partials)
-      ((__attribute__((address_space(1))) unsigned long long*)g.partials)[(blockIdx.x * 8 + w) * 16 + i] =
-          __builtin_amdgcn_s_memtime();
-  };
-#else
-  auto stamp = [](int) {};
-#endif
-  stamp(0);
   // A into LDS: every thread's PER float4 loads issued before the B ring's first loads and
   // before any LDS write (a load -> wait -> write loop serialised PER round trips: 17.5k
   // cycles of prologue at M = 64, profiles/r04y_smallm_stamps.txt)
@@ -627,11 +605,7 @@ __global__ __launch_bounds__(512) void gemm_smallm_res_kernel(XaGemmArgs g, int 
   constexpr int RS_R = RS_NR * CH;
   f32x4 rb[RS_R][2];
   auto load_b = [&](int gi, f32x4 (&dst)[2]) {
-#if XA_SMALLM_DIAG == 2
-    const float* p = brow(0) + 32 * (gi % CH);  // diagnostic: every round re-reads round 0 (L2 hits)
-#else
     const float* p = brow(gi / CH) + 32 * (gi % CH);
-#endif
     dst[0] = *reinterpret_cast<const f32x4*>(p);
     dst[1] = *reinterpret_cast<const f32x4*>(p + 16);
   };
@@ -640,7 +614,6 @@ __global__ __launch_bounds__(512) void gemm_smallm_res_kernel(XaGemmArgs g, int 
 #pragma unroll
   for (int i = 0; i < PER; ++i) *reinterpret_cast<f32x4*>(As + va_at[i]) = va[i];
   __syncthreads();
-  stamp(1);
   const float* as = As + li * PA + lq * SR + kp * (KQ / 4);  // k = kp KQ + 16 b' + 4 lq + j
   const int mt_fin = min(kp, MT - 1);  // the m tile this wave finishes (kp < MT)
   for (int r0 = 0; r0 < rounds; r0 += RS_NR) {
@@ -680,15 +653,10 @@ __global__ __launch_bounds__(512) void gemm_smallm_res_kernel(XaGemmArgs g, int 
             for (int j = 0; j < 4; ++j)
 #pragma unroll
               for (int mt = 0; mt < MT; ++mt)
-#if XA_SMALLM_DIAG == 1
-                acc[mt][j] = fmaf(aq[mt][j], rb[u][h][j], acc[mt][j]);  // diagnostic: no MFMA
-#else
                 acc[mt] = mfma4(aq[mt][j], rb[u][h][j], acc[mt]);
-#endif
           }
         }
       }
-      if (r < 7) stamp(2 + 2 * r);
       // slot of part p in m tile mt's scratch: p, or p - 1 past the finishing wave mt
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
@@ -722,7 +690,6 @@ __global__ __launch_bounds__(512) void gemm_smallm_res_kernel(XaGemmArgs g, int 
         }
       }
       __syncthreads();
-      if (r < 7) stamp(3 + 2 * r);
     }
   }
 }
@@ -805,118 +772,6 @@ bool rowdot_ok(const XaGemmArgs& g) {
          g.a_pk == 1 && g.a_rk == 1 && g.N <= RD_MAXN && g.K <= 4096 && g.M <= (1 << 20);
 }
 
-// ---------------------------------------------------------------------------
-// Few-row dense forward over a huge K (the NatureCNN dense layer's forward at the acting
-// batch: 17 <= M <= 32, N = 512, K = 37632; see fwd_splitk_ok): split z of the S workgroups owns the k range
-// [z per, (z + 1) per) for EVERY output -- its A slice [M][per] in LDS (read once), its W
-// rows streamed from HBM straight into MFMA operand registers (lane (q, i) loads
-// W[k + q][16 ct + i] for the wave's 8 column tiles, an 8-deep register ring of k steps), the
-// whole M x N partial in the wave's accumulators; the partial goes to the split workspace and
-// the split reduce sums the S partials in split order (+ bias / activation / beta). Each W
-// byte is read once and A once per split, against the tile kernels' N / 64 re-reads of A and
-// K / 256-row splits (traffic-bound there).
-// 256 threads = 4 waves; wave w owns column tiles [w NT / 4, (w + 1) NT / 4) of every row tile.
-// ---------------------------------------------------------------------------
-#ifndef XA_FS_RING
-#define XA_FS_RING 8
-#endif
-constexpr int FS_RING = XA_FS_RING;  // k steps of W in the register ring per wave (7 in flight:
-                                     // ~56 KB per CU, the W stream's latency x rate)
-constexpr int FS_CTW = 8;    // column tiles per wave (N <= 512)
-template <int MT>
-__global__ __launch_bounds__(256) void gemm_fwd_splitk_kernel(XaGemmArgs g, int per, int stride) {
-  extern __shared__ __attribute__((aligned(16))) float As[];  // [16 MT][stride]
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int i = lane & 15, q = lane >> 4;
-  const int M = g.M, N = g.N, K = g.K;
-  const int z = blockIdx.x, k0 = z * per, kn = max(0, min(K, k0 + per) - k0);
-  const int NT = N >> 4, ctw = NT >> 2, ct0 = w * ctw;  // (N % 64 == 0: whole tiles per wave)
-  const float* af = static_cast<const float*>(g.a);
-  // A slice into LDS (zeros past M and past the split's k range), float4 per thread
-  for (int e = tid; e < 16 * MT * (per >> 2); e += 256) {
-    const int r = e / (per >> 2), kk = 4 * (e - r * (per >> 2));
-    f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
-    if (r < M && kk < kn) {
-      const float* src = af + (int64_t)r * g.a_rm + k0 + kk;
-      if (kk + 4 <= kn) {
-        v = *reinterpret_cast<const f32x4*>(src);
-      } else {
-        for (int u = 0; u < 4; ++u) v[u] = kk + u < kn ? src[u] : 0.0f;
-      }
-    }
-    *reinterpret_cast<f32x4*>(As + r * stride + kk) = v;
-  }
-  // W ring: step s = rows k0 + 4 s .. + 3, this lane's row k0 + 4 s + q, its 8 columns
-  const int steps = (kn + 3) >> 2;
-  const float* bq = g.b + (int64_t)(k0 + q) * g.b_ks + 16 * ct0 + i;
-  auto load_w = [&](int st, float (&dst)[FS_CTW]) {
-    const bool ok = st < steps && 4 * st + q < kn;
-    const float* p = bq + (int64_t)(4 * st) * g.b_ks;
-#pragma unroll
-    for (int c = 0; c < FS_CTW; ++c) dst[c] = (ok && c < ctw) ? p[16 * c] : 0.0f;
-  };
-  float rb[FS_RING][FS_CTW];
-#pragma unroll
-  for (int u = 0; u < FS_RING - 1; ++u) load_w(u, rb[u]);
-  __syncthreads();
-  f32x4 acc[MT][FS_CTW];
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-    for (int c = 0; c < FS_CTW; ++c) acc[mt][c] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-  const float* ar = As + i * stride + q;
-  for (int s0 = 0; s0 < steps; s0 += FS_RING) {
-#pragma unroll
-    for (int u = 0; u < FS_RING; ++u) {
-      // (the slot the previous step freed takes step s + FS_RING - 1)
-      load_w(s0 + u + FS_RING - 1, rb[(u + FS_RING - 1) % FS_RING]);
-      __builtin_amdgcn_sched_barrier(0);
-      if (s0 + u < steps) {
-        float av[MT];
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) av[mt] = ar[mt * 16 * stride + 4 * (s0 + u)];
-#pragma unroll
-        for (int c = 0; c < FS_CTW; ++c)
-#pragma unroll
-          for (int mt = 0; mt < MT; ++mt)
-            if (c < ctw) acc[mt][c] = mfma4(av[mt], rb[u][c], acc[mt][c]);
-      }
-    }
-  }
-  // the partial: lane holds D[4 (lane >> 4) + r][lane & 15] of each tile
-  float* part = g.partials + (int64_t)z * M * N;
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-    for (int c = 0; c < FS_CTW; ++c) {
-      if (c >= ctw) continue;
-      const int n = 16 * (ct0 + c) + i;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = 16 * mt + 4 * q + r;
-        if (m < M) part[(int64_t)m * N + n] = acc[mt][c][r];
-      }
-    }
-}
-
-// the split-K forward path's contract (and its per-split k range, a multiple of 4). Measured
-// (profiles/r04v_fwd_splitk_ab.txt, 256 splits, N 512, K 37632): M = 32 34.0 us vs 37.7 us on
-// the tile kernels; M = 64 48.7 vs 40.5 us -- the 256 whole-width partials (M N 4 B each,
-// written and read back by the split reduce) cost more than the A re-reads they save -- and
-// M = 16 98.6 vs 35.1 us (the one-row-tile form); ring depth 4 / 8 / 12 within noise. So
-// 17 <= M <= 32 only, and only on request (force_small = 4): its summation order differs
-// from the tile kernels' that every other batch size takes, and the data-parallel test
-// compares a rank's 32-row minibatch forward with the union's 64-row one -- theta deviated
-// 1.2e-4 from the union step with this path vs 1.3e-6 without (profiles/r04ad_dprel.txt),
-// for a 3.7-us gain at C3's acting batch.
-bool fwd_splitk_ok(const XaGemmArgs& g) {
-  return g.force_small == 4 && !g.a_ones_row && g.a != nullptr && !g.a_u8 && g.a_pm == 1 && g.a_pk == 1 &&
-         g.a_rk == 1 && g.a_rm % 4 == 0 && ((uintptr_t)g.a & 15) == 0 && g.b_ns == 1 &&
-         g.M > 16 && g.M <= 32 && g.N % 64 == 0 && g.N <= 64 * FS_CTW && g.K >= 8192 &&
-         !g.gate &&
-         g.splits > 1 && g.partials != nullptr;
-}
-int fwd_splitk_per(const XaGemmArgs& g) { return ((g.K + g.splits - 1) / g.splits + 3) & ~3; }
 
 // ---------------------------------------------------------------------------
 // Skinny path (weight gradients of the convs: M, N <= 256 / 64, K = rows x positions in
@@ -1520,29 +1375,6 @@ extern "C" int xa_gemm(const XaGemmArgs* p, void* stream) {
   if (rowdot_ok(g)) {
     hipLaunchKernelGGL(gemm_rowdot_kernel, dim3((g.M + 3) / 4), dim3(256), 0, s, g);
     XA_CHECK_LAUNCH("xa_gemm (row dot)");
-    return 0;
-  }
-  if (fwd_splitk_ok(g) && fwd_splitk_per(g) <= 512) {
-    const int per = fwd_splitk_per(g), stride = per % 8 == 0 ? per + 4 : per;
-    const int mt = (g.M + 15) / 16;
-    const size_t lds = sizeof(float) * (size_t)16 * (mt <= 1 ? 1 : mt <= 2 ? 2 : 4) * stride;
-    if (mt <= 1)
-      hipLaunchKernelGGL(gemm_fwd_splitk_kernel<1>, dim3(g.splits), dim3(256), lds, s, g, per, stride);
-    else if (mt <= 2)
-      hipLaunchKernelGGL(gemm_fwd_splitk_kernel<2>, dim3(g.splits), dim3(256), lds, s, g, per, stride);
-    else
-      hipLaunchKernelGGL(gemm_fwd_splitk_kernel<4>, dim3(g.splits), dim3(256), lds, s, g, per, stride);
-    XA_CHECK_LAUNCH("xa_gemm (split-K forward)");
-    const int64_t total = (int64_t)g.M * g.N;
-    if (total <= 65536 && g.splits >= 64) {
-      hipLaunchKernelGGL(gemm_split_reduce_wide_kernel, dim3((int)((total + 63) / 64)),
-                         dim3(1024), 0, s, g, g.splits);
-    } else {
-      const int64_t want = (total + 255) / 256;
-      const int blocks = (int)(want < 4096 ? want : 4096);
-      hipLaunchKernelGGL(gemm_split_reduce_kernel, dim3(blocks), dim3(256), 0, s, g, g.splits);
-    }
-    XA_CHECK_LAUNCH("xa_gemm (split reduce)");
     return 0;
   }
   dim3 grid((g.M + BM - 1) / BM, (g.N + BN - 1) / BN, g.splits);

@@ -35,12 +35,6 @@ constexpr int kWaves = 4;       // xa_mlp_forward: waves (samples in flight) per
 #define XA_ROLLOUT_WAVES 1
 #endif
 constexpr int kRollWaves = XA_ROLLOUT_WAVES;
-// (measurement variant) XA_ROLL_SPLIT=1: the replay env's step on TWO waves of one
-// workgroup -- layer-2 chains 0-3 on the env's wave, chains 4-7 on a helper wave that hands
-// its half-sum over LDS each step (the same association as one wave: bit-exact)
-#ifndef XA_ROLL_SPLIT
-#define XA_ROLL_SPLIT 0
-#endif
 constexpr int kFusedMaxT = 1024;
 constexpr int kChunk = 64;     // steps per chunk (one per lane in the chunk pass)
 constexpr int kHS = H + 4;     // h2 chunk-buffer row stride (floats): conflict-free row reads
@@ -124,29 +118,6 @@ struct LaneMlp {
     }
     return xa_tanhf((((c01.x + c01.y) + (c23.x + c23.y)) + ((c45.x + c45.y) + (c67.x + c67.y))) +
                     b2);
-  }
-
-  // split step: layer 1 into this wave's LDS row, then this wave's half of the h1 broadcast
-  // (odd = 0: quads 2m -> chains 0-3; odd = 1: quads 2m + 1 -> chains 4-7) and its two
-  // packed chains, summed as the one-wave form sums them
-  XA_DEV float half_step(const float (&x)[OBS], float* sh, int lane, int odd) const {
-    float z1 = 0.0f;
-#pragma unroll
-    for (int k = 0; k < OBS; ++k) z1 = fmaf(x[k], w1[k], z1);
-    sh[lane] = xa_tanhf(z1 + b1);
-    wave_sync();
-    float4 hq[H / 8];
-#pragma unroll
-    for (int m = 0; m < H / 8; ++m) hq[m] = reinterpret_cast<const float4*>(sh)[2 * m + odd];
-    wave_sync();
-    xa_f2 ca = {0.0f, 0.0f}, cb = ca;
-#pragma unroll
-    for (int m = 0; m < H / 8; ++m) {
-      const int o = 8 * m + 4 * odd;
-      ca = xa_fma2(xa_f2{hq[m].x, hq[m].y}, xa_f2{w2[o + 0], w2[o + 1]}, ca);
-      cb = xa_fma2(xa_f2{hq[m].z, hq[m].w}, xa_f2{w2[o + 2], w2[o + 3]}, cb);
-    }
-    return (ca.x + ca.y) + (cb.x + cb.y);
   }
 
   XA_DEV void heads(float h2, float (&logits)[A], float& value) const {
@@ -344,66 +315,33 @@ XA_DEV float xa_readlane(float v, int l) {
 }
 
 template <int OBS, int A, bool REPLAY>
-__global__ __launch_bounds__(XA_ROLL_SPLIT ? 128 : 64 * kRollWaves) void mlp_rollout_kernel(XaRolloutArgs p) {
+__global__ __launch_bounds__(64 * kRollWaves) void mlp_rollout_kernel(XaRolloutArgs p) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int AH = A + 1, AHP = (AH + 3) & ~3;
   constexpr int HF = REPLAY ? 0 : A;  // first head of the chunk pass
   __shared__ __attribute__((aligned(16))) float hbuf[kRollWaves][kChunk * kHS];
   __shared__ __attribute__((aligned(16))) float wtab[kRollWaves][H * AHP];
-  constexpr bool SPLIT = REPLAY && XA_ROLL_SPLIT != 0;
-  __shared__ float rpart[2][64];  // (split) the helper wave's half-sums, by step parity
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
-  const int env = SPLIT ? (int)blockIdx.x : blockIdx.x * kRollWaves + wid;
-  if (env >= p.n_envs) return;  // workgroup-uniform when split; else wave-uniform (no
-                                // block barriers below outside the split form)
+  const int env = blockIdx.x * kRollWaves + wid;
+  if (env >= p.n_envs) return;  // wave-uniform (no block barriers below)
   const int T = p.n_steps;
   float* sh = smem + wid * H;
   const bool fused = p.ret_out != nullptr && p.return_kind != XA_RETURNS_NONE;
-  // [rew | val | done] per wave when fused (split: the env's wave 0 only)
-  float* hist = smem + (SPLIT ? 2 : kRollWaves) * H + (SPLIT ? 0 : wid * 3 * T);
+  // [rew | val | done] per wave when fused
+  float* hist = smem + kRollWaves * H + wid * 3 * T;
   float* const hb = hbuf[wid];  // h2 of the chunk's steps, row j = step t0 + j
 
   XA_STAMP_DECL
   LaneMlp<OBS, A> net;
   net.load(p.theta, lane);
-  if (!(SPLIT && wid == 1)) {  // the chunk pass's head weights, lane j writes row j
+  {  // the chunk pass's head weights, lane j writes row j
     float* wr = wtab[wid] + lane * AHP;
 #pragma unroll
     for (int a = 0; a < AHP; ++a) wr[a] = a < A ? net.w3[a] : a == A ? net.w4 : 0.0f;
   }
 
   const uint64_t ctr = p.rng_counter ? *p.rng_counter : 0ull;
-
-  if constexpr (SPLIT) {
-    if (wid == 1) {
-      // the helper wave: the same inputs (the record obs of the previous step), layer-2
-      // chains 4-7 of every step into rpart[t & 1], one workgroup barrier per step
-      float xh[OBS];
-#pragma unroll
-      for (int k = 0; k < OBS; ++k) xh[k] = p.env_state[(size_t)env * OBS + k];
-      const int cur0h = p.env_cursor[env];
-      StepChunk<OBS> ha, hbk;
-      auto helper_chunk = [&](const StepChunk<OBS>& c, int t0) {
-        const int n = min(64, T - t0);
-        for (int j = 0; j < n; ++j) {
-          rpart[(t0 + j) & 1][lane] = net.half_step(xh, sh, lane, 1);
-          __syncthreads();
-#pragma unroll
-          for (int k = 0; k < OBS; ++k) xh[k] = xa_readlane(c.obs[k], j);
-        }
-      };
-      load_chunk<OBS, REPLAY>(p, env, lane, cur0h, 0, ctr, ha);
-      for (int t0 = 0; t0 < T; t0 += 128) {
-        load_chunk<OBS, REPLAY>(p, env, lane, cur0h, t0 + 64, ctr, hbk);
-        helper_chunk(ha, t0);
-        if (t0 + 64 >= T) break;
-        load_chunk<OBS, REPLAY>(p, env, lane, cur0h, t0 + 128, ctr, ha);
-        helper_chunk(hbk, t0 + 64);
-      }
-      return;
-    }
-  }
 
   float x[OBS];  // policy input (wave-uniform)
   float st[OBS]; // post-reset env state
@@ -439,17 +377,10 @@ __global__ __launch_bounds__(XA_ROLL_SPLIT ? 128 : 64 * kRollWaves) void mlp_rol
       XA_STAMP(0);
       float logits[A];
       {
-        float h2;
-        if constexpr (SPLIT) {
-          const float pa = net.half_step(x, sh, lane, 0);
-          __syncthreads();  // the helper's half of this step is in rpart
-          h2 = xa_tanhf((pa + rpart[(t0 + j) & 1][lane]) + net.b2);
-        } else {
-          float4 hv[H / 4];
-          net.layer1(x, sh, lane, hv);
-          XA_STAMP(1);
-          h2 = net.layer2(hv);
-        }
+        float4 hv[H / 4];
+        net.layer1(x, sh, lane, hv);
+        XA_STAMP(1);
+        const float h2 = net.layer2(hv);
         XA_STAMP(2);
         hb[j * kHS + lane] = h2;  // the chunk pass's heads
         if constexpr (!REPLAY) {
@@ -654,11 +585,7 @@ int launch_rollout(const XaRolloutArgs* p, hipStream_t s) {
   const size_t lds = (size_t)kRollWaves * H * sizeof(float) +
                      (fused ? (size_t)kRollWaves * 3 * p->n_steps * sizeof(float) : 0);
   dim3 grid((p->n_envs + kRollWaves - 1) / kRollWaves);
-  if (p->env_kind == XA_ENV_REPLAY && XA_ROLL_SPLIT) {
-    // one env per workgroup of two waves (LDS: two h1 rows + the env's history)
-    const size_t lds2 = 2 * H * sizeof(float) + (fused ? 3 * (size_t)p->n_steps * sizeof(float) : 0);
-    hipLaunchKernelGGL((mlp_rollout_kernel<OBS, A, true>), dim3(p->n_envs), dim3(128), lds2, s, *p);
-  } else if (p->env_kind == XA_ENV_REPLAY) {
+  if (p->env_kind == XA_ENV_REPLAY) {
     hipLaunchKernelGGL((mlp_rollout_kernel<OBS, A, true>), grid, dim3(64 * kRollWaves), lds, s, *p);
   } else if constexpr (OBS == 4 && A == 2) {
     hipLaunchKernelGGL((mlp_rollout_kernel<OBS, A, false>), grid, dim3(64 * kRollWaves), lds, s, *p);

@@ -60,7 +60,6 @@ constexpr int kRows = 64, kCols = 16;   // weight-gradient / narrow job rows, ti
 constexpr int kTR = 32;                 // rows of a forward / input-gradient job
 constexpr int kMaxK = 416;              // largest GEMM depth (H1, H2, batch, in)
 constexpr int kAux = 2048 + 1024;       // LDS floats: W3 slice + dZ3 rows of the dZ2 former
-constexpr int kU = 8;                   // loads in flight per thread while staging
 
 XA_DEV f32x4v mfma4(float a, float b, f32x4v c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -247,19 +246,30 @@ __shared__ __attribute__((aligned(16))) float td3_part[2 * 32 * 16];
 
 // (diagnostic) block 0 stamps the wall clock at points of the first job of every phase into
 // the workspace's detail trace (tools/td3_grad_steps.py): slot 8 p + point
-__shared__ int td3_dslot;
-__shared__ unsigned long long* td3_dbuf;
 // (diagnostic builds only: -DXA_TD3_TRACE=1, tools/build_variant.py; a trace store in the
-// product would hold block 0 one store round trip at every barrier)
+// product would hold block 0 one store round trip at every barrier, so the product build
+// compiles no trace code at all)
 #ifndef XA_TD3_TRACE
 #define XA_TD3_TRACE 0
 #endif
+#if XA_TD3_TRACE
+__shared__ int td3_dslot;
+__shared__ unsigned long long* td3_dbuf;
 XA_DEV void dstamp(int point) {
-  if (!XA_TD3_TRACE) return;
   if (threadIdx.x == 0 && td3_dslot >= 0)
     *((__attribute__((address_space(1))) unsigned long long*)td3_dbuf + td3_dslot + point) =
         wall_clock64();
 }
+#define XA_TD3_DSLOT(v) \
+  do {                  \
+    if (threadIdx.x == 0) td3_dslot = (v); \
+  } while (0)
+#define XA_TD3_CLOCK(dst) ((dst) = wall_clock64())
+#else
+#define dstamp(point) ((void)0)
+#define XA_TD3_DSLOT(v) ((void)0)
+#define XA_TD3_CLOCK(dst) ((void)0)
+#endif
 
 // Operand layouts in LDS (both written by LDS-DMA, 1 KB per wave instruction):
 //   CR  chunked rows: element (row r, k) at (k / 16 * nrow + r) * 16 + k % 16 -- a 16-row x
@@ -1349,11 +1359,13 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
   y.status = p.status;
   y.trace = b == 0 ? ws.trace : nullptr;
   if (XA_TD3_TRACE && b == 0 && tid == 0) ws.trace[0] = wall_clock64();
+  if (tid == 0) td3_bpre = 0;
+#if XA_TD3_TRACE
   if (tid == 0) {
     td3_dslot = b == 0 ? 8 * 15 : -1;  // (diagnostic) the prologue's points in slot 15
     td3_dbuf = ws.dtrace;
-    td3_bpre = 0;
   }
+#endif
   dstamp(0);
   // networks; the step counters as the launch finds them are read here (in flight with the
   // slot loads) and the Adam step sizes formed only where the optimizer steps run
@@ -1369,7 +1381,7 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
   const Net tc1 = make_net(p.target_critic1, C, H1, H2, 1, false);
   const Net tc2 = make_net(twin ? p.target_critic2 : p.target_critic1, C, H1, H2, 1, false);
   const int64_t* slots = p.slots;
-  const int RT = (B + kRows - 1) / kRows, RTT = (B + kTR - 1) / kTR;
+  const int RTT = (B + kTR - 1) / kTR;
   const int CT1 = (H1 + kCols - 1) / kCols, CT2 = (H2 + kCols - 1) / kCols;
   // column tiles per weight-gradient job (they share the staged A; the B region holds
   // kCols x kMaxK floats, one k-major [pad16(B)][16] tile per column tile)
@@ -1485,7 +1497,7 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
   for (int layer = 1; layer <= 2; ++layer) {
     const int CT = layer == 1 ? CT1 : CT2, per = RTT * CT;
     for (int j = b; j < nn * per; j += G) {
-      if (tid == 0) td3_dslot = (b == 0 && j == b) ? 8 * (int)y.n : -1;
+      XA_TD3_DSLOT((b == 0 && j == b) ? 8 * (int)y.n : -1);
       const int id = net_id(j / per), rem = j % per, rt = rem / CT, ct = rem % CT;
       const Net n = net_of(id);
       if (layer == 1) {
@@ -1534,7 +1546,7 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
   for (int layer = 1; layer <= 2; ++layer) {
     const int CT = layer == 1 ? CT1 : CT2, per = RTT * CT;
     for (int j = b; j < nt * per; j += G) {
-      if (tid == 0) td3_dslot = (b == 0 && j == b) ? 8 * (int)y.n : -1;
+      XA_TD3_DSLOT((b == 0 && j == b) ? 8 * (int)y.n : -1);
       const int id = N_TC1 + j / per, rem = j % per, rt = rem / CT, ct = rem % CT;
       const Net n = net_of(id);
       if (layer == 1) {
@@ -1587,7 +1599,7 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
     const int n_dx = RTT * CT1, n_dw2 = IT1 * CTW2, n_dw3 = IT2;
     const int per = n_dx + n_dw2 + n_dw3;  // the heavy input-gradient jobs first
     for (int j = b; j < nt * per; j += G) {
-      if (tid == 0) td3_dslot = (b == 0 && j == b) ? 8 * (int)y.n : -1;
+      XA_TD3_DSLOT((b == 0 && j == b) ? 8 * (int)y.n : -1);
       const int ci = j / per, q = j % per;
       const Net n = ci ? c2 : c1;
       const int id = ci ? N_C2 : N_C1;
@@ -1626,7 +1638,7 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
     const int per = n_w1 + n_ad;
     p8_jobs = nt * per;
     for (int j = b; j < nt * per; j += G) {
-      if (tid == 0) td3_dslot = (b == 0 && j == b) ? 8 * (int)y.n : -1;
+      XA_TD3_DSLOT((b == 0 && j == b) ? 8 * (int)y.n : -1);
       const int ci = j / per, q = j % per;
       const Net n = ci ? c2 : c1;
       const XaTdNet& opt = ci ? p.critic2 : p.critic1;
@@ -1674,7 +1686,7 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
     for (int layer = 1; layer <= 2; ++layer) {
       const int CT = layer == 1 ? CT1 : CT2;
       for (int j = b; j < RTT * CT; j += G) {
-        if (tid == 0) td3_dslot = (b == 0 && j == b) ? 8 * (int)y.n : -1;
+        XA_TD3_DSLOT((b == 0 && j == b) ? 8 * (int)y.n : -1);
         const int rt = j / CT, ct = j % CT;
         if (layer == 1)
           fwd_job(spa, slots, rt * kTR, B, c1.th + c1.w1, c1.th + c1.b1, C, H1, ct * kCols,
@@ -1691,7 +1703,7 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
     // gradient d pi (1 - pi^2) ----
     const DZ dq2 = dz_h2(ws.q2, H2, c1.th + c1.w3, 1, nullptr, -1.0f / (float)B);
     for (int j = b; j < RTT * CT1; j += G) {
-      if (tid == 0) td3_dslot = (b == 0 && j == b) ? 8 * (int)y.n : -1;
+      XA_TD3_DSLOT((b == 0 && j == b) ? 8 * (int)y.n : -1);
       const int rt = j / CT1, ct = j % CT1, c0 = ct * kCols;
       const Head hd{c1.th + c1.w1 + (size_t)S * H1, ws.hpp, ws.ticket(6, rt), 1, H1, A, ct, CT1,
                     true};
@@ -1714,7 +1726,7 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
       const int n_dx = RTT * CT1, n_dw2 = IT1 * CTW2, n_dw3 = IT2;
       const DZ d2 = dz_h2(ws.h2(N_AC), H2, ac.th + ac.w3, A, ws.dz3, 0.0f);
       for (int j = b; j < n_dx + n_dw2 + n_dw3; j += G) {
-        if (tid == 0) td3_dslot = (b == 0 && j == b) ? 8 * (int)y.n : -1;
+        XA_TD3_DSLOT((b == 0 && j == b) ? 8 * (int)y.n : -1);
         if (j < n_dx) {
           const int rt = j / CT1, ct = j % CT1, c0 = ct * kCols;
           dx_tile(d2, rt * kTR, B, ac.th + ac.w2, H2, c0, min(kCols, H1 - c0), false,
@@ -1741,7 +1753,7 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
       const int rest = ac.P - ac.w2, chunk = adam_chunk(rest, max(1, G - CTW1));
       const int n_ad = stage == 2 ? 0 : (rest + chunk - 1) / chunk;
       for (int j = b; j < CTW1 + n_ad; j += G) {
-        if (tid == 0) td3_dslot = (b == 0 && j == b) ? 8 * (int)y.n : -1;
+        XA_TD3_DSLOT((b == 0 && j == b) ? 8 * (int)y.n : -1);
         if (j < CTW1) {
           dw_job(xsrc(p.out_s, S, S, false, true), slots, dz_buf(ws.dh1a, H1), S, H1, 0,
                  j * NTW * kCols, NTW, B, p.g_actor, ac.w1, ac.b1, ac,
@@ -1808,11 +1820,13 @@ __global__ __launch_bounds__(256) void td3_act_kernel(XaTd3ActArgs p) {
   y.n = 0;
   y.status = p.status;
   y.trace = nullptr;
+  if (tid == 0) td3_bpre = 0;
+#if XA_TD3_TRACE
   if (tid == 0) {
     td3_dslot = -1;
     td3_dbuf = ws.dtrace;
-    td3_bpre = 0;
   }
+#endif
   const uint64_t ctr = p.rng_counter ? *p.rng_counter : 0ull;
   XaTdNet d{};
   d.theta = const_cast<float*>(p.theta);
