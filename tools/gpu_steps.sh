@@ -61,6 +61,14 @@ for step in "$@"; do
     configs) run_pytest configs 400 tests/test_gpu_configs.py ;;
     td3) run_pytest td3 600 tests/test_gpu_td3.py tests/test_gpu_scale.py tests/test_gpu_configs.py::test_c5_td3_64_envs_rb2 ;;
     td3dp) run_pytest td3dp 450 tests/test_gpu_dp.py -k td3 ;;
+    fixab)
+      # the fixed-shape 16-env update kernel (BF = 3) vs the generic one, interleaved
+      B="python bench.py --steps 40 --warmup 5 --cpu-baseline-seconds 0 --no-secondary"
+      run fix_on1 200 $B
+      XA_PPO_FIXED_SHAPE=0 run fix_off1 200 $B
+      run fix_on2 200 $B
+      XA_PPO_FIXED_SHAPE=0 run fix_off2 200 $B
+      python tools/bench_brief.py gpurun_out/${T}_fix_*.out ;;
     dqn) run_pytest dqn 400 tests/test_gpu_dqn.py tests/test_gpu_scale.py -k "dqn" tests/test_gpu_configs.py::test_c3_dqn_32_envs_rb1_1m_batch_64 ;;
     td3time)
       # wall time per gradient step on the product build, per-phase barrier times on the

@@ -497,9 +497,16 @@ XA_DEV int elect_local(unsigned* ctl, int G, unsigned par, int xcc, unsigned epo
 // (spread grids of >= kTwoLevelMinG blocks with 32-sample tiles). Compiling the unused forms
 // out lowers the register allocation of the whole kernel body (16-env update 167 -> 161 us,
 // profiles/r03ah_variants.txt)
+// BF = 3: the column form AND the headline shape compiled in (16 envs x 128 steps, 4 epochs
+// x 4 minibatches of 512, 32 XCD-local blocks of 16-sample tiles: every loop bound, tile
+// count and exchange offset a constant, fewer live uniform values -- xa_ppo_update picks it
+// when the launch is exactly that shape)
+constexpr int kFixB = 2048, kFixMB = 512, kFixK = 16, kFixNmb = 4, kFixG = 32;
 template <int OBS, int A, int TS, bool DP, bool PRE, int BF = 0>
-__global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws ws, int K,
-                                                          int n_mb, int loc) {
+__global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws ws, int K_,
+                                                          int n_mb_, int loc_) {
+  constexpr bool FIX = BF == 3;
+  const int K = FIX ? kFixK : K_, n_mb = FIX ? kFixNmb : n_mb_, loc = FIX ? 1 : loc_;
   constexpr int RPT = Dims<OBS, A>::RPT;
   __shared__ __attribute__((aligned(16))) UpdLds<OBS, A, TS> U;
   PtLds<OBS, A, TS>& L = U.t;
@@ -515,14 +522,14 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
   const unsigned epoch = gen + 1u;
   const unsigned par = gen & 1u;
   const int xcc = xcc_id();
-  const int G = loc ? p.n_blocks : (int)gridDim.x;
+  const int G = FIX ? kFixG : loc ? p.n_blocks : (int)gridDim.x;
   const int b = loc ? elect_local(ws.ctl, G, par, xcc, epoch, p.status, U.flag) : (int)blockIdx.x;
   if (b < 0) return;
   XA_STAMP_BLOCK(b == 0)
   XA_STAMP(30);
   XA_TRACE_PT(b, kTraceSteps - 1, 6);  // launch start (after the election)
   XA_TRACE_CLK(b, 0);
-  const int B = p.batch, MB = p.mb_size;
+  const int B = FIX ? kFixB : p.batch, MB = FIX ? kFixMB : p.mb_size;
   const uint64_t ctr = p.shuffle.rng_counter ? *p.shuffle.rng_counter : 0ull;
   // hand-off stores: write-through across XCDs, plain inside the elected XCD's L2
   const bool kWt = !loc;
@@ -1069,7 +1076,7 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
       }
     }
     // (BF = 1: the host guarantees col_b wherever nc > 0; BF = 2: two_level everywhere)
-    constexpr bool flat_ok = BF == 0, gen_ok = BF != 1;
+    constexpr bool flat_ok = BF == 0, gen_ok = BF != 1 && BF != 3;
     const bool flat_b = flat_ok && !col_b && !two_level && G * nc <= 256 * kBF;
     if (nc > 0 && flat_b) {
       const bool bad = gather_rows(rows_r, G, nc, [&](int r) {
@@ -1410,6 +1417,7 @@ int occupancy_min() {
       (void*)ppo_update_kernel<OBS, A, 16, true, false, 1>,
       (void*)ppo_update_kernel<OBS, A, 16, false, true, 1>,
       (void*)ppo_update_kernel<OBS, A, 16, true, true, 1>,
+      (void*)ppo_update_kernel<OBS, A, 16, false, true, 3>,
       (void*)ppo_update_kernel<OBS, A, S, false, false, 2>,
       (void*)ppo_update_kernel<OBS, A, S, true, false, 2>,
       (void*)ppo_update_kernel<OBS, A, S, false, true, 2>,
@@ -1487,7 +1495,14 @@ void launch_ts(const XaPpoUpdateArgs* a, int G, bool dp, bool loc, const Ws& ws,
   const int l = loc ? 1 : 0;
   if constexpr (TS == 16) {  // 16-sample tiles: small grids, one-level reduce
     if (col_b_everywhere(G, offs(OBS, A).P)) {
-      if (dp && pre)
+      static const bool fix_on = [] {
+        const char* e = getenv("XA_PPO_FIXED_SHAPE");
+        return !(e && e[0] == '0');
+      }();
+      if (fix_on && !dp && pre && loc && G == kFixG && K == kFixK && n_mb == kFixNmb &&
+          a->batch == kFixB && a->mb_size == kFixMB && a->n_blocks == kFixG)
+        hipLaunchKernelGGL((ppo_update_kernel<OBS, A, TS, false, true, 3>), grid, dim3(256), 0, s, *a, ws, K, n_mb, l);
+      else if (dp && pre)
         hipLaunchKernelGGL((ppo_update_kernel<OBS, A, TS, true, true, 1>), grid, dim3(256), 0, s, *a, ws, K, n_mb, l);
       else if (dp)
         hipLaunchKernelGGL((ppo_update_kernel<OBS, A, TS, true, false, 1>), grid, dim3(256), 0, s, *a, ws, K, n_mb, l);
