@@ -501,12 +501,19 @@ XA_DEV int elect_local(unsigned* ctl, int G, unsigned par, int xcc, unsigned epo
 // x 4 minibatches of 512, 32 XCD-local blocks of 16-sample tiles: every loop bound, tile
 // count and exchange offset a constant, fewer live uniform values -- xa_ppo_update picks it
 // when the launch is exactly that shape)
-constexpr int kFixB = 2048, kFixMB = 512, kFixK = 16, kFixNmb = 4, kFixG = 32;
+// BF = 4: the same for BASELINE configs[1] (256 envs x 128 steps, minibatches of 8192, 256
+// spread blocks of 32-sample tiles, the two-level reduce)
+template <int BF>
+struct FixShape {  // (B, MB, K, n_mb, G, XCD-local) of a fixed-shape instantiation
+  static constexpr int B = BF == 3 ? 2048 : 32768, MB = BF == 3 ? 512 : 8192, K = 16, NMB = 4;
+  static constexpr int G = BF == 3 ? 32 : 256, LOC = BF == 3 ? 1 : 0;
+};
 template <int OBS, int A, int TS, bool DP, bool PRE, int BF = 0>
 __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws ws, int K_,
                                                           int n_mb_, int loc_) {
-  constexpr bool FIX = BF == 3;
-  const int K = FIX ? kFixK : K_, n_mb = FIX ? kFixNmb : n_mb_, loc = FIX ? 1 : loc_;
+  constexpr bool FIX = BF == 3 || BF == 4;
+  typedef FixShape<BF> FS;
+  const int K = FIX ? FS::K : K_, n_mb = FIX ? FS::NMB : n_mb_, loc = FIX ? FS::LOC : loc_;
   constexpr int RPT = Dims<OBS, A>::RPT;
   __shared__ __attribute__((aligned(16))) UpdLds<OBS, A, TS> U;
   PtLds<OBS, A, TS>& L = U.t;
@@ -522,21 +529,21 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
   const unsigned epoch = gen + 1u;
   const unsigned par = gen & 1u;
   const int xcc = xcc_id();
-  const int G = FIX ? kFixG : loc ? p.n_blocks : (int)gridDim.x;
+  const int G = FIX ? FS::G : loc ? p.n_blocks : (int)gridDim.x;
   const int b = loc ? elect_local(ws.ctl, G, par, xcc, epoch, p.status, U.flag) : (int)blockIdx.x;
   if (b < 0) return;
   XA_STAMP_BLOCK(b == 0)
   XA_STAMP(30);
   XA_TRACE_PT(b, kTraceSteps - 1, 6);  // launch start (after the election)
   XA_TRACE_CLK(b, 0);
-  const int B = FIX ? kFixB : p.batch, MB = FIX ? kFixMB : p.mb_size;
+  const int B = FIX ? FS::B : p.batch, MB = FIX ? FS::MB : p.mb_size;
   const uint64_t ctr = p.shuffle.rng_counter ? *p.shuffle.rng_counter : 0ull;
   // hand-off stores: write-through across XCDs, plain inside the elected XCD's L2
   const bool kWt = !loc;
 
   // ---- census: which XCD this block runs on (a granule, read after the phase-0 hop) ----
   // 16-sample tiles run only on small grids (<= 32 blocks): one level, known at compile time
-  const bool two_level = BF == 2 || (BF == 0 && !loc && TS == S && G >= kTwoLevelMinG);
+  const bool two_level = BF == 2 || BF == 4 || (BF == 0 && !loc && TS == S && G >= kTwoLevelMinG);
   const __amdgpu_buffer_rsrc_t cen_r = rsrc(ws.cen_g, (uint32_t)(G * 16));
   if (two_level && tid == 0) st_gran2(cen_r, (uint32_t)(16 * b), __uint_as_float((unsigned)xcc),
                                       __uint_as_float((unsigned)xcc), epoch, true);
@@ -1418,6 +1425,7 @@ int occupancy_min() {
       (void*)ppo_update_kernel<OBS, A, 16, false, true, 1>,
       (void*)ppo_update_kernel<OBS, A, 16, true, true, 1>,
       (void*)ppo_update_kernel<OBS, A, 16, false, true, 3>,
+      (void*)ppo_update_kernel<OBS, A, S, false, true, 4>,
       (void*)ppo_update_kernel<OBS, A, S, false, false, 2>,
       (void*)ppo_update_kernel<OBS, A, S, true, false, 2>,
       (void*)ppo_update_kernel<OBS, A, S, false, true, 2>,
@@ -1493,14 +1501,20 @@ void launch_ts(const XaPpoUpdateArgs* a, int G, bool dp, bool loc, const Ws& ws,
   const int TPB = (n_tiles_max + G - 1) / G;
   const bool pre = K * TPB * TS <= pre_max<OBS>();
   const int l = loc ? 1 : 0;
+  // the fixed-shape instantiations (BF 3 / 4) for exactly their shape; XA_PPO_FIXED_SHAPE=0
+  // forces the generic ones (A/B)
+  static const bool fix_on = [] {
+    const char* e = getenv("XA_PPO_FIXED_SHAPE");
+    return !(e && e[0] == '0');
+  }();
+  auto is_fix = [&](auto fs) {
+    typedef decltype(fs) F;
+    return fix_on && !dp && pre && (int)loc == F::LOC && G == F::G && K == F::K &&
+           n_mb == F::NMB && a->batch == F::B && a->mb_size == F::MB;
+  };
   if constexpr (TS == 16) {  // 16-sample tiles: small grids, one-level reduce
     if (col_b_everywhere(G, offs(OBS, A).P)) {
-      static const bool fix_on = [] {
-        const char* e = getenv("XA_PPO_FIXED_SHAPE");
-        return !(e && e[0] == '0');
-      }();
-      if (fix_on && !dp && pre && loc && G == kFixG && K == kFixK && n_mb == kFixNmb &&
-          a->batch == kFixB && a->mb_size == kFixMB && a->n_blocks == kFixG)
+      if (is_fix(FixShape<3>{}))
         hipLaunchKernelGGL((ppo_update_kernel<OBS, A, TS, false, true, 3>), grid, dim3(256), 0, s, *a, ws, K, n_mb, l);
       else if (dp && pre)
         hipLaunchKernelGGL((ppo_update_kernel<OBS, A, TS, true, true, 1>), grid, dim3(256), 0, s, *a, ws, K, n_mb, l);
@@ -1514,7 +1528,9 @@ void launch_ts(const XaPpoUpdateArgs* a, int G, bool dp, bool loc, const Ws& ws,
     }
   } else {  // 32-sample tiles on a spread grid of >= kTwoLevelMinG blocks: two-level only
     if (!loc && G >= kTwoLevelMinG) {
-      if (dp && pre)
+      if (is_fix(FixShape<4>{}))
+        hipLaunchKernelGGL((ppo_update_kernel<OBS, A, TS, false, true, 4>), grid, dim3(256), 0, s, *a, ws, K, n_mb, l);
+      else if (dp && pre)
         hipLaunchKernelGGL((ppo_update_kernel<OBS, A, TS, true, true, 2>), grid, dim3(256), 0, s, *a, ws, K, n_mb, l);
       else if (dp)
         hipLaunchKernelGGL((ppo_update_kernel<OBS, A, TS, true, false, 2>), grid, dim3(256), 0, s, *a, ws, K, n_mb, l);
