@@ -23,6 +23,10 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 
 N, T, E, M, T_REC = 8, 16, 4, 4, 256
+if os.environ.get('XA_TEST_DP_SHAPE') == 'headline':
+    # the metric's per-rank shape (16 envs x 128 steps, 4 x 4 minibatches of 512): the ranks
+    # run the fixed-shape data-parallel update instantiation
+    N, T = 16, 128
 
 
 def make(record, n, data_parallel=None):

@@ -34,12 +34,18 @@ def _run(worker, world, tag, extra_env=None, timeout=110):
         assert f'{tag} {r}' in out, out[-4000:]
 
 
-@pytest.mark.parametrize('mode,world', [('persistent', 2), ('chain', 2), ('persistent', 4)])
-def test_ppo_data_parallel_equals_union(device, mode, world):
+@pytest.mark.parametrize('mode,world,shape', [('persistent', 2, None), ('chain', 2, None),
+                                              ('persistent', 4, None),
+                                              ('persistent', 2, 'headline')])
+def test_ppo_data_parallel_equals_union(device, mode, world, shape):
     """xagents/ppo/agent.py:157-191 on the union of W shards vs the W-rank data-parallel
     step (advantage sums and gradients exchanged), tests/ppo_dp_worker.py: the persistent
-    update exchanging inside its launch (W = 2 and 4), and the per-minibatch chain."""
-    _run('ppo_dp_worker.py', world, 'PPO DP OK', extra_env={'XA_PPO_UPDATE': mode})
+    update exchanging inside its launch (W = 2 and 4), the per-minibatch chain, and the
+    metric's per-rank shape (16 envs x 128 steps: the fixed-shape DP instantiation)."""
+    env = {'XA_PPO_UPDATE': mode}
+    if shape:
+        env['XA_TEST_DP_SHAPE'] = shape
+    _run('ppo_dp_worker.py', world, 'PPO DP OK', extra_env=env)
 
 
 @pytest.mark.parametrize('world,bucket_mb,seed', [(2, None, 55), (2, None, 155), (2, None, 255),

@@ -498,22 +498,22 @@ XA_DEV int elect_local(unsigned* ctl, int G, unsigned par, int xcc, unsigned epo
 // out lowers the register allocation of the whole kernel body (16-env update 167 -> 161 us,
 // profiles/r03ah_variants.txt)
 // BF = 3: the column form AND the headline shape compiled in (16 envs x 128 steps, 4 epochs
-// x 4 minibatches of 512, 32 XCD-local blocks of 16-sample tiles: every loop bound, tile
+// x 4 minibatches of 512 per rank, 32 blocks of 16-sample tiles: every loop bound, tile
 // count and exchange offset a constant, fewer live uniform values -- xa_ppo_update picks it
 // when the launch is exactly that shape)
 // BF = 4: the same for BASELINE configs[1] (256 envs x 128 steps, minibatches of 8192, 256
 // spread blocks of 32-sample tiles, the two-level reduce)
 template <int BF>
-struct FixShape {  // (B, MB, K, n_mb, G, XCD-local) of a fixed-shape instantiation
+struct FixShape {  // (B, MB, K, n_mb, G) of a fixed-shape instantiation (per rank)
   static constexpr int B = BF == 3 ? 2048 : 32768, MB = BF == 3 ? 512 : 8192, K = 16, NMB = 4;
-  static constexpr int G = BF == 3 ? 32 : 256, LOC = BF == 3 ? 1 : 0;
+  static constexpr int G = BF == 3 ? 32 : 256;
 };
 template <int OBS, int A, int TS, bool DP, bool PRE, int BF = 0>
 __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws ws, int K_,
                                                           int n_mb_, int loc_) {
   constexpr bool FIX = BF == 3 || BF == 4;
   typedef FixShape<BF> FS;
-  const int K = FIX ? FS::K : K_, n_mb = FIX ? FS::NMB : n_mb_, loc = FIX ? FS::LOC : loc_;
+  const int K = FIX ? FS::K : K_, n_mb = FIX ? FS::NMB : n_mb_, loc = loc_;
   constexpr int RPT = Dims<OBS, A>::RPT;
   __shared__ __attribute__((aligned(16))) UpdLds<OBS, A, TS> U;
   PtLds<OBS, A, TS>& L = U.t;
@@ -1426,6 +1426,8 @@ int occupancy_min() {
       (void*)ppo_update_kernel<OBS, A, 16, true, true, 1>,
       (void*)ppo_update_kernel<OBS, A, 16, false, true, 3>,
       (void*)ppo_update_kernel<OBS, A, S, false, true, 4>,
+      (void*)ppo_update_kernel<OBS, A, 16, true, true, 3>,
+      (void*)ppo_update_kernel<OBS, A, S, true, true, 4>,
       (void*)ppo_update_kernel<OBS, A, S, false, false, 2>,
       (void*)ppo_update_kernel<OBS, A, S, true, false, 2>,
       (void*)ppo_update_kernel<OBS, A, S, false, true, 2>,
@@ -1509,12 +1511,14 @@ void launch_ts(const XaPpoUpdateArgs* a, int G, bool dp, bool loc, const Ws& ws,
   }();
   auto is_fix = [&](auto fs) {
     typedef decltype(fs) F;
-    return fix_on && !dp && pre && (int)loc == F::LOC && G == F::G && K == F::K &&
-           n_mb == F::NMB && a->batch == F::B && a->mb_size == F::MB;
+    return fix_on && pre && G == F::G && K == F::K && n_mb == F::NMB && a->batch == F::B &&
+           a->mb_size == F::MB;
   };
   if constexpr (TS == 16) {  // 16-sample tiles: small grids, one-level reduce
     if (col_b_everywhere(G, offs(OBS, A).P)) {
-      if (is_fix(FixShape<3>{}))
+      if (is_fix(FixShape<3>{}) && dp)
+        hipLaunchKernelGGL((ppo_update_kernel<OBS, A, TS, true, true, 3>), grid, dim3(256), 0, s, *a, ws, K, n_mb, l);
+      else if (is_fix(FixShape<3>{}))
         hipLaunchKernelGGL((ppo_update_kernel<OBS, A, TS, false, true, 3>), grid, dim3(256), 0, s, *a, ws, K, n_mb, l);
       else if (dp && pre)
         hipLaunchKernelGGL((ppo_update_kernel<OBS, A, TS, true, true, 1>), grid, dim3(256), 0, s, *a, ws, K, n_mb, l);
@@ -1528,7 +1532,9 @@ void launch_ts(const XaPpoUpdateArgs* a, int G, bool dp, bool loc, const Ws& ws,
     }
   } else {  // 32-sample tiles on a spread grid of >= kTwoLevelMinG blocks: two-level only
     if (!loc && G >= kTwoLevelMinG) {
-      if (is_fix(FixShape<4>{}))
+      if (is_fix(FixShape<4>{}) && dp)
+        hipLaunchKernelGGL((ppo_update_kernel<OBS, A, TS, true, true, 4>), grid, dim3(256), 0, s, *a, ws, K, n_mb, l);
+      else if (is_fix(FixShape<4>{}))
         hipLaunchKernelGGL((ppo_update_kernel<OBS, A, TS, false, true, 4>), grid, dim3(256), 0, s, *a, ws, K, n_mb, l);
       else if (dp && pre)
         hipLaunchKernelGGL((ppo_update_kernel<OBS, A, TS, true, true, 2>), grid, dim3(256), 0, s, *a, ws, K, n_mb, l);
