@@ -93,7 +93,8 @@ XA_DEV void zero4(float* d) { d[0] = d[1] = d[2] = d[3] = 0.0f; }
 // ADAM: the epilogue applies Keras Adam to the parameters the tile is the gradient of
 // (xa_gemm_adam; one K split, no bias / activation / gate / beta, N % 4 == 0)
 template <bool A_KMAJOR, bool B_NMAJOR, bool A_U8, bool ADAM = false>
-__global__ __launch_bounds__(256) void gemm_kernel(XaGemmK kargs) {
+// (ADAM: 4 blocks per CU -- the parameter / moment prefetch fits 121 VGPRs instead of 184)
+__global__ __launch_bounds__(256, ADAM ? 4 : 1) void gemm_kernel(XaGemmK kargs) {
   const XaGemmArgs& g = kargs.g;
   const bool vec_a = kargs.vec_a, vec_b = kargs.vec_b;
   __shared__ __attribute__((aligned(16))) float As[2][BK * LDA];
