@@ -357,6 +357,17 @@ typedef struct XaPpoUpdateArgs {
   int placement;      /* XA_PPO_PLACE_* */
   float* theta_trace; /* optional diagnostic outputs (above) */
   float* grad_trace;
+  /* episode statistics to the host inside the launch (replaces the xa_copy_to_host launch
+   * of a train step): stats_words (> 0) 32-bit words of stats_src (device: the rollout's
+   * done flags / running returns / this status word, as the caller packs them) are
+   * stored into stats_dst[g & 1] (device pointers of mapped pinned host buffers of
+   * stats_words + 1 words), g = the launch number kept in the workspace (0 for the first
+   * launch on a zeroed workspace), and word stats_words of that buffer receives g. The
+   * words are copied when the launch starts (the status word as the previous launches
+   * left it). stats_words = 0: nothing. */
+  const void* stats_src;
+  void* stats_dst[2];
+  int stats_words;
 } XaPpoUpdateArgs;
 
 int xa_ppo_update_blocks(int obs_dim, int n_actions, int mb_size);

@@ -314,3 +314,29 @@ def test_every_optimizer_step_teacher_forced_vs_f64(device, B, mb, placement):
     assert worst['grad'] < 1e-5
     assert worst['pg'] < 1e-5 and worst['vl'] < 1e-5 and worst['ent'] < 1e-5
     assert worst['step'] <= 1.0
+
+
+@pytest.mark.parametrize('use_graph', [True, False])
+def test_episode_statistics_stored_by_the_update_launch(device, monkeypatch, use_graph):
+    """The persistent update stores the train step's episode statistics into its two
+    mapped host slots (launch-number parity) instead of an xa_copy_to_host launch: over
+    12 train steps -- graph replays and eager launches, a bench-style event-timed step in
+    between -- the folded episode returns, game count and per-env running state equal the
+    copy path's exactly, and every fold saw the launch number it expected."""
+    from test_gpu_agent import make_agent
+    out = []
+    for fused in ('1', '0'):
+        monkeypatch.setenv('XA_STATS_IN_UPDATE', fused)
+        a = make_agent(n_envs=16, n_steps=128, seed=13, use_graph=use_graph, t_rec=256)
+        assert a._stats_fused == (fused == '1')
+        for i in range(12):
+            if i == 5:
+                a.timed_train_step()
+                continue
+            a.train_step()
+        a._drain_episode_stats()
+        torch.cuda.synchronize()
+        assert a.games > 0
+        out.append((list(a.total_rewards), a.games, list(a.dones),
+                    np.asarray(a.episode_rewards).tolist()))
+    assert out[0] == out[1]

@@ -61,6 +61,14 @@ for step in "$@"; do
     configs) run_pytest configs 400 tests/test_gpu_configs.py ;;
     td3) run_pytest td3 600 tests/test_gpu_td3.py tests/test_gpu_scale.py tests/test_gpu_configs.py::test_c5_td3_64_envs_rb2 ;;
     td3dp) run_pytest td3dp 450 tests/test_gpu_dp.py -k td3 ;;
+    statab)
+      # episode statistics stored by the update launch vs the xa_copy_to_host launch
+      B="python bench.py --steps 40 --warmup 5 --cpu-baseline-seconds 0 --no-secondary"
+      run stat_on1 200 $B
+      XA_STATS_IN_UPDATE=0 run stat_off1 200 $B
+      run stat_on2 200 $B
+      XA_STATS_IN_UPDATE=0 run stat_off2 200 $B
+      python tools/bench_brief.py gpurun_out/${T}_stat_*.out ;;
     fixab)
       # the fixed-shape 16-env update kernel (BF = 3) vs the generic one, interleaved
       B="python bench.py --steps 40 --warmup 5 --cpu-baseline-seconds 0 --no-secondary"

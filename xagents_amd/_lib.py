@@ -157,6 +157,7 @@ class XaPpoUpdateArgs(Structure):
         ('dp_blocks', c_void_p * 16),
         ('placement', c_int),
         ('theta_trace', c_void_p), ('grad_trace', c_void_p),
+        ('stats_src', c_void_p), ('stats_dst', c_void_p * 2), ('stats_words', c_int),
     ]
 
 

@@ -385,6 +385,7 @@ class A2C(ExecutorActorCritic, OnPolicy):
         if self.use_graph and self._graph is not None and not events and \
                 not self.stats_side_stream:
             self._graph[2].replay()
+            self._count_update_replay()
         elif self.use_graph and self._graph is not None:
             rec(0)
             self._graph[0].replay()
@@ -392,6 +393,7 @@ class A2C(ExecutorActorCritic, OnPolicy):
                 self._rollout_ev.record()
             rec(1)
             self._graph[1].replay()
+            self._count_update_replay()
             rec(2)
         else:
             rec(0)
@@ -408,6 +410,12 @@ class A2C(ExecutorActorCritic, OnPolicy):
         self._queue_episode_stats(self.b_done, self.b_epret,
                                   after=self._rollout_ev if self.stats_side_stream else None)
         self._maybe_check_peer()
+
+    def _count_update_replay(self):
+        """A graph replay that ran the persistent update: one more launch number (the
+        in-launch statistics slots, PPO._setup_fused_stats)."""
+        if getattr(self, '_stats_fused', False) and self.update_mode == 'persistent':
+            self._upd_launches += 1
 
     # every rank reaches the same train-step count, so this collective check lines up
     PEER_CHECK_STEPS = 64

@@ -401,8 +401,27 @@ class BaseAgent(ABC):
         (with the persistent update's status word). `after`: an event recorded on the
         launch stream right after the rollout -- the copy then runs on a side stream
         behind it, overlapping the update, and the next rollout waits for it
-        (_sync_stats_copy)."""
-        if self._pending_stats is None or self._pending_stats[0].shape != done_out.shape:
+        (_sync_stats_copy). When the persistent update stores the statistics into its host
+        slots itself (PPO._setup_fused_stats) there is nothing to launch: the step's slot is
+        its launch number's parity, and the fold checks the number the launch wrote."""
+        if getattr(self, '_stats_fused', False) and after is None and \
+                done_out.data_ptr() == self.b_done.data_ptr():
+            if getattr(self, '_stats_queue', None) is None or \
+                    getattr(self, '_stats_queue_kind', None) != 'fused':
+                self._drain_episode_stats()
+                self._stats_queue = []
+                self._stats_queue_kind = 'fused'
+                self._fused_events = [torch.cuda.Event(), torch.cuda.Event()]
+            gen = self._upd_launches - 1
+            ev = self._fused_events[gen & 1]
+            ev.record()
+            self._stats_queue.append((gen & 1, ev, gen))
+            self._pending_stats = (done_out, epret_out)
+            while len(self._stats_queue) > 1:
+                self._fold_stats(*self._stats_queue.pop(0))
+            return
+        if self._pending_stats is None or self._pending_stats[0].shape != done_out.shape or \
+                getattr(self, '_stats_queue_kind', None) == 'fused':
             self._drain_episode_stats()
             self._host_done = [torch.empty(done_out.shape, dtype=done_out.dtype).pin_memory()
                                for _ in range(2)]
@@ -415,6 +434,7 @@ class BaseAgent(ABC):
             self._stats_events = [torch.cuda.Event(), torch.cuda.Event()]
             self._stats_slot = 0
             self._stats_queue = []
+            self._stats_queue_kind = 'copy'
         slot = self._stats_slot
         side = None
         if after is not None:
@@ -505,14 +525,29 @@ class BaseAgent(ABC):
             torch.cuda.current_stream().wait_event(ev)
             self._stats_guard = None
 
-    def _fold_stats(self, slot, ev):
+    def _fold_stats(self, slot, ev, gen=None):
         ev.synchronize()
-        if getattr(self, 'device_status', None) is not None and int(self._host_status[slot].max()):
+        if gen is None:
+            host_done, host_epret, host_status = (self._host_done[slot], self._host_epret[slot],
+                                                  getattr(self, '_host_status', None))
+            host_status = host_status[slot] if host_status is not None else None
+        else:
+            # the update launch number `gen` stored this slot (checked: a launch the host
+            # did not count would otherwise fold another step's statistics)
+            host_done, host_epret, host_status = (self._fused_done[slot],
+                                                  self._fused_epret[slot],
+                                                  self._fused_status[slot])
+            got = int(self._fused_gen[slot].item())
+            if got != gen:
+                raise RuntimeError(f'{self.__class__.__name__}: episode statistics slot {slot} '
+                                   f'holds update launch {got}, expected {gen}')
+        if getattr(self, 'device_status', None) is not None and host_status is not None and \
+                int(host_status.max()):
             raise RuntimeError(
                 f'{self.__class__.__name__}: an in-launch exchange of the persistent update '
                 f'timed out (device status word set); the parameters are invalid')
-        done = self._host_done[slot].numpy()[:, 1:]
-        epret = self._host_epret[slot].numpy()
+        done = host_done.numpy()[:, 1:]
+        epret = host_epret.numpy()
         t_idx, env_idx = np.nonzero(done.T)  # step-major, env-minor like step_envs
         finished = epret[env_idx, t_idx]
         for env, ret in zip(env_idx, finished):
@@ -530,7 +565,8 @@ class BaseAgent(ABC):
         # a side-stream copy reads the status word before the step's update ends: the
         # last update's status is read here
         status = getattr(self, 'device_status', None)
-        if status is not None and getattr(self, '_stats_stream', None) is not None and \
+        if status is not None and (getattr(self, '_stats_stream', None) is not None or
+                                   getattr(self, '_stats_fused', False)) and \
                 int(status.max().item()):
             raise RuntimeError(
                 f'{self.__class__.__name__}: an in-launch exchange of the persistent update '

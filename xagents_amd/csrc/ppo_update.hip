@@ -532,6 +532,14 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
   const int G = FIX ? FS::G : loc ? p.n_blocks : (int)gridDim.x;
   const int b = loc ? elect_local(ws.ctl, G, par, xcc, epoch, p.status, U.flag) : (int)blockIdx.x;
   if (b < 0) return;
+  // the train step's episode statistics into host slot gen & 1 (posted stores, issued
+  // first: they drain while the update runs)
+  if (p.stats_words > 0) {
+    const unsigned* src = static_cast<const unsigned*>(p.stats_src);
+    unsigned* dst = static_cast<unsigned*>(p.stats_dst[gen & 1u]);
+    for (int i = b * 256 + tid; i < p.stats_words; i += G * 256) dst[i] = src[i];
+    if (b == 0 && tid == 0) dst[p.stats_words] = gen;
+  }
   XA_STAMP_BLOCK(b == 0)
   XA_STAMP(30);
   XA_TRACE_PT(b, kTraceSteps - 1, 6);  // launch start (after the election)
@@ -1627,6 +1635,11 @@ extern "C" int xa_ppo_update(const XaPpoUpdateArgs* a, void* stream) {
   const size_t need = ws_bytes(G, offs(a->obs_dim, a->n_actions).P, K);
   XA_CHECK_ARG(a->workspace_bytes >= need, "xa_ppo_update: workspace %zu bytes < %zu needed",
                a->workspace_bytes, need);
+  XA_CHECK_ARG(a->stats_words <= 0 ||
+                   (a->stats_src && a->stats_dst[0] && a->stats_dst[1] &&
+                    (((uintptr_t)a->stats_src | (uintptr_t)a->stats_dst[0] |
+                      (uintptr_t)a->stats_dst[1]) & 3) == 0),
+               "xa_ppo_update: stats_words > 0 needs stats_src and both (4-B aligned) stats_dst");
   hipStream_t s = (hipStream_t)stream;
   if (a->obs_dim == 4 && a->n_actions == 2) return launch<4, 2>(a, G, K, n_mb, s);
   if (a->obs_dim == 6 && a->n_actions == 3) return launch<6, 3>(a, G, K, n_mb, s);

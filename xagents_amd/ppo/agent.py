@@ -183,6 +183,7 @@ class PPO(A2C):
         if getattr(self, 'update_ws', None) is None or getattr(self, '_ws_key', None) != key:
             self.update_ws = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
             self._ws_key = key
+            self._upd_launches = 0  # the launch number the zeroed workspace starts from
         # the status word rides in the packed episode-statistics buffer (one D2H copy)
         self.device_status = self._stats_status
         self.device_status.zero_()
@@ -234,9 +235,42 @@ class PPO(A2C):
             u.dp_world, u.dp_rank = self.world_size, self.rank
             for r, ptr in enumerate(self.dp_blocks.pointers):
                 u.dp_blocks[r] = ptr
+        self._setup_fused_stats(u)
         self._uargs = u
         self.update_mode = 'persistent'
         self.update_blocks = n_blocks
+
+    def _setup_fused_stats(self, u):
+        """The train step's episode statistics (done flags, running returns, the status word:
+        the packed buffer a2c/agent.py lays out) leave the device inside the update launch,
+        into two mapped pinned host slots chosen by the launch number's parity -- no
+        xa_copy_to_host launch per train step. Off with XA_STATS_IN_UPDATE=0 or the opt-in
+        side-stream copy."""
+        import ctypes
+        from xagents_amd._lib import call
+        u.stats_words = 0
+        self._stats_fused = False
+        if os.environ.get('XA_STATS_IN_UPDATE', '1') == '0' or \
+                getattr(self, 'stats_side_stream', False):
+            return
+        nd, sd, oe, se, os_ = self._stats_views
+        nw = os_ + 1  # through the status word
+        if getattr(self, '_fused_host', None) is None or self._fused_host[0].numel() != nw + 1:
+            self._fused_host = [torch.zeros(nw + 1, dtype=torch.float32).pin_memory()
+                                for _ in range(2)]
+            self._fused_done = [h[:nd].view(sd) for h in self._fused_host]
+            self._fused_epret = [h[oe:oe + se[0] * se[1]].view(se) for h in self._fused_host]
+            self._fused_status = [h[os_:os_ + 1].view(torch.int32) for h in self._fused_host]
+            self._fused_gen = [h[nw:nw + 1].view(torch.int32) for h in self._fused_host]
+            self._fused_dev = []
+            for h in self._fused_host:
+                dp = ctypes.c_void_p()
+                call('xa_host_device_pointer', ctypes.c_void_p(h.data_ptr()), ctypes.byref(dp))
+                self._fused_dev.append(dp.value)
+        u.stats_src = self._stats_pack.data_ptr()
+        u.stats_dst[0], u.stats_dst[1] = self._fused_dev
+        u.stats_words = nw
+        self._stats_fused = True
 
     def set_minibatch_permutation(self, perm):
         """Parity mode: the fused update takes every epoch's shuffle from `perm`, an
@@ -268,6 +302,8 @@ class PPO(A2C):
             self._kernel_event('ppo_update', 0, 0)
             kernels.ppo_update(self._uargs)
             self._kernel_event('ppo_update', 0, 1)
+            if not torch.cuda.is_current_stream_capturing():
+                self._upd_launches += 1  # (a captured launch counts at its replays)
             return
         kernels.minibatches(self._mbargs)
         self._all_reduce(self.adv_stats)
