@@ -139,6 +139,12 @@ for step in "$@"; do
         > gpurun_out/${T}_profc3_shapes.txt 2>&1
       python tools/step_timeline.py gpurun_out/${T}_profc3/run_kernel_trace.csv \
         > gpurun_out/${T}_profc3_timeline.txt 2>&1 ;;
+    profc4)
+      (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/${T}_profc4 \
+        -o run --output-format csv -- python $R/bench.py --config c4 --steps 2 --warmup 1 \
+        --cpu-baseline-seconds 0 > $R/gpurun_out/${T}_profc4_bench.json 2>&1) || exit $?
+      python tools/kernel_shapes.py gpurun_out/${T}_profc4/run_kernel_trace.csv 30 \
+        > gpurun_out/${T}_profc4_shapes.txt 2>&1 ;;
     profc5)
       # C5 (TD3): the whole bench line, then one gradient step's launches on their own
       (cd /tmp && timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/${T}_profc5 \
