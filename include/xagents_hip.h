@@ -443,6 +443,24 @@ typedef struct XaAdamApply {
  * args->c (optional, may be NULL) receives the raw gradient. Replaces the dense layer's
  * share of tape.gradient + Adam.apply_gradients (dqn/agent.py:170-171). */
 int xa_gemm_adam(const XaGemmArgs* args, const XaAdamApply* adam, void* stream);
+
+/* The NatureCNN convolution stack's forward in one launch (the three Conv1D layers of
+ * the cnn .cfg models (xagents/dqn/models/cnn.cfg, the ppo / a2c / acer
+ * cnn-actor-critic.cfg) as built by xagents/utils/common.py:225-240 over (84, 84, 1)
+ * frames: 32 x 8 / 4, 64 x 4 / 2, 64 x 3 / 1, ReLU; Keras convolves each 84-pixel frame row
+ * separately). rows = frames x 84; x [rows][84] uint8 (/ 255, x_u8) or f32; w1 [8][32],
+ * w2 [4][32][64], w3 [3][64][64] (Keras kernel order), biases; outputs h1 [rows][20][32],
+ * h2 [rows][9][64] (optional, NULL skips: kept for the backward) and h3 [rows][7][64]
+ * (the flattened 37632-float features per frame). Same values as three xa_gemm launches
+ * up to f32 association. */
+typedef struct XaConvStackArgs {
+  const void* x;
+  int x_u8;
+  int rows;
+  const float *w1, *b1, *w2, *b2, *w3, *b3;
+  float *h1, *h2, *h3;
+} XaConvStackArgs;
+int xa_conv_stack_fwd(const XaConvStackArgs* args, void* stream);
 int xa_gemm_splits(int M, int N, int K);
 /* the kernel shape xa_gemm picks for a tile-path GEMM with `splits` K splits (0 = the
  * 64 x 64 kernel, the only one that takes a_ones_row) */
@@ -535,11 +553,13 @@ int xa_dqn_act(const float* q, int n, int n_actions, const int* random_actions, 
  * 0 elsewhere; loss[b] (optional) = (y - q[b][a_b])^2 / A.
  * huber_delta > 0 (opt-in, not in the reference -- BASELINE north_star's Huber-TD loss):
  * tf.keras.losses.Huber(delta) in place of MSE, x = y - q[b][a_b]:
- * dq[b][a_b] = -clip(x, -delta, delta) / A, loss[b] = huber(x) / A. <= 0: MSE (parity). */
+ * dq[b][a_b] = -clip(x, -delta, delta) / A, loss[b] = huber(x) / A. <= 0: MSE (parity).
+ * adam_step (optional): the Keras optimizer's iteration counter, bumped by one in the same
+ * launch (the update's t += 1 before its Adam step, without a launch of its own). */
 int xa_dqn_td_grad(const float* q, const float* q_next_target, const float* q_next_online,
                    const int* actions, const float* rewards, const float* dones, int batch,
                    int n_actions, float gamma, float huber_delta, float* dq, float* loss,
-                   void* stream);
+                   int* adam_step, void* stream);
 
 /* Replay rings (ReplayBuffer1 xagents/utils/buffers.py:59-98, ReplayBuffer2 101-148):
  * ring[slots[i]] = src[i] / dst[i] = ring[slots[i]] for items of item_bytes. The host

@@ -37,7 +37,9 @@ _SHAPES = [(37, 50, 29, 1), (64, 512, 3000, 8), (130, 70, 1000, 4), (300, 257, 4
 @pytest.mark.parametrize('small', [False, True])
 @pytest.mark.parametrize('M,N,K,splits', _SHAPES + [
     # few rows over a huge K (the NatureCNN dense forward at the acting batch)
-    (32, 512, 37632, 256), (17, 448, 12345, 100)])
+    (32, 512, 37632, 256), (17, 448, 12345, 100),
+    # the streaming path: two 512-column blocks, a 2-row-block M, a ragged K split
+    (48, 1024, 20000, 128), (7, 512, 37632, 300)])
 def test_gemm_plain_bias_relu_split(device, M, N, K, splits, small):
     from xagents_amd.layers import gemm
     from xagents_amd._lib import XA_ACT_RELU
@@ -210,7 +212,13 @@ def test_layer_executor_forward_backward_vs_f64(device, cfg, units, shape, B):
     douts = [rng.normal(size=o.shape).astype(np.float32) for o in outs]
     grad = torch.zeros(model.n_params, device=device)
     ex.backward([torch.from_numpy(d).to(device) for d in douts], grad)
-    ref_g = O.backward(model.layers, theta, x64, ref_outs,
+    # backward parity with the device's ReLU gates: an f32 / f64 disagreement on a gate
+    # (pre-activation within 1e-5 of 0, asserted) moves one gradient element by its full
+    # value, which is not an arithmetic error of the backward
+    dev = {i: ex.outs[i].cpu().numpy() for i, l in enumerate(model.layers) if l.kind != 'flatten'}
+    gated, flips = O.adopt_gates(model.layers, ref_outs, dev)
+    print(f'{flips} gate flips')
+    ref_g = O.backward(model.layers, theta, x64, gated,
                        {i: d for i, d in zip(model.outputs, douts)})
     # per parameter tensor, relative to that tensor's scale
     sls, _ = O.param_slices(model.layers)
@@ -363,3 +371,35 @@ def test_layer_executor_cnn_backward_on_leading_rows(device, B, half):
 
 def _rel_err(got, want):
     return float(np.linalg.norm(np.asarray(got, np.float64) - want) / np.linalg.norm(want))
+
+
+@pytest.mark.parametrize('B,u8', [(1, True), (5, True), (37, False), (128, True)])
+def test_conv_stack_fused_forward(device, B, u8, monkeypatch):
+    """xa_conv_stack_fwd (the NatureCNN Conv1D stack in one launch) against the per-layer
+    GEMM path and the f64 restatement: every hidden activation, ragged last groups of 16
+    frame rows (B = 1, 5, 37), f32 and uint8 frames; keep_hidden=False leaves the features
+    bit-identical."""
+    import sys
+    sys.path.insert(0, str(ROOT / 'oracle'))
+    import nets_f64 as O
+    from xagents_amd.layers import LayerExecutor
+    model = _model(ROOT / 'xagents_amd' / 'dqn/models/cnn.cfg', [6], (84, 84, 1), device)
+    rng = np.random.default_rng(B)
+    x = (rng.integers(0, 256, size=(B, 84, 84, 1), dtype=np.uint8) if u8 else
+         rng.random(size=(B, 84, 84, 1)).astype(np.float32))
+    xt = torch.from_numpy(x).to(device)
+    monkeypatch.setenv('XA_CONV_STACK', '0')
+    ex0 = LayerExecutor(model, B)
+    monkeypatch.setenv('XA_CONV_STACK', '1')
+    ex1, ex2 = LayerExecutor(model, B), LayerExecutor(model, B)
+    assert not ex0.stack and ex1.stack and ex2.stack
+    ex2.keep_hidden = False
+    o0, o1, o2 = ex0.forward(xt), ex1.forward(xt), ex2.forward(xt)
+    _, ref = O.forward(model.layers, model.theta.cpu().numpy(), x, (84, 84, 1))
+    for i in range(3):
+        _close(ex1.outs[i].cpu().numpy(), ex0.outs[i].cpu().numpy(), rtol=1e-5)
+        _close(ex1.outs[i].cpu().numpy(), ref[i])
+    assert torch.equal(ex2.outs[2], ex1.outs[2])
+    for a, b, c in zip(o0, o1, o2):
+        _close(b.cpu().numpy(), a.cpu().numpy(), rtol=1e-5)
+        assert torch.equal(b, c)

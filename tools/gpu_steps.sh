@@ -18,6 +18,9 @@
 #   pollab   persistent-update poll sleep variants: bench + C2 FETCH_SIZE
 #   c2g      C2 bench lines at update grids $C2_GS (XA_PPO_MAX_BLOCKS)
 #   profc3   rocprofv3 kernel trace of the C3 bench + per-(kernel, grid) summary
+#   layers   tests/test_gpu_layers.py (GEMM paths, layer executor)
+#   streamab C3 bench lines, streaming dense forward on / off, interleaved
+#   stackab  C3 bench lines, fused conv-stack forward on / off, interleaved
 #   gemm     GEMM tests, small-M timings, PMC passes on the dense dX GEMM
 #   icache   instruction-cache counters of the 16-env update
 #   stamps   per-phase stamp shares of the persistent update (tools/diag_ppo_update.py)
@@ -77,6 +80,21 @@ for step in "$@"; do
       run fix_on2 200 $B
       XA_PPO_FIXED_SHAPE=0 run fix_off2 200 $B
       python tools/bench_brief.py gpurun_out/${T}_fix_*.out ;;
+    layers) run_pytest layers 300 tests/test_gpu_layers.py ;;
+    streamab)
+      # the streaming few-row dense forward vs the tile kernels (XA_GEMM_STREAM=0), C3 lines
+      B="python bench.py --config c3 --steps 30 --warmup 5 --cpu-baseline-seconds 0"
+      run st_on1 300 $B
+      XA_GEMM_STREAM=0 run st_off1 300 $B
+      run st_on2 300 $B
+      XA_GEMM_STREAM=0 run st_off2 300 $B ;;
+    stackab)
+      # the fused conv-stack forward vs per-layer GEMMs (XA_CONV_STACK=0), C3 lines
+      B="python bench.py --config c3 --steps 30 --warmup 5 --cpu-baseline-seconds 0"
+      run sk_on1 300 $B
+      XA_CONV_STACK=0 run sk_off1 300 $B
+      run sk_on2 300 $B
+      XA_CONV_STACK=0 run sk_off2 300 $B ;;
     dqn) run_pytest dqn 400 tests/test_gpu_dqn.py tests/test_gpu_scale.py -k "dqn" tests/test_gpu_configs.py::test_c3_dqn_32_envs_rb1_1m_batch_64 ;;
     td3time)
       # wall time per gradient step on the product build, per-phase barrier times on the

@@ -206,6 +206,15 @@ class XaAdamApply(Structure):
     ]
 
 
+class XaConvStackArgs(Structure):
+    _fields_ = [
+        ('x', c_void_p), ('x_u8', c_int), ('rows', c_int),
+        ('w1', c_void_p), ('b1', c_void_p), ('w2', c_void_p), ('b2', c_void_p),
+        ('w3', c_void_p), ('b3', c_void_p),
+        ('h1', c_void_p), ('h2', c_void_p), ('h3', c_void_p),
+    ]
+
+
 class XaAtariStepArgs(Structure):
     _fields_ = [
         ('n_envs', c_int), ('t_raw', c_int), ('height', c_int), ('width', c_int),
@@ -409,6 +418,7 @@ _SIGNATURES = {
     'xa_ppo_update': (c_int, [POINTER(XaPpoUpdateArgs), c_void_p]),
     'xa_gemm': (c_int, [POINTER(XaGemmArgs), c_void_p]),
     'xa_gemm_adam': (c_int, [POINTER(XaGemmArgs), POINTER(XaAdamApply), c_void_p]),
+    'xa_conv_stack_fwd': (c_int, [POINTER(XaConvStackArgs), c_void_p]),
     'xa_gemm_splits': (c_int, [c_int, c_int, c_int]),
     'xa_gemm_shape': (c_int, [c_int, c_int, c_int, c_int]),
     'xa_gemm_workspace_floats': (ctypes.c_size_t, [c_int, c_int, c_int, c_int]),
@@ -440,7 +450,7 @@ _SIGNATURES = {
     'xa_dqn_td_grad': (
         c_int,
         [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float,
-         c_float, c_void_p, c_void_p, c_void_p],
+         c_float, c_void_p, c_void_p, c_void_p, c_void_p],
     ),
     'xa_ring_scatter': (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int64, c_void_p]),
     'xa_ring_gather': (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int64, c_void_p]),

@@ -21,6 +21,7 @@
 // blockIdx.z; split partial sums are reduced in fixed order by a second kernel that
 // applies the epilogue (deterministic, no atomics).
 #include <algorithm>
+#include <cstdlib>
 
 #include "../../include/xagents_hip.h"
 #include "xa_adam.hpp"
@@ -841,6 +842,156 @@ __global__ __launch_bounds__(64) void gemm_skinny_kernel(XaGemmArgs g) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Streaming few-row forward (the dense layer over a big flattened input, M <= 64 rows:
+// DQN's act / target forwards, 32 / 64 x 512 x 37632): HBM-bound on the weight, which every
+// other path reads in short K pieces per 64-column tile. Here workgroup z owns one
+// contiguous K range and ALL 512 columns of a column block, so the weight streams in
+// whole 2-KB rows, once: lane l loads 16 B of row k + (l >> 5) (lanes 0..31 one 512-B
+// half-row each wave, 4 waves = 512 columns) and feeds the 4 floats to 4 MFMAs whose
+// column i is the real column 4 i + j (a column permutation the epilogue undoes with one
+// 16-B partial store per row). A's slice sits in LDS (k-major, zero-padded), 16 k-pairs of
+// the weight are in flight per lane, and nothing synchronises after the A fill. Partials
+// [splits][M][N] go to the usual fixed-order split reduce (bias / activation / gate / beta).
+// ---------------------------------------------------------------------------
+constexpr int ST_U = 16;       // k-pairs in flight per lane (vmcnt allows 63)
+constexpr int ST_NCOL = 512;   // columns per workgroup
+constexpr int ST_MAX_LDS = 64 * 1024;
+constexpr int kStRsrcWord3 = 0x00020000;  // raw buffer, gfx9-family resource word 3
+constexpr int kStAuxNt = 2;               // buffer load aux bits: nontemporal (streamed once)
+constexpr int ST_NCH = 6;                 // chunks per workgroup: K ranges <= 2 ST_NCH ST_U
+
+// K per workgroup (a multiple of 4: 16-B A loads) and the LDS rows the loop reads (rounded
+// up to its 2 ST_U-k chunk, zero past the range)
+__host__ __device__ inline int stream_per(int K, int splits) {
+  return ((K + splits - 1) / splits + 3) / 4 * 4;
+}
+__host__ __device__ inline int stream_rows(int per) {
+  return (per + 2 * ST_U - 1) / (2 * ST_U) * (2 * ST_U);
+}
+
+template <int MB>
+__global__ __launch_bounds__(256) void gemm_stream_kernel(XaGemmArgs g) {
+  constexpr int MR = 32 * MB, LDA = MR + 1;
+  extern __shared__ float as[];  // [per][LDA]: A(m, kb + kk) at as[kk LDA + m]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
+  const int z = blockIdx.x, n_base = blockIdx.y * ST_NCOL;
+  const int per = stream_per(g.K, (int)gridDim.x);
+  const int kb = min(g.K, z * per), ke = min(g.K, kb + per);
+  const float* a = static_cast<const float*>(g.a);
+  const int np = (ke - kb) / 2;  // K ranges are multiples of 4 (K % 4 == 0 is checked)
+  const int col = n_base + 128 * w + 4 * (lane & 31);
+  f32x16 acc[MB][4];
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[mb][j][r] = 0.0f;
+  // the weight through a raw buffer resource at this range's first row (lane offset + pair
+  // stride in bytes; the host checks the range fits 2^31 bytes). The chunk loop is unrolled
+  // whole (ST_NCH chunks, the host bounds the range): with no loop-carried registers the
+  // compiler neither merges a prefetch into a load at its use nor waits for every load at
+  // a loop head, and the scheduling barrier per pair keeps each prefetch where it is
+  // issued, so ST_U pairs stay in flight and each MFMA waits for its own load only.
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(g.b + (int64_t)kb * g.b_ks), 0, 0x7FFFFFF0, kStRsrcWord3);
+  const uint32_t lane_off = (uint32_t)(h * g.b_ks + col) * 4u;
+  const uint32_t pbytes = (uint32_t)(2 * g.b_ks) * 4u;
+  const int last = max(np - 1, 0), nch = (np + ST_U - 1) / ST_U;
+  f32x4 wv[ST_U];
+  // the first ST_U pairs' loads go out before the A fill (their latency overlaps it)
+  if (np > 0) {
+#pragma unroll
+    for (int u = 0; u < ST_U; ++u)
+      wv[u] = __builtin_amdgcn_raw_buffer_load_b128(wr, lane_off + (uint32_t)min(u, last) * pbytes,
+                                                    0, kStAuxNt);
+  }
+  // A slice -> LDS (16-B loads along k, transposed scalar stores), zeros past ke / M
+  const int q_per = stream_rows(per) / 4, total = MR * q_per;
+  if (ke > kb) {
+    // 8 loads in flight per thread (clamped in-range addresses, masked after the load)
+    for (int i0 = 0; i0 < total; i0 += 256 * 8) {
+      f32x4 v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int i = min(i0 + 256 * j + tid, total - 1);
+        const int m = i / q_per, k = kb + 4 * (i - m * q_per);
+        v[j] = *reinterpret_cast<const f32x4*>(a + (int64_t)min(m, g.M - 1) * g.a_rm +
+                                               min(k, ke - 4));
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int i = i0 + 256 * j + tid;
+        if (i >= total) break;
+        const int m = i / q_per, kq = i - m * q_per;
+        const bool ok = m < g.M && kb + 4 * kq < ke;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) as[(4 * kq + e) * LDA + m] = ok ? v[j][e] : 0.0f;
+      }
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int c = 0; c < ST_NCH; ++c) {
+    if (c < nch) {  // uniform; pairs past np read zero A rows (a padded chunk adds 0)
+#pragma unroll
+      for (int u = 0; u < ST_U; ++u) {
+        const int p = c * ST_U + u;
+        const float* ar = as + (2 * p + h) * LDA + (lane & 31);
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb) {
+          const float av = ar[32 * mb];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[mb][j] = mfma32(av, wv[u][j], acc[mb][j]);
+        }
+        if (c + 1 < ST_NCH)
+          wv[u] = __builtin_amdgcn_raw_buffer_load_b128(
+              wr, lane_off + (uint32_t)min(p + ST_U, last) * pbytes, 0, kStAuxNt);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  }
+  // D(row (r&3) + 8 (r>>2) + 4 h, col i = l&31) of MFMA j is C(row, 4 i + j)
+  float* part = g.partials + (int64_t)z * g.M * g.N;
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = 32 * mb + (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (m >= g.M) continue;
+      const f32x4 v = {acc[mb][0][r], acc[mb][1][r], acc[mb][2][r], acc[mb][3][r]};
+      *reinterpret_cast<f32x4*>(part + (int64_t)m * g.N + col) = v;
+    }
+}
+
+// the streaming path's contract: f32 A with plain 16-B aligned rows, n-major 16-B aligned
+// B, M <= 64, N a multiple of 512, K % 4 == 0, a K split of >= 64 ranges whose padded A
+// slice fits 64 KB of LDS (the caller's split count is the grid)
+size_t stream_lds(const XaGemmArgs& g) {
+  const int mr = g.M <= 32 ? 32 : 64;
+  return sizeof(float) * (size_t)stream_rows(stream_per(g.K, g.splits)) * (mr + 1);
+}
+
+// XA_GEMM_STREAM=0 keeps these shapes on the tile kernels (A/B measurements)
+bool stream_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("XA_GEMM_STREAM");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+bool stream_ok(const XaGemmArgs& g) {
+  return !g.force_small && !g.a_ones_row && g.a != nullptr && !g.a_u8 && g.a_pm == 1 &&
+         g.a_pk == 1 && g.a_rk == 1 && g.a_rm % 4 == 0 && ((uintptr_t)g.a & 15) == 0 &&
+         g.b_ns == 1 && g.b_ks % 4 == 0 && ((uintptr_t)g.b & 15) == 0 && g.M <= 64 &&
+         g.N % ST_NCOL == 0 && g.K % 4 == 0 && g.splits >= 64 && g.partials &&
+         ((uintptr_t)g.partials & 15) == 0 && stream_lds(g) <= ST_MAX_LDS &&
+         stream_per(g.K, g.splits) <= 2 * ST_NCH * ST_U &&
+         ((int64_t)stream_per(g.K, g.splits) + 2) * g.b_ks * 4 < (1ll << 31) && stream_on();
+}
+
 // column sums of B (A == NULL, M == 1: bias gradients): rows split over workgroups, each
 // workgroup 4 waves x 64 columns, partial rows summed in fixed order by the split reduce
 __global__ __launch_bounds__(256) void colsum_kernel(XaGemmArgs g) {
@@ -1379,6 +1530,7 @@ extern "C" int xa_gemm(const XaGemmArgs* p, void* stream) {
     return 0;
   }
   dim3 grid((g.M + BM - 1) / BM, (g.N + BN - 1) / BN, g.splits);
+  const bool use_stream = stream_ok(g);
   const bool ak = g.a_pk == 1 && g.a_rk == 1;
   const bool bn = g.b_ns == 1;
   const bool u8 = g.a_u8 != 0;
@@ -1388,7 +1540,13 @@ extern "C" int xa_gemm(const XaGemmArgs* p, void* stream) {
                "xa_gemm: a_ones_row needs the 64 x 64 kernel (xa_gemm_shape == 0), A and M >= 2 "
                "(got shape %d, M %d)", shape, g.M);
   const XaGemmK kg = kernel_args(g);
-  if (shape == 2) {
+  if (use_stream) {
+    const dim3 gs(g.splits, g.N / ST_NCOL);
+    if (g.M <= 32)
+      hipLaunchKernelGGL(gemm_stream_kernel<1>, gs, dim3(256), stream_lds(g), s, g);
+    else
+      hipLaunchKernelGGL(gemm_stream_kernel<2>, gs, dim3(256), stream_lds(g), s, g);
+  } else if (shape == 2) {
     hipLaunchKernelGGL(colsum_kernel, dim3(1, (g.N + 63) / 64, g.splits), dim3(256), 0, s, g);
   } else if (shape == 1) {
     dim3 gs((g.M + 31) / 32, (g.N + 31) / 32, g.splits);

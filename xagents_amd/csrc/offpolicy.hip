@@ -71,8 +71,9 @@ __global__ void dqn_td_kernel(const float* __restrict__ q, const float* __restri
                               const float* __restrict__ q_next_o, const int* __restrict__ act,
                               const float* __restrict__ rew, const float* __restrict__ done,
                               int B, int A, float gamma, float huber, float* __restrict__ dq,
-                              float* __restrict__ loss) {
+                              float* __restrict__ loss, int* __restrict__ adam_step) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (adam_step && b == 0) adam_step[0] += 1;  // the update's t += 1, one launch fewer
   if (b >= B) return;
   const float* qt = q_next_t + (size_t)b * A;
   float v;
@@ -453,13 +454,13 @@ extern "C" int xa_dqn_td_grad(const float* q, const float* q_next_target,
                               const float* q_next_online, const int* actions,
                               const float* rewards, const float* dones, int batch, int n_actions,
                               float gamma, float huber_delta, float* dq, float* loss,
-                              void* stream) {
+                              int* adam_step, void* stream) {
   XA_CHECK_ARG(q && q_next_target && actions && rewards && dones && dq && batch > 0 &&
                    n_actions > 0,
                "xa_dqn_td_grad: bad arguments");
   hipLaunchKernelGGL(dqn_td_kernel, dim3((batch + 63) / 64), dim3(64), 0, (hipStream_t)stream, q,
                      q_next_target, q_next_online, actions, rewards, dones, batch, n_actions,
-                     gamma, huber_delta, dq, loss);
+                     gamma, huber_delta, dq, loss, adam_step);
   XA_CHECK_LAUNCH("xa_dqn_td_grad");
   return 0;
 }

@@ -79,6 +79,8 @@ class DQN(OffPolicy):
         self.ex_online = LayerExecutor(self.model, 2 * B if self.double else B)
         self.ex_target = LayerExecutor(self.target_model, B)
         self.ex_act = LayerExecutor(self.model, self.n_envs)
+        # forward-only executors skip the conv stack's hidden activations
+        self.ex_target.keep_hidden = self.ex_act.keep_hidden = False
         self._sync_params(self.model, self.target_model)
 
     # ---- reference surface ---------------------------------------------------
@@ -135,6 +137,8 @@ class DQN(OffPolicy):
         return [self.xb[:B], self.b_act, self.b_rew, self.b_done, self.xb[B:]]
 
     def _td_grad(self):
+        """TD targets + loss gradient; the same launch bumps the optimizer's t (the update's
+        Adam reads it after the backward)."""
         B = self.batch_size
         q_all = self.ex_online.forward(self.xb if self.double else self.xb[:B])[0]
         q_next_t = self.ex_target.forward(self.xb[B:])[0]
@@ -142,7 +146,8 @@ class DQN(OffPolicy):
         call('xa_dqn_td_grad', q_all.data_ptr(), q_next_t.data_ptr(), q_next_o,
              self.b_act.data_ptr(), self.b_rew.data_ptr(), self.b_done.data_ptr(), B,
              self.n_actions, kernels._f32(self.gamma), kernels._f32(self.huber_delta or 0.0),
-             self.dq.data_ptr(), self.td_loss.data_ptr(), stream())
+             self.dq.data_ptr(), self.td_loss.data_ptr(),
+             self.model.optimizer.iterations.data_ptr(), stream())
 
     # the raw gradient of the dense layers whose Adam step runs inside their weight-gradient
     # GEMM is written to self.grad only on request (the raw-gradient parity tests)
@@ -176,10 +181,9 @@ class DQN(OffPolicy):
         opt = self.model.optimizer
         fl, rest = self._fused_adam_layers()
         if fl:
-            # t += 1 first: the fused epilogues read it; the dense layers' Adam runs inside
-            # the backward, the rest of the parameters in one launch per range
+            # t += 1 happened in _td_grad (the fused epilogues read it); the dense layers'
+            # Adam runs inside the backward, the rest of the parameters in one launch per range
             th, m, v = self.model.theta, opt.m, opt.v
-            call('xa_adam_step_bump', opt.iterations.data_ptr(), stream())
             spec = {i: (adam_apply(th, m, v, opt.iterations, opt, self.ex_online.offsets[i][0]),
                         self.write_raw_grad) for i in fl}
             self.ex_online.backward([self.dq], self.grad, batch=self.batch_size, adam=spec)
@@ -190,7 +194,6 @@ class DQN(OffPolicy):
             return
         self.ex_online.backward([self.dq], self.grad, batch=self.batch_size)
         scale = self._reduce_grad(self.grad)
-        call('xa_adam_step_bump', opt.iterations.data_ptr(), stream())
         kernels.clip_adam(self.model.theta, opt.m, opt.v, self.grad, opt.iterations,
                           opt.learning_rate, opt.beta_1, opt.beta_2, opt.epsilon,
                           clip_norm=0.0, grad_scale=scale, workspace=self.adam_ws)

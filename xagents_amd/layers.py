@@ -8,7 +8,8 @@ is an implicit-im2col GEMM, its weight gradient the same GEMM with the im2col mo
 the reduction index, its input gradient one implicit transposed-conv GEMM
 (`xa_conv1d_dgrad`; a dY W^T GEMM + fixed-order col2im gather, `xa_conv1d_input_grad`,
 when the filter count is not a multiple of 4). Biases, ReLU / tanh and the ReLU gate of the backward
-pass are GEMM epilogues. Image inputs stay uint8 in HBM and are scaled f32(x) / 255 in
+pass are GEMM epilogues. The NatureCNN stack (three Conv1D layers over 84 x 84 x 1 frames)
+runs forward as one fused launch out of LDS (`xa_conv_stack_fwd`, conv_stack.hip). Image inputs stay uint8 in HBM and are scaled f32(x) / 255 in
 the GEMM loader (xagents/base.py:505-506).
 
 Buffers are allocated per batch size and reused; all launches go to torch's current
@@ -20,8 +21,8 @@ import os
 import torch
 
 from xagents_amd import _lib
-from xagents_amd._lib import (XA_ACT_NONE, XA_ACT_RELU, XA_ACT_TANH, XaAdamApply, XaGemmArgs,
-                              call, stream)
+from xagents_amd._lib import (XA_ACT_NONE, XA_ACT_RELU, XA_ACT_TANH, XaAdamApply,
+                              XaConvStackArgs, XaGemmArgs, call, stream)
 
 _FORCE = int(os.environ.get('XA_GEMM_FORCE', '0'))
 _ACTS = {None: XA_ACT_NONE, 'linear': XA_ACT_NONE, 'relu': XA_ACT_RELU, 'tanh': XA_ACT_TANH}
@@ -150,6 +151,41 @@ class LayerExecutor:
         self.wg_floats = [int(lib.xa_conv1d_wgrad_workspace_floats(l.size, l.in_features, l.filters))
                           if l.kind == 'convolutional' else 0 for l in self.layers]
         self.wg_ws = torch.empty(max(self.wg_floats + [1]), **f32)
+        self.stack = self._conv_stack()
+
+    # the forward writes the conv stack's h1 / h2 (the backward's gates and weight-gradient
+    # operands); forward-only executors (acting, target networks) may turn this off
+    keep_hidden = True
+
+    def _conv_stack(self):
+        """True when layers 0-2 are the NatureCNN Conv1D stack over (84, 84, 1) frames
+        (32 x 8 / 4, 64 x 4 / 2, 64 x 3 / 1, ReLU): the forward then runs them as one
+        xa_conv_stack_fwd launch (XA_CONV_STACK=0: per-layer GEMMs)."""
+        import os
+        if os.environ.get('XA_CONV_STACK', '1') == '0' or len(self.layers) < 3:
+            return False
+        want = ((-1, 8, 4, 32, 1), (0, 4, 2, 64, 32), (1, 3, 1, 64, 64))
+        for i, (src, k, st, f, c) in enumerate(want):
+            l = self.layers[i]
+            if (l.kind != 'convolutional' or l.input_index != src or l.size != k or
+                    l.stride != st or l.filters != f or l.in_features != c or
+                    self._act(i) != XA_ACT_RELU):
+                return False
+        return (tuple(self.in_shape[-3:]) == (84, 84, 1) and
+                tuple(self.layers[2].out_shape[-2:]) == (7, 64) and
+                all(self.offsets[i][0] % 4 == 0 for i in range(3)))
+
+    def _conv_stack_fwd(self, x, tp):
+        a = XaConvStackArgs()
+        a.x, a.x_u8 = x.data_ptr(), int(x.dtype == torch.uint8)
+        a.rows = self.B * self.in_shape[-3]
+        (w1, b1), (w2, b2), (w3, b3) = ((int(u), int(v)) for u, v in self.offsets[:3])
+        a.w1, a.b1, a.w2, a.b2 = tp + 4 * w1, tp + 4 * b1, tp + 4 * w2, tp + 4 * b2
+        a.w3, a.b3 = tp + 4 * w3, tp + 4 * b3
+        if self.keep_hidden:
+            a.h1, a.h2 = self.outs[0].data_ptr(), self.outs[1].data_ptr()
+        a.h3 = self.outs[2].data_ptr()
+        call('xa_conv_stack_fwd', ctypes_ref(a), stream())
 
     def _act(self, i):
         """Epilogue of layer i. A softmax output layer (the ACER actor,
@@ -241,8 +277,10 @@ class LayerExecutor:
         tp = theta.data_ptr()
         u8 = x.dtype == torch.uint8
         self.x = x
+        if self.stack:
+            self._conv_stack_fwd(x, tp)
         for i, l in enumerate(self.layers):
-            if l.kind == 'flatten':
+            if l.kind == 'flatten' or (self.stack and i < 3):
                 continue
             j = self._src_layer(i)
             src = x if j == -1 else self.outs[j]

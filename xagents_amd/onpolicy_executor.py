@@ -66,6 +66,7 @@ class ExecutorActorCritic:
         seed = self.seed if self.seed is not None else int(np.random.SeedSequence().entropy % 2**63)
         self.rng_seed = (int(seed) * 1000003 + self.rank * 7919 + 17) % 2**64
         self.ex_roll = LayerExecutor(self.model, N)
+        self.ex_roll.keep_hidden = False  # forward only
         self._sa = XaReplayStepArgs()
         env.fill_step_args(self._sa)
         self._sa.ring_states = None
