@@ -461,6 +461,26 @@ typedef struct XaConvStackArgs {
   float *h1, *h2, *h3;
 } XaConvStackArgs;
 int xa_conv_stack_fwd(const XaConvStackArgs* args, void* stream);
+
+/* The stack's backward in one launch + a fixed-order reduce: from dz3 = dL/d(conv3
+ * pre-activation) [rows][7][64] (h3's ReLU gate applied), the forward's h1 / h2 and the
+ * frames, the gradient of the stack's 20896 parameters [w1 b1 w2 b2 w3 b3] (Keras variable
+ * order, contiguous in theta) into grad (+= when accumulate); no input gradient (the input
+ * is the frame). ws: xa_conv_stack_bwd_workspace_floats(rows) floats. Same values as the
+ * per-layer weight-gradient / transposed-conv GEMMs up to f32 association. */
+typedef struct XaConvStackBwdArgs {
+  const void* x;
+  int x_u8;
+  int rows;
+  const float *w2, *w3;
+  const float *h1, *h2, *dz3;
+  float* ws;
+  size_t ws_floats;
+  float* grad;
+  int accumulate;
+} XaConvStackBwdArgs;
+size_t xa_conv_stack_bwd_workspace_floats(int rows);
+int xa_conv_stack_bwd(const XaConvStackBwdArgs* args, void* stream);
 int xa_gemm_splits(int M, int N, int K);
 /* the kernel shape xa_gemm picks for a tile-path GEMM with `splits` K splits (0 = the
  * 64 x 64 kernel, the only one that takes a_ones_row) */

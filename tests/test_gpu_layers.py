@@ -403,3 +403,36 @@ def test_conv_stack_fused_forward(device, B, u8, monkeypatch):
     for a, b, c in zip(o0, o1, o2):
         _close(b.cpu().numpy(), a.cpu().numpy(), rtol=1e-5)
         assert torch.equal(b, c)
+
+
+@pytest.mark.parametrize('B,Bb,u8,acc', [(2, 2, True, False), (5, 3, True, True),
+                                         (37, 37, False, False), (64, 64, True, False)])
+def test_conv_stack_fused_backward(device, B, Bb, u8, acc, monkeypatch):
+    """xa_conv_stack_bwd (the stack's weight / bias gradients in one launch + a fixed-order
+    reduce) against the per-layer GEMM backward on the same forward: all six parameter
+    tensors at 1e-5 of their scale, a leading-rows batch (Bb < B), accumulate=True, ragged
+    last groups; the dense layers' gradients are untouched by the switch (bitwise)."""
+    from xagents_amd.layers import LayerExecutor
+    model = _model(ROOT / 'xagents_amd' / 'dqn/models/cnn.cfg', [6], (84, 84, 1), device)
+    rng = np.random.default_rng(100 + B)
+    x = (rng.integers(0, 256, size=(B, 84, 84, 1), dtype=np.uint8) if u8 else
+         rng.random(size=(B, 84, 84, 1)).astype(np.float32))
+    xt = torch.from_numpy(x).to(device)
+    ex = LayerExecutor(model, B)
+    assert ex.stack and ex._stack_bwd_ok()
+    outs = ex.forward(xt)
+    d = torch.from_numpy(rng.normal(size=(Bb, 6)).astype(np.float32)).to(device)
+    base = torch.from_numpy(rng.normal(size=model.n_params).astype(np.float32)).to(device)
+    grads = []
+    for flag in ('0', '1'):
+        monkeypatch.setenv('XA_CONV_STACK_BWD', flag)
+        g = base.clone() if acc else torch.zeros_like(base)
+        ex.backward([d], g, batch=Bb, accumulate=acc)
+        grads.append(g.cpu().numpy())
+    ref, got = grads
+    n_conv = ex.offsets[2][1] + model.layers[2].filters
+    for i in range(3):
+        (w0, b0), l = ex.offsets[i], model.layers[i]
+        for lo, hi in ((w0, b0), (b0, b0 + l.filters)):
+            _close(got[lo:hi], ref[lo:hi], rtol=1e-5)
+    assert np.array_equal(got[n_conv:], ref[n_conv:])

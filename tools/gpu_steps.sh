@@ -21,6 +21,8 @@
 #   layers   tests/test_gpu_layers.py (GEMM paths, layer executor)
 #   streamab C3 bench lines, streaming dense forward on / off, interleaved
 #   stackab  C3 bench lines, fused conv-stack forward on / off, interleaved
+#   bwdab    C3 / C4 bench lines, fused conv-stack backward on / off
+#   cnn      CNN on-policy, ACER and Atari GPU tests
 #   gemm     GEMM tests, small-M timings, PMC passes on the dense dX GEMM
 #   icache   instruction-cache counters of the 16-env update
 #   stamps   per-phase stamp shares of the persistent update (tools/diag_ppo_update.py)
@@ -95,6 +97,17 @@ for step in "$@"; do
       XA_CONV_STACK=0 run sk_off1 300 $B
       run sk_on2 300 $B
       XA_CONV_STACK=0 run sk_off2 300 $B ;;
+    bwdab)
+      # the fused conv-stack backward vs per-layer GEMMs (XA_CONV_STACK_BWD=0): C3 x2, C4 x1
+      B="python bench.py --config c3 --steps 30 --warmup 5 --cpu-baseline-seconds 0"
+      run bw_on1 300 $B
+      XA_CONV_STACK_BWD=0 run bw_off1 300 $B
+      run bw_on2 300 $B
+      XA_CONV_STACK_BWD=0 run bw_off2 300 $B
+      B4="python bench.py --config c4 --steps 3 --warmup 1 --cpu-baseline-seconds 0"
+      run bw4_on 400 $B4
+      XA_CONV_STACK_BWD=0 run bw4_off 400 $B4 ;;
+    cnn) run_pytest cnn 600 tests/test_gpu_cnn_onpolicy.py tests/test_gpu_acer.py tests/test_gpu_atari.py ;;
     dqn) run_pytest dqn 400 tests/test_gpu_dqn.py tests/test_gpu_scale.py -k "dqn" tests/test_gpu_configs.py::test_c3_dqn_32_envs_rb1_1m_batch_64 ;;
     td3time)
       # wall time per gradient step on the product build, per-phase barrier times on the

@@ -215,6 +215,15 @@ class XaConvStackArgs(Structure):
     ]
 
 
+class XaConvStackBwdArgs(Structure):
+    _fields_ = [
+        ('x', c_void_p), ('x_u8', c_int), ('rows', c_int),
+        ('w2', c_void_p), ('w3', c_void_p),
+        ('h1', c_void_p), ('h2', c_void_p), ('dz3', c_void_p),
+        ('ws', c_void_p), ('ws_floats', ctypes.c_size_t), ('grad', c_void_p), ('accumulate', c_int),
+    ]
+
+
 class XaAtariStepArgs(Structure):
     _fields_ = [
         ('n_envs', c_int), ('t_raw', c_int), ('height', c_int), ('width', c_int),
@@ -419,6 +428,8 @@ _SIGNATURES = {
     'xa_gemm': (c_int, [POINTER(XaGemmArgs), c_void_p]),
     'xa_gemm_adam': (c_int, [POINTER(XaGemmArgs), POINTER(XaAdamApply), c_void_p]),
     'xa_conv_stack_fwd': (c_int, [POINTER(XaConvStackArgs), c_void_p]),
+    'xa_conv_stack_bwd': (c_int, [POINTER(XaConvStackBwdArgs), c_void_p]),
+    'xa_conv_stack_bwd_workspace_floats': (ctypes.c_size_t, [c_int]),
     'xa_gemm_splits': (c_int, [c_int, c_int, c_int]),
     'xa_gemm_shape': (c_int, [c_int, c_int, c_int, c_int]),
     'xa_gemm_workspace_floats': (ctypes.c_size_t, [c_int, c_int, c_int, c_int]),

@@ -48,20 +48,23 @@ static_assert(CK1 * 1 == 8 && CF1 == 32 && CF2 == 64 && CF3 == 64, "tile mapping
 
 // the 4 input values of item i (row i / 21, pixels 4 (i % 21) ..) of the group at row0;
 // rows past the batch read as 0
-XA_DEV f32x4 load_x4(const XaConvStackArgs& p, int row0, int i) {
+XA_DEV f32x4 load_x4(const void* x, int x_u8, int rows, int row0, int i) {
   const int r = i / (CW0 / 4), c = i - r * (CW0 / 4);
   f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
-  if (row0 + r < p.rows) {
+  if (row0 + r < rows) {
     const int64_t off = (int64_t)(row0 + r) * CW0 + 4 * c;
-    if (p.x_u8) {
-      const uint32_t u = *reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(p.x) + off);
+    if (x_u8) {
+      const uint32_t u = *reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(x) + off);
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] = (float)((u >> (8 * e)) & 0xFFu) / 255.0f;
     } else {
-      v = *reinterpret_cast<const f32x4*>(static_cast<const float*>(p.x) + off);
+      v = *reinterpret_cast<const f32x4*>(static_cast<const float*>(x) + off);
     }
   }
   return v;
+}
+XA_DEV f32x4 load_x4(const XaConvStackArgs& p, int row0, int i) {
+  return load_x4(p.x, p.x_u8, p.rows, row0, i);
 }
 
 XA_DEV void store_x4(float* xs, int i, f32x4 v) {
@@ -212,6 +215,334 @@ __global__ __launch_bounds__(256) void conv_stack_fwd_kernel(XaConvStackArgs p) 
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// Fused backward of the same stack. Input: dZ3 = dL/d(conv3 pre-activation) [rows][7][64]
+// (the dense layer's input gradient with h3's ReLU gate applied), the forward's h1 / h2 and
+// the frames. Per 16-sequence group, out of LDS (x, h1, h2, dZ3: 121 KB):
+//   (a) dW3 += im2col(h2)^T dZ3, db3 += colsum dZ3
+//   (b) dZ2 = (dZ3 (*) W3^T, transposed conv) . [h2 > 0]       -> over h2 in place
+//   (c) dW2 += im2col(h1)^T dZ2, db2 += colsum dZ2
+//   (d) dZ1 = (dZ2 (*) W2^T, stride-2 transposed conv) . [h1 > 0] -> over h1 in place;
+//       output position 2 h + par takes taps t = 2 s + par from dZ2 rows h - s (s = 0, 1),
+//       so each wave's (par, 16-channel) tile is a K = 2 x 64 GEMM with no zero taps
+//   (e) dW1 += im2col(x)^T dZ1, db1 += colsum dZ1
+// Weight-gradient tiles stay in registers over all of a workgroup's groups (wave w owns
+// filter columns 16 w .. of dW3 / dW2); the dgrad phases keep their 16-column slice of
+// W3^T / W2^T in registers as the forward does. Each workgroup writes its partial
+// [w1 b1 w2 b2 w3 b3] (20896 floats, theta order) to ws[blockIdx]; a second launch sums
+// the partials in workgroup order (deterministic) into the gradient (+= when accumulate).
+// ---------------------------------------------------------------------------
+constexpr int LD3 = CF3 + 4;
+constexpr int NW1 = CK1 * CF1, NB1 = CF1;                // 256, 32
+constexpr int NW2 = CK2 * CF1 * CF2, NB2 = CF2;          // 8192, 64
+constexpr int NW3 = CK3 * CF2 * CF3, NB3 = CF3;          // 12288, 64
+constexpr int OW1 = 0, OB1 = NW1, OW2 = OB1 + NB1, OB2 = OW2 + NW2, OW3 = OB2 + NB2,
+              OB3 = OW3 + NW3, NPAR = OB3 + NB3;         // 20896
+constexpr int KT3 = CK3 * CF2 / 16, KT2 = CK2 * CF1 / 16;  // 12, 8 weight-gradient k tiles
+constexpr int HH = CP1 / 2;                              // 10 output pairs of conv1
+
+
+// LDS rows [m][LD] <- global rows [m][C] (m < valid; later rows 0), NT float4 per thread:
+// stage_load issues the loads (clamped to the valid rows), stage_store masks and stores
+template <int NT, int C>
+XA_DEV void stage_load(f32x4 (&v)[NT], const float* src, int valid) {
+  const f32x4* g = reinterpret_cast<const f32x4*>(src);
+  const int last = valid * (C / 4) - 1;  // >= 0: a group holds >= 1 row
+#pragma unroll
+  for (int u = 0; u < NT; ++u) v[u] = g[min((int)threadIdx.x + 256 * u, last)];
+}
+template <int NT, int C, int LD>
+XA_DEV void stage_store(float* dst, const f32x4 (&v)[NT], int valid) {
+  const int last = valid * (C / 4) - 1;
+#pragma unroll
+  for (int u = 0; u < NT; ++u) {
+    const int i = threadIdx.x + 256 * u, m = i / (C / 4), c = 4 * (i - m * (C / 4));
+    *reinterpret_cast<f32x4*>(dst + m * LD + c) = i <= last ? v[u] : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  }
+}
+constexpr int NT1 = M1 * CF1 / 4 / 256, NT2 = M2 * CF2 / 4 / 256, NT3 = M3 * CF3 / 4 / 256;
+static_assert(NT1 * 1024 == M1 * CF1 && NT2 * 1024 == M2 * CF2 && NT3 * 1024 == M3 * CF3,
+              "whole float4 rounds per thread");
+
+__global__ __launch_bounds__(256) void conv_stack_bwd_kernel(XaConvStackBwdArgs p) {
+  __shared__ __attribute__((aligned(16))) float xs[CR * CW0];
+  __shared__ __attribute__((aligned(16))) float h1s[M1 * LD1];  // h1, then dZ1
+  __shared__ __attribute__((aligned(16))) float h2s[M2 * LD2];  // h2, then dZ2
+  __shared__ __attribute__((aligned(16))) float d3s[M3 * LD3];  // dZ3
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, q = lane >> 4, i16 = lane & 15;
+  const int G = (p.rows + CR - 1) / CR;
+
+  // (b) / (d) B operands: W3^T columns cb = 16 w + i16 (k = (t, n) = 16 kb + 4 q + j) and
+  // W2^T for parity par = w >> 1, channels cd = 16 (w & 1) + i16 (k = (s, n), tap 2 s + par);
+  // re-read (L2) at their phase so they do not hold registers through the others
+  const int cb = 16 * w + i16, par = w >> 1, cd = 16 * (w & 1) + i16;
+  const f32x4 z4 = {0.0f, 0.0f, 0.0f, 0.0f};
+  f32x4 g3[KT3], g2[KT2], g1 = z4;
+#pragma unroll
+  for (int i = 0; i < KT3; ++i) g3[i] = z4;
+#pragma unroll
+  for (int i = 0; i < KT2; ++i) g2[i] = z4;
+  float bs3 = 0.0f, bs2 = 0.0f, bs1 = 0.0f;
+
+  for (int gi = blockIdx.x; gi < G; gi += gridDim.x) {
+    const int row0 = gi * CR;
+    const int nrow = min(CR, p.rows - row0);
+    // ---- stage x, h1, h2, dZ3 (rows past the batch read as 0); every load of the group
+    // goes out before the first store (a load per loop trip behind a branch waited out one
+    // memory latency each) ----
+    {
+      f32x4 v1[NT1], v2[NT2], v3[NT3], vx[2];
+      stage_load<NT1, CF1>(v1, p.h1 + (int64_t)row0 * CP1 * CF1, nrow * CP1);
+      stage_load<NT2, CF2>(v2, p.h2 + (int64_t)row0 * CP2 * CF2, nrow * CP2);
+      stage_load<NT3, CF3>(v3, p.dz3 + (int64_t)row0 * CP3 * CF3, nrow * CP3);
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+        vx[u] = load_x4(p.x, p.x_u8, p.rows, row0, min(tid + 256 * u, XQ - 1));
+      stage_store<NT1, CF1, LD1>(h1s, v1, nrow * CP1);
+      stage_store<NT2, CF2, LD2>(h2s, v2, nrow * CP2);
+      stage_store<NT3, CF3, LD3>(d3s, v3, nrow * CP3);
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+        if (tid + 256 * u < XQ) store_x4(xs, tid + 256 * u, vx[u]);
+    }
+    __syncthreads();
+    // ---- (a) dW3 [k = (t, c)][n]: rows 16 kt + i16 of tile kt, K = the group's m3 ----
+    for (int mb = 0; mb < M3 / 16; ++mb) {
+      float bq[4];
+      int rb[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = 16 * mb + 4 * q + j, r = m / CP3, pp = m - r * CP3;
+        bq[j] = d3s[m * LD3 + 16 * w + i16];
+        rb[j] = (r * CP2 + pp) * LD2;
+        bs3 += bq[j];
+      }
+      // A of row j + 1 (12 k tiles) is read while row j's 12 MFMAs run (pinned: the
+      // scheduler otherwise reads one pair of A values at a time right before its MFMAs)
+      float av[2][KT3];
+      auto koff3 = [&](int kt) { return (kt >> 2) * LD2 + ((kt & 3) << 4) + i16; };
+#pragma unroll
+      for (int kt = 0; kt < KT3; ++kt) av[0][kt] = h2s[rb[0] + koff3(kt)];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (j < 3) {
+#pragma unroll
+          for (int kt = 0; kt < KT3; ++kt) av[(j + 1) & 1][kt] = h2s[rb[j + 1] + koff3(kt)];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int kt = 0; kt < KT3; ++kt) g3[kt] = mfma4(av[j & 1][kt], bq[j], g3[kt]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    __syncthreads();  // (a) has read h2
+    // ---- (b) dZ2 = transposed conv3 of dZ3, gated by h2 > 0, over h2; two M tiles per
+    // pass (M2 / 16 = 9: the last pass repeats tile 8 and skips its store) ----
+    {
+      float wb3[KT3][4];
+#pragma unroll
+      for (int kb = 0; kb < KT3; ++kb)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          wb3[kb][j] = p.w3[((kb >> 2) * CF2 + cb) * CF3 + ((kb & 3) << 4) + 4 * q + j];
+      for (int mt = 0; mt < M2 / 16; mt += 2) {
+        int r[2], p2[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int m = 16 * min(mt + u, M2 / 16 - 1) + i16;
+          r[u] = m / CP2;
+          p2[u] = m - r[u] * CP2;
+        }
+        f32x4 acc[2] = {z4, z4};
+#pragma unroll
+        for (int kb = 0; kb < KT3; ++kb) {
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            const int p3 = p2[u] - (kb >> 2);
+            const f32x4 a = (p3 >= 0 && p3 < CP3)
+                                ? *reinterpret_cast<const f32x4*>(d3s + (r[u] * CP3 + p3) * LD3 +
+                                                                  ((kb & 3) << 4) + 4 * q)
+                                : z4;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[u] = mfma4(a[j], wb3[kb][j], acc[u]);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          if (mt + u >= M2 / 16) break;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float* hp = h2s + (16 * (mt + u) + 4 * q + e) * LD2 + cb;
+            *hp = *hp > 0.0f ? acc[u][e] : 0.0f;
+          }
+        }
+      }
+    }
+    __syncthreads();  // dZ2 complete
+    // ---- (c) dW2 [k = (t, c)][n] over the group's m2 ----
+    for (int mb = 0; mb < M2 / 16; ++mb) {
+      float bq[4];
+      int rb[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = 16 * mb + 4 * q + j, r = m / CP2, pp = m - r * CP2;
+        bq[j] = h2s[m * LD2 + 16 * w + i16];
+        rb[j] = (r * CP1 + CS2 * pp) * LD1;
+        bs2 += bq[j];
+      }
+      float av[2][KT2];  // as in (a)
+      auto koff2 = [&](int kt) { return (kt >> 1) * LD1 + ((kt & 1) << 4) + i16; };
+#pragma unroll
+      for (int kt = 0; kt < KT2; ++kt) av[0][kt] = h1s[rb[0] + koff2(kt)];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (j < 3) {
+#pragma unroll
+          for (int kt = 0; kt < KT2; ++kt) av[(j + 1) & 1][kt] = h1s[rb[j + 1] + koff2(kt)];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int kt = 0; kt < KT2; ++kt) g2[kt] = mfma4(av[j & 1][kt], bq[j], g2[kt]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    __syncthreads();  // (c) has read h1
+    // ---- (d) dZ1 = transposed conv2 of dZ2, gated by h1 > 0, over h1; two M tiles per
+    // pass (CR HH / 16 = 10) ----
+    {
+      float wb2[KT2][4];
+#pragma unroll
+      for (int kb = 0; kb < KT2; ++kb)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          wb2[kb][j] =
+              p.w2[((2 * (kb >> 2) + par) * CF1 + cd) * CF2 + ((kb & 3) << 4) + 4 * q + j];
+      static_assert((CR * HH / 16) % 2 == 0, "pairs of M tiles");
+      for (int mt = 0; mt < CR * HH / 16; mt += 2) {
+        int r[2], hh[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int m = 16 * (mt + u) + i16;
+          r[u] = m / HH;
+          hh[u] = m - r[u] * HH;
+        }
+        f32x4 acc[2] = {z4, z4};
+#pragma unroll
+        for (int kb = 0; kb < KT2; ++kb) {
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            const int p2 = hh[u] - (kb >> 2);
+            const f32x4 a = (p2 >= 0 && p2 < CP2)
+                                ? *reinterpret_cast<const f32x4*>(h2s + (r[u] * CP2 + p2) * LD2 +
+                                                                  ((kb & 3) << 4) + 4 * q)
+                                : z4;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[u] = mfma4(a[j], wb2[kb][j], acc[u]);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int mo = 16 * (mt + u) + 4 * q + e, ro = mo / HH, ho = mo - ro * HH;
+            float* hp = h1s + (ro * CP1 + 2 * ho + par) * LD1 + cd;
+            *hp = *hp > 0.0f ? acc[u][e] : 0.0f;
+          }
+      }
+    }
+    __syncthreads();  // dZ1 complete
+    // ---- (e) dW1 [k1 (8 of the tile's 16 rows)][n1]: wave w -> n tile w & 1, m blocks of
+    // parity w >> 1 ----
+    for (int mb = par; mb < M1 / 16; mb += 2) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = 16 * mb + 4 * q + j, r = m / CP1, pp = m - r * CP1;
+        const float b = h1s[m * LD1 + cd];
+        const float a = i16 < CK1 ? xs[r * CW0 + CS1 * pp + i16] : 0.0f;
+        g1 = mfma4(a, b, g1);
+        bs1 += b;
+      }
+    }
+    __syncthreads();  // LDS free for the next group
+  }
+
+  // ---- this workgroup's partial gradient -> ws[blockIdx.x][NPAR] ----
+  float* out = p.ws + (int64_t)blockIdx.x * NPAR;
+#pragma unroll
+  for (int kt = 0; kt < KT3; ++kt)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) out[OW3 + (16 * kt + 4 * q + e) * CF3 + 16 * w + i16] = g3[kt][e];
+#pragma unroll
+  for (int kt = 0; kt < KT2; ++kt)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) out[OW2 + (16 * kt + 4 * q + e) * CF2 + 16 * w + i16] = g2[kt][e];
+  // the small pieces combine lanes / waves in fixed order through LDS
+  float* red = h1s;
+  red[tid] = bs3;
+  red[256 + tid] = bs2;
+  red[512 + tid] = bs1;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) red[768 + e * 256 + tid] = g1[e];
+  __syncthreads();
+  if (tid < CF3) {  // db3 / db2: column n = 16 w + i16 summed over its wave's 4 lane groups
+    const int wn = tid >> 4, ln = tid & 15;
+    float s3 = 0.0f, s2 = 0.0f;
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq) {
+      s3 += red[wn * 64 + qq * 16 + ln];
+      s2 += red[256 + wn * 64 + qq * 16 + ln];
+    }
+    out[OB3 + tid] = s3;
+    out[OB2 + tid] = s2;
+  }
+  if (tid < CF1) {  // db1: column 16 (w & 1) + i16 over lane groups and both parities
+    const int wt = tid >> 4, ln = tid & 15;
+    float s1 = 0.0f;
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr)
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) s1 += red[512 + (2 * pr + wt) * 64 + qq * 16 + ln];
+    out[OB1 + tid] = s1;
+  }
+  if (tid < NW1) {  // dW1 [k1][n1]: D rows k1 = 4 q + e (q < 2) of waves wt and wt + 2
+    const int k1 = tid / CF1, n1 = tid - k1 * CF1, wt = n1 >> 4, ln = n1 & 15;
+    const int qq = k1 >> 2, e = k1 & 3;
+    float s = 0.0f;
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) s += red[768 + e * 256 + (2 * pr + wt) * 64 + qq * 16 + ln];
+    out[OW1 + tid] = s;
+  }
+}
+
+// grad[e] (+)= sum over workgroups z of ws[z][e]: 4 waves per 64 elements, wave v sums the
+// z slice [v nz / 4, (v + 1) nz / 4) in order, the slices combined in order
+__global__ __launch_bounds__(256) void conv_stack_bwd_reduce_kernel(const float* __restrict__ ws,
+                                                                    int nz, float* __restrict__ grad,
+                                                                    int accumulate) {
+  __shared__ float part[4][64];
+  const int lane = threadIdx.x & 63, v = threadIdx.x >> 6, e = blockIdx.x * 64 + lane;
+  const int z0 = v * nz / 4, z1 = (v + 1) * nz / 4;
+  float s = 0.0f;
+  if (e < NPAR) {
+    int z = z0;
+    for (; z + 8 <= z1; z += 8) {
+      float t[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) t[u] = ws[(int64_t)(z + u) * NPAR + e];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += t[u];
+    }
+    for (; z < z1; ++z) s += ws[(int64_t)z * NPAR + e];
+  }
+  part[v][lane] = s;
+  __syncthreads();
+  if (v == 0 && e < NPAR) {
+    const float t = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
+    grad[e] = accumulate ? grad[e] + t : t;
+  }
+}
+
 int cu_count() {
   static int cus = [] {
     int dev = 0, n = 0;
@@ -236,5 +567,31 @@ extern "C" int xa_conv_stack_fwd(const XaConvStackArgs* a, void* stream) {
   const int grid = G < cu_count() ? G : cu_count();
   hipLaunchKernelGGL(conv_stack_fwd_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, p);
   XA_CHECK_LAUNCH("xa_conv_stack_fwd");
+  return 0;
+}
+
+extern "C" size_t xa_conv_stack_bwd_workspace_floats(int rows) {
+  const int G = (rows + CR - 1) / CR;
+  return (size_t)(G < cu_count() ? G : cu_count()) * NPAR;
+}
+
+extern "C" int xa_conv_stack_bwd(const XaConvStackBwdArgs* a, void* stream) {
+  XA_CHECK_ARG(a != nullptr, "xa_conv_stack_bwd: null args");
+  const XaConvStackBwdArgs& p = *a;
+  XA_CHECK_ARG(p.x && p.w2 && p.w3 && p.h1 && p.h2 && p.dz3 && p.ws && p.grad && p.rows > 0,
+               "xa_conv_stack_bwd: null operand or rows <= 0");
+  XA_CHECK_ARG(((uintptr_t)p.x & (p.x_u8 ? 3 : 15)) == 0 &&
+                   (((uintptr_t)p.h1 | (uintptr_t)p.h2 | (uintptr_t)p.dz3) & 15) == 0,
+               "xa_conv_stack_bwd: x, h1, h2, dz3 misaligned");
+  XA_CHECK_ARG(p.ws_floats >= xa_conv_stack_bwd_workspace_floats(p.rows),
+               "xa_conv_stack_bwd: workspace of %zu floats needed",
+               xa_conv_stack_bwd_workspace_floats(p.rows));
+  const int G = (p.rows + CR - 1) / CR;
+  const int grid = G < cu_count() ? G : cu_count();
+  hipLaunchKernelGGL(conv_stack_bwd_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, p);
+  XA_CHECK_LAUNCH("xa_conv_stack_bwd");
+  hipLaunchKernelGGL(conv_stack_bwd_reduce_kernel, dim3((NPAR + 63) / 64), dim3(256), 0,
+                     (hipStream_t)stream, p.ws, grid, p.grad, p.accumulate);
+  XA_CHECK_LAUNCH("xa_conv_stack_bwd (reduce)");
   return 0;
 }

@@ -22,7 +22,7 @@ import torch
 
 from xagents_amd import _lib
 from xagents_amd._lib import (XA_ACT_NONE, XA_ACT_RELU, XA_ACT_TANH, XaAdamApply,
-                              XaConvStackArgs, XaGemmArgs, call, stream)
+                              XaConvStackArgs, XaConvStackBwdArgs, XaGemmArgs, call, stream)
 
 _FORCE = int(os.environ.get('XA_GEMM_FORCE', '0'))
 _ACTS = {None: XA_ACT_NONE, 'linear': XA_ACT_NONE, 'relu': XA_ACT_RELU, 'tanh': XA_ACT_TANH}
@@ -152,6 +152,9 @@ class LayerExecutor:
                           if l.kind == 'convolutional' else 0 for l in self.layers]
         self.wg_ws = torch.empty(max(self.wg_floats + [1]), **f32)
         self.stack = self._conv_stack()
+        # the fused stack backward's per-workgroup partials (allocated on first use; executors
+        # that run one at a time may share one, as they share `workspace`)
+        self.stack_ws = None
 
     # the forward writes the conv stack's h1 / h2 (the backward's gates and weight-gradient
     # operands); forward-only executors (acting, target networks) may turn this off
@@ -186,6 +189,43 @@ class LayerExecutor:
             a.h1, a.h2 = self.outs[0].data_ptr(), self.outs[1].data_ptr()
         a.h3 = self.outs[2].data_ptr()
         call('xa_conv_stack_fwd', ctypes_ref(a), stream())
+
+    def _conv_stack_bwd(self, Bb, gp, accumulate):
+        """Layers 2..0's parameter gradient in one fused launch + reduce (xa_conv_stack_bwd)
+        from douts[2] (conv3's gated output gradient) and the forward's h1 / h2."""
+        rows = Bb * self.in_shape[-3]
+        lib = _lib.load()
+        need = int(lib.xa_conv_stack_bwd_workspace_floats(int(self.B * self.in_shape[-3])))
+        if self.stack_ws is None or self.stack_ws.numel() < need:
+            self.stack_ws = torch.empty(need, dtype=torch.float32, device=self.dev)
+        tp = self.model.theta.data_ptr()
+        (w1, _), (w2, _), (w3, _) = ((int(u), int(v)) for u, v in self.offsets[:3])
+        a = XaConvStackBwdArgs()
+        a.x, a.x_u8, a.rows = self.x.data_ptr(), int(self.x.dtype == torch.uint8), int(rows)
+        a.w2, a.w3 = tp + 4 * w2, tp + 4 * w3
+        a.h1, a.h2, a.dz3 = (self.outs[0].data_ptr(), self.outs[1].data_ptr(),
+                             self.douts[2].data_ptr())
+        a.ws, a.ws_floats = self.stack_ws.data_ptr(), self.stack_ws.numel()
+        a.grad, a.accumulate = gp + 4 * w1, int(accumulate)
+        call('xa_conv_stack_bwd', ctypes_ref(a), stream())
+
+    def _stack_bwd_ok(self):
+        """The fused backward covers layers 0-2 when they are the stack, contiguous in theta
+        ([w1 b1 w2 b2 w3 b3]), and the forward kept h1 / h2 (XA_CONV_STACK_BWD=0: per
+        layer)."""
+        if not self.stack or not self.keep_hidden or \
+                os.environ.get('XA_CONV_STACK_BWD', '1') == '0':
+            return False
+        end = None
+        for i in range(3):
+            w0, b0 = self.offsets[i]
+            l = self.layers[i]
+            if end is not None and w0 != end:
+                return False
+            if b0 != w0 + l.size * l.in_features * l.filters:
+                return False
+            end = b0 + l.filters
+        return True
 
     def _act(self, i):
         """Epilogue of layer i. A softmax output layer (the ACER actor,
@@ -392,6 +432,13 @@ class LayerExecutor:
                          self.douts[i].data_ptr(), stream())
                 dz[i] = self.douts[i]
             d = dz[i]
+            if i == 2 and gp is not None and self._stack_bwd_ok():
+                # the whole conv stack at once; layers finish in reverse order as below
+                self._conv_stack_bwd(Bb, gp, accumulate)
+                if on_grad is not None:
+                    for k in (2, 1, 0):
+                        on_grad(self.offsets[k][0])
+                break
             j = self._src_layer(i)
             src = self.x if j == -1 else self.outs[j]
             src_u8 = u8 and j == -1
