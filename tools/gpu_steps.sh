@@ -23,6 +23,8 @@
 #   stackab  C3 bench lines, fused conv-stack forward on / off, interleaved
 #   bwdab    C3 / C4 bench lines, fused conv-stack backward on / off
 #   cnn      CNN on-policy, ACER and Atari GPU tests
+#   cstamps  per-phase stamps of the fused conv backward (tools/conv_stack_stamps.py; build
+#            tools/diag_lib/libxa_cstamp.so first: tools/build_variant.py cstamp -DXA_STAMPS --src conv_stack)
 #   gemm     GEMM tests, small-M timings, PMC passes on the dense dX GEMM
 #   icache   instruction-cache counters of the 16-env update
 #   stamps   per-phase stamp shares of the persistent update (tools/diag_ppo_update.py)
@@ -107,6 +109,7 @@ for step in "$@"; do
       B4="python bench.py --config c4 --steps 3 --warmup 1 --cpu-baseline-seconds 0"
       run bw4_on 400 $B4
       XA_CONV_STACK_BWD=0 run bw4_off 400 $B4 ;;
+    cstamps) XA_LIB=tools/diag_lib/libxa_cstamp.so run cstamps 200 python tools/conv_stack_stamps.py 64 1024 ;;
     cnn) run_pytest cnn 600 tests/test_gpu_cnn_onpolicy.py tests/test_gpu_acer.py tests/test_gpu_atari.py ;;
     dqn) run_pytest dqn 400 tests/test_gpu_dqn.py tests/test_gpu_scale.py -k "dqn" tests/test_gpu_configs.py::test_c3_dqn_32_envs_rb1_1m_batch_64 ;;
     td3time)

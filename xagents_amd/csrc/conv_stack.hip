@@ -241,6 +241,13 @@ constexpr int OW1 = 0, OB1 = NW1, OW2 = OB1 + NB1, OB2 = OW2 + NW2, OW3 = OB2 + 
               OB3 = OW3 + NW3, NPAR = OB3 + NB3;         // 20896
 constexpr int KT3 = CK3 * CF2 / 16, KT2 = CK2 * CF1 / 16;  // 12, 8 weight-gradient k tiles
 constexpr int HH = CP1 / 2;                              // 10 output pairs of conv1
+// the backward's dZ3 / h2 rows per sequence with zero rows around them, so the transposed
+// convolutions read out-of-range taps as zeros instead of selecting (a select waits for its
+// LDS read on the spot): dZ3 rows p3 = -2 .. 8 (taps of (b)), h2 rows p2 = -1 .. 9 ((d))
+constexpr int D3B = CK3 - 1, D3R = CP3 + 2 * D3B;       // 2 before, 11 per sequence
+constexpr int H2B = 1, H2R = CP2 + 2 * H2B;              // 1 before, 11 per sequence
+XA_DEV int d3row(int m) { return (m / CP3) * D3R + D3B + m % CP3; }
+XA_DEV int h2row(int m) { return (m / CP2) * H2R + H2B + m % CP2; }
 
 
 // LDS rows [m][LD] <- global rows [m][C] (m < valid; later rows 0), NT float4 per thread:
@@ -252,13 +259,15 @@ XA_DEV void stage_load(f32x4 (&v)[NT], const float* src, int valid) {
 #pragma unroll
   for (int u = 0; u < NT; ++u) v[u] = g[min((int)threadIdx.x + 256 * u, last)];
 }
-template <int NT, int C, int LD>
+template <int NT, int C, int LD, int P = 1, int PR = 1, int PB = 0>
 XA_DEV void stage_store(float* dst, const f32x4 (&v)[NT], int valid) {
+  // row m of the group -> LDS row (m / P) PR + PB + m % P (the padded layouts)
   const int last = valid * (C / 4) - 1;
 #pragma unroll
   for (int u = 0; u < NT; ++u) {
     const int i = threadIdx.x + 256 * u, m = i / (C / 4), c = 4 * (i - m * (C / 4));
-    *reinterpret_cast<f32x4*>(dst + m * LD + c) = i <= last ? v[u] : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    const int row = (m / P) * PR + PB + m % P;
+    *reinterpret_cast<f32x4*>(dst + row * LD + c) = i <= last ? v[u] : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
   }
 }
 constexpr int NT1 = M1 * CF1 / 4 / 256, NT2 = M2 * CF2 / 4 / 256, NT3 = M3 * CF3 / 4 / 256;
@@ -268,10 +277,12 @@ static_assert(NT1 * 1024 == M1 * CF1 && NT2 * 1024 == M2 * CF2 && NT3 * 1024 == 
 __global__ __launch_bounds__(256) void conv_stack_bwd_kernel(XaConvStackBwdArgs p) {
   __shared__ __attribute__((aligned(16))) float xs[CR * CW0];
   __shared__ __attribute__((aligned(16))) float h1s[M1 * LD1];  // h1, then dZ1
-  __shared__ __attribute__((aligned(16))) float h2s[M2 * LD2];  // h2, then dZ2
-  __shared__ __attribute__((aligned(16))) float d3s[M3 * LD3];  // dZ3
+  __shared__ __attribute__((aligned(16))) float h2s[CR * H2R * LD2];  // h2, then dZ2 (padded)
+  __shared__ __attribute__((aligned(16))) float d3s[CR * D3R * LD3];  // dZ3 (padded)
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, q = lane >> 4, i16 = lane & 15;
   const int G = (p.rows + CR - 1) / CR;
+  XA_STAMP_DECL  // diagnostic build only (-DXA_STAMPS, tools/conv_stack_stamps.py)
+  XA_STAMP(7);
 
   // (b) / (d) B operands: W3^T columns cb = 16 w + i16 (k = (t, n) = 16 kb + 4 q + j) and
   // W2^T for parity par = w >> 1, channels cd = 16 (w & 1) + i16 (k = (s, n), tap 2 s + par);
@@ -284,6 +295,10 @@ __global__ __launch_bounds__(256) void conv_stack_bwd_kernel(XaConvStackBwdArgs 
 #pragma unroll
   for (int i = 0; i < KT2; ++i) g2[i] = z4;
   float bs3 = 0.0f, bs2 = 0.0f, bs1 = 0.0f;
+  // the pad rows stay zero (staging and the in-place dZ2 write only real rows)
+  for (int i = tid; i < CR * H2R * LD2 / 4; i += 256) reinterpret_cast<f32x4*>(h2s)[i] = z4;
+  for (int i = tid; i < CR * D3R * LD3 / 4; i += 256) reinterpret_cast<f32x4*>(d3s)[i] = z4;
+  __syncthreads();  // before any staging store lands on a zeroed row
 
   for (int gi = blockIdx.x; gi < G; gi += gridDim.x) {
     const int row0 = gi * CR;
@@ -300,13 +315,14 @@ __global__ __launch_bounds__(256) void conv_stack_bwd_kernel(XaConvStackBwdArgs 
       for (int u = 0; u < 2; ++u)
         vx[u] = load_x4(p.x, p.x_u8, p.rows, row0, min(tid + 256 * u, XQ - 1));
       stage_store<NT1, CF1, LD1>(h1s, v1, nrow * CP1);
-      stage_store<NT2, CF2, LD2>(h2s, v2, nrow * CP2);
-      stage_store<NT3, CF3, LD3>(d3s, v3, nrow * CP3);
+      stage_store<NT2, CF2, LD2, CP2, H2R, H2B>(h2s, v2, nrow * CP2);
+      stage_store<NT3, CF3, LD3, CP3, D3R, D3B>(d3s, v3, nrow * CP3);
 #pragma unroll
       for (int u = 0; u < 2; ++u)
         if (tid + 256 * u < XQ) store_x4(xs, tid + 256 * u, vx[u]);
     }
     __syncthreads();
+    XA_STAMP(0);
     // ---- (a) dW3 [k = (t, c)][n]: rows 16 kt + i16 of tile kt, K = the group's m3 ----
     for (int mb = 0; mb < M3 / 16; ++mb) {
       float bq[4];
@@ -314,8 +330,8 @@ __global__ __launch_bounds__(256) void conv_stack_bwd_kernel(XaConvStackBwdArgs 
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int m = 16 * mb + 4 * q + j, r = m / CP3, pp = m - r * CP3;
-        bq[j] = d3s[m * LD3 + 16 * w + i16];
-        rb[j] = (r * CP2 + pp) * LD2;
+        bq[j] = d3s[d3row(m) * LD3 + 16 * w + i16];
+        rb[j] = (r * H2R + H2B + pp) * LD2;
         bs3 += bq[j];
       }
       // A of row j + 1 (12 k tiles) is read while row j's 12 MFMAs run (pinned: the
@@ -337,6 +353,7 @@ __global__ __launch_bounds__(256) void conv_stack_bwd_kernel(XaConvStackBwdArgs 
       }
     }
     __syncthreads();  // (a) has read h2
+    XA_STAMP(1);
     // ---- (b) dZ2 = transposed conv3 of dZ3, gated by h2 > 0, over h2; two M tiles per
     // pass (M2 / 16 = 9: the last pass repeats tile 8 and skips its store) ----
     {
@@ -355,31 +372,41 @@ __global__ __launch_bounds__(256) void conv_stack_bwd_kernel(XaConvStackBwdArgs 
           p2[u] = m - r[u] * CP2;
         }
         f32x4 acc[2] = {z4, z4};
+        // A one k block ahead of its MFMAs, the two tiles' chains interleaved (pinned: the
+        // scheduler otherwise ran each 4-MFMA chain back to back behind its own read)
+        auto rd3 = [&](int kb, int u) {  // taps past the row ends read the zero pads
+          return *reinterpret_cast<const f32x4*>(
+              d3s + (r[u] * D3R + D3B + p2[u] - (kb >> 2)) * LD3 + ((kb & 3) << 4) + 4 * q);
+        };
+        f32x4 an[2] = {rd3(0, 0), rd3(0, 1)};
 #pragma unroll
         for (int kb = 0; kb < KT3; ++kb) {
-#pragma unroll
-          for (int u = 0; u < 2; ++u) {
-            const int p3 = p2[u] - (kb >> 2);
-            const f32x4 a = (p3 >= 0 && p3 < CP3)
-                                ? *reinterpret_cast<const f32x4*>(d3s + (r[u] * CP3 + p3) * LD3 +
-                                                                  ((kb & 3) << 4) + 4 * q)
-                                : z4;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) acc[u] = mfma4(a[j], wb3[kb][j], acc[u]);
+          const f32x4 a0 = an[0], a1 = an[1];
+          if (kb + 1 < KT3) {
+            an[0] = rd3(kb + 1, 0);
+            an[1] = rd3(kb + 1, 1);
           }
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            acc[0] = mfma4(a0[j], wb3[kb][j], acc[0]);
+            acc[1] = mfma4(a1[j], wb3[kb][j], acc[1]);
+          }
+          __builtin_amdgcn_sched_barrier(0);
         }
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
           if (mt + u >= M2 / 16) break;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            float* hp = h2s + (16 * (mt + u) + 4 * q + e) * LD2 + cb;
+            float* hp = h2s + h2row(16 * (mt + u) + 4 * q + e) * LD2 + cb;
             *hp = *hp > 0.0f ? acc[u][e] : 0.0f;
           }
         }
       }
     }
     __syncthreads();  // dZ2 complete
+    XA_STAMP(2);
     // ---- (c) dW2 [k = (t, c)][n] over the group's m2 ----
     for (int mb = 0; mb < M2 / 16; ++mb) {
       float bq[4];
@@ -387,7 +414,7 @@ __global__ __launch_bounds__(256) void conv_stack_bwd_kernel(XaConvStackBwdArgs 
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int m = 16 * mb + 4 * q + j, r = m / CP2, pp = m - r * CP2;
-        bq[j] = h2s[m * LD2 + 16 * w + i16];
+        bq[j] = h2s[h2row(m) * LD2 + 16 * w + i16];
         rb[j] = (r * CP1 + CS2 * pp) * LD1;
         bs2 += bq[j];
       }
@@ -408,6 +435,7 @@ __global__ __launch_bounds__(256) void conv_stack_bwd_kernel(XaConvStackBwdArgs 
       }
     }
     __syncthreads();  // (c) has read h1
+    XA_STAMP(3);
     // ---- (d) dZ1 = transposed conv2 of dZ2, gated by h1 > 0, over h1; two M tiles per
     // pass (CR HH / 16 = 10) ----
     {
@@ -428,18 +456,25 @@ __global__ __launch_bounds__(256) void conv_stack_bwd_kernel(XaConvStackBwdArgs 
           hh[u] = m - r[u] * HH;
         }
         f32x4 acc[2] = {z4, z4};
+        auto rd2 = [&](int kb, int u) {  // as in (b): p2 = -1 and 9 are zero pads
+          return *reinterpret_cast<const f32x4*>(
+              h2s + (r[u] * H2R + H2B + hh[u] - (kb >> 2)) * LD2 + ((kb & 3) << 4) + 4 * q);
+        };
+        f32x4 an[2] = {rd2(0, 0), rd2(0, 1)};
 #pragma unroll
         for (int kb = 0; kb < KT2; ++kb) {
-#pragma unroll
-          for (int u = 0; u < 2; ++u) {
-            const int p2 = hh[u] - (kb >> 2);
-            const f32x4 a = (p2 >= 0 && p2 < CP2)
-                                ? *reinterpret_cast<const f32x4*>(h2s + (r[u] * CP2 + p2) * LD2 +
-                                                                  ((kb & 3) << 4) + 4 * q)
-                                : z4;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) acc[u] = mfma4(a[j], wb2[kb][j], acc[u]);
+          const f32x4 a0 = an[0], a1 = an[1];
+          if (kb + 1 < KT2) {
+            an[0] = rd2(kb + 1, 0);
+            an[1] = rd2(kb + 1, 1);
           }
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            acc[0] = mfma4(a0[j], wb2[kb][j], acc[0]);
+            acc[1] = mfma4(a1[j], wb2[kb][j], acc[1]);
+          }
+          __builtin_amdgcn_sched_barrier(0);
         }
 #pragma unroll
         for (int u = 0; u < 2; ++u)
@@ -452,6 +487,7 @@ __global__ __launch_bounds__(256) void conv_stack_bwd_kernel(XaConvStackBwdArgs 
       }
     }
     __syncthreads();  // dZ1 complete
+    XA_STAMP(4);
     // ---- (e) dW1 [k1 (8 of the tile's 16 rows)][n1]: wave w -> n tile w & 1, m blocks of
     // parity w >> 1 ----
     for (int mb = par; mb < M1 / 16; mb += 2) {
@@ -465,6 +501,7 @@ __global__ __launch_bounds__(256) void conv_stack_bwd_kernel(XaConvStackBwdArgs 
       }
     }
     __syncthreads();  // LDS free for the next group
+    XA_STAMP(5);
   }
 
   // ---- this workgroup's partial gradient -> ws[blockIdx.x][NPAR] ----
@@ -513,6 +550,7 @@ __global__ __launch_bounds__(256) void conv_stack_bwd_kernel(XaConvStackBwdArgs 
     for (int pr = 0; pr < 2; ++pr) s += red[768 + e * 256 + (2 * pr + wt) * 64 + qq * 16 + ln];
     out[OW1 + tid] = s;
   }
+  XA_STAMP(6);
 }
 
 // grad[e] (+)= sum over workgroups z of ws[z][e]: 4 waves per 64 elements, wave v sums the
@@ -555,6 +593,8 @@ int cu_count() {
 }
 
 }  // namespace
+
+XA_DIAG_READER(xa_diag_read_stamps_conv)
 
 extern "C" int xa_conv_stack_fwd(const XaConvStackArgs* a, void* stream) {
   XA_CHECK_ARG(a != nullptr, "xa_conv_stack_fwd: null args");
