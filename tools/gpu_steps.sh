@@ -110,6 +110,9 @@ for step in "$@"; do
       run bw4_on 400 $B4
       XA_CONV_STACK_BWD=0 run bw4_off 400 $B4 ;;
     cstamps) XA_LIB=tools/diag_lib/libxa_cstamp.so run cstamps 200 python tools/conv_stack_stamps.py 64 1024 ;;
+    cstampv)
+      # stamp variants tools/diag_lib/libxa_<v>.so for v in $CS_VARIANTS
+      for v in $CS_VARIANTS; do XA_LIB=tools/diag_lib/libxa_$v.so run cstamp_$v 200 python tools/conv_stack_stamps.py 1024; done ;;
     cnn) run_pytest cnn 600 tests/test_gpu_cnn_onpolicy.py tests/test_gpu_acer.py tests/test_gpu_atari.py ;;
     dqn) run_pytest dqn 400 tests/test_gpu_dqn.py tests/test_gpu_scale.py -k "dqn" tests/test_gpu_configs.py::test_c3_dqn_32_envs_rb1_1m_batch_64 ;;
     td3time)
