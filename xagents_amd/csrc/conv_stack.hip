@@ -352,17 +352,18 @@ __global__ __launch_bounds__(256) void conv_stack_bwd_kernel(XaConvStackBwdArgs 
         __builtin_amdgcn_sched_barrier(0);
       }
     }
+    // (b)'s weights (L2) go out before the barrier, their latency under its wait
+    float wb3[KT3][4];
+#pragma unroll
+    for (int kb = 0; kb < KT3; ++kb)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        wb3[kb][j] = p.w3[((kb >> 2) * CF2 + cb) * CF3 + ((kb & 3) << 4) + 4 * q + j];
     __syncthreads();  // (a) has read h2
     XA_STAMP(1);
     // ---- (b) dZ2 = transposed conv3 of dZ3, gated by h2 > 0, over h2; two M tiles per
     // pass (M2 / 16 = 9: the last pass repeats tile 8 and skips its store) ----
     {
-      float wb3[KT3][4];
-#pragma unroll
-      for (int kb = 0; kb < KT3; ++kb)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          wb3[kb][j] = p.w3[((kb >> 2) * CF2 + cb) * CF3 + ((kb & 3) << 4) + 4 * q + j];
       for (int mt = 0; mt < M2 / 16; mt += 2) {
         int r[2], p2[2];
 #pragma unroll
@@ -434,18 +435,17 @@ __global__ __launch_bounds__(256) void conv_stack_bwd_kernel(XaConvStackBwdArgs 
         __builtin_amdgcn_sched_barrier(0);
       }
     }
+    float wb2[KT2][4];  // (d)'s weights, as wb3
+#pragma unroll
+    for (int kb = 0; kb < KT2; ++kb)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        wb2[kb][j] = p.w2[((2 * (kb >> 2) + par) * CF1 + cd) * CF2 + ((kb & 3) << 4) + 4 * q + j];
     __syncthreads();  // (c) has read h1
     XA_STAMP(3);
     // ---- (d) dZ1 = transposed conv2 of dZ2, gated by h1 > 0, over h1; two M tiles per
     // pass (CR HH / 16 = 10) ----
     {
-      float wb2[KT2][4];
-#pragma unroll
-      for (int kb = 0; kb < KT2; ++kb)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          wb2[kb][j] =
-              p.w2[((2 * (kb >> 2) + par) * CF1 + cd) * CF2 + ((kb & 3) << 4) + 4 * q + j];
       static_assert((CR * HH / 16) % 2 == 0, "pairs of M tiles");
       for (int mt = 0; mt < CR * HH / 16; mt += 2) {
         int r[2], hh[2];
@@ -489,16 +489,26 @@ __global__ __launch_bounds__(256) void conv_stack_bwd_kernel(XaConvStackBwdArgs 
     __syncthreads();  // dZ1 complete
     XA_STAMP(4);
     // ---- (e) dW1 [k1 (8 of the tile's 16 rows)][n1]: wave w -> n tile w & 1, m blocks of
-    // parity w >> 1 ----
-    for (int mb = par; mb < M1 / 16; mb += 2) {
+    // parity w >> 1, two blocks per pass with all 16 reads ahead of the 8 MFMAs ----
+    static_assert((M1 / 16) % 4 == 0, "pairs of same-parity m blocks");
+    for (int mb = par; mb < M1 / 16; mb += 4) {
+      float av[2][4], bv[2][4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int m = 16 * mb + 4 * q + j, r = m / CP1, pp = m - r * CP1;
-        const float b = h1s[m * LD1 + cd];
-        const float a = i16 < CK1 ? xs[r * CW0 + CS1 * pp + i16] : 0.0f;
-        g1 = mfma4(a, b, g1);
-        bs1 += b;
-      }
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int m = 16 * (mb + 2 * u) + 4 * q + j, r = m / CP1, pp = m - r * CP1;
+          bv[u][j] = h1s[m * LD1 + cd];
+          const float a = xs[r * CW0 + CS1 * pp + (i16 & (CK1 - 1))];
+          av[u][j] = i16 < CK1 ? a : 0.0f;
+        }
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          g1 = mfma4(av[u][j], bv[u][j], g1);
+          bs1 += bv[u][j];
+        }
     }
     __syncthreads();  // LDS free for the next group
     XA_STAMP(5);
