@@ -1,6 +1,7 @@
 """Per-phase shader-clock stamps of the fused conv-stack backward (diagnostic build:
 python tools/build_variant.py cstamp -DXA_STAMPS --src conv_stack): block 0 wave 0's cycles
-in staging, (a) dW3, (b) dZ2, (c) dW2, (d) dZ1, (e) dW1 (each up to the barrier that ends it)
+in staging, (a) dW3, (b) dZ2, (c) dW2, (d) dZ1, (e) dW1 (each up to the barrier that ends it;
+the phases' work is split over 8 waves, wave 0's share is stamped)
 and the partial write, summed over the launch's groups, averaged over launches.
 usage: XA_LIB=tools/diag_lib/libxa_cstamp.so python tools/conv_stack_stamps.py [frames ...]"""
 import ctypes

@@ -113,6 +113,16 @@ for step in "$@"; do
     cstampv)
       # stamp variants tools/diag_lib/libxa_<v>.so for v in $CS_VARIANTS
       for v in $CS_VARIANTS; do XA_LIB=tools/diag_lib/libxa_$v.so run cstamp_$v 200 python tools/conv_stack_stamps.py 1024; done ;;
+    bwd8ab)
+      # 8-wave vs 4-wave fused conv backward (XA_CONV_BWD8=0): C3 x2, C4 x1
+      B="python bench.py --config c3 --steps 30 --warmup 5 --cpu-baseline-seconds 0"
+      run b8_on1 300 $B
+      XA_CONV_BWD8=0 run b8_off1 300 $B
+      run b8_on2 300 $B
+      XA_CONV_BWD8=0 run b8_off2 300 $B
+      B4="python bench.py --config c4 --steps 3 --warmup 1 --cpu-baseline-seconds 0"
+      run b84_on 400 $B4
+      XA_CONV_BWD8=0 run b84_off 400 $B4 ;;
     cnn) run_pytest cnn 600 tests/test_gpu_cnn_onpolicy.py tests/test_gpu_acer.py tests/test_gpu_atari.py ;;
     dqn) run_pytest dqn 400 tests/test_gpu_dqn.py tests/test_gpu_scale.py -k "dqn" tests/test_gpu_configs.py::test_c3_dqn_32_envs_rb1_1m_batch_64 ;;
     td3time)

@@ -219,7 +219,7 @@ __global__ __launch_bounds__(256) void conv_stack_fwd_kernel(XaConvStackArgs p) 
 // ---------------------------------------------------------------------------
 // Fused backward of the same stack. Input: dZ3 = dL/d(conv3 pre-activation) [rows][7][64]
 // (the dense layer's input gradient with h3's ReLU gate applied), the forward's h1 / h2 and
-// the frames. Per 16-sequence group, out of LDS (x, h1, h2, dZ3: 121 KB):
+// the frames. Per 16-sequence group, out of LDS (x, h1, h2, dZ3: 147 KB with the pads):
 //   (a) dW3 += im2col(h2)^T dZ3, db3 += colsum dZ3
 //   (b) dZ2 = (dZ3 (*) W3^T, transposed conv) . [h2 > 0]       -> over h2 in place
 //   (c) dW2 += im2col(h1)^T dZ2, db2 += colsum dZ2
@@ -227,9 +227,9 @@ __global__ __launch_bounds__(256) void conv_stack_fwd_kernel(XaConvStackArgs p) 
 //       output position 2 h + par takes taps t = 2 s + par from dZ2 rows h - s (s = 0, 1),
 //       so each wave's (par, 16-channel) tile is a K = 2 x 64 GEMM with no zero taps
 //   (e) dW1 += im2col(x)^T dZ1, db1 += colsum dZ1
-// Weight-gradient tiles stay in registers over all of a workgroup's groups (wave w owns
-// filter columns 16 w .. of dW3 / dW2); the dgrad phases keep their 16-column slice of
-// W3^T / W2^T in registers as the forward does. Each workgroup writes its partial
+// Weight-gradient tiles stay in registers over all of a workgroup's groups (a wave owns
+// filter columns 16 (w & 3) .. of dW3 / dW2 and half of their k tiles); the dgrad phases
+// hold their 16-column slice of W3^T / W2^T in registers, loaded per group from L2. Each workgroup writes its partial
 // [w1 b1 w2 b2 w3 b3] (20896 floats, theta order) to ws[blockIdx]; a second launch sums
 // the partials in workgroup order (deterministic) into the gradient (+= when accumulate).
 // ---------------------------------------------------------------------------
@@ -250,109 +250,106 @@ XA_DEV int d3row(int m) { return (m / CP3) * D3R + D3B + m % CP3; }
 XA_DEV int h2row(int m) { return (m / CP2) * H2R + H2B + m % CP2; }
 
 
-// LDS rows [m][LD] <- global rows [m][C] (m < valid; later rows 0), NT float4 per thread:
-// stage_load issues the loads (clamped to the valid rows), stage_store masks and stores
-template <int NT, int C>
-XA_DEV void stage_load(f32x4 (&v)[NT], const float* src, int valid) {
+// 8 waves (512 threads): two waves per 16-column tile, so every SIMD runs two waves whose
+// MFMA chains and LDS waits interleave (a 4-wave version, one wave per SIMD holding ~512
+// registers, reached ~56 % of its MFMA issue time: profiles/r05zm_conv_bwd_stamps.txt; this
+// one is 1.2-2 % faster end to end, profiles/r05zo_conv_bwd8_ab.txt). Waves w and w + 4
+// share column tile wc = w & 3 and split the work by wh = w >> 2: (a) / (c) the weight-
+// gradient k tiles (6 / 4 each), (b) / (d) the M tiles (5 + 4 / 6 + 4), (e) m blocks by
+// residue w >> 1 (mod 4). Staging: LDS rows [m][LD] <- global rows [m][C] (m < valid, later
+// rows 0), every load of a group issued before the first store (a load per loop trip behind
+// a branch waited out one memory latency each).
+template <int NTT, int C>
+XA_DEV void stage_load8(f32x4 (&v)[NTT], const float* src, int valid, int tot) {
   const f32x4* g = reinterpret_cast<const f32x4*>(src);
-  const int last = valid * (C / 4) - 1;  // >= 0: a group holds >= 1 row
+  const int last = min(valid * (C / 4), tot) - 1;
 #pragma unroll
-  for (int u = 0; u < NT; ++u) v[u] = g[min((int)threadIdx.x + 256 * u, last)];
+  for (int u = 0; u < NTT; ++u) v[u] = g[min((int)threadIdx.x + 512 * u, last)];
 }
-template <int NT, int C, int LD, int P = 1, int PR = 1, int PB = 0>
-XA_DEV void stage_store(float* dst, const f32x4 (&v)[NT], int valid) {
-  // row m of the group -> LDS row (m / P) PR + PB + m % P (the padded layouts)
+template <int NTT, int C, int LD, int P = 1, int PR = 1, int PB = 0>
+XA_DEV void stage_store8(float* dst, const f32x4 (&v)[NTT], int valid, int tot) {
   const int last = valid * (C / 4) - 1;
 #pragma unroll
-  for (int u = 0; u < NT; ++u) {
-    const int i = threadIdx.x + 256 * u, m = i / (C / 4), c = 4 * (i - m * (C / 4));
+  for (int u = 0; u < NTT; ++u) {
+    const int i = threadIdx.x + 512 * u;
+    if (i >= tot) break;
+    const int m = i / (C / 4), c = 4 * (i - m * (C / 4));
     const int row = (m / P) * PR + PB + m % P;
     *reinterpret_cast<f32x4*>(dst + row * LD + c) = i <= last ? v[u] : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
   }
 }
-constexpr int NT1 = M1 * CF1 / 4 / 256, NT2 = M2 * CF2 / 4 / 256, NT3 = M3 * CF3 / 4 / 256;
-static_assert(NT1 * 1024 == M1 * CF1 && NT2 * 1024 == M2 * CF2 && NT3 * 1024 == M3 * CF3,
-              "whole float4 rounds per thread");
+constexpr int TOT1 = M1 * CF1 / 4, TOT2 = M2 * CF2 / 4, TOT3 = M3 * CF3 / 4;
+constexpr int N81 = (TOT1 + 511) / 512, N82 = (TOT2 + 511) / 512, N83 = (TOT3 + 511) / 512;
+constexpr int KH3 = KT3 / 2, KH2 = KT2 / 2;  // weight-gradient k tiles per wave
 
-__global__ __launch_bounds__(256) void conv_stack_bwd_kernel(XaConvStackBwdArgs p) {
+__global__ __launch_bounds__(512) void conv_stack_bwd8_kernel(XaConvStackBwdArgs p) {
   __shared__ __attribute__((aligned(16))) float xs[CR * CW0];
-  __shared__ __attribute__((aligned(16))) float h1s[M1 * LD1];  // h1, then dZ1
-  __shared__ __attribute__((aligned(16))) float h2s[CR * H2R * LD2];  // h2, then dZ2 (padded)
-  __shared__ __attribute__((aligned(16))) float d3s[CR * D3R * LD3];  // dZ3 (padded)
+  __shared__ __attribute__((aligned(16))) float h1s[M1 * LD1];          // h1, then dZ1
+  __shared__ __attribute__((aligned(16))) float h2s[CR * H2R * LD2];    // h2, then dZ2
+  __shared__ __attribute__((aligned(16))) float d3s[CR * D3R * LD3];    // dZ3
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, q = lane >> 4, i16 = lane & 15;
+  const int wc = w & 3, wh = w >> 2;
   const int G = (p.rows + CR - 1) / CR;
+  const int cb = 16 * wc + i16, par = wc >> 1, cd = 16 * (wc & 1) + i16;
   XA_STAMP_DECL  // diagnostic build only (-DXA_STAMPS, tools/conv_stack_stamps.py)
   XA_STAMP(7);
-
-  // (b) / (d) B operands: W3^T columns cb = 16 w + i16 (k = (t, n) = 16 kb + 4 q + j) and
-  // W2^T for parity par = w >> 1, channels cd = 16 (w & 1) + i16 (k = (s, n), tap 2 s + par);
-  // re-read (L2) at their phase so they do not hold registers through the others
-  const int cb = 16 * w + i16, par = w >> 1, cd = 16 * (w & 1) + i16;
   const f32x4 z4 = {0.0f, 0.0f, 0.0f, 0.0f};
-  f32x4 g3[KT3], g2[KT2], g1 = z4;
+  f32x4 g3[KH3], g2[KH2], g1 = z4;
 #pragma unroll
-  for (int i = 0; i < KT3; ++i) g3[i] = z4;
+  for (int i = 0; i < KH3; ++i) g3[i] = z4;
 #pragma unroll
-  for (int i = 0; i < KT2; ++i) g2[i] = z4;
+  for (int i = 0; i < KH2; ++i) g2[i] = z4;
   float bs3 = 0.0f, bs2 = 0.0f, bs1 = 0.0f;
-  // the pad rows stay zero (staging and the in-place dZ2 write only real rows)
-  for (int i = tid; i < CR * H2R * LD2 / 4; i += 256) reinterpret_cast<f32x4*>(h2s)[i] = z4;
-  for (int i = tid; i < CR * D3R * LD3 / 4; i += 256) reinterpret_cast<f32x4*>(d3s)[i] = z4;
-  __syncthreads();  // before any staging store lands on a zeroed row
+  for (int i = tid; i < CR * H2R * LD2 / 4; i += 512) reinterpret_cast<f32x4*>(h2s)[i] = z4;
+  for (int i = tid; i < CR * D3R * LD3 / 4; i += 512) reinterpret_cast<f32x4*>(d3s)[i] = z4;
+  __syncthreads();
 
   for (int gi = blockIdx.x; gi < G; gi += gridDim.x) {
     const int row0 = gi * CR;
     const int nrow = min(CR, p.rows - row0);
-    // ---- stage x, h1, h2, dZ3 (rows past the batch read as 0); every load of the group
-    // goes out before the first store (a load per loop trip behind a branch waited out one
-    // memory latency each) ----
     {
-      f32x4 v1[NT1], v2[NT2], v3[NT3], vx[2];
-      stage_load<NT1, CF1>(v1, p.h1 + (int64_t)row0 * CP1 * CF1, nrow * CP1);
-      stage_load<NT2, CF2>(v2, p.h2 + (int64_t)row0 * CP2 * CF2, nrow * CP2);
-      stage_load<NT3, CF3>(v3, p.dz3 + (int64_t)row0 * CP3 * CF3, nrow * CP3);
-#pragma unroll
-      for (int u = 0; u < 2; ++u)
-        vx[u] = load_x4(p.x, p.x_u8, p.rows, row0, min(tid + 256 * u, XQ - 1));
-      stage_store<NT1, CF1, LD1>(h1s, v1, nrow * CP1);
-      stage_store<NT2, CF2, LD2, CP2, H2R, H2B>(h2s, v2, nrow * CP2);
-      stage_store<NT3, CF3, LD3, CP3, D3R, D3B>(d3s, v3, nrow * CP3);
-#pragma unroll
-      for (int u = 0; u < 2; ++u)
-        if (tid + 256 * u < XQ) store_x4(xs, tid + 256 * u, vx[u]);
+      f32x4 v1[N81], v2[N82], v3[N83], vx;
+      stage_load8<N81, CF1>(v1, p.h1 + (int64_t)row0 * CP1 * CF1, nrow * CP1, TOT1);
+      stage_load8<N82, CF2>(v2, p.h2 + (int64_t)row0 * CP2 * CF2, nrow * CP2, TOT2);
+      stage_load8<N83, CF3>(v3, p.dz3 + (int64_t)row0 * CP3 * CF3, nrow * CP3, TOT3);
+      vx = load_x4(p.x, p.x_u8, p.rows, row0, min(tid, XQ - 1));
+      stage_store8<N81, CF1, LD1>(h1s, v1, nrow * CP1, TOT1);
+      stage_store8<N82, CF2, LD2, CP2, H2R, H2B>(h2s, v2, nrow * CP2, TOT2);
+      stage_store8<N83, CF3, LD3, CP3, D3R, D3B>(d3s, v3, nrow * CP3, TOT3);
+      if (tid < XQ) store_x4(xs, tid, vx);
     }
     __syncthreads();
     XA_STAMP(0);
-    // ---- (a) dW3 [k = (t, c)][n]: rows 16 kt + i16 of tile kt, K = the group's m3 ----
+    // ---- (a) dW3: k tiles 6 wh .. 6 wh + 5, n tile wc ----
     for (int mb = 0; mb < M3 / 16; ++mb) {
       float bq[4];
       int rb[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int m = 16 * mb + 4 * q + j, r = m / CP3, pp = m - r * CP3;
-        bq[j] = d3s[d3row(m) * LD3 + 16 * w + i16];
+        bq[j] = d3s[d3row(m) * LD3 + cb];
         rb[j] = (r * H2R + H2B + pp) * LD2;
-        bs3 += bq[j];
+        if (wh == 0) bs3 += bq[j];
       }
-      // A of row j + 1 (12 k tiles) is read while row j's 12 MFMAs run (pinned: the
-      // scheduler otherwise reads one pair of A values at a time right before its MFMAs)
-      float av[2][KT3];
-      auto koff3 = [&](int kt) { return (kt >> 2) * LD2 + ((kt & 3) << 4) + i16; };
+      float av[2][KH3];
+      auto koff3 = [&](int kt) {
+        const int k = KH3 * wh + kt;
+        return (k >> 2) * LD2 + ((k & 3) << 4) + i16;
+      };
 #pragma unroll
-      for (int kt = 0; kt < KT3; ++kt) av[0][kt] = h2s[rb[0] + koff3(kt)];
+      for (int kt = 0; kt < KH3; ++kt) av[0][kt] = h2s[rb[0] + koff3(kt)];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         if (j < 3) {
 #pragma unroll
-          for (int kt = 0; kt < KT3; ++kt) av[(j + 1) & 1][kt] = h2s[rb[j + 1] + koff3(kt)];
+          for (int kt = 0; kt < KH3; ++kt) av[(j + 1) & 1][kt] = h2s[rb[j + 1] + koff3(kt)];
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int kt = 0; kt < KT3; ++kt) g3[kt] = mfma4(av[j & 1][kt], bq[j], g3[kt]);
+        for (int kt = 0; kt < KH3; ++kt) g3[kt] = mfma4(av[j & 1][kt], bq[j], g3[kt]);
         __builtin_amdgcn_sched_barrier(0);
       }
     }
-    // (b)'s weights (L2) go out before the barrier, their latency under its wait
     float wb3[KT3][4];
 #pragma unroll
     for (int kb = 0; kb < KT3; ++kb)
@@ -361,21 +358,19 @@ __global__ __launch_bounds__(256) void conv_stack_bwd_kernel(XaConvStackBwdArgs 
         wb3[kb][j] = p.w3[((kb >> 2) * CF2 + cb) * CF3 + ((kb & 3) << 4) + 4 * q + j];
     __syncthreads();  // (a) has read h2
     XA_STAMP(1);
-    // ---- (b) dZ2 = transposed conv3 of dZ3, gated by h2 > 0, over h2; two M tiles per
-    // pass (M2 / 16 = 9: the last pass repeats tile 8 and skips its store) ----
+    // ---- (b) dZ2 over h2: column tile wc, M tiles 0..4 (wh 0) / 5..8 (wh 1) ----
     {
-      for (int mt = 0; mt < M2 / 16; mt += 2) {
+      const int t0 = wh ? 5 : 0, nt = wh ? 4 : 5;
+      for (int i = 0; i < nt; i += 2) {
         int r[2], p2[2];
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-          const int m = 16 * min(mt + u, M2 / 16 - 1) + i16;
+          const int m = 16 * (t0 + min(i + u, nt - 1)) + i16;
           r[u] = m / CP2;
           p2[u] = m - r[u] * CP2;
         }
         f32x4 acc[2] = {z4, z4};
-        // A one k block ahead of its MFMAs, the two tiles' chains interleaved (pinned: the
-        // scheduler otherwise ran each 4-MFMA chain back to back behind its own read)
-        auto rd3 = [&](int kb, int u) {  // taps past the row ends read the zero pads
+        auto rd3 = [&](int kb, int u) {
           return *reinterpret_cast<const f32x4*>(
               d3s + (r[u] * D3R + D3B + p2[u] - (kb >> 2)) * LD3 + ((kb & 3) << 4) + 4 * q);
         };
@@ -397,10 +392,10 @@ __global__ __launch_bounds__(256) void conv_stack_bwd_kernel(XaConvStackBwdArgs 
         }
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-          if (mt + u >= M2 / 16) break;
+          if (i + u >= nt) break;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            float* hp = h2s + h2row(16 * (mt + u) + 4 * q + e) * LD2 + cb;
+            float* hp = h2s + h2row(16 * (t0 + i + u) + 4 * q + e) * LD2 + cb;
             *hp = *hp > 0.0f ? acc[u][e] : 0.0f;
           }
         }
@@ -408,34 +403,37 @@ __global__ __launch_bounds__(256) void conv_stack_bwd_kernel(XaConvStackBwdArgs 
     }
     __syncthreads();  // dZ2 complete
     XA_STAMP(2);
-    // ---- (c) dW2 [k = (t, c)][n] over the group's m2 ----
+    // ---- (c) dW2: k tiles 4 wh .. 4 wh + 3, n tile wc ----
     for (int mb = 0; mb < M2 / 16; ++mb) {
       float bq[4];
       int rb[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int m = 16 * mb + 4 * q + j, r = m / CP2, pp = m - r * CP2;
-        bq[j] = h2s[h2row(m) * LD2 + 16 * w + i16];
+        bq[j] = h2s[h2row(m) * LD2 + cb];
         rb[j] = (r * CP1 + CS2 * pp) * LD1;
-        bs2 += bq[j];
+        if (wh == 0) bs2 += bq[j];
       }
-      float av[2][KT2];  // as in (a)
-      auto koff2 = [&](int kt) { return (kt >> 1) * LD1 + ((kt & 1) << 4) + i16; };
+      float av[2][KH2];
+      auto koff2 = [&](int kt) {
+        const int k = KH2 * wh + kt;
+        return (k >> 1) * LD1 + ((k & 1) << 4) + i16;
+      };
 #pragma unroll
-      for (int kt = 0; kt < KT2; ++kt) av[0][kt] = h1s[rb[0] + koff2(kt)];
+      for (int kt = 0; kt < KH2; ++kt) av[0][kt] = h1s[rb[0] + koff2(kt)];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         if (j < 3) {
 #pragma unroll
-          for (int kt = 0; kt < KT2; ++kt) av[(j + 1) & 1][kt] = h1s[rb[j + 1] + koff2(kt)];
+          for (int kt = 0; kt < KH2; ++kt) av[(j + 1) & 1][kt] = h1s[rb[j + 1] + koff2(kt)];
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int kt = 0; kt < KT2; ++kt) g2[kt] = mfma4(av[j & 1][kt], bq[j], g2[kt]);
+        for (int kt = 0; kt < KH2; ++kt) g2[kt] = mfma4(av[j & 1][kt], bq[j], g2[kt]);
         __builtin_amdgcn_sched_barrier(0);
       }
     }
-    float wb2[KT2][4];  // (d)'s weights, as wb3
+    float wb2[KT2][4];
 #pragma unroll
     for (int kb = 0; kb < KT2; ++kb)
 #pragma unroll
@@ -443,20 +441,19 @@ __global__ __launch_bounds__(256) void conv_stack_bwd_kernel(XaConvStackBwdArgs 
         wb2[kb][j] = p.w2[((2 * (kb >> 2) + par) * CF1 + cd) * CF2 + ((kb & 3) << 4) + 4 * q + j];
     __syncthreads();  // (c) has read h1
     XA_STAMP(3);
-    // ---- (d) dZ1 = transposed conv2 of dZ2, gated by h1 > 0, over h1; two M tiles per
-    // pass (CR HH / 16 = 10) ----
+    // ---- (d) dZ1 over h1: column (par, 16-channel tile) wc, M tiles 0..5 / 6..9 ----
     {
-      static_assert((CR * HH / 16) % 2 == 0, "pairs of M tiles");
-      for (int mt = 0; mt < CR * HH / 16; mt += 2) {
+      const int t0 = wh ? 6 : 0, nt = wh ? 4 : 6;
+      for (int i = 0; i < nt; i += 2) {
         int r[2], hh[2];
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-          const int m = 16 * (mt + u) + i16;
+          const int m = 16 * (t0 + i + u) + i16;
           r[u] = m / HH;
           hh[u] = m - r[u] * HH;
         }
         f32x4 acc[2] = {z4, z4};
-        auto rd2 = [&](int kb, int u) {  // as in (b): p2 = -1 and 9 are zero pads
+        auto rd2 = [&](int kb, int u) {
           return *reinterpret_cast<const f32x4*>(
               h2s + (r[u] * H2R + H2B + hh[u] - (kb >> 2)) * LD2 + ((kb & 3) << 4) + 4 * q);
         };
@@ -480,7 +477,7 @@ __global__ __launch_bounds__(256) void conv_stack_bwd_kernel(XaConvStackBwdArgs 
         for (int u = 0; u < 2; ++u)
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            const int mo = 16 * (mt + u) + 4 * q + e, ro = mo / HH, ho = mo - ro * HH;
+            const int mo = 16 * (t0 + i + u) + 4 * q + e, ro = mo / HH, ho = mo - ro * HH;
             float* hp = h1s + (ro * CP1 + 2 * ho + par) * LD1 + cd;
             *hp = *hp > 0.0f ? acc[u][e] : 0.0f;
           }
@@ -488,22 +485,21 @@ __global__ __launch_bounds__(256) void conv_stack_bwd_kernel(XaConvStackBwdArgs 
     }
     __syncthreads();  // dZ1 complete
     XA_STAMP(4);
-    // ---- (e) dW1 [k1 (8 of the tile's 16 rows)][n1]: wave w -> n tile w & 1, m blocks of
-    // parity w >> 1, two blocks per pass with all 16 reads ahead of the 8 MFMAs ----
-    static_assert((M1 / 16) % 4 == 0, "pairs of same-parity m blocks");
-    for (int mb = par; mb < M1 / 16; mb += 4) {
-      float av[2][4], bv[2][4];
+    // ---- (e) dW1: n tile w & 1, m blocks w >> 1 (mod 4), all reads of a pass first ----
+    {
+      const int n1 = 16 * (w & 1) + i16;
+      float av[M1 / 64][4], bv[M1 / 64][4];
 #pragma unroll
-      for (int u = 0; u < 2; ++u)
+      for (int u = 0; u < M1 / 64; ++u)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const int m = 16 * (mb + 2 * u) + 4 * q + j, r = m / CP1, pp = m - r * CP1;
-          bv[u][j] = h1s[m * LD1 + cd];
+          const int m = 16 * (4 * u + (w >> 1)) + 4 * q + j, r = m / CP1, pp = m - r * CP1;
+          bv[u][j] = h1s[m * LD1 + n1];
           const float a = xs[r * CW0 + CS1 * pp + (i16 & (CK1 - 1))];
           av[u][j] = i16 < CK1 ? a : 0.0f;
         }
 #pragma unroll
-      for (int u = 0; u < 2; ++u)
+      for (int u = 0; u < M1 / 64; ++u)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           g1 = mfma4(av[u][j], bv[u][j], g1);
@@ -514,50 +510,51 @@ __global__ __launch_bounds__(256) void conv_stack_bwd_kernel(XaConvStackBwdArgs 
     XA_STAMP(5);
   }
 
-  // ---- this workgroup's partial gradient -> ws[blockIdx.x][NPAR] ----
+  // ---- partials -> ws[blockIdx.x][NPAR] ----
   float* out = p.ws + (int64_t)blockIdx.x * NPAR;
 #pragma unroll
-  for (int kt = 0; kt < KT3; ++kt)
+  for (int kt = 0; kt < KH3; ++kt)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) out[OW3 + (16 * kt + 4 * q + e) * CF3 + 16 * w + i16] = g3[kt][e];
+    for (int e = 0; e < 4; ++e)
+      out[OW3 + (16 * (KH3 * wh + kt) + 4 * q + e) * CF3 + cb] = g3[kt][e];
 #pragma unroll
-  for (int kt = 0; kt < KT2; ++kt)
+  for (int kt = 0; kt < KH2; ++kt)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) out[OW2 + (16 * kt + 4 * q + e) * CF2 + 16 * w + i16] = g2[kt][e];
-  // the small pieces combine lanes / waves in fixed order through LDS
+    for (int e = 0; e < 4; ++e)
+      out[OW2 + (16 * (KH2 * wh + kt) + 4 * q + e) * CF2 + cb] = g2[kt][e];
   float* red = h1s;
   red[tid] = bs3;
-  red[256 + tid] = bs2;
-  red[512 + tid] = bs1;
+  red[512 + tid] = bs2;
+  red[1024 + tid] = bs1;
 #pragma unroll
-  for (int e = 0; e < 4; ++e) red[768 + e * 256 + tid] = g1[e];
+  for (int e = 0; e < 4; ++e) red[1536 + e * 512 + tid] = g1[e];
   __syncthreads();
-  if (tid < CF3) {  // db3 / db2: column n = 16 w + i16 summed over its wave's 4 lane groups
+  if (tid < CF3) {  // db3 / db2: column n = 16 wc + i16 from waves wc (wh = 0), 4 lane groups
     const int wn = tid >> 4, ln = tid & 15;
     float s3 = 0.0f, s2 = 0.0f;
 #pragma unroll
     for (int qq = 0; qq < 4; ++qq) {
       s3 += red[wn * 64 + qq * 16 + ln];
-      s2 += red[256 + wn * 64 + qq * 16 + ln];
+      s2 += red[512 + wn * 64 + qq * 16 + ln];
     }
     out[OB3 + tid] = s3;
     out[OB2 + tid] = s2;
   }
-  if (tid < CF1) {  // db1: column 16 (w & 1) + i16 over lane groups and both parities
+  if (tid < CF1) {  // db1: column 16 t + i16 from waves w = 2 rr + t (rr = 0..3), lane groups
     const int wt = tid >> 4, ln = tid & 15;
     float s1 = 0.0f;
 #pragma unroll
-    for (int pr = 0; pr < 2; ++pr)
+    for (int rr = 0; rr < 4; ++rr)
 #pragma unroll
-      for (int qq = 0; qq < 4; ++qq) s1 += red[512 + (2 * pr + wt) * 64 + qq * 16 + ln];
+      for (int qq = 0; qq < 4; ++qq) s1 += red[1024 + (2 * rr + wt) * 64 + qq * 16 + ln];
     out[OB1 + tid] = s1;
   }
-  if (tid < NW1) {  // dW1 [k1][n1]: D rows k1 = 4 q + e (q < 2) of waves wt and wt + 2
+  if (tid < NW1) {  // dW1 [k1][n1]: D rows k1 = 4 q + e (q < 2) of waves 2 rr + (n1 >> 4)
     const int k1 = tid / CF1, n1 = tid - k1 * CF1, wt = n1 >> 4, ln = n1 & 15;
     const int qq = k1 >> 2, e = k1 & 3;
     float s = 0.0f;
 #pragma unroll
-    for (int pr = 0; pr < 2; ++pr) s += red[768 + e * 256 + (2 * pr + wt) * 64 + qq * 16 + ln];
+    for (int rr = 0; rr < 4; ++rr) s += red[1536 + e * 512 + (2 * rr + wt) * 64 + qq * 16 + ln];
     out[OW1 + tid] = s;
   }
   XA_STAMP(6);
@@ -638,7 +635,7 @@ extern "C" int xa_conv_stack_bwd(const XaConvStackBwdArgs* a, void* stream) {
                xa_conv_stack_bwd_workspace_floats(p.rows));
   const int G = (p.rows + CR - 1) / CR;
   const int grid = G < cu_count() ? G : cu_count();
-  hipLaunchKernelGGL(conv_stack_bwd_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, p);
+  hipLaunchKernelGGL(conv_stack_bwd8_kernel, dim3(grid), dim3(512), 0, (hipStream_t)stream, p);
   XA_CHECK_LAUNCH("xa_conv_stack_bwd");
   hipLaunchKernelGGL(conv_stack_bwd_reduce_kernel, dim3((NPAR + 63) / 64), dim3(256), 0,
                      (hipStream_t)stream, p.ws, grid, p.grad, p.accumulate);
