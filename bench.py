@@ -246,10 +246,12 @@ def _data_note(args, what):
     return what
 
 
-def dense_dx_roofline(executors, step):
-    """Roofline of the CNN's dominant GEMM -- the dense 37632 x 512 layer's input gradient
-    dX = dZ W^T -- from HIP events recorded on the launch stream around each of its launches
-    during one more (eager) `step`."""
+def dominant_kernel_roofline(executors, step):
+    """Roofline of the CNN step's dominant launch: the recorded launch kind (dense dX, dense
+    dW (+ Adam), the fused conv-stack forward / backward) with the largest total time in one
+    more (eager) `step`, from HIP events recorded on the launch stream around each launch.
+    HBM basis for launches that carry algorithmic bytes (the fused dense dW + Adam), MFMA f32
+    otherwise (2 x MACs of the launch's GEMMs / convolutions)."""
     import torch
     timing = []
     for ex in executors:
@@ -260,18 +262,31 @@ def dense_dx_roofline(executors, step):
     finally:
         for ex in executors:
             ex.timing = None
-    top = max((fl for *_, fl in timing), default=0)
-    big = [x for x in timing if x[3] == top]
-    full = [(e0.elapsed_time(e1), fl) for _, e0, e1, fl in big]
-    if not full:
+    tot = {}
+    for name, e0, e1, fl, nb in timing:
+        t = tot.setdefault(name, [0.0, 0, fl, nb])
+        t[0] += e0.elapsed_time(e1)
+        t[1] += 1
+    if not tot:
         return None
-    ms = sum(t for t, _ in full) / len(full)
-    tf = full[0][1] / (ms * 1e-3) / 1e12
-    return {'kernel': f'xa_gemm {big[0][0]} (MFMA f32; small-M resident-A kernel at M <= 64, tile kernels above; ReLU-gate epilogue)',
-            'bound': 'mfma', 'achieved': round(tf, 3), 'peak': 157.3, 'unit': 'TFLOP/s',
-            'frac': round(tf / 157.3, 4), 'traffic': None, 'launch_ms': round(ms, 4),
-            'note': f'2 M N K FLOP per launch, mean of {len(full)} launches; the 77 MB '
-                    f'kernel read alone bounds it at {77.07e6 / 8e12 * 1e3:.4f} ms (HBM)'}
+    name, (ms_sum, cnt, fl, nb) = max(tot.items(), key=lambda kv: kv[1][0])
+    ms = ms_sum / cnt
+    share = ms_sum / sum(v[0] for v in tot.values())
+    tf = fl / (ms * 1e-3) / 1e12
+    mfma = {'achieved': round(tf, 3), 'peak': F32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
+            'frac': round(tf / F32_MFMA_PEAK_TFLOPS, 4)}
+    note = (f'mean of {cnt} launches; {share:.0%} of the recorded launch time of the step '
+            f'({", ".join(sorted(tot))})')
+    if nb:
+        gbs = nb / (ms * 1e-3) / 1e9
+        return {'kernel': name, 'bound': 'hbm', 'achieved': round(gbs, 2),
+                'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': round(gbs / HBM_PEAK_GBS, 4),
+                'traffic': None, 'launch_ms': round(ms, 4), 'bytes_per_launch': int(nb),
+                'mfma': mfma, 'note': 'algorithmic bytes (24 B per parameter: theta, m, v '
+                'read and written; the layer input and output gradient read) / event time; '
+                + note}
+    return dict(kernel=name, bound='mfma', traffic=None, launch_ms=round(ms, 4),
+                note='2 x MACs per launch / event time; ' + note, **mfma)
 
 
 def dominant_gemm_roofline(executors, step):
@@ -288,7 +303,7 @@ def dominant_gemm_roofline(executors, step):
         for ex in executors:
             ex.timing = None
     tot = {}
-    for name, e0, e1, fl in timing:
+    for name, e0, e1, fl, _ in timing:
         t = tot.setdefault((name, fl), [0.0, 0])
         t[0] += e0.elapsed_time(e1)
         t[1] += 1
@@ -406,7 +421,7 @@ def run_secondary(args, config, world, rank, device, steps, warmup, cpu_seconds,
         env_steps = n * steps * world
         # one eager learner phase for the event pairs (the timed steps replay it as a graph)
         agent.use_graph = False
-        rl = dense_dx_roofline([agent.ex_online], step)
+        rl = dominant_kernel_roofline([agent.ex_online], step)
         agent.use_graph = True
         if rl:
             line['roofline'] = rl
@@ -427,9 +442,7 @@ def run_secondary(args, config, world, rank, device, steps, warmup, cpu_seconds,
         agent = PPO(envs, model, n_steps=128, seed=args.seed, quiet=True)
         el = _timed(agent.fused_train_step, steps, warmup, world)
         env_steps = n * 128 * steps * world
-        # dominant kernel: the dense 37632 x 512 layer's input gradient (gemm_tile_kernel,
-        # 128 x 128 tiles on v_mfma_f32_32x32x2_f32)
-        rl = dense_dx_roofline(agent.ex_chunks, agent.fused_train_step)
+        rl = dominant_kernel_roofline(agent.ex_chunks, agent.fused_train_step)
         if rl:
             line['roofline'] = rl
         line.update(scaling='strong', data=_data_note(
@@ -470,7 +483,7 @@ def run_secondary(args, config, world, rank, device, steps, warmup, cpu_seconds,
         el = _timed(agent.train_step, steps, warmup, world)
         env_steps = n * T * steps * world
         updates = int(agent.model.optimizer.iterations.item())
-        rl = dense_dx_roofline(agent.ex_chunks, agent.train_step)
+        rl = dominant_kernel_roofline(agent.ex_chunks, agent.train_step)
         if rl:
             line['roofline'] = rl
         line.update(scaling='weak', data=_data_note(

@@ -71,14 +71,17 @@ XA_DEV void store_x4(float* xs, int i, f32x4 v) {
   *reinterpret_cast<f32x4*>(xs + 4 * i) = v;  // item i covers xs[4 i .. 4 i + 3]
 }
 
-__global__ __launch_bounds__(256) void conv_stack_fwd_kernel(XaConvStackArgs p) {
+__global__ __launch_bounds__(512) void conv_stack_fwd_kernel(XaConvStackArgs p) {
   __shared__ __attribute__((aligned(16))) float xs[CR * CW0];
   __shared__ __attribute__((aligned(16))) float h1s[M1 * LD1];
   __shared__ __attribute__((aligned(16))) float h2s[M2 * LD2];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, q = lane >> 4, i16 = lane & 15;
+  // 8 waves: waves w and w + 4 share column tile wc = w & 3 of conv2 / conv3 (and its
+  // weights) and split the M tiles by wh = w >> 2, so two waves per SIMD interleave
+  const int wc = w & 3, wh = w >> 2;
 
-  // this wave's weights: conv2 / conv3 columns 16 w + i16, k = 16 kb + 4 q + j
-  const int n2 = 16 * w + i16;
+  // this wave's weights: conv2 / conv3 columns 16 wc + i16, k = 16 kb + 4 q + j
+  const int n2 = 16 * wc + i16;
   float wr2[CK2 * CF1 / 16][4], wr3[CK3 * CF2 / 16][4];
 #pragma unroll
   for (int kb = 0; kb < CK2 * CF1 / 16; ++kb)
@@ -89,20 +92,20 @@ __global__ __launch_bounds__(256) void conv_stack_fwd_kernel(XaConvStackArgs p) 
 #pragma unroll
     for (int j = 0; j < 4; ++j) wr3[kb][j] = p.w3[(16 * kb + 4 * q + j) * CF3 + n2];
   const float bias2 = p.b2[n2], bias3 = p.b3[n2];
-  // conv1 (K = 8, 32 columns): column tile w & 1, M tiles of parity w >> 1; MFMA j takes
+  // conv1 (K = 8, 32 columns): column tile w & 1, M tiles w >> 1 (mod 4); MFMA j takes
   // k = 4 j + q
   const int n1 = 16 * (w & 1) + i16;
   const float w1a = p.w1[q * CF1 + n1], w1b = p.w1[(4 + q) * CF1 + n1], bias1 = p.b1[n1];
 
   const int G = (p.rows + CR - 1) / CR;
   if ((int)blockIdx.x >= G) return;
-  for (int i = tid; i < XQ; i += 256) store_x4(xs, i, load_x4(p, (int)blockIdx.x * CR, i));
+  for (int i = tid; i < XQ; i += 512) store_x4(xs, i, load_x4(p, (int)blockIdx.x * CR, i));
   __syncthreads();
 
   for (int gi = blockIdx.x; gi < G; gi += gridDim.x) {
     const int row0 = gi * CR;
     // ---- conv1: x -> h1 (bias + ReLU) ----
-    for (int mt = w >> 1; mt < M1 / 16; mt += 2) {
+    for (int mt = w >> 1; mt < M1 / 16; mt += 4) {
       const int m = 16 * mt + i16, r = m / CP1, pp = m - r * CP1;
       const float* xr = xs + r * CW0 + CS1 * pp + q;
       f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -119,94 +122,91 @@ __global__ __launch_bounds__(256) void conv_stack_fwd_kernel(XaConvStackArgs p) 
     __syncthreads();  // h1s complete; xs free
     // the next group's input, in flight during conv2
     const int gn = gi + (int)gridDim.x;
-    f32x4 xn[2];
+    const f32x4 xn = (gn < G && tid < XQ) ? load_x4(p, gn * CR, tid) : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    // ---- conv2: h1 -> h2, M tiles 0..4 (wh 0) / 5..8 (wh 1), two per pass ----
+    {
+      const int t0 = wh ? 5 : 0, nt = wh ? 4 : 5;
+      for (int i = 0; i < nt; i += 2) {
+        const bool two = i + 1 < nt;
+        int base[2];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int i = tid + 256 * u;
-      xn[u] = (gn < G && i < XQ) ? load_x4(p, gn * CR, i) : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    }
-    // ---- conv2: h1 -> h2, two M tiles per pass (independent accumulators) ----
-    for (int mt = 0; mt < M2 / 16; mt += 2) {
-      const bool two = mt + 1 < M2 / 16;
-      int base[2];
+        for (int s = 0; s < 2; ++s) {
+          const int m = 16 * (t0 + min(i + s, nt - 1)) + i16, r = m / CP2, pp = m - r * CP2;
+          base[s] = (r * CP1 + CS2 * pp) * LD1 + 4 * q;
+        }
+        f32x4 acc[2] = {{0.0f, 0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}};
+        // k = 16 kb + 4 q + j: tap kb / 2, channel 16 (kb % 2) + 4 q + j; the next block's A
+        // reads are issued before this block's MFMAs (pinning them there with scheduling
+        // barriers measured slower on the 4-wave kernel: 46.2 vs 42.4 us, profiles/r05y)
+        auto off2 = [](int kb) { return (kb >> 1) * LD1 + (kb & 1) * 16; };
+        f32x4 nx0 = *reinterpret_cast<const f32x4*>(h1s + base[0] + off2(0));
+        f32x4 nx1 = *reinterpret_cast<const f32x4*>(h1s + base[1] + off2(0));
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const int m = 16 * min(mt + s, M2 / 16 - 1) + i16, r = m / CP2, pp = m - r * CP2;
-        base[s] = (r * CP1 + CS2 * pp) * LD1 + 4 * q;
-      }
-      f32x4 acc[2] = {{0.0f, 0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}};
-      // k = 16 kb + 4 q + j: tap kb / 2, channel 16 (kb % 2) + 4 q + j; the next block's A
-      // reads are issued before this block's MFMAs (pinning them there with scheduling
-      // barriers measured slower: 46.2 vs 42.4 us, profiles/r05y)
-      auto off2 = [](int kb) { return (kb >> 1) * LD1 + (kb & 1) * 16; };
-      f32x4 nx0 = *reinterpret_cast<const f32x4*>(h1s + base[0] + off2(0));
-      f32x4 nx1 = *reinterpret_cast<const f32x4*>(h1s + base[1] + off2(0));
+        for (int kb = 0; kb < CK2 * CF1 / 16; ++kb) {
+          const f32x4 a0 = nx0, a1 = nx1;
+          if (kb + 1 < CK2 * CF1 / 16) {
+            nx0 = *reinterpret_cast<const f32x4*>(h1s + base[0] + off2(kb + 1));
+            nx1 = *reinterpret_cast<const f32x4*>(h1s + base[1] + off2(kb + 1));
+          }
 #pragma unroll
-      for (int kb = 0; kb < CK2 * CF1 / 16; ++kb) {
-        const f32x4 a0 = nx0, a1 = nx1;
-        if (kb + 1 < CK2 * CF1 / 16) {
-          nx0 = *reinterpret_cast<const f32x4*>(h1s + base[0] + off2(kb + 1));
-          nx1 = *reinterpret_cast<const f32x4*>(h1s + base[1] + off2(kb + 1));
+          for (int j = 0; j < 4; ++j) {
+            acc[0] = mfma4(a0[j], wr2[kb][j], acc[0]);
+            acc[1] = mfma4(a1[j], wr2[kb][j], acc[1]);
+          }
         }
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          acc[0] = mfma4(a0[j], wr2[kb][j], acc[0]);
-          acc[1] = mfma4(a1[j], wr2[kb][j], acc[1]);
-        }
-      }
+        for (int s = 0; s < 2; ++s) {
+          if (s == 1 && !two) break;
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        if (s == 1 && !two) break;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int mo = 16 * (mt + s) + 4 * q + e;
-          const float v = fmaxf(acc[s][e] + bias2, 0.0f);
-          h2s[mo * LD2 + n2] = v;
-          if (p.h2 && row0 + mo / CP2 < p.rows) p.h2[((int64_t)row0 * CP2 + mo) * CF2 + n2] = v;
+          for (int e = 0; e < 4; ++e) {
+            const int mo = 16 * (t0 + i + s) + 4 * q + e;
+            const float v = fmaxf(acc[s][e] + bias2, 0.0f);
+            h2s[mo * LD2 + n2] = v;
+            if (p.h2 && row0 + mo / CP2 < p.rows) p.h2[((int64_t)row0 * CP2 + mo) * CF2 + n2] = v;
+          }
         }
       }
     }
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int i = tid + 256 * u;
-      if (gn < G && i < XQ) store_x4(xs, i, xn[u]);
-    }
+    if (gn < G && tid < XQ) store_x4(xs, tid, xn);
     __syncthreads();  // h2s complete; the next group's xs staged
-    // ---- conv3: h2 -> h3 (HBM) ----
-    for (int mt = 0; mt < M3 / 16; mt += 2) {
-      const bool two = mt + 1 < M3 / 16;
-      int base[2];
+    // ---- conv3: h2 -> h3 (HBM), M tiles 0..3 (wh 0) / 4..6 (wh 1) ----
+    {
+      const int t0 = wh ? 4 : 0, nt = wh ? 3 : 4;
+      for (int i = 0; i < nt; i += 2) {
+        const bool two = i + 1 < nt;
+        int base[2];
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const int m = 16 * min(mt + s, M3 / 16 - 1) + i16, r = m / CP3, pp = m - r * CP3;
-        base[s] = (r * CP2 + CS3 * pp) * LD2 + 4 * q;
-      }
-      f32x4 acc[2] = {{0.0f, 0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}};
-      // tap kb / 4, channel 16 (kb % 4) + 4 q + j; reads one block ahead as in conv2
-      auto off3 = [](int kb) { return (kb >> 2) * LD2 + (kb & 3) * 16; };
-      f32x4 nx0 = *reinterpret_cast<const f32x4*>(h2s + base[0] + off3(0));
-      f32x4 nx1 = *reinterpret_cast<const f32x4*>(h2s + base[1] + off3(0));
+        for (int s = 0; s < 2; ++s) {
+          const int m = 16 * (t0 + min(i + s, nt - 1)) + i16, r = m / CP3, pp = m - r * CP3;
+          base[s] = (r * CP2 + CS3 * pp) * LD2 + 4 * q;
+        }
+        f32x4 acc[2] = {{0.0f, 0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}};
+        // tap kb / 4, channel 16 (kb % 4) + 4 q + j; reads one block ahead as in conv2
+        auto off3 = [](int kb) { return (kb >> 2) * LD2 + (kb & 3) * 16; };
+        f32x4 nx0 = *reinterpret_cast<const f32x4*>(h2s + base[0] + off3(0));
+        f32x4 nx1 = *reinterpret_cast<const f32x4*>(h2s + base[1] + off3(0));
 #pragma unroll
-      for (int kb = 0; kb < CK3 * CF2 / 16; ++kb) {
-        const f32x4 a0 = nx0, a1 = nx1;
-        if (kb + 1 < CK3 * CF2 / 16) {
-          nx0 = *reinterpret_cast<const f32x4*>(h2s + base[0] + off3(kb + 1));
-          nx1 = *reinterpret_cast<const f32x4*>(h2s + base[1] + off3(kb + 1));
+        for (int kb = 0; kb < CK3 * CF2 / 16; ++kb) {
+          const f32x4 a0 = nx0, a1 = nx1;
+          if (kb + 1 < CK3 * CF2 / 16) {
+            nx0 = *reinterpret_cast<const f32x4*>(h2s + base[0] + off3(kb + 1));
+            nx1 = *reinterpret_cast<const f32x4*>(h2s + base[1] + off3(kb + 1));
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            acc[0] = mfma4(a0[j], wr3[kb][j], acc[0]);
+            acc[1] = mfma4(a1[j], wr3[kb][j], acc[1]);
+          }
         }
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          acc[0] = mfma4(a0[j], wr3[kb][j], acc[0]);
-          acc[1] = mfma4(a1[j], wr3[kb][j], acc[1]);
-        }
-      }
+        for (int s = 0; s < 2; ++s) {
+          if (s == 1 && !two) break;
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        if (s == 1 && !two) break;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int mo = 16 * (mt + s) + 4 * q + e;
-          if (row0 + mo / CP3 < p.rows)
-            p.h3[((int64_t)row0 * CP3 + mo) * CF3 + n2] = fmaxf(acc[s][e] + bias3, 0.0f);
+          for (int e = 0; e < 4; ++e) {
+            const int mo = 16 * (t0 + i + s) + 4 * q + e;
+            if (row0 + mo / CP3 < p.rows)
+              p.h3[((int64_t)row0 * CP3 + mo) * CF3 + n2] = fmaxf(acc[s][e] + bias3, 0.0f);
+          }
         }
       }
     }
@@ -612,7 +612,7 @@ extern "C" int xa_conv_stack_fwd(const XaConvStackArgs* a, void* stream) {
                "xa_conv_stack_fwd: x must be %d-B aligned", p.x_u8 ? 4 : 16);
   const int G = (p.rows + CR - 1) / CR;
   const int grid = G < cu_count() ? G : cu_count();
-  hipLaunchKernelGGL(conv_stack_fwd_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, p);
+  hipLaunchKernelGGL(conv_stack_fwd_kernel, dim3(grid), dim3(512), 0, (hipStream_t)stream, p);
   XA_CHECK_LAUNCH("xa_conv_stack_fwd");
   return 0;
 }

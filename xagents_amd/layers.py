@@ -25,6 +25,11 @@ from xagents_amd._lib import (XA_ACT_NONE, XA_ACT_RELU, XA_ACT_TANH, XaAdamApply
                               XaConvStackArgs, XaConvStackBwdArgs, XaGemmArgs, call, stream)
 
 _FORCE = int(os.environ.get('XA_GEMM_FORCE', '0'))
+# algorithmic FLOPs per frame row of the NatureCNN conv stack (2 x MACs): forward conv1 +
+# conv2 + conv3 = 2 (20 x 32 x 8 + 9 x 64 x 128 + 7 x 64 x 192); backward = every layer's
+# weight gradient (= its forward) + the input gradients of conv2 and conv3
+STACK_FWD_FLOPS = 2 * (20 * 32 * 8 + 9 * 64 * 128 + 7 * 64 * 192)
+STACK_BWD_FLOPS = STACK_FWD_FLOPS + 2 * (9 * 64 * 128 + 7 * 64 * 192)
 _ACTS = {None: XA_ACT_NONE, 'linear': XA_ACT_NONE, 'relu': XA_ACT_RELU, 'tanh': XA_ACT_TANH}
 
 
@@ -188,7 +193,9 @@ class LayerExecutor:
         if self.keep_hidden:
             a.h1, a.h2 = self.outs[0].data_ptr(), self.outs[1].data_ptr()
         a.h3 = self.outs[2].data_ptr()
+        ev = self._timing_start()
         call('xa_conv_stack_fwd', ctypes_ref(a), stream())
+        self._timing_end(ev, f'conv stack fwd {a.rows} rows', float(STACK_FWD_FLOPS) * a.rows)
 
     def _conv_stack_bwd(self, Bb, gp, accumulate):
         """Layers 2..0's parameter gradient in one fused launch + reduce (xa_conv_stack_bwd)
@@ -207,7 +214,10 @@ class LayerExecutor:
                              self.douts[2].data_ptr())
         a.ws, a.ws_floats = self.stack_ws.data_ptr(), self.stack_ws.numel()
         a.grad, a.accumulate = gp + 4 * w1, int(accumulate)
+        ev = self._timing_start()
         call('xa_conv_stack_bwd', ctypes_ref(a), stream())
+        self._timing_end(ev, f'conv stack bwd {rows} rows (+ reduce)',
+                         float(STACK_BWD_FLOPS) * rows)
 
     def _stack_bwd_ok(self):
         """The fused backward covers layers 0-2 when they are the stack, contiguous in theta
@@ -265,11 +275,13 @@ class LayerExecutor:
         e.record()
         return e
 
-    def _timing_end(self, e0, name, flops):
+    def _timing_end(self, e0, name, flops, nbytes=None):
+        """(name, start, end, algorithmic FLOPs, algorithmic HBM bytes or None when the
+        launch is MFMA-bound) -- bench.py's dominant-kernel roofline."""
         if e0 is not None:
             e1 = torch.cuda.Event(enable_timing=True)
             e1.record()
-            self.timing.append((name, e0, e1, flops))
+            self.timing.append((name, e0, e1, flops, nbytes))
 
     # ---- shapes --------------------------------------------------------------
     def _src_shape(self, i):
@@ -327,10 +339,13 @@ class LayerExecutor:
             src_u8 = u8 and j == -1
             w0, b0 = self.offsets[i]
             if l.kind == 'dense':
+                ev = self._timing_start()
                 gemm(self.B, l.units, l.in_features, src.data_ptr(), tp + 4 * w0,
                      self.outs[i].data_ptr(), a_u8=src_u8, a_m=(1, l.in_features, 0),
                      b_ks=l.units, b_ns=1, ldc=l.units, bias=tp + 4 * b0,
                      act=self._act(i), workspace=self.workspace)
+                self._timing_end(ev, f'dense fwd {self.B}x{l.units}x{l.in_features}',
+                                 2.0 * self.B * l.units * l.in_features)
             else:
                 rows, Win, P, C = self._conv_dims(i)
                 gemm(rows * P, l.filters, l.size * C, src.data_ptr(), tp + 4 * w0,
@@ -451,6 +466,7 @@ class LayerExecutor:
                 fused = adam is not None and i in adam
 
                 def wgrad():
+                    ev = self._timing_start()
                     if fused:
                         # [W; b] gradient + the layer's Adam step in one launch; reads W's
                         # old value nowhere (the input gradient below ran first)
@@ -471,6 +487,14 @@ class LayerExecutor:
                             gemm(1, n_out, Bb, None, d.data_ptr(), gp + 4 * b0, a_m=(1, 0, 0),
                                  a_k=(1, 0, 0), b_ks=n_out, b_ns=1, ldc=n_out, beta=accumulate,
                                  workspace=self.workspace)
+                    if fused:
+                        # HBM-bound: theta, m, v read + written (24 B per parameter), X, dZ
+                        self._timing_end(ev, f'dense dW+Adam {n_in}x{n_out}x{Bb}',
+                                         2.0 * (n_in + 1) * n_out * Bb,
+                                         24.0 * (n_in + 1) * n_out + 4.0 * Bb * (n_in + n_out))
+                    elif gp is not None:
+                        self._timing_end(ev, f'dense dW {n_in}x{n_out}x{Bb}',
+                                         2.0 * (n_in + 1) * n_out * Bb)
                     if gp is not None and on_grad is not None:
                         on_grad(w0)
 
