@@ -847,10 +847,10 @@ __global__ __launch_bounds__(64) void gemm_skinny_kernel(XaGemmArgs g) {
 // DQN's act / target forwards, 32 / 64 x 512 x 37632): HBM-bound on the weight, which every
 // other path reads in short K pieces per 64-column tile. Here workgroup z owns one
 // contiguous K range and ALL 512 columns of a column block, so the weight streams in
-// whole 2-KB rows, once: lane l loads 16 B of row k + (l >> 5) (lanes 0..31 one 512-B
-// half-row each wave, 4 waves = 512 columns) and feeds the 4 floats to 4 MFMAs whose
-// column i is the real column 4 i + j (a column permutation the epilogue undoes with one
-// 16-B partial store per row). A's slice sits in LDS (k-major, zero-padded), 16 k-pairs of
+// whole 2-KB rows, once: lane l loads CW floats of row k + (l >> 5) (lanes 0..31 one
+// 32 CW-column slice each wave, 512 columns per workgroup) and feeds them to CW MFMAs whose
+// column i is the real column CW i + j (a column permutation the epilogue undoes with one
+// 4 CW-byte partial store per row). A's slice sits in LDS (k-major, zero-padded), 16 k-pairs of
 // the weight are in flight per lane, and nothing synchronises after the A fill. Partials
 // [splits][M][N] go to the usual fixed-order split reduce (bias / activation / gate / beta).
 // ---------------------------------------------------------------------------
@@ -870,9 +870,22 @@ __host__ __device__ inline int stream_rows(int per) {
   return (per + 2 * ST_U - 1) / (2 * ST_U) * (2 * ST_U);
 }
 
-template <int MB>
-__global__ __launch_bounds__(256) void gemm_stream_kernel(XaGemmArgs g) {
-  constexpr int MR = 32 * MB, LDA = MR + 1;
+template <int CW>
+XA_DEV auto stream_load(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  if constexpr (CW == 4) {
+    return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, kStAuxNt);
+  } else {
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, kStAuxNt));
+  }
+}
+
+// CW columns per lane: CW = 2 -> 8 waves of 64 columns (8-B loads, the launched form: two
+// waves per SIMD interleave their MFMA chains and LDS waits), CW = 4 -> 4 waves of 128
+template <int MB, int CW>
+__global__ __launch_bounds__(ST_NCOL / CW * 2) void gemm_stream_kernel(XaGemmArgs g) {
+  constexpr int MR = 32 * MB, LDA = MR + 1, NTH = ST_NCOL / CW * 2, WCOL = 32 * CW;
+  typedef float fv __attribute__((ext_vector_type(CW)));
   extern __shared__ float as[];  // [per][LDA]: A(m, kb + kk) at as[kk LDA + m]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
   const int z = blockIdx.x, n_base = blockIdx.y * ST_NCOL;
@@ -880,12 +893,12 @@ __global__ __launch_bounds__(256) void gemm_stream_kernel(XaGemmArgs g) {
   const int kb = min(g.K, z * per), ke = min(g.K, kb + per);
   const float* a = static_cast<const float*>(g.a);
   const int np = (ke - kb) / 2;  // K ranges are multiples of 4 (K % 4 == 0 is checked)
-  const int col = n_base + 128 * w + 4 * (lane & 31);
-  f32x16 acc[MB][4];
+  const int col = n_base + WCOL * w + CW * (lane & 31);
+  f32x16 acc[MB][CW];
 #pragma unroll
   for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < CW; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[mb][j][r] = 0.0f;
   // the weight through a raw buffer resource at this range's first row (lane offset + pair
@@ -899,30 +912,29 @@ __global__ __launch_bounds__(256) void gemm_stream_kernel(XaGemmArgs g) {
   const uint32_t lane_off = (uint32_t)(h * g.b_ks + col) * 4u;
   const uint32_t pbytes = (uint32_t)(2 * g.b_ks) * 4u;
   const int last = max(np - 1, 0), nch = (np + ST_U - 1) / ST_U;
-  f32x4 wv[ST_U];
+  fv wv[ST_U];
   // the first ST_U pairs' loads go out before the A fill (their latency overlaps it)
   if (np > 0) {
 #pragma unroll
     for (int u = 0; u < ST_U; ++u)
-      wv[u] = __builtin_amdgcn_raw_buffer_load_b128(wr, lane_off + (uint32_t)min(u, last) * pbytes,
-                                                    0, kStAuxNt);
+      wv[u] = stream_load<CW>(wr, lane_off + (uint32_t)min(u, last) * pbytes);
   }
   // A slice -> LDS (16-B loads along k, transposed scalar stores), zeros past ke / M
   const int q_per = stream_rows(per) / 4, total = MR * q_per;
   if (ke > kb) {
     // 8 loads in flight per thread (clamped in-range addresses, masked after the load)
-    for (int i0 = 0; i0 < total; i0 += 256 * 8) {
+    for (int i0 = 0; i0 < total; i0 += NTH * 8) {
       f32x4 v[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const int i = min(i0 + 256 * j + tid, total - 1);
+        const int i = min(i0 + NTH * j + tid, total - 1);
         const int m = i / q_per, k = kb + 4 * (i - m * q_per);
         v[j] = *reinterpret_cast<const f32x4*>(a + (int64_t)min(m, g.M - 1) * g.a_rm +
                                                min(k, ke - 4));
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const int i = i0 + 256 * j + tid;
+        const int i = i0 + NTH * j + tid;
         if (i >= total) break;
         const int m = i / q_per, kq = i - m * q_per;
         const bool ok = m < g.M && kb + 4 * kq < ke;
@@ -943,16 +955,14 @@ __global__ __launch_bounds__(256) void gemm_stream_kernel(XaGemmArgs g) {
         for (int mb = 0; mb < MB; ++mb) {
           const float av = ar[32 * mb];
 #pragma unroll
-          for (int j = 0; j < 4; ++j) acc[mb][j] = mfma32(av, wv[u][j], acc[mb][j]);
+          for (int j = 0; j < CW; ++j) acc[mb][j] = mfma32(av, wv[u][j], acc[mb][j]);
         }
-        if (c + 1 < ST_NCH)
-          wv[u] = __builtin_amdgcn_raw_buffer_load_b128(
-              wr, lane_off + (uint32_t)min(p + ST_U, last) * pbytes, 0, kStAuxNt);
+        if (c + 1 < ST_NCH) wv[u] = stream_load<CW>(wr, lane_off + (uint32_t)min(p + ST_U, last) * pbytes);
         __builtin_amdgcn_sched_barrier(0);
       }
     }
   }
-  // D(row (r&3) + 8 (r>>2) + 4 h, col i = l&31) of MFMA j is C(row, 4 i + j)
+  // D(row (r&3) + 8 (r>>2) + 4 h, col i = l&31) of MFMA j is C(row, CW i + j)
   float* part = g.partials + (int64_t)z * g.M * g.N;
 #pragma unroll
   for (int mb = 0; mb < MB; ++mb)
@@ -960,8 +970,10 @@ __global__ __launch_bounds__(256) void gemm_stream_kernel(XaGemmArgs g) {
     for (int r = 0; r < 16; ++r) {
       const int m = 32 * mb + (r & 3) + 8 * (r >> 2) + 4 * h;
       if (m >= g.M) continue;
-      const f32x4 v = {acc[mb][0][r], acc[mb][1][r], acc[mb][2][r], acc[mb][3][r]};
-      *reinterpret_cast<f32x4*>(part + (int64_t)m * g.N + col) = v;
+      fv v;
+#pragma unroll
+      for (int j = 0; j < CW; ++j) v[j] = acc[mb][j][r];
+      *reinterpret_cast<fv*>(part + (int64_t)m * g.N + col) = v;
     }
 }
 
@@ -1542,10 +1554,12 @@ extern "C" int xa_gemm(const XaGemmArgs* p, void* stream) {
   const XaGemmK kg = kernel_args(g);
   if (use_stream) {
     const dim3 gs(g.splits, g.N / ST_NCOL);
+    // 8 waves of 64 columns (8-B loads): 20.5 / 32.9 us at M = 32 / 64 against 21.0 / 34.2
+    // for 4 waves of 128 columns (16-B loads), profiles/r05zs_stream_cw_ab.txt
     if (g.M <= 32)
-      hipLaunchKernelGGL(gemm_stream_kernel<1>, gs, dim3(256), stream_lds(g), s, g);
+      hipLaunchKernelGGL((gemm_stream_kernel<1, 2>), gs, dim3(512), stream_lds(g), s, g);
     else
-      hipLaunchKernelGGL(gemm_stream_kernel<2>, gs, dim3(256), stream_lds(g), s, g);
+      hipLaunchKernelGGL((gemm_stream_kernel<2, 2>), gs, dim3(512), stream_lds(g), s, g);
   } else if (shape == 2) {
     hipLaunchKernelGGL(colsum_kernel, dim3(1, (g.N + 63) / 64, g.splits), dim3(256), 0, s, g);
   } else if (shape == 1) {
