@@ -581,6 +581,27 @@ int xa_dqn_td_grad(const float* q, const float* q_next_target, const float* q_ne
                    int n_actions, float gamma, float huber_delta, float* dq, float* loss,
                    int* adam_step, void* stream);
 
+/* The Q head (the last dense layer, N <= 8 actions: xa_gemm's row-dot shape) with DQN's
+ * per-row step fused into the same launch. mode 0: actions[m] = first argmax of row m
+ * (xa_dqn_act's greedy branch); mode 1: the head is the TARGET network's over s', and row b
+ * finishes xa_dqn_td_grad's arithmetic for sample b (q = the online Q [B][A], q_next_online
+ * for double DQN or NULL, act / rewards / dones, gamma, huber, dq / loss outputs, adam_step
+ * bumped). args->c still receives the head's Q values. */
+typedef struct XaDqnHeadArgs {
+  int mode;
+  int* actions;
+  const float* q;
+  const float* q_next_online;
+  const int* act;
+  const float* rewards;
+  const float* dones;
+  float gamma, huber;
+  float* dq;
+  float* loss;
+  int* adam_step;
+} XaDqnHeadArgs;
+int xa_dqn_head(const XaGemmArgs* head, const XaDqnHeadArgs* dqn, void* stream);
+
 /* Replay rings (ReplayBuffer1 xagents/utils/buffers.py:59-98, ReplayBuffer2 101-148):
  * ring[slots[i]] = src[i] / dst[i] = ring[slots[i]] for items of item_bytes. The host
  * computes slots with the reference's index semantics (deque order + random.sample for

@@ -123,6 +123,13 @@ for step in "$@"; do
       B4="python bench.py --config c4 --steps 3 --warmup 1 --cpu-baseline-seconds 0"
       run b84_on 400 $B4
       XA_CONV_BWD8=0 run b84_off 400 $B4 ;;
+    headab)
+      # DQN argmax / TD step fused into the Q head launch (default) vs separate launches
+      B="python bench.py --config c3 --steps 30 --warmup 5 --cpu-baseline-seconds 0"
+      run hd_on1 300 $B
+      XA_DQN_FUSED_HEAD=0 run hd_off1 300 $B
+      run hd_on2 300 $B
+      XA_DQN_FUSED_HEAD=0 run hd_off2 300 $B ;;
     cnn) run_pytest cnn 600 tests/test_gpu_cnn_onpolicy.py tests/test_gpu_acer.py tests/test_gpu_atari.py ;;
     dqn) run_pytest dqn 400 tests/test_gpu_dqn.py tests/test_gpu_scale.py -k "dqn" tests/test_gpu_configs.py::test_c3_dqn_32_envs_rb1_1m_batch_64 ;;
     td3time)

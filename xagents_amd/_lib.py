@@ -224,6 +224,15 @@ class XaConvStackBwdArgs(Structure):
     ]
 
 
+class XaDqnHeadArgs(Structure):
+    _fields_ = [
+        ('mode', c_int), ('actions', c_void_p), ('q', c_void_p), ('q_next_online', c_void_p),
+        ('act', c_void_p), ('rewards', c_void_p), ('dones', c_void_p),
+        ('gamma', c_float), ('huber', c_float), ('dq', c_void_p), ('loss', c_void_p),
+        ('adam_step', c_void_p),
+    ]
+
+
 class XaAtariStepArgs(Structure):
     _fields_ = [
         ('n_envs', c_int), ('t_raw', c_int), ('height', c_int), ('width', c_int),
@@ -428,6 +437,7 @@ _SIGNATURES = {
     'xa_gemm': (c_int, [POINTER(XaGemmArgs), c_void_p]),
     'xa_gemm_adam': (c_int, [POINTER(XaGemmArgs), POINTER(XaAdamApply), c_void_p]),
     'xa_conv_stack_fwd': (c_int, [POINTER(XaConvStackArgs), c_void_p]),
+    'xa_dqn_head': (c_int, [POINTER(XaGemmArgs), POINTER(XaDqnHeadArgs), c_void_p]),
     'xa_conv_stack_bwd': (c_int, [POINTER(XaConvStackBwdArgs), c_void_p]),
     'xa_conv_stack_bwd_workspace_floats': (ctypes.c_size_t, [c_int]),
     'xa_gemm_splits': (c_int, [c_int, c_int, c_int]),

@@ -706,10 +706,8 @@ __global__ __launch_bounds__(512) void gemm_smallm_res_kernel(XaGemmArgs g, int 
 // ---------------------------------------------------------------------------
 constexpr int RD_MAXN = 8;
 
-__global__ __launch_bounds__(256) void gemm_rowdot_kernel(XaGemmArgs g) {
-  const int lane = threadIdx.x & 63;
-  const int m = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (m >= g.M) return;
+// lane n (< N) returns column n of row m (epilogue applied); other lanes 0
+XA_DEV float rowdot_row(const XaGemmArgs& g, int m, int lane) {
   const float* a = static_cast<const float*>(g.a) + (int64_t)m * g.a_rm;
   float acc[RD_MAXN];
 #pragma unroll
@@ -742,7 +740,83 @@ __global__ __launch_bounds__(256) void gemm_rowdot_kernel(XaGemmArgs g) {
     for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off);
     if (lane == n) v = t;
   }
-  if (lane < g.N) store_c(epilogue(v, lane, g), m, lane, g);
+  return lane < g.N ? epilogue(v, lane, g) : 0.0f;
+}
+
+__global__ __launch_bounds__(256) void gemm_rowdot_kernel(XaGemmArgs g) {
+  const int lane = threadIdx.x & 63;
+  const int m = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (m >= g.M) return;
+  const float v = rowdot_row(g, m, lane);
+  if (lane < g.N) store_c(v, m, lane, g);
+}
+
+// DQN's per-row heads fused into the Q head's row-dot launch (one launch fewer per use):
+// mode 0 (act, dqn/agent.py:107-116): actions[m] = first argmax of the row's Q values;
+// mode 1 (TD, dqn/agent.py:118-171): the head is the TARGET network's, row b = sample b:
+// exactly xa_dqn_td_grad's arithmetic (offpolicy.hip dqn_td_kernel) with Qt(s') taken from
+// the lanes instead of memory; the optimizer step bump rides along
+__global__ __launch_bounds__(256) void dqn_head_kernel(XaGemmArgs g, XaDqnHeadArgs d) {
+  const int lane = threadIdx.x & 63;
+  const int m = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (d.mode == 1 && d.adam_step && blockIdx.x == 0 && threadIdx.x == 0) d.adam_step[0] += 1;
+  if (m >= g.M) return;
+  const float v = rowdot_row(g, m, lane);
+  if (lane < g.N) store_c(v, m, lane, g);
+  const int A = g.N;
+  float qv[RD_MAXN];
+#pragma unroll
+  for (int n = 0; n < RD_MAXN; ++n) qv[n] = __shfl(v, n);
+  if (d.mode == 0) {
+    if (lane == 0) {
+      int best = 0;
+      float bv = qv[0];
+#pragma unroll
+      for (int a = 1; a < RD_MAXN; ++a)
+        if (a < A && qv[a] > bv) {
+          bv = qv[a];
+          best = a;
+        }
+      d.actions[m] = best;
+    }
+    return;
+  }
+  const int b = m;
+  float vn;
+  if (d.q_next_online) {
+    const float* qo = d.q_next_online + (int64_t)b * A;
+    int best = 0;
+    float bv = qo[0];
+    for (int a = 1; a < A; ++a)
+      if (qo[a] > bv) {
+        bv = qo[a];
+        best = a;
+      }
+    vn = qv[0];
+#pragma unroll
+    for (int a = 1; a < RD_MAXN; ++a)
+      if (a == best) vn = qv[a];
+  } else {
+    vn = qv[0];
+#pragma unroll
+    for (int a = 1; a < RD_MAXN; ++a)
+      if (a < A) vn = fmaxf(vn, qv[a]);
+  }
+  if (d.dones[b] != 0.0f) vn = 0.0f;
+  const float y = vn * d.gamma + d.rewards[b];
+  const int ab = d.act[b];
+  const float diff = y - d.q[(int64_t)b * A + ab];
+  float dqa, l;
+  if (d.huber > 0.0f) {
+    const float ad = fabsf(diff);
+    dqa = -fminf(fmaxf(diff, -d.huber), d.huber) / (float)A;
+    l = (ad <= d.huber ? 0.5f * (diff * diff) : d.huber * (ad - 0.5f * d.huber)) / (float)A;
+  } else {
+    dqa = (-2.0f * diff) / (float)A;
+    l = (diff * diff) / (float)A;
+  }
+  if (lane < A) d.dq[(int64_t)b * A + lane] = lane == ab ? dqa : 0.0f;
+  if (lane == 0 && d.loss) d.loss[b] = l;
 }
 
 // Few-k GEMM (K <= 8: the network heads' input gradient dZ W^T, K = the head width): one
@@ -1593,6 +1667,21 @@ extern "C" int xa_gemm(const XaGemmArgs* p, void* stream) {
     }
     XA_CHECK_LAUNCH("xa_gemm (split reduce)");
   }
+  return 0;
+}
+
+
+extern "C" int xa_dqn_head(const XaGemmArgs* p, const XaDqnHeadArgs* d, void* stream) {
+  XA_CHECK_ARG(p != nullptr && d != nullptr, "xa_dqn_head: null args");
+  const XaGemmArgs& g = *p;
+  XA_CHECK_ARG(g.M > 0 && g.N > 0 && g.K > 0 && g.b && g.c && rowdot_ok(g) && !g.gate && !g.beta,
+               "xa_dqn_head: needs the row-dot head shape (f32 plain rows, N <= %d, K <= 4096, "
+               "no gate / beta)", RD_MAXN);
+  XA_CHECK_ARG(d->mode == 0 ? d->actions != nullptr
+                            : (d->mode == 1 && d->q && d->act && d->rewards && d->dones && d->dq),
+               "xa_dqn_head: mode 0 needs actions, mode 1 q / act / rewards / dones / dq");
+  hipLaunchKernelGGL(dqn_head_kernel, dim3((g.M + 3) / 4), dim3(256), 0, (hipStream_t)stream, g, *d);
+  XA_CHECK_LAUNCH("xa_dqn_head");
   return 0;
 }
 

@@ -113,11 +113,51 @@ class DQN(OffPolicy):
             self._rand_actions.copy_(torch.from_numpy(r.astype(np.int32)))
             call('xa_dqn_act', None, self.n_envs, self.n_actions,
                  self._rand_actions.data_ptr(), 1, self.actions.data_ptr(), stream())
+        elif self._head_fused():
+            # greedy: the argmax rides in the Q head's launch (xa_dqn_head mode 0)
+            self.ex_act.forward(self.envs.state, head=self._head_args('act'))
         else:
             q = self.ex_act.forward(self.envs.state)[0]
             call('xa_dqn_act', q.data_ptr(), self.n_envs, self.n_actions, None, 0,
                  self.actions.data_ptr(), stream())
         return self.actions
+
+    def _head_fused(self):
+        """The Q head (last layer: dense, <= 8 actions, linear, K <= 4096) can run as
+        xa_dqn_head (XA_DQN_FUSED_HEAD=0: separate xa_dqn_act / xa_dqn_td_grad launches)."""
+        if '_hf' not in self.__dict__:
+            import os
+            ls = self.model.layers
+            last = ls[-1]
+            self._hf = (os.environ.get('XA_DQN_FUSED_HEAD', '1') != '0' and
+                        last.kind == 'dense' and last.units <= 8 and
+                        last.in_features <= 4096 and last.activation in (None, 'linear') and
+                        list(self.model.outputs) == [len(ls) - 1])
+        return self._hf
+
+    def _head_args(self, kind):
+        """XaDqnHeadArgs of the acting head (argmax into self.actions) or of the target
+        head (TD target + MSE / Huber gradient of the sampled batch, t += 1)."""
+        cache = self.__dict__.setdefault('_head_cache', {})
+        if kind not in cache:
+            from xagents_amd._lib import XaDqnHeadArgs
+            h = XaDqnHeadArgs()
+            if kind == 'act':
+                h.mode, h.actions = 0, self.actions.data_ptr()
+            else:
+                B = self.batch_size
+                q_all = self.ex_online.outs[-1]
+                h.mode = 1
+                h.q = q_all.data_ptr()
+                h.q_next_online = q_all[B:].data_ptr() if self.double else None
+                h.act, h.rewards = self.b_act.data_ptr(), self.b_rew.data_ptr()
+                h.dones = self.b_done.data_ptr()
+                h.gamma = kernels._f32(self.gamma)
+                h.huber = kernels._f32(self.huber_delta or 0.0)
+                h.dq, h.loss = self.dq.data_ptr(), self.td_loss.data_ptr()
+                h.adam_step = self.model.optimizer.iterations.data_ptr()
+            cache[kind] = h
+        return cache[kind]
 
     def _play_actions(self):
         """play(): greedy argmax Q for every env (get_model_outputs(...)[0],
@@ -141,6 +181,10 @@ class DQN(OffPolicy):
         Adam reads it after the backward)."""
         B = self.batch_size
         q_all = self.ex_online.forward(self.xb if self.double else self.xb[:B])[0]
+        if self._head_fused():
+            # the TD target and its gradient ride in the target head's launch (mode 1)
+            self.ex_target.forward(self.xb[B:], head=self._head_args('td'))
+            return
         q_next_t = self.ex_target.forward(self.xb[B:])[0]
         q_next_o = q_all[B:].data_ptr() if self.double else None
         call('xa_dqn_td_grad', q_all.data_ptr(), q_next_t.data_ptr(), q_next_o,

@@ -322,8 +322,10 @@ class LayerExecutor:
         return []
 
     # ---- forward ---------------------------------------------------------------
-    def forward(self, x):
-        """x: [B, *input_shape] uint8 (images) or f32. Returns the output layers' tensors."""
+    def forward(self, x, head=None):
+        """x: [B, *input_shape] uint8 (images) or f32. Returns the output layers' tensors.
+        `head` (an XaDqnHeadArgs): the last layer, a row-dot-shaped Q head, runs as
+        xa_dqn_head with DQN's per-row step (argmax or TD target + gradient) in its launch."""
         assert x.shape[0] == self.B and x.is_contiguous()
         theta = self.model.theta
         tp = theta.data_ptr()
@@ -340,10 +342,16 @@ class LayerExecutor:
             w0, b0 = self.offsets[i]
             if l.kind == 'dense':
                 ev = self._timing_start()
-                gemm(self.B, l.units, l.in_features, src.data_ptr(), tp + 4 * w0,
-                     self.outs[i].data_ptr(), a_u8=src_u8, a_m=(1, l.in_features, 0),
-                     b_ks=l.units, b_ns=1, ldc=l.units, bias=tp + 4 * b0,
-                     act=self._act(i), workspace=self.workspace)
+                kw = dict(a_u8=src_u8, a_m=(1, l.in_features, 0), b_ks=l.units, b_ns=1,
+                          ldc=l.units, bias=tp + 4 * b0, act=self._act(i),
+                          workspace=self.workspace)
+                if head is not None and i == len(self.layers) - 1:
+                    g = _gemm_args(self.B, l.units, l.in_features, src.data_ptr(), tp + 4 * w0,
+                                   self.outs[i].data_ptr(), **kw)
+                    call('xa_dqn_head', ctypes_ref(g), ctypes_ref(head), stream())
+                else:
+                    gemm(self.B, l.units, l.in_features, src.data_ptr(), tp + 4 * w0,
+                         self.outs[i].data_ptr(), **kw)
                 self._timing_end(ev, f'dense fwd {self.B}x{l.units}x{l.in_features}',
                                  2.0 * self.B * l.units * l.in_features)
             else:
