@@ -148,6 +148,17 @@ def test_rollout_replay_uniforms_bit_exact(device, return_kind):
     assert ref['done'].sum() > 0
 
 
+@pytest.mark.parametrize('n,t,t_rec,return_kind', [(3, 1, 7, 1), (5, 255, 97, 2), (4, 256, 300, 2),
+                                                  (2, 300, 61, 1), (9, 16, 5, 1)])
+def test_rollout_replay_ragged_rows_bit_exact(device, n, t, t_rec, return_kind):
+    """Step counts around the batched rollout's 16-row tiles and 256-row passes (T + 1 rows,
+    the last the bootstrap value), records that wrap inside a pass."""
+    rec = _replay_env(n, t_rec, seed=t)
+    rng = np.random.default_rng(t)
+    u = [rng.random((n, t), dtype=np.float32) for _ in range(2)]
+    _run_rollout(_theta(4, 2, t, 0.4), rec, n, t, u, 0, 0, return_kind)
+
+
 def test_rollout_replay_philox_bit_exact(device):
     n, t = 64, 128
     rec = _replay_env(n, 300, seed=6)

@@ -18,6 +18,9 @@
 #   pollab   persistent-update poll sleep variants: bench + C2 FETCH_SIZE
 #   c2g      C2 bench lines at update grids $C2_GS (XA_PPO_MAX_BLOCKS)
 #   profc3   rocprofv3 kernel trace of the C3 bench + per-(kernel, grid) summary
+#   rollab   replay rollout tests + bench A/B, batched MFMA rollout on / off (XA_REPLAY_BATCHED)
+#   rstamps  per-phase stamps of the batched replay rollout (tools/rollout_stamps.py; build
+#            tools/diag_lib/libxa_rstamp.so first: tools/build_variant.py rstamp -DXA_STAMPS --src mlp_rollout)
 #   layers   tests/test_gpu_layers.py (GEMM paths, layer executor)
 #   streamab C3 bench lines, streaming dense forward on / off, interleaved
 #   stackab  C3 bench lines, fused conv-stack forward on / off, interleaved
@@ -84,6 +87,16 @@ for step in "$@"; do
       run fix_on2 200 $B
       XA_PPO_FIXED_SHAPE=0 run fix_off2 200 $B
       python tools/bench_brief.py gpurun_out/${T}_fix_*.out ;;
+    rollab)
+      # the batched replay rollout (all T + 1 forwards as MFMA row tiles) vs the step loop
+      run_pytest roll 200 tests/test_gpu_kernels.py -k rollout
+      XA_LIB=tools/diag_lib/libxa_rstamp.so run rstamps 200 python tools/rollout_stamps.py 16 256
+      B="python bench.py --steps 40 --warmup 5 --cpu-baseline-seconds 0 --no-secondary"
+      run roll_on1 200 $B
+      XA_REPLAY_BATCHED=0 run roll_off1 200 $B
+      run roll_on2 200 $B
+      XA_REPLAY_BATCHED=0 run roll_off2 200 $B
+      python tools/bench_brief.py gpurun_out/${T}_roll_*.out ;;
     layers) run_pytest layers 300 tests/test_gpu_layers.py ;;
     streamab)
       # the streaming few-row dense forward vs the tile kernels (XA_GEMM_STREAM=0), C3 lines
@@ -109,6 +122,7 @@ for step in "$@"; do
       B4="python bench.py --config c4 --steps 3 --warmup 1 --cpu-baseline-seconds 0"
       run bw4_on 400 $B4
       XA_CONV_STACK_BWD=0 run bw4_off 400 $B4 ;;
+    rstamps) XA_LIB=tools/diag_lib/libxa_rstamp.so run rstamps 200 python tools/rollout_stamps.py 16 256 ;;
     cstamps) XA_LIB=tools/diag_lib/libxa_cstamp.so run cstamps 200 python tools/conv_stack_stamps.py 64 1024 ;;
     cstampv)
       # stamp variants tools/diag_lib/libxa_<v>.so for v in $CS_VARIANTS

@@ -579,9 +579,369 @@ __global__ __launch_bounds__(256) void mlp_forward_kernel(const float* __restric
   }
 }
 
+// ---- replay env: every step's policy input is known before the rollout starts ----------
+// The record stream ignores the actions, so step t's input is fixed in advance: the env
+// state for t = 0 and the record obs of step t - 1 after that; the bootstrap
+// V(get_states()) of ppo/agent.py:72 takes the post-reset record state of step T - 1. All
+// T forwards are therefore independent rows of one batched forward: 16-row tiles, one per
+// tile wave, W2 on v_mfma_f32_16x16x4f32 (an exact k-ordered fmaf chain), one accumulator
+// per interleaved chain r (k = r (mod 8)), so each h2 unit is the same 8 chains and the same
+// sum tree as the step loop's packed chains, bit for bit. Lane l of a tile holds row
+// m = l & 15 and chain slot j = l >> 4 (k = r + 32 h + 8 j for MFMA half h); layer 1 is
+// computed straight into that operand layout. Then lane per row: heads (chunk_heads'
+// butterfly tree), sample, log-prob, entropy, stores. Beside the tiles, one wave runs the
+// bootstrap forward (lane per unit, as the step loop) and one the episode-return scan
+// (records only); the fused returns follow the last pass. The two step-order chains run on
+// one lane from LDS with the per-step terms precomputed lane-parallel (same operations,
+// same order as xo_gae / xo_nstep and the step loop).
+constexpr int kRTW = 8;               // tile waves: 16-row tiles per pass
+constexpr int kRW = kRTW + 2;         // + the bootstrap wave and the episode-return wave
+constexpr int kRRows = 16 * kRTW;     // rows per pass (T = 128: one pass)
+constexpr int kBootW = kRTW, kScanW = kRTW + 1;
+
+typedef float rf32x4 __attribute__((ext_vector_type(4)));
+
+// xa_tanhf on two values with packed f32 ops: every lane of every op rounds exactly as the
+// scalar sequence does
+XA_DEV xa_f2 xa_tanhf2(xa_f2 x) {
+  const float c = 7.90531110763549805f;
+  const xa_f2 xc = {fminf(fmaxf(x.x, -c), c), fminf(fmaxf(x.y, -c), c)};
+  const xa_f2 x2 = xc * xc;
+  auto k2 = [](float v) { return xa_f2{v, v}; };
+  xa_f2 p = xa_fma2(x2, k2(-2.76076847742355e-16f), k2(2.00018790482477e-13f));
+  p = xa_fma2(x2, p, k2(-8.60467152213735e-11f));
+  p = xa_fma2(x2, p, k2(5.12229709037114e-08f));
+  p = xa_fma2(x2, p, k2(1.48572235717979e-05f));
+  p = xa_fma2(x2, p, k2(6.37261928875436e-04f));
+  p = xa_fma2(x2, p, k2(4.89352455891786e-03f));
+  p = xc * p;
+  xa_f2 q = xa_fma2(x2, k2(1.19825839466702e-06f), k2(1.18534705686654e-04f));
+  q = xa_fma2(x2, q, k2(2.26843463243900e-03f));
+  q = xa_fma2(x2, q, k2(4.89352518554385e-03f));
+  xa_f2 r = {__int_as_float(0x7EF311C3 - __float_as_int(q.x)),
+             __int_as_float(0x7EF311C3 - __float_as_int(q.y))};
+  r = xa_fma2(r, xa_fma2(-q, r, k2(1.0f)), r);
+  r = xa_fma2(r, xa_fma2(-q, r, k2(1.0f)), r);
+  const xa_f2 t = p * r;
+  return xa_fma2(r, xa_fma2(-q, t, p), t);
+}
+
+// record index of step t (the cursor wraps at t_rec)
+XA_DEV size_t replay_rec(const XaRolloutArgs& p, int env, int cur0, int t) {
+  return (size_t)env * p.t_rec + (size_t)(((uint32_t)cur0 + (uint32_t)t) % (uint32_t)p.t_rec);
+}
+
+// policy input of step t (0 <= t < T); t = T: the bootstrap input
+template <int OBS>
+XA_DEV const float* replay_input(const XaRolloutArgs& p, int env, int cur0, int t, int T) {
+  if (t == 0) return p.env_state + (size_t)env * OBS;
+  const size_t base = replay_rec(p, env, cur0, t - 1) * OBS;
+  return (t >= T ? p.rep_state : p.rep_obs) + base;
+}
+
+// a chunk-pass row's inputs, fetched a pass ahead
+template <int OBS>
+struct ReplayRow {
+  float r, d, u, x[OBS];
+  XA_DEV void load(const XaRolloutArgs& p, int env, int cur0, int t, int T, uint64_t ctr) {
+    const int tc = min(t, T - 1);
+    const size_t rb = replay_rec(p, env, cur0, tc);
+    r = p.rep_rew[rb];
+    d = p.rep_done[rb];
+    if (p.uniforms) {
+      u = p.uniforms[(size_t)env * T + tc];
+    } else {
+      const xa_u4 rr = xa_philox((uint32_t)env, (uint32_t)tc, (uint32_t)ctr, (uint32_t)(ctr >> 32),
+                                 (uint32_t)p.seed, (uint32_t)(p.seed >> 32));
+      u = xa_u01(rr.x);
+    }
+    const float* xin = replay_input<OBS>(p, env, cur0, tc, T);
+#pragma unroll
+    for (int k = 0; k < OBS; ++k) x[k] = xin[k];
+  }
+};
+
+template <int OBS, int A>
+__global__ __launch_bounds__(64 * kRW) void replay_rollout_kernel(XaRolloutArgs p) {
+  constexpr int AH = A + 1, AHP = (AH + 3) & ~3;
+  constexpr int W1S = (OBS + 1 + 3) & ~3;
+  __shared__ __attribute__((aligned(16))) float hb[kRRows * kHS];  // h2 rows of one pass
+  __shared__ __attribute__((aligned(16))) float wtab[H * AHP];     // (W3[j][.], w4[j], pad)
+  // weights in the tile's operand order: layer-1 unit k = r + 32 h + 8 js of operand
+  // q = 2 r + h as [q][js][W1[0..OBS) b1 pad] (the 16 lanes of one js read the same row),
+  // the W2 fragments as [nt][q][lane] (B[slot js][col 16 nt + mr])
+  __shared__ __attribute__((aligned(16))) float sw1[16 * 4 * W1S];
+  __shared__ __attribute__((aligned(16))) float sw2[4 * 16 * 64];
+  __shared__ __attribute__((aligned(16))) float sx[3][64];  // per-wave chain rows
+  __shared__ __attribute__((aligned(16))) float sy[3][64];
+  __shared__ __attribute__((aligned(16))) float sz[3][64];
+  __shared__ float s_ep, s_dlast, s_vnext;
+  extern __shared__ __attribute__((aligned(16))) float hist[];  // fused: (rew, val, done, .)
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int env = blockIdx.x;
+  const int T = p.n_steps;
+  const int mr = lane & 15, js = lane >> 4;
+  const bool fused = p.ret_out != nullptr && p.return_kind != XA_RETURNS_NONE;
+  const ParamOffsets o = param_offsets(OBS, A);
+  const float* __restrict__ th = p.theta;
+  XA_STAMP_DECL
+  XA_STAMP(15);
+
+  // ---- prologue: every load the first pass needs is issued before the barrier
+  const int cur0 = p.env_cursor[env];
+  const uint64_t ctr = p.rng_counter ? *p.rng_counter : 0ull;
+  for (int e = threadIdx.x; e < 4 * 16 * 64; e += 64 * kRW) {
+    const int l = e & 63, q = (e >> 6) & 15, nt = e >> 10;
+    const int k = (q >> 1) + 32 * (q & 1) + 8 * (l >> 4);
+    sw2[e] = th[o.w2 + k * H + 16 * nt + (l & 15)];
+  }
+  for (int e = threadIdx.x; e < 16 * 4 * W1S; e += 64 * kRW) {
+    const int i = e % W1S, jq = e / W1S, q = jq >> 2;
+    const int k = (q >> 1) + 32 * (q & 1) + 8 * (jq & 3);
+    sw1[e] = i < OBS ? th[o.w1 + i * H + k] : i == OBS ? th[o.b1 + k] : 0.0f;
+  }
+  if (w == kBootW) {
+    float* wr = wtab + lane * AHP;
+#pragma unroll
+    for (int a = 0; a < AHP; ++a)
+      wr[a] = a < A ? th[o.w3 + lane * A + a] : a == A ? th[o.w4 + lane] : 0.0f;
+  }
+  if (threadIdx.x == 0) p.done_out[(size_t)env * (T + 1)] = p.env_done[env];
+  float b2[4];
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) b2[nt] = th[o.b2 + 16 * nt + mr];
+  float xt[OBS];  // tile waves: this lane's tile row input, a pass ahead
+  if (w < kRTW) {
+    const float* xin = replay_input<OBS>(p, env, cur0, min(16 * w + mr, T - 1), T);
+#pragma unroll
+    for (int i = 0; i < OBS; ++i) xt[i] = xin[i];
+  }
+  ReplayRow<OBS> row;  // chunk-pass waves: this lane's row, a pass ahead
+  if (w < kRRows / 64) row.load(p, env, cur0, 64 * w + lane, T, ctr);
+  __syncthreads();  // weights staged; every read of the env's carried state is done
+  XA_STAMP(8);
+
+  if (w == kBootW) {
+    // bootstrap V(s_T): the step loop's lane-per-unit forward (layer1 / layer2 order), the
+    // value head by chunk_heads on the h2 row
+    const float* st = replay_input<OBS>(p, env, cur0, T, T);
+    float z1 = 0.0f;
+#pragma unroll
+    for (int i = 0; i < OBS; ++i) z1 = fmaf(st[i], th[o.w1 + i * H + lane], z1);
+    sx[0][lane] = xa_tanhf(z1 + th[o.b1 + lane]);
+    wave_sync();
+    const int nt = lane >> 4, ml = lane & 15;
+    float c[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int k = 0; k < H; ++k) {  // W2[k][lane] from the fragment table
+      const int q = 2 * (k & 7) + (k >> 5), l = 16 * ((k >> 3) & 3) + ml;
+      c[k & 7] = fmaf(sx[0][k], sw2[(nt * 16 + q) * 64 + l], c[k & 7]);
+    }
+    sy[0][lane] = xa_tanhf((((c[0] + c[1]) + (c[2] + c[3])) + ((c[4] + c[5]) + (c[6] + c[7]))) +
+                           th[o.b2 + lane]);
+    wave_sync();
+    if (lane == 0) {
+      float z[AH];
+      chunk_heads<A, A>(sy[0], wtab, z);
+      const float vn = z[A] + th[o.b4];
+      p.next_val[env] = vn;
+      s_vnext = vn;
+    }
+  } else if (w == kScanW) {
+    // episode returns in step order (a2c/agent.py:119-126), from the records alone
+    float ep = p.ep_return[env], dl = 0.0f;
+    for (int b0 = 0; b0 < T; b0 += 64) {
+      const int t = b0 + lane;
+      const size_t rb = replay_rec(p, env, cur0, min(t, T - 1));
+      sx[1][lane] = p.rep_rew[rb];
+      sy[1][lane] = t < T ? p.rep_done[rb] : -1.0f;  // -1: past the last step
+      wave_sync();
+      if (lane == 0) {
+#pragma unroll
+        for (int q4 = 0; q4 < 64; q4 += 4) {
+          const float4 r4 = *reinterpret_cast<const float4*>(&sx[1][q4]);
+          const float4 d4 = *reinterpret_cast<const float4*>(&sy[1][q4]);
+          const float rr[4] = {r4.x, r4.y, r4.z, r4.w}, dd[4] = {d4.x, d4.y, d4.z, d4.w};
+          float o4[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const bool in = dd[e] >= 0.0f;
+            const float s = ep + rr[e];
+            o4[e] = s;
+            ep = in ? (dd[e] != 0.0f ? 0.0f : s) : ep;
+            dl = in ? dd[e] : dl;
+          }
+          *reinterpret_cast<float4*>(&sz[1][q4]) = float4{o4[0], o4[1], o4[2], o4[3]};
+        }
+      }
+      wave_sync();
+      if (p.epret_out && t < T) p.epret_out[(size_t)env * T + t] = sz[1][lane];
+      wave_sync();  // the next block rewrites the rows
+    }
+    if (lane == 0) {
+      s_ep = ep;
+      s_dlast = dl;
+    }
+  }
+
+  for (int c0 = 0; c0 < T; c0 += kRRows) {
+    const int nr = min(kRRows, T - c0);
+    if (w < kRTW && 16 * w < nr) {  // tile w of the pass: rows c0 + 16 w + m
+      float h1[16];
+#pragma unroll
+      for (int q = 0; q < 16; q += 2) {
+        float zz[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const float* wr = sw1 + ((q + e) * 4 + js) * W1S;
+          float wv[W1S];
+#pragma unroll
+          for (int i4 = 0; i4 < W1S; i4 += 4) {
+            const float4 t4 = *reinterpret_cast<const float4*>(wr + i4);
+            wv[i4] = t4.x; wv[i4 + 1] = t4.y; wv[i4 + 2] = t4.z; wv[i4 + 3] = t4.w;
+          }
+          float z = 0.0f;
+#pragma unroll
+          for (int i = 0; i < OBS; ++i) z = fmaf(xt[i], wv[i], z);
+          zz[e] = z + wv[OBS];
+        }
+        const xa_f2 h = xa_tanhf2(xa_f2{zz[0], zz[1]});
+        h1[q] = h.x;
+        h1[q + 1] = h.y;
+      }
+      if (c0 + kRRows < T) {  // the next pass's tile row
+        const float* xin =
+            replay_input<OBS>(p, env, cur0, min(c0 + kRRows + 16 * w + mr, T - 1), T);
+#pragma unroll
+        for (int i = 0; i < OBS; ++i) xt[i] = xin[i];
+      }
+#pragma unroll 1
+      for (int nt = 0; nt < 4; ++nt) {
+        float wb[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) wb[q] = sw2[(nt * 16 + q) * 64 + lane];
+        rf32x4 acc[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r)
+          acc[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(h1[2 * r], wb[2 * r],
+                                                        rf32x4{0.0f, 0.0f, 0.0f, 0.0f}, 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 8; ++r)
+          acc[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(h1[2 * r + 1], wb[2 * r + 1], acc[r], 0, 0,
+                                                        0);
+        float bn = 0.0f;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) bn = nt == u ? b2[u] : bn;
+#pragma unroll
+        for (int i = 0; i < 4; i += 2) {
+          float s[2];
+#pragma unroll
+          for (int e = 0; e < 2; ++e)
+            s[e] = (((acc[0][i + e] + acc[1][i + e]) + (acc[2][i + e] + acc[3][i + e])) +
+                    ((acc[4][i + e] + acc[5][i + e]) + (acc[6][i + e] + acc[7][i + e]))) + bn;
+          const xa_f2 h = xa_tanhf2(xa_f2{s[0], s[1]});
+          hb[(16 * w + 4 * js + i) * kHS + 16 * nt + mr] = h.x;
+          hb[(16 * w + 4 * js + i + 1) * kHS + 16 * nt + mr] = h.y;
+        }
+      }
+    }
+    XA_STAMP(9);  // tiles (+ wave 0 has nothing else before the barrier)
+    __syncthreads();  // the pass's h2 rows are in LDS
+    XA_STAMP(10);
+    const int rl = 64 * w + lane, t = c0 + rl;
+    if (w < kRRows / 64 && rl < nr) {
+      float z[AH];
+      chunk_heads<A, 0>(hb + rl * kHS, wtab, z);
+      const size_t it = (size_t)env * T + t;
+      float l[A];
+#pragma unroll
+      for (int a = 0; a < A; ++a) l[a] = z[a] + th[o.b3 + a];
+      const float val = z[A] + th[o.b4];
+      const CatOut<A> cat = categorical<A>(l, row.u, -1);
+#pragma unroll
+      for (int k = 0; k < OBS; ++k) p.obs_out[it * OBS + k] = row.x[k];
+      p.act_out[it] = cat.action;
+      p.logp_out[it] = cat.logp;
+      p.val_out[it] = val;
+      if (p.ent_out) p.ent_out[it] = cat.entropy;
+      p.rew_out[it] = row.r;
+      p.done_out[(size_t)env * (T + 1) + 1 + t] = row.d;
+      if (fused) *reinterpret_cast<float4*>(hist + 4 * t) = float4{row.r, val, row.d, 0.0f};
+      if (c0 + kRRows < T) row.load(p, env, cur0, t + kRRows, T, ctr);
+    }
+    XA_STAMP(11);  // chunk pass
+    __syncthreads();  // the next pass rewrites hb; the last pass's values are in LDS
+    XA_STAMP(12);
+  }
+
+  if (w == 0) {
+    if (fused) {
+      // returns backwards in 64-step blocks: the terms that do not depend on the carry
+      // lane-parallel, the carry chain on lane 0 (xo_gae / xo_nstep order)
+      const bool gae = p.return_kind == XA_RETURNS_GAE;
+      float carry = gae ? 0.0f : s_vnext;
+      for (int b0 = (T - 1) & ~63; b0 >= 0; b0 -= 64) {
+        const int t = b0 + lane, tc = min(t, T - 1);
+        const float4 hv = *reinterpret_cast<const float4*>(hist + 4 * tc);
+        const float nnt = 1.0f - hv.z;
+        if (gae) {
+          const float vn = tc + 1 < T ? hist[4 * (tc + 1) + 1] : s_vnext;
+          sx[2][lane] = (hv.x + (p.gamma * vn) * nnt) - hv.y;  // delta
+          sy[2][lane] = p.gamma_lam * nnt;
+        } else {
+          sx[2][lane] = hv.x;
+          sy[2][lane] = nnt;
+        }
+        wave_sync();
+        if (lane == 0) {
+          const int nb = min(64, T - b0);
+#pragma unroll
+          for (int q4 = 60; q4 >= 0; q4 -= 4) {
+            const float4 a4 = *reinterpret_cast<const float4*>(&sx[2][q4]);
+            const float4 c4 = *reinterpret_cast<const float4*>(&sy[2][q4]);
+            const float aa[4] = {a4.x, a4.y, a4.z, a4.w}, cc[4] = {c4.x, c4.y, c4.z, c4.w};
+            float o4[4];
+#pragma unroll
+            for (int e = 3; e >= 0; --e) {
+              const float nc = gae ? aa[e] + (cc[e] * carry) : aa[e] + (p.gamma * carry) * cc[e];
+              carry = q4 + e < nb ? nc : carry;
+              o4[e] = carry;
+            }
+            *reinterpret_cast<float4*>(&sz[2][q4]) = float4{o4[0], o4[1], o4[2], o4[3]};
+          }
+        }
+        wave_sync();
+        if (t < T) p.ret_out[(size_t)env * T + t] = gae ? sz[2][lane] + hv.y : sz[2][lane];
+        wave_sync();  // the next block rewrites the rows
+      }
+    }
+    if (lane < OBS) {
+      const float* st = replay_input<OBS>(p, env, cur0, T, T);
+      p.env_state[(size_t)env * OBS + lane] = st[lane];
+    }
+    if (lane == 0) {
+      p.env_cursor[env] = (int)(((uint32_t)cur0 + (uint32_t)T) % (uint32_t)p.t_rec);
+      p.ep_return[env] = s_ep;
+      p.env_done[env] = s_dlast;
+    }
+  }
+  XA_STAMP(14);  // state + returns
+}
+
 template <int OBS, int A>
 int launch_rollout(const XaRolloutArgs* p, hipStream_t s) {
   const bool fused = p->ret_out != nullptr && p->return_kind != XA_RETURNS_NONE;
+  static const bool batched = [] {
+    const char* e = getenv("XA_REPLAY_BATCHED");
+    return !(e && e[0] == '0');
+  }();
+  if (p->env_kind == XA_ENV_REPLAY && batched) {
+    const size_t lds = fused ? (size_t)4 * p->n_steps * sizeof(float) : 0;
+    hipLaunchKernelGGL((replay_rollout_kernel<OBS, A>), dim3(p->n_envs), dim3(64 * kRW), lds, s,
+                       *p);
+    XA_CHECK_LAUNCH("xa_mlp_rollout");
+    return 0;
+  }
   const size_t lds = (size_t)kRollWaves * H * sizeof(float) +
                      (fused ? (size_t)kRollWaves * 3 * p->n_steps * sizeof(float) : 0);
   dim3 grid((p->n_envs + kRollWaves - 1) / kRollWaves);
