@@ -657,12 +657,14 @@ def bench_ppo(args, world, rank, device, n_envs):
     roll_bytes = ROLLOUT_BYTES_PER_ENV_STEP * B
     roll_gbs = roll_bytes / (roll_ms * 1e-3) / 1e9
     out['rollout_roofline'] = {
-        'kernel': 'xa_mlp_rollout (mlp_rollout_kernel<4,2,replay>)', 'bound': 'hbm',
+        'kernel': 'xa_mlp_rollout (replay_rollout_kernel<4,2>)', 'bound': 'hbm',
         'achieved': round(roll_gbs, 3), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
         'frac': round(roll_gbs / HBM_PEAK_GBS, 6),
         'traffic': load_traffic(f'rollout_n{n_envs}'), 'launch_ms': round(roll_ms, 5),
-        'note': f'latency-bound: {T} dependent policy steps per env (one wave64 per env); '
-                f'{ROLLOUT_BYTES_PER_ENV_STEP} algorithmic B/env-step x {B} env-steps per launch'}
+        'note': f'latency-bound: one 8-wave workgroup per env runs its {T} policy forwards '
+                f'(+ the bootstrap row) as 16-row MFMA tiles, then the step-order '
+                f'episode-return and return chains; {ROLLOUT_BYTES_PER_ENV_STEP} algorithmic '
+                f'B/env-step x {B} env-steps per launch'}
     if agent.update_mode == 'persistent':
         upd_ms = float(np.mean(ktimes['ppo_update']))
         flops = flops_sample * B * agent.ppo_epochs  # every sample once per epoch

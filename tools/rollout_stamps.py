@@ -44,6 +44,13 @@ def main():
         for s, name in names.items():
             print(f'  slot {s:2d} {name:18s} {st[s]:10.0f}')
         print(f'  total {st[8:15].sum():10.0f}')
+        print('  per-wave arrival at the first tile barrier (cycles from the wave start): ' +
+              ' '.join(f'w{w}={st[32 + w]:.0f}' for w in range(8)))
+        print('  bootstrap wave: start / end ' + ' '.join(f'{st[k]:.0f}' for k in (54, 55)))
+        print('  return wave: start / LDS rows / chain / sync / stores / sync ' +
+              ' '.join(f'{st[k]:.0f}' for k in range(48, 54)))
+        print('  returns wave: start / deltas / chain / stores ' +
+              ' '.join(f'{st[k]:.0f}' for k in range(56, 60)))
 
 
 if __name__ == '__main__':

@@ -4,7 +4,10 @@
 // (xagents/base.py:388-426) and the return computation (ppo/agent.py:48-94,
 // a2c/agent.py:141-171).
 //
-// Schedule: ONE wave64 per env, lane j = hidden unit j. Each lane keeps the
+// Two schedules. The replay env (records that ignore the actions) runs every step's
+// forward as an independent row of one batched forward (replay_rollout_kernel, below).
+// The CartPole-dynamics env, whose next input depends on the sampled action, runs the
+// step loop: ONE wave64 per env, lane j = hidden unit j. Each lane keeps the
 // weights it needs for the whole rollout in VGPRs (column j of W1 and W2, row j of
 // the heads: ~75 registers), so the T-step loop touches HBM only for the replay
 // stream and the rollout stores. Per step:
@@ -140,14 +143,14 @@ struct LaneMlp {
 // rounded and summed as pairs, quads, octets, 16-unit rows, then (S2 + S3) + (S0 + S1) --
 // the tree xa_wave_sum's butterfly builds in lane 63, so every head equals its in-step
 // value bit for bit. wt: the wave's [H][AHP] table of (W3[j][0 .. A), w4[j], pad).
-template <int A, int HF>
+template <int A, int HF, int UNROLL = 1>
 XA_DEV void chunk_heads(const float* __restrict__ hrow, const float* __restrict__ wt,
                         float (&z)[A + 1]) {
   constexpr int AH = A + 1, AHP = (AH + 3) & ~3;
   float s_prev[AH], p01[AH];
-  // one 16-unit row per iteration, not unrolled: the row's 16 h2 values and table rows are
-  // all that is live on top of the step loop's state
-#pragma unroll 1
+  // one 16-unit row per iteration, not unrolled in the step loop (the row's 16 h2 values and
+  // table rows are all that is live on top of its state); UNROLL 4 where registers allow
+#pragma unroll UNROLL
   for (int r = 0; r < 4; ++r) {
     float O[AH][2];
 #pragma unroll
@@ -594,12 +597,42 @@ __global__ __launch_bounds__(256) void mlp_forward_kernel(const float* __restric
 // (records only); the fused returns follow the last pass. The two step-order chains run on
 // one lane from LDS with the per-step terms precomputed lane-parallel (same operations,
 // same order as xo_gae / xo_nstep and the step loop).
-constexpr int kRTW = 8;               // tile waves: 16-row tiles per pass
-constexpr int kRW = kRTW + 2;         // + the bootstrap wave and the episode-return wave
-constexpr int kRRows = 16 * kRTW;     // rows per pass (T = 128: one pass)
-constexpr int kBootW = kRTW, kScanW = kRTW + 1;
+constexpr int kRW = 8;                // waves per env: 16-row tiles per pass
+constexpr int kRRows = 16 * kRW;      // rows per pass (T = 128: one pass)
+// the chunk pass takes waves 0 and 1; in the last pass waves 2 and 3 run the bootstrap
+// forward and the episode-return chain after their tiles, before the tile barrier
+constexpr int kBootW = 2, kScanW = 3;
+// the fused returns after the last pass: a wave with no global stores of its own in flight
+// (a loop head waits for every outstanding vector-memory op of its wave)
+constexpr int kRetW = 4;
 
 typedef float rf32x4 __attribute__((ext_vector_type(4)));
+#define XA_STR_(x) #x
+#define XA_UNROLL(n) _Pragma(XA_STR_(unroll n))
+#ifndef XA_RNT_UNROLL
+#define XA_RNT_UNROLL 1  // output-column tiles of W2 in flight per tile wave
+#endif
+#ifndef XA_RHEADS_UNROLL
+#define XA_RHEADS_UNROLL 4
+#endif
+
+#ifdef XA_STAMPS
+// (diagnostic) lane 0 of block 0's wave: cycles since the wave start into slot
+#define XA_WSTAMP(slot)                                                              \
+  do {                                                                               \
+    if (blockIdx.x == 0 && lane == 0) {                                              \
+      unsigned long long t_;                                                         \
+      __builtin_amdgcn_sched_barrier(0);                                             \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");     \
+      __builtin_amdgcn_sched_barrier(0);                                             \
+      xa_stamp_acc[slot] += t_ - xa_w0_;                                             \
+    }                                                                                \
+  } while (0)
+#else
+#define XA_WSTAMP(slot) \
+  do {                  \
+  } while (0)
+#endif
 
 // xa_tanhf on two values with packed f32 ops: every lane of every op rounds exactly as the
 // scalar sequence does
@@ -661,6 +694,73 @@ struct ReplayRow {
   }
 };
 
+// The step-order chains: lane q holds step b0 + q of a 64-step block; lane 0 walks the
+// block with v_readlane (constant lane indices on a whole block), so a step is two dependent
+// VALU ops on lane 0's register and the per-step operands come from SGPRs; the results go
+// to LDS row o (o[q] = the value after step q), read back lane-parallel.
+// episode returns (a2c/agent.py:119-126): ep += r_q, o_q = ep, ep = +0 after a done (km_q =
+// d_q != 0 ? 0 : ~0, so the reset is one AND)
+XA_DEV void epret_block(float r, int km, int n, float* __restrict__ o, float& ep) {
+  if (n == 64) {
+#pragma unroll
+    for (int q0 = 0; q0 < 64; q0 += 8) {
+      float r8[8];
+      int k8[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {  // 8 steps' operands read ahead of their chain
+        r8[e] = xa_readlane(r, q0 + e);
+        k8[e] = __builtin_amdgcn_readlane(km, q0 + e);
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float sm = ep + r8[e];
+        o[q0 + e] = sm;
+        ep = __int_as_float(__float_as_int(sm) & k8[e]);
+      }
+    }
+  } else {
+    for (int q = 0; q < n; ++q) {
+      const float sm = ep + xa_readlane(r, q);
+      o[q] = sm;
+      ep = __int_as_float(__float_as_int(sm) & __builtin_amdgcn_readlane(km, q));
+    }
+  }
+}
+
+// returns backwards over a block (xo_gae / xo_nstep): GAE carry = a_q + c_q carry with
+// a = delta, c = gamma lambda (1 - d); n-step carry = a_q + (gamma carry) c_q with a = r,
+// c = 1 - d. o[q] = the carry after step q.
+template <bool GAE>
+XA_DEV float returns_op(float aq, float cq, float gamma, float carry) {
+  return GAE ? aq + (cq * carry) : aq + (gamma * carry) * cq;
+}
+
+template <bool GAE>
+XA_DEV void returns_block(float a, float c, int n, float gamma, float* __restrict__ o,
+                          float& carry) {
+  if (n == 64) {
+#pragma unroll
+    for (int q0 = 63; q0 >= 0; q0 -= 8) {
+      float a8[8], c8[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {  // 8 steps' operands read ahead of their chain
+        a8[e] = xa_readlane(a, q0 - e);
+        c8[e] = xa_readlane(c, q0 - e);
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        carry = returns_op<GAE>(a8[e], c8[e], gamma, carry);
+        o[q0 - e] = carry;
+      }
+    }
+  } else {
+    for (int q = n - 1; q >= 0; --q) {
+      carry = returns_op<GAE>(xa_readlane(a, q), xa_readlane(c, q), gamma, carry);
+      o[q] = carry;
+    }
+  }
+}
+
 template <int OBS, int A>
 __global__ __launch_bounds__(64 * kRW) void replay_rollout_kernel(XaRolloutArgs p) {
   constexpr int AH = A + 1, AHP = (AH + 3) & ~3;
@@ -672,10 +772,9 @@ __global__ __launch_bounds__(64 * kRW) void replay_rollout_kernel(XaRolloutArgs 
   // the W2 fragments as [nt][q][lane] (B[slot js][col 16 nt + mr])
   __shared__ __attribute__((aligned(16))) float sw1[16 * 4 * W1S];
   __shared__ __attribute__((aligned(16))) float sw2[4 * 16 * 64];
-  __shared__ __attribute__((aligned(16))) float sx[3][64];  // per-wave chain rows
-  __shared__ __attribute__((aligned(16))) float sy[3][64];
-  __shared__ __attribute__((aligned(16))) float sz[3][64];
-  __shared__ float s_ep, s_dlast, s_vnext;
+  __shared__ __attribute__((aligned(16))) float sx[64], sy[64];  // bootstrap h1 / h2 rows
+  __shared__ __attribute__((aligned(16))) float sep[64], sret[64];  // chain result rows
+  __shared__ float s_vnext;
   extern __shared__ __attribute__((aligned(16))) float hist[];  // fused: (rew, val, done, .)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int env = blockIdx.x;
@@ -686,6 +785,11 @@ __global__ __launch_bounds__(64 * kRW) void replay_rollout_kernel(XaRolloutArgs 
   const float* __restrict__ th = p.theta;
   XA_STAMP_DECL
   XA_STAMP(15);
+#ifdef XA_STAMPS
+  // (diagnostic) every wave's arrival at the first tile barrier, from its own start
+  unsigned long long xa_w0_;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(xa_w0_)::"memory");
+#endif
 
   // ---- prologue: every load the first pass needs is issued before the barrier
   const int cur0 = p.env_cursor[env];
@@ -710,83 +814,86 @@ __global__ __launch_bounds__(64 * kRW) void replay_rollout_kernel(XaRolloutArgs 
   float b2[4];
 #pragma unroll
   for (int nt = 0; nt < 4; ++nt) b2[nt] = th[o.b2 + 16 * nt + mr];
-  float xt[OBS];  // tile waves: this lane's tile row input, a pass ahead
-  if (w < kRTW) {
+  float xt[OBS];  // this lane's tile row input, a pass ahead
+  {
     const float* xin = replay_input<OBS>(p, env, cur0, min(16 * w + mr, T - 1), T);
 #pragma unroll
     for (int i = 0; i < OBS; ++i) xt[i] = xin[i];
   }
   ReplayRow<OBS> row;  // chunk-pass waves: this lane's row, a pass ahead
   if (w < kRRows / 64) row.load(p, env, cur0, 64 * w + lane, T, ctr);
+  // bootstrap wave: s_T and this unit's layer-1 / layer-2 constants; return wave: the
+  // records of the first 128 steps and the carried return
+  float bx[OBS], bw1[OBS], bb1 = 0.0f, bb2 = 0.0f;
+  float sr[2] = {0.0f, 0.0f}, sd[2] = {-1.0f, -1.0f}, ep0 = 0.0f;
+  if (w == kBootW) {
+    const float* st = replay_input<OBS>(p, env, cur0, T, T);
+#pragma unroll
+    for (int i = 0; i < OBS; ++i) {
+      bx[i] = st[i];
+      bw1[i] = th[o.w1 + i * H + lane];
+    }
+    bb1 = th[o.b1 + lane];
+    bb2 = th[o.b2 + lane];
+  } else if (w == kScanW) {
+    ep0 = p.ep_return[env];
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int t = 64 * b + lane;
+      const size_t rb = replay_rec(p, env, cur0, min(t, T - 1));
+      sr[b] = p.rep_rew[rb];
+      sd[b] = t < T ? p.rep_done[rb] : -1.0f;  // -1: past the last step
+    }
+  }
   __syncthreads();  // weights staged; every read of the env's carried state is done
   XA_STAMP(8);
 
-  if (w == kBootW) {
-    // bootstrap V(s_T): the step loop's lane-per-unit forward (layer1 / layer2 order), the
-    // value head by chunk_heads on the h2 row
-    const float* st = replay_input<OBS>(p, env, cur0, T, T);
-    float z1 = 0.0f;
+  if (w == kBootW) {  // the env's carried state: every read of it is behind the barrier
 #pragma unroll
-    for (int i = 0; i < OBS; ++i) z1 = fmaf(st[i], th[o.w1 + i * H + lane], z1);
-    sx[0][lane] = xa_tanhf(z1 + th[o.b1 + lane]);
-    wave_sync();
-    const int nt = lane >> 4, ml = lane & 15;
-    float c[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-    for (int k = 0; k < H; ++k) {  // W2[k][lane] from the fragment table
-      const int q = 2 * (k & 7) + (k >> 5), l = 16 * ((k >> 3) & 3) + ml;
-      c[k & 7] = fmaf(sx[0][k], sw2[(nt * 16 + q) * 64 + l], c[k & 7]);
-    }
-    sy[0][lane] = xa_tanhf((((c[0] + c[1]) + (c[2] + c[3])) + ((c[4] + c[5]) + (c[6] + c[7]))) +
-                           th[o.b2 + lane]);
-    wave_sync();
-    if (lane == 0) {
-      float z[AH];
-      chunk_heads<A, A>(sy[0], wtab, z);
-      const float vn = z[A] + th[o.b4];
-      p.next_val[env] = vn;
-      s_vnext = vn;
-    }
-  } else if (w == kScanW) {
-    // episode returns in step order (a2c/agent.py:119-126), from the records alone
-    float ep = p.ep_return[env], dl = 0.0f;
-    for (int b0 = 0; b0 < T; b0 += 64) {
-      const int t = b0 + lane;
-      const size_t rb = replay_rec(p, env, cur0, min(t, T - 1));
-      sx[1][lane] = p.rep_rew[rb];
-      sy[1][lane] = t < T ? p.rep_done[rb] : -1.0f;  // -1: past the last step
-      wave_sync();
-      if (lane == 0) {
-#pragma unroll
-        for (int q4 = 0; q4 < 64; q4 += 4) {
-          const float4 r4 = *reinterpret_cast<const float4*>(&sx[1][q4]);
-          const float4 d4 = *reinterpret_cast<const float4*>(&sy[1][q4]);
-          const float rr[4] = {r4.x, r4.y, r4.z, r4.w}, dd[4] = {d4.x, d4.y, d4.z, d4.w};
-          float o4[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const bool in = dd[e] >= 0.0f;
-            const float s = ep + rr[e];
-            o4[e] = s;
-            ep = in ? (dd[e] != 0.0f ? 0.0f : s) : ep;
-            dl = in ? dd[e] : dl;
-          }
-          *reinterpret_cast<float4*>(&sz[1][q4]) = float4{o4[0], o4[1], o4[2], o4[3]};
-        }
-      }
-      wave_sync();
-      if (p.epret_out && t < T) p.epret_out[(size_t)env * T + t] = sz[1][lane];
-      wave_sync();  // the next block rewrites the rows
-    }
-    if (lane == 0) {
-      s_ep = ep;
-      s_dlast = dl;
-    }
+    for (int i = 0; i < OBS; ++i)
+      if (lane == i) p.env_state[(size_t)env * OBS + i] = bx[i];
+    if (lane == 0) p.env_cursor[env] = (int)(((uint32_t)cur0 + (uint32_t)T) % (uint32_t)p.t_rec);
   }
+
+  // episode returns in step order (a2c/agent.py:119-126), from the records alone, one 64-step
+  // block at a time with the next block's records in flight; the return wave runs the first
+  // half of the blocks after its last tile (beside the other waves' tiles) and the rest
+  // beside the last chunk pass
+  float sc_ep = ep0, sc_dl = 0.0f;
+  int sc_b0 = 0;
+  auto scan_blocks = [&](int until_block) {
+    for (; sc_b0 < T && sc_b0 < 64 * until_block; sc_b0 += 64) {
+      const int b0 = sc_b0;
+      const float r = sr[0], d = sd[0];
+      sr[0] = sr[1];
+      sd[0] = sd[1];
+      if (b0 + 128 < T) {
+        const int t = b0 + 128 + lane;
+        const size_t rb = replay_rec(p, env, cur0, min(t, T - 1));
+        sr[1] = p.rep_rew[rb];
+        sd[1] = t < T ? p.rep_done[rb] : -1.0f;
+      }
+      const int nv = min(64, T - b0);
+      sc_dl = xa_readlane(d, nv - 1);
+      // every lane's operands: the asm pins them here, in all lanes (the compiler would
+      // otherwise sink them into the lane-0 branch, and the readlanes read other lanes)
+      int km = d != 0.0f ? 0 : -1;
+      float rv = r;
+      asm volatile("" : "+v"(km), "+v"(rv));
+      if (lane == 0) epret_block(rv, km, nv, sep, sc_ep);
+      wave_sync();
+      if (p.epret_out && b0 + lane < T) p.epret_out[(size_t)env * T + b0 + lane] = sep[lane];
+      wave_sync();  // the next block rewrites the row
+    }
+    if (sc_b0 >= T && lane == 0) {
+      p.ep_return[env] = sc_ep;
+      p.env_done[env] = sc_dl;
+    }
+  };
 
   for (int c0 = 0; c0 < T; c0 += kRRows) {
     const int nr = min(kRRows, T - c0);
-    if (w < kRTW && 16 * w < nr) {  // tile w of the pass: rows c0 + 16 w + m
+    if (16 * w < nr) {  // tile w of the pass: rows c0 + 16 w + m
       float h1[16];
 #pragma unroll
       for (int q = 0; q < 16; q += 2) {
@@ -815,7 +922,7 @@ __global__ __launch_bounds__(64 * kRW) void replay_rollout_kernel(XaRolloutArgs 
 #pragma unroll
         for (int i = 0; i < OBS; ++i) xt[i] = xin[i];
       }
-#pragma unroll 1
+      XA_UNROLL(XA_RNT_UNROLL)
       for (int nt = 0; nt < 4; ++nt) {
         float wb[16];
 #pragma unroll
@@ -845,13 +952,56 @@ __global__ __launch_bounds__(64 * kRW) void replay_rollout_kernel(XaRolloutArgs 
         }
       }
     }
+    // last pass: waves 2 and 3 (done with their tiles, while the second wave of each SIMD
+    // still runs its) compute the bootstrap value and the episode returns
+    if (c0 + kRRows >= T) {
+      if (w == kBootW) {
+        XA_WSTAMP(54);
+        // bootstrap V(s_T): the step loop's lane-per-unit forward (layer1 / layer2 order), the
+        // value head by chunk_heads on the h2 row
+        float z1 = 0.0f;
+#pragma unroll
+        for (int i = 0; i < OBS; ++i) z1 = fmaf(bx[i], bw1[i], z1);
+        sx[lane] = xa_tanhf(z1 + bb1);
+        wave_sync();
+        const int nt = lane >> 4, ml = lane & 15;
+        float c[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int k = 0; k < H; ++k) {  // W2[k][lane] from the fragment table
+          const int q = 2 * (k & 7) + (k >> 5), l = 16 * ((k >> 3) & 3) + ml;
+          c[k & 7] = fmaf(sx[k], sw2[(nt * 16 + q) * 64 + l], c[k & 7]);
+        }
+        sy[lane] = xa_tanhf((((c[0] + c[1]) + (c[2] + c[3])) + ((c[4] + c[5]) + (c[6] + c[7]))) +
+                               bb2);
+        wave_sync();
+        if (lane == 0) {
+          float z[AH];
+          chunk_heads<A, A, 2>(sy, wtab, z);
+          const float vn = z[A] + th[o.b4];
+          p.next_val[env] = vn;
+          s_vnext = vn;
+        }
+        XA_WSTAMP(55);
+      } else if (w == kScanW) {
+        scan_blocks(((T + 63) / 64 + 1) / 2);  // the first half of the 64-step blocks
+      }
+    }
     XA_STAMP(9);  // tiles (+ wave 0 has nothing else before the barrier)
+#ifdef XA_STAMPS
+    if (c0 == 0 && blockIdx.x == 0 && lane == 0) {
+      unsigned long long t_;
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");
+      __builtin_amdgcn_sched_barrier(0);
+      xa_stamp_acc[32 + w] += t_ - xa_w0_;
+    }
+#endif
     __syncthreads();  // the pass's h2 rows are in LDS
     XA_STAMP(10);
     const int rl = 64 * w + lane, t = c0 + rl;
     if (w < kRRows / 64 && rl < nr) {
       float z[AH];
-      chunk_heads<A, 0>(hb + rl * kHS, wtab, z);
+      chunk_heads<A, 0, XA_RHEADS_UNROLL>(hb + rl * kHS, wtab, z);
       const size_t it = (size_t)env * T + t;
       float l[A];
 #pragma unroll
@@ -868,61 +1018,43 @@ __global__ __launch_bounds__(64 * kRW) void replay_rollout_kernel(XaRolloutArgs 
       p.done_out[(size_t)env * (T + 1) + 1 + t] = row.d;
       if (fused) *reinterpret_cast<float4*>(hist + 4 * t) = float4{row.r, val, row.d, 0.0f};
       if (c0 + kRRows < T) row.load(p, env, cur0, t + kRRows, T, ctr);
+    } else if (w == kScanW && c0 + kRRows >= T) {
+      scan_blocks((T + 63) / 64);  // the rest of the blocks
     }
     XA_STAMP(11);  // chunk pass
     __syncthreads();  // the next pass rewrites hb; the last pass's values are in LDS
     XA_STAMP(12);
   }
 
-  if (w == 0) {
+  if (w == kRetW) {
+    XA_WSTAMP(56);
     if (fused) {
-      // returns backwards in 64-step blocks: the terms that do not depend on the carry
-      // lane-parallel, the carry chain on lane 0 (xo_gae / xo_nstep order)
+      // returns (xo_gae / xo_nstep order), backwards one 64-step block at a time: the terms
+      // that do not depend on the carry lane-parallel, the carry chain on lane 0
       const bool gae = p.return_kind == XA_RETURNS_GAE;
       float carry = gae ? 0.0f : s_vnext;
+      XA_WSTAMP(57);
       for (int b0 = (T - 1) & ~63; b0 >= 0; b0 -= 64) {
-        const int t = b0 + lane, tc = min(t, T - 1);
+        const int t = b0 + lane, tc = min(t, T - 1), nb = min(64, T - b0);
         const float4 hv = *reinterpret_cast<const float4*>(hist + 4 * tc);
         const float nnt = 1.0f - hv.z;
         if (gae) {
           const float vn = tc + 1 < T ? hist[4 * (tc + 1) + 1] : s_vnext;
-          sx[2][lane] = (hv.x + (p.gamma * vn) * nnt) - hv.y;  // delta
-          sy[2][lane] = p.gamma_lam * nnt;
+          float delta = (hv.x + (p.gamma * vn) * nnt) - hv.y;
+          float coef = p.gamma_lam * nnt;
+          asm volatile("" : "+v"(delta), "+v"(coef));  // in all lanes (see the episode returns)
+          if (lane == 0) returns_block<true>(delta, coef, nb, p.gamma, sret, carry);
         } else {
-          sx[2][lane] = hv.x;
-          sy[2][lane] = nnt;
+          float rr = hv.x, nn = nnt;
+          asm volatile("" : "+v"(rr), "+v"(nn));
+          if (lane == 0) returns_block<false>(rr, nn, nb, p.gamma, sret, carry);
         }
         wave_sync();
-        if (lane == 0) {
-          const int nb = min(64, T - b0);
-#pragma unroll
-          for (int q4 = 60; q4 >= 0; q4 -= 4) {
-            const float4 a4 = *reinterpret_cast<const float4*>(&sx[2][q4]);
-            const float4 c4 = *reinterpret_cast<const float4*>(&sy[2][q4]);
-            const float aa[4] = {a4.x, a4.y, a4.z, a4.w}, cc[4] = {c4.x, c4.y, c4.z, c4.w};
-            float o4[4];
-#pragma unroll
-            for (int e = 3; e >= 0; --e) {
-              const float nc = gae ? aa[e] + (cc[e] * carry) : aa[e] + (p.gamma * carry) * cc[e];
-              carry = q4 + e < nb ? nc : carry;
-              o4[e] = carry;
-            }
-            *reinterpret_cast<float4*>(&sz[2][q4]) = float4{o4[0], o4[1], o4[2], o4[3]};
-          }
-        }
-        wave_sync();
-        if (t < T) p.ret_out[(size_t)env * T + t] = gae ? sz[2][lane] + hv.y : sz[2][lane];
-        wave_sync();  // the next block rewrites the rows
+        if (t < T) p.ret_out[(size_t)env * T + t] = gae ? sret[lane] + hv.y : sret[lane];
+        wave_sync();  // the next block rewrites the row
       }
-    }
-    if (lane < OBS) {
-      const float* st = replay_input<OBS>(p, env, cur0, T, T);
-      p.env_state[(size_t)env * OBS + lane] = st[lane];
-    }
-    if (lane == 0) {
-      p.env_cursor[env] = (int)(((uint32_t)cur0 + (uint32_t)T) % (uint32_t)p.t_rec);
-      p.ep_return[env] = s_ep;
-      p.env_done[env] = s_dlast;
+      XA_WSTAMP(58);
+      XA_WSTAMP(59);
     }
   }
   XA_STAMP(14);  // state + returns
