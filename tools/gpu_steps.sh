@@ -18,7 +18,7 @@
 #   pollab   persistent-update poll sleep variants: bench + C2 FETCH_SIZE
 #   c2g      C2 bench lines at update grids $C2_GS (XA_PPO_MAX_BLOCKS)
 #   profc3   rocprofv3 kernel trace of the C3 bench + per-(kernel, grid) summary
-#   rollab   replay rollout tests + bench A/B, batched MFMA rollout on / off (XA_REPLAY_BATCHED)
+#   rollab   replay rollout tests, stamps (build libxa_rstamp.so first) and two bench lines
 #   rstamps  per-phase stamps of the batched replay rollout (tools/rollout_stamps.py; build
 #            tools/diag_lib/libxa_rstamp.so first: tools/build_variant.py rstamp -DXA_STAMPS --src mlp_rollout)
 #   layers   tests/test_gpu_layers.py (GEMM paths, layer executor)
@@ -88,14 +88,13 @@ for step in "$@"; do
       XA_PPO_FIXED_SHAPE=0 run fix_off2 200 $B
       python tools/bench_brief.py gpurun_out/${T}_fix_*.out ;;
     rollab)
-      # the batched replay rollout (all T + 1 forwards as MFMA row tiles) vs the step loop
+      # replay rollout tests, per-phase stamps, two bench lines (the step-loop replay path it
+      # replaced was A/B'd in r05ra-r05rr, profiles/r05r*_replay_rollout_ab.txt)
       run_pytest roll 200 tests/test_gpu_kernels.py -k rollout
       XA_LIB=tools/diag_lib/libxa_rstamp.so run rstamps 200 python tools/rollout_stamps.py 16 256
       B="python bench.py --steps 40 --warmup 5 --cpu-baseline-seconds 0 --no-secondary"
       run roll_on1 200 $B
-      XA_REPLAY_BATCHED=0 run roll_off1 200 $B
       run roll_on2 200 $B
-      XA_REPLAY_BATCHED=0 run roll_off2 200 $B
       python tools/bench_brief.py gpurun_out/${T}_roll_*.out ;;
     layers) run_pytest layers 300 tests/test_gpu_layers.py ;;
     streamab)

@@ -7,22 +7,19 @@
 // Two schedules. The replay env (records that ignore the actions) runs every step's
 // forward as an independent row of one batched forward (replay_rollout_kernel, below).
 // The CartPole-dynamics env, whose next input depends on the sampled action, runs the
-// step loop: ONE wave64 per env, lane j = hidden unit j. Each lane keeps the
-// weights it needs for the whole rollout in VGPRs (column j of W1 and W2, row j of
-// the heads: ~75 registers), so the T-step loop touches HBM only for the replay
-// stream and the rollout stores. Per step:
+// step loop (mlp_rollout_kernel): ONE wave64 per env, lane j = hidden unit j. Each lane
+// keeps the weights it needs for the whole rollout in VGPRs (column j of W1 and W2, row j
+// of the heads: ~75 registers). Per step:
 //   h1_j = tanh(sum_k x_k W1[k][j] + b1_j)              (fma chain over k)
 //   h1 -> LDS (wave-private row), 16 x ds_read_b128 broadcast back
 //   h2_j = tanh(sum of 8 interleaved 8-long fma chains + b2_j)
 //   h2 -> the wave's LDS row of this step (a [64 steps][64 units] chunk buffer)
-//   cartpole only: logit_a = butterfly_sum_j(h2_j * W3[j][a]) + b3_a (the sample needs them)
-//   env step (replay: records of 64 steps fetched a chunk ahead, one lane per step,
-//   read back with readlane; cartpole: inverse-CDF sample, then f64 dynamics)
-// and once per 64-step chunk, lane j on step t0 + j: the heads the step loop did not need
-// (the value; the logits too for the replay env, whose record stream ignores the action)
-// from the step's h2 row, summed in the pairwise order of the wave butterfly (bitwise the
-// same sums as in-step); softmax, log-prob, entropy and (replay env) the sample.
-// Envs are independent, so no inter-wave synchronisation exists anywhere.
+//   logit_a = butterfly_sum_j(h2_j * W3[j][a]) + b3_a (the sample needs them)
+//   inverse-CDF sample, then the f64 CartPole dynamics
+// and once per 64-step chunk, lane j on step t0 + j: the value head from the step's h2
+// row, summed in the pairwise order of the wave butterfly (bitwise the same sums as
+// in-step); softmax, log-prob and entropy. Envs are independent, so no inter-wave
+// synchronisation exists anywhere.
 // The arithmetic order above is restated exactly by oracle/xa_oracle.c.
 #include "../../include/xagents_hip.h"
 #include "xa_common.hpp"
@@ -279,19 +276,14 @@ XA_DEV bool cartpole_step(double (&s)[4], int action) {
   return s[0] < -2.4 || s[0] > 2.4 || s[2] < -theta_thr || s[2] > theta_thr;
 }
 
-// The per-step inputs of 64 consecutive steps, lane j holding step t0 + j: the
-// sampling uniform and, for the replay env, the record (the record stream does not
-// depend on the actions, so a whole chunk is fetched a chunk ahead and read back per
-// step with readlane -- no memory access on the step's critical path).
-template <int OBS>
+// The sampling uniforms of 64 consecutive steps, lane j holding step t0 + j, fetched a
+// chunk ahead and read back per step with readlane (no memory access on the step chain).
 struct StepChunk {
   float u_given, u_philox;  // picked per step: a select here would wait on the load
-  float obs[OBS], st[OBS], r, d;
 };
 
-template <int OBS, bool REPLAY>
 XA_DEV void load_chunk(const XaRolloutArgs& p, int env, int lane, int cur0, int t0, uint64_t ctr,
-                       StepChunk<OBS>& c) {
+                       StepChunk& c) {
   const int T = p.n_steps;
   const int tj = t0 + lane;
   // loads are unconditional (indices clamped) so every path issues the same number
@@ -301,27 +293,18 @@ XA_DEV void load_chunk(const XaRolloutArgs& p, int env, int lane, int cur0, int 
   const xa_u4 r = xa_philox((uint32_t)env, (uint32_t)tj, (uint32_t)ctr, (uint32_t)(ctr >> 32),
                             (uint32_t)p.seed, (uint32_t)(p.seed >> 32));
   c.u_philox = xa_u01(r.x);
-  if constexpr (REPLAY) {
-    const size_t base = (size_t)env * p.t_rec + (size_t)(((long long)cur0 + tj) % p.t_rec);
-#pragma unroll
-    for (int k = 0; k < OBS; ++k) {
-      c.obs[k] = p.rep_obs[base * OBS + k];
-      c.st[k] = p.rep_state[base * OBS + k];
-    }
-    c.r = p.rep_rew[base];
-    c.d = p.rep_done[base];
-  }
 }
 
 XA_DEV float xa_readlane(float v, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
 
-template <int OBS, int A, bool REPLAY>
+// the CartPole-dynamics env (the next input depends on the sampled action)
+template <int OBS, int A>
 __global__ __launch_bounds__(64 * kRollWaves) void mlp_rollout_kernel(XaRolloutArgs p) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int AH = A + 1, AHP = (AH + 3) & ~3;
-  constexpr int HF = REPLAY ? 0 : A;  // first head of the chunk pass
+  constexpr int HF = A;  // first head of the chunk pass: the value
   __shared__ __attribute__((aligned(16))) float hbuf[kRollWaves][kChunk * kHS];
   __shared__ __attribute__((aligned(16))) float wtab[kRollWaves][H * AHP];
   const int lane = threadIdx.x & 63;
@@ -350,11 +333,9 @@ __global__ __launch_bounds__(64 * kRollWaves) void mlp_rollout_kernel(XaRolloutA
   float st[OBS]; // post-reset env state
 #pragma unroll
   for (int k = 0; k < OBS; ++k) st[k] = x[k] = p.env_state[(size_t)env * OBS + k];
-  double cp[4] = {0.0, 0.0, 0.0, 0.0};
-  if constexpr (!REPLAY) {
+  double cp[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) cp[k] = p.env_state64[(size_t)env * 4 + k];
-  }
+  for (int k = 0; k < 4; ++k) cp[k] = p.env_state64[(size_t)env * 4 + k];
   const int cur0 = p.env_cursor[env];
   int cur = cur0;
   float ep_ret = p.ep_return[env];
@@ -363,19 +344,15 @@ __global__ __launch_bounds__(64 * kRollWaves) void mlp_rollout_kernel(XaRolloutA
 
   // per-step scalars park in lane (t & 63) and leave as one coalesced store per
   // output after each 64-step chunk (no stores inside the step loop). What the next
-  // step does not read -- log-prob and entropy always, the sample too for the replay
-  // env, whose record stream ignores the action -- is computed once per chunk with
-  // lane j on step t0 + j (the same operations as in-step, so bit for bit the same).
-  float b_obs[OBS] = {};  // CartPole only: replay inputs are the shifted record obs
-  int b_act = 0;          // CartPole only: the replay action is drawn in the chunk pass
+  // step does not read -- the value, log-prob and entropy -- is computed once per chunk
+  // with lane j on step t0 + j (the same operations as in-step, so bit for bit the same).
+  float b_obs[OBS] = {};
+  int b_act = 0;
   float b_l[A] = {};
   float b_val = 0.0f, b_rew = 0.0f, b_done = 0.0f, b_epret = 0.0f;
 
-  auto run_chunk = [&](const StepChunk<OBS>& c, int t0) {
+  auto run_chunk = [&](const StepChunk& c, int t0) {
     const int n = min(64, T - t0);
-    float x0[OBS];  // the chunk's first policy input
-#pragma unroll
-    for (int k = 0; k < OBS; ++k) x0[k] = x[k];
     for (int j = 0; j < n; ++j) {
       XA_STAMP(0);
       float logits[A];
@@ -385,21 +362,14 @@ __global__ __launch_bounds__(64 * kRollWaves) void mlp_rollout_kernel(XaRolloutA
         XA_STAMP(1);
         const float h2 = net.layer2(hv);
         XA_STAMP(2);
-        hb[j * kHS + lane] = h2;  // the chunk pass's heads
-        if constexpr (!REPLAY) {
+        hb[j * kHS + lane] = h2;  // the chunk pass's value head
 #pragma unroll
-          for (int a = 0; a < A; ++a) logits[a] = xa_wave_sum(h2 * net.w3[a]) + net.b3[a];
-        }
+        for (int a = 0; a < A; ++a) logits[a] = xa_wave_sum(h2 * net.w3[a]) + net.b3[a];
       }
       XA_STAMP(3);
       const bool mine = lane == j;
       float r, d;
-      if constexpr (REPLAY) {
-        r = xa_readlane(c.r, j);
-        d = xa_readlane(c.d, j);
-#pragma unroll
-        for (int k = 0; k < OBS; ++k) x[k] = xa_readlane(c.obs[k], j);  // pre-reset obs
-      } else {
+      {
         const float u = p.uniforms ? xa_readlane(c.u_given, j) : xa_readlane(c.u_philox, j);
         const int act = cat_sample<A>(logits, u);
         XA_STAMP(4);
@@ -429,11 +399,9 @@ __global__ __launch_bounds__(64 * kRollWaves) void mlp_rollout_kernel(XaRolloutA
           cur = 0;
         }
       }
-      if constexpr (!REPLAY) {
-        if (mine) {
+      if (mine) {
 #pragma unroll
-          for (int a = 0; a < A; ++a) b_l[a] = logits[a];
-        }
+        for (int a = 0; a < A; ++a) b_l[a] = logits[a];
       }
       ep_ret = ep_ret + r;
       if (mine) b_epret = ep_ret;
@@ -446,31 +414,16 @@ __global__ __launch_bounds__(64 * kRollWaves) void mlp_rollout_kernel(XaRolloutA
     {
       float z[AH];
       chunk_heads<A, HF>(hb + lane * kHS, wtab[wid], z);
-      if constexpr (REPLAY) {
-#pragma unroll
-        for (int a = 0; a < A; ++a) b_l[a] = z[a] + net.b3[a];
-      }
       b_val = z[A] + net.b4;
     }
     wave_sync();  // the next chunk rewrites the rows
     const float u = p.uniforms ? c.u_given : c.u_philox;
-    const CatOut<A> cat = categorical<A>(b_l, u, REPLAY ? -1 : b_act);
+    const CatOut<A> cat = categorical<A>(b_l, u, b_act);
     float o_obs[OBS];
-    if constexpr (REPLAY) {
 #pragma unroll
-      for (int k = 0; k < OBS; ++k) {
-        const float prev = __shfl_up(c.obs[k], 1);  // step j's input = record obs of j - 1
-        o_obs[k] = lane == 0 ? x0[k] : prev;
-        st[k] = xa_readlane(c.st[k], n - 1);
-      }
-      b_rew = c.r;
-      b_done = c.d;
-    } else {
-#pragma unroll
-      for (int k = 0; k < OBS; ++k) {
-        o_obs[k] = b_obs[k];
-        st[k] = (float)cp[k < 4 ? k : 3];  // post-reset state
-      }
+    for (int k = 0; k < OBS; ++k) {
+      o_obs[k] = b_obs[k];
+      st[k] = (float)cp[k < 4 ? k : 3];  // post-reset state
     }
     XA_STAMP(7);
     if (lane < n) {
@@ -493,25 +446,22 @@ __global__ __launch_bounds__(64 * kRollWaves) void mlp_rollout_kernel(XaRolloutA
   };
 
   // two chunk buffers: the next chunk's loads are in flight while this one runs
-  StepChunk<OBS> ca, cb;
-  load_chunk<OBS, REPLAY>(p, env, lane, cur0, 0, ctr, ca);
+  StepChunk ca, cb;
+  load_chunk(p, env, lane, cur0, 0, ctr, ca);
   for (int t0 = 0; t0 < T; t0 += 128) {
-    load_chunk<OBS, REPLAY>(p, env, lane, cur0, t0 + 64, ctr, cb);
+    load_chunk(p, env, lane, cur0, t0 + 64, ctr, cb);
     run_chunk(ca, t0);
     if (t0 + 64 >= T) break;
-    load_chunk<OBS, REPLAY>(p, env, lane, cur0, t0 + 128, ctr, ca);
+    load_chunk(p, env, lane, cur0, t0 + 128, ctr, ca);
     run_chunk(cb, t0 + 64);
   }
-  if constexpr (REPLAY) cur = (int)(((long long)cur0 + T) % p.t_rec);
 
   XA_STAMP(5);
   // bootstrap V(get_states()) on the post-reset state (ppo/agent.py:72)
   float logits[A], v_next;
   net.forward(st, sh, lane, logits, v_next);
   if (lane < OBS) p.env_state[(size_t)env * OBS + lane] = st[lane];
-  if constexpr (!REPLAY) {
-    if (lane < 4) p.env_state64[(size_t)env * 4 + lane] = cp[lane];
-  }
+  if (lane < 4) p.env_state64[(size_t)env * 4 + lane] = cp[lane];
   if (lane == 0) {
     p.env_cursor[env] = cur;
     p.ep_return[env] = ep_ret;
@@ -1063,11 +1013,7 @@ __global__ __launch_bounds__(64 * kRW) void replay_rollout_kernel(XaRolloutArgs 
 template <int OBS, int A>
 int launch_rollout(const XaRolloutArgs* p, hipStream_t s) {
   const bool fused = p->ret_out != nullptr && p->return_kind != XA_RETURNS_NONE;
-  static const bool batched = [] {
-    const char* e = getenv("XA_REPLAY_BATCHED");
-    return !(e && e[0] == '0');
-  }();
-  if (p->env_kind == XA_ENV_REPLAY && batched) {
+  if (p->env_kind == XA_ENV_REPLAY) {
     const size_t lds = fused ? (size_t)4 * p->n_steps * sizeof(float) : 0;
     hipLaunchKernelGGL((replay_rollout_kernel<OBS, A>), dim3(p->n_envs), dim3(64 * kRW), lds, s,
                        *p);
@@ -1077,11 +1023,8 @@ int launch_rollout(const XaRolloutArgs* p, hipStream_t s) {
   const size_t lds = (size_t)kRollWaves * H * sizeof(float) +
                      (fused ? (size_t)kRollWaves * 3 * p->n_steps * sizeof(float) : 0);
   dim3 grid((p->n_envs + kRollWaves - 1) / kRollWaves);
-  if (p->env_kind == XA_ENV_REPLAY) {
-    hipLaunchKernelGGL((mlp_rollout_kernel<OBS, A, true>), grid, dim3(64 * kRollWaves), lds, s, *p);
-  } else if constexpr (OBS == 4 && A == 2) {
-    hipLaunchKernelGGL((mlp_rollout_kernel<OBS, A, false>), grid, dim3(64 * kRollWaves), lds, s, *p);
-  }
+  if constexpr (OBS == 4 && A == 2)
+    hipLaunchKernelGGL((mlp_rollout_kernel<OBS, A>), grid, dim3(64 * kRollWaves), lds, s, *p);
   XA_CHECK_LAUNCH("xa_mlp_rollout");
   return 0;
 }
