@@ -11,7 +11,7 @@ from collections import defaultdict
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
-KERNELS = {'ac_grad': 'ac_grad_kernel<4, 2>', 'rollout': 'mlp_rollout_kernel<4, 2, true>',
+KERNELS = {'ac_grad': 'ac_grad_kernel<4, 2>', 'rollout': 'replay_rollout_kernel<4, 2>',
            'grad_reduce': 'grad_reduce_kernel', 'minibatch': 'minibatch_kernel',
            'ppo_update': 'ppo_update_kernel<4, 2,'}
 
