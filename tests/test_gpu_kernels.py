@@ -90,8 +90,9 @@ def _replay_env(n, t_rec, seed):
     return record_cartpole_replay(n, t_rec, seed=seed)
 
 
-def _run_rollout(theta, rec, n, t, uniforms, seed, ctr, return_kind, n_rollouts=2):
+def _run_rollout(theta, rec, n, t, uniforms, seed, ctr, return_kind, n_rollouts=2, n_actions=2):
     s0, rep_obs, rep_state, rep_rew, rep_done = rec
+    od = s0.shape[1]
     dev_env = dict(state=T(s0), done=torch.zeros(n, device='cuda'),
                    cursor=torch.zeros(n, dtype=torch.int32, device='cuda'),
                    ep_return=torch.zeros(n, device='cuda'))
@@ -102,14 +103,14 @@ def _run_rollout(theta, rec, n, t, uniforms, seed, ctr, return_kind, n_rollouts=
     th = T(theta)
     ctr_t = torch.tensor([ctr], dtype=torch.int64, device='cuda')
     for r in range(n_rollouts):
-        bufs = dict(obs=torch.zeros(n, t, 4, device='cuda'),
+        bufs = dict(obs=torch.zeros(n, t, od, device='cuda'),
                     act=torch.zeros(n, t, dtype=torch.int32, device='cuda'),
                     logp=torch.zeros(n, t, device='cuda'), val=torch.zeros(n, t, device='cuda'),
                     ent=torch.zeros(n, t, device='cuda'), rew=torch.zeros(n, t, device='cuda'),
                     done=torch.zeros(n, t + 1, device='cuda'), epret=torch.zeros(n, t, device='cuda'),
                     next_val=torch.zeros(n, device='cuda'), ret=torch.zeros(n, t, device='cuda'))
         a = _lib.XaRolloutArgs()
-        a.n_envs, a.n_steps, a.obs_dim, a.n_actions = n, t, 4, 2
+        a.n_envs, a.n_steps, a.obs_dim, a.n_actions = n, t, od, n_actions
         a.theta = th.data_ptr()
         a.env_kind = 0
         a.env_state, a.env_done = dev_env['state'].data_ptr(), dev_env['done'].data_ptr()
@@ -128,7 +129,7 @@ def _run_rollout(theta, rec, n, t, uniforms, seed, ctr, return_kind, n_rollouts=
         a.return_kind = return_kind
         a.gamma, a.gamma_lam = 0.99, GAE_GL(0.99, 0.95)
         kernels.rollout(a)
-        ref = oracle.mlp_rollout(theta, 2, host_env, t, uniforms=u_r, seed=seed, ctr=ctr + r,
+        ref = oracle.mlp_rollout(theta, n_actions, host_env, t, uniforms=u_r, seed=seed, ctr=ctr + r,
                                  return_kind=return_kind)
         kernels.counter_bump(ctr_t)
         for k, v in bufs.items():
@@ -157,6 +158,24 @@ def test_rollout_replay_ragged_rows_bit_exact(device, n, t, t_rec, return_kind):
     rng = np.random.default_rng(t)
     u = [rng.random((n, t), dtype=np.float32) for _ in range(2)]
     _run_rollout(_theta(4, 2, t, 0.4), rec, n, t, u, 0, 0, return_kind)
+
+
+@pytest.mark.parametrize('obs_dim,A', [(8, 4), (2, 3), (6, 3), (4, 2)])
+def test_rollout_replay_synthetic_records_bit_exact(device, obs_dim, A):
+    """Every (obs, actions) shape the library instantiates, on synthetic records with
+    non-integer rewards (the episode-return and return chains must keep the step order
+    exactly) and dones at random steps; 160 steps: two passes of 128 rows."""
+    n, t, t_rec = 5, 160, 211
+    rng = np.random.default_rng(obs_dim * 10 + A)
+    s0 = rng.standard_normal((n, obs_dim)).astype(np.float32)
+    rep_obs = rng.standard_normal((n, t_rec, obs_dim)).astype(np.float32)
+    rep_state = rng.standard_normal((n, t_rec, obs_dim)).astype(np.float32)
+    rep_rew = (rng.standard_normal((n, t_rec)) * 3.1).astype(np.float32)
+    rep_done = (rng.random((n, t_rec)) < 0.05).astype(np.float32)
+    u = [rng.random((n, t), dtype=np.float32) for _ in range(2)]
+    for rk in (1, 2):
+        _run_rollout(_theta(obs_dim, A, obs_dim + A, 0.4), (s0, rep_obs, rep_state, rep_rew,
+                     rep_done), n, t, u, 0, 0, rk, n_actions=A)
 
 
 def test_rollout_replay_philox_bit_exact(device):
