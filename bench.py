@@ -2,7 +2,10 @@
 observation replay), one process per GPU.
 
     python bench.py --gpus N --steps K --warmup W
-    (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+    (N>1 started plainly: bench.py starts the N ranks itself under torch.distributed.run,
+    one process per GPU, before any GPU call; under an external
+    `python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...` it runs as
+    one rank and checks WORLD_SIZE == N)
 
 A step = one PPO train_step: fused rollout of n_envs x 128 steps (+GAE) and 4 epochs x 4
 minibatches (shuffle, forward, clipped loss, backward, global-norm clip, Keras Adam; one
@@ -30,6 +33,9 @@ F32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: f32-input MFMA dense peak (
 # rollout kernel algorithmic bytes per env-step (replay env): reads obs 16 + state 16 +
 # reward 4 + done 4; writes obs 16 + action/logp/value/entropy/reward/done/epret/return 32
 ROLLOUT_BYTES_PER_ENV_STEP = 40 + 48
+# CartPole-dynamics rollout: the env state lives in registers for the whole launch (read and
+# written once per env); per env-step only the outputs: obs 16 + 32 as above
+DYNAMICS_ROLLOUT_BYTES_PER_ENV_STEP = 48
 # persistent update: the rollout buffers one epoch reads per sample (obs 16 B + action,
 # old log-prob, old value, return 4 B each)
 UPDATE_BYTES_PER_SAMPLE_EPOCH = 16 + 16
@@ -54,6 +60,9 @@ def parse():
                    help='skip the compact C3 / C4 / C5 objects of the default one-GPU line')
     p.add_argument('--no-c2', dest='c2', action='store_false',
                    help='skip the secondary BASELINE configs[1] (256 envs per GPU) measurement')
+    p.add_argument('--no-dynamics', dest='dynamics', action='store_false',
+                   help='skip the `dynamics` object (the headline workload on the CartPole-v1 '
+                        'dynamics env: the step-loop rollout of an action-dependent env)')
     p.add_argument('--n-steps', type=int, default=128)
     p.add_argument('--t-rec', type=int, default=4096)
     p.add_argument('--seed', type=int, default=55)
@@ -118,16 +127,51 @@ def load_traffic(key):
     return entry.get('bytes_per_launch') if entry else None
 
 
-def _dist_setup():
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args):
+    """`bench.py --gpus N` (N > 1) started as a plain process: start N ranks under
+    torch.distributed.run (one process per GPU, 127.0.0.1 rendezvous) as a CHILD process,
+    before this process makes any GPU call (an exec after a GPU call is forbidden on this
+    pool, and the ranks must own their devices), pass rank 0's one JSON line through and exit
+    with the launcher's status. Under an external launcher (WORLD_SIZE set) nothing is
+    spawned; `_dist_setup` then checks WORLD_SIZE == --gpus."""
+    import subprocess
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1',
+           f'--nproc-per-node={args.gpus}', '--master-addr', '127.0.0.1',
+           '--master-port', str(_free_port()), str(ROOT / 'bench.py'), *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')  # dmabuf IPC only on this driver
+    print(f'bench: launching {args.gpus} ranks: {" ".join(cmd[1:])}', file=sys.stderr,
+          flush=True)
+    return subprocess.run(cmd, env=env, check=False).returncode
+
+
+def _dist_setup(args=None):
     """One process per GPU over RCCL. Rehearsal knob for a one-GPU box only:
     XA_BENCH_SHARED_DEVICE=1 puts every rank on cuda:0 with a gloo group (RCCL refuses
     two ranks on one device); the peer all-reduce then runs between processes that
-    share the GPU, so that run checks the N>1 code path, not its speed."""
-    import torch
-    import torch.distributed as dist
+    share the GPU, so that run checks the N>1 code path, not its speed. The world must be
+    the --gpus the line reports (SystemExit otherwise: a 1-GPU line from `--gpus 8` would be
+    a wrong measurement, not a smaller one)."""
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local_rank = int(os.environ.get('LOCAL_RANK', '0'))
+    if args is not None and world != args.gpus:
+        raise SystemExit(f'bench: --gpus {args.gpus} but the process group has WORLD_SIZE '
+                         f'{world}')
+    import torch
+    import torch.distributed as dist
+    if os.environ.get('XA_BENCH_LAUNCH_CHECK') == '1':
+        # CPU check of the launcher path (tests/test_host.py): gloo, no device
+        if world > 1:
+            dist.init_process_group('gloo')
+        return world, rank, torch.device('cpu')
     if os.environ.get('XA_BENCH_SHARED_DEVICE') == '1':
         local_rank = 0
         if world > 1:
@@ -379,9 +423,26 @@ def fused_td3_bytes(agent, policy=True):
     return 7 * 4 * trained + targets + batch
 
 
+def launch_check(args):
+    """XA_BENCH_LAUNCH_CHECK=1: the rank / world plumbing of an N-rank line without a GPU
+    (every rank all-reduces its rank over gloo; rank 0 prints the line's n_gpus /
+    parallelism fields)."""
+    import torch
+    import torch.distributed as dist
+    world, rank, _ = _dist_setup(args)
+    t = torch.tensor([float(rank)])
+    if world > 1:
+        dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({'launch_check': True, 'n_gpus': world, 'parallelism': f'dp{world}',
+                          'rank_sum': int(t.item()), 'config': args.config}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def bench_offpolicy_and_cnn(args):
     """Secondary configs (TRPO, ACER); one JSON line each."""
-    world, rank, device = _dist_setup()
+    world, rank, device = _dist_setup(args)
     line = run_secondary(args, args.config, world, rank, device, args.steps, args.warmup,
                          args.cpu_baseline_seconds)
     if rank == 0:
@@ -589,18 +650,27 @@ def compact_secondaries(args, device):
     return out
 
 
-def bench_ppo(args, world, rank, device, n_envs):
-    """Time PPO train steps on n_envs CartPole replay envs per rank; returns the
-    measurements and the per-kernel roofline of this workload."""
+def bench_ppo(args, world, rank, device, n_envs, env='replay'):
+    """Time PPO train steps on n_envs CartPole envs per rank; returns the measurements and
+    the per-kernel roofline of this workload. env 'replay': the synthetic observation replay
+    of the metric (the record stream ignores the actions, so the rollout runs its T policy
+    forwards as one batched launch, `replay_rollout_kernel`); 'dynamics': CartPole-v1
+    dynamics on the device (`CartPoleVecEnv`, f64 as gym), whose next observation depends on
+    the sampled action, so the rollout is the sequential step loop (`mlp_rollout_kernel`) --
+    the rate a real device env gets."""
     import numpy as np
     import torch
     import torch.distributed as dist
     from xagents_amd import PPO
-    from xagents_amd.envs import ReplayVecEnv, record_cartpole_replay
+    from xagents_amd.envs import CartPoleVecEnv, ReplayVecEnv, record_cartpole_replay
     from xagents_amd.utils.common import create_model
 
-    record = record_cartpole_replay(n_envs, args.t_rec, seed=args.seed + rank)
-    envs = ReplayVecEnv('CartPole-v1', n_envs, device=device, record=record)
+    if env == 'dynamics':
+        record = None
+        envs = CartPoleVecEnv(n_envs, seed=args.seed + rank, device=device)
+    else:
+        record = record_cartpole_replay(n_envs, args.t_rec, seed=args.seed + rank)
+        envs = ReplayVecEnv('CartPole-v1', n_envs, device=device, record=record)
     model = create_model(envs, 'ppo', 'model', optimizer_kwargs=dict(learning_rate=7e-4),
                          seed=args.seed, device=device)
     theta0 = model.theta.cpu().numpy().copy()
@@ -654,17 +724,28 @@ def bench_ppo(args, world, rank, device, n_envs):
         'update_mode': agent.update_mode, 'record': record, 'theta0': theta0, 'agent': agent,
     }
     roll_ms = float(np.mean(ktimes['rollout']))
-    roll_bytes = ROLLOUT_BYTES_PER_ENV_STEP * B
-    roll_gbs = roll_bytes / (roll_ms * 1e-3) / 1e9
+    if env == 'dynamics':
+        per = DYNAMICS_ROLLOUT_BYTES_PER_ENV_STEP
+        kname = 'xa_mlp_rollout (mlp_rollout_kernel<4,2>, CartPole-v1 dynamics step loop)'
+        tkey = f'rollout_dyn_n{n_envs}'
+        note = (f'latency-bound: one wave64 per env runs its {T} steps in order (policy '
+                f'forward, categorical sample, f64 CartPole step: the next input depends on '
+                f'the sampled action), heads / log-prob / entropy per 64-step chunk, fused '
+                f'GAE; {per} algorithmic B/env-step x {B} env-steps per launch')
+    else:
+        per = ROLLOUT_BYTES_PER_ENV_STEP
+        kname = 'xa_mlp_rollout (replay_rollout_kernel<4,2>)'
+        tkey = f'rollout_n{n_envs}'
+        note = (f'latency-bound: the replay records ignore the actions, so one 8-wave '
+                f'workgroup per env runs its {T} policy forwards (+ the bootstrap row) as '
+                f'independent 16-row MFMA tiles, then the step-order episode-return and '
+                f'return chains; {per} algorithmic B/env-step x {B} env-steps per launch')
+    roll_gbs = per * B / (roll_ms * 1e-3) / 1e9
     out['rollout_roofline'] = {
-        'kernel': 'xa_mlp_rollout (replay_rollout_kernel<4,2>)', 'bound': 'hbm',
+        'kernel': kname, 'bound': 'hbm',
         'achieved': round(roll_gbs, 3), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
         'frac': round(roll_gbs / HBM_PEAK_GBS, 6),
-        'traffic': load_traffic(f'rollout_n{n_envs}'), 'launch_ms': round(roll_ms, 5),
-        'note': f'latency-bound: one 8-wave workgroup per env runs its {T} policy forwards '
-                f'(+ the bootstrap row) as 16-row MFMA tiles, then the step-order '
-                f'episode-return and return chains; {ROLLOUT_BYTES_PER_ENV_STEP} algorithmic '
-                f'B/env-step x {B} env-steps per launch'}
+        'traffic': load_traffic(tkey), 'launch_ms': round(roll_ms, 5), 'note': note}
     if agent.update_mode == 'persistent':
         upd_ms = float(np.mean(ktimes['ppo_update']))
         flops = flops_sample * B * agent.ppo_epochs  # every sample once per epoch
@@ -710,6 +791,12 @@ def bench_ppo(args, world, rank, device, n_envs):
 
 def main():
     args = parse()
+    if args.gpus < 1:
+        raise SystemExit('--gpus must be >= 1')
+    if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
+        sys.exit(launch_ranks(args))  # before anything touches the GPU
+    if os.environ.get('XA_BENCH_LAUNCH_CHECK') == '1':
+        return launch_check(args)
     if args.lib:
         from xagents_amd import _lib
         _lib._lib = _lib.load(args.lib)
@@ -717,7 +804,7 @@ def main():
         return bench_offpolicy_and_cnn(args)
     import torch.distributed as dist
 
-    world, rank, device = _dist_setup()
+    world, rank, device = _dist_setup(args)
     # headline: the metric's PPO CartPole-v1 16-env workload (BASELINE metric / configs[0]
     # shape) on the GPU; secondary: BASELINE configs[1] (256 envs per GPU); strong scaling
     # (--global-envs): the given env count split over the ranks
@@ -726,6 +813,9 @@ def main():
     n_head = args.global_envs // world if args.global_envs else args.n_envs
     head = bench_ppo(args, world, rank, device, n_head)
     c2 = bench_ppo(args, world, rank, device, 256) if args.c2 and n_head != 256 else None
+    # the same 16-env PPO on the CartPole-v1 dynamics env: the sequential step-loop rollout a
+    # real (action-dependent) device env runs, beside the replay headline
+    dyn = bench_ppo(args, world, rank, device, n_head, env='dynamics') if args.dynamics else None
     # BASELINE configs[2..4] as compact objects of the same one-GPU line
     sec = compact_secondaries(args, device) if world == 1 and args.secondary else {}
 
@@ -756,7 +846,11 @@ def main():
                              f'synthetic obs replay' + (' (the metric\'s 16-env configuration)'
                                                         if n_head * world == 16 or
                                                         (n_head == 16 and not args.global_envs)
-                                                        else '')),
+                                                        else '')
+                             + '; the replay records ignore the actions, so the rollout runs '
+                               'its policy forwards as one batched launch (the `dynamics` '
+                               'object times the sequential step loop of an action-dependent '
+                               'env)'),
                 'n_envs_per_gpu': n_head,
                 'n_steps': args.n_steps,
                 'batch_per_gpu': n_head * args.n_steps,
@@ -786,6 +880,22 @@ def main():
                 'update_roofline': c2['update_roofline'],
                 'rollout_roofline': c2['rollout_roofline'],
             }
+        if dyn is not None:
+            line['dynamics'] = {
+                'workload': f'PPO CartPole-v1, {n_head} envs/GPU, MLP[64,64], n_steps='
+                            f'{args.n_steps}, 4x4 minibatches, CartPole-v1 dynamics on the '
+                            f'device (CartPoleVecEnv, f64 state as gym; the next observation '
+                            f'depends on the sampled action, so the rollout is the sequential '
+                            f'step loop)',
+                'value': round(dyn['value'], 1), 'unit': 'env-steps/s',
+                'ms_per_step': round(dyn['ms_per_step'], 4),
+                'update_ms': round(dyn['update_ms'], 4),
+                'rollout_ms': round(dyn['rollout_ms'], 4),
+                'update': dyn['update_mode'],
+                'roofline': dominant(dyn),
+                'update_roofline': dyn['update_roofline'],
+                'rollout_roofline': dyn['rollout_roofline'],
+            }
         line.update(sec)
         if world == 1 and args.cpu_baseline_seconds > 0:
             line['cpu_baseline'] = cpu_baseline(args, head['record'], head['theta0'])
@@ -793,7 +903,7 @@ def main():
             line['cpu_baseline'] = None
         print(json.dumps(line), flush=True)
     if world > 1:
-        for r in (head, c2):
+        for r in (head, c2, dyn):
             if r is not None and r['agent'].peer is not None:
                 r['agent'].peer.close()
         dist.destroy_process_group()

@@ -91,10 +91,11 @@ def test_td3_data_parallel_done_patterns(device, path):
     """TD3 and DDPG at W = 2 (BASELINE configs[4]'s data-parallel step) on both gradient-step
     paths: DP gradients = the rank sum of local ones, vs float64 on the union batch, and
     different per-rank done patterns (ddpg/agent.py:157-166), tests/td3_dp_worker.py. The
-    fused stages run on 96 workgroups per rank, so both ranks' persistent launches are
-    resident together on the one test GPU."""
+    grid is the agent's default: ranks sharing the one test GPU each cap their persistent
+    launches at 3/4 of their share of the CUs (DDPG._shared_blocks), so both
+    ranks' launches are resident together."""
     _run('td3_dp_worker.py', 2, 'TD3 DP OK',
-         extra_env={'XA_TEST_TD3_PATH': path, 'XA_TD3_BLOCKS': '96'}, timeout=200)
+         extra_env={'XA_TEST_TD3_PATH': path}, timeout=200)
 
 
 def test_peer_stall_falls_back_to_rccl(device):

@@ -160,6 +160,13 @@ for step in "$@"; do
       XA_BENCH_SHARED_DEVICE=1 HSA_ENABLE_IPC_MODE_LEGACY=0 run c4w2 400 python -m torch.distributed.run \
         --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py \
         --config c4 --gpus 2 --steps 2 --warmup 1 --cpu-baseline-seconds 0 ;;
+    w2)
+      # bench.py --gpus 2 started plainly: it launches its 2 ranks itself (VERDICT r05
+      # item 1); both ranks on the one GPU over gloo (speed meaningless, n_gpus / dp2 checked)
+      XA_BENCH_SHARED_DEVICE=1 run w2 400 python bench.py --gpus 2 --steps 10 --warmup 3 \
+        --cpu-baseline-seconds 0
+      XA_BENCH_SHARED_DEVICE=1 run w2c4 500 python bench.py --config c4 --gpus 2 --steps 2 \
+        --warmup 1 --cpu-baseline-seconds 0 ;;
     c4dp) run_pytest c4dp 600 -s tests/test_gpu_dp.py -k cnn tests/test_gpu_configs.py::test_c4_ppo_cnn_128_env_shard ;;
     c5w2)
       # W = 2 rehearsal of the C5 data-parallel bench with both ranks on the one GPU (gloo;

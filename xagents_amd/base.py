@@ -405,6 +405,7 @@ class BaseAgent(ABC):
         slots itself (PPO._setup_fused_stats) there is nothing to launch: the step's slot is
         its launch number's parity, and the fold checks the number the launch wrote."""
         if getattr(self, '_stats_fused', False) and after is None and \
+                getattr(self, 'update_mode', None) == 'persistent' and \
                 done_out.data_ptr() == self.b_done.data_ptr():
             if getattr(self, '_stats_queue', None) is None or \
                     getattr(self, '_stats_queue_kind', None) != 'fused':
@@ -536,9 +537,17 @@ class BaseAgent(ABC):
             # did not count would otherwise fold another step's statistics)
             host_done, host_epret, host_status = (self._fused_done[slot],
                                                   self._fused_epret[slot],
-                                                  self._fused_status[slot])
+                                                  self._fused_host_status[slot])
             got = int(self._fused_gen[slot].item())
+            # a launch that aborted (exchange timeout) may never have stored its slot: the
+            # device status word names that cause, so it is checked before the slot's number
             if got != gen:
+                status = getattr(self, 'device_status', None)
+                if status is not None and int(status.max().item()):
+                    raise RuntimeError(
+                        f'{self.__class__.__name__}: an in-launch exchange of the persistent '
+                        f'update timed out (device status word set); the parameters are '
+                        f'invalid')
                 raise RuntimeError(f'{self.__class__.__name__}: episode statistics slot {slot} '
                                    f'holds update launch {got}, expected {gen}')
         if getattr(self, 'device_status', None) is not None and host_status is not None and \
@@ -663,6 +672,12 @@ class OffPolicy(BaseAgent, ABC):
         self.distributed = dist.is_available() and dist.is_initialized()
         self.world_size = dist.get_world_size() if self.distributed else 1
         self.rank = dist.get_rank() if self.distributed else 0
+        # ranks sharing one GPU (the multi-process tests) split its resident-workgroup
+        # capacity for the persistent kernels (DDPG / TD3 fused step): collective, so once here
+        self._ranks_share = 1
+        if self.distributed and torch.device(self.device).type == 'cuda':
+            from xagents_amd.comm import ranks_per_device
+            self._ranks_share = ranks_per_device()
         env = self.envs
         self.replay = DeviceReplay(self.buffers, env.obs_shape, env.obs_dtype, act_shape,
                                    act_dtype, self.device)

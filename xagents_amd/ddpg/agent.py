@@ -169,7 +169,7 @@ class DDPG(OffPolicy):
             nbytes = _lib.load().xa_td3_act_workspace_bytes(n, S, A, H1, H2)
             self._fused_act_ws = torch.zeros(nbytes, dtype=torch.uint8, device=self.device)
             fa.workspace, fa.workspace_bytes = self._fused_act_ws.data_ptr(), nbytes
-            fa.n_blocks = int(os.environ.get('XA_TD3_ACT_BLOCKS', '0'))
+            fa.n_blocks = int(os.environ.get('XA_TD3_ACT_BLOCKS', '0')) or self._shared_blocks()
             if '_fused_status' not in self.__dict__:
                 self._fused_status = torch.zeros(1, dtype=torch.int32, device=self.device)
             fa.status = self._fused_status.data_ptr()
@@ -243,6 +243,17 @@ class DDPG(OffPolicy):
                 self._run_phase('actor', self._actor_phase)
 
     # ---- the fused gradient step (xa_td3_update) -------------------------------------
+    def _shared_blocks(self):
+        """Grid of the persistent TD3 launches (0 = the kernel's default, one workgroup per
+        CU up to 256). Ranks sharing one GPU each take 3/4 of their share of
+        the CUs, so every rank's launch is resident at once and the grid barriers cannot
+        wait on a workgroup that is queued behind another rank's spinning grid."""
+        share = getattr(self, '_ranks_share', 1)
+        if share <= 1:
+            return 0
+        cus = torch.cuda.get_device_properties(self.device).multi_processor_count
+        return max(16, min(256, cus) // share * 3 // 4)
+
     def _fused_ok(self):
         import os
         if os.environ.get('XA_TD3_FUSED', '1') == '0':
@@ -331,7 +342,7 @@ class DDPG(OffPolicy):
                 self._fused_status = torch.zeros(1, dtype=torch.int32, device=self.device)
             a.workspace, a.workspace_bytes = self._fused_ws.data_ptr(), nbytes
             import os
-            a.n_blocks = int(os.environ.get('XA_TD3_BLOCKS', '0'))
+            a.n_blocks = int(os.environ.get('XA_TD3_BLOCKS', '0')) or self._shared_blocks()
             a.status = self._fused_status.data_ptr()
             a.stage = 0
             # data parallel: the critics' losses are batch sums (Keras MSE + minimize), the

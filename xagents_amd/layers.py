@@ -425,6 +425,12 @@ class LayerExecutor:
         Bb = batch or self.B
         assert adam is None or not accumulate
         assert Bb <= self.B
+        # a forward-only executor's fused conv-stack forward never wrote h1 / h2, which the
+        # backward reads as gates and weight-gradient operands
+        if not (self.keep_hidden or not self.stack):
+            raise RuntimeError('LayerExecutor.backward: this executor runs the fused conv '
+                               'stack forward-only (keep_hidden=False); its hidden '
+                               'activations are not materialised')
         tp = self.model.theta.data_ptr()
         gp = grad.data_ptr() if grad is not None else None
         written = [False] * len(self.layers)

@@ -62,6 +62,13 @@ class PPO(A2C):
         super(PPO, self).__init__(envs, model, **kwargs)
 
     def _setup_update(self):
+        # a re-plan (a peer timeout dropping to the chain, a new permutation source) starts
+        # with no statistics stored by an update launch: fold what earlier launches stored,
+        # and only `_setup_fused_stats` (persistent mode) turns the fused slots back on
+        # (a chain step must not fold the last persistent launch's slot again)
+        if getattr(self, '_stats_fused', False):
+            self._drain_episode_stats()
+        self._stats_fused = False
         # optimizer step placement of the chain: 'prologue' (next minibatch's xa_ac_grad
         # recomputes it in every block) or 'kernel' (a standalone xa_clip_adam launch)
         self._opt_kernel = os.environ.get('XA_PPO_OPT', 'prologue') == 'kernel'
@@ -260,7 +267,8 @@ class PPO(A2C):
                                 for _ in range(2)]
             self._fused_done = [h[:nd].view(sd) for h in self._fused_host]
             self._fused_epret = [h[oe:oe + se[0] * se[1]].view(se) for h in self._fused_host]
-            self._fused_status = [h[os_:os_ + 1].view(torch.int32) for h in self._fused_host]
+            self._fused_host_status = [h[os_:os_ + 1].view(torch.int32)
+                                       for h in self._fused_host]
             self._fused_gen = [h[nw:nw + 1].view(torch.int32) for h in self._fused_host]
             self._fused_dev = []
             for h in self._fused_host:
