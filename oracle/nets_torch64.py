@@ -27,9 +27,21 @@ def _act(name, z):
     return z
 
 
-def forward(layers, theta, x, input_shape):
+def forward(layers, theta, x, input_shape, gates=None):
     """theta: flat float64 tensor (may require grad); x: uint8 or float tensor [B, ...].
-    Returns (x as float64, [every layer's output])."""
+    Returns (x as float64, [every layer's output]). gates {layer: bool tensor of the layer's
+    output shape}: those ReLU layers take the given gate pattern instead of z > 0 (y = z
+    where the gate is on, 0 elsewhere, and the same mask in the gradient) -- the f64 replay
+    of a device run adopts the device's gates, which differ from the f64 forward's only at
+    pre-activations within f32 rounding of zero (nets_f64.adopt_gates)."""
+    gates = gates or {}
+
+    def act(i, name, z):
+        if i in gates:
+            assert name == 'relu', name
+            return z * gates[i].reshape(z.shape).to(z.dtype)
+        return _act(name, z)
+
     if x.dtype == torch.uint8:
         x = (x.float() / 255.0).double()  # f32(u8) / 255 as the device loader, then f64
     else:
@@ -50,7 +62,7 @@ def forward(layers, theta, x, input_shape):
         W = theta[o1:o1 + n1].reshape(s1)
         b = theta[o2:o2 + s2[0]]
         if l.kind == 'dense':
-            outs.append(_act(l.activation, src.reshape(B, -1) @ W + b))
+            outs.append(act(i, l.activation, src.reshape(B, -1) @ W + b))
         else:
             H, Win, C = src.shape[1:]
             k, s = l.size, l.stride
@@ -59,7 +71,7 @@ def forward(layers, theta, x, input_shape):
                    + torch.arange(k, device=x.device)[None, :])
             cols = src.reshape(B * H, Win, C)[:, idx, :].reshape(B * H, P, k * C)
             y = cols @ W.reshape(k * C, l.filters) + b
-            outs.append(_act(l.activation, y).reshape(B, H, P, l.filters))
+            outs.append(act(i, l.activation, y).reshape(B, H, P, l.filters))
     return x, outs
 
 

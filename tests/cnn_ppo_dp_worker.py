@@ -11,14 +11,21 @@ rollout uniforms and the rank-major union of the ranks' minibatch permutations. 
 data-parallel train step must equal the union step (xagents/ppo/agent.py:157-191):
 actions bit for bit, log-probs / values / returns to f32 rounding (the union's GEMMs run
 at twice the batch, which may pick another split-K count and so another summation
-order), parameters identical on every rank and 16 optimizer steps taken. The parameter
-bound separates branch flips from everything else: every optimizer step's per-sample head
-gradients (d logits, d value) of the data-parallel ranks are compared row by row with the
-union's; a sample whose PPO ratio or value sits within f32 rounding of its clip boundary
-can take the other branch in one of the two runs, which changes its row by O(1) (every
-other row agrees to ~1e-5). Without such a flip the parameters must agree within 2e-5 of
-the update's norm; with one (counted and reported, at most 8 per train step) within 5e-4.
-ReLU gate flips of units at pre-activation ~0 are counted and reported too.
+order), parameters identical on every rank and 16 optimizer steps taken.
+
+The parameter bound is against a float64 REPLAY of the union train step that takes the
+data-parallel ranks' own discrete decisions: starting from theta_0,
+every optimizer step runs the f64 forward of the union minibatch (oracle/nets_torch64.py
+on the test GPU) with the ReLU gate pattern the ranks' f32 forwards produced, the clipped
+PPO loss gradient with each sample's clip branches (policy: ratio clip active or not;
+value: unclipped, clipped or cut) as the ranks took them, then clip_by_global_norm and
+Keras Adam in f64. A sample whose PPO ratio or value sits within f32 rounding of a clip
+boundary, or a unit at pre-activation ~0, may decide differently in f32 and f64; adopting
+the device's decisions removes those O(1) jumps, so the data-parallel theta must match the
+replay within 2e-5 of the update's norm at every record seed, flips or not. A rank's
+branch decision is read from its recorded head-gradient row: the candidate row (f64) of
+each branch nearest to it (candidates differ by O(1); an argmin, no threshold). The f32
+union run is still compared and its flip counts reported (information only).
 Prints 'CNN DP OK <rank>'."""
 import os
 import sys
@@ -103,6 +110,86 @@ def gate_flips(dp_gates, un_gates):
     return out
 
 
+def replay_f64(model, theta0, it0, grad_norm, rows, heads, gates, world, dev='cuda'):
+    """The float64 replay of the union train step with the data-parallel ranks' decisions.
+    rows[k] = (x uint8 [n, ...], act, old logp, old value, return) of union minibatch k
+    (rank-major), heads[k] = the ranks' recorded [d logits | d value] rows (each rank's
+    loss is its local mean: W x the union's scale), gates[k] = their packed ReLU gate rows.
+    Returns theta after the E x M steps and the adopted flip counts (samples whose adopted
+    branch differs from the f64 forward's own choice; gates likewise)."""
+    import nets_torch64 as OT
+    import oracle as OR
+    dev = torch.device(dev)
+    opt = model.optimizer
+    f32 = lambda v: float(np.float32(v))  # noqa: E731 (TF ApplyAdam's f32 hyper-parameters)
+    th = torch.from_numpy(theta0).to(dev)
+    m = np.zeros_like(theta0)
+    v = np.zeros_like(theta0)
+    relu = [i for i, l in enumerate(model.layers)
+            if l.kind != 'flatten' and getattr(l, 'activation', None) == 'relu']
+    o_logits, o_value = model.outputs
+    clip, ent_coef, v_coef, eps = 0.1, 0.01, 0.5, 1e-8
+    branch_flips = gate_flips = 0
+    for k, ((x, act, oldlp, oldv, ret), hd, gk) in enumerate(zip(rows, heads, gates)):
+        n = x.shape[0]
+        assert len(gk) == len(relu), (len(gk), relu)
+        gmap = {}
+        for i, packed in zip(relu, gk):
+            units = int(np.prod(model.layers[i].out_shape))
+            mask = np.unpackbits(packed.numpy(), axis=1)[:, :units].astype(bool)
+            gmap[i] = torch.from_numpy(mask).to(dev)
+        thg = th.clone().requires_grad_(True)
+        xd = torch.from_numpy(x).to(dev)
+        _, outs = OT.forward(model.layers, thg, xd, model.input_shape, gates=gmap)
+        with torch.no_grad():
+            _, own = OT.forward(model.layers, th, xd, model.input_shape)
+            for i in relu:
+                gate_flips += int(((own[i] > 0) != gmap[i].reshape(own[i].shape)).sum())
+            del own
+        logits, val = outs[o_logits], outs[o_value][:, 0]
+        lg = logits.detach().cpu().numpy()
+        vv = val.detach().cpu().numpy()
+        lsm = OR.log_softmax(lg)
+        p = np.exp(lsm)
+        A = lg.shape[1]
+        logp = lsm[np.arange(n), act]
+        H = -(p * lsm).sum(-1)
+        adv = ret - oldv
+        adv = (adv - adv.mean()) / (adv.std() + eps)
+        ratio = np.exp(logp - oldlp)
+        onehot = np.eye(A)[act]
+        ent = (ent_coef / n) * p * (lsm + H[:, None])
+        # candidate rows of every branch (xagents/ppo/agent.py:112-134 as the device's
+        # loss: tf.maximum / clip_by_value tie rules)
+        dz_on = (-adv * ratio / n)[:, None] * (onehot - p) + ent
+        dz_off = ent
+        dvo = vv - oldv
+        vclip = oldv + np.clip(dvo, -clip, clip)
+        dv_c = [v_coef * (vv - ret) / n, v_coef * (vclip - ret) / n, np.zeros(n)]
+        d = hd.double().numpy() / world
+        pick_on = (np.linalg.norm(dz_on - d[:, :-1], axis=1) <=
+                   np.linalg.norm(dz_off - d[:, :-1], axis=1))
+        vi = np.argmin(np.stack([np.abs(c - d[:, -1]) for c in dv_c]), axis=0)
+        # the f64 forward's own decisions, for the report
+        pg1, pg2 = -adv * ratio, -adv * np.clip(ratio, 1 - clip, 1 + clip)
+        own_on = (pg1 >= pg2) | ((ratio >= 1 - clip) & (ratio <= 1 + clip))
+        vl1, vl2 = (vv - ret) ** 2, (vclip - ret) ** 2
+        own_vi = np.where(vl1 >= vl2, 0, np.where((dvo >= -clip) & (dvo <= clip), 1, 2))
+        branch_flips += int((pick_on != own_on).sum() + (vi != own_vi).sum())
+        dz = np.where(pick_on[:, None], dz_on, dz_off)
+        dv = np.choose(vi, dv_c)
+        g, = torch.autograd.grad([logits, outs[o_value]], [thg], grad_outputs=[
+            torch.from_numpy(dz).to(dev), torch.from_numpy(dv[:, None]).to(dev)])
+        del outs, logits, val, thg
+        g = g.cpu().numpy()
+        gc = OR.clip_by_global_norm_f64(g, grad_norm)[0]
+        t0 = th.cpu().numpy()
+        t1, m, v = OR.keras_adam_f64(t0, m, v, gc, it0 + k + 1, f32(opt.learning_rate),
+                                     f32(opt.beta_1), f32(opt.beta_2), f32(opt.epsilon))
+        th = torch.from_numpy(t1).to(dev)
+    return th.cpu().numpy(), branch_flips, gate_flips
+
+
 def main():
     if os.environ.get('XA_LIB'):  # a diagnostic variant library (tools/cnn_dp_rel.sh)
         from xagents_amd import _lib
@@ -131,6 +218,7 @@ def main():
     dp.train_step()
     torch.cuda.synchronize()
     got = {k: getattr(dp, k).cpu() for k in ('b_act', 'b_logp', 'b_val', 'b_ret')}
+    got['obs'] = dp.obs_buf[:T].cpu()  # [T, N, 84, 84, 1] uint8, the step's frames
     got['theta'] = dp.model.theta.cpu()
     gathered = {}
     for k, t in got.items():
@@ -148,6 +236,26 @@ def main():
         assert torch.equal(p, gathered['theta'][0]), 'ranks disagree on theta'
     assert int(dp.model.optimizer.iterations.item()) - it0 == E * M
     if rank == 0:
+        sys.path.insert(0, str(ROOT / 'oracle'))
+        # the union minibatch rows of every optimizer step: rank-major, each rank's own
+        # minibatch slice of its shard (the order the gathered head rows / gates follow)
+        rows = []
+        for k in range(E * M):
+            e, mi = divmod(k, M)
+            xs, fields = [], [[] for _ in range(4)]
+            for r in range(world):
+                idx = perms[r][e][mi * mb:(mi + 1) * mb]
+                env, t = idx // T, idx % T  # flat env-major index i = env * T + t
+                xs.append(gathered['obs'][r].numpy()[t, env])
+                for f, key in enumerate(('b_act', 'b_logp', 'b_val', 'b_ret')):
+                    fields[f].append(gathered[key][r].reshape(-1).numpy()[idx])
+            act, oldlp, oldv, ret = (np.concatenate(f) for f in fields)
+            rows.append((np.concatenate(xs), act.astype(np.int64), oldlp.astype(np.float64),
+                         oldv.astype(np.float64), ret.astype(np.float64)))
+        th64, bflips64, gflips64 = replay_f64(dp.model, theta0, it0, dp.grad_norm, rows, heads,
+                                              gates, world)
+        td = gathered['theta'][0].numpy().astype(np.float64)
+        rel64 = np.linalg.norm(td - th64) / np.linalg.norm(th64 - theta0)
         union_rec = tuple(np.concatenate([r[i] for r in records]) for i in range(5))
         un = make(union_rec, world * N, data_parallel=False)
         assert un.executor_path and not un.distributed
@@ -173,20 +281,18 @@ def main():
         rel = np.linalg.norm(td - tu) / np.linalg.norm(tu - theta0)
         flips, worst = head_flips(heads, un_rows, world)
         gflips = gate_flips(gates, un_gates)
-        print(f'CNN DP W={world} seed {base}: rollout buffers bit-equal {exact}, theta rel '
-              f'{rel:.2e}, clip-branch flips (step, row, part) {flips}, other head rows within '
-              f'{worst:.1e}, ReLU gate flips (step, layer, units) {gflips}', flush=True)
-        # the union sums each minibatch's weight gradient over W x the rows in one pass, the
-        # ranks in parts + an all-reduce: f32 regrouping, which also moves a few ReLU units
-        # whose pre-activation sits at ~0 across their gate (reported; measured harmless:
-        # 2.4e-7 .. 2.0e-6 with 4 .. 21 of them), unless a sample flips its PPO ratio or
-        # value clip branch: that changes its gradient row by O(1) (round 4's 1.2e-4 at
-        # record seed 55, profiles/r04ag_dprel.txt). A wrong exchange (a missing rank, a
-        # stale bucket) deviates by O(1)
-        assert len(flips) <= 8, f'{len(flips)} clip-branch flips: {flips}'
-        bound = 2e-5 if not flips else 5e-4
-        assert rel < bound, (f'data-parallel update deviates from the union update: {rel:.2e} '
-                             f'({len(flips)} clip-branch flips {flips}, gate flips {gflips})')
+        print(f'CNN DP W={world} seed {base}: theta vs the f64 replay with the ranks\' '
+              f'decisions {rel64:.2e} (adopted: {bflips64} clip branches, {gflips64} ReLU gates '
+              f'differ from the f64 forward\'s own); vs the f32 union run {rel:.2e} '
+              f'(information: rollout buffers bit-equal {exact}, clip-branch flips (step, row, '
+              f'part) {flips}, other head rows within {worst:.1e}, ReLU gate flips (step, '
+              f'layer, units) {gflips})', flush=True)
+        # one bound, flips or not: the replay takes the ranks' discrete decisions, so what
+        # remains is f32 rounding (regrouped sums, the all-reduce); a wrong exchange (a
+        # missing rank, a stale bucket) deviates by O(1)
+        assert rel64 < 2e-5, (f'data-parallel update deviates from the f64 replay of the '
+                              f'union step: {rel64:.2e} ({bflips64} adopted branch flips, '
+                              f'{gflips64} gate flips)')
         assert int(un.model.optimizer.iterations.item()) == E * M
     dist.barrier()
     print(f'CNN DP OK {rank}', flush=True)

@@ -49,16 +49,18 @@ def test_ppo_data_parallel_equals_union(device, mode, world, shape):
 
 
 @pytest.mark.parametrize('world,bucket_mb,seed', [(2, None, 55), (2, None, 155), (2, None, 255),
-                                                  (4, None, 55), (2, '0', 55)])
+                                                  (4, None, 55), (4, None, 155), (4, None, 255),
+                                                  (2, '0', 55)])
 def test_cnn_ppo_data_parallel_equals_union(device, world, bucket_mb, seed):
     """BASELINE configs[3]'s path: PPO with the CNN actor-critic on the layer executor,
     data parallel over W ranks (advantage statistics all-reduced once per train step, the
     77 MB gradient all-reduced per minibatch in buckets overlapping the conv backward),
-    equal to one process on the union of the shards (tests/cnn_ppo_dp_worker.py;
-    xagents/ppo/agent.py:157-191): within 2e-5 of the update's norm unless a sample's clip
-    branch flips between the two runs (detected per optimizer step from the per-sample head
-    gradients, counted, then 5e-4). Record seeds 55 / 155 / 255. bucket_mb '0': one bucket
-    per layer (every layer's slice goes out as soon as it is final)."""
+    equal to the union of the shards (tests/cnn_ppo_dp_worker.py; xagents/ppo/agent.py:
+    157-191): theta within 2e-5 of the update's norm of a float64 replay of the union train
+    step that adopts the ranks' ReLU gates and clip-branch decisions (one bound, no flip
+    escape), plus the f32 single-process union run (rollout equality; its theta deviation
+    reported). Record seeds 55 / 155 / 255 at W = 2 and 4. bucket_mb '0': one bucket per
+    layer (every layer's slice goes out as soon as it is final)."""
     env = {'XA_DP_SEED': str(seed)}
     if bucket_mb:
         env['XA_TEST_BUCKET_MB'] = bucket_mb

@@ -160,6 +160,14 @@ for step in "$@"; do
       XA_BENCH_SHARED_DEVICE=1 HSA_ENABLE_IPC_MODE_LEGACY=0 run c4w2 400 python -m torch.distributed.run \
         --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py \
         --config c4 --gpus 2 --steps 2 --warmup 1 --cpu-baseline-seconds 0 ;;
+    tl16)
+      # kernel trace of the 16-env headline alone: the per-step timeline (idle gaps between
+      # the rollout and update launches, and between train steps)
+      (cd /tmp && timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/${T}_tl16 \
+        -o run --output-format csv -- python $R/bench.py --steps 40 --warmup 5 --no-c2 \
+        --no-dynamics --no-secondary --cpu-baseline-seconds 0 > $R/gpurun_out/${T}_tl16_bench.json 2>&1) || exit $?
+      python tools/step_timeline.py gpurun_out/${T}_tl16/run_kernel_trace.csv ppo_update_kernel 30 \
+        > gpurun_out/${T}_tl16_timeline.txt 2>&1 ;;
     w2)
       # bench.py --gpus 2 started plainly: it launches its 2 ranks itself (VERDICT r05
       # item 1); both ranks on the one GPU over gloo (speed meaningless, n_gpus / dp2 checked)

@@ -136,6 +136,11 @@ XA_DEV double gran_f64(const f32x4v& v) {
 // grid's polls onto one L2 channel), so a granule that lands just after a round was
 // issued is seen one round trip later.
 // (measurement knob) s_sleep units (64 cycles) between poll rounds
+// (A/B knob) every block forms the global gradient norm from its own copy of the reduced g
+// (phase C) instead of polling per-wave sum-of-squares partials published in phase B
+#ifndef XA_SELF_NORM
+#define XA_SELF_NORM 0
+#endif
 #ifndef XA_POLL_SLEEP
 #define XA_POLL_SLEEP 1
 #endif
@@ -1239,6 +1244,7 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
       }
       if (__syncthreads_or(bad)) return;
     }
+#if !XA_SELF_NORM
     sq = xa_wave_sum_f64(sq);
     if (wave_sq) {
       if (lane == 0) st_gran_f64(g_r, sq0 + (uint32_t)(16 * (4 * b + w)), sq, tag, kWt);
@@ -1249,6 +1255,9 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
         st_gran_f64(g_r, sq0 + (uint32_t)(16 * b),
                     (U.wsum[0] + U.wsum[1]) + (U.wsum[2] + U.wsum[3]), tag, kWt);
     }
+#else
+    (void)sq;
+#endif
     XA_STAMP(40);
     XA_TRACE_PT(b, k, 3);
 
@@ -1271,7 +1280,9 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
       bv[4 * q4] = v01.x; bv[4 * q4 + 1] = v01.y; bv[4 * q4 + 2] = v23.x; bv[4 * q4 + 3] = v23.y;
     }
     {
-      constexpr int NG = 8 + RPT, NQ = 4;  // g slice pairs; norm partials per lane (G <= 256)
+      // g slice pairs; norm partials per lane (G <= 256; none when every block forms the
+      // norm from its own full copy of g, XA_SELF_NORM)
+      constexpr int NG = 8 + RPT, NQ = XA_SELF_NORM ? 0 : 4;
       uint32_t off[NG + NQ];
       f32x4v x[NG + NQ];
       // exchange order: the thread's 16 W2 values are pairs 256 h + tid (coalesced)
@@ -1289,20 +1300,21 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
 #ifndef XA_C_POLL_SPLIT_G
 #define XA_C_POLL_SPLIT_G 32
 #endif
-      if (G <= XA_C_POLL_SPLIT_G) {
+      if (NQ == 0 || G <= XA_C_POLL_SPLIT_G) {
         // few blocks: one round trip for both
         bad = !poll_gran<NG + NQ>(g_r, off, n, tag, x, ws.ctl, epoch, p.status);
       } else {
         // many blocks: the g slice, then the norm partials (a failed poll re-reads only
         // its own granules)
-        uint32_t offg[NG], offq[NQ];
-        f32x4v xg[NG], xq[NQ];
+        constexpr int NQ1 = NQ > 0 ? NQ : 1;
+        uint32_t offg[NG], offq[NQ1];
+        f32x4v xg[NG], xq[NQ1];
 #pragma unroll
         for (int u = 0; u < NG; ++u) offg[u] = off[u];
 #pragma unroll
         for (int u = 0; u < NQ; ++u) offq[u] = off[NG + u];
         bad = !poll_gran<NG>(g_r, offg, NG, tag, xg, ws.ctl, epoch, p.status);
-        if (!bad) bad = !poll_gran<NQ>(g_r, offq, n - NG, tag, xq, ws.ctl, epoch, p.status);
+        if (!bad) bad = !poll_gran<NQ1>(g_r, offq, n - NG, tag, xq, ws.ctl, epoch, p.status);
 #pragma unroll
         for (int u = 0; u < NG; ++u) x[u] = xg[u];
 #pragma unroll
@@ -1321,11 +1333,31 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
       for (int u = 0; u < NQ; ++u)
         if (NG + u < n) tot += gran_f64(x[NG + u]);
     }
+#if XA_SELF_NORM
+    {
+      // the block holds all of g (each parameter on exactly one thread): its own f64 sum of
+      // squares in a fixed thread / wave order, identical in every block
+      double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+      for (int q = 0; q < 16; q += 2) {
+        s0 = fma((double)gw[q], (double)gw[q], s0);
+        s1 = fma((double)gw[q + 1], (double)gw[q + 1], s1);
+      }
+#pragma unroll
+      for (int q = 0; q < RPT; ++q) s0 = fma((double)gr[q], (double)gr[q], s0);
+      const double ws = xa_wave_sum_f64(s0 + s1);
+      if (lane == 0) U.wsum[w] = ws;
+    }
+#endif
     if (__syncthreads_or(bad)) return;
     XA_STAMP(47);
     XA_TRACE_PT(b, k, 4);
 #ifndef XA_ABL_CNORM
+#if XA_SELF_NORM
+    tot = (U.wsum[0] + U.wsum[1]) + (U.wsum[2] + U.wsum[3]);
+#else
     tot = xa_wave_sum_f64(tot);
+#endif
     // tf.clip_by_global_norm's scale clip * min(1 / norm, 1 / clip), on the hardware sqrt /
     // reciprocal units (the update is checked against float64 with a tolerance)
     const float gn = __builtin_amdgcn_sqrtf((float)tot);

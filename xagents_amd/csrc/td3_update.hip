@@ -1181,7 +1181,50 @@ struct Sync {
   unsigned target, G, n, epoch;
   int* status;
   unsigned long long* trace;  // block 0 only: the wall clock as each barrier completes
+  // launch-entry rendezvous (block 0 only): every block adds 1 to *ent once it holds the
+  // launch-start words in registers; block 0 writes the next launch's start words only
+  // after *ent reached ent_target (seen while it waits at a barrier, or polled at the end)
+  unsigned* ent;
+  unsigned ent_target;
+  int ent_ok;
 };
+
+// block 0, thread 0: has every block of the launch entered (read its start words)?
+XA_DEV bool entered_all(const Sync& y) {
+  return (int)(__hip_atomic_load((gu32*)y.ent, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) -
+               y.ent_target) >= 0;
+}
+
+// Every block, once its launch-start words (barrier base, epoch, step / noise / entry
+// counters) are in registers: drain the loads, then one lane counts the block in. Contains a
+// __syncthreads().
+XA_DEV void enter_launch(unsigned* ent) {
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    __hip_atomic_fetch_add((gu32*)ent, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// block 0, thread 0, before it writes the next launch's start words: wait (bounded) until
+// every block entered. False on timeout / abort.
+XA_DEV bool wait_entered(Sync& y) {
+  const uint64_t t0 = wall_clock64();
+  while (!y.ent_ok) {
+    if (entered_all(y)) {
+      y.ent_ok = 1;
+      break;
+    }
+    if (__hip_atomic_load((gu32*)y.abort_w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == y.epoch)
+      return false;
+    if (wall_clock64() - t0 > kSpinTicks) {
+      __hip_atomic_store((gu32*)y.abort_w, y.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (y.status) __hip_atomic_store((gu32*)y.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  return true;
+}
 
 XA_DEV unsigned shard_sum(const unsigned* cnt) {
   unsigned v[kShards];
@@ -1205,12 +1248,11 @@ XA_DEV bool grid_sync(Sync& y, int& lds_flag, int jobs, const PreB& pb = no_preb
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   y.n += 1;
-  // EVERY block arrives at a launch's first barrier: each block reads the launch-start words
-  // (barrier base, epoch, step and noise counters) before it arrives, so once block 0 has
-  // passed this barrier its end-of-launch writes cannot reach a block that has not yet
-  // read them, however late that block was dispatched. Later barriers count
-  // only the blocks that held a job.
-  const unsigned m = y.n == 1 ? y.G : (unsigned)min((int)y.G, max(jobs, 0));
+  // only the blocks that held a job arrive (a block dispatched late never holds up a
+  // barrier it has no work before); block 0's end-of-launch writes are ordered behind every
+  // block's reads of the launch-start words by the entry counter instead (enter_launch /
+  // wait_entered; ADVICE r04's hazard)
+  const unsigned m = (unsigned)min((int)y.G, max(jobs, 0));
   y.target += m;
   if (threadIdx.x == 0 && blockIdx.x < m)
     __hip_atomic_fetch_add((gu32*)(y.cnt + kShardStride * (blockIdx.x % kShards)), 1u,
@@ -1231,6 +1273,8 @@ XA_DEV bool grid_sync(Sync& y, int& lds_flag, int jobs, const PreB& pb = no_preb
     int ok = 1;
     const uint64_t t0 = wall_clock64();
     for (unsigned it = 0;; ++it) {
+      // block 0 checks the entry counter while it waits anyway (same round trip)
+      if (y.ent && !y.ent_ok && entered_all(y)) y.ent_ok = 1;
       if ((int)(shard_sum(y.cnt) - y.target) >= 0) break;  // wrap-safe: the shards only grow
       if ((it & 15u) == 15u) {
         if (__hip_atomic_load((gu32*)y.abort_w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
@@ -1262,6 +1306,8 @@ struct Ws {
   unsigned* base;     // the shards' sum at the start of the next launch
   unsigned* abort_w;  // the epoch of a launch that timed out
   unsigned* epoch;    // launches so far
+  unsigned* ent;      // launch-entry counter: every block of every launch adds 1
+  unsigned* ent_base;  // the entry counter at the start of the next launch
   unsigned long long* dtrace;  // [16][8] points inside block 0's first job of each phase
   unsigned long long* trace;  // [16] wall clock at launch start and after every barrier
                               // (block 0; tools/td3_grad_steps.py reads it)
@@ -1307,6 +1353,8 @@ __host__ __device__ inline Ws carve(void* base_p, int B, int H1, int H2, int A) 
   w.abort_w = ctl + 288;
   w.epoch = ctl + 320;
   w.trace = (unsigned long long*)(ctl + 384);
+  w.ent = ctl + 448;       // byte 1792: the launch-entry counter (monotonic)
+  w.ent_base = ctl + 480;  // byte 1920: its value at the start of the next launch
   w.dtrace = (unsigned long long*)take(8192);
   w.h1s = align_up((size_t)B * H1, 64);
   w.h2s = align_up((size_t)B * H2, 64);
@@ -1358,6 +1406,9 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
   y.n = 0;
   y.status = p.status;
   y.trace = b == 0 ? ws.trace : nullptr;
+  y.ent = b == 0 && tid == 0 ? ws.ent : nullptr;
+  y.ent_target = *ws.ent_base + (unsigned)G;
+  y.ent_ok = 0;
   if (XA_TD3_TRACE && b == 0 && tid == 0) ws.trace[0] = wall_clock64();
   if (tid == 0) td3_bpre = 0;
 #if XA_TD3_TRACE
@@ -1376,7 +1427,7 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
   const int step_ac = pol ? *p.actor.step : 0;
   if (tid < p.batch) td3_slots[tid] = p.slots[tid];  // (batch <= 256)
   dstamp(1);
-  __syncthreads();
+  enter_launch(ws.ent);  // (the launch-start words are in registers; contains the barrier)
   dstamp(2);
   const Net tc1 = make_net(p.target_critic1, C, H1, H2, 1, false);
   const Net tc2 = make_net(twin ? p.target_critic2 : p.target_critic1, C, H1, H2, 1, false);
@@ -1660,9 +1711,6 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
   // ---- stage 2, P8': the critics' Keras Adam (+ Polyak of their targets on policy steps)
   // from the all-reduced gradients, every parameter in chunks that fill the grid ----
   if (stage == 2) {
-    // (a launch with no later barrier opens with one: every block reads the step counters
-    // before block 0 bumps them)
-    if (!pol && !grid_sync(y, s_flag, G)) return;
     c1.alpha = adam_alpha(p.critic1.lr, p.critic1.beta1, p.critic1.beta2, step_c1 + 1);
     if (twin) c2.alpha = adam_alpha(p.critic2.lr, p.critic2.beta1, p.critic2.beta2, step_c2 + 1);
     const int chunk = adam_chunk(c1.P, max(1, G / nt)), per = (c1.P + chunk - 1) / chunk;
@@ -1771,7 +1819,6 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
   // ---- stage 3: the actor's Keras Adam + Polyak of the target actor from the all-reduced
   // gradient (scaled: the ranks' -mean Q gradients are summed) ----
   if (stage == 3) {
-    if (!grid_sync(y, s_flag, G)) return;  // (every block has read the actor's step)
     ac.alpha = adam_alpha(p.actor.lr, p.actor.beta1, p.actor.beta2, step_ac + 1);
     const int chunk = adam_chunk(ac.P, G), per = (ac.P + chunk - 1) / chunk;
     for (int j = b; j < per; j += G) {
@@ -1782,10 +1829,11 @@ __global__ __launch_bounds__(256) void td3_update_kernel(XaTd3UpdateArgs p) {
     }
   }
 
-  // the step counters, the noise counter and the next launch's barrier base: every block
-  // read them before its first barrier, which block 0 has passed and which every block
-  // arrives at
+  // the step counters, the noise counter and the next launch's barrier base and entry
+  // base: written once every block of the launch has entered (read them)
   if (b == 0 && tid == 0) {
+    if (!wait_entered(y)) return;
+    *ws.ent_base = y.ent_target;
     if (stage == 0 || stage == 2) {
       *p.critic1.step += 1;
       if (twin) *p.critic2.step += 1;
@@ -1820,6 +1868,9 @@ __global__ __launch_bounds__(256) void td3_act_kernel(XaTd3ActArgs p) {
   y.n = 0;
   y.status = p.status;
   y.trace = nullptr;
+  y.ent = b == 0 && tid == 0 ? ws.ent : nullptr;
+  y.ent_target = *ws.ent_base + (unsigned)G;
+  y.ent_ok = 0;
   if (tid == 0) td3_bpre = 0;
 #if XA_TD3_TRACE
   if (tid == 0) {
@@ -1833,7 +1884,7 @@ __global__ __launch_bounds__(256) void td3_act_kernel(XaTd3ActArgs p) {
   const Net ac = make_net(d, S, H1, H2, A, false);
   const int RTT = (n + kTR - 1) / kTR;
   const int CT1 = (H1 + kCols - 1) / kCols, CT2 = (H2 + kCols - 1) / kCols;
-  __syncthreads();
+  enter_launch(ws.ent);
   for (int j = b; j < RTT * CT1; j += G) {
     const int rt = j / CT1, ct = j % CT1;
     fwd_job(xsrc(p.states, S, S, false, false), nullptr, rt * kTR, n, ac.th + ac.w1,
@@ -1867,6 +1918,8 @@ __global__ __launch_bounds__(256) void td3_act_kernel(XaTd3ActArgs p) {
     __syncthreads();
   }
   if (b == 0 && tid == 0) {
+    if (!wait_entered(y)) return;
+    *ws.ent_base = y.ent_target;
     if (p.bump && p.rng_counter) *p.rng_counter += 1ull;
     *ws.base = y.target;
     *ws.epoch = y.epoch;
