@@ -683,13 +683,13 @@ def bench_ppo(args, world, rank, device, n_envs, env='replay'):
     transport = agent.check_peer_all_reduce()
     if transport == 'rccl' and world > 1:
         agent.train_step()  # re-capture on RCCL after a peer-path fallback
+    agent.fused_train_steps(agent.graph_steps())  # (the multi-step graph's first replay)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        agent.fused_train_step()
+    agent.fused_train_steps(args.steps)  # (groups of graph_steps() per graph replay)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -721,6 +721,7 @@ def bench_ppo(args, world, rank, device, n_envs, env='replay'):
         'rollout_ms': float(np.mean([e[0].elapsed_time(e[1]) for e in events])),
         'update_ms': float(np.mean([e[1].elapsed_time(e[2]) for e in events])),
         'transport': transport, 'graph': bool(agent.use_graph and agent._graph is not None),
+        'graph_steps': getattr(agent, '_graph_S', 1) if agent._graph is not None else 0,
         'update_mode': agent.update_mode, 'record': record, 'theta0': theta0, 'agent': agent,
     }
     roll_ms = float(np.mean(ktimes['rollout']))
@@ -858,6 +859,7 @@ def main():
                 'ppo_epochs': 4,
                 'parallelism': f'dp{world}',
                 'graph': head['graph'],
+                'train_steps_per_graph_replay': head['graph_steps'],
                 'update': head['update_mode'],
                 'allreduce': head['transport'],
             },

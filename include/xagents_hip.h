@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define XA_ABI_VERSION 1
+#define XA_ABI_VERSION 2
 #define XA_MLP_HIDDEN 64
 
 /* environment kinds for the fused rollout */
@@ -317,6 +317,7 @@ int xa_clip_adam(float* theta, float* adam_m, float* adam_v, const float* grad, 
  * every optimizer step k and step k's reduced gradient (before the clip).
  */
 #define XA_PPO_DP_MAX 16
+#define XA_PPO_STATS_SLOTS 8 /* host slots of the in-launch episode statistics */
 #define XA_PPO_PLACE_AUTO 0   /* XCD-local when eligible; not for data-parallel launches */
 #define XA_PPO_PLACE_SPREAD 1 /* never XCD-local */
 #define XA_PPO_PLACE_LOCAL 2  /* XCD-local when eligible, data parallel included (every
@@ -360,13 +361,15 @@ typedef struct XaPpoUpdateArgs {
   /* episode statistics to the host inside the launch (replaces the xa_copy_to_host launch
    * of a train step): stats_words (> 0) 32-bit words of stats_src (device: the rollout's
    * done flags / running returns / this status word, as the caller packs them) are
-   * stored into stats_dst[g & 1] (device pointers of mapped pinned host buffers of
-   * stats_words + 1 words), g = the launch number kept in the workspace (0 for the first
-   * launch on a zeroed workspace), and word stats_words of that buffer receives g. The
-   * words are copied when the launch starts (the status word as the previous launches
-   * left it). stats_words = 0: nothing. */
+   * stored into stats_dst[g % XA_PPO_STATS_SLOTS] (device pointers of mapped pinned host
+   * buffers of stats_words + 1 words), g = the launch number kept in the workspace (0 for
+   * the first launch on a zeroed workspace), and word stats_words of that buffer receives
+   * g. The words are copied when the launch starts (the status word as the previous
+   * launches left it). stats_words = 0: nothing. The host may keep up to
+   * XA_PPO_STATS_SLOTS - 1 launches in flight before it folds the oldest slot (several
+   * train steps per hipGraph replay). */
   const void* stats_src;
-  void* stats_dst[2];
+  void* stats_dst[XA_PPO_STATS_SLOTS];
   int stats_words;
 } XaPpoUpdateArgs;
 
@@ -444,6 +447,16 @@ typedef struct XaAdamApply {
  * share of tape.gradient + Adam.apply_gradients (dqn/agent.py:170-171). */
 int xa_gemm_adam(const XaGemmArgs* args, const XaAdamApply* adam, void* stream);
 
+/* The backward of a row-dot-shaped head (the last Dense of the DQN / actor-critic cfgs, A <= 8
+ * outputs over K <= 4096 hidden units, utils/common.py:239-258) in ONE launch: its input
+ * gradient dx[m][k] = (sum_a dz[m][a] W[k][a]) * [gate[m][k] > 0] (xa_gemm's few-k path:
+ * the same k-order fmaf chain, so the same values; += when beta) and its [W; b] gradient
+ * gw[k][a] (+)= sum_m x[m][k] dz[m][a], gb[a] (+)= sum_m dz[m][a] (m-order fmaf chains; gw,
+ * gb = NULL: none). x, dz, dx rows of K / A / K floats (ld = K / A / K), W (K, A) in Keras
+ * layout, gate rows of K (NULL: none). */
+int xa_head_bwd(const float* x, const float* dz, const float* W, const float* gate, int M, int K,
+                int A, float* dx, int beta, float* gw, float* gb, int accumulate, void* stream);
+
 /* The NatureCNN convolution stack's forward in one launch (the three Conv1D layers of
  * the cnn .cfg models (xagents/dqn/models/cnn.cfg, the ppo / a2c / acer
  * cnn-actor-critic.cfg) as built by xagents/utils/common.py:225-240 over (84, 84, 1)
@@ -478,6 +491,18 @@ typedef struct XaConvStackBwdArgs {
   size_t ws_floats;
   float* grad;
   int accumulate;
+  /* optional, for an update without a gradient clip (DQN, dqn/agent.py:158-171): adam_on = 1
+   * applies Keras Adam (`adam`: theta / m / v / step of the stack's first parameter, t already
+   * bumped) to the stack's parameters inside the reduce launch, the raw gradient written to
+   * grad only when write_grad (accumulate must be 0); n_rest > 0 also applies Adam (`rest`)
+   * to n_rest more parameters whose gradient rest_grad is final when this launch runs (the
+   * Q head's): the xa_clip_adam launches of those ranges folded into the reduce */
+  int adam_on;
+  int write_grad;
+  XaAdamApply adam;
+  XaAdamApply rest;
+  const float* rest_grad;
+  int n_rest;
 } XaConvStackBwdArgs;
 size_t xa_conv_stack_bwd_workspace_floats(int rows);
 int xa_conv_stack_bwd(const XaConvStackBwdArgs* args, void* stream);
@@ -601,6 +626,19 @@ typedef struct XaDqnHeadArgs {
   int* adam_step;
 } XaDqnHeadArgs;
 int xa_dqn_head(const XaGemmArgs* head, const XaDqnHeadArgs* dqn, void* stream);
+
+/* A split-K dense layer and the row-dot head that reads its output (Keras Dense -> Dense,
+ * utils/common.py:239-258: the NatureCNN cfgs' 512-unit hidden layer and their Q head), with
+ * DQN's per-row step (dqn = NULL: the plain head; else xa_dqn_head's mode 0 / 1) -- the split
+ * partials as xa_gemm launches them, then ONE launch for the split reduce, the dense epilogue
+ * (its rows stored to dense->c), the head and the DQN step: the same values as xa_gemm(dense)
+ * followed by xa_gemm(head) / xa_dqn_head, bit for bit. Shapes xa_gemm_head_ok accepts (1):
+ * dense on xa_gemm's wide split reduce (M N <= 65536, >= 64 splits), N <= 512, no gate /
+ * beta; head a row-dot shape (xa_dqn_head's) with head->a == dense->c, lda = dense->ldc,
+ * K = dense N, the same M. */
+int xa_gemm_head(const XaGemmArgs* dense, const XaGemmArgs* head, const XaDqnHeadArgs* dqn,
+                 void* stream);
+int xa_gemm_head_ok(const XaGemmArgs* dense, const XaGemmArgs* head);
 
 /* Replay rings (ReplayBuffer1 xagents/utils/buffers.py:59-98, ReplayBuffer2 101-148):
  * ring[slots[i]] = src[i] / dst[i] = ring[slots[i]] for items of item_bytes. The host

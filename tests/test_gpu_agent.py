@@ -33,6 +33,81 @@ def test_graph_replay_equals_eager(device):
     assert a.steps == b.steps == 4 * 16 * 32
 
 
+@pytest.mark.parametrize('env', ['replay', 'dynamics'])
+def test_multi_step_graph_equals_single_steps(device, monkeypatch, env):
+    """fused_train_steps with XA_GRAPH_STEPS = 4 (four train steps per hipGraph replay, the
+    episode statistics of each in its own host slot, folded in groups) against single-step
+    replays: parameters, Adam state, rollout buffers and the episode bookkeeping
+    (total_rewards, games, the last dones) identical after 11 steps (two groups + three
+    single steps), on the replay env and on the CartPole-dynamics env (both with episode
+    ends inside the window)."""
+    from xagents_amd import PPO
+    from xagents_amd.envs import CartPoleVecEnv, ReplayVecEnv
+    from xagents_amd.utils.common import create_model
+
+    def make(steps_per_graph):
+        monkeypatch.setenv('XA_GRAPH_STEPS', str(steps_per_graph))
+        if env == 'replay':
+            envs = ReplayVecEnv('CartPole-v1', 16, t_rec=100, seed=5, device='cuda')
+        else:
+            envs = CartPoleVecEnv(16, seed=5, device='cuda')
+        model = create_model(envs, 'ppo', 'model', seed=5, device='cuda')
+        agent = PPO(envs, model, n_steps=32, seed=5, quiet=True)
+        agent.train_step()  # eager step + capture (with this XA_GRAPH_STEPS)
+        return agent
+
+    a, b = make(4), make(1)
+    assert a.update_mode == 'persistent' and a._graph_S == 4 and len(a._graph) == 4
+    assert b._graph_S == 1 and len(b._graph) == 3
+    a.fused_train_steps(11)
+    for _ in range(11):
+        b.fused_train_step()
+    for x in (a, b):
+        x._drain_episode_stats()
+    torch.cuda.synchronize()
+    assert a.steps == b.steps == 12 * 16 * 32
+    for name in ('theta', ):
+        np.testing.assert_array_equal(a.model.theta.cpu().numpy(), b.model.theta.cpu().numpy())
+    np.testing.assert_array_equal(a.model.optimizer.m.cpu().numpy(),
+                                  b.model.optimizer.m.cpu().numpy())
+    assert int(a.model.optimizer.iterations.item()) == int(b.model.optimizer.iterations.item())
+    for buf in ('b_act', 'b_logp', 'b_ret', 'b_done'):
+        np.testing.assert_array_equal(getattr(a, buf).cpu().numpy(), getattr(b, buf).cpu().numpy())
+    assert a.games == b.games > 0
+    assert list(a.total_rewards) == list(b.total_rewards)
+    assert a.dones == b.dones
+
+
+def test_replan_to_chain_keeps_episode_stats(device, monkeypatch):
+    """a re-plan from the persistent update (statistics stored by the update
+    launch) to the per-minibatch chain mid-run (what a peer timeout triggers) must fold
+    every step once. Agent a runs with the in-launch statistics, agent b with the copy-launch
+    path (XA_STATS_IN_UPDATE=0); both re-plan to the chain after 3 steps, so their parameters
+    and rollouts stay identical and so must the folded episode statistics."""
+    def make(in_update):
+        monkeypatch.setenv('XA_STATS_IN_UPDATE', '1' if in_update else '0')
+        return make_agent(n_envs=16, n_steps=32, seed=11, t_rec=60)
+
+    a, b = make(True), make(False)
+    assert a._stats_fused and not b._stats_fused
+    for x in (a, b):
+        for _ in range(3):
+            x.train_step()
+    monkeypatch.setenv('XA_PPO_UPDATE', 'chain')
+    for x in (a, b):
+        x._setup_update()
+        x._graph = None
+        assert x.update_mode == 'chain' and not x._stats_fused
+        for _ in range(3):
+            x.train_step()
+        x._drain_episode_stats()
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(a.model.theta.cpu().numpy(), b.model.theta.cpu().numpy())
+    assert a.games == b.games > 0
+    assert list(a.total_rewards) == list(b.total_rewards)
+    assert a.done_envs == b.done_envs
+
+
 def test_ppo_train_step_vs_oracle_pipeline(device):
     """One full train step: rollout buffers bit-exact vs the C oracle (same Philox
     stream), then 4 epochs x 4 minibatches against the float64 restatement of the

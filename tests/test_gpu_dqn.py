@@ -223,17 +223,19 @@ def test_fused_dense_adam_is_bit_identical(device, double):
 
 
 @pytest.mark.parametrize('double', [False, True])
-def test_fused_q_head_is_bit_identical(device, double):
-    """xa_dqn_head (argmax / TD target + gradient inside the Q head's row-dot launch)
+def test_fused_q_head_is_bit_identical(device, double, monkeypatch):
+    """xa_dqn_head (argmax / TD target + gradient inside the Q head's row-dot launch) and
+    xa_gemm_head (the 512-unit layer's split reduce + the head + that step in one launch)
     against the separate xa_gemm + xa_dqn_act / xa_dqn_td_grad launches: actions, the TD
     gradient and per-sample losses, parameters, moments and step counter bit-identical over
-    3 chained greedy train steps."""
+    3 chained greedy train steps, in every combination."""
     import random
     from xagents_amd import DQN
     from xagents_amd.envs import create_envs
     from xagents_amd.utils.common import create_buffers, create_model
     out = []
-    for fused in (False, True):
+    for fused, gemm_head in ((False, '0'), (True, '0'), (True, '1'), (False, '1')):
+        monkeypatch.setenv('XA_GEMM_HEAD', gemm_head)
         envs = create_envs('PongNoFrameskip-v4', 2, device=device, seed=4)
         model = create_model(envs, 'dqn', 'model', seed=5, device=device,
                              optimizer_kwargs=dict(learning_rate=1e-3))
@@ -244,6 +246,8 @@ def test_fused_q_head_is_bit_identical(device, double):
                     epsilon_end=0.0, gamma=0.99)
         agent.__dict__['_hf'] = fused
         assert agent._head_fused() == fused
+        for ex in (agent.ex_act, agent.ex_online, agent.ex_target):
+            assert (ex._fused_head_layer() is not None) == (gemm_head == '1')
         agent.fill_buffers()
         rec = []
         for _ in range(3):
@@ -254,5 +258,6 @@ def test_fused_q_head_is_bit_identical(device, double):
         torch.cuda.synchronize()
         opt = model.optimizer
         out.append([t.cpu().numpy() for t in rec + [model.theta, opt.m, opt.v, opt.iterations]])
-    for x, y in zip(*out):
-        np.testing.assert_array_equal(x, y)
+    for other in out[1:]:
+        for x, y in zip(out[0], other):
+            np.testing.assert_array_equal(x, y)

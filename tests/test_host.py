@@ -195,7 +195,7 @@ def test_library_exports_every_header_symbol():
     lib = _lib.load()  # no compute calls without a GPU
     for name in declared:
         assert hasattr(lib, name), name
-    assert lib.xa_abi_version() == 1
+    assert lib.xa_abi_version() == 2
     assert lib.xa_mlp_param_count(4, 2) == 4675 == oracle.lib().xo_mlp_param_count(4, 2)
     assert lib.xa_ac_grad_blocks(8192) == 256 and lib.xa_ac_grad_blocks(100) == 4
     assert lib.xa_ppo_adv_stats_size(32768, 8192, 4) == 2 * 4 * 4 * 8

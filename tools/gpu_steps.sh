@@ -160,6 +160,18 @@ for step in "$@"; do
       XA_BENCH_SHARED_DEVICE=1 HSA_ENABLE_IPC_MODE_LEGACY=0 run c4w2 400 python -m torch.distributed.run \
         --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py \
         --config c4 --gpus 2 --steps 2 --warmup 1 --cpu-baseline-seconds 0 ;;
+    gsab)
+      # train steps per graph replay (XA_GRAPH_STEPS) and events per statistics group
+      # (XA_STATS_EVERY), interleaved bench lines (headline + C2, no secondaries)
+      B="python bench.py --steps 40 --warmup 5 --cpu-baseline-seconds 0 --no-secondary --no-dynamics"
+      run gs1a 200 $B
+      XA_GRAPH_STEPS=4 run gs4a 200 $B
+      XA_STATS_EVERY=4 run se4a 200 $B
+      run gs1b 200 $B
+      XA_GRAPH_STEPS=4 run gs4b 200 $B
+      XA_GRAPH_STEPS=2 run gs2b 200 $B
+      python tools/bench_brief.py gpurun_out/${T}_gs*.out gpurun_out/${T}_se*.out ;;
+    agent) run_pytest agent 300 tests/test_gpu_agent.py ;;
     tl16)
       # kernel trace of the 16-env headline alone: the per-step timeline (idle gaps between
       # the rollout and update launches, and between train steps)

@@ -27,6 +27,7 @@ MLP_HIDDEN = 64
 XA_PPO_PLACE_AUTO = 0
 XA_PPO_PLACE_SPREAD = 1
 XA_PPO_PLACE_LOCAL = 2
+XA_PPO_STATS_SLOTS = 8  # host slots of the persistent update's in-launch statistics
 
 
 class XaRolloutArgs(Structure):
@@ -157,7 +158,8 @@ class XaPpoUpdateArgs(Structure):
         ('dp_blocks', c_void_p * 16),
         ('placement', c_int),
         ('theta_trace', c_void_p), ('grad_trace', c_void_p),
-        ('stats_src', c_void_p), ('stats_dst', c_void_p * 2), ('stats_words', c_int),
+        ('stats_src', c_void_p), ('stats_dst', c_void_p * XA_PPO_STATS_SLOTS),
+        ('stats_words', c_int),
     ]
 
 
@@ -221,6 +223,8 @@ class XaConvStackBwdArgs(Structure):
         ('w2', c_void_p), ('w3', c_void_p),
         ('h1', c_void_p), ('h2', c_void_p), ('dz3', c_void_p),
         ('ws', c_void_p), ('ws_floats', ctypes.c_size_t), ('grad', c_void_p), ('accumulate', c_int),
+        ('adam_on', c_int), ('write_grad', c_int), ('adam', XaAdamApply), ('rest', XaAdamApply),
+        ('rest_grad', c_void_p), ('n_rest', c_int),
     ]
 
 
@@ -438,6 +442,11 @@ _SIGNATURES = {
     'xa_gemm_adam': (c_int, [POINTER(XaGemmArgs), POINTER(XaAdamApply), c_void_p]),
     'xa_conv_stack_fwd': (c_int, [POINTER(XaConvStackArgs), c_void_p]),
     'xa_dqn_head': (c_int, [POINTER(XaGemmArgs), POINTER(XaDqnHeadArgs), c_void_p]),
+    'xa_gemm_head': (c_int, [POINTER(XaGemmArgs), POINTER(XaGemmArgs), POINTER(XaDqnHeadArgs),
+                             c_void_p]),
+    'xa_gemm_head_ok': (c_int, [POINTER(XaGemmArgs), POINTER(XaGemmArgs)]),
+    'xa_head_bwd': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
+                            c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p]),
     'xa_conv_stack_bwd': (c_int, [POINTER(XaConvStackBwdArgs), c_void_p]),
     'xa_conv_stack_bwd_workspace_floats': (ctypes.c_size_t, [c_int]),
     'xa_gemm_splits': (c_int, [c_int, c_int, c_int]),

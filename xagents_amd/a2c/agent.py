@@ -336,10 +336,18 @@ class A2C(ExecutorActorCritic, OnPolicy):
         ok = True
         try:
             graphs = []
-            # rollout, update, and both back to back: the timed loop replays the third (one
-            # graph launch per train step), the per-phase event pass the first two
-            for fns in ((self._rollout_impl,), (self._update_impl,),
-                        (self._rollout_impl, self._update_impl)):
+            # rollout, update, and both back to back: a train step replays the third (one
+            # graph launch per train step), the per-phase event pass the first two; with the
+            # persistent update (every exchange and the statistics copy inside its launch)
+            # a fourth graph holds graph_steps() train steps back to back
+            # (fused_train_steps: one replay per group of steps)
+            seqs = [(self._rollout_impl,), (self._update_impl,),
+                    (self._rollout_impl, self._update_impl)]
+            S = self.graph_steps()
+            if S > 1:
+                seqs.append((self._rollout_impl, self._update_impl) * S)
+            self._graph_S = S
+            for fns in seqs:
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
                     for fn in fns:
@@ -410,6 +418,37 @@ class A2C(ExecutorActorCritic, OnPolicy):
         self._queue_episode_stats(self.b_done, self.b_epret,
                                   after=self._rollout_ev if self.stats_side_stream else None)
         self._maybe_check_peer()
+
+    def graph_steps(self):
+        """Train steps per replay of the multi-step graph (XA_GRAPH_STEPS, at most
+        BaseAgent.FUSED_GROUP_MAX; 1 = none): only with the persistent update, whose launch
+        stores each step's episode statistics into a host slot of its own."""
+        if self.executor_path or getattr(self, 'update_mode', None) != 'persistent' or \
+                not getattr(self, '_stats_fused', False) or self.stats_side_stream:
+            return 1
+        return max(1, min(int(os.environ.get('XA_GRAPH_STEPS', '4')), self.FUSED_GROUP_MAX))
+
+    def fused_train_steps(self, n):
+        """n train steps: groups of graph_steps() steps as one replay of the multi-step
+        hipGraph (the kernel sequence of the single-step replays back to back, so the same
+        arithmetic; one graph launch and one completion event per group), the rest one
+        step at a time. The host bookkeeping of every step (step count, statistics fold,
+        peer health check) runs after its group."""
+        while n > 0:
+            g = self._graph if self.use_graph else None
+            S = self._graph_S if g is not None and len(g) > 3 else 1
+            if S <= 1 or n < S:
+                self.fused_train_step()
+                n -= 1
+                continue
+            self._sync_stats_copy()
+            g[3].replay()
+            for i in range(S):
+                self._count_update_replay()
+                self.steps += self.n_envs * self.n_steps
+                self._queue_episode_stats(self.b_done, self.b_epret, group_end=i == S - 1)
+                self._maybe_check_peer()
+            n -= S
 
     def _count_update_replay(self):
         """A graph replay that ran the persistent update: one more launch number (the

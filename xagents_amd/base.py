@@ -396,14 +396,18 @@ class BaseAgent(ABC):
         return concatenated
 
     # ---- device episode bookkeeping ----------------------------------------
-    def _queue_episode_stats(self, done_out, epret_out, after=None):
+    def _queue_episode_stats(self, done_out, epret_out, after=None, group_end=True):
         """Async D2H copy of one rollout's done flags [N,T+1] and running returns [N,T]
         (with the persistent update's status word). `after`: an event recorded on the
         launch stream right after the rollout -- the copy then runs on a side stream
         behind it, overlapping the update, and the next rollout waits for it
         (_sync_stats_copy). When the persistent update stores the statistics into its host
         slots itself (PPO._setup_fused_stats) there is nothing to launch: the step's slot is
-        its launch number's parity, and the fold checks the number the launch wrote."""
+        its launch number modulo XA_PPO_STATS_SLOTS, and the fold checks the number the
+        launch wrote. Steps are folded in groups behind one completion event (`group_end`:
+        the caller closes a group, e.g. after a hipGraph replay of several train steps;
+        XA_STATS_EVERY groups single steps), at most half the slots per group, so that a
+        slot is folded before a later launch reuses it."""
         if getattr(self, '_stats_fused', False) and after is None and \
                 getattr(self, 'update_mode', None) == 'persistent' and \
                 done_out.data_ptr() == self.b_done.data_ptr():
@@ -412,14 +416,15 @@ class BaseAgent(ABC):
                 self._drain_episode_stats()
                 self._stats_queue = []
                 self._stats_queue_kind = 'fused'
-                self._fused_events = [torch.cuda.Event(), torch.cuda.Event()]
-            gen = self._upd_launches - 1
-            ev = self._fused_events[gen & 1]
-            ev.record()
-            self._stats_queue.append((gen & 1, ev, gen))
+                self._fused_events = [torch.cuda.Event() for _ in range(4)]
+                self._fused_ev_i = 0
+                self._fused_pending = []
+            self._fused_pending.append(self._upd_launches - 1)
             self._pending_stats = (done_out, epret_out)
-            while len(self._stats_queue) > 1:
-                self._fold_stats(*self._stats_queue.pop(0))
+            every = min(int(os.environ.get('XA_STATS_EVERY', '1')), self.FUSED_GROUP_MAX)
+            if group_end and len(self._fused_pending) >= every or \
+                    len(self._fused_pending) >= self.FUSED_GROUP_MAX:
+                self._close_fused_group()
             return
         if self._pending_stats is None or self._pending_stats[0].shape != done_out.shape or \
                 getattr(self, '_stats_queue_kind', None) == 'fused':
@@ -491,7 +496,32 @@ class BaseAgent(ABC):
         self._pending_stats = (done_out, epret_out)
         # keep at most one rollout in flight: fold the previous one now
         while len(self._stats_queue) > 1:
-            self._fold_stats(*self._stats_queue.pop(0))
+            self._fold_item(self._stats_queue.pop(0))
+
+    # steps folded behind one event: half the in-launch statistics slots (_lib.XA_PPO_STATS_SLOTS)
+    FUSED_GROUP_MAX = 4
+
+    def _close_fused_group(self):
+        """One completion event behind the pending fused steps; fold the previous group
+        (its slots are complete once its event is), so one group stays in flight."""
+        if not getattr(self, '_fused_pending', None):
+            return
+        ev = self._fused_events[self._fused_ev_i % len(self._fused_events)]
+        self._fused_ev_i += 1
+        ev.record()
+        self._stats_queue.append(('fused', ev, tuple(self._fused_pending)))
+        self._fused_pending = []
+        while len(self._stats_queue) > 1:
+            self._fold_item(self._stats_queue.pop(0))
+
+    def _fold_item(self, item):
+        if item[0] == 'fused':
+            _, ev, gens = item
+            ev.synchronize()
+            for gen in gens:
+                self._fold_stats(None, None, gen)
+        else:
+            self._fold_stats(*item)
 
     def _copy_to_host(self, segs):
         """(device, pinned host) tensor pairs to the host in ONE xa_copy_to_host launch on
@@ -527,7 +557,11 @@ class BaseAgent(ABC):
             self._stats_guard = None
 
     def _fold_stats(self, slot, ev, gen=None):
-        ev.synchronize()
+        if ev is not None:
+            ev.synchronize()
+        if gen is not None:
+            from xagents_amd._lib import XA_PPO_STATS_SLOTS
+            slot = gen % XA_PPO_STATS_SLOTS
         if gen is None:
             host_done, host_epret, host_status = (self._host_done[slot], self._host_epret[slot],
                                                   getattr(self, '_host_status', None))
@@ -569,8 +603,10 @@ class BaseAgent(ABC):
         self.dones = [bool(d) for d in done[:, -1]]
 
     def _drain_episode_stats(self):
+        if getattr(self, '_fused_pending', None):
+            self._close_fused_group()
         while getattr(self, '_stats_queue', None):
-            self._fold_stats(*self._stats_queue.pop(0))
+            self._fold_item(self._stats_queue.pop(0))
         # a side-stream copy reads the status word before the step's update ends: the
         # last update's status is read here
         status = getattr(self, 'device_status', None)

@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 
 #include "../../include/xagents_hip.h"
+#include "xa_adam.hpp"
 #include "xa_common.hpp"
 
 namespace {
@@ -562,10 +563,33 @@ __global__ __launch_bounds__(512) void conv_stack_bwd8_kernel(XaConvStackBwdArgs
 
 // grad[e] (+)= sum over workgroups z of ws[z][e]: 4 waves per 64 elements, wave v sums the
 // z slice [v nz / 4, (v + 1) nz / 4) in order, the slices combined in order
+// (+ optionally Keras Adam on those parameters and on a second range whose gradient is already
+// final: blocks past the reduce's take that range, one element per thread -- xa_clip_adam's
+// element arithmetic with no clip, so the same values as the separate launches)
 __global__ __launch_bounds__(256) void conv_stack_bwd_reduce_kernel(const float* __restrict__ ws,
-                                                                    int nz, float* __restrict__ grad,
-                                                                    int accumulate) {
+                                                                    int nz, XaConvStackBwdArgs p) {
   __shared__ float part[4][64];
+  __shared__ float s_alpha;
+  constexpr int kMain = (NPAR + 63) / 64;
+  if (p.adam_on && threadIdx.x == 0) {
+    const XaAdamApply& ad = (int)blockIdx.x < kMain ? p.adam : p.rest;
+    s_alpha = adam_alpha(ad.lr, ad.beta1, ad.beta2, *ad.step);
+  }
+  if ((int)blockIdx.x >= kMain) {  // the second Adam range
+    __syncthreads();
+    const XaAdamApply& ad = p.rest;
+    const int i = ((int)blockIdx.x - kMain) * 256 + (int)threadIdx.x;
+    if (i < p.n_rest) {
+      float th = ad.theta[i], mm = ad.m[i], vv = ad.v[i];
+      adam_elem((p.rest_grad[i] * ad.grad_scale) * 1.0f, th, mm, vv, s_alpha, 1.0f - ad.beta1,
+                1.0f - ad.beta2, ad.eps);
+      ad.theta[i] = th;
+      ad.m[i] = mm;
+      ad.v[i] = vv;
+    }
+    return;
+  }
+  float* __restrict__ grad = p.grad;
   const int lane = threadIdx.x & 63, v = threadIdx.x >> 6, e = blockIdx.x * 64 + lane;
   const int z0 = v * nz / 4, z1 = (v + 1) * nz / 4;
   float s = 0.0f;
@@ -584,7 +608,18 @@ __global__ __launch_bounds__(256) void conv_stack_bwd_reduce_kernel(const float*
   __syncthreads();
   if (v == 0 && e < NPAR) {
     const float t = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
-    grad[e] = accumulate ? grad[e] + t : t;
+    if (!p.adam_on) {
+      grad[e] = p.accumulate ? grad[e] + t : t;
+    } else {
+      if (p.write_grad) grad[e] = t;
+      const XaAdamApply& ad = p.adam;
+      float th = ad.theta[e], mm = ad.m[e], vv = ad.v[e];
+      adam_elem((t * ad.grad_scale) * 1.0f, th, mm, vv, s_alpha, 1.0f - ad.beta1,
+                1.0f - ad.beta2, ad.eps);
+      ad.theta[e] = th;
+      ad.m[e] = mm;
+      ad.v[e] = vv;
+    }
   }
 }
 
@@ -625,8 +660,15 @@ extern "C" size_t xa_conv_stack_bwd_workspace_floats(int rows) {
 extern "C" int xa_conv_stack_bwd(const XaConvStackBwdArgs* a, void* stream) {
   XA_CHECK_ARG(a != nullptr, "xa_conv_stack_bwd: null args");
   const XaConvStackBwdArgs& p = *a;
-  XA_CHECK_ARG(p.x && p.w2 && p.w3 && p.h1 && p.h2 && p.dz3 && p.ws && p.grad && p.rows > 0,
+  XA_CHECK_ARG(p.x && p.w2 && p.w3 && p.h1 && p.h2 && p.dz3 && p.ws && p.rows > 0 &&
+                   (p.grad || (p.adam_on && !p.write_grad)),
                "xa_conv_stack_bwd: null operand or rows <= 0");
+  XA_CHECK_ARG(!p.adam_on || (!p.accumulate && p.adam.theta && p.adam.m && p.adam.v &&
+                              p.adam.step && (p.n_rest <= 0 || (p.rest.theta && p.rest.m &&
+                                                                p.rest.v && p.rest.step &&
+                                                                p.rest_grad))),
+               "xa_conv_stack_bwd: adam_on needs accumulate 0 and the Adam pointers (and the "
+               "rest range's with n_rest > 0)");
   XA_CHECK_ARG(((uintptr_t)p.x & (p.x_u8 ? 3 : 15)) == 0 &&
                    (((uintptr_t)p.h1 | (uintptr_t)p.h2 | (uintptr_t)p.dz3) & 15) == 0,
                "xa_conv_stack_bwd: x, h1, h2, dz3 misaligned");
@@ -637,8 +679,9 @@ extern "C" int xa_conv_stack_bwd(const XaConvStackBwdArgs* a, void* stream) {
   const int grid = G < cu_count() ? G : cu_count();
   hipLaunchKernelGGL(conv_stack_bwd8_kernel, dim3(grid), dim3(512), 0, (hipStream_t)stream, p);
   XA_CHECK_LAUNCH("xa_conv_stack_bwd");
-  hipLaunchKernelGGL(conv_stack_bwd_reduce_kernel, dim3((NPAR + 63) / 64), dim3(256), 0,
-                     (hipStream_t)stream, p.ws, grid, p.grad, p.accumulate);
+  const int rest_blocks = p.adam_on && p.n_rest > 0 ? (p.n_rest + 255) / 256 : 0;
+  hipLaunchKernelGGL(conv_stack_bwd_reduce_kernel, dim3((NPAR + 63) / 64 + rest_blocks), dim3(256),
+                     0, (hipStream_t)stream, p.ws, grid, p);
   XA_CHECK_LAUNCH("xa_conv_stack_bwd (reduce)");
   return 0;
 }

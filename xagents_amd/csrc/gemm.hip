@@ -756,6 +756,8 @@ __global__ __launch_bounds__(256) void gemm_rowdot_kernel(XaGemmArgs g) {
 // mode 1 (TD, dqn/agent.py:118-171): the head is the TARGET network's, row b = sample b:
 // exactly xa_dqn_td_grad's arithmetic (offpolicy.hip dqn_td_kernel) with Qt(s') taken from
 // the lanes instead of memory; the optimizer step bump rides along
+XA_DEV void dqn_row_step(const XaGemmArgs& g, const XaDqnHeadArgs& d, int m, int lane, float v);
+
 __global__ __launch_bounds__(256) void dqn_head_kernel(XaGemmArgs g, XaDqnHeadArgs d) {
   const int lane = threadIdx.x & 63;
   const int m = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -763,6 +765,11 @@ __global__ __launch_bounds__(256) void dqn_head_kernel(XaGemmArgs g, XaDqnHeadAr
   if (m >= g.M) return;
   const float v = rowdot_row(g, m, lane);
   if (lane < g.N) store_c(v, m, lane, g);
+  dqn_row_step(g, d, m, lane, v);
+}
+
+// the per-row DQN step after the head's row-dot (lane n < A holds Q[m][n])
+XA_DEV void dqn_row_step(const XaGemmArgs& g, const XaDqnHeadArgs& d, int m, int lane, float v) {
   const int A = g.N;
   float qv[RD_MAXN];
 #pragma unroll
@@ -817,6 +824,143 @@ __global__ __launch_bounds__(256) void dqn_head_kernel(XaGemmArgs g, XaDqnHeadAr
   }
   if (lane < A) d.dq[(int64_t)b * A + lane] = lane == ab ? dqa : 0.0f;
   if (lane == 0 && d.loss) d.loss[b] = l;
+}
+
+// A dense layer's split-K reduce and the row-dot head that reads it (the NatureCNN Q head over
+// the 512 hidden units), with DQN's per-row step when asked, in ONE launch instead of two
+// (xa_gemm's wide split reduce, then xa_gemm's row-dot / xa_dqn_head): one 1024-thread
+// workgroup per row m. Stage 1 sums every output of the row exactly as
+// gemm_split_reduce_wide_kernel does (wave w: the contiguous split piece w, in split order;
+// the 16 pieces combined in wave order; the dense epilogue), with every load of a row's piece
+// in flight at once, and stores the row (the backward's operand); stage 2 runs rowdot_row's
+// arithmetic on the row from LDS and dqn_head_kernel's per-row step: bit-identical to the two
+// launches.
+constexpr int DH_NCH = 8;  // 64-output chunks per row: dense N <= 512
+
+XA_DEV float rowdot_lds(const XaGemmArgs& g, const float* arow, int lane) {
+  float acc[RD_MAXN];
+#pragma unroll
+  for (int n = 0; n < RD_MAXN; ++n) acc[n] = 0.0f;
+  constexpr int RD_U = 8;  // (rowdot_row's pass structure and order)
+  for (int k0 = lane; k0 < g.K; k0 += 64 * RD_U) {
+    float av[RD_U], wv[RD_U][RD_MAXN];
+#pragma unroll
+    for (int u = 0; u < RD_U; ++u) {
+      const int k = k0 + 64 * u;
+      const bool in = k < g.K;
+      av[u] = in ? arow[k] : 0.0f;
+      const float* w = g.b + (int64_t)(in ? k : 0) * g.b_ks;
+#pragma unroll
+      for (int n = 0; n < RD_MAXN; ++n)
+        wv[u][n] = (in && n < g.N) ? w[(int64_t)n * g.b_ns] : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < RD_U; ++u)
+#pragma unroll
+      for (int n = 0; n < RD_MAXN; ++n) acc[n] = fmaf(av[u], wv[u][n], acc[n]);
+  }
+  float v = 0.0f;
+#pragma unroll
+  for (int n = 0; n < RD_MAXN; ++n) {
+    float t = acc[n];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off);
+    if (lane == n) v = t;
+  }
+  return lane < g.N ? epilogue(v, lane, g) : 0.0f;
+}
+
+__global__ __launch_bounds__(1024) void dense_head_kernel(XaGemmArgs dn, int splits, XaGemmArgs hd,
+                                                          XaDqnHeadArgs q, int mode) {
+  __shared__ float part[16][64 * DH_NCH];
+  __shared__ float hrow[64 * DH_NCH];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int m = blockIdx.x;
+  const int N = dn.N;
+  const int64_t total = (int64_t)dn.M * N;
+  const int per = (splits + 15) / 16;
+  const int z0 = w * per, z1 = min(splits, z0 + per);
+  const float* src = dn.partials + (int64_t)m * N + lane;
+  float acc[DH_NCH];
+#pragma unroll
+  for (int c = 0; c < DH_NCH; ++c) acc[c] = 0.0f;
+  for (int z = z0; z < z1; z += 8) {
+    float v[DH_NCH][8];
+#pragma unroll
+    for (int c = 0; c < DH_NCH; ++c)
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        v[c][u] = (z + u < z1 && 64 * c + lane < N) ? src[(int64_t)(z + u) * total + 64 * c] : 0.0f;
+#pragma unroll
+    for (int c = 0; c < DH_NCH; ++c)
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (z + u < z1) acc[c] = acc[c] + v[c][u];
+  }
+#pragma unroll
+  for (int c = 0; c < DH_NCH; ++c) part[w][64 * c + lane] = acc[c];
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t < N) {
+    float s = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s = s + part[i][t];
+    const float h = epilogue(s, t, dn);
+    store_c(h, m, t, dn);
+    hrow[t] = h;
+  }
+  __syncthreads();
+  if (w != 0) return;
+  if (mode == 1 && q.adam_step && m == 0 && lane == 0) q.adam_step[0] += 1;
+  const float v = rowdot_lds(hd, hrow, lane);
+  if (lane < hd.N) store_c(v, m, lane, hd);
+  if (mode >= 0) dqn_row_step(hd, q, m, lane, v);
+}
+
+constexpr int SK_MAXK_H = 8;  // (the head width bound of xa_head_bwd, as SK_MAXK)
+
+// A row-dot head's backward in one launch (xa_head_bwd): blocks [0, nbx) the input gradient
+// (one thread per (m, k): gemm_smallk_kernel's arithmetic), the rest the [W; b] gradient (one
+// thread per (k, a) of K + 1 rows, k fastest so a row m of x is read coalesced; m-order fmaf)
+struct HeadBwd {
+  const float *x, *dz, *W, *gate;
+  int M, K, A;
+  float* dx;
+  int beta;
+  float *gw, *gb;
+  int accumulate, nbx;
+};
+
+__global__ __launch_bounds__(256) void head_bwd_kernel(HeadBwd h) {
+  if ((int)blockIdx.x < h.nbx) {
+    const int64_t e = blockIdx.x * 256ll + threadIdx.x;
+    if (e >= (int64_t)h.M * h.K) return;
+    const int m = (int)(e / h.K), k = (int)(e - (int64_t)m * h.K);
+    const float* a = h.dz + (int64_t)m * h.A;
+    const float* b = h.W + (int64_t)k * h.A;
+    float v = 0.0f;
+#pragma unroll
+    for (int j = 0; j < SK_MAXK_H; ++j)
+      if (j < h.A) v = fmaf(a[j], b[j], v);
+    if (h.gate && !(h.gate[e] > 0.0f)) v = 0.0f;
+    h.dx[e] = h.beta ? h.dx[e] + v : v;
+    return;
+  }
+  const int o = ((int)blockIdx.x - h.nbx) * 256 + (int)threadIdx.x;  // (row r, a), r fastest
+  const int rows = h.K + 1;
+  if (o >= rows * h.A) return;
+  const int a = o / rows, r = o - a * rows;
+  float acc = 0.0f;
+  if (r < h.K) {
+    for (int m = 0; m < h.M; ++m) acc = fmaf(h.x[(int64_t)m * h.K + r], h.dz[(int64_t)m * h.A + a], acc);
+    if (h.gw) {
+      float* p = h.gw + (int64_t)r * h.A + a;
+      *p = h.accumulate ? *p + acc : acc;
+    }
+  } else {
+    for (int m = 0; m < h.M; ++m) acc = acc + h.dz[(int64_t)m * h.A + a];
+    if (h.gb) h.gb[a] = h.accumulate ? h.gb[a] + acc : acc;
+  }
 }
 
 // Few-k GEMM (K <= 8: the network heads' input gradient dZ W^T, K = the head width): one
@@ -1573,6 +1717,9 @@ extern "C" int xa_gemm_adam(const XaGemmArgs* p, const XaAdamApply* ad, void* st
   return 0;
 }
 
+static bool wide_reduce(const XaGemmArgs& g);
+static void launch_main(const XaGemmArgs& g, hipStream_t s);
+
 extern "C" int xa_gemm(const XaGemmArgs* p, void* stream) {
   XA_CHECK_ARG(p != nullptr, "xa_gemm: null args");
   const XaGemmArgs& g = *p;
@@ -1615,6 +1762,36 @@ extern "C" int xa_gemm(const XaGemmArgs* p, void* stream) {
     XA_CHECK_LAUNCH("xa_gemm (row dot)");
     return 0;
   }
+  XA_CHECK_ARG(!g.a_ones_row || ((g.force_small == 1 ||
+                                   pick_shape(g.M, g.N, g.K, (g.K + g.splits - 1) / g.splits,
+                                              g.a == nullptr) == 0) &&
+                                  g.a != nullptr && g.M >= 2),
+               "xa_gemm: a_ones_row needs the 64 x 64 kernel (xa_gemm_shape == 0), A and M >= 2");
+  launch_main(g, s);
+  XA_CHECK_LAUNCH("xa_gemm");
+  if (g.splits > 1) {
+    const int64_t total = (int64_t)g.M * g.N;
+    if (wide_reduce(g)) {
+      hipLaunchKernelGGL(gemm_split_reduce_wide_kernel, dim3((int)((total + 63) / 64)),
+                         dim3(1024), 0, s, g, g.splits);
+    } else {
+      const int64_t want = (total + 255) / 256;
+      const int blocks = (int)(want < 4096 ? want : 4096);
+      hipLaunchKernelGGL(gemm_split_reduce_kernel, dim3(blocks), dim3(256), 0, s, g, g.splits);
+    }
+    XA_CHECK_LAUNCH("xa_gemm (split reduce)");
+  }
+  return 0;
+}
+
+// the split-reduce form xa_gemm takes: lane-per-output over 16 contiguous split pieces
+static bool wide_reduce(const XaGemmArgs& g) {
+  return (int64_t)g.M * g.N <= 65536 && g.splits >= 64;
+}
+
+// the main GEMM launch of xa_gemm's tile / stream / skinny / colsum paths (the split partials
+// when g.splits > 1)
+static void launch_main(const XaGemmArgs& g, hipStream_t s) {
   dim3 grid((g.M + BM - 1) / BM, (g.N + BN - 1) / BN, g.splits);
   const bool use_stream = stream_ok(g);
   const bool ak = g.a_pk == 1 && g.a_rk == 1;
@@ -1622,9 +1799,6 @@ extern "C" int xa_gemm(const XaGemmArgs* p, void* stream) {
   const bool u8 = g.a_u8 != 0;
   const int per_split = (g.K + g.splits - 1) / g.splits;
   const int shape = g.force_small == 1 ? 0 : pick_shape(g.M, g.N, g.K, per_split, g.a == nullptr);
-  XA_CHECK_ARG(!g.a_ones_row || (shape == 0 && g.a != nullptr && g.M >= 2),
-               "xa_gemm: a_ones_row needs the 64 x 64 kernel (xa_gemm_shape == 0), A and M >= 2 "
-               "(got shape %d, M %d)", shape, g.M);
   const XaGemmK kg = kernel_args(g);
   if (use_stream) {
     const dim3 gs(g.splits, g.N / ST_NCOL);
@@ -1654,20 +1828,6 @@ extern "C" int xa_gemm(const XaGemmArgs* p, void* stream) {
     else if (bn) launch<false, true, false>(kg, grid, s);
     else launch<false, false, false>(kg, grid, s);
   }
-  XA_CHECK_LAUNCH("xa_gemm");
-  if (g.splits > 1) {
-    const int64_t total = (int64_t)g.M * g.N;
-    if (total <= 65536 && g.splits >= 64) {
-      hipLaunchKernelGGL(gemm_split_reduce_wide_kernel, dim3((int)((total + 63) / 64)),
-                         dim3(1024), 0, s, g, g.splits);
-    } else {
-      const int64_t want = (total + 255) / 256;
-      const int blocks = (int)(want < 4096 ? want : 4096);
-      hipLaunchKernelGGL(gemm_split_reduce_kernel, dim3(blocks), dim3(256), 0, s, g, g.splits);
-    }
-    XA_CHECK_LAUNCH("xa_gemm (split reduce)");
-  }
-  return 0;
 }
 
 
@@ -1682,6 +1842,57 @@ extern "C" int xa_dqn_head(const XaGemmArgs* p, const XaDqnHeadArgs* d, void* st
                "xa_dqn_head: mode 0 needs actions, mode 1 q / act / rewards / dones / dq");
   hipLaunchKernelGGL(dqn_head_kernel, dim3((g.M + 3) / 4), dim3(256), 0, (hipStream_t)stream, g, *d);
   XA_CHECK_LAUNCH("xa_dqn_head");
+  return 0;
+}
+
+extern "C" int xa_gemm_head(const XaGemmArgs* dp, const XaGemmArgs* hp, const XaDqnHeadArgs* q,
+                            void* stream) {
+  XA_CHECK_ARG(dp != nullptr && hp != nullptr, "xa_gemm_head: null args");
+  const XaGemmArgs& d = *dp;
+  const XaGemmArgs& h = *hp;
+  XA_CHECK_ARG(xa_gemm_head_ok(dp, hp) == 1,
+               "xa_gemm_head: needs a split-K dense layer on the wide reduce (M N <= 65536, >= 64 "
+               "splits, N <= %d, no gate / beta) and a row-dot head on its output rows (M equal, "
+               "K = the dense N, A = the dense C, no gate / beta)", 64 * DH_NCH);
+  XA_CHECK_ARG(q == nullptr || (q->mode == 0 ? q->actions != nullptr
+                                             : (q->mode == 1 && q->q && q->act && q->rewards &&
+                                                q->dones && q->dq)),
+               "xa_gemm_head: mode 0 needs actions, mode 1 q / act / rewards / dones / dq");
+  hipStream_t s = (hipStream_t)stream;
+  launch_main(d, s);
+  XA_CHECK_LAUNCH("xa_gemm_head (split partials)");
+  XaDqnHeadArgs qq{};
+  if (q) qq = *q;
+  hipLaunchKernelGGL(dense_head_kernel, dim3(d.M), dim3(1024), 0, s, d, d.splits, h, qq,
+                     q ? q->mode : -1);
+  XA_CHECK_LAUNCH("xa_gemm_head (reduce + head)");
+  return 0;
+}
+
+extern "C" int xa_gemm_head_ok(const XaGemmArgs* dp, const XaGemmArgs* hp) {
+  if (!dp || !hp) return 0;
+  const XaGemmArgs& d = *dp;
+  const XaGemmArgs& h = *hp;
+  const bool dense = d.M > 0 && d.N > 0 && d.K > 0 && d.b && d.c && d.a_pm > 0 && d.a_pk > 0 &&
+                     d.splits > 1 && d.splits <= 4096 && d.partials && wide_reduce(d) &&
+                     d.N <= 64 * DH_NCH && !d.gate && !d.beta && !d.a_ones_row &&
+                     !smallm_res_ok(d) && !smallk_ok(d) && !rowdot_ok(d);
+  const bool head = h.M == d.M && h.K == d.N && h.b && h.c && rowdot_ok(h) && !h.gate &&
+                    !h.beta && h.a == (const void*)d.c && h.a_rm == d.ldc;
+  return dense && head ? 1 : 0;
+}
+
+extern "C" int xa_head_bwd(const float* x, const float* dz, const float* W, const float* gate,
+                           int M, int K, int A, float* dx, int beta, float* gw, float* gb,
+                           int accumulate, void* stream) {
+  XA_CHECK_ARG(x && dz && W && dx && M > 0 && K > 0 && A > 0 && A <= SK_MAXK_H && K <= 4096 &&
+                   (int64_t)M * K < (1ll << 31),
+               "xa_head_bwd: bad operands or sizes (A <= %d, K <= 4096)", SK_MAXK_H);
+  HeadBwd h{x, dz, W, gate, M, K, A, dx, beta, gw, gb, accumulate, 0};
+  h.nbx = (int)(((int64_t)M * K + 255) / 256);
+  const int nbw = ((K + 1) * A + 255) / 256;
+  hipLaunchKernelGGL(head_bwd_kernel, dim3(h.nbx + nbw), dim3(256), 0, (hipStream_t)stream, h);
+  XA_CHECK_LAUNCH("xa_head_bwd");
   return 0;
 }
 

@@ -128,6 +128,55 @@ XA_DEV double gran_f64(const f32x4v& v) {
                                           __float_as_uint(v[0])));
 }
 
+// The blocks' gradient rows (the bulk of the in-launch exchange) as TAGGED PAIRS: 8 bytes
+// per two values, the step's tag parity in each value's lowest mantissa bit (the value moves
+// by at most one ulp, 6e-8 relative; the update is checked against float64 with a
+// tolerance). Parity suffices: a row word is rewritten every step, tags are consecutive
+// integers (gen K + k + 1) across launches, a kernel boundary writes the previous launch's
+// words back, and a reader that has seen step k - 1's value at an address never sees an
+// older one there (per-address coherence of one L2 / the fabric). Every 4-byte word carries
+// its own tag, so no store width has to be untorn. Half the bytes of the {value, tag}
+// granule pairs (XA_ROW_PAIRS=0: those, the round-5 format).
+#ifndef XA_ROW_PAIRS
+#define XA_ROW_PAIRS 1
+#endif
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+typedef unsigned u32x2v __attribute__((ext_vector_type(2)));
+#if XA_ROW_PAIRS
+typedef f32x2v RowG;
+constexpr uint32_t kRowPB = 8;  // bytes per pair column of a row
+XA_DEV float row_tagged(float v, unsigned tag) {
+  return __uint_as_float((__float_as_uint(v) & ~1u) | (tag & 1u));
+}
+XA_DEV void st_row(__amdgpu_buffer_rsrc_t r, uint32_t off, float v0, float v1, unsigned tag,
+                   bool wt) {
+  const u32x2v u = {__float_as_uint(row_tagged(v0, tag)), __float_as_uint(row_tagged(v1, tag))};
+  if (wt) __builtin_amdgcn_raw_buffer_store_b64(u, r, off, 0, kAuxSc1);
+  else __builtin_amdgcn_raw_buffer_store_b64(u, r, off, 0, 0);
+}
+XA_DEV RowG ld_row(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(f32x2v, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, kAuxSc1));
+}
+XA_DEV bool row_ok(const RowG& v, unsigned tag) {
+  return ((__float_as_uint(v[0]) ^ tag) & 1u) == 0u && ((__float_as_uint(v[1]) ^ tag) & 1u) == 0u;
+}
+XA_DEV float row_v0(const RowG& v) { return v[0]; }
+XA_DEV float row_v1(const RowG& v) { return v[1]; }
+#else
+typedef f32x4v RowG;
+constexpr uint32_t kRowPB = 16;
+XA_DEV void st_row(__amdgpu_buffer_rsrc_t r, uint32_t off, float v0, float v1, unsigned tag,
+                   bool wt) {
+  st_gran2(r, off, v0, v1, tag, wt);
+}
+XA_DEV RowG ld_row(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, kAuxSc1);
+}
+XA_DEV bool row_ok(const RowG& v, unsigned tag) { return gran_ok(v, tag); }
+XA_DEV float row_v0(const RowG& v) { return v[0]; }
+XA_DEV float row_v1(const RowG& v) { return v[2]; }
+#endif
+
 // Poll n (<= N) granule pairs (write-through loads) until every tag equals `tag`. Bounded
 // by the wall clock and the abort word; false on timeout / abort (the caller leaves).
 // One poll round is ONE L2 round trip: the abort word and the wall clock are read only
@@ -136,10 +185,14 @@ XA_DEV double gran_f64(const f32x4v& v) {
 // grid's polls onto one L2 channel), so a granule that lands just after a round was
 // issued is seen one round trip later.
 // (measurement knob) s_sleep units (64 cycles) between poll rounds
-// (A/B knob) every block forms the global gradient norm from its own copy of the reduced g
-// (phase C) instead of polling per-wave sum-of-squares partials published in phase B
+// every block forms the global gradient norm from its own copy of the reduced g (phase C:
+// each parameter sits on exactly one thread, f64 squares summed in a fixed thread / wave
+// order, identical in every block) instead of polling per-wave sum-of-squares partials that
+// phase B publishes after its column sums (XA_SELF_NORM=0, the round-5 form): phase B
+// publishes g one wave sum earlier and phase C polls only g (16-env update 145 -> 141 us,
+// C2 267 -> 257 us event-timed, profiles/r06d_variants_ab.txt)
 #ifndef XA_SELF_NORM
-#define XA_SELF_NORM 0
+#define XA_SELF_NORM 1
 #endif
 #ifndef XA_POLL_SLEEP
 #define XA_POLL_SLEEP 1
@@ -160,6 +213,43 @@ XA_DEV bool poll_gran(__amdgpu_buffer_rsrc_t r, const uint32_t (&off)[N], int n,
 #pragma unroll
     for (int u = 0; u < N; ++u)
       if (u < n) ok = ok && gran_ok(v[u], tag);
+    if (ok) return true;
+    if (!slow) {
+#ifndef XA_POLL_NOSLEEP
+      __builtin_amdgcn_s_sleep(XA_POLL_SLEEP);
+#endif
+      continue;
+    }
+    if (ab == epoch) return false;
+    {
+      const uint64_t now = wall_clock64();
+      if (t0 == 0) t0 = now;
+      else if (now - t0 > kSpinTicks) {
+        __hip_atomic_store((gu32*)(ctl + kAbort), epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (status) __hip_atomic_store((gu32*)status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return false;
+      }
+    }
+  }
+}
+
+// poll_gran over row granules (tagged pairs or granule pairs, above)
+template <int N>
+XA_DEV bool poll_row(__amdgpu_buffer_rsrc_t r, const uint32_t (&off)[N], int n, unsigned tag,
+                     RowG (&v)[N], unsigned* ctl, unsigned epoch, int* status) {
+  uint64_t t0 = 0;
+  for (unsigned it = 0;; ++it) {
+    const bool slow = (it & 15u) == 15u;
+#pragma unroll
+    for (int u = 0; u < N; ++u)
+      if (u < n) v[u] = ld_row(r, off[u]);
+    const unsigned ab = slow ? __hip_atomic_load((gu32*)(ctl + kAbort), __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT)
+                             : 0u;
+    bool ok = true;
+#pragma unroll
+    for (int u = 0; u < N; ++u)
+      if (u < n) ok = ok && row_ok(v[u], tag);
     if (ok) return true;
     if (!slow) {
 #ifndef XA_POLL_NOSLEEP
@@ -541,7 +631,7 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
   // first: they drain while the update runs)
   if (p.stats_words > 0) {
     const unsigned* src = static_cast<const unsigned*>(p.stats_src);
-    unsigned* dst = static_cast<unsigned*>(p.stats_dst[gen & 1u]);
+    unsigned* dst = static_cast<unsigned*>(p.stats_dst[gen % XA_PPO_STATS_SLOTS]);
     for (int i = b * 256 + tid; i < p.stats_words; i += G * 256) dst[i] = src[i];
     if (b == 0 && tid == 0) dst[p.stats_words] = gen;
   }
@@ -841,22 +931,22 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
                          unsigned tg) -> bool {
     const int total = nrow * ncol;
     uint32_t off[kBF];
-    f32x4v x[kBF];
+    RowG x[kBF];
     int n = 0;
 #pragma unroll
     for (int u = 0; u < kBF; ++u) {
       const int f = tid + 256 * u;
       const int rr = f / ncol;
-      off[u] = f < total ? base(rr) + (uint32_t)(16 * (f - rr * ncol)) : 0u;
+      off[u] = f < total ? base(rr) + kRowPB * (uint32_t)(f - rr * ncol) : 0u;
       n += f < total;
     }
-    const bool bad = !poll_gran<kBF>(r, off, n, tg, x, ws.ctl, epoch, p.status);
+    const bool bad = !poll_row<kBF>(r, off, n, tg, x, ws.ctl, epoch, p.status);
 #pragma unroll
     for (int u = 0; u < kBF; ++u)
       if (u < n) {
         const int f = tid + 256 * u;
-        scr[2 * f] = x[u][0];
-        scr[2 * f + 1] = x[u][2];
+        scr[2 * f] = row_v0(x[u]);
+        scr[2 * f + 1] = row_v1(x[u]);
       }
     return bad;
   };
@@ -896,7 +986,7 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
     auto w2_out = [&](const PtAcc<OBS, A>& a) {
 #ifndef XA_ABL_ROW
       pt_write_row_w2<OBS, A>(a, [&](int pr, float v0, float v1) {
-        st_gran2(rows_r, (uint32_t)(((size_t)b * NP2 + pr) * 16), v0, v1, tag, row_wt);
+        st_row(rows_r, (uint32_t)((size_t)b * NP2 + pr) * kRowPB, v0, v1, tag, row_wt);
       });
 #endif
     };
@@ -950,8 +1040,8 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
     }
     __syncthreads();
     for (int c = H * H / 2 + tid; c < NP2; c += 256)
-      st_gran2(rows_r, (uint32_t)(((size_t)b * NP2 + c) * 16), srow[2 * c], srow[2 * c + 1], tag,
-               row_wt);
+      st_row(rows_r, (uint32_t)((size_t)b * NP2 + c) * kRowPB, srow[2 * c], srow[2 * c + 1], tag,
+             row_wt);
     XA_STAMP(45);
     XA_TRACE_PT(b, k, 2);
     fetch_tile(k + 1, b);  // the next step's first tile, while the other blocks finish
@@ -966,7 +1056,7 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
       const bool flat = false && ng * xnc <= 256 * kBF;  // measured slower at 32 rows (C2)
       if (flat && xnc > 0) {
         const bool bad = gather_rows(rows_r, ng, xnc, [&](int j) {
-          return (uint32_t)(((size_t)U.xmem[j] * NP2 + xc0) * 16);
+          return (uint32_t)((size_t)U.xmem[j] * NP2 + xc0) * kRowPB;
         }, tag);
         if (__syncthreads_or(bad)) return;
         for (int c = tid; c < xnc; c += 256) {
@@ -991,20 +1081,20 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
           constexpr int kB = kBF;  // 32 XCD members over 3 row groups: one poll round
           for (int j0 = rg; j0 < ng && !bad; j0 += RG * kB) {
             uint32_t off[kB];
-            f32x4v x[kB];
+            RowG x[kB];
             int n = 0;
 #pragma unroll
             for (int u = 0; u < kB; ++u) {
               const int j = j0 + u * RG;
-              off[u] = j < ng ? (uint32_t)(((size_t)U.xmem[j] * NP2 + c) * 16) : 0u;
+              off[u] = j < ng ? (uint32_t)((size_t)U.xmem[j] * NP2 + c) * kRowPB : 0u;
               n += j < ng;
             }
-            bad = !poll_gran<kB>(rows_r, off, n, tag, x, ws.ctl, epoch, p.status);
+            bad = !poll_row<kB>(rows_r, off, n, tag, x, ws.ctl, epoch, p.status);
 #pragma unroll
             for (int u = 0; u < kB; ++u)
               if (u < n) {
-                a0 += (double)x[u][0];
-                a1 += (double)x[u][2];
+                a0 += (double)row_v0(x[u]);
+                a1 += (double)row_v1(x[u]);
               }
           }
           U.red[(rg * ncol + cq) * 2] = a0;
@@ -1066,20 +1156,20 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
       if (tid < parts_b * nc) {
         const int part = tid / nc, c = tid - part * nc;
         uint32_t off[kBF];
-        f32x4v x[kBF];
+        RowG x[kBF];
         int n = 0;
 #pragma unroll
         for (int u = 0; u < kBF; ++u) {
           const int r = part + parts_b * u;
-          off[u] = r < G ? (uint32_t)(((size_t)r * NP2 + c0 + c) * 16) : 0u;
+          off[u] = r < G ? (uint32_t)((size_t)r * NP2 + c0 + c) * kRowPB : 0u;
           n += r < G;
         }
-        bad = !poll_gran<kBF>(rows_r, off, n, tag, x, ws.ctl, epoch, p.status);
+        bad = !poll_row<kBF>(rows_r, off, n, tag, x, ws.ctl, epoch, p.status);
 #pragma unroll
         for (int u = 0; u < kBF; ++u)
           if (u < n) {
-            t0 += (double)x[u][0];
-            t1 += (double)x[u][2];
+            t0 += (double)row_v0(x[u]);
+            t1 += (double)row_v1(x[u]);
           }
         U.red[(part * nc + c) * 2] = t0;
         U.red[(part * nc + c) * 2 + 1] = t1;
@@ -1100,7 +1190,7 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
     const bool flat_b = flat_ok && !col_b && !two_level && G * nc <= 256 * kBF;
     if (nc > 0 && flat_b) {
       const bool bad = gather_rows(rows_r, G, nc, [&](int r) {
-        return (uint32_t)(((size_t)r * NP2 + c0) * 16);
+        return (uint32_t)((size_t)r * NP2 + c0) * kRowPB;
       }, tag);
       if (__syncthreads_or(bad)) return;
       // few columns: `parts` threads per column sum interleaved rows, combined in part
@@ -1178,18 +1268,19 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
                 a1 += gran_f64(x[u + 1]);
               }
             } else {
+              RowG xr[kB];
 #pragma unroll
               for (int u = 0; u < kB; ++u) {
                 const int r = j0 + u * RG;
-                off[u] = r < G ? (uint32_t)(((size_t)r * NP2 + c) * 16) : 0u;
+                off[u] = r < G ? (uint32_t)((size_t)r * NP2 + c) * kRowPB : 0u;
                 n += r < G;
               }
-              bad = !poll_gran<kB>(rows_r, off, n, tag, x, ws.ctl, epoch, p.status);
+              bad = !poll_row<kB>(rows_r, off, n, tag, xr, ws.ctl, epoch, p.status);
 #pragma unroll
               for (int u = 0; u < kB; ++u)
                 if (u < n) {
-                  a0 += (double)x[u][0];
-                  a1 += (double)x[u][2];
+                  a0 += (double)row_v0(xr[u]);
+                  a1 += (double)row_v1(xr[u]);
                 }
             }
           }
@@ -1667,11 +1758,17 @@ extern "C" int xa_ppo_update(const XaPpoUpdateArgs* a, void* stream) {
   const size_t need = ws_bytes(G, offs(a->obs_dim, a->n_actions).P, K);
   XA_CHECK_ARG(a->workspace_bytes >= need, "xa_ppo_update: workspace %zu bytes < %zu needed",
                a->workspace_bytes, need);
-  XA_CHECK_ARG(a->stats_words <= 0 ||
-                   (a->stats_src && a->stats_dst[0] && a->stats_dst[1] &&
-                    (((uintptr_t)a->stats_src | (uintptr_t)a->stats_dst[0] |
-                      (uintptr_t)a->stats_dst[1]) & 3) == 0),
-               "xa_ppo_update: stats_words > 0 needs stats_src and both (4-B aligned) stats_dst");
+  if (a->stats_words > 0) {
+    uintptr_t bits = (uintptr_t)a->stats_src;
+    bool all = a->stats_src != nullptr;
+    for (int i = 0; i < XA_PPO_STATS_SLOTS; ++i) {
+      all = all && a->stats_dst[i] != nullptr;
+      bits |= (uintptr_t)a->stats_dst[i];
+    }
+    XA_CHECK_ARG(all && (bits & 3) == 0,
+                 "xa_ppo_update: stats_words > 0 needs stats_src and every (4-B aligned) "
+                 "stats_dst slot");
+  }
   hipStream_t s = (hipStream_t)stream;
   if (a->obs_dim == 4 && a->n_actions == 2) return launch<4, 2>(a, G, K, n_mb, s);
   if (a->obs_dim == 6 && a->n_actions == 3) return launch<6, 3>(a, G, K, n_mb, s);

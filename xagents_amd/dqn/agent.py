@@ -15,6 +15,8 @@ train_step (dqn/agent.py:182-197), all on device except the reference's host RNG
                          gradient round trip), the other layers' via xa_clip_adam
 at_step_end: hard target copy when steps % target_sync_steps == 0 (xa_polyak, tau 1).
 """
+import os
+
 import numpy as np
 import torch
 
@@ -228,9 +230,26 @@ class DQN(OffPolicy):
             # t += 1 happened in _td_grad (the fused epilogues read it); the dense layers'
             # Adam runs inside the backward, the rest of the parameters in one launch per range
             th, m, v = self.model.theta, opt.m, opt.v
-            spec = {i: (adam_apply(th, m, v, opt.iterations, opt, self.ex_online.offsets[i][0]),
+            ex = self.ex_online
+            spec = {i: (adam_apply(th, m, v, opt.iterations, opt, ex.offsets[i][0]),
                         self.write_raw_grad) for i in fl}
-            self.ex_online.backward([self.dq], self.grad, batch=self.batch_size, adam=spec)
+            rest = list(rest)
+            stack_end = ex.offsets[2][1] + ex.layers[2].filters if ex.stack else None
+            if ex.stack and ex._stack_bwd_ok() and (0, stack_end) in rest and \
+                    os.environ.get('XA_STACK_ADAM', '1') != '0':
+                # the conv stack's Adam inside its backward's reduce launch, with the one
+                # other range (the Q head's, final by then) folded into the same launch
+                rest.remove((0, stack_end))
+                tail = None
+                later = [r for r in rest if r[0] >= stack_end]
+                if later:
+                    lo, hi = later[0]
+                    rest.remove(later[0])
+                    tail = (adam_apply(th, m, v, opt.iterations, opt, lo),
+                            self.grad.data_ptr() + 4 * lo, hi - lo)
+                spec['stack'] = (adam_apply(th, m, v, opt.iterations, opt, 0),
+                                 self.write_raw_grad, tail)
+            ex.backward([self.dq], self.grad, batch=self.batch_size, adam=spec)
             for lo, hi in rest:
                 kernels.clip_adam(th[lo:hi], m[lo:hi], v[lo:hi], self.grad[lo:hi],
                                   opt.iterations, opt.learning_rate, opt.beta_1, opt.beta_2,
@@ -291,15 +310,29 @@ class DQN(OffPolicy):
         self.get_actions()
         self._env_step(self.actions)
         self.steps += self.n_envs
-        # host index draw in the reference's order, then the device learner phase
-        self.replay.upload_slots(self.replay.sample_slots())
-        self._run_learn()
+        # host index draw in the reference's order, then the device learner phase (its
+        # gather reads the staged slots from mapped pinned memory: no upload launch;
+        # XA_PINNED_SLOTS=0: the upload copy)
+        if self._pinned_slots():
+            self.replay.stage_slots(self.replay.sample_slots())
+            self._run_learn()
+            self.replay.stage_consumed()
+        else:
+            self.replay.upload_slots(self.replay.sample_slots())
+            self._run_learn()
+
+    def _pinned_slots(self):
+        if '_pslots' not in self.__dict__:
+            self._pslots = os.environ.get('XA_PINNED_SLOTS', '1') != '0' and \
+                torch.device(self.device).type == 'cuda'
+        return self._pslots
 
     def _learn_phase(self):
         """gather the sampled batch -> TD gradient -> CNN backward -> Keras Adam."""
         B = self.batch_size
-        self.replay.gather(self.replay.slots, self.xb[:B], self.b_act, self.b_rew, self.b_done,
-                           self.xb[B:])
+        r = self.replay
+        src = (r.stage_ptr(), r.slots.numel()) if self._pinned_slots() else r.slots
+        r.gather(src, self.xb[:B], self.b_act, self.b_rew, self.b_done, self.xb[B:])
         self._td_grad()
         self._apply()
 

@@ -197,9 +197,13 @@ class LayerExecutor:
         call('xa_conv_stack_fwd', ctypes_ref(a), stream())
         self._timing_end(ev, f'conv stack fwd {a.rows} rows', float(STACK_FWD_FLOPS) * a.rows)
 
-    def _conv_stack_bwd(self, Bb, gp, accumulate):
+    def _conv_stack_bwd(self, Bb, gp, accumulate, adam=None):
         """Layers 2..0's parameter gradient in one fused launch + reduce (xa_conv_stack_bwd)
-        from douts[2] (conv3's gated output gradient) and the forward's h1 / h2."""
+        from douts[2] (conv3's gated output gradient) and the forward's h1 / h2. adam
+        (XaAdamApply of the stack's first parameter, keep_grad, rest): Keras Adam on the
+        stack's parameters inside the reduce (the raw gradient to grad only when keep_grad),
+        and rest = (XaAdamApply, gradient pointer, count) of one more range whose gradient
+        is final by now, or None."""
         rows = Bb * self.in_shape[-3]
         lib = _lib.load()
         need = int(lib.xa_conv_stack_bwd_workspace_floats(int(self.B * self.in_shape[-3])))
@@ -213,7 +217,12 @@ class LayerExecutor:
         a.h1, a.h2, a.dz3 = (self.outs[0].data_ptr(), self.outs[1].data_ptr(),
                              self.douts[2].data_ptr())
         a.ws, a.ws_floats = self.stack_ws.data_ptr(), self.stack_ws.numel()
-        a.grad, a.accumulate = gp + 4 * w1, int(accumulate)
+        a.grad, a.accumulate = (gp + 4 * w1 if gp is not None else None), int(accumulate)
+        if adam is not None:
+            ad, keep, rest = adam
+            a.adam_on, a.write_grad, a.adam = 1, int(bool(keep)), ad
+            if rest is not None:
+                a.rest, a.rest_grad, a.n_rest = rest[0], rest[1], int(rest[2])
         ev = self._timing_start()
         call('xa_conv_stack_bwd', ctypes_ref(a), stream())
         self._timing_end(ev, f'conv stack bwd {rows} rows (+ reduce)',
@@ -333,8 +342,9 @@ class LayerExecutor:
         self.x = x
         if self.stack:
             self._conv_stack_fwd(x, tp)
+        fused_head = self._fused_head_layer()
         for i, l in enumerate(self.layers):
-            if l.kind == 'flatten' or (self.stack and i < 3):
+            if l.kind == 'flatten' or (self.stack and i < 3) or i == fused_head:
                 continue
             j = self._src_layer(i)
             src = x if j == -1 else self.outs[j]
@@ -345,6 +355,24 @@ class LayerExecutor:
                 kw = dict(a_u8=src_u8, a_m=(1, l.in_features, 0), b_ks=l.units, b_ns=1,
                           ldc=l.units, bias=tp + 4 * b0, act=self._act(i),
                           workspace=self.workspace)
+                if fused_head is not None and i == fused_head - 1:
+                    # this layer's split reduce, the head and (head given) DQN's row step in
+                    # one launch after the split partials (xa_gemm_head)
+                    lh = self.layers[fused_head]
+                    wh, bh = self.offsets[fused_head]
+                    gd = _gemm_args(self.B, l.units, l.in_features, src.data_ptr(), tp + 4 * w0,
+                                    self.outs[i].data_ptr(), **kw)
+                    gh = _gemm_args(self.B, lh.units, lh.in_features, self.outs[i].data_ptr(),
+                                    tp + 4 * wh, self.outs[fused_head].data_ptr(),
+                                    a_m=(1, lh.in_features, 0), b_ks=lh.units, b_ns=1,
+                                    ldc=lh.units, bias=tp + 4 * bh, act=self._act(fused_head),
+                                    workspace=self.workspace)
+                    call('xa_gemm_head', ctypes_ref(gd), ctypes_ref(gh),
+                         None if head is None else ctypes_ref(head), stream())
+                    self._timing_end(ev, f'dense fwd {self.B}x{l.units}x{l.in_features} + head',
+                                     2.0 * self.B * (l.units * l.in_features +
+                                                     lh.units * lh.in_features))
+                    continue
                 if head is not None and i == len(self.layers) - 1:
                     g = _gemm_args(self.B, l.units, l.in_features, src.data_ptr(), tp + 4 * w0,
                                    self.outs[i].data_ptr(), **kw)
@@ -361,6 +389,44 @@ class LayerExecutor:
                      b_ks=l.filters, b_ns=1, ldc=l.filters, bias=tp + 4 * b0,
                      act=self._act(i), workspace=self.workspace)
         return [self.outs[i] for i in self.model.outputs]
+
+    def _head_bwd_on(self):
+        """xa_head_bwd for row-dot heads (XA_HEAD_BWD=0: the dW GEMM + few-k dX launches)."""
+        if '_hb' not in self.__dict__:
+            self._hb = os.environ.get('XA_HEAD_BWD', '1') != '0'
+        return self._hb
+
+    def _fused_head_layer(self):
+        """The index of the model's single output layer when it is a row-dot head on the
+        dense layer right before it and that pair takes xa_gemm_head (one launch for the
+        dense layer's split reduce and the head); None otherwise (XA_GEMM_HEAD=0: never)."""
+        if '_fh' not in self.__dict__:
+            fh = None
+            h = len(self.layers) - 1
+            if os.environ.get('XA_GEMM_HEAD', '1') != '0' and h >= 1 and \
+                    list(self.model.outputs) == [h] and self.layers[h].kind == 'dense' and \
+                    self.layers[h - 1].kind == 'dense' and self._src_layer(h) == h - 1 and \
+                    self._src_layer(h - 1) != -1:
+                l, lh = self.layers[h - 1], self.layers[h]
+                tp = self.model.theta.data_ptr()
+                (w0, b0), (wh, bh) = self.offsets[h - 1], self.offsets[h]
+                src = self.outs[self._src_layer(h - 1)]
+                try:
+                    gd = _gemm_args(self.B, l.units, l.in_features, src.data_ptr(), tp + 4 * w0,
+                                    self.outs[h - 1].data_ptr(), a_m=(1, l.in_features, 0),
+                                    b_ks=l.units, b_ns=1, ldc=l.units, bias=tp + 4 * b0,
+                                    act=self._act(h - 1), workspace=self.workspace)
+                    gh = _gemm_args(self.B, lh.units, lh.in_features, self.outs[h - 1].data_ptr(),
+                                    tp + 4 * wh, self.outs[h].data_ptr(),
+                                    a_m=(1, lh.in_features, 0), b_ks=lh.units, b_ns=1,
+                                    ldc=lh.units, bias=tp + 4 * bh, act=self._act(h),
+                                    workspace=self.workspace)
+                    if _lib.load().xa_gemm_head_ok(ctypes_ref(gd), ctypes_ref(gh)) == 1:
+                        fh = h
+                except _lib.HipLibraryError:
+                    fh = None
+            self._fh = fh
+        return self._fh
 
     # ---- forward-mode derivative ------------------------------------------------
     def jvp(self, v):
@@ -421,7 +487,9 @@ class LayerExecutor:
         data-parallel path's bucketed all-reduce). `adam` {layer index: (XaAdamApply,
         keep_grad)}: those dense layers (adam_fusable) take their Keras Adam step inside the
         weight-gradient GEMM (xa_gemm_adam) after their input gradient has read W; `grad`
-        then receives their raw gradient only when keep_grad."""
+        then receives their raw gradient only when keep_grad. adam['stack'] (see
+        _conv_stack_bwd): the fused conv stack's Adam (+ one more final range) inside its
+        reduce launch."""
         Bb = batch or self.B
         assert adam is None or not accumulate
         assert Bb <= self.B
@@ -463,7 +531,8 @@ class LayerExecutor:
             d = dz[i]
             if i == 2 and gp is not None and self._stack_bwd_ok():
                 # the whole conv stack at once; layers finish in reverse order as below
-                self._conv_stack_bwd(Bb, gp, accumulate)
+                self._conv_stack_bwd(Bb, gp, accumulate,
+                                     adam.get('stack') if adam is not None else None)
                 if on_grad is not None:
                     for k in (2, 1, 0):
                         on_grad(self.offsets[k][0])
@@ -512,6 +581,20 @@ class LayerExecutor:
                     if gp is not None and on_grad is not None:
                         on_grad(w0)
 
+                if not fused and gp is not None and j != -1 and n_out <= 8 and Bb <= 256 and \
+                        n_in <= 4096 and not src_u8 and self._head_bwd_on():
+                    # a row-dot head: its input gradient and [W; b] gradient in one launch
+                    ev = self._timing_start()
+                    call('xa_head_bwd', src.data_ptr(), d.data_ptr(), int(tp + 4 * w0),
+                         None if gate_j is None else int(gate_j), int(Bb), int(n_in), int(n_out),
+                         self.douts[j].data_ptr(), int(written[j]), int(gp + 4 * w0),
+                         int(gp + 4 * b0), int(accumulate), stream())
+                    self._timing_end(ev, f'head bwd {Bb}x{n_in}x{n_out}',
+                                     4.0 * Bb * n_in * n_out)
+                    written[j] = True
+                    if on_grad is not None:
+                        on_grad(w0)
+                    continue
                 if not fused:
                     wgrad()
                 if j == -1 and dinput is not None:

@@ -250,8 +250,8 @@ class PPO(A2C):
     def _setup_fused_stats(self, u):
         """The train step's episode statistics (done flags, running returns, the status word:
         the packed buffer a2c/agent.py lays out) leave the device inside the update launch,
-        into two mapped pinned host slots chosen by the launch number's parity -- no
-        xa_copy_to_host launch per train step. Off with XA_STATS_IN_UPDATE=0 or the opt-in
+        into XA_PPO_STATS_SLOTS mapped pinned host slots chosen by the launch number -- no
+        xa_copy_to_host launch per train step, and several train steps per graph replay. Off with XA_STATS_IN_UPDATE=0 or the opt-in
         side-stream copy."""
         import ctypes
         from xagents_amd._lib import call
@@ -264,7 +264,7 @@ class PPO(A2C):
         nw = os_ + 1  # through the status word
         if getattr(self, '_fused_host', None) is None or self._fused_host[0].numel() != nw + 1:
             self._fused_host = [torch.zeros(nw + 1, dtype=torch.float32).pin_memory()
-                                for _ in range(2)]
+                                for _ in range(_lib.XA_PPO_STATS_SLOTS)]
             self._fused_done = [h[:nd].view(sd) for h in self._fused_host]
             self._fused_epret = [h[oe:oe + se[0] * se[1]].view(se) for h in self._fused_host]
             self._fused_host_status = [h[os_:os_ + 1].view(torch.int32)
@@ -276,7 +276,8 @@ class PPO(A2C):
                 call('xa_host_device_pointer', ctypes.c_void_p(h.data_ptr()), ctypes.byref(dp))
                 self._fused_dev.append(dp.value)
         u.stats_src = self._stats_pack.data_ptr()
-        u.stats_dst[0], u.stats_dst[1] = self._fused_dev
+        for i, dp in enumerate(self._fused_dev):
+            u.stats_dst[i] = dp
         u.stats_words = nw
         self._stats_fused = True
 

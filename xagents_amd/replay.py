@@ -129,6 +129,7 @@ class DeviceReplay:
         self._pin_ev = [None, None]
         self._pin_slot = 0
         self.slots = torch.zeros(n * self.k, dtype=torch.int64, device=device)
+        self._stage = None  # the staged (mapped pinned) slots, allocated on first use
 
     # ---- append (device) + host mirror -----------------------------------------
     def fill_step_args(self, a, actions):
@@ -193,10 +194,50 @@ class DeviceReplay:
         self._pin_slot ^= 1
         return self.slots
 
+    # ---- staged slots: the consuming launch reads them from mapped pinned memory ------
+    def stage_ptr(self):
+        """Device address of the mapped pinned buffer the staged slots live in (fixed for
+        the buffer's life, so a captured hipGraph may read it)."""
+        if self._stage is None:
+            from xagents_amd._lib import call as _call
+            self._stage = torch.zeros(self.n * self.k, dtype=torch.int64).pin_memory()
+            dp = ctypes.c_void_p()
+            _call('xa_host_device_pointer', ctypes.c_void_p(self._stage.data_ptr()),
+                  ctypes.byref(dp))
+            self._stage_dev = dp.value
+            self._stage_ev = torch.cuda.Event()
+            self._stage_open = False
+        return self._stage_dev
+
+    def stage_slots(self, slots):
+        """The next batch's slots into the staged buffer (no upload copy: the gather reads
+        them over the host link, 8 B per sampled item). The previous batch's consumer must
+        have run: its completion event (stage_consumed) is waited for first; without one the
+        whole stream is (safe, slower)."""
+        self.stage_ptr()
+        if self._stage_open:
+            torch.cuda.current_stream().synchronize()
+        else:
+            self._stage_ev.synchronize()
+        self._stage.numpy()[:] = slots
+        self._stage_open = True
+        return self._stage_dev
+
+    def stage_consumed(self):
+        """Call right after enqueueing the launch (or graph replay) that read the staged
+        slots."""
+        self._stage_ev.record()
+        self._stage_open = False
+
     def gather(self, slots, states, actions, rewards, dones, new_states):
         """The five fields of one sampled batch in one xa_ring_gather_fields launch (the
-        argument block is built once per destination set and reused)."""
-        key = (slots.data_ptr(), slots.numel(), states.data_ptr(), actions.data_ptr(),
+        argument block is built once per destination set and reused). slots: a device
+        int64 tensor, or an (address, count) pair (the staged slots)."""
+        if isinstance(slots, tuple):
+            sp, sn = slots
+        else:
+            sp, sn = slots.data_ptr(), slots.numel()
+        key = (sp, sn, states.data_ptr(), actions.data_ptr(),
                rewards.data_ptr(), dones.data_ptr(), new_states.data_ptr())
         if getattr(self, '_gkey', None) != key:
             a = XaGatherArgs()
@@ -207,6 +248,6 @@ class DeviceReplay:
             for f, (ring, dst, nb) in enumerate(fields):
                 a.field[f].ring, a.field[f].dst, a.field[f].item_bytes = \
                     ring.data_ptr(), dst.data_ptr(), nb
-            a.n_fields, a.n_items, a.slots = len(fields), slots.numel(), slots.data_ptr()
+            a.n_fields, a.n_items, a.slots = len(fields), sn, sp
             self._gargs, self._gkey = a, key
         call('xa_ring_gather_fields', ctypes.byref(self._gargs), stream())
