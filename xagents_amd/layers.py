@@ -222,7 +222,7 @@ class LayerExecutor:
             ad, keep, rest = adam
             a.adam_on, a.write_grad, a.adam = 1, int(bool(keep)), ad
             if rest is not None:
-                a.rest, a.rest_grad, a.n_rest = rest[0], rest[1], int(rest[2])
+                a.rest, a.rest_grad, a.n_rest = rest[0], int(rest[1]), int(rest[2])
         ev = self._timing_start()
         call('xa_conv_stack_bwd', ctypes_ref(a), stream())
         self._timing_end(ev, f'conv stack bwd {rows} rows (+ reduce)',
