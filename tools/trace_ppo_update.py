@@ -33,10 +33,14 @@ def build():
 
 
 def analyse(tr, G, K):
-    # [block, step, point] in 10-ns ticks: low 32 bits, re-based (wrap-safe within a launch)
+    # [block, step, point] in 10-ns ticks: low 32 bits, re-based (wrap-safe within a launch);
+    # the shader clock words (slot STEPS - 1, points 9 and 11) keep their raw values
     base = int(tr[0, 0, 0])
-    tr = ((tr.astype(np.int64) - base) & 0xFFFFFFFF).astype(np.int64)
+    raw = tr.astype(np.int64)
+    tr = ((raw - base) & 0xFFFFFFFF).astype(np.int64)
     tr[tr > 0x7FFFFFFF] -= 1 << 32
+    tr[:, STEPS - 1, 9] = raw[:, STEPS - 1, 9]
+    tr[:, STEPS - 1, 11] = raw[:, STEPS - 1, 11]
     t = tr[:G, :K, :6]
     us = lambda x: x / 100.0  # noqa: E731
     names = ['A: tile (+row into LDS)', 'row granule stores', 'B: wait rows + reduce + publish',
@@ -77,6 +81,24 @@ def analyse(tr, G, K):
           f'{us(np.median(c_last - b_last)):8.3f}')
     print(f'  A start skew (first -> last block at loop top) '
           f'{us(np.median(t[:, :, 0].max(0) - t[:, :, 0].min(0))):8.3f}')
+    # the launch outside the step loop: start (after the election) -> phase-0 hop done ->
+    # first loop top; last step's Adam done -> the block's end
+    pro = tr[:G, STEPS - 1]
+    start, hop = pro[:, 6], pro[:, 7]
+    print(f'  launch start skew (first -> last block)       {us(start.max() - start.min()):8.3f}')
+    for a_, b_, nm in ((6, 0, 'start -> gather done'), (0, 1, 'gather -> adv sums stored'),
+                       (1, 2, 'm / v + weights to LDS'), (2, 4, 'advantage totals polled'),
+                       (4, 3, 'minibatch statistics')):
+        d = pro[:, b_] - pro[:, a_]
+        print(f'    phase 0: {nm:34s} {us(np.median(d)):8.3f} {us(d.max()):8.3f}')
+    print(f'  first start -> last phase-0 hop done          {us(hop.max() - start.min()):8.3f}')
+    print(f'  phase-0 hop done -> first / last loop top     {us(t[:, 0, 0].min() - hop.max()):8.3f} '
+          f'{us(t[:, 0, 0].max() - hop.max()):8.3f}')
+    st = pro[:, 3]
+    print(f'  statistics done -> first / last loop top      {us(t[:, 0, 0].min() - st.max()):8.3f} '
+          f'{us(t[:, 0, 0].max() - st.max()):8.3f}')
+    print(f'  first start -> last step done (loop span)     {us(t[:, K - 1, 5].max() - start.min()):8.3f}')
+    print(f'  last step done -> block 0 end                 {us(pro[0, 10] - t[:, K - 1, 5].max()):8.3f}')
 
 
 def main():

@@ -52,11 +52,28 @@ def source_hash():
     return h.hexdigest()[:16]
 
 
+_INCLUDE_RE = re.compile(rb'^\s*#\s*include\s+"([^"]+)"', re.M)
+
+
+def _local_includes(src):
+    """The quoted #include files of src, transitively (resolved next to the including
+    file: csrc headers and ../../include/xagents_hip.h), src itself first."""
+    seen, todo = [], [Path(src)]
+    while todo:
+        f = todo.pop()
+        if f in seen or not f.exists():
+            continue
+        seen.append(f)
+        todo += [(f.parent / m.decode()).resolve() for m in _INCLUDE_RE.findall(f.read_bytes())]
+    return seen
+
+
 def _object_key(src):
-    """What one object depends on: its source, every csrc header and the C ABI header
-    (the .hip files include no other .hip), the compiler command."""
+    """What one object depends on: its source, the csrc / C-ABI headers it includes
+    (transitively), the compiler command."""
     h = hashlib.sha256()
-    for f in [src] + sorted(CSRC.glob('*.hpp')) + [PKG_DIR.parent / 'include' / 'xagents_hip.h']:
+    deps = _local_includes(src)
+    for f in deps[:1] + sorted(deps[1:]):
         h.update(f.name.encode() + b'\0' + f.read_bytes() + b'\0')
     h.update(_flags_key())
     return h.hexdigest()
