@@ -231,7 +231,7 @@ for step in "$@"; do
         --cpu-baseline-seconds 0 > $R/gpurun_out/${T}_profc3_bench.json 2>&1) || exit $?
       python tools/kernel_shapes.py gpurun_out/${T}_profc3/run_kernel_trace.csv 25 \
         > gpurun_out/${T}_profc3_shapes.txt 2>&1
-      python tools/step_timeline.py gpurun_out/${T}_profc3/run_kernel_trace.csv \
+      python tools/step_timeline.py gpurun_out/${T}_profc3/run_kernel_trace.csv conv_stack_bwd_reduce \
         > gpurun_out/${T}_profc3_timeline.txt 2>&1 ;;
     profc4)
       (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/${T}_profc4 \

@@ -85,6 +85,9 @@ def analyse(tr, G, K):
     # first loop top; last step's Adam done -> the block's end
     pro = tr[:G, STEPS - 1]
     start, hop = pro[:, 6], pro[:, 7]
+    ent = pro[:, 5]
+    print(f'  kernel entry (first) -> first / last start    {us(start.min() - ent.min()):8.3f} '
+          f'{us(start.max() - ent.min()):8.3f}  (election)')
     print(f'  launch start skew (first -> last block)       {us(start.max() - start.min()):8.3f}')
     for a_, b_, nm in ((6, 0, 'start -> gather done'), (0, 1, 'gather -> adv sums stored'),
                        (1, 2, 'm / v + weights to LDS'), (2, 4, 'advantage totals polled'),

@@ -567,38 +567,47 @@ struct UpdLds {
 // shared L2) and L1-bypassing sc1 loads, no write-through round trip to the fabric.
 // Placement decides speed, never correctness: a workgroup learns its XCD from
 // HW_REG_XCC_ID and only workgroups of the elected XCD exchange data.
-// Returns the logical block id, or -1 (leave). Contains a __syncthreads().
-XA_DEV int elect_local(unsigned* ctl, int G, unsigned par, int xcc, unsigned epoch, int* status,
-                       int& lds) {
+// Two halves, so that phase 0's gather runs while the election completes (speculatively:
+// nothing is stored before the winner is known). elect_rank: the workgroup's arrival rank
+// on its XCD (its logical block id if the XCD wins; >= G: leave); the G-th arrival claims the
+// winner word. Contains a __syncthreads().
+XA_DEV int elect_rank(unsigned* ctl, int G, unsigned par, int xcc, int& lds) {
   if (threadIdx.x == 0) {
-    int id = -1;
     const unsigned r = __hip_atomic_fetch_add((gu32*)(ctl + kElect + par * kXcds + xcc), 1u,
                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (r < (unsigned)G) {
-      gu32* win_w = (gu32*)(ctl + kWin + par);
-      if (r == (unsigned)G - 1u) {
-        unsigned expect = 0u;
-        __hip_atomic_compare_exchange_strong(win_w, &expect, (unsigned)xcc + 1u, __ATOMIC_RELAXED,
-                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      const uint64_t t0 = wall_clock64();
-      unsigned win;
-      while ((win = __hip_atomic_load(win_w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0u) {
-        if (wall_clock64() - t0 > kSpinTicks) {
-          __hip_atomic_store((gu32*)(ctl + kAbort), epoch, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-          if (status)
-            __hip_atomic_store((gu32*)status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(XA_POLL_SLEEP);
-      }
-      if (win == (unsigned)xcc + 1u) id = (int)r;
+    int id = r < (unsigned)G ? (int)r : -1;
+    if (r == (unsigned)G - 1u) {
+      // the G-th arrival: claim the winner word (no wait for the result here: elect_won
+      // reads it later); the claim's own result then decides without a poll
+      unsigned expect = 0u;
+      const bool mine = __hip_atomic_compare_exchange_strong(
+          (gu32*)(ctl + kWin + par), &expect, (unsigned)xcc + 1u, __ATOMIC_RELAXED,
+          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      id = mine ? id : -2 - id;  // (-2 - r: rank r of a losing XCD, decided already)
     }
     lds = id;
   }
   __syncthreads();
-  return lds;
+  const int v = lds;
+  return v <= -2 ? -2 - v : v;
+}
+// elect_won (thread 0 only): did this XCD win? The G-th arrival knows from its claim; the
+// others poll the winner word (bounded: a timeout raises the abort word and `status`)
+XA_DEV bool elect_won(unsigned* ctl, unsigned par, int xcc, int claim, unsigned epoch,
+                      int* status) {
+  if (claim != 0) return claim > 0;
+  gu32* win_w = (gu32*)(ctl + kWin + par);
+  const uint64_t t0 = wall_clock64();
+  unsigned win;
+  while ((win = __hip_atomic_load(win_w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0u) {
+    if (wall_clock64() - t0 > kSpinTicks) {
+      __hip_atomic_store((gu32*)(ctl + kAbort), epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (status) __hip_atomic_store((gu32*)status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(XA_POLL_SLEEP);
+  }
+  return win == (unsigned)xcc + 1u;
 }
 
 // TS = samples per tile (32; 16 when the minibatch has at most 16 tiles of 32: twice the
@@ -633,6 +642,10 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
   const int P = o.P;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   XA_STAMP_DECL
+#ifdef XA_TRACE
+  unsigned long long t_entry_;  // (diagnostic) kernel entry, before the election
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_entry_)::"memory");
+#endif
 
   // the launch generation (written write-through by block 0 at the end of the previous
   // launch; block 0 of this launch writes the next one only after it polled every block's
@@ -643,15 +656,31 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
   const unsigned par = gen & 1u;
   const int xcc = xcc_id();
   const int G = FIX ? FS::G : loc ? p.n_blocks : (int)gridDim.x;
-  const int b = loc ? elect_local(ws.ctl, G, par, xcc, epoch, p.status, U.flag) : (int)blockIdx.x;
-  if (b < 0) return;
-  // the train step's episode statistics into host slot gen & 1 (posted stores, issued
-  // first: they drain while the update runs)
-  if (p.stats_words > 0) {
-    const unsigned* src = static_cast<const unsigned*>(p.stats_src);
-    unsigned* dst = static_cast<unsigned*>(p.stats_dst[gen % XA_PPO_STATS_SLOTS]);
-    for (int i = b * 256 + tid; i < p.stats_words; i += G * 256) dst[i] = src[i];
-    if (b == 0 && tid == 0) dst[p.stats_words] = gen;
+  // XCD-local mode: the arrival rank (the block id if this XCD wins); the G-th arrival's
+  // claim result rides in U.flag's sign until elect_won (claim: +1 won, -1 lost, 0 poll)
+  int claim = 0;
+  int b = (int)blockIdx.x;
+  if (loc) {
+    b = elect_rank(ws.ctl, G, par, xcc, U.flag);
+    if (b < 0) return;
+    if (b == G - 1 && tid == 0) claim = U.flag >= 0 ? 1 : -1;
+  }
+#ifdef XA_TRACE
+  if (tid == 0) U.trace[(kTraceSteps - 1) * kTracePts + 5] = (unsigned)t_entry_;
+#endif
+  // the train step's episode statistics into host slot gen % XA_PPO_STATS_SLOTS (posted
+  // stores to mapped host memory that drain while the update runs): the thread's first
+  // kSW words loaded now and stored after the phase-0 gather (a store waits for its load:
+  // issued here it held the block for an HBM round trip before any other work)
+  constexpr int kSW = 2;
+  const unsigned* const st_src = static_cast<const unsigned*>(p.stats_src);
+  unsigned* const st_dst =
+      p.stats_words > 0 ? static_cast<unsigned*>(p.stats_dst[gen % XA_PPO_STATS_SLOTS]) : nullptr;
+  unsigned st_w[kSW];
+#pragma unroll
+  for (int u = 0; u < kSW; ++u) {
+    const int i = b * 256 + tid + u * G * 256;
+    st_w[u] = i < p.stats_words ? st_src[i] : 0u;
   }
   XA_STAMP_BLOCK(b == 0)
   XA_STAMP(30);
@@ -723,6 +752,12 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
       slot[OBS + 3] = p.old_logp[idx];
     }
     __syncthreads();
+  }
+  if (loc) {
+    // stores follow: leave unless this XCD won the election
+    if (tid == 0) U.flag = elect_won(ws.ctl, par, xcc, claim, epoch, p.status) ? 1 : 0;
+    __syncthreads();
+    if (U.flag == 0) return;
   }
   XA_TRACE_PT(b, kTraceSteps - 1, 0);  // phase-0 gather done
   // preloaded inputs of <= 32 samples per step: each minibatch's sums on a 16- or 32-lane row
@@ -810,6 +845,16 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
     if (lane == 0) st_d2_tagged(adv_r, (uint32_t)((k * G + b) * 16), s1, s2, epoch);
   }
   XA_TRACE_PT(b, kTraceSteps - 1, 1);  // advantage sums stored
+  if (p.stats_words > 0) {
+#pragma unroll
+    for (int u = 0; u < kSW; ++u) {
+      const int i = b * 256 + tid + u * G * 256;
+      if (i < p.stats_words) st_dst[i] = st_w[u];
+    }
+    for (int i = b * 256 + tid + kSW * G * 256; i < p.stats_words; i += G * 256)
+      st_dst[i] = st_src[i];
+    if (b == 0 && tid == 0) st_dst[p.stats_words] = gen;
+  }
   XA_STAMP(31);
 
   constexpr int NS = UpdLds<OBS, A, TS>::NS, NQ4 = UpdLds<OBS, A, TS>::NQ4;
