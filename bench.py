@@ -683,7 +683,8 @@ def bench_ppo(args, world, rank, device, n_envs, env='replay'):
     transport = agent.check_peer_all_reduce()
     if transport == 'rccl' and world > 1:
         agent.train_step()  # re-capture on RCCL after a peer-path fallback
-    agent.fused_train_steps(agent.graph_steps())  # (the multi-step graph's first replay)
+    for s in getattr(agent, '_graph_sizes', None) or [1]:
+        agent.fused_train_steps(s)  # (each multi-step graph's first replay, untimed)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

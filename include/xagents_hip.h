@@ -317,7 +317,7 @@ int xa_clip_adam(float* theta, float* adam_m, float* adam_v, const float* grad, 
  * every optimizer step k and step k's reduced gradient (before the clip).
  */
 #define XA_PPO_DP_MAX 16
-#define XA_PPO_STATS_SLOTS 8 /* host slots of the in-launch episode statistics */
+#define XA_PPO_STATS_SLOTS 16 /* host slots of the in-launch episode statistics */
 #define XA_PPO_PLACE_AUTO 0   /* XCD-local when eligible; not for data-parallel launches */
 #define XA_PPO_PLACE_SPREAD 1 /* never XCD-local */
 #define XA_PPO_PLACE_LOCAL 2  /* XCD-local when eligible, data parallel included (every

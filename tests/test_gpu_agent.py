@@ -35,12 +35,12 @@ def test_graph_replay_equals_eager(device):
 
 @pytest.mark.parametrize('env', ['replay', 'dynamics'])
 def test_multi_step_graph_equals_single_steps(device, monkeypatch, env):
-    """fused_train_steps with XA_GRAPH_STEPS = 4 (four train steps per hipGraph replay, the
-    episode statistics of each in its own host slot, folded in groups) against single-step
-    replays: parameters, Adam state, rollout buffers and the episode bookkeeping
-    (total_rewards, games, the last dones) identical after 11 steps (two groups + three
-    single steps), on the replay env and on the CartPole-dynamics env (both with episode
-    ends inside the window)."""
+    """fused_train_steps with XA_GRAPH_STEPS = 8 (eight train steps per hipGraph replay, and
+    graphs of 4 and 2 for what is left; the episode statistics of each step in its own host
+    slot, folded in groups) against single-step replays: parameters, Adam state, rollout
+    buffers and the episode bookkeeping (total_rewards, games, the last dones) identical
+    after 11 steps (groups of 8 and 2 + one single step), on the replay env and on the
+    CartPole-dynamics env (both with episode ends inside the window)."""
     from xagents_amd import PPO
     from xagents_amd.envs import CartPoleVecEnv, ReplayVecEnv
     from xagents_amd.utils.common import create_model
@@ -56,8 +56,9 @@ def test_multi_step_graph_equals_single_steps(device, monkeypatch, env):
         agent.train_step()  # eager step + capture (with this XA_GRAPH_STEPS)
         return agent
 
-    a, b = make(4), make(1)
-    assert a.update_mode == 'persistent' and a._graph_S == 4 and len(a._graph) == 4
+    a, b = make(8), make(1)
+    assert a.update_mode == 'persistent' and a._graph_S == 8 and len(a._graph) == 6
+    assert a._graph_sizes == [8, 4, 2]
     assert b._graph_S == 1 and len(b._graph) == 3
     a.fused_train_steps(11)
     for _ in range(11):

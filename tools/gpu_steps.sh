@@ -248,7 +248,39 @@ for step in "$@"; do
         -o run --output-format csv -- python $R/tools/td3_grad_steps.py 50 \
         > $R/gpurun_out/${T}_profc5g.log 2>&1) || exit $?
       python tools/kernel_shapes.py gpurun_out/${T}_profc5g/run_kernel_trace.csv 40 \
-        > gpurun_out/${T}_profc5g_shapes.txt 2>&1 ;;
+        > gpurun_out/${T}_profc5g_shapes.txt 2>&1
+      python tools/step_timeline.py gpurun_out/${T}_profc5g/run_kernel_trace.csv td3_update 40 \
+        > gpurun_out/${T}_profc5g_timeline.txt 2>&1
+      python tools/step_timeline.py gpurun_out/${T}_profc5/run_kernel_trace.csv walker_step 30 \
+        > gpurun_out/${T}_profc5_timeline.txt 2>&1 ;;
+    td3gab)
+      # fused TD3 gradient step: graph replay vs direct launch (XA_TD3_GRAPH), interleaved
+      for r in 1 2; do
+        run td3g_on$r 120 python tools/td3_grad_steps.py 100
+        XA_TD3_GRAPH=0 run td3g_off$r 120 python tools/td3_grad_steps.py 100
+        run c5g_on$r 300 python bench.py --config c5 --steps 30 --warmup 5 --cpu-baseline-seconds 0
+        XA_TD3_GRAPH=0 run c5g_off$r 300 python bench.py --config c5 --steps 30 --warmup 5 --cpu-baseline-seconds 0
+      done ;;
+    stageab)
+      # TD3 env-step rows in mapped host memory vs device rows + copies (XA_TD3_HOST_STAGE)
+      for r in 1 2; do
+        run c5s_on$r 300 python bench.py --config c5 --steps 30 --warmup 5 --cpu-baseline-seconds 0
+        XA_TD3_HOST_STAGE=0 run c5s_off$r 300 python bench.py --config c5 --steps 30 --warmup 5 --cpu-baseline-seconds 0
+      done ;;
+    stepgab)
+      # TD3 env step: hipGraph replay vs direct launches (XA_TD3_STEP_GRAPH), interleaved
+      for r in 1 2 3; do
+        run c5t_on$r 300 python bench.py --config c5 --steps 30 --warmup 5 --cpu-baseline-seconds 0
+        XA_TD3_STEP_GRAPH=0 run c5t_off$r 300 python bench.py --config c5 --steps 30 --warmup 5 --cpu-baseline-seconds 0
+      done ;;
+    gs8ab)
+      # PPO train steps per graph replay: XA_GRAPH_STEPS 8 (default) vs 4, interleaved
+      B="python bench.py --steps 20 --warmup 5 --cpu-baseline-seconds 0 --no-secondary"
+      for r in 1 2 3; do
+        run gs8_$r 200 $B
+        XA_GRAPH_STEPS=4 run gs4_$r 200 $B
+      done
+      python tools/bench_brief.py gpurun_out/${T}_gs8_*.out gpurun_out/${T}_gs4_*.out ;;
     c2g)
       # C2 update grid A/B: fewer workgroups with more tiles each (XA_PPO_MAX_BLOCKS)
       for G in ${C2_GS:-256 128}; do

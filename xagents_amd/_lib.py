@@ -27,7 +27,7 @@ MLP_HIDDEN = 64
 XA_PPO_PLACE_AUTO = 0
 XA_PPO_PLACE_SPREAD = 1
 XA_PPO_PLACE_LOCAL = 2
-XA_PPO_STATS_SLOTS = 8  # host slots of the persistent update's in-launch statistics
+XA_PPO_STATS_SLOTS = 16  # host slots of the persistent update's in-launch statistics
 
 
 class XaRolloutArgs(Structure):

@@ -339,14 +339,19 @@ class A2C(ExecutorActorCritic, OnPolicy):
             # rollout, update, and both back to back: a train step replays the third (one
             # graph launch per train step), the per-phase event pass the first two; with the
             # persistent update (every exchange and the statistics copy inside its launch)
-            # a fourth graph holds graph_steps() train steps back to back
-            # (fused_train_steps: one replay per group of steps)
+            # further graphs hold graph_steps() train steps back to back, then half as
+            # many, ... down to 2 (fused_train_steps: one replay per group of steps, the
+            # largest group that fits what is left)
             seqs = [(self._rollout_impl,), (self._update_impl,),
                     (self._rollout_impl, self._update_impl)]
             S = self.graph_steps()
-            if S > 1:
-                seqs.append((self._rollout_impl, self._update_impl) * S)
+            sizes, s = [], S
+            while s > 1:
+                sizes.append(s)
+                seqs.append((self._rollout_impl, self._update_impl) * s)
+                s //= 2
             self._graph_S = S
+            self._graph_sizes = sizes
             for fns in seqs:
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
@@ -426,7 +431,11 @@ class A2C(ExecutorActorCritic, OnPolicy):
         if self.executor_path or getattr(self, 'update_mode', None) != 'persistent' or \
                 not getattr(self, '_stats_fused', False) or self.stats_side_stream:
             return 1
-        return max(1, min(int(os.environ.get('XA_GRAPH_STEPS', '4')), self.FUSED_GROUP_MAX))
+        # default: 8 steps per replay for small rollouts (16 envs: 0.1453 -> 0.1435 ms per
+        # step), 4 when a step's host-side statistics fold is heavy (256 envs: 8 per replay
+        # measured 0.27 -> 0.32 ms per step; profiles/r06t_graph_steps_ab.txt)
+        dflt = 8 if self.n_envs * self.n_steps <= 4096 else 4
+        return max(1, min(int(os.environ.get('XA_GRAPH_STEPS', dflt)), self.FUSED_GROUP_MAX))
 
     def fused_train_steps(self, n):
         """n train steps: groups of graph_steps() steps as one replay of the multi-step
@@ -436,13 +445,15 @@ class A2C(ExecutorActorCritic, OnPolicy):
         peer health check) runs after its group."""
         while n > 0:
             g = self._graph if self.use_graph else None
-            S = self._graph_S if g is not None and len(g) > 3 else 1
-            if S <= 1 or n < S:
+            sizes = getattr(self, '_graph_sizes', []) if g is not None and len(g) > 3 else []
+            j = next((j for j, s in enumerate(sizes) if s <= n), None)
+            if j is None:
                 self.fused_train_step()
                 n -= 1
                 continue
+            S = sizes[j]
             self._sync_stats_copy()
-            g[3].replay()
+            g[3 + j].replay()
             for i in range(S):
                 self._count_update_replay()
                 self.steps += self.n_envs * self.n_steps

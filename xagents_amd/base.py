@@ -499,7 +499,7 @@ class BaseAgent(ABC):
             self._fold_item(self._stats_queue.pop(0))
 
     # steps folded behind one event: half the in-launch statistics slots (_lib.XA_PPO_STATS_SLOTS)
-    FUSED_GROUP_MAX = 4
+    FUSED_GROUP_MAX = 8
 
     def _close_fused_group(self):
         """One completion event behind the pending fused steps; fold the previous group

@@ -300,9 +300,9 @@ XA_DEV void dma_wait() {
   __syncthreads();
 }
 
-// (the row map is read BEFORE the first DMA is issued: loads, stores and LDS-DMA retire in
-// issue order, so a row-map load between two DMAs would make the second wait for the first)
-typedef __attribute__((address_space(1))) const int64_t gi64;
+// (the row map is the block's LDS slot table td3_slots, filled once at the launch start: the
+// sampled slots may live in mapped host memory, read once per block; it is read BEFORE the
+// first DMA is issued)
 
 // CR tile of nrow (64 / 16) rows: tile row r = source row (rowmap ? rowmap[r] : r0 + r) of a
 // row-major matrix (ld floats, K % 4 == 0 and ld % 4 == 0), k < K; rows >= vrows and k >= K
@@ -317,7 +317,7 @@ XA_DEV void dma_cr(float* dst, int nrow, const float* base, int64_t ld, int r0,
 #pragma unroll
   for (int rb = 0; rb < 4; ++rb) {
     const int row = 16 * rb + rr;
-    gr[rb] = (rb < nrb && row < vrows) ? (rowmap ? ((gi64*)rowmap)[row] : (int64_t)(r0 + row)) : -1;
+    gr[rb] = (rb < nrb && row < vrows) ? (rowmap ? rowmap[row] : (int64_t)(r0 + row)) : -1;
   }
   for (int t = w; t < ninst; t += 4) {
     const int kc = t / nrb, rb = t - kc * nrb, k = 16 * kc + kk;
@@ -343,7 +343,7 @@ XA_DEV void dma_km(float* dst, int wd, const float* base, int64_t ld, int c0,
 #pragma unroll
     for (int m = 0; m < kKmMax; ++m) {
       const int k = (w + 4 * m) * rows_per + kr;
-      gr[m] = (w + 4 * m < ninst && k < vK) ? ((gi64*)rowmap)[k] : -1;
+      gr[m] = (w + 4 * m < ninst && k < vK) ? rowmap[k] : -1;
     }
 #pragma unroll
     for (int m = 0; m < kKmMax; ++m) {
@@ -719,7 +719,7 @@ __device__ __noinline__ bool fwd_tile(const int64_t* slots) {
   float wv[4][4];
   head_weights(h, c, st, wv);
   if (dma_src(x) && (K & 3) == 0)
-    dma_cr(s.A, kTR, x.p0, x.ld0, r0, x.slot0 ? slots + r0 : nullptr, nrows, K, Kp, x.coh0);
+    dma_cr(s.A, kTR, x.p0, x.ld0, r0, x.slot0 ? td3_slots + r0 : nullptr, nrows, K, Kp, x.coh0);
   else if (quad_src(x, 0) && (K & 3) == 0)
     xgather4(x, r0, kTR, nrows, 0, K, Kp, [&](int r, int k, f32x4v v) {
       *reinterpret_cast<f32x4v*>(s.A + cr_idx(r, k, kTR)) = v;
@@ -862,7 +862,7 @@ __device__ __noinline__ Acc4 dw_tile_lds(const int64_t* slots) {
   const int Kp = pad16(B);
   const AuxRegs ax = aux_load(d, j0, nc, 0, B);
   if (dma_src(x) && (ni & 3) == 0 && (i0 & 3) == 0)
-    dma_km(s.A, kRows, x.p0, x.ld0, i0, x.slot0 ? slots : nullptr, B, ni, Kp, x.coh0);
+    dma_km(s.A, kRows, x.p0, x.ld0, i0, x.slot0 ? td3_slots : nullptr, B, ni, Kp, x.coh0);
   else if (quad_src(x, i0) && (ni & 3) == 0)
     xgather4(x, 0, Kp, B, i0, ni, kRows, [&](int k, int i, f32x4v v) {
       *reinterpret_cast<f32x4v*>(s.A + k * kRows + i) = v;

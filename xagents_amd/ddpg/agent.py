@@ -229,12 +229,25 @@ class DDPG(OffPolicy):
         executor's ~40-90 launches, captured once per phase and replayed as hipGraphs."""
         fused = self._fused_args()
         for gradient_step in range(int(gradient_steps)):
-            self.replay.upload_slots(self.replay.sample_slots())
             policy = gradient_step % self.policy_delay == 0
+            if fused is not None and not self.distributed and self._staged_slots_ok():
+                # the launch reads the sampled slots from one of two mapped pinned buffers
+                # (no upload copy); one captured graph per (phase, buffer)
+                i = self._stage_fused_slots(self.replay.sample_slots())
+                fused.slots = self._fslots['dev'][i]
+                if self._fused_graph():
+                    self._run_phase(('fused_actor' if policy else 'fused') + f'@{i}',
+                                    lambda p=policy: self._fused_step(p))
+                else:
+                    self._fused_step(policy)
+                self._fslots['ev'][i].record()
+                continue
+            self.replay.upload_slots(self.replay.sample_slots())
             if fused is not None and self.distributed:
                 self._fused_dp_step(policy)
                 continue
             if fused is not None:
+                fused.slots = self.replay.slots.data_ptr()
                 self._run_phase('fused_actor' if policy else 'fused',
                                 lambda p=policy: self._fused_step(p))
                 continue
@@ -243,6 +256,49 @@ class DDPG(OffPolicy):
                 self._run_phase('actor', self._actor_phase)
 
     # ---- the fused gradient step (xa_td3_update) -------------------------------------
+    def _staged_slots_ok(self):
+        """(XA_TD3_STAGED_SLOTS=0: the upload copy into the device slot buffer instead)"""
+        if '_sslots' not in self.__dict__:
+            import os
+            self._sslots = os.environ.get('XA_TD3_STAGED_SLOTS', '1') != '0' and \
+                torch.device(self.device).type == 'cuda'
+        return self._sslots
+
+    def _fused_graph(self):
+        """Launch the one-kernel gradient step directly (default) or replay it from a captured
+        hipGraph (XA_TD3_GRAPH=1): a replay adds its own submission latency in front of the
+        kernel (C5 gradient step 0.128 -> 0.121 ms launched directly,
+        profiles/r06p_td3_graph_ab.txt)."""
+        if '_fgraph' not in self.__dict__:
+            import os
+            self._fgraph = os.environ.get('XA_TD3_GRAPH', '0') == '1'
+        return self._fgraph
+
+    def _stage_fused_slots(self, slots):
+        """The gradient step's sample slots into one of two mapped pinned buffers, which the
+        fused launch reads over the host link (each workgroup once, into its LDS slot
+        table), replacing the host -> device copy launch. Alternates buffers; the launch
+        that read this buffer two gradient steps ago must have finished (its event).
+        Returns the buffer index."""
+        st = self.__dict__.get('_fslots')
+        if st is None:
+            bufs, devs = [], []
+            for _ in range(2):
+                t = torch.zeros(len(slots), dtype=torch.int64).pin_memory()
+                dp = ctypes.c_void_p()
+                call('xa_host_device_pointer', ctypes.c_void_p(t.data_ptr()), ctypes.byref(dp))
+                bufs.append(t)
+                devs.append(dp.value)
+            st = self._fslots = {'buf': bufs, 'dev': devs, 'i': 0,
+                                 'ev': [torch.cuda.Event(), torch.cuda.Event()], 'used': [False] * 2}
+        i = st['i']
+        if st['used'][i]:
+            st['ev'][i].synchronize()
+        st['buf'][i].numpy()[:] = slots
+        st['used'][i] = True
+        st['i'] = i ^ 1
+        return i
+
     def _shared_blocks(self):
         """Grid of the persistent TD3 launches (0 = the kernel's default, one workgroup per
         CU up to 256). Ranks sharing one GPU each take 3/4 of their share of
@@ -460,14 +516,51 @@ class DDPG(OffPolicy):
         self.__dict__['_warm'] = set()
         self.__dict__.pop('_fused', None)  # (and into the fused step's arguments)
 
+    def _setup_step_stage(self):
+        """The [done row | episode-return row] the captured env step writes: a mapped pinned
+        host buffer the kernel stores into and the host reads after one event (default), or
+        (XA_TD3_HOST_STAGE=0) a device buffer copied into the statistics rows and read back
+        with a D2H copy each step."""
+        import os
+        self._stage_host = os.environ.get('XA_TD3_HOST_STAGE', '1') != '0' and \
+            torch.device(self.device).type == 'cuda'
+        if self._stage_host:
+            self._stage = torch.zeros(2, self.n_envs, dtype=torch.float32).pin_memory()
+            dp = ctypes.c_void_p()
+            call('xa_host_device_pointer', ctypes.c_void_p(self._stage.data_ptr()), ctypes.byref(dp))
+            self._stage_ptrs = (dp.value, dp.value + 4 * self.n_envs)
+            self._stage_ev = torch.cuda.Event()
+            self._stage_rows = 0
+        else:
+            self._stage = torch.zeros(2, self.n_envs, dtype=torch.float32, device=self.device)
+            self._stage_ptrs = (self._stage[0].data_ptr(), self._stage[1].data_ptr())
+        self._stage_done, self._stage_epret = self._stage[0], self._stage[1]
+        # the env step's two launches launched directly, or (XA_TD3_STEP_GRAPH=1) replayed
+        # from a hipGraph
+        # (direct by default: C5 0.1069 -> 0.1047 ms per step, profiles/r06r_td3_step_graph_ab.txt)
+        self._step_graph = os.environ.get('XA_TD3_STEP_GRAPH', '0') == '1'
+
+    def _fold_step_row(self, d, e):
+        """One step's episode statistics (host rows), env order as step_envs; the device
+        status word is checked every _STATS_ROWS steps (as the statistics flush does)."""
+        for i in np.nonzero(d)[0]:
+            if self.history_checkpoint:
+                self.update_history(float(e[i]))
+            self.total_rewards.append(float(e[i]))
+            self.games += 1
+            self.done_envs += 1
+        self._stage_rows += 1
+        if self._stage_rows == self._STATS_ROWS:
+            self._stage_rows = 0
+            self._device_checks()
+
     def _step_phase(self):
         """get_step_actions + one xa_replay_env_step (ring append) writing the step's
         done / episode-return row into fixed staging rows (graph-capturable)."""
         actions = self.get_step_actions()
         a = self._step_args
         self.replay.fill_step_args(a, actions)
-        a.out_dones = self._stage_done.data_ptr()
-        a.done_epret = self._stage_epret.data_ptr()
+        a.out_dones, a.done_epret = self._stage_ptrs
         call('xa_replay_env_step', ctypes.byref(a), stream())
 
     def train_step(self):
@@ -483,19 +576,26 @@ class DDPG(OffPolicy):
             dones = self._host_row_dones(row)
         else:
             if not hasattr(self, '_stage'):
-                # [done row | episode-return row] written by the captured env step
-                self._stage = torch.zeros(2, self.n_envs, dtype=torch.float32,
-                                          device=self.device)
-                self._stage_done, self._stage_epret = self._stage[0], self._stage[1]
-            self._run_phase('step', self._step_phase)
-            r = self._st_row
-            self._st[r].copy_(self._stage)  # both rows in one copy
+                self._setup_step_stage()
+            if self._step_graph:
+                self._run_phase('step', self._step_phase)
+            else:
+                self._step_phase()
+            if self._stage_host:
+                # the step's rows land in mapped host memory: one event wait, no copies
+                self._stage_ev.record()
+                self._stage_ev.synchronize()
+                dones = self._stage[0].numpy().copy()
+                self._fold_step_row(dones, self._stage[1].numpy())
+            else:
+                r = self._st_row
+                self._st[r].copy_(self._stage)  # both rows in one copy
+                self._st_row += 1
+                if self._st_row == self._STATS_ROWS:
+                    self._flush_offpolicy_stats()
+                dones = self._stage_done.cpu().numpy()
             self.replay.appended()
-            self._st_row += 1
-            if self._st_row == self._STATS_ROWS:
-                self._flush_offpolicy_stats()
             self.steps += self.n_envs
-            dones = self._stage_done.cpu().numpy()
         if self.distributed:
             # every rank runs the gradient steps of the union of the ranks' finished
             # episodes, in global (rank-major) env order -- what one process stepping all
