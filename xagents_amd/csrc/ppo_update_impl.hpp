@@ -158,6 +158,13 @@ XA_DEV void st_row(__amdgpu_buffer_rsrc_t r, uint32_t off, float v0, float v1, u
 XA_DEV RowG ld_row(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return __builtin_bit_cast(f32x2v, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, kAuxSc1));
 }
+// one tagged word of a row (byte offset off): every word carries its own tag parity, so a
+// pair's two words may come from two stores
+XA_DEV void st_row1(__amdgpu_buffer_rsrc_t r, uint32_t off, float v, unsigned tag, bool wt) {
+  const unsigned u = __float_as_uint(row_tagged(v, tag));
+  if (wt) __builtin_amdgcn_raw_buffer_store_b32(u, r, off, 0, kAuxSc1);
+  else __builtin_amdgcn_raw_buffer_store_b32(u, r, off, 0, 0);
+}
 XA_DEV bool row_ok(const RowG& v, unsigned tag) {
   return ((__float_as_uint(v[0]) ^ tag) & 1u) == 0u && ((__float_as_uint(v[1]) ^ tag) & 1u) == 0u;
 }
@@ -1057,7 +1064,6 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
   for (int i = P + tid; i < PP; i += 256) srow[i] = 0.0f;  // the pad stays zero
   // granule tags: unique per (launch, step)
   auto tag_of = [&](int k) { return gen * (unsigned)K + (unsigned)k + 1u; };
-  int* const fail = &U.flag;
   // Flat gather of nrow rows x ncol pair columns in ONE poll round (row r's pair column c
   // at byte offset base(r) + 16 c of `r`), staged as f32 pairs in LDS scratch (the W2
   // tiles: dead between the row write and phase C's refresh); summed afterwards in
@@ -1159,11 +1165,22 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
       XA_STAMP(36);
     }
     if (b >= n_tiles) w2_out(acc);  // no tile of this minibatch: a zero row
-    // the rest of the row, staged in LDS and stored coalesced behind a barrier (measured:
-    // storing it straight from the lanes' registers as scattered pairs made the step slower,
-    // DESIGN.md section 5)
+    // the rest of the row: 32-sample tiles store it straight from the lanes that hold its
+    // values, one tagged word each, plus the pad words behind P (no LDS staging, no barrier:
+    // C2 step 14.9 -> 14.4 us); 16-sample tiles stage it in LDS and store it coalesced
+    // behind a barrier (the scattered word stores made their step slower: 7.5 -> 7.9 us,
+    // profiles/r06v_ppo_update_trace.txt)
+    constexpr bool kRowDirect = TS == S;
 #ifndef XA_ABL_ROW
-    pt_write_row_rest<OBS, A>(acc, [&](int x, float v) { srow[x] = v; }, p.loss_out != nullptr);
+    if constexpr (kRowDirect) {
+      pt_write_row_rest<OBS, A>(acc, [&](int x, float v) {
+        st_row1(rows_r, (uint32_t)(((size_t)b * NP2 * 2 + x) * 4), v, tag, row_wt);
+      }, p.loss_out != nullptr);
+      if (tid < PP - P)
+        st_row1(rows_r, (uint32_t)(((size_t)b * NP2 * 2 + P + tid) * 4), 0.0f, tag, row_wt);
+    } else {
+      pt_write_row_rest<OBS, A>(acc, [&](int x, float v) { srow[x] = v; }, p.loss_out != nullptr);
+    }
 #endif
     XA_STAMP(44);
     XA_TRACE_PT(b, k, 1);
@@ -1174,15 +1191,20 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
       lo[2] = acc.l_ent;
       lo[3] = acc.l_cnt;
     }
-    __syncthreads();
-    for (int c = H * H / 2 + tid; c < NP2; c += 256)
-      st_row(rows_r, (uint32_t)((size_t)b * NP2 + c) * kRowPB, srow[2 * c], srow[2 * c + 1], tag,
-             row_wt);
+    if constexpr (!kRowDirect) {
+      __syncthreads();
+      for (int c = H * H / 2 + tid; c < NP2; c += 256)
+        st_row(rows_r, (uint32_t)((size_t)b * NP2 + c) * kRowPB, srow[2 * c], srow[2 * c + 1], tag,
+               row_wt);
+    } else if constexpr (BF == 0) {
+      // (the generic kernels' flat phase-B gather stages rows in the 32-sample tile's
+      // activation buffers, which the slowest wave's dH1 phase may still read)
+      __syncthreads();
+    }
     XA_STAMP(45);
     XA_TRACE_PT(b, k, 2);
     fetch_tile(k + 1, b);  // the next step's first tile, while the other blocks finish
     XA_STAMP(37);
-    if (tid == 0) *fail = 0;
     if (two_level) {
       // ---- level 1, inside the XCD: its members' rows (in this XCD's L2) -> this XCD's
       // f64 partial of pair columns [xc0, xc0 + xnc), published write-through ----
