@@ -147,15 +147,17 @@ def test_dqn_fit_epsilon_and_target_sync(device):
 
 
 @pytest.mark.parametrize('double', [False, True])
-def test_dqn_captured_learner_matches_eager(device, double):
+def test_dqn_captured_learner_matches_eager(device, double, monkeypatch):
     """The learner phase (gather -> TD gradient -> backward -> Adam) replayed as a hipGraph
-    from the third train step on gives bit-identical weights to eager launches."""
+    from the third train step on (XA_DQN_LEARN_GRAPH=1; direct launches are the default)
+    gives bit-identical weights to eager launches."""
     import random
     from xagents_amd import DQN
     from xagents_amd.envs import create_envs
     from xagents_amd.utils.common import create_buffers, create_model
     out = []
     for use_graph in (False, True):
+        monkeypatch.setenv('XA_DQN_LEARN_GRAPH', '1' if use_graph else '0')
         np.random.seed(4)
         random.seed(4)
         envs = create_envs('PongNoFrameskip-v4', 2, device=device, seed=3)

@@ -281,6 +281,13 @@ for step in "$@"; do
         XA_GRAPH_STEPS=4 run gs4_$r 200 $B
       done
       python tools/bench_brief.py gpurun_out/${T}_gs8_*.out gpurun_out/${T}_gs4_*.out ;;
+    lgab)
+      # DQN learner phase: hipGraph replay vs direct launches (XA_DQN_LEARN_GRAPH), C3 lines
+      B="python bench.py --config c3 --steps 30 --warmup 5 --cpu-baseline-seconds 0"
+      for r in 1 2; do
+        run lg_on$r 300 $B
+        XA_DQN_LEARN_GRAPH=0 run lg_off$r 300 $B
+      done ;;
     c2g)
       # C2 update grid A/B: fewer workgroups with more tiles each (XA_PPO_MAX_BLOCKS)
       for G in ${C2_GS:-256 128}; do

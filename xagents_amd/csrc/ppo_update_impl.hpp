@@ -1610,7 +1610,10 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
     __hip_atomic_store((gu32*)(ws.ctl + kWin + (par ^ 1u)), 0u, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
   }
-  if (b == 0) {
+  // theta / m / v out: every block holds the same final values, so block b stores the
+  // slices of threads tid = b, b + G, ... (all blocks share the stores instead of block 0
+  // issuing every one of them at the launch's end); block 0 alone the counters
+  if (tid % G == b % 256) {
     ps.store(p.theta, wv, rv);
     float mw[16], mr[RPT], vw[16], vr[RPT];
 #pragma unroll
@@ -1628,6 +1631,8 @@ __global__ __launch_bounds__(256) void ppo_update_kernel(XaPpoUpdateArgs p, Ws w
     }
     ps.store(p.adam_m, mw, mr);
     ps.store(p.adam_v, vw, vr);
+  }
+  if (b == 0) {
     if (tid == 0) {
       *p.adam_step = t0 + K;
       // every block read the counter before its last gradient row, which block 0 has

@@ -339,7 +339,7 @@ class DQN(OffPolicy):
     def _run_learn(self):
         """Eager once, then captured and replayed as a hipGraph (the sample slots live in a
         fixed device buffer); data-parallel steps stay eager (torch collective)."""
-        if not getattr(self, 'use_graph', True) or self.distributed:
+        if not getattr(self, 'use_graph', True) or self.distributed or not self._learn_graph():
             self._learn_phase()
         elif getattr(self, '_lgraph', None) is not None:
             self._lgraph.replay()
@@ -352,6 +352,15 @@ class DQN(OffPolicy):
         else:
             self._learn_phase()
             self._lwarm = True
+
+    def _learn_graph(self):
+        """Launch the learner phase directly (default: between the eager acting launches a
+        graph replay adds its own transition latency; C3 0.4886 -> 0.4840 ms per step,
+        profiles/r06zb_dqn_learn_graph_ab.txt) or replay it from a hipGraph
+        (XA_DQN_LEARN_GRAPH=1)."""
+        if '_lg_on' not in self.__dict__:
+            self._lg_on = os.environ.get('XA_DQN_LEARN_GRAPH', '0') == '1'
+        return self._lg_on
 
     def _on_lr_change(self):
         self._lgraph = None  # the learning rate is baked into the Adam launch
