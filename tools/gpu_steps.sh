@@ -288,6 +288,13 @@ for step in "$@"; do
         run lg_on$r 300 $B
         XA_DQN_LEARN_GRAPH=0 run lg_off$r 300 $B
       done ;;
+    xmapab)
+      # fused dense dW + Adam: XCD-aware 1-D tile order vs the 2-D grid (XA_GEMM_ADAM_XMAP), C3
+      B="python bench.py --config c3 --steps 30 --warmup 5 --cpu-baseline-seconds 0"
+      for r in 1 2; do
+        run xm_on$r 300 $B
+        XA_GEMM_ADAM_XMAP=0 run xm_off$r 300 $B
+      done ;;
     c2g)
       # C2 update grid A/B: fewer workgroups with more tiles each (XA_PPO_MAX_BLOCKS)
       for G in ${C2_GS:-256 128}; do

@@ -68,6 +68,8 @@ struct XaGemmK {
   int vec_a, vec_b;
   int ones_m;  // a_ones_row: the constant-one row (M - 1), else -1 (gemm_kernel only)
   XaAdamApply ad;  // (gemm_kernel<..., ADAM = true> only) the epilogue's Adam step
+  // (ADAM only) > 0: 1-D grid, XCD-aware tile order over xmap_nt column tiles (below)
+  int xmap_nt;
 };
 
 template <bool U8>
@@ -102,7 +104,20 @@ __global__ __launch_bounds__(256, ADAM ? 4 : 1) void gemm_kernel(XaGemmK kargs) 
   __shared__ __attribute__((aligned(16))) float Bs[2][BK * LDB];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w >> 1, wn = w & 1;
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  int bx = (int)blockIdx.x, by = (int)blockIdx.y;
+  if constexpr (ADAM) {
+    if (kargs.xmap_nt > 0) {
+      // consecutive workgroups go to consecutive XCDs, so ids x + 8 (n + xmap_nt j) all run
+      // on XCD x: give them the xmap_nt column tiles of row tile x + 8 j -- the row tile's A
+      // slice (the layer input, shared by every column tile) is then read into one L2, not
+      // once per column tile from the fabric
+      const int id = (int)blockIdx.x, r = id >> 3;
+      by = r % kargs.xmap_nt;
+      bx = (id & 7) + 8 * (r / kargs.xmap_nt);
+      if (bx * BM >= g.M) return;
+    }
+  }
+  const int m0 = bx * BM, n0 = by * BN;
   const int tiles_k = (g.K + BK - 1) / BK;
   const int per = (tiles_k + (int)gridDim.z - 1) / (int)gridDim.z;
   const int k_begin = blockIdx.z * per * BK;
@@ -1692,7 +1707,7 @@ extern "C" size_t xa_gemm_workspace_floats(int M, int N, int K, int splits) {
 // the kernel argument: the public args + the host's vectorisation verdicts (XaGemmK)
 static XaGemmK kernel_args(const XaGemmArgs& g) {
   const bool ak = g.a_pk == 1 && g.a_rk == 1, bn = g.b_ns == 1, u8 = g.a_u8 != 0;
-  XaGemmK kg{g, 0, 0, g.a_ones_row ? g.M - 1 : -1, XaAdamApply{}};
+  XaGemmK kg{g, 0, 0, g.a_ones_row ? g.M - 1 : -1, XaAdamApply{}, 0};
   const int m_real = g.a_ones_row ? g.M - 1 : g.M;
   if (g.a != nullptr && ((uintptr_t)g.a & (u8 ? 3 : 15)) == 0) {
     const bool rows4 = g.a_rm % 4 == 0 && (g.a_pm == 1 || g.a_sm % 4 == 0);
@@ -1724,7 +1739,16 @@ extern "C" int xa_gemm_adam(const XaGemmArgs* p, const XaAdamApply* ad, void* st
                "xa_gemm_adam: theta / m / v / step missing or not 16-B aligned");
   XaGemmK kg = kernel_args(g);
   kg.ad = *ad;
-  dim3 grid((g.M + BM - 1) / BM, (g.N + BN - 1) / BN, 1);
+  const int mt = (g.M + BM - 1) / BM, nt = (g.N + BN - 1) / BN;
+  static const bool xmap = [] {
+    const char* e = getenv("XA_GEMM_ADAM_XMAP");
+    return !(e && e[0] == '0');
+  }();
+  dim3 grid(mt, nt, 1);
+  if (xmap) {  // the XCD-aware 1-D tile order (gemm_kernel)
+    kg.xmap_nt = nt;
+    grid = dim3(8 * nt * ((mt + 7) / 8), 1, 1);
+  }
   hipLaunchKernelGGL((gemm_kernel<false, true, false, true>), grid, dim3(256), 0,
                      (hipStream_t)stream, kg);
   XA_CHECK_LAUNCH("xa_gemm_adam");
