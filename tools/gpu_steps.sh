@@ -295,6 +295,14 @@ for step in "$@"; do
         run xm_on$r 300 $B
         XA_GEMM_ADAM_XMAP=0 run xm_off$r 300 $B
       done ;;
+    c2gs)
+      # C2 train steps per graph replay: 8 (forced) vs the default (4 above 4096 env-steps)
+      B="python bench.py --n-envs 256 --no-c2 --steps 24 --warmup 5 --cpu-baseline-seconds 0 --no-secondary --no-dynamics"
+      for r in 1 2; do
+        XA_GRAPH_STEPS=8 run c2gs8_$r 200 $B
+        run c2gs4_$r 200 $B
+      done
+      python tools/bench_brief.py gpurun_out/${T}_c2gs*.out ;;
     c2g)
       # C2 update grid A/B: fewer workgroups with more tiles each (XA_PPO_MAX_BLOCKS)
       for G in ${C2_GS:-256 128}; do

@@ -431,11 +431,10 @@ class A2C(ExecutorActorCritic, OnPolicy):
         if self.executor_path or getattr(self, 'update_mode', None) != 'persistent' or \
                 not getattr(self, '_stats_fused', False) or self.stats_side_stream:
             return 1
-        # default: 8 steps per replay for small rollouts (16 envs: 0.1453 -> 0.1435 ms per
-        # step), 4 when a step's host-side statistics fold is heavy (256 envs: 8 per replay
-        # measured 0.27 -> 0.32 ms per step; profiles/r06t_graph_steps_ab.txt)
-        dflt = 8 if self.n_envs * self.n_steps <= 4096 else 4
-        return max(1, min(int(os.environ.get('XA_GRAPH_STEPS', dflt)), self.FUSED_GROUP_MAX))
+        # default 8 steps per replay (16 envs 0.1453 -> 0.1435 ms per step,
+        # profiles/r06t_graph_steps_ab.txt; 256 envs 0.2553 -> 0.2515 ms once the host's
+        # statistics fold was vectorised, profiles/r06zh_c2_graph_steps_ab.txt)
+        return max(1, min(int(os.environ.get('XA_GRAPH_STEPS', 8)), self.FUSED_GROUP_MAX))
 
     def fused_train_steps(self, n):
         """n train steps: groups of graph_steps() steps as one replay of the multi-step
