@@ -316,7 +316,8 @@ class DQN(OffPolicy):
         if self._pinned_slots():
             self.replay.stage_slots(self.replay.sample_slots())
             self._run_learn()
-            self.replay.stage_consumed()
+            if self.replay._stage_open:  # (graph replay: no event inside the capture)
+                self.replay.stage_consumed()
         else:
             self.replay.upload_slots(self.replay.sample_slots())
             self._run_learn()
@@ -327,12 +328,25 @@ class DQN(OffPolicy):
                 torch.device(self.device).type == 'cuda'
         return self._pslots
 
+    def _stage_early(self):
+        """Record the staged slots' completion event right behind the gather (default;
+        XA_DQN_STAGE_EARLY=0: behind the whole learner phase, for A/B)."""
+        if '_se_on' not in self.__dict__:
+            self._se_on = os.environ.get('XA_DQN_STAGE_EARLY', '1') != '0'
+        return self._se_on
+
     def _learn_phase(self):
         """gather the sampled batch -> TD gradient -> CNN backward -> Keras Adam."""
         B = self.batch_size
         r = self.replay
         src = (r.stage_ptr(), r.slots.numel()) if self._pinned_slots() else r.slots
         r.gather(src, self.xb[:B], self.b_act, self.b_rew, self.b_done, self.xb[B:])
+        if self._pinned_slots() and self._stage_early() and \
+                not torch.cuda.is_current_stream_capturing():
+            # the gather is the staged slots' only reader: the next step's stage_slots waits
+            # for it alone, not for the whole learner phase, so the host enqueues the next
+            # acting launches while this backward runs (no idle gap between steps)
+            r.stage_consumed()
         self._td_grad()
         self._apply()
 
