@@ -101,6 +101,51 @@ def test_gemm_ones_row_weight_and_bias_gradient(device, M, N, K, beta):
     _close(C.cpu().numpy(), ref)
 
 
+@pytest.mark.parametrize('M,N,K', [(37632, 512, 64), (128, 68, 33), (129, 68, 33),
+                                   (3000, 512, 40), (64, 8, 100)])
+def test_gemm_adam_is_gemm_then_adam_bit_for_bit(device, M, N, K):
+    """xa_gemm_adam (the [W; b] weight gradient with Keras Adam in its epilogue, XCD-ordered
+    1-D tile grid) against the gradient GEMM (same 64 x 64 kernel, one split) followed by
+    xa_clip_adam with no clip: parameters, moments and the written raw gradient
+    bit-identical; 2 chained steps so the second reads moments the first wrote. Covers the
+    C3 shape (37632 x 512: 4712 tiles), ragged M / K, the scalar A loader (M + 1 = 130) and
+    grids padded past the last row tile."""
+    from xagents_amd import _lib, kernels
+    from xagents_amd.layers import adam_apply, fold_bias_ok, gemm, gemm_adam
+    if not fold_bias_ok(M, N, K):
+        pytest.skip('shape not on the 64 x 64 kernel')
+    rng = np.random.default_rng(M + N + K)
+    X = torch.from_numpy(rng.normal(size=(K, M)).astype(np.float32)).to(device)
+    dZ = torch.from_numpy(rng.normal(size=(K, N)).astype(np.float32)).to(device)
+    th0 = rng.normal(size=(M + 1) * N).astype(np.float32)
+
+    class Opt:
+        learning_rate, beta_1, beta_2, epsilon = 1e-3, 0.9, 0.999, 1e-7
+
+    kw = dict(a_m=(1, 1, 0), a_k=(1, M, 0), b_ks=N, b_ns=1, ldc=N, a_ones_row=True)
+    res = []
+    for fused in (False, True):
+        th = torch.from_numpy(th0.copy()).to(device)
+        m = torch.zeros_like(th)
+        v = torch.zeros_like(th)
+        step = torch.zeros(1, dtype=torch.int32, device=device)
+        g = torch.empty_like(th)
+        for _ in range(2):
+            _lib.call('xa_adam_step_bump', step.data_ptr(), _lib.stream())
+            if fused:
+                gemm_adam(M + 1, N, K, X.data_ptr(), dZ.data_ptr(), g.data_ptr(),
+                          adam_apply(th, m, v, step, Opt, 0), **kw)
+            else:
+                gemm(M + 1, N, K, X.data_ptr(), dZ.data_ptr(), g.data_ptr(), splits=1,
+                     workspace=torch.empty(1, device=device), **kw)
+                kernels.clip_adam(th, m, v, g, step, Opt.learning_rate, Opt.beta_1,
+                                  Opt.beta_2, Opt.epsilon, clip_norm=0.0)
+        torch.cuda.synchronize()
+        res.append([t.cpu().numpy() for t in (th, m, v, g)])
+    for a, b in zip(*res):
+        np.testing.assert_array_equal(a, b)
+
+
 @pytest.mark.parametrize('M,N,K', [(70, 45, 33), (260, 300, 77), (700, 60, 45), (60, 400, 50)])
 def test_gemm_transposes_gate_beta_u8(device, M, N, K):
     from xagents_amd.layers import gemm
