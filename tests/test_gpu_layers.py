@@ -422,12 +422,14 @@ def _rel_err(got, want):
     return float(np.linalg.norm(np.asarray(got, np.float64) - want) / np.linalg.norm(want))
 
 
-@pytest.mark.parametrize('B,u8', [(1, True), (5, True), (37, False), (128, True)])
+@pytest.mark.parametrize('B,u8', [(1, True), (5, True), (37, False), (32, True), (64, True),
+                                  (128, True)])
 def test_conv_stack_fused_forward(device, B, u8, monkeypatch):
     """xa_conv_stack_fwd (the NatureCNN Conv1D stack in one launch) against the per-layer
-    GEMM path and the f64 restatement: every hidden activation, ragged last groups of 16
-    frame rows (B = 1, 5, 37), f32 and uint8 frames; keep_hidden=False leaves the features
-    bit-identical."""
+    GEMM path and the f64 restatement: every hidden activation, f32 and uint8 frames, row
+    shares that end in partial chunks of 16 frame rows (B = 1: one row per workgroup; 5, 37;
+    32: 10-11 rows per workgroup; 64: 16 + 5; 128: 16 + 16 + 10); keep_hidden=False leaves the
+    features bit-identical."""
     import sys
     sys.path.insert(0, str(ROOT / 'oracle'))
     import nets_f64 as O
@@ -455,7 +457,8 @@ def test_conv_stack_fused_forward(device, B, u8, monkeypatch):
 
 
 @pytest.mark.parametrize('B,Bb,u8,acc', [(2, 2, True, False), (5, 3, True, True),
-                                         (37, 37, False, False), (64, 64, True, False)])
+                                         (37, 37, False, False), (64, 64, True, False),
+                                         (128, 128, True, False)])
 def test_conv_stack_fused_backward(device, B, Bb, u8, acc, monkeypatch):
     """xa_conv_stack_bwd (the stack's weight / bias gradients in one launch + a fixed-order
     reduce) against the per-layer GEMM backward on the same forward: all six parameter

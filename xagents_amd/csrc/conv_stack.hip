@@ -64,8 +64,15 @@ XA_DEV f32x4 load_x4(const void* x, int x_u8, int rows, int row0, int i) {
   }
   return v;
 }
-XA_DEV f32x4 load_x4(const XaConvStackArgs& p, int row0, int i) {
-  return load_x4(p.x, p.x_u8, p.rows, row0, i);
+
+// workgroup blockIdx.x's share [s0, s1) of `rows` sequences: even shares over the grid (sizes
+// differ by at most one), so a batch that is not a multiple of CR per workgroup leaves no
+// workgroup with a whole extra chunk (64 frames = 5376 rows on 256 workgroups: 16 + 5 rows
+// each, where one 16-row group per workgroup plus 80 second groups took two group times)
+XA_DEV void stack_share(int rows, int& s0, int& s1) {
+  const int64_t n = gridDim.x, b = blockIdx.x;
+  s0 = (int)((int64_t)rows * b / n);
+  s1 = (int)((int64_t)rows * (b + 1) / n);
 }
 
 XA_DEV void store_x4(float* xs, int i, f32x4 v) {
@@ -98,15 +105,21 @@ __global__ __launch_bounds__(512) void conv_stack_fwd_kernel(XaConvStackArgs p) 
   const int n1 = 16 * (w & 1) + i16;
   const float w1a = p.w1[q * CF1 + n1], w1b = p.w1[(4 + q) * CF1 + n1], bias1 = p.b1[n1];
 
-  const int G = (p.rows + CR - 1) / CR;
-  if ((int)blockIdx.x >= G) return;
-  for (int i = tid; i < XQ; i += 512) store_x4(xs, i, load_x4(p, (int)blockIdx.x * CR, i));
+  // this workgroup's rows [s0, s1): an even share of the batch, walked in chunks of <= CR
+  int s0, s1;
+  stack_share(p.rows, s0, s1);
+  if (s0 >= s1) return;
+  for (int i = tid; i < XQ; i += 512)
+    store_x4(xs, i, load_x4(p.x, p.x_u8, min(s0 + CR, s1), s0, i));
   __syncthreads();
 
-  for (int gi = blockIdx.x; gi < G; gi += gridDim.x) {
-    const int row0 = gi * CR;
+  for (int row0 = s0; row0 < s1; row0 += CR) {
+    const int nrow = min(CR, s1 - row0);
+    // M tiles holding any of the chunk's rows (the rest are skipped; a partial tile's rows
+    // past the chunk read zero inputs or stale LDS rows and are never stored)
+    const int nt1 = (nrow * CP1 + 15) / 16, nt2 = (nrow * CP2 + 15) / 16, nt3 = (nrow * CP3 + 15) / 16;
     // ---- conv1: x -> h1 (bias + ReLU) ----
-    for (int mt = w >> 1; mt < M1 / 16; mt += 4) {
+    for (int mt = w >> 1; mt < nt1; mt += 4) {
       const int m = 16 * mt + i16, r = m / CP1, pp = m - r * CP1;
       const float* xr = xs + r * CW0 + CS1 * pp + q;
       f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -117,16 +130,17 @@ __global__ __launch_bounds__(512) void conv_stack_fwd_kernel(XaConvStackArgs p) 
         const int mo = 16 * mt + 4 * q + e;
         const float v = fmaxf(acc[e] + bias1, 0.0f);
         h1s[mo * LD1 + n1] = v;
-        if (p.h1 && row0 + mo / CP1 < p.rows) p.h1[((int64_t)row0 * CP1 + mo) * CF1 + n1] = v;
+        if (p.h1 && mo < nrow * CP1) p.h1[((int64_t)row0 * CP1 + mo) * CF1 + n1] = v;
       }
     }
     __syncthreads();  // h1s complete; xs free
     // the next group's input, in flight during conv2
-    const int gn = gi + (int)gridDim.x;
-    const f32x4 xn = (gn < G && tid < XQ) ? load_x4(p, gn * CR, tid) : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    // ---- conv2: h1 -> h2, M tiles 0..4 (wh 0) / 5..8 (wh 1), two per pass ----
+    const int rn = row0 + CR;
+    const f32x4 xn = (rn < s1 && tid < XQ) ? load_x4(p.x, p.x_u8, min(rn + CR, s1), rn, tid)
+                                            : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    // ---- conv2: h1 -> h2, M tiles 0..4 (wh 0) / 5..8 (wh 1) of a full chunk, two per pass ----
     {
-      const int t0 = wh ? 5 : 0, nt = wh ? 4 : 5;
+      const int h0 = (nt2 + 1) / 2, t0 = wh ? h0 : 0, nt = wh ? nt2 - h0 : h0;
       for (int i = 0; i < nt; i += 2) {
         const bool two = i + 1 < nt;
         int base[2];
@@ -163,16 +177,16 @@ __global__ __launch_bounds__(512) void conv_stack_fwd_kernel(XaConvStackArgs p) 
             const int mo = 16 * (t0 + i + s) + 4 * q + e;
             const float v = fmaxf(acc[s][e] + bias2, 0.0f);
             h2s[mo * LD2 + n2] = v;
-            if (p.h2 && row0 + mo / CP2 < p.rows) p.h2[((int64_t)row0 * CP2 + mo) * CF2 + n2] = v;
+            if (p.h2 && mo < nrow * CP2) p.h2[((int64_t)row0 * CP2 + mo) * CF2 + n2] = v;
           }
         }
       }
     }
-    if (gn < G && tid < XQ) store_x4(xs, tid, xn);
-    __syncthreads();  // h2s complete; the next group's xs staged
-    // ---- conv3: h2 -> h3 (HBM), M tiles 0..3 (wh 0) / 4..6 (wh 1) ----
+    if (rn < s1 && tid < XQ) store_x4(xs, tid, xn);
+    __syncthreads();  // h2s complete; the next chunk's xs staged
+    // ---- conv3: h2 -> h3 (HBM), M tiles 0..3 (wh 0) / 4..6 (wh 1) of a full chunk ----
     {
-      const int t0 = wh ? 4 : 0, nt = wh ? 3 : 4;
+      const int h0 = (nt3 + 1) / 2, t0 = wh ? h0 : 0, nt = wh ? nt3 - h0 : h0;
       for (int i = 0; i < nt; i += 2) {
         const bool two = i + 1 < nt;
         int base[2];
@@ -205,7 +219,7 @@ __global__ __launch_bounds__(512) void conv_stack_fwd_kernel(XaConvStackArgs p) 
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int mo = 16 * (t0 + i + s) + 4 * q + e;
-            if (row0 + mo / CP3 < p.rows)
+            if (mo < nrow * CP3)
               p.h3[((int64_t)row0 * CP3 + mo) * CF3 + n2] = fmaxf(acc[s][e] + bias3, 0.0f);
           }
         }
@@ -290,7 +304,6 @@ __global__ __launch_bounds__(512) void conv_stack_bwd8_kernel(XaConvStackBwdArgs
   __shared__ __attribute__((aligned(16))) float d3s[CR * D3R * LD3];    // dZ3
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, q = lane >> 4, i16 = lane & 15;
   const int wc = w & 3, wh = w >> 2;
-  const int G = (p.rows + CR - 1) / CR;
   const int cb = 16 * wc + i16, par = wc >> 1, cd = 16 * (wc & 1) + i16;
   XA_STAMP_DECL  // diagnostic build only (-DXA_STAMPS, tools/conv_stack_stamps.py)
   XA_STAMP(7);
@@ -305,15 +318,20 @@ __global__ __launch_bounds__(512) void conv_stack_bwd8_kernel(XaConvStackBwdArgs
   for (int i = tid; i < CR * D3R * LD3 / 4; i += 512) reinterpret_cast<f32x4*>(d3s)[i] = z4;
   __syncthreads();
 
-  for (int gi = blockIdx.x; gi < G; gi += gridDim.x) {
-    const int row0 = gi * CR;
-    const int nrow = min(CR, p.rows - row0);
+  // this workgroup's rows [s0, s1) in chunks of <= CR (stack_share); M tiles past a chunk's
+  // rows are skipped: their staged rows are zero, so they would add exact zeros
+  int s0, s1;
+  stack_share(p.rows, s0, s1);
+  for (int row0 = s0; row0 < s1; row0 += CR) {
+    const int nrow = min(CR, s1 - row0);
+    const int nt1 = (nrow * CP1 + 15) / 16, nt2 = (nrow * CP2 + 15) / 16;
+    const int nt3 = (nrow * CP3 + 15) / 16, ntp = (nrow * HH + 15) / 16;
     {
       f32x4 v1[N81], v2[N82], v3[N83], vx;
       stage_load8<N81, CF1>(v1, p.h1 + (int64_t)row0 * CP1 * CF1, nrow * CP1, TOT1);
       stage_load8<N82, CF2>(v2, p.h2 + (int64_t)row0 * CP2 * CF2, nrow * CP2, TOT2);
       stage_load8<N83, CF3>(v3, p.dz3 + (int64_t)row0 * CP3 * CF3, nrow * CP3, TOT3);
-      vx = load_x4(p.x, p.x_u8, p.rows, row0, min(tid, XQ - 1));
+      vx = load_x4(p.x, p.x_u8, row0 + nrow, row0, min(tid, XQ - 1));
       stage_store8<N81, CF1, LD1>(h1s, v1, nrow * CP1, TOT1);
       stage_store8<N82, CF2, LD2, CP2, H2R, H2B>(h2s, v2, nrow * CP2, TOT2);
       stage_store8<N83, CF3, LD3, CP3, D3R, D3B>(d3s, v3, nrow * CP3, TOT3);
@@ -322,7 +340,7 @@ __global__ __launch_bounds__(512) void conv_stack_bwd8_kernel(XaConvStackBwdArgs
     __syncthreads();
     XA_STAMP(0);
     // ---- (a) dW3: k tiles 6 wh .. 6 wh + 5, n tile wc ----
-    for (int mb = 0; mb < M3 / 16; ++mb) {
+    for (int mb = 0; mb < nt3; ++mb) {
       float bq[4];
       int rb[4];
 #pragma unroll
@@ -361,7 +379,7 @@ __global__ __launch_bounds__(512) void conv_stack_bwd8_kernel(XaConvStackBwdArgs
     XA_STAMP(1);
     // ---- (b) dZ2 over h2: column tile wc, M tiles 0..4 (wh 0) / 5..8 (wh 1) ----
     {
-      const int t0 = wh ? 5 : 0, nt = wh ? 4 : 5;
+      const int h0 = (nt2 + 1) / 2, t0 = wh ? h0 : 0, nt = wh ? nt2 - h0 : h0;
       for (int i = 0; i < nt; i += 2) {
         int r[2], p2[2];
 #pragma unroll
@@ -405,7 +423,7 @@ __global__ __launch_bounds__(512) void conv_stack_bwd8_kernel(XaConvStackBwdArgs
     __syncthreads();  // dZ2 complete
     XA_STAMP(2);
     // ---- (c) dW2: k tiles 4 wh .. 4 wh + 3, n tile wc ----
-    for (int mb = 0; mb < M2 / 16; ++mb) {
+    for (int mb = 0; mb < nt2; ++mb) {
       float bq[4];
       int rb[4];
 #pragma unroll
@@ -444,12 +462,13 @@ __global__ __launch_bounds__(512) void conv_stack_bwd8_kernel(XaConvStackBwdArgs
     XA_STAMP(3);
     // ---- (d) dZ1 over h1: column (par, 16-channel tile) wc, M tiles 0..5 / 6..9 ----
     {
-      const int t0 = wh ? 6 : 0, nt = wh ? 4 : 6;
+      // 6 + 4 of a full chunk's 10 tiles: whole passes of two
+      const int h0 = min(ntp, 2 * ((ntp + 3) / 4)), t0 = wh ? h0 : 0, nt = wh ? ntp - h0 : h0;
       for (int i = 0; i < nt; i += 2) {
         int r[2], hh[2];
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-          const int m = 16 * (t0 + i + u) + i16;
+          const int m = 16 * (t0 + min(i + u, nt - 1)) + i16;
           r[u] = m / HH;
           hh[u] = m - r[u] * HH;
         }
@@ -475,13 +494,15 @@ __global__ __launch_bounds__(512) void conv_stack_bwd8_kernel(XaConvStackBwdArgs
           __builtin_amdgcn_sched_barrier(0);
         }
 #pragma unroll
-        for (int u = 0; u < 2; ++u)
+        for (int u = 0; u < 2; ++u) {
+          if (i + u >= nt) break;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int mo = 16 * (t0 + i + u) + 4 * q + e, ro = mo / HH, ho = mo - ro * HH;
             float* hp = h1s + (ro * CP1 + 2 * ho + par) * LD1 + cd;
             *hp = *hp > 0.0f ? acc[u][e] : 0.0f;
           }
+        }
       }
     }
     __syncthreads();  // dZ1 complete
@@ -495,9 +516,10 @@ __global__ __launch_bounds__(512) void conv_stack_bwd8_kernel(XaConvStackBwdArgs
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int m = 16 * (4 * u + (w >> 1)) + 4 * q + j, r = m / CP1, pp = m - r * CP1;
-          bv[u][j] = h1s[m * LD1 + n1];
+          const bool in = 4 * u + (w >> 1) < nt1;  // (a skipped tile's rows add zeros)
+          bv[u][j] = in ? h1s[m * LD1 + n1] : 0.0f;
           const float a = xs[r * CW0 + CS1 * pp + (i16 & (CK1 - 1))];
-          av[u][j] = i16 < CK1 ? a : 0.0f;
+          av[u][j] = in && i16 < CK1 ? a : 0.0f;
         }
 #pragma unroll
       for (int u = 0; u < M1 / 64; ++u)
@@ -634,6 +656,9 @@ int cu_count() {
   return cus;
 }
 
+// one workgroup per CU, each an even share of the rows (at most one per row)
+int stack_grid(int rows) { return rows < cu_count() ? rows : cu_count(); }
+
 }  // namespace
 
 XA_DIAG_READER(xa_diag_read_stamps_conv)
@@ -645,16 +670,14 @@ extern "C" int xa_conv_stack_fwd(const XaConvStackArgs* a, void* stream) {
                "xa_conv_stack_fwd: null operand or rows <= 0");
   XA_CHECK_ARG(((uintptr_t)p.x & (p.x_u8 ? 3 : 15)) == 0,
                "xa_conv_stack_fwd: x must be %d-B aligned", p.x_u8 ? 4 : 16);
-  const int G = (p.rows + CR - 1) / CR;
-  const int grid = G < cu_count() ? G : cu_count();
+  const int grid = stack_grid(p.rows);
   hipLaunchKernelGGL(conv_stack_fwd_kernel, dim3(grid), dim3(512), 0, (hipStream_t)stream, p);
   XA_CHECK_LAUNCH("xa_conv_stack_fwd");
   return 0;
 }
 
 extern "C" size_t xa_conv_stack_bwd_workspace_floats(int rows) {
-  const int G = (rows + CR - 1) / CR;
-  return (size_t)(G < cu_count() ? G : cu_count()) * NPAR;
+  return (size_t)stack_grid(rows) * NPAR;
 }
 
 extern "C" int xa_conv_stack_bwd(const XaConvStackBwdArgs* a, void* stream) {
@@ -675,8 +698,7 @@ extern "C" int xa_conv_stack_bwd(const XaConvStackBwdArgs* a, void* stream) {
   XA_CHECK_ARG(p.ws_floats >= xa_conv_stack_bwd_workspace_floats(p.rows),
                "xa_conv_stack_bwd: workspace of %zu floats needed",
                xa_conv_stack_bwd_workspace_floats(p.rows));
-  const int G = (p.rows + CR - 1) / CR;
-  const int grid = G < cu_count() ? G : cu_count();
+  const int grid = stack_grid(p.rows);
   hipLaunchKernelGGL(conv_stack_bwd8_kernel, dim3(grid), dim3(512), 0, (hipStream_t)stream, p);
   XA_CHECK_LAUNCH("xa_conv_stack_bwd");
   const int rest_blocks = p.adam_on && p.n_rest > 0 ? (p.n_rest + 255) / 256 : 0;
