@@ -744,6 +744,38 @@ XA_DEV void returns_block(float a, float c, int n, float gamma, float* __restric
   }
 }
 
+// returns_block's full-block form with the per-step terms staged in LDS rows sa / sc (written
+// lane-parallel): lane 0 reads them 4 steps per 16-B broadcast read, two groups ahead of the
+// chain, so a step is its two dependent VALU ops with no v_readlane beside them; the carries
+// leave 4 per 16-B store. Same operations, same order as returns_block.
+template <bool GAE>
+XA_DEV void returns_block64_lds(const float* __restrict__ sa, const float* __restrict__ sc,
+                                float gamma, float* __restrict__ o, float& carry) {
+  const float4* a4 = reinterpret_cast<const float4*>(sa);
+  const float4* c4 = reinterpret_cast<const float4*>(sc);
+  float4 a_n = a4[15], c_n = c4[15], a_nn = a4[14], c_nn = c4[14];
+#pragma unroll
+  for (int g = 15; g >= 0; --g) {
+    const float4 a = a_n, c = c_n;
+    a_n = a_nn;
+    c_n = c_nn;
+    if (g >= 2) {
+      a_nn = a4[g - 2];
+      c_nn = c4[g - 2];
+    }
+    float4 r;
+    carry = returns_op<GAE>(a.w, c.w, gamma, carry);
+    r.w = carry;
+    carry = returns_op<GAE>(a.z, c.z, gamma, carry);
+    r.z = carry;
+    carry = returns_op<GAE>(a.y, c.y, gamma, carry);
+    r.y = carry;
+    carry = returns_op<GAE>(a.x, c.x, gamma, carry);
+    r.x = carry;
+    reinterpret_cast<float4*>(o)[g] = r;
+  }
+}
+
 template <int OBS, int A>
 __global__ __launch_bounds__(64 * kRW) void replay_rollout_kernel(XaRolloutArgs p) {
   constexpr int AH = A + 1, AHP = (AH + 3) & ~3;
@@ -757,6 +789,7 @@ __global__ __launch_bounds__(64 * kRW) void replay_rollout_kernel(XaRolloutArgs 
   __shared__ __attribute__((aligned(16))) float sw2[4 * 16 * 64];
   __shared__ __attribute__((aligned(16))) float sx[64], sy[64];  // bootstrap h1 / h2 rows
   __shared__ __attribute__((aligned(16))) float sep[64], sret[64];  // chain result rows
+  __shared__ __attribute__((aligned(16))) float sra[64], src[64];    // the returns' step terms
   __shared__ float s_vnext;
   extern __shared__ __attribute__((aligned(16))) float hist[];  // fused: (rew, val, done, .)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -1026,11 +1059,25 @@ __global__ __launch_bounds__(64 * kRW) void replay_rollout_kernel(XaRolloutArgs 
           float delta = (hv.x + (p.gamma * vn) * nnt) - hv.y;
           float coef = p.gamma_lam * nnt;
           asm volatile("" : "+v"(delta), "+v"(coef));  // in all lanes (see the episode returns)
-          if (lane == 0) returns_block<true>(delta, coef, nb, p.gamma, sret, carry);
+          if (nb == 64) {
+            sra[lane] = delta;
+            src[lane] = coef;
+            wave_sync();
+            if (lane == 0) returns_block64_lds<true>(sra, src, p.gamma, sret, carry);
+          } else if (lane == 0) {
+            returns_block<true>(delta, coef, nb, p.gamma, sret, carry);
+          }
         } else {
           float rr = hv.x, nn = nnt;
           asm volatile("" : "+v"(rr), "+v"(nn));
-          if (lane == 0) returns_block<false>(rr, nn, nb, p.gamma, sret, carry);
+          if (nb == 64) {
+            sra[lane] = rr;
+            src[lane] = nn;
+            wave_sync();
+            if (lane == 0) returns_block64_lds<false>(sra, src, p.gamma, sret, carry);
+          } else if (lane == 0) {
+            returns_block<false>(rr, nn, nb, p.gamma, sret, carry);
+          }
         }
         wave_sync();
         if (t < T) p.ret_out[(size_t)env * T + t] = gae ? sret[lane] + hv.y : sret[lane];
