@@ -590,8 +590,17 @@ def ptr(t):
     return t.data_ptr()
 
 
-def stream():
-    return torch.cuda.current_stream().cuda_stream
+if hasattr(torch._C, '_cuda_getCurrentRawStream') and hasattr(torch._C, '_cuda_getDevice'):
+    _raw_stream, _cur_dev = torch._C._cuda_getCurrentRawStream, torch._C._cuda_getDevice
+
+    def stream():
+        """The current HIP stream of the current device (a capture stream inside hipGraph
+        capture), as a raw handle: two C calls instead of torch.cuda.current_stream()'s
+        Python wrappers (~3 us per launch on the C3 host path, tools/c3_host_profile.py)."""
+        return _raw_stream(_cur_dev())
+else:
+    def stream():
+        return torch.cuda.current_stream().cuda_stream
 
 
 def call(name, *args):
