@@ -145,9 +145,9 @@ class DeviceReplay:
             self.host_count = np.minimum(self.host_count + 1, self.cap)
         else:
             self.host_count = self.host_count + 1
-        size = np.minimum(self.host_count, self.cap)
+        size = np.minimum(self.host_count, self.cap).tolist()  # Python ints in one call
         for b, s in zip(self.buffers, size):
-            b.current_size = int(s)
+            b.current_size = s
 
     def reset_counts(self):
         self.count.zero_()
